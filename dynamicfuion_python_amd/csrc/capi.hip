@@ -1,0 +1,869 @@
+// Host orchestration and the C-ABI (include/nnrt_mi355x.h).
+//
+// FitToImage (cpp/alignment/DeformableMeshToImageFitter.cpp:85-276) as a static-shape loop: every buffer is sized at
+// prepare() time, nothing in the iteration synchronizes with the host or allocates, so one GN iteration per iteration
+// mode is captured into a hipGraph and replayed (the reference's per-stage host syncs: SURVEY.md section 3 CS-1).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "fitter_kernels.hpp"
+#include "warp_field.hpp"
+
+namespace nnrt {
+
+namespace {
+thread_local std::string g_error;
+}
+void set_error(const std::string& message) { g_error = message; }
+const std::string& get_error() { return g_error; }
+
+NdcSetup make_ndc_setup(const double* K, int height, int width) {
+	// CoordinateSystemConversions.h:109-146
+	const double fx = K[0], fy = K[4], cx = K[2], cy = K[5];
+	const double h = height, w = width;
+	const double s = std::min(w, h);
+	const float range_x = ndc_range(width, height);
+	const float range_y = ndc_range(height, width);
+	const double fx_ndc = 2.0 * fx / s, fy_ndc = -2.0 * fy / s;
+	const double cx_ndc = -(2.0 * cx - w) / s, cy_ndc = (2.0 * cy - h) / s;
+	NdcSetup r;
+	r.ndc = Camera{static_cast<float>(fx_ndc), static_cast<float>(fy_ndc), static_cast<float>(cx_ndc), static_cast<float>(cy_ndc)};
+	r.min_x = static_cast<float>(cx_ndc - range_x / 2.f);
+	r.max_x = static_cast<float>(cx_ndc + range_x / 2.f);
+	r.min_y = static_cast<float>(cy_ndc - range_y / 2.f);
+	r.max_y = static_cast<float>(cy_ndc + range_y / 2.f);
+	return r;
+}
+
+WarpExtrinsics make_extrinsics(const double* E) {
+	WarpExtrinsics r{};
+	r.identity = 1;
+	const double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+	for (int i = 0; i < 12; i++) {
+		const double v = E ? E[i] : I[i];
+		r.m[i] = static_cast<float>(v);
+		if (v != I[i]) r.identity = 0;
+	}
+	return r;
+}
+
+Camera pixel_camera(const double* K) {
+	return Camera{static_cast<float>(K[0]), static_cast<float>(K[4]), static_cast<float>(K[2]), static_cast<float>(K[5])};
+}
+
+// ---- device buffer helper ----
+template <typename T>
+struct DeviceBuffer {
+	T* ptr = nullptr;
+	size_t count = 0;
+	nnrt_status ensure(size_t n) {
+		if (n <= count && ptr) return NNRT_OK;
+		if (ptr) hipFree(ptr);
+		ptr = nullptr;
+		count = 0;
+		const size_t bytes = sizeof(T) * std::max<size_t>(n, 1);
+		hipError_t e = hipMalloc(reinterpret_cast<void**>(&ptr), bytes);
+		if (e != hipSuccess) {
+			set_error(std::string("hipMalloc failed: ") + hipGetErrorString(e));
+			ptr = nullptr;
+			return NNRT_ERROR_HIP;
+		}
+		count = std::max<size_t>(n, 1);
+		return NNRT_OK;
+	}
+	void release() {
+		if (ptr) hipFree(ptr);
+		ptr = nullptr;
+		count = 0;
+	}
+};
+
+struct DeviceGuard {
+	int prev = -1;
+	explicit DeviceGuard(int device) {
+		hipGetDevice(&prev);
+		if (device >= 0 && device != prev) hipSetDevice(device);
+	}
+	~DeviceGuard() {
+		int cur = -1;
+		hipGetDevice(&cur);
+		if (prev >= 0 && cur != prev) hipSetDevice(prev);
+	}
+};
+
+} // namespace nnrt
+
+using namespace nnrt;
+
+// =====================================================================================================================
+// warp field
+// =====================================================================================================================
+struct nnrt_warp_field {
+	int device = 0;
+	int N = 0;
+	float coverage = 0.05f;
+	int threshold = 0;
+	int anchor_count = 4;
+	int minimum_valid = 0;
+	int coverage_method = NNRT_MINIMAL_K_NEIGHBOR_NODE_DISTANCE;
+	Hierarchy h;
+	std::vector<float> nodes_original;     // [N,3] original order
+	std::vector<float> weights_virtual;    // [N] coverage weights, virtual order
+	DeviceBuffer<float> state;             // [N,16] virtual order
+	DeviceBuffer<float> node_positions;    // [N,3] virtual order (anchor computation input)
+	DeviceBuffer<float> node_weights;      // [N] virtual order
+	DeviceBuffer<int32_t> edges;           // [E,2]
+	DeviceBuffer<int8_t> edge_layers;      // [E]
+	DeviceBuffer<float> radii;             // [layers]
+	uint64_t version = 0;                  // bumped when device buffers are re-allocated
+	int E() const { return static_cast<int>(h.edge_layers.size()); }
+};
+
+namespace {
+nnrt_status wf_download_state(const nnrt_warp_field* wf, std::vector<float>& host) {
+	host.resize(static_cast<size_t>(wf->N) * NODE_STRIDE);
+	NNRT_HIP(hipMemcpy(host.data(), wf->state.ptr, sizeof(float) * host.size(), hipMemcpyDeviceToHost));
+	return NNRT_OK;
+}
+nnrt_status wf_upload_state(nnrt_warp_field* wf, const std::vector<float>& host) {
+	NNRT_HIP(hipMemcpy(wf->state.ptr, host.data(), sizeof(float) * host.size(), hipMemcpyHostToDevice));
+	return NNRT_OK;
+}
+} // namespace
+
+extern "C" {
+
+const char* nnrt_last_error(void) { return get_error().c_str(); }
+
+int32_t nnrt_runtime_version(void) {
+	int v = 0;
+	if (hipRuntimeGetVersion(&v) != hipSuccess) return -1;
+	return v;
+}
+
+int32_t nnrt_device_count(void) {
+	int n = 0;
+	if (hipGetDeviceCount(&n) != hipSuccess) return -1;
+	return n;
+}
+
+nnrt_status nnrt_warp_field_create(const float* h_nodes, int32_t node_count, float node_coverage, int32_t threshold_nodes_by_distance,
+                                   int32_t anchor_count, int32_t minimum_valid_anchor_count, int32_t coverage_method, int32_t layer_count,
+                                   int32_t max_vertex_degree, const float* h_layer_radii, int32_t device, nnrt_warp_field** out) {
+	NNRT_CHECK_ARG(out != nullptr && h_nodes != nullptr, "null pointer");
+	NNRT_CHECK_ARG(node_count >= 1, "node_count must be positive");
+	NNRT_CHECK_ARG(anchor_count >= 1 && anchor_count <= MAX_ANCHORS, "anchor_count must be in [1, 8]");
+	if (node_count < anchor_count) {
+		set_error("Anchor count for warp field exceeds node count (WarpField.cpp:57-61)");
+		return NNRT_ERROR_ARGUMENT;
+	}
+	NNRT_CHECK_ARG(minimum_valid_anchor_count >= 0 && minimum_valid_anchor_count <= anchor_count, "minimum_valid_anchor_count > anchor_count");
+	NNRT_CHECK_ARG(coverage_method == NNRT_FIXED_NODE_COVERAGE || coverage_method == NNRT_MINIMAL_K_NEIGHBOR_NODE_DISTANCE,
+	               "unknown coverage method");
+	DeviceGuard guard(device);
+	auto wf = std::make_unique<nnrt_warp_field>();
+	wf->device = device;
+	wf->N = node_count;
+	wf->coverage = node_coverage;
+	wf->threshold = threshold_nodes_by_distance;
+	wf->anchor_count = anchor_count;
+	wf->minimum_valid = minimum_valid_anchor_count;
+	wf->coverage_method = coverage_method;
+	wf->nodes_original.assign(h_nodes, h_nodes + 3 * static_cast<size_t>(node_count));
+	nnrt_status st = build_hierarchy(h_nodes, node_count, node_coverage, layer_count, max_vertex_degree, h_layer_radii, wf->h);
+	if (st) return st;
+	std::vector<float> weights_original;
+	node_coverage_weights(h_nodes, node_count, node_coverage, weights_original);
+	std::vector<float> state(static_cast<size_t>(node_count) * NODE_STRIDE, 0.f), pos(3 * static_cast<size_t>(node_count));
+	wf->weights_virtual.resize(node_count);
+	for (int v = 0; v < node_count; v++) {
+		const int64_t o = wf->h.virtual_indices[v];
+		float* s = &state[static_cast<size_t>(v) * NODE_STRIDE];
+		for (int c = 0; c < 3; c++) {
+			s[c] = h_nodes[3 * o + c];
+			pos[3 * v + c] = h_nodes[3 * o + c];
+		}
+		s[6] = s[10] = s[14] = 1.f;   // identity rotation (WarpField::ResetRotations)
+		wf->weights_virtual[v] = weights_original[o];
+	}
+	if ((st = wf->state.ensure(state.size()))) return st;
+	if ((st = wf->node_positions.ensure(pos.size()))) return st;
+	if ((st = wf->node_weights.ensure(node_count))) return st;
+	const int E = wf->E();
+	if ((st = wf->edges.ensure(2 * static_cast<size_t>(E)))) return st;
+	if ((st = wf->edge_layers.ensure(E))) return st;
+	if ((st = wf->radii.ensure(wf->h.radii.size()))) return st;
+	NNRT_HIP(hipMemcpy(wf->state.ptr, state.data(), sizeof(float) * state.size(), hipMemcpyHostToDevice));
+	NNRT_HIP(hipMemcpy(wf->node_positions.ptr, pos.data(), sizeof(float) * pos.size(), hipMemcpyHostToDevice));
+	NNRT_HIP(hipMemcpy(wf->node_weights.ptr, wf->weights_virtual.data(), sizeof(float) * node_count, hipMemcpyHostToDevice));
+	if (E > 0) {
+		NNRT_HIP(hipMemcpy(wf->edges.ptr, wf->h.edges.data(), sizeof(int32_t) * 2 * E, hipMemcpyHostToDevice));
+		NNRT_HIP(hipMemcpy(wf->edge_layers.ptr, wf->h.edge_layers.data(), sizeof(int8_t) * E, hipMemcpyHostToDevice));
+	}
+	NNRT_HIP(hipMemcpy(wf->radii.ptr, wf->h.radii.data(), sizeof(float) * wf->h.radii.size(), hipMemcpyHostToDevice));
+	*out = wf.release();
+	return NNRT_OK;
+}
+
+void nnrt_warp_field_destroy(nnrt_warp_field* wf) {
+	if (!wf) return;
+	DeviceGuard guard(wf->device);
+	wf->state.release();
+	wf->node_positions.release();
+	wf->node_weights.release();
+	wf->edges.release();
+	wf->edge_layers.release();
+	wf->radii.release();
+	delete wf;
+}
+
+int32_t nnrt_warp_field_node_count(const nnrt_warp_field* wf) { return wf ? wf->N : -1; }
+int32_t nnrt_warp_field_edge_count(const nnrt_warp_field* wf) { return wf ? wf->E() : -1; }
+int32_t nnrt_warp_field_layer_counts(const nnrt_warp_field* wf, int32_t* h_counts) {
+	if (!wf) return -1;
+	for (size_t i = 0; i < wf->h.layer_counts.size(); i++)
+		if (h_counts) h_counts[i] = wf->h.layer_counts[i];
+	return static_cast<int32_t>(wf->h.layer_counts.size());
+}
+
+nnrt_status nnrt_warp_field_get_virtual_node_indices(const nnrt_warp_field* wf, int64_t* h_out) {
+	NNRT_CHECK_ARG(wf && h_out, "null pointer");
+	std::memcpy(h_out, wf->h.virtual_indices.data(), sizeof(int64_t) * wf->N);
+	return NNRT_OK;
+}
+
+nnrt_status nnrt_warp_field_get_edges(const nnrt_warp_field* wf, int32_t* h_edges, int8_t* h_edge_layers) {
+	NNRT_CHECK_ARG(wf, "null pointer");
+	if (h_edges) std::memcpy(h_edges, wf->h.edges.data(), sizeof(int32_t) * wf->h.edges.size());
+	if (h_edge_layers) std::memcpy(h_edge_layers, wf->h.edge_layers.data(), wf->h.edge_layers.size());
+	return NNRT_OK;
+}
+
+static nnrt_status wf_get(const nnrt_warp_field* wf, float* h_out, int virtual_order, int offset, int width) {
+	NNRT_CHECK_ARG(wf && h_out, "null pointer");
+	DeviceGuard guard(wf->device);
+	std::vector<float> s;
+	nnrt_status st = wf_download_state(wf, s);
+	if (st) return st;
+	for (int v = 0; v < wf->N; v++) {
+		const int64_t dst = virtual_order ? v : wf->h.virtual_indices[v];
+		for (int c = 0; c < width; c++) h_out[dst * width + c] = s[static_cast<size_t>(v) * NODE_STRIDE + offset + c];
+	}
+	return NNRT_OK;
+}
+
+static nnrt_status wf_set(nnrt_warp_field* wf, const float* h_in, int virtual_order, int offset, int width) {
+	NNRT_CHECK_ARG(wf && h_in, "null pointer");
+	DeviceGuard guard(wf->device);
+	std::vector<float> s;
+	nnrt_status st = wf_download_state(wf, s);
+	if (st) return st;
+	for (int v = 0; v < wf->N; v++) {
+		const int64_t src = virtual_order ? v : wf->h.virtual_indices[v];
+		for (int c = 0; c < width; c++) s[static_cast<size_t>(v) * NODE_STRIDE + offset + c] = h_in[src * width + c];
+	}
+	return wf_upload_state(wf, s);
+}
+
+nnrt_status nnrt_warp_field_get_node_positions(const nnrt_warp_field* wf, float* h_out, int32_t virtual_order) {
+	return wf_get(wf, h_out, virtual_order, 0, 3);
+}
+nnrt_status nnrt_warp_field_get_node_translations(const nnrt_warp_field* wf, float* h_out, int32_t virtual_order) {
+	return wf_get(wf, h_out, virtual_order, 3, 3);
+}
+nnrt_status nnrt_warp_field_get_node_rotations(const nnrt_warp_field* wf, float* h_out, int32_t virtual_order) {
+	return wf_get(wf, h_out, virtual_order, 6, 9);
+}
+nnrt_status nnrt_warp_field_set_node_translations(nnrt_warp_field* wf, const float* h_in, int32_t virtual_order) {
+	return wf_set(wf, h_in, virtual_order, 3, 3);
+}
+nnrt_status nnrt_warp_field_set_node_rotations(nnrt_warp_field* wf, const float* h_in, int32_t virtual_order) {
+	return wf_set(wf, h_in, virtual_order, 6, 9);
+}
+nnrt_status nnrt_warp_field_get_node_coverage_weights(const nnrt_warp_field* wf, float* h_out) {
+	NNRT_CHECK_ARG(wf && h_out, "null pointer");
+	std::memcpy(h_out, wf->weights_virtual.data(), sizeof(float) * wf->N);
+	return NNRT_OK;
+}
+
+} // extern "C"
+
+// =====================================================================================================================
+// fitter
+// =====================================================================================================================
+struct nnrt_fitter {
+	nnrt_fitter_params p{};
+	int device = 0;
+	hipStream_t work = nullptr;
+	hipEvent_t ev_in = nullptr, ev_out = nullptr;
+	// frame dims
+	int64_t V = 0, F = 0;
+	int H = 0, W = 0, N = 0, K = 0, E = 0;
+	bool prepared = false;
+	const nnrt_warp_field* wf = nullptr;
+	uint64_t wf_version = 0;
+	// frame constants
+	NdcSetup ndc{};
+	Camera pix{};
+	WarpExtrinsics extr{};
+	// buffers
+	DeviceBuffer<float> mesh_p, mesh_n;
+	DeviceBuffer<int4> faces4;
+	DeviceBuffer<int32_t> anchors;
+	DeviceBuffer<float> weights;
+	DeviceBuffer<float4> wpos, wnrm, jv, jn;
+	DeviceBuffer<float> ref_depth;
+	DeviceBuffer<uint64_t> keys;
+	DeviceBuffer<float> residuals;
+	DeviceBuffer<uint8_t> residual_mask;
+	DeviceBuffer<int32_t> pixel_face;
+	DeviceBuffer<float> acc, arap_acc;
+	DeviceBuffer<float> updates, gradient, hessian;
+	DeviceBuffer<int> error_flag;
+	// ARAP / arrowhead
+	DeviceBuffer<float> wing, edge_residuals, a_diag, a_dinv, a_dinvb, a_schur, a_rhs, a_x;
+	DeviceBuffer<int> a_offsets, a_list;
+	ArrowheadWorkspace aw;
+	int n0 = 0;
+	int last_mode = 0;
+	// graphs (one per iteration mode)
+	hipGraphExec_t graph[3] = {nullptr, nullptr, nullptr};
+
+	void drop_graphs() {
+		for (auto& g : graph)
+			if (g) {
+				hipGraphExecDestroy(g);
+				g = nullptr;
+			}
+	}
+};
+
+namespace {
+
+__global__ void k_prepare_reference(const float* __restrict__ depth, const uint8_t* __restrict__ mask, int64_t P, float scale, float max_depth,
+                                    float* __restrict__ out) {
+	const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (i >= P) return;
+	const float d = depth[i] / scale;
+	const bool valid = d > 0 && d < max_depth && (mask == nullptr || mask[i] != 0);
+	out[i] = valid ? d : 0.f;
+}
+
+__global__ void k_faces_to_int4(const int64_t* __restrict__ faces, int64_t F, int4* __restrict__ out) {
+	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (f >= F) return;
+	out[f] = make_int4(static_cast<int>(faces[3 * f]), static_cast<int>(faces[3 * f + 1]), static_cast<int>(faces[3 * f + 2]), 0);
+}
+
+nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mode, hipStream_t s) {
+	nnrt_status st;
+	const bool with_jacobians = true;
+	if ((st = launch_warp_mesh(ft->mesh_p.ptr, ft->mesh_n.ptr, ft->V, wf->state.ptr, ft->anchors.ptr, ft->weights.ptr, ft->K, ft->extr,
+	                           ft->wpos.ptr, ft->wnrm.ptr, with_jacobians ? ft->jv.ptr : nullptr, ft->jn.ptr, s)))
+		return st;
+	RasterOptions ro{ft->H, ft->W, 0.5f / (static_cast<float>(fminf(ft->H, ft->W)) / 2.0f), ft->p.use_perspective_correction, 0, 1};
+	if ((st = launch_raster_scatter_mesh(ft->wpos.ptr, ft->faces4.ptr, ft->F, ft->ndc, 0.0f, 10.0f, ro, ft->keys.ptr, s))) return st;
+	FitPixelArgs fa{};
+	fa.H = ft->H;
+	fa.W = ft->W;
+	fa.tiles_x = static_cast<int>(ceil_div(ft->W, 16));
+	fa.tiles_y = static_cast<int>(ceil_div(ft->H, 16));
+	fa.pix = ft->pix;
+	fa.ndc = ft->ndc;
+	fa.blur = ro.blur;
+	fa.perspective = ft->p.use_perspective_correction;
+	fa.max_depth = ft->p.max_depth;
+	fa.use_tukey = ft->p.use_tukey_penalty_for_data_term;
+	fa.tukey_c = ft->p.tukey_penalty_cutoff_cm;
+	fa.anchor_count = ft->K;
+	fa.keys = ft->keys.ptr;
+	fa.faces4 = ft->faces4.ptr;
+	fa.wpos = ft->wpos.ptr;
+	fa.wnrm = ft->wnrm.ptr;
+	fa.anchors = ft->anchors.ptr;
+	fa.jv = ft->jv.ptr;
+	fa.jn = ft->jn.ptr;
+	fa.ref_depth = ft->ref_depth.ptr;
+	fa.residuals = ft->residuals.ptr;
+	fa.residual_mask = ft->residual_mask.ptr;
+	fa.pixel_face = ft->pixel_face.ptr;
+	fa.acc = ft->acc.ptr;
+	if ((st = launch_fit_pixels(mode, fa, s))) return st;
+	if (ft->E > 0) {
+		ArapArgs aa{};
+		aa.E = ft->E;
+		aa.N = ft->N;
+		aa.n0 = ft->n0;
+		aa.lambda = ft->p.arap_term_weight;
+		aa.use_huber = ft->p.use_huber_penalty_for_arap_term;
+		aa.huber_delta = ft->p.huber_penalty_constant;
+		aa.coverage_variable = wf->coverage_method == NNRT_MINIMAL_K_NEIGHBOR_NODE_DISTANCE;
+		aa.edges = wf->edges.ptr;
+		aa.edge_layers = wf->edge_layers.ptr;
+		aa.radii = wf->radii.ptr;
+		aa.node_weights = wf->node_weights.ptr;
+		aa.node_state = wf->state.ptr;
+		aa.acc = ft->arap_acc.ptr;
+		aa.wing = ft->wing.ptr;
+		aa.edge_residuals = ft->edge_residuals.ptr;
+		aa.error_flag = ft->error_flag.ptr;
+		if ((st = launch_arap_edges(aa, s))) return st;
+		const float lm = ft->p.preconditioning_dampening_factor;
+		if ((st = launch_arrowhead_iteration(ft->aw, ft->acc.ptr, lm, wf->edges.ptr, ft->wing.ptr, wf->state.ptr, ft->arap_acc.ptr,
+		                                     ft->updates.ptr, ft->gradient.ptr, ft->hessian.ptr, ft->error_flag.ptr, s)))
+			return st;
+	} else {
+		SolveArgs sa{};
+		sa.N = ft->N;
+		sa.lm = ft->p.preconditioning_dampening_factor;
+		sa.acc = ft->acc.ptr;
+		sa.node_state = wf->state.ptr;
+		sa.updates_out = ft->updates.ptr;
+		sa.gradient_out = ft->gradient.ptr;
+		sa.hessian_out = ft->hessian.ptr;
+		sa.error_flag = ft->error_flag.ptr;
+		if ((st = launch_solve_update(mode, sa, s))) return st;
+	}
+	return NNRT_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+void nnrt_fitter_default_params(nnrt_fitter_params* p) {
+	if (!p) return;
+	std::memset(p, 0, sizeof(*p));
+	p->max_iteration_count = 100;
+	p->iteration_mode_count = 1;
+	p->iteration_modes[0] = NNRT_ITERATION_ALL;
+	p->minimal_update_threshold = 1e-6f;
+	p->use_perspective_correction = 1;
+	p->max_depth = 10.f;
+	p->use_tukey_penalty_for_data_term = 0;
+	p->tukey_penalty_cutoff_cm = 0.01f;
+	p->preconditioning_dampening_factor = 0.f;
+	p->arap_term_weight = 200.f;
+	p->use_huber_penalty_for_arap_term = 0;
+	p->huber_penalty_constant = 1e-4f;
+	p->use_hip_graph = 1;
+}
+
+nnrt_status nnrt_fitter_create(const nnrt_fitter_params* params, int32_t device, nnrt_fitter** out) {
+	NNRT_CHECK_ARG(params && out, "null pointer");
+	if (params->preconditioning_dampening_factor < 0.f || params->preconditioning_dampening_factor > 1.f) {
+		set_error("`preconditioning_dampening_factor` should be a small non-negative value between 0 and 1 (DeformableMeshToImageFitter.cpp:79-82)");
+		return NNRT_ERROR_ARGUMENT;
+	}
+	NNRT_CHECK_ARG(params->iteration_mode_count >= 1 && params->iteration_mode_count <= 16, "iteration_mode_count must be in [1, 16]");
+	for (int i = 0; i < params->iteration_mode_count; i++)
+		NNRT_CHECK_ARG(params->iteration_modes[i] >= 0 && params->iteration_modes[i] <= 2, "unknown iteration mode");
+	DeviceGuard guard(device);
+	auto ft = std::make_unique<nnrt_fitter>();
+	ft->p = *params;
+	ft->device = device;
+	NNRT_HIP(hipStreamCreateWithFlags(&ft->work, hipStreamNonBlocking));
+	NNRT_HIP(hipEventCreateWithFlags(&ft->ev_in, hipEventDisableTiming));
+	NNRT_HIP(hipEventCreateWithFlags(&ft->ev_out, hipEventDisableTiming));
+	nnrt_status st = ft->error_flag.ensure(1);
+	if (st) return st;
+	NNRT_HIP(hipMemset(ft->error_flag.ptr, 0, sizeof(int)));
+	*out = ft.release();
+	return NNRT_OK;
+}
+
+void nnrt_fitter_destroy(nnrt_fitter* ft) {
+	if (!ft) return;
+	DeviceGuard guard(ft->device);
+	hipStreamSynchronize(ft->work);
+	ft->drop_graphs();
+	for (auto* b : {&ft->mesh_p, &ft->mesh_n, &ft->weights, &ft->ref_depth, &ft->residuals, &ft->acc, &ft->arap_acc, &ft->updates, &ft->gradient,
+	                &ft->hessian, &ft->wing, &ft->edge_residuals, &ft->a_diag, &ft->a_dinv, &ft->a_dinvb, &ft->a_schur, &ft->a_rhs, &ft->a_x})
+		b->release();
+	ft->faces4.release();
+	ft->anchors.release();
+	ft->wpos.release();
+	ft->wnrm.release();
+	ft->jv.release();
+	ft->jn.release();
+	ft->keys.release();
+	ft->residual_mask.release();
+	ft->pixel_face.release();
+	ft->error_flag.release();
+	ft->a_offsets.release();
+	ft->a_list.release();
+	if (ft->ev_in) hipEventDestroy(ft->ev_in);
+	if (ft->ev_out) hipEventDestroy(ft->ev_out);
+	if (ft->work) hipStreamDestroy(ft->work);
+	delete ft;
+}
+
+nnrt_status nnrt_fitter_prepare(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_vertices, const float* d_normals, int64_t V,
+                                const int64_t* d_faces, int64_t F, const float* d_depth, const uint8_t* d_mask, int32_t H, int32_t W,
+                                const double* h_K, const double* h_E, float depth_scale, void* stream) {
+	NNRT_CHECK_ARG(ft && wf && d_vertices && d_normals && d_faces && d_depth && h_K, "null pointer");
+	NNRT_CHECK_ARG(V > 0 && F > 0 && H > 0 && W > 0, "empty mesh or image");
+	NNRT_CHECK_ARG(V < (int64_t(1) << 31) && F < (int64_t(1) << 31), "mesh too large for int32 indexing");
+	NNRT_CHECK_ARG(depth_scale > 0.f, "depth_scale must be positive");
+	DeviceGuard guard(ft->device);
+	hipStream_t us = static_cast<hipStream_t>(stream);
+	const int64_t P = static_cast<int64_t>(H) * W;
+	const int N = wf->N, K = wf->anchor_count, E = wf->E();
+	if (E > 0) {
+		for (int i = 0; i < ft->p.iteration_mode_count; i++)
+			if (ft->p.iteration_modes[i] != NNRT_ITERATION_ALL) {
+				set_error("the regularized (ARAP) solve supports IterationMode ALL only (reference A15: the ARAP Hessian is 6x6-only)");
+				return NNRT_ERROR_UNSUPPORTED;
+			}
+	}
+	// (re)allocate; any reallocation invalidates captured graphs
+	const auto before = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->a_schur.ptr);
+	nnrt_status st;
+	if ((st = ft->mesh_p.ensure(3 * V)) || (st = ft->mesh_n.ensure(3 * V)) || (st = ft->faces4.ensure(F)) ||
+	    (st = ft->anchors.ensure(static_cast<size_t>(V) * K)) || (st = ft->weights.ensure(static_cast<size_t>(V) * K)) ||
+	    (st = ft->wpos.ensure(V)) || (st = ft->wnrm.ensure(V)) || (st = ft->jv.ensure(static_cast<size_t>(V) * K)) ||
+	    (st = ft->jn.ensure(static_cast<size_t>(V) * K)) || (st = ft->ref_depth.ensure(P)) || (st = ft->keys.ensure(P)) ||
+	    (st = ft->residuals.ensure(P)) || (st = ft->residual_mask.ensure(P)) || (st = ft->pixel_face.ensure(P)) ||
+	    (st = ft->acc.ensure(static_cast<size_t>(N) * ACC_STRIDE)) || (st = ft->arap_acc.ensure(static_cast<size_t>(N) * ACC_STRIDE)) ||
+	    (st = ft->updates.ensure(static_cast<size_t>(N) * 6)) || (st = ft->gradient.ensure(static_cast<size_t>(N) * 6)) ||
+	    (st = ft->hessian.ensure(static_cast<size_t>(N) * 36)))
+		return st;
+	// ARAP workspace
+	ft->E = E;
+	ft->n0 = wf->h.layer_counts.empty() ? N : wf->h.layer_counts[0];
+	if (E > 0) {
+		const int n0 = ft->n0, m = 6 * (N - n0);
+		if ((st = ft->wing.ensure(static_cast<size_t>(E) * 36)) || (st = ft->edge_residuals.ensure(3 * static_cast<size_t>(E))) ||
+		    (st = ft->a_diag.ensure(static_cast<size_t>(N) * 36)) || (st = ft->a_dinv.ensure(static_cast<size_t>(n0) * 36)) ||
+		    (st = ft->a_dinvb.ensure(static_cast<size_t>(E) * 36)) || (st = ft->a_schur.ensure(static_cast<size_t>(m) * m)) ||
+		    (st = ft->a_rhs.ensure(6 * static_cast<size_t>(N))) || (st = ft->a_x.ensure(6 * static_cast<size_t>(N))) ||
+		    (st = ft->a_offsets.ensure(n0 + 1)) || (st = ft->a_list.ensure(E)))
+			return st;
+		// CSR of stem edges by source node
+		std::vector<int> counts(n0 + 1, 0), list(E), fill;
+		for (int e = 0; e < E; e++) {
+			const int i = wf->h.edges[2 * e];
+			if (i < n0) counts[i + 1]++;
+		}
+		for (int i = 0; i < n0; i++) counts[i + 1] += counts[i];
+		fill.assign(counts.begin(), counts.end() - 1);
+		for (int e = 0; e < E; e++) {
+			const int i = wf->h.edges[2 * e];
+			if (i < n0) list[fill[i]++] = e;
+		}
+		NNRT_HIP(hipMemcpy(ft->a_offsets.ptr, counts.data(), sizeof(int) * (n0 + 1), hipMemcpyHostToDevice));
+		NNRT_HIP(hipMemcpy(ft->a_list.ptr, list.data(), sizeof(int) * E, hipMemcpyHostToDevice));
+		ft->aw.N = N;
+		ft->aw.n0 = n0;
+		ft->aw.E = E;
+		ft->aw.m = m;
+		ft->aw.diag = ft->a_diag.ptr;
+		ft->aw.dinv = ft->a_dinv.ptr;
+		ft->aw.dinv_b = ft->a_dinvb.ptr;
+		ft->aw.schur = ft->a_schur.ptr;
+		ft->aw.rhs = ft->a_rhs.ptr;
+		ft->aw.x = ft->a_x.ptr;
+		ft->aw.edge_offsets = ft->a_offsets.ptr;
+		ft->aw.edge_list = ft->a_list.ptr;
+	}
+	const auto after = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->a_schur.ptr);
+	if (before != after || ft->wf != wf || ft->V != V || ft->F != F || ft->H != H || ft->W != W || ft->N != N || ft->K != K) ft->drop_graphs();
+	ft->V = V;
+	ft->F = F;
+	ft->H = H;
+	ft->W = W;
+	ft->N = N;
+	ft->K = K;
+	ft->wf = wf;
+	ft->ndc = make_ndc_setup(h_K, H, W);
+	ft->pix = pixel_camera(h_K);
+	const WarpExtrinsics ne = make_extrinsics(h_E);
+	if (std::memcmp(&ne, &ft->extr, sizeof(ne)) != 0) ft->drop_graphs();
+	ft->extr = ne;
+	// order the work stream after the caller's stream
+	NNRT_HIP(hipEventRecord(ft->ev_in, us));
+	NNRT_HIP(hipStreamWaitEvent(ft->work, ft->ev_in, 0));
+	hipStream_t s = ft->work;
+	NNRT_HIP(hipMemcpyAsync(ft->mesh_p.ptr, d_vertices, sizeof(float) * 3 * V, hipMemcpyDeviceToDevice, s));
+	NNRT_HIP(hipMemcpyAsync(ft->mesh_n.ptr, d_normals, sizeof(float) * 3 * V, hipMemcpyDeviceToDevice, s));
+	k_faces_to_int4<<<static_cast<unsigned>(ceil_div(F, 256)), 256, 0, s>>>(d_faces, F, ft->faces4.ptr);
+	NNRT_LAUNCH_CHECK();
+	// once per frame (:96-106): anchors & weights on the canonical mesh in virtual node order
+	if ((st = launch_compute_anchors(ft->mesh_p.ptr, V, wf->node_positions.ptr, N, K, wf->coverage,
+	                                 wf->coverage_method == NNRT_MINIMAL_K_NEIGHBOR_NODE_DISTANCE ? wf->node_weights.ptr : nullptr,
+	                                 wf->threshold ? wf->minimum_valid : 0, ft->anchors.ptr, ft->weights.ptr, s)))
+		return st;
+	// reference point cloud (:289-306): depth / scale with 0 < d < max_depth, AND the user mask; stored as depth (0 = masked)
+	k_prepare_reference<<<static_cast<unsigned>(ceil_div(P, 256)), 256, 0, s>>>(d_depth, d_mask, P, depth_scale, ft->p.max_depth,
+	                                                                            ft->ref_depth.ptr);
+	NNRT_LAUNCH_CHECK();
+	NNRT_HIP(hipMemsetAsync(ft->keys.ptr, 0xff, sizeof(uint64_t) * P, s));
+	NNRT_HIP(hipMemsetAsync(ft->acc.ptr, 0, sizeof(float) * N * ACC_STRIDE, s));
+	NNRT_HIP(hipMemsetAsync(ft->arap_acc.ptr, 0, sizeof(float) * N * ACC_STRIDE, s));
+	NNRT_HIP(hipEventRecord(ft->ev_out, s));
+	NNRT_HIP(hipStreamWaitEvent(us, ft->ev_out, 0));
+	ft->prepared = true;
+	return NNRT_OK;
+}
+
+nnrt_status nnrt_fitter_iterate(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_iteration, int32_t count, void* stream) {
+	NNRT_CHECK_ARG(ft && wf, "null pointer");
+	if (!ft->prepared || ft->wf != wf) {
+		set_error("nnrt_fitter_prepare must be called with this warp field before nnrt_fitter_iterate");
+		return NNRT_ERROR_ARGUMENT;
+	}
+	DeviceGuard guard(ft->device);
+	hipStream_t us = static_cast<hipStream_t>(stream);
+	NNRT_HIP(hipEventRecord(ft->ev_in, us));
+	NNRT_HIP(hipStreamWaitEvent(ft->work, ft->ev_in, 0));
+	hipStream_t s = ft->work;
+	nnrt_status st;
+	for (int it = first_iteration; it < first_iteration + count; it++) {
+		const int mode = ft->p.iteration_modes[it % ft->p.iteration_mode_count];
+		ft->last_mode = mode;
+		if (ft->p.use_hip_graph) {
+			if (!ft->graph[mode]) {
+				hipGraph_t g = nullptr;
+				NNRT_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+				st = enqueue_iteration(ft, wf, mode, s);
+				hipError_t ce = hipStreamEndCapture(s, &g);
+				if (st) {
+					if (g) hipGraphDestroy(g);
+					return st;
+				}
+				NNRT_HIP(ce);
+				hipError_t ie = hipGraphInstantiate(&ft->graph[mode], g, nullptr, nullptr, 0);
+				hipGraphDestroy(g);
+				NNRT_HIP(ie);
+			}
+			NNRT_HIP(hipGraphLaunch(ft->graph[mode], s));
+		} else {
+			if ((st = enqueue_iteration(ft, wf, mode, s))) return st;
+		}
+	}
+	NNRT_HIP(hipEventRecord(ft->ev_out, s));
+	NNRT_HIP(hipStreamWaitEvent(us, ft->ev_out, 0));
+	return NNRT_OK;
+}
+
+nnrt_status nnrt_fitter_check(nnrt_fitter* ft, void* stream) {
+	NNRT_CHECK_ARG(ft, "null pointer");
+	DeviceGuard guard(ft->device);
+	NNRT_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+	NNRT_HIP(hipStreamSynchronize(ft->work));
+	int flag = 0;
+	NNRT_HIP(hipMemcpy(&flag, ft->error_flag.ptr, sizeof(int), hipMemcpyDeviceToHost));
+	NNRT_HIP(hipMemset(ft->error_flag.ptr, 0, sizeof(int)));
+	if (flag & 1) {
+		set_error("potrf failed: a Hessian block (or the Schur complement) is not positive-definite (reference NNRT_LAPACK_CHECK, "
+		          "SolveBlockDiagonalCholeskyCPU.cpp:48-51)");
+		return NNRT_ERROR_NOT_POSITIVE_DEFINITE;
+	}
+	if (flag & 2) {
+		set_error("fixed-coverage ARAP residual indexes edge_layer_indices[node_j] out of bounds (reference quirk A3)");
+		return NNRT_ERROR_UNSUPPORTED;
+	}
+	return NNRT_OK;
+}
+
+nnrt_status nnrt_fitter_fit_to_image(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_vertices, const float* d_normals, int64_t V,
+                                     const int64_t* d_faces, int64_t F, const float* d_depth, const uint8_t* d_mask, int32_t H, int32_t W,
+                                     const double* h_K, const double* h_E, float depth_scale, void* stream) {
+	nnrt_status st = nnrt_fitter_prepare(ft, wf, d_vertices, d_normals, V, d_faces, F, d_depth, d_mask, H, W, h_K, h_E, depth_scale, stream);
+	if (st) return st;
+	// A14: the reference never updates `maximum_update`, so the loop always runs max_iteration_count iterations
+	if ((st = nnrt_fitter_iterate(ft, wf, 0, ft->p.max_iteration_count, stream))) return st;
+	return nnrt_fitter_check(ft, stream);
+}
+
+nnrt_status nnrt_fitter_get_diagnostics(nnrt_fitter* ft, float* h_residuals, uint8_t* h_mask, int32_t* h_faces, float* h_updates,
+                                        float* h_gradient, float* h_hessian, void* stream) {
+	NNRT_CHECK_ARG(ft && ft->prepared, "fitter not prepared");
+	DeviceGuard guard(ft->device);
+	NNRT_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+	NNRT_HIP(hipStreamSynchronize(ft->work));
+	const int64_t P = static_cast<int64_t>(ft->H) * ft->W;
+	const int s = ft->last_mode == NNRT_ITERATION_ALL ? 6 : 3;
+	if (h_residuals) NNRT_HIP(hipMemcpy(h_residuals, ft->residuals.ptr, sizeof(float) * P, hipMemcpyDeviceToHost));
+	if (h_mask) NNRT_HIP(hipMemcpy(h_mask, ft->residual_mask.ptr, P, hipMemcpyDeviceToHost));
+	if (h_faces) NNRT_HIP(hipMemcpy(h_faces, ft->pixel_face.ptr, sizeof(int32_t) * P, hipMemcpyDeviceToHost));
+	if (h_updates) NNRT_HIP(hipMemcpy(h_updates, ft->updates.ptr, sizeof(float) * ft->N * s, hipMemcpyDeviceToHost));
+	if (h_gradient) NNRT_HIP(hipMemcpy(h_gradient, ft->gradient.ptr, sizeof(float) * ft->N * s, hipMemcpyDeviceToHost));
+	if (h_hessian) NNRT_HIP(hipMemcpy(h_hessian, ft->hessian.ptr, sizeof(float) * ft->N * s * s, hipMemcpyDeviceToHost));
+	return NNRT_OK;
+}
+
+nnrt_status nnrt_fitter_get_anchors(nnrt_fitter* ft, int32_t* h_anchors, float* h_weights, void* stream) {
+	NNRT_CHECK_ARG(ft && ft->prepared, "fitter not prepared");
+	DeviceGuard guard(ft->device);
+	NNRT_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+	NNRT_HIP(hipStreamSynchronize(ft->work));
+	if (h_anchors) NNRT_HIP(hipMemcpy(h_anchors, ft->anchors.ptr, sizeof(int32_t) * ft->V * ft->K, hipMemcpyDeviceToHost));
+	if (h_weights) NNRT_HIP(hipMemcpy(h_weights, ft->weights.ptr, sizeof(float) * ft->V * ft->K, hipMemcpyDeviceToHost));
+	return NNRT_OK;
+}
+
+// ---------------------------------------------------------------------------------------------------------------------
+// stage entry points
+// ---------------------------------------------------------------------------------------------------------------------
+nnrt_status nnrt_compute_anchors_and_weights(const float* d_points, int64_t V, const float* d_nodes, int32_t N, int32_t K, float coverage,
+                                             const float* d_node_weights, int32_t minimum_valid, int32_t* d_anchors, float* d_weights,
+                                             void* stream) {
+	NNRT_CHECK_ARG(minimum_valid <= K, "minimum_valid_anchor_count has to be <= anchor_count (WarpAnchorComputation.cpp:92-95)");
+	return launch_compute_anchors(d_points, V, d_nodes, N, K, coverage, d_node_weights, minimum_valid, d_anchors, d_weights,
+	                              static_cast<hipStream_t>(stream));
+}
+
+nnrt_status nnrt_warp_mesh(const float* d_vertices, const float* d_normals, int64_t V, const float* d_nodes, const float* d_rotations,
+                           const float* d_translations, int32_t N, const int32_t* d_anchors, const float* d_weights, int32_t K,
+                           const double* h_E, float* d_out_vertices, float* d_out_normals, void* stream) {
+	NNRT_CHECK_ARG(d_vertices && d_normals && d_nodes && d_anchors && d_weights && d_out_vertices && d_out_normals, "null pointer");
+	hipStream_t s = static_cast<hipStream_t>(stream);
+	float* state = nullptr;
+	float4 *wp = nullptr, *wn = nullptr;
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&state), sizeof(float) * NODE_STRIDE * std::max(N, 1), s));
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&wp), sizeof(float4) * std::max<int64_t>(V, 1), s));
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&wn), sizeof(float4) * std::max<int64_t>(V, 1), s));
+	nnrt_status st = launch_pack_nodes(d_nodes, d_rotations, d_translations, N, state, s);
+	if (!st) st = launch_warp_mesh(d_vertices, d_normals, V, state, d_anchors, d_weights, K, make_extrinsics(h_E), wp, wn, nullptr, nullptr, s);
+	if (!st) st = launch_unpack_float4x3(wp, V, d_out_vertices, s);
+	if (!st) st = launch_unpack_float4x3(wn, V, d_out_normals, s);
+	hipFreeAsync(state, s);
+	hipFreeAsync(wp, s);
+	hipFreeAsync(wn, s);
+	return st;
+}
+
+nnrt_status nnrt_get_mesh_ndc_face_vertices_and_clip_mask(const float* d_vertices, const int64_t* d_faces, int64_t F, const double* h_K, int32_t H,
+                                                          int32_t W, float near_clip, float far_clip, float* d_face_ndc, uint8_t* d_clip_mask,
+                                                          void* stream) {
+	NNRT_CHECK_ARG(h_K && d_vertices && d_faces && d_face_ndc && d_clip_mask, "null pointer");
+	NNRT_CHECK_ARG(near_clip >= 0.f, "near_clipping_distance cannot be less than 0 (ExtractFaceVertices.cpp:40-44)");
+	NNRT_CHECK_ARG(near_clip <= far_clip, "near_clipping_distance cannot be greater than far_clipping_distance");
+	return launch_extract_face_ndc(d_vertices, d_faces, F, make_ndc_setup(h_K, H, W), near_clip, far_clip, d_face_ndc, d_clip_mask,
+	                               static_cast<hipStream_t>(stream));
+}
+
+nnrt_status nnrt_rasterize_ndc_triangles(const float* d_face_ndc, const uint8_t* d_clip_mask, int64_t F, int32_t H, int32_t W,
+                                         float blur_radius_pixels, int32_t faces_per_pixel, int32_t bin_size, int32_t max_faces_per_bin,
+                                         int32_t perspective, int32_t clip_barycentric, int32_t cull_back_faces, int64_t* d_faces_out,
+                                         float* d_depth_out, float* d_bary_out, float* d_dist_out, void* stream) {
+	(void) max_faces_per_bin;
+	NNRT_CHECK_ARG(H > 0 && W > 0, "image_size must be positive");
+	if (faces_per_pixel > MAX_FACES_PER_PIXEL || faces_per_pixel < 1) {
+		set_error("Need faces_per_pixel <= 8 (RasterizeNdcTriangles.cpp:45-47)");
+		return NNRT_ERROR_ARGUMENT;
+	}
+	// bin-size validation kept for error parity (RasterizeNdcTriangles.cpp:53-76); bins themselves are not needed here
+	const int max_dim = std::max(H, W);
+	if (bin_size == -1) bin_size = max_dim <= 64 ? 8 : static_cast<int>(std::pow(2, std::max(static_cast<int>(std::ceil(std::log2(static_cast<double>(max_dim)))) - 4, 4)));
+	if (bin_size != 0 && 1 + (max_dim - 1) / bin_size >= 22) {
+		set_error("The provided bin_size is too small (RasterizeNdcTriangles.cpp:70-76)");
+		return NNRT_ERROR_ARGUMENT;
+	}
+	hipStream_t s = static_cast<hipStream_t>(stream);
+	RasterOptions o{H, W, blur_radius_pixels / (static_cast<float>(fminf(H, W)) / 2.0f), perspective, clip_barycentric, cull_back_faces};
+	if (faces_per_pixel == 1) {
+		const int64_t P = static_cast<int64_t>(H) * W;
+		uint64_t* keys = nullptr;
+		NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&keys), sizeof(uint64_t) * P, s));
+		NNRT_HIP(hipMemsetAsync(keys, 0xff, sizeof(uint64_t) * P, s));
+		nnrt_status st = launch_raster_scatter_ndc(d_face_ndc, d_clip_mask, F, o, keys, s);
+		if (!st) st = launch_raster_resolve(d_face_ndc, F, o, keys, d_faces_out, d_depth_out, d_bary_out, d_dist_out, s);
+		hipFreeAsync(keys, s);
+		return st;
+	}
+	return launch_raster_multi(d_face_ndc, d_clip_mask, F, o, faces_per_pixel, d_faces_out, d_depth_out, d_bary_out, d_dist_out, s);
+}
+
+nnrt_status nnrt_interpolate_face_attributes(const int64_t* d_pixel_faces, const float* d_bary, int64_t P, int32_t Kf, const float* d_attrs,
+                                             int32_t C, float* d_out, void* stream) {
+	return launch_interpolate(d_pixel_faces, d_bary, P, Kf, d_attrs, C, d_out, static_cast<hipStream_t>(stream));
+}
+
+nnrt_status nnrt_unproject_depth(const float* d_depth, int32_t H, int32_t W, const double* h_K, float depth_scale, float depth_max,
+                                 float* d_points, uint8_t* d_mask, void* stream) {
+	NNRT_CHECK_ARG(h_K, "null intrinsics");
+	return launch_unproject(d_depth, H, W, pixel_camera(h_K), depth_scale, depth_max, d_points, d_mask, static_cast<hipStream_t>(stream));
+}
+
+nnrt_status nnrt_axis_angle_to_matrices_rodrigues(const float* d_vectors, int32_t count, float* d_matrices, void* stream) {
+	return launch_rodrigues(d_vectors, count, d_matrices, static_cast<hipStream_t>(stream));
+}
+
+nnrt_status nnrt_solve_block_diagonal_cholesky(const float* d_blocks, const float* d_b, int32_t count, int32_t block_size, float* d_x,
+                                               void* stream) {
+	hipStream_t s = static_cast<hipStream_t>(stream);
+	int* flag = nullptr;
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&flag), sizeof(int), s));
+	NNRT_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
+	nnrt_status st = launch_solve_block_diagonal(d_blocks, d_b, count, block_size, d_x, flag, s);
+	int host_flag = 0;
+	if (!st) {
+		NNRT_HIP(hipMemcpyAsync(&host_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
+		NNRT_HIP(hipStreamSynchronize(s));
+	}
+	hipFreeAsync(flag, s);
+	if (st) return st;
+	if (host_flag) {
+		set_error("potrf failed in SolveBlockDiagonalCholesky (block not positive-definite)");
+		return NNRT_ERROR_NOT_POSITIVE_DEFINITE;
+	}
+	return NNRT_OK;
+}
+
+nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, const float* d_wing, const int32_t* d_coords, int32_t E, int32_t N,
+                                                       int32_t n0, const float* d_b, float* d_x, void* stream) {
+	NNRT_CHECK_ARG(n0 >= 0 && n0 <= N, "arrow_base_block_index out of range");
+	hipStream_t s = static_cast<hipStream_t>(stream);
+	std::vector<int32_t> coords(2 * static_cast<size_t>(E));
+	if (E > 0) {
+		NNRT_HIP(hipMemcpyAsync(coords.data(), d_coords, sizeof(int32_t) * 2 * E, hipMemcpyDeviceToHost, s));
+		NNRT_HIP(hipStreamSynchronize(s));
+	}
+	std::vector<int> counts(n0 + 1, 0), list(std::max(E, 1)), fill;
+	for (int e = 0; e < E; e++)
+		if (coords[2 * e] < n0) counts[coords[2 * e] + 1]++;
+	for (int i = 0; i < n0; i++) counts[i + 1] += counts[i];
+	fill.assign(counts.begin(), counts.end() - 1);
+	for (int e = 0; e < E; e++)
+		if (coords[2 * e] < n0) list[fill[coords[2 * e]]++] = e;
+	ArrowheadWorkspace ws;
+	ws.N = N;
+	ws.n0 = n0;
+	ws.E = E;
+	ws.m = 6 * (N - n0);
+	int* flag = nullptr;
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.dinv), sizeof(float) * 36 * std::max(n0, 1), s));
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.dinv_b), sizeof(float) * 36 * std::max(E, 1), s));
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.schur), sizeof(float) * std::max<int64_t>(static_cast<int64_t>(ws.m) * ws.m, 1), s));
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.edge_offsets), sizeof(int) * (n0 + 1), s));
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.edge_list), sizeof(int) * std::max(E, 1), s));
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&flag), sizeof(int), s));
+	NNRT_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
+	NNRT_HIP(hipMemcpyAsync(ws.edge_offsets, counts.data(), sizeof(int) * (n0 + 1), hipMemcpyHostToDevice, s));
+	NNRT_HIP(hipMemcpyAsync(ws.edge_list, list.data(), sizeof(int) * std::max(E, 1), hipMemcpyHostToDevice, s));
+	ws.diag = const_cast<float*>(d_diag);
+	ws.rhs = const_cast<float*>(d_b);
+	ws.x = d_x;
+	nnrt_status st = arrowhead_solve_core(ws, d_coords, d_wing, flag, s);
+	int host_flag = 0;
+	if (!st) {
+		NNRT_HIP(hipMemcpyAsync(&host_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
+		NNRT_HIP(hipStreamSynchronize(s));
+	}
+	for (void* p : {static_cast<void*>(ws.dinv), static_cast<void*>(ws.dinv_b), static_cast<void*>(ws.schur), static_cast<void*>(ws.edge_offsets),
+	                static_cast<void*>(ws.edge_list), static_cast<void*>(flag)})
+		hipFreeAsync(p, s);
+	if (st) return st;
+	if (host_flag) {
+		set_error("arrowhead solve: a stem block or the Schur complement is not positive-definite");
+		return NNRT_ERROR_NOT_POSITIVE_DEFINITE;
+	}
+	return NNRT_OK;
+}
+
+} // extern "C"

@@ -1,0 +1,486 @@
+// GN iteration kernels for gfx950 (DeformableMeshToImageFitter.cpp:111-275).
+//
+// k_fit_pixels fuses, per pixel, stages S3b-S10 of the reference loop: raster resolve, depth residual
+// (ComputeDepthResiduals :331-390), rasterized-surface Jacobians (RasterizedSurfaceJacobiansImpl.h:114-200),
+// pixel->node Jacobians (PixelVertexAnchorJacobiansImpl.h:179-363) and the block-diagonal data JtJ / Jt r reduction
+// (DeformableMeshToImageFitterImpl.h:199-456). The reference materialises [P,12,6] pixel Jacobians, [P,3,19] rasterized
+// Jacobians and [N,4000] node lists (capped: A4) and reduces each node serially; here each 16x16-pixel workgroup reduces
+// its pixels' per-node contributions (21 JtJ entries + 6 Jt r) in an LDS hash table and flushes them to HBM with one
+// float atomic per (node, entry) -- no intermediate tensors, no cap.
+#include "fitter_kernels.hpp"
+
+namespace nnrt {
+
+constexpr int PIX_TILE = 16;
+constexpr int PIX_BLOCK = PIX_TILE * PIX_TILE;
+constexpr int LDS_SLOTS = 128;
+
+template <int MODE>
+struct ModeTraits;
+template <>
+struct ModeTraits<NNRT_ITERATION_ALL> {
+	static constexpr int S = 6, NH = 21, NACC = 27;
+};
+template <>
+struct ModeTraits<NNRT_ITERATION_TRANSLATION_ONLY> {
+	static constexpr int S = 3, NH = 6, NACC = 9;
+};
+template <>
+struct ModeTraits<NNRT_ITERATION_ROTATION_ONLY> {
+	static constexpr int S = 3, NH = 6, NACC = 9;
+};
+
+__device__ inline int lds_find_slot(int* keys, int node) {
+	const unsigned h = (static_cast<unsigned>(node) * 2654435761u) >> (32 - 7);
+	for (int probe = 0; probe < LDS_SLOTS; probe++) {
+		const int s = (h + probe) & (LDS_SLOTS - 1);
+		const int k = __hip_atomic_load(keys + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+		if (k == node) return s;
+		if (k == -1) {
+			const int prev = atomicCAS(keys + s, -1, node);
+			if (prev == -1 || prev == node) return s;
+		}
+	}
+	return -1;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(PIX_BLOCK) void k_fit_pixels(FitPixelArgs a) {
+	using T = ModeTraits<MODE>;
+	constexpr int S = T::S;
+	__shared__ int s_keys[LDS_SLOTS];
+	__shared__ float s_acc[LDS_SLOTS * ACC_STRIDE];
+	for (int i = threadIdx.x; i < LDS_SLOTS; i += PIX_BLOCK) s_keys[i] = -1;
+	for (int i = threadIdx.x; i < LDS_SLOTS * ACC_STRIDE; i += PIX_BLOCK) s_acc[i] = 0.f;
+	__syncthreads();
+
+	// XCD-aware tile order: consecutive workgroups are dealt round-robin over the 8 XCDs, so give each XCD a contiguous
+	// band of tiles (neighbouring tiles share vertices, anchors and nodes -> L2 reuse within the XCD).
+	const int tiles = a.tiles_x * a.tiles_y;
+	const int per_xcd = (tiles + 7) / 8;
+	const int b = blockIdx.x;
+	const int tile = (b % 8) * per_xcd + b / 8;
+	const int tu = tile % a.tiles_x, tv = tile / a.tiles_x;
+	const int u = tu * PIX_TILE + static_cast<int>(threadIdx.x % PIX_TILE);
+	const int v = tv * PIX_TILE + static_cast<int>(threadIdx.x / PIX_TILE);
+	const bool in_image = tile < tiles && u < a.W && v < a.H;
+	const int64_t p = static_cast<int64_t>(v) * a.W + u;
+
+	if (in_image) {
+		const uint64_t key = a.keys[p];
+		a.keys[p] = EMPTY_KEY;   // ready for the next iteration's scatter
+		int32_t face = -1;
+		RasterHit h{0.f, 0.f, 0.f, 0.f, 0.f};
+		f3 V3[3], N3[3];
+		FaceNdc fn;
+		int vid[3] = {0, 0, 0};
+		const float px = pixel_to_ndc(u, a.W, a.H), py = pixel_to_ndc(v, a.H, a.W);
+		if (key != EMPTY_KEY) {
+			face = static_cast<int32_t>(key & 0xffffffffu);
+			const int4 fi = a.faces4[face];
+			vid[0] = fi.x;
+			vid[1] = fi.y;
+			vid[2] = fi.z;
+#pragma unroll
+			for (int i = 0; i < 3; i++) {
+				const float4 wp = a.wpos[vid[i]];
+				const float4 wn = a.wnrm[vid[i]];
+				V3[i] = make3(wp.x, wp.y, wp.z);
+				N3[i] = make3(wn.x, wn.y, wn.z);
+				a.ndc.ndc.project(V3[i].x, V3[i].y, V3[i].z, &fn.x[i], &fn.y[i]);
+				fn.z[i] = V3[i].z;
+			}
+			if (!face_test(fn, px, py, a.blur, a.perspective, false, true, h)) face = -1;
+		}
+		// ---- ComputeDepthResiduals (:331-390) ----
+		const float depth = face >= 0 ? h.depth : -1.f;
+		const bool rendered_valid = depth > 0 && depth < a.max_depth;
+		f3 nl = make3(0.f, 0.f, 0.f), prast = make3(0.f, 0.f, 0.f);
+		if (face >= 0) {
+			float acc;
+			acc = 0.0f;
+			acc += h.b0 * N3[0].x;
+			acc += h.b1 * N3[1].x;
+			acc += h.b2 * N3[2].x;
+			nl.x = acc;
+			acc = 0.0f;
+			acc += h.b0 * N3[0].y;
+			acc += h.b1 * N3[1].y;
+			acc += h.b2 * N3[2].y;
+			nl.y = acc;
+			acc = 0.0f;
+			acc += h.b0 * N3[0].z;
+			acc += h.b1 * N3[1].z;
+			acc += h.b2 * N3[2].z;
+			nl.z = acc;
+		}
+		if (rendered_valid) {
+			prast = make3((static_cast<float>(u) - a.pix.cx) * depth / a.pix.fx, (static_cast<float>(v) - a.pix.cy) * depth / a.pix.fy, depth);
+		}
+		const float dref = a.ref_depth[p];
+		f3 q = make3(0.f, 0.f, 0.f);
+		const bool ref_valid = dref > 0.f;
+		if (ref_valid) q = make3((static_cast<float>(u) - a.pix.cx) * dref / a.pix.fx, (static_cast<float>(v) - a.pix.cy) * dref / a.pix.fy, dref);
+		const bool mask = ref_valid && rendered_valid;
+		const f3 d = sub3(prast, q);   // point map vector w_l - o_l
+		float dist = dot3(nl, d);
+		if (!mask) dist = 0.0f;
+		float residual = dist;
+		if (a.use_tukey) {
+			const float c = a.tukey_c;
+			const float c6 = (c * c / 6.f);
+			const float qq = dist / c;
+			const float left = 1.f - (qq * qq);
+			residual = c6 * (1.f - left * left * left);
+			if (dist <= c) residual = c6;   // (:384-385 as written: A8)
+		}
+		a.residuals[p] = residual;
+		a.residual_mask[p] = mask ? 1 : 0;
+		a.pixel_face[p] = face;
+
+		bool contributes = mask;
+		f3 dr_dwl = nl, dr_dnl = d;
+		if (contributes && a.use_tukey) {
+			const float r = dot3(nl, d);
+			if (fabsf(r) > a.tukey_c) contributes = false;
+			const float qq = r / a.tukey_c;
+			float psi = 1 - qq * qq;
+			psi = r * psi * psi;
+			dr_dnl = make3(psi * d.x, psi * d.y, psi * d.z);
+			dr_dwl = make3(psi * nl.x, psi * nl.y, psi * nl.z);
+		}
+		if (contributes) {
+			// ---- rasterized surface Jacobians (RasterizedSurfaceJacobiansImpl.h:114-200) ----
+			const float rho[3] = {h.b0, h.b1, h.b2};
+			float A, sa[3], drho[3] = {0.f, 0.f, 0.f};
+			A = spa_cw(fn.x[0], fn.y[0], fn.x[1], fn.y[1], fn.x[2], fn.y[2]) + K_EPSILON;
+			if (a.perspective) {
+				sa[0] = spa_cw(px, py, fn.x[1], fn.y[1], fn.x[2], fn.y[2]);
+				sa[1] = spa_cw(px, py, fn.x[2], fn.y[2], fn.x[0], fn.y[0]);
+				sa[2] = spa_cw(px, py, fn.x[0], fn.y[0], fn.x[1], fn.y[1]);
+#pragma unroll
+				for (int i = 0; i < 3; i++) drho[i] = sa[i] / A;
+			} else {
+#pragma unroll
+				for (int i = 0; i < 3; i++) sa[i] = rho[i] * A;
+			}
+			// d rho / d ndc (BarycentricCoordinateJacobians.h:85-181)
+			const float den = A * A + K_EPSILON;
+			const float dA[3][2] = {{fn.y[1] - fn.y[2], fn.x[2] - fn.x[1]}, {fn.y[2] - fn.y[0], fn.x[0] - fn.x[2]}, {fn.y[0] - fn.y[1], fn.x[1] - fn.x[0]}};
+			// sub-area derivatives: (p, va, vb) -> d/dva = (vb.y - p.y, p.x - vb.x), d/dvb = (p.y - va.y, va.x - p.x)
+			const float s0a[2] = {fn.y[2] - py, px - fn.x[2]}, s0b[2] = {py - fn.y[1], fn.x[1] - px};   // (p, v1, v2)
+			const float s1a[2] = {fn.y[0] - py, px - fn.x[0]}, s1b[2] = {py - fn.y[2], fn.x[2] - px};   // (p, v2, v0)
+			const float s2a[2] = {fn.y[1] - py, px - fn.x[1]}, s2b[2] = {py - fn.y[0], fn.x[0] - px};   // (p, v0, v1)
+			float Dn[3][3][2];
+#pragma unroll
+			for (int c = 0; c < 2; c++) {
+				Dn[0][0][c] = (-sa[0] * dA[0][c]) / den;
+				Dn[1][0][c] = (A * s0a[c] - sa[0] * dA[1][c]) / den;
+				Dn[2][0][c] = (A * s0b[c] - sa[0] * dA[2][c]) / den;
+				Dn[0][1][c] = (A * s1b[c] - sa[1] * dA[0][c]) / den;
+				Dn[1][1][c] = (-sa[1] * dA[1][c]) / den;
+				Dn[2][1][c] = (A * s1a[c] - sa[1] * dA[2][c]) / den;
+				Dn[0][2][c] = (A * s2a[c] - sa[2] * dA[0][c]) / den;
+				Dn[1][2][c] = (A * s2b[c] - sa[2] * dA[1][c]) / den;
+				Dn[2][2][c] = (-sa[2] * dA[2][c]) / den;
+			}
+			float J[3][9];
+#pragma unroll
+			for (int i = 0; i < 3; i++) {
+				const float z = V3[i].z;
+				const float z2 = z * z;
+				const float P0[3] = {a.ndc.ndc.fx / z, 0.f, -a.ndc.ndc.fx * V3[i].x / z2};
+				const float P1[3] = {0.f, a.ndc.ndc.fy / z, -a.ndc.ndc.fy * V3[i].y / z2};
+#pragma unroll
+				for (int r = 0; r < 3; r++)
+#pragma unroll
+					for (int c = 0; c < 3; c++) J[r][3 * i + c] = Dn[i][r][0] * P0[c] + Dn[i][r][1] * P1[c];
+			}
+			if (a.perspective) {
+				const float z0 = V3[0].z, z1 = V3[1].z, z2 = V3[2].z;
+				const float v12 = z1 * z2, v02 = z0 * z2, v01 = z0 * z1;
+				const float n0 = drho[0] * v12, n1 = drho[1] * v02, n2 = drho[2] * v01;
+				const float dd = fmaxf(n0 + n1 + n2, K_EPSILON);
+				const float dd2 = dd * dd;
+				float Pd[3][3] = {{(dd - n0) * v12, -n0 * v02, -n0 * v01}, {-n1 * v12, (dd - n1) * v02, -n1 * v01}, {-n2 * v12, -n2 * v02, (dd - n2) * v01}};
+				const float pz0 = drho[1] * z2 + z1 * drho[2];
+				const float pz1 = drho[0] * z2 + z0 * drho[2];
+				const float pz2 = drho[0] * z1 + z0 * drho[1];
+				float Pz[3][3] = {{-n0 * pz0, dd * drho[0] * z2 - n0 * pz1, dd * drho[0] * z1 - n0 * pz2},
+				                  {dd * drho[1] * z2 - n1 * pz0, -n1 * pz1, dd * drho[1] * z0 - n1 * pz2},
+				                  {dd * drho[2] * z1 - n2 * pz0, dd * drho[2] * z0 - n2 * pz1, -n2 * pz2}};
+#pragma unroll
+				for (int r = 0; r < 3; r++)
+#pragma unroll
+					for (int c = 0; c < 3; c++) {
+						Pd[r][c] /= dd2;
+						Pz[r][c] /= dd2;
+					}
+				float J2[3][9];
+#pragma unroll
+				for (int r = 0; r < 3; r++)
+#pragma unroll
+					for (int c = 0; c < 9; c++) J2[r][c] = (Pd[r][0] * J[0][c] + Pd[r][1] * J[1][c]) + Pd[r][2] * J[2][c];
+#pragma unroll
+				for (int r = 0; r < 3; r++)
+#pragma unroll
+					for (int i = 0; i < 3; i++) J2[r][3 * i + 2] += Pz[r][i];
+#pragma unroll
+				for (int r = 0; r < 3; r++)
+#pragma unroll
+					for (int c = 0; c < 9; c++) J[r][c] = J2[r][c];
+			}
+			// dr/dV = dr/dwl * dwl/dV + dr/dnl * dnl/dV ; dr/dN = dr/dnl (rho (x) I)
+			float dr_dV[9];
+			const float Vr[3][3] = {{V3[0].x, V3[0].y, V3[0].z}, {V3[1].x, V3[1].y, V3[1].z}, {V3[2].x, V3[2].y, V3[2].z}};
+			const float Nr[3][3] = {{N3[0].x, N3[0].y, N3[0].z}, {N3[1].x, N3[1].y, N3[1].z}, {N3[2].x, N3[2].y, N3[2].z}};
+			const float rw[3] = {dr_dwl.x, dr_dwl.y, dr_dwl.z}, rn[3] = {dr_dnl.x, dr_dnl.y, dr_dnl.z};
+#pragma unroll
+			for (int c = 0; c < 9; c++) {
+				float w_rc[3], n_rc[3];
+#pragma unroll
+				for (int r = 0; r < 3; r++) {
+					w_rc[r] = (Vr[0][r] * J[0][c] + Vr[1][r] * J[1][c]) + Vr[2][r] * J[2][c];
+					if (c / 3 * 3 + r == c) w_rc[r] += rho[c / 3];
+					n_rc[r] = (Nr[0][r] * J[0][c] + Nr[1][r] * J[1][c]) + Nr[2][r] * J[2][c];
+				}
+				const float x = (rw[0] * w_rc[0] + rw[1] * w_rc[1]) + rw[2] * w_rc[2];
+				const float y = (rn[0] * n_rc[0] + rn[1] * n_rc[1]) + rn[2] * n_rc[2];
+				dr_dV[c] = x + y;
+			}
+			// ---- pixel -> node Jacobians (PixelVertexAnchorJacobiansImpl.h:229-363), merged per unique node ----
+			const int KA = a.anchor_count;
+			int anc[3][MAX_ANCHORS];
+#pragma unroll
+			for (int fv = 0; fv < 3; fv++)
+#pragma unroll
+				for (int k = 0; k < MAX_ANCHORS; k++) anc[fv][k] = (k < KA) ? a.anchors[static_cast<int64_t>(vid[fv]) * KA + k] : -1;
+			const float r_used = residual;
+#pragma unroll
+			for (int fv0 = 0; fv0 < 3; fv0++) {
+#pragma unroll
+				for (int k0 = 0; k0 < MAX_ANCHORS; k0++) {
+					const int node = anc[fv0][k0];
+					if (node < 0) continue;
+					// first occurrence only (the reference keeps one face-anchor per unique node, in first-appearance order)
+					bool seen = false;
+#pragma unroll
+					for (int fv1 = 0; fv1 <= fv0; fv1++)
+#pragma unroll
+						for (int k1 = 0; k1 < MAX_ANCHORS; k1++)
+							if ((fv1 < fv0 || k1 < k0) && anc[fv1][k1] == node) seen = true;
+					if (seen) continue;
+					float jr[3] = {0.f, 0.f, 0.f}, jt[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+					for (int fv = fv0; fv < 3; fv++) {
+#pragma unroll
+						for (int k = 0; k < MAX_ANCHORS; k++) {
+							if (anc[fv][k] != node) continue;
+							const int64_t vk = static_cast<int64_t>(vid[fv]) * KA + k;
+							const float4 jv = a.jv[vk];
+							const f3 dv = make3(dr_dV[3 * fv], dr_dV[3 * fv + 1], dr_dV[3 * fv + 2]);
+							if (MODE != NNRT_ITERATION_ROTATION_ONLY) {
+								jt[0] += dv.x * jv.w;
+								jt[1] += dv.y * jv.w;
+								jt[2] += dv.z * jv.w;
+							}
+							if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) {
+								const float4 jn = a.jn[vk];
+								const f3 dn = make3(rn[0] * rho[fv], rn[1] * rho[fv], rn[2] * rho[fv]);
+								const f3 t1 = row_times_skew(dv, make3(jv.x, jv.y, jv.z));
+								const f3 t2 = row_times_skew(dn, make3(jn.x, jn.y, jn.z));
+								jr[0] += t1.x + t2.x;
+								jr[1] += t1.y + t2.y;
+								jr[2] += t1.z + t2.z;
+							}
+						}
+					}
+					float Jn[S];
+					if (MODE == NNRT_ITERATION_ALL) {
+						Jn[0] = jr[0];
+						Jn[1] = jr[1];
+						Jn[2] = jr[2];
+						Jn[3 % S] = jt[0];
+						Jn[4 % S] = jt[1];
+						Jn[5 % S] = jt[2];
+					} else if (MODE == NNRT_ITERATION_TRANSLATION_ONLY) {
+						Jn[0] = jt[0];
+						Jn[1] = jt[1];
+						Jn[2] = jt[2];
+					} else {
+						Jn[0] = jr[0];
+						Jn[1] = jr[1];
+						Jn[2] = jr[2];
+					}
+					// ---- accumulate JJ^T (upper triangle) and J r into the workgroup's LDS table ----
+					float vals[T::NACC];
+					int e = 0;
+#pragma unroll
+					for (int c0 = 0; c0 < S; c0++)
+#pragma unroll
+						for (int c1 = c0; c1 < S; c1++) vals[e++] = Jn[c0] * Jn[c1];
+#pragma unroll
+					for (int c = 0; c < S; c++) vals[T::NH + c] = Jn[c] * r_used;
+					const int slot = lds_find_slot(s_keys, node);
+					if (slot >= 0) {
+						float* dst = s_acc + slot * ACC_STRIDE;
+#pragma unroll
+						for (int k = 0; k < T::NACC; k++) atomicAdd(dst + k, vals[k]);
+					} else {   // table full: fall back to global atomics (correct, slower)
+						float* dst = a.acc + static_cast<int64_t>(node) * ACC_STRIDE;
+#pragma unroll
+						for (int k = 0; k < T::NACC; k++) atomicAdd(dst + k, vals[k]);
+					}
+				}
+			}
+		}
+	}
+	__syncthreads();
+	for (int i = threadIdx.x; i < LDS_SLOTS * T::NACC; i += PIX_BLOCK) {
+		const int s = i / T::NACC, k = i % T::NACC;
+		const int node = s_keys[s];
+		if (node >= 0) atomicAdd(a.acc + static_cast<int64_t>(node) * ACC_STRIDE + k, s_acc[s * ACC_STRIDE + k]);
+	}
+}
+
+nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t stream) {
+	const int tiles = args.tiles_x * args.tiles_y;
+	const unsigned grid = static_cast<unsigned>(((tiles + 7) / 8) * 8);
+	switch (mode) {
+		case NNRT_ITERATION_ALL: k_fit_pixels<NNRT_ITERATION_ALL><<<grid, PIX_BLOCK, 0, stream>>>(args); break;
+		case NNRT_ITERATION_TRANSLATION_ONLY: k_fit_pixels<NNRT_ITERATION_TRANSLATION_ONLY><<<grid, PIX_BLOCK, 0, stream>>>(args); break;
+		case NNRT_ITERATION_ROTATION_ONLY: k_fit_pixels<NNRT_ITERATION_ROTATION_ONLY><<<grid, PIX_BLOCK, 0, stream>>>(args); break;
+		default: set_error("unknown iteration mode"); return NNRT_ERROR_ARGUMENT;
+	}
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+// =====================================================================================================================
+// Block-diagonal LM solve + update (S11 no-edge path + S12): PreconditionDiagonalBlocksImpl.h, SolveBlockDiagonalCholesky
+// (potrf + 2 trsm per block), RodriguesImpl.h:66-88, HierarchicalGraphWarpField::TranslateNodes/RotateNodes (:261-282:
+// t += dt, R <- R * dR). One thread per node; consumes and re-zeroes the accumulator row.
+// =====================================================================================================================
+template <int MODE>
+__device__ inline void apply_update(float* ns, const float* x) {
+	if (MODE == NNRT_ITERATION_ALL) {
+		ns[3] += x[3];
+		ns[4] += x[4];
+		ns[5] += x[5];
+	} else if (MODE == NNRT_ITERATION_TRANSLATION_ONLY) {
+		ns[3] += x[0];
+		ns[4] += x[1];
+		ns[5] += x[2];
+	}
+	if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) {
+		float dR[9], R[9], o[9];
+		rodrigues_device(x[0], x[1], x[2], dR);
+#pragma unroll
+		for (int i = 0; i < 9; i++) R[i] = ns[6 + i];
+#pragma unroll
+		for (int r = 0; r < 3; r++)
+#pragma unroll
+			for (int c = 0; c < 3; c++) o[3 * r + c] = (R[3 * r] * dR[c] + R[3 * r + 1] * dR[3 + c]) + R[3 * r + 2] * dR[6 + c];
+#pragma unroll
+		for (int i = 0; i < 9; i++) ns[6 + i] = o[i];
+	}
+}
+
+template <int MODE>
+__global__ void k_solve_update(SolveArgs a) {
+	using T = ModeTraits<MODE>;
+	constexpr int S = T::S;
+	const int n = blockIdx.x * blockDim.x + threadIdx.x;
+	if (n >= a.N) return;
+	float* acc = a.acc + static_cast<int64_t>(n) * ACC_STRIDE;
+	float H[S][S], g[S];
+	int e = 0;
+#pragma unroll
+	for (int c0 = 0; c0 < S; c0++)
+#pragma unroll
+		for (int c1 = c0; c1 < S; c1++) {
+			H[c0][c1] = acc[e];
+			H[c1][c0] = acc[e];
+			e++;
+		}
+#pragma unroll
+	for (int c = 0; c < S; c++) g[c] = 0.f - acc[T::NH + c];
+#pragma unroll
+	for (int k = 0; k < T::NACC; k++) acc[k] = 0.f;
+	if (a.hessian_out) {
+#pragma unroll
+		for (int r = 0; r < S; r++)
+#pragma unroll
+			for (int c = 0; c < S; c++) a.hessian_out[static_cast<int64_t>(n) * S * S + r * S + c] = H[r][c];
+	}
+#pragma unroll
+	for (int c = 0; c < S; c++) a.gradient_out[static_cast<int64_t>(n) * S + c] = g[c];
+	if (a.lm > 0.f) {
+#pragma unroll
+		for (int i = 0; i < S; i++) H[i][i] += a.lm;
+	}
+	float x[S];
+	if (!cholesky_small<S>(H)) {
+		atomicOr(a.error_flag, 1);
+#pragma unroll
+		for (int c = 0; c < S; c++) x[c] = NAN;
+	} else {
+#pragma unroll
+		for (int c = 0; c < S; c++) x[c] = g[c];
+		cholesky_solve_small<S>(H, x);
+	}
+#pragma unroll
+	for (int c = 0; c < S; c++) a.updates_out[static_cast<int64_t>(n) * S + c] = x[c];
+	apply_update<MODE>(a.node_state + static_cast<int64_t>(n) * NODE_STRIDE, x);
+}
+
+nnrt_status launch_solve_update(int mode, const SolveArgs& args, hipStream_t stream) {
+	const unsigned grid = static_cast<unsigned>(ceil_div(args.N, 256));
+	switch (mode) {
+		case NNRT_ITERATION_ALL: k_solve_update<NNRT_ITERATION_ALL><<<grid, 256, 0, stream>>>(args); break;
+		case NNRT_ITERATION_TRANSLATION_ONLY: k_solve_update<NNRT_ITERATION_TRANSLATION_ONLY><<<grid, 256, 0, stream>>>(args); break;
+		case NNRT_ITERATION_ROTATION_ONLY: k_solve_update<NNRT_ITERATION_ROTATION_ONLY><<<grid, 256, 0, stream>>>(args); break;
+		default: set_error("unknown iteration mode"); return NNRT_ERROR_ARGUMENT;
+	}
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+// generic block-diagonal Cholesky solve (API stage entry point)
+template <int S>
+__global__ void k_block_diag_solve(const float* __restrict__ blocks, const float* __restrict__ b, int count, float* __restrict__ x,
+                                   int* error_flag) {
+	const int n = blockIdx.x * blockDim.x + threadIdx.x;
+	if (n >= count) return;
+	float H[S][S], y[S];
+#pragma unroll
+	for (int r = 0; r < S; r++) {
+#pragma unroll
+		for (int c = 0; c < S; c++) H[r][c] = blocks[static_cast<int64_t>(n) * S * S + r * S + c];
+		y[r] = b[static_cast<int64_t>(n) * S + r];
+	}
+	if (!cholesky_small<S>(H)) {
+		atomicOr(error_flag, 1);
+#pragma unroll
+		for (int r = 0; r < S; r++) y[r] = NAN;
+	} else {
+		cholesky_solve_small<S>(H, y);
+	}
+#pragma unroll
+	for (int r = 0; r < S; r++) x[static_cast<int64_t>(n) * S + r] = y[r];
+}
+
+nnrt_status launch_solve_block_diagonal(const float* blocks, const float* b, int count, int s, float* x, int* error_flag, hipStream_t stream) {
+	if (count == 0) return NNRT_OK;
+	const unsigned grid = static_cast<unsigned>(ceil_div(count, 256));
+	if (s == 6) k_block_diag_solve<6><<<grid, 256, 0, stream>>>(blocks, b, count, x, error_flag);
+	else if (s == 3) k_block_diag_solve<3><<<grid, 256, 0, stream>>>(blocks, b, count, x, error_flag);
+	else {
+		set_error("block size must be 3 or 6");
+		return NNRT_ERROR_ARGUMENT;
+	}
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+} // namespace nnrt

@@ -1,0 +1,84 @@
+// Argument blocks of the GN-iteration kernels (passed by value; stable pointers so iterations can be hipGraph-captured).
+#pragma once
+
+#include "kernels.hpp"
+
+namespace nnrt {
+
+constexpr int ACC_STRIDE = 28;   // per node: 21 JtJ upper-triangle entries + 6 Jt r (+1 pad); 3-dof modes use 6 + 3
+
+struct FitPixelArgs {
+	int H, W, tiles_x, tiles_y;
+	Camera pix;             // pixel-space intrinsics (float)
+	NdcSetup ndc;
+	float blur;             // NDC units
+	int perspective;
+	float max_depth;
+	int use_tukey;
+	float tukey_c;
+	int anchor_count;
+	uint64_t* keys;         // [P] raster keys (consumed and reset)
+	const int4* faces4;     // [F]
+	const float4* wpos;     // [V] warped positions
+	const float4* wnrm;     // [V] warped normals
+	const int32_t* anchors; // [V,K]
+	const float4* jv;       // [V,K] (-w R (v-g), w)
+	const float4* jn;       // [V,K] (-w R n, 0)
+	const float* ref_depth; // [P] reference depth / scale, 0 where the reference point is masked out
+	float* residuals;       // [P]
+	uint8_t* residual_mask; // [P]
+	int32_t* pixel_face;    // [P]
+	float* acc;             // [N, ACC_STRIDE]
+};
+
+struct SolveArgs {
+	int N;
+	float lm;
+	float* acc;
+	float* node_state;
+	float* updates_out;     // [N*s]
+	float* gradient_out;    // [N*s]
+	float* hessian_out;     // [N*s*s] (nullable)
+	int* error_flag;
+};
+
+nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t stream);
+nnrt_status launch_solve_update(int mode, const SolveArgs& args, hipStream_t stream);
+
+// ARAP (regularized, mode ALL) path
+struct ArapArgs {
+	int E, N, n0;
+	float lambda;
+	int use_huber;
+	float huber_delta;
+	int coverage_variable;          // 1: edge weight = max(c2_i, c2_j)
+	const int32_t* edges;           // [E,2] virtual
+	const int8_t* edge_layers;      // [E]
+	const float* radii;             // [layers]
+	const float* node_weights;      // [N] (variable coverage)
+	const float* node_state;        // [N,16]
+	float* acc;                     // [N, ACC_STRIDE]: ARAP diagonal JtJ and -(-J^T e) added (acc stores +J^T r)
+	float* wing;                    // [E,36]: dEi^T dEj
+	float* edge_residuals;          // [3E]
+	int* error_flag;
+};
+nnrt_status launch_arap_edges(const ArapArgs& args, hipStream_t stream);
+
+struct ArrowheadWorkspace {
+	int N = 0, n0 = 0, E = 0, m = 0;
+	float* diag = nullptr;      // [N,36] full diagonal blocks (with LM)
+	float* dinv = nullptr;      // [n0,36]
+	float* dinv_b = nullptr;    // [E,36]
+	float* schur = nullptr;     // [m,m]
+	float* rhs = nullptr;       // [6N] negative gradient
+	float* x = nullptr;         // [6N]
+	int* edge_offsets = nullptr;// [n0+1] CSR of stem edges by source node (edges grouped by source)
+	int* edge_list = nullptr;   // [E]
+};
+// acc -> diagonal blocks (+lm) + rhs ; arrowhead solve ; update node state
+nnrt_status launch_arrowhead_iteration(const ArrowheadWorkspace& ws, const float* acc, float lm, const int32_t* edges, const float* wing,
+                                       float* node_state, float* acc_mut, float* updates_out, float* gradient_out, float* hessian_out,
+                                       int* error_flag, hipStream_t stream);
+nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* edges, const float* wing, int* error_flag, hipStream_t stream);
+
+} // namespace nnrt

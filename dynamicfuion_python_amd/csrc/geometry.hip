@@ -1,0 +1,363 @@
+// Geometry stages of the hot path on gfx950: anchors (once per frame), mesh warp (+ warped-surface Jacobians),
+// NDC face extraction, depth unprojection, attribute interpolation, Rodrigues.
+#include "kernels.hpp"
+
+namespace nnrt {
+
+// =====================================================================================================================
+// Anchors: brute-force K-NN in ascending node order with replace-the-current-maximum insertion
+// (cpp/core/kernel/KnnUtilities.h:64-117) + Gaussian weights (WarpUtilities.h:34-247, WarpAnchorComputationImpl.h:42-140).
+// One thread per point; node positions are staged through LDS in chunks shared by the workgroup.
+// =====================================================================================================================
+constexpr int ANCHOR_BLOCK = 256;
+constexpr int ANCHOR_CHUNK = 2048;
+
+template <int K>
+__global__ __launch_bounds__(ANCHOR_BLOCK) void k_compute_anchors(const float* __restrict__ points, int64_t point_count,
+                                                                    const float* __restrict__ nodes, int node_count,
+                                                                    float coverage_squared, const float* __restrict__ node_weights,
+                                                                    int minimum_valid, int32_t* __restrict__ anchors,
+                                                                    float* __restrict__ weights) {
+	__shared__ float s_nodes[ANCHOR_CHUNK * 3];
+	const int64_t i = static_cast<int64_t>(blockIdx.x) * ANCHOR_BLOCK + threadIdx.x;
+	const bool active = i < point_count;
+	float px = 0.f, py = 0.f, pz = 0.f;
+	if (active) {
+		px = points[3 * i];
+		py = points[3 * i + 1];
+		pz = points[3 * i + 2];
+	}
+	int32_t idx[K];
+	float d2[K];
+#pragma unroll
+	for (int k = 0; k < K; k++) {
+		idx[k] = -1;
+		d2[k] = INFINITY;
+	}
+	int max_at = 0;
+	float maxd = INFINITY;
+	for (int base = 0; base < node_count; base += ANCHOR_CHUNK) {
+		const int count = min(ANCHOR_CHUNK, node_count - base);
+		__syncthreads();
+		for (int j = threadIdx.x; j < count * 3; j += ANCHOR_BLOCK) s_nodes[j] = nodes[3 * static_cast<int64_t>(base) + j];
+		__syncthreads();
+		if (!active) continue;
+		for (int j = 0; j < count; j++) {
+			const float dx = s_nodes[3 * j] - px, dy = s_nodes[3 * j + 1] - py, dz = s_nodes[3 * j + 2] - pz;
+			const float sq = (dx * dx + dy * dy) + dz * dz;
+			if (sq < maxd) {
+#pragma unroll
+				for (int k = 0; k < K; k++) {
+					if (k == max_at) {
+						d2[k] = sq;
+						idx[k] = base + j;
+					}
+				}
+				max_at = 0;
+				maxd = d2[0];
+#pragma unroll
+				for (int k = 1; k < K; k++) {
+					if (d2[k] > maxd) {
+						max_at = k;
+						maxd = d2[k];
+					}
+				}
+			}
+		}
+	}
+	if (!active) return;
+	float w[K];
+	float sum = 0.f;
+	int valid = 0;
+	bool normalize = true;
+	if (minimum_valid > 0) {
+#pragma unroll
+		for (int k = 0; k < K; k++) {
+			const float c2 = node_weights ? node_weights[idx[k]] : coverage_squared;
+			w[k] = d2[k];   // reference repurposes the weight array for squared distances
+			if (d2[k] > 4 * c2) {
+				idx[k] = -1;
+				continue;
+			}
+			const float wt = exp_cr(-d2[k] / (2 * c2));
+			sum += wt;
+			w[k] = wt;
+			valid++;
+		}
+		if (valid < minimum_valid) normalize = false;   // WarpUtilities.h:242-244
+	} else {
+#pragma unroll
+		for (int k = 0; k < K; k++) {
+			const float c2 = node_weights ? node_weights[idx[k]] : coverage_squared;
+			const float wt = exp_cr(-d2[k] / (2 * c2));
+			sum += wt;
+			w[k] = wt;
+		}
+		valid = K;
+	}
+	if (normalize) {
+		if (sum > 0.0f) {
+#pragma unroll
+			for (int k = 0; k < K; k++) w[k] /= sum;
+		} else if (valid > 0) {
+#pragma unroll
+			for (int k = 0; k < K; k++) w[k] = 1.0f / static_cast<float>(valid);
+		}
+	}
+#pragma unroll
+	for (int k = 0; k < K; k++) {
+		anchors[i * K + k] = idx[k];
+		weights[i * K + k] = w[k];
+	}
+}
+
+nnrt_status launch_compute_anchors(const float* points, int64_t V, const float* nodes, int N, int K, float coverage,
+                                   const float* node_weights, int minimum_valid, int32_t* anchors, float* weights, hipStream_t stream) {
+	NNRT_CHECK_ARG(K >= 1 && K <= MAX_ANCHORS, "anchor_count must be in [1, 8]");
+	NNRT_CHECK_ARG(N >= K, "anchor count exceeds node count");
+	if (V == 0) return NNRT_OK;
+	const dim3 grid(static_cast<unsigned>(ceil_div(V, ANCHOR_BLOCK)));
+	const float c2 = coverage * coverage;
+#define NNRT_ANCHOR_CASE(KK)                                                                                                 \
+	case KK:                                                                                                                 \
+		k_compute_anchors<KK><<<grid, ANCHOR_BLOCK, 0, stream>>>(points, V, nodes, N, c2, node_weights, minimum_valid, anchors, weights); \
+		break;
+	switch (K) {
+		NNRT_ANCHOR_CASE(1)
+		NNRT_ANCHOR_CASE(2)
+		NNRT_ANCHOR_CASE(3)
+		NNRT_ANCHOR_CASE(4)
+		NNRT_ANCHOR_CASE(5)
+		NNRT_ANCHOR_CASE(6)
+		NNRT_ANCHOR_CASE(7)
+		NNRT_ANCHOR_CASE(8)
+	}
+#undef NNRT_ANCHOR_CASE
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+// =====================================================================================================================
+// Warp + warped-surface Jacobians, fused (S1 + S6). One thread per vertex.
+//   warped point  v' = sum_k w_k (g_k + R_k (E v - g_k) + t_k)        Warp3dPointsAndNormalsImpl.h:334-390, WarpUtilities.h:448-467
+//   warped normal n' = sum_k w_k R_k (E_R n)    (not normalized: A12)
+//   Jv[v,k] = (-w R_k (v - g_k), w) ; Jn[v,k] = -w R_k n   (canonical v, n)   WarpedSurfaceJacobiansImpl.h:117-156
+// Outputs: float4 warped positions / normals [V] (w unused), Jv/Jn float4 [V,K] (internal layout).
+// =====================================================================================================================
+__global__ __launch_bounds__(256) void k_warp_mesh(const float* __restrict__ points, const float* __restrict__ normals, int64_t V,
+                                                   const float* __restrict__ node_state, const int32_t* __restrict__ anchors,
+                                                   const float* __restrict__ weights, int K, WarpExtrinsics E, float4* __restrict__ out_p,
+                                                   float4* __restrict__ out_n, float4* __restrict__ jv, float4* __restrict__ jn) {
+	const int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (v >= V) return;
+	const f3 p = make3(points[3 * v], points[3 * v + 1], points[3 * v + 2]);
+	const f3 n = make3(normals[3 * v], normals[3 * v + 1], normals[3 * v + 2]);
+	f3 pc = p, nc = n;
+	if (!E.identity) {
+		pc = make3(((p.x * E.m[0] + p.y * E.m[1]) + p.z * E.m[2]) + E.m[3], ((p.x * E.m[4] + p.y * E.m[5]) + p.z * E.m[6]) + E.m[7],
+		           ((p.x * E.m[8] + p.y * E.m[9]) + p.z * E.m[10]) + E.m[11]);
+		nc = make3((n.x * E.m[0] + n.y * E.m[1]) + n.z * E.m[2], (n.x * E.m[4] + n.y * E.m[5]) + n.z * E.m[6],
+		           (n.x * E.m[8] + n.y * E.m[9]) + n.z * E.m[10]);
+	}
+	f3 wp = make3(0.f, 0.f, 0.f), wn = make3(0.f, 0.f, 0.f);
+	for (int k = 0; k < K; k++) {
+		const int32_t a = anchors[v * K + k];
+		float4 ojv = make_float4(0.f, 0.f, 0.f, 0.f), ojn = make_float4(0.f, 0.f, 0.f, 0.f);
+		if (a != -1) {
+			const float w = weights[v * K + k];
+			const float* ns = node_state + static_cast<int64_t>(a) * NODE_STRIDE;
+			const f3 g = make3(ns[0], ns[1], ns[2]);
+			const f3 t = make3(ns[3], ns[4], ns[5]);
+			const float* R = ns + 6;
+			const f3 Rd = matvec3(R, sub3(pc, g));
+			wp.x += w * ((g.x + Rd.x) + t.x);
+			wp.y += w * ((g.y + Rd.y) + t.y);
+			wp.z += w * ((g.z + Rd.z) + t.z);
+			const f3 Rn = matvec3(R, nc);
+			wn.x += w * Rn.x;
+			wn.y += w * Rn.y;
+			wn.z += w * Rn.z;
+			if (jv) {
+				const f3 Rj = E.identity ? Rd : matvec3(R, sub3(p, g));
+				const f3 Rnj = E.identity ? Rn : matvec3(R, n);
+				ojv = make_float4(-w * Rj.x, -w * Rj.y, -w * Rj.z, w);
+				ojn = make_float4(-w * Rnj.x, -w * Rnj.y, -w * Rnj.z, 0.f);
+			}
+		}
+		if (jv) {
+			jv[v * K + k] = ojv;
+			jn[v * K + k] = ojn;
+		}
+	}
+	out_p[v] = make_float4(wp.x, wp.y, wp.z, 0.f);
+	out_n[v] = make_float4(wn.x, wn.y, wn.z, 0.f);
+}
+
+nnrt_status launch_warp_mesh(const float* points, const float* normals, int64_t V, const float* node_state, const int32_t* anchors,
+                             const float* weights, int K, const WarpExtrinsics& E, float4* out_p, float4* out_n, float4* jv, float4* jn,
+                             hipStream_t stream) {
+	if (V == 0) return NNRT_OK;
+	k_warp_mesh<<<static_cast<unsigned>(ceil_div(V, 256)), 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p,
+	                                                                          out_n, jv, jn);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+__global__ void k_pack_nodes(const float* __restrict__ nodes, const float* __restrict__ R, const float* __restrict__ t, int N,
+                             float* __restrict__ state) {
+	const int n = blockIdx.x * blockDim.x + threadIdx.x;
+	if (n >= N) return;
+	float* s = state + static_cast<int64_t>(n) * NODE_STRIDE;
+	for (int c = 0; c < 3; c++) {
+		s[c] = nodes[3 * n + c];
+		s[3 + c] = t ? t[3 * n + c] : 0.f;
+	}
+	for (int c = 0; c < 9; c++) s[6 + c] = R ? R[9 * n + c] : ((c % 4 == 0) ? 1.f : 0.f);
+	s[15] = 0.f;
+}
+
+__global__ void k_unpack_float4x3(const float4* __restrict__ in, int64_t count, float* __restrict__ out) {
+	const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (i >= count) return;
+	const float4 v = in[i];
+	out[3 * i] = v.x;
+	out[3 * i + 1] = v.y;
+	out[3 * i + 2] = v.z;
+}
+
+nnrt_status launch_pack_nodes(const float* nodes, const float* R, const float* t, int N, float* state, hipStream_t stream) {
+	if (N == 0) return NNRT_OK;
+	k_pack_nodes<<<static_cast<unsigned>(ceil_div(N, 256)), 256, 0, stream>>>(nodes, R, t, N, state);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+nnrt_status launch_unpack_float4x3(const float4* in, int64_t count, float* out, hipStream_t stream) {
+	if (count == 0) return NNRT_OK;
+	k_unpack_float4x3<<<static_cast<unsigned>(ceil_div(count, 256)), 256, 0, stream>>>(in, count, out);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+// =====================================================================================================================
+// NDC face extraction + clip mask: ExtractClippedFaceVerticesImpl.h:108-179 (near/far OR test: A6). Clipped faces are
+// zero-filled (the reference leaves them uninitialized). Vertices given as [V,3] floats or float4.
+// =====================================================================================================================
+template <typename TVertexLoader>
+__device__ inline void extract_face(int64_t f, const int64_t* faces, TVertexLoader load, const NdcSetup& s, float near_clip, float far_clip,
+                                    float* out, uint8_t* mask) {
+	f3 v[3];
+	for (int i = 0; i < 3; i++) v[i] = load(faces[3 * f + i]);
+	bool in_range = false;
+	for (int i = 0; i < 3; i++) {
+		in_range |= v[i].z >= near_clip;
+		in_range |= v[i].z <= far_clip;
+	}
+	bool inlier = false;
+	float xy[3][2];
+	if (in_range) {
+		for (int i = 0; i < 3; i++) {
+			s.ndc.project(v[i].x, v[i].y, v[i].z, &xy[i][0], &xy[i][1]);
+			inlier |= (xy[i][1] >= s.min_y && xy[i][0] >= s.min_x && xy[i][1] <= s.max_y && xy[i][0] <= s.max_x);
+		}
+	}
+	if (!in_range || !inlier) {
+		mask[f] = 0;
+		for (int i = 0; i < 9; i++) out[9 * f + i] = 0.f;
+		return;
+	}
+	mask[f] = 1;
+	for (int i = 0; i < 3; i++) {
+		out[9 * f + 3 * i] = xy[i][0];
+		out[9 * f + 3 * i + 1] = xy[i][1];
+		out[9 * f + 3 * i + 2] = v[i].z;
+	}
+}
+
+__global__ void k_extract_face_ndc(const float* __restrict__ verts, const int64_t* __restrict__ faces, int64_t F, NdcSetup s, float near_clip,
+                                   float far_clip, float* __restrict__ out, uint8_t* __restrict__ mask) {
+	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (f >= F) return;
+	extract_face(f, faces, [&](int64_t i) { return make3(verts[3 * i], verts[3 * i + 1], verts[3 * i + 2]); }, s, near_clip, far_clip, out, mask);
+}
+
+nnrt_status launch_extract_face_ndc(const float* verts, const int64_t* faces, int64_t F, const NdcSetup& s, float near_clip, float far_clip,
+                                    float* out, uint8_t* mask, hipStream_t stream) {
+	if (F == 0) return NNRT_OK;
+	k_extract_face_ndc<<<static_cast<unsigned>(ceil_div(F, 256)), 256, 0, stream>>>(verts, faces, F, s, near_clip, far_clip, out, mask);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+// =====================================================================================================================
+// Unprojection (PerspectiveProjectionImpl.h:117-144, identity extrinsics) and attribute interpolation
+// (InterpolateFaceAttributesImpl.h:30-75)
+// =====================================================================================================================
+__global__ void k_unproject(const float* __restrict__ depth, int H, int W, Camera K, float scale, float depth_max, float* __restrict__ pts,
+                            uint8_t* __restrict__ mask) {
+	const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (i >= static_cast<int64_t>(H) * W) return;
+	const int y = static_cast<int>(i / W), x = static_cast<int>(i % W);
+	const float d = depth[i] / scale;
+	if (d > 0 && d < depth_max) {
+		pts[3 * i] = (static_cast<float>(x) - K.cx) * d / K.fx;
+		pts[3 * i + 1] = (static_cast<float>(y) - K.cy) * d / K.fy;
+		pts[3 * i + 2] = d;
+		mask[i] = 1;
+	} else {
+		pts[3 * i] = pts[3 * i + 1] = pts[3 * i + 2] = 0.f;
+		mask[i] = 0;
+	}
+}
+
+nnrt_status launch_unproject(const float* depth, int H, int W, const Camera& K, float scale, float depth_max, float* pts, uint8_t* mask,
+                             hipStream_t stream) {
+	const int64_t P = static_cast<int64_t>(H) * W;
+	if (P == 0) return NNRT_OK;
+	k_unproject<<<static_cast<unsigned>(ceil_div(P, 256)), 256, 0, stream>>>(depth, H, W, K, scale, depth_max, pts, mask);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+__global__ void k_interpolate(const int64_t* __restrict__ pixel_faces, const float* __restrict__ bary, int64_t P, int Kf,
+                              const float* __restrict__ attrs, int C, float* __restrict__ out) {
+	const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (i >= P * C) return;
+	const int64_t p = i / C;
+	const int c = static_cast<int>(i % C);
+	bool done = false;
+	for (int k = 0; k < Kf; k++) {
+		const int64_t f = done ? -1 : pixel_faces[p * Kf + k];
+		if (f < 0) done = true;
+		float acc = 0.0f;
+		if (!done) {
+			for (int v = 0; v < 3; v++) acc += bary[(p * Kf + k) * 3 + v] * attrs[f * 3 * C + v * C + c];
+		}
+		out[(p * Kf + k) * C + c] = acc;
+	}
+}
+
+nnrt_status launch_interpolate(const int64_t* pixel_faces, const float* bary, int64_t P, int Kf, const float* attrs, int C, float* out,
+                               hipStream_t stream) {
+	if (P * C == 0) return NNRT_OK;
+	k_interpolate<<<static_cast<unsigned>(ceil_div(P * C, 256)), 256, 0, stream>>>(pixel_faces, bary, P, Kf, attrs, C, out);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+__global__ void k_rodrigues(const float* __restrict__ w, int N, float* __restrict__ R) {
+	const int n = blockIdx.x * blockDim.x + threadIdx.x;
+	if (n >= N) return;
+	float m[9];
+	rodrigues_device(w[3 * n], w[3 * n + 1], w[3 * n + 2], m);
+	for (int i = 0; i < 9; i++) R[9 * n + i] = m[i];
+}
+
+nnrt_status launch_rodrigues(const float* w, int N, float* R, hipStream_t stream) {
+	if (N == 0) return NNRT_OK;
+	k_rodrigues<<<static_cast<unsigned>(ceil_div(N, 256)), 256, 0, stream>>>(w, N, R);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+} // namespace nnrt

@@ -1,0 +1,320 @@
+// Rasterizer for gfx950. Semantics: cpp/rendering/RasterizeNdcTriangles.cpp:33-129 and RayFaceIntersection.h:162-255
+// (perspective-correct barycentrics, back-face culling, blur radius compared against the squared point-face distance: A13).
+//
+// faces_per_pixel == 1 (the fitter's call, DeformableMeshToImageFitter.cpp:125): instead of the reference's coarse
+// grid bins + per-pixel bin walk, each face scatters into the pixels of its bounding box a 64-bit key
+// (float depth bits << 32 | face) with a global atomicMin. The minimum key is exactly the lexicographic (depth, face)
+// winner that the reference's queue logic selects, so no bin capacity (and no silent truncation) exists. A resolve pass
+// recomputes the winner's barycentrics/depth with the same device function, bit-identically.
+// faces_per_pixel > 1 (API only): 16x16-pixel tiles; every face is binned into the tiles its box touches, bin lists are
+// sorted by face index and each pixel walks its tile's list with the reference's bounded queue.
+#include "kernels.hpp"
+
+#include <hipcub/hipcub.hpp>
+
+namespace nnrt {
+
+__device__ inline FaceNdc load_face_ndc(const float* face_ndc, int64_t f) {
+	FaceNdc r;
+	const float* p = face_ndc + 9 * f;
+#pragma unroll
+	for (int i = 0; i < 3; i++) {
+		r.x[i] = p[3 * i];
+		r.y[i] = p[3 * i + 1];
+		r.z[i] = p[3 * i + 2];
+	}
+	return r;
+}
+
+// scatter all pixels of the face's box; returns nothing, updates keys
+__device__ inline void scatter_face(const FaceNdc& fn, int32_t face, const RasterOptions& o, uint64_t* keys) {
+	const float area = spa_cw(fn.x[0], fn.y[0], fn.x[1], fn.y[1], fn.x[2], fn.y[2]);
+	const bool back = area < 0.f;
+	const bool zero_area = (area <= K_EPSILON && area >= -1.f * K_EPSILON);
+	const bool zinv = fmax3f(fn.z[0], fn.z[1], fn.z[2]) < K_EPSILON;
+	if ((o.cull_back_faces && back) || zero_area || zinv) return;   // rejected for every pixel by face_test
+	const float xmin = fmin3f(fn.x[0], fn.x[1], fn.x[2]) - o.blur;
+	const float xmax = fmax3f(fn.x[0], fn.x[1], fn.x[2]) + o.blur;
+	const float ymin = fmin3f(fn.y[0], fn.y[1], fn.y[2]) - o.blur;
+	const float ymax = fmax3f(fn.y[0], fn.y[1], fn.y[2]) + o.blur;
+	if (!(xmax >= xmin) || !(ymax >= ymin)) return;
+	int u0, u1, v0, v1;
+	pixel_span(xmin, xmax, o.W, o.H, &u0, &u1);
+	pixel_span(ymin, ymax, o.H, o.W, &v0, &v1);
+	for (int v = v0; v <= v1; v++) {
+		const float py = pixel_to_ndc(v, o.H, o.W);
+		for (int u = u0; u <= u1; u++) {
+			const float px = pixel_to_ndc(u, o.W, o.H);
+			RasterHit h;
+			if (!face_test(fn, px, py, o.blur, o.perspective, o.clip_barycentric, o.cull_back_faces, h)) continue;
+			atomicMin(reinterpret_cast<unsigned long long*>(keys + static_cast<int64_t>(v) * o.W + u),
+			          static_cast<unsigned long long>(raster_key(h.depth, face)));
+		}
+	}
+}
+
+__global__ __launch_bounds__(256) void k_raster_scatter_ndc(const float* __restrict__ face_ndc, const uint8_t* __restrict__ mask, int64_t F,
+                                                            RasterOptions o, uint64_t* __restrict__ keys) {
+	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (f >= F) return;
+	if (mask && !mask[f]) return;
+	scatter_face(load_face_ndc(face_ndc, f), static_cast<int32_t>(f), o, keys);
+}
+
+nnrt_status launch_raster_scatter_ndc(const float* face_ndc, const uint8_t* mask, int64_t F, const RasterOptions& o, uint64_t* keys,
+                                      hipStream_t stream) {
+	if (F == 0) return NNRT_OK;
+	k_raster_scatter_ndc<<<static_cast<unsigned>(ceil_div(F, 256)), 256, 0, stream>>>(face_ndc, mask, F, o, keys);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+// fitter path: NDC extraction + clip test (ExtractClippedFaceVerticesImpl.h:108-179) fused with the scatter
+__device__ inline bool project_mesh_face(const float4* __restrict__ wpos, int4 fi, const NdcSetup& s, float near_clip, float far_clip,
+                                         FaceNdc& fn) {
+	const int vi[3] = {fi.x, fi.y, fi.z};
+	bool in_range = false, inlier = false;
+	f3 v[3];
+#pragma unroll
+	for (int i = 0; i < 3; i++) {
+		const float4 p = wpos[vi[i]];
+		v[i] = make3(p.x, p.y, p.z);
+		in_range |= v[i].z >= near_clip;
+		in_range |= v[i].z <= far_clip;
+	}
+	if (!in_range) return false;
+#pragma unroll
+	for (int i = 0; i < 3; i++) {
+		s.ndc.project(v[i].x, v[i].y, v[i].z, &fn.x[i], &fn.y[i]);
+		fn.z[i] = v[i].z;
+		inlier |= (fn.y[i] >= s.min_y && fn.x[i] >= s.min_x && fn.y[i] <= s.max_y && fn.x[i] <= s.max_x);
+	}
+	return inlier;
+}
+
+__global__ __launch_bounds__(256) void k_raster_scatter_mesh(const float4* __restrict__ wpos, const int4* __restrict__ faces4, int64_t F,
+                                                             NdcSetup s, float near_clip, float far_clip, RasterOptions o,
+                                                             uint64_t* __restrict__ keys) {
+	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (f >= F) return;
+	FaceNdc fn;
+	if (!project_mesh_face(wpos, faces4[f], s, near_clip, far_clip, fn)) return;
+	scatter_face(fn, static_cast<int32_t>(f), o, keys);
+}
+
+nnrt_status launch_raster_scatter_mesh(const float4* wpos, const int4* faces4, int64_t F, const NdcSetup& s, float near_clip, float far_clip,
+                                       const RasterOptions& o, uint64_t* keys, hipStream_t stream) {
+	if (F == 0) return NNRT_OK;
+	k_raster_scatter_mesh<<<static_cast<unsigned>(ceil_div(F, 256)), 256, 0, stream>>>(wpos, faces4, F, s, near_clip, far_clip, o, keys);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+// resolve the winner per pixel into reference-layout fragments ([H,W,1]); resets keys for the next call
+__global__ __launch_bounds__(256) void k_raster_resolve(const float* __restrict__ face_ndc, RasterOptions o, uint64_t* __restrict__ keys,
+                                                        int64_t* __restrict__ out_face, float* __restrict__ out_depth,
+                                                        float* __restrict__ out_bary, float* __restrict__ out_dist) {
+	const int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (p >= static_cast<int64_t>(o.H) * o.W) return;
+	const uint64_t key = keys[p];
+	keys[p] = EMPTY_KEY;
+	int64_t face = -1;
+	RasterHit h{-1.f, -1.f, -1.f, -1.f, -1.f};
+	if (key != EMPTY_KEY) {
+		const int32_t f = static_cast<int32_t>(key & 0xffffffffu);
+		const int v = static_cast<int>(p / o.W), u = static_cast<int>(p % o.W);
+		if (face_test(load_face_ndc(face_ndc, f), pixel_to_ndc(u, o.W, o.H), pixel_to_ndc(v, o.H, o.W), o.blur, o.perspective,
+		              o.clip_barycentric, o.cull_back_faces, h)) {
+			face = f;
+		} else {
+			h = RasterHit{-1.f, -1.f, -1.f, -1.f, -1.f};
+		}
+	}
+	out_face[p] = face;
+	out_depth[p] = h.depth;
+	out_dist[p] = h.dist;
+	out_bary[3 * p] = h.b0;
+	out_bary[3 * p + 1] = h.b1;
+	out_bary[3 * p + 2] = h.b2;
+}
+
+nnrt_status launch_raster_resolve(const float* face_ndc, int64_t F, const RasterOptions& o, uint64_t* keys, int64_t* out_face, float* out_depth,
+                                  float* out_bary, float* out_dist, hipStream_t stream) {
+	(void) F;
+	const int64_t P = static_cast<int64_t>(o.H) * o.W;
+	if (P == 0) return NNRT_OK;
+	k_raster_resolve<<<static_cast<unsigned>(ceil_div(P, 256)), 256, 0, stream>>>(face_ndc, o, keys, out_face, out_depth, out_bary, out_dist);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+// =====================================================================================================================
+// faces_per_pixel > 1: tile-binned queues (API path)
+// =====================================================================================================================
+constexpr int TILE = 16;
+
+__device__ inline bool face_tile_range(const FaceNdc& fn, const RasterOptions& o, int& tx0, int& tx1, int& ty0, int& ty1) {
+	const float area = spa_cw(fn.x[0], fn.y[0], fn.x[1], fn.y[1], fn.x[2], fn.y[2]);
+	const bool zero_area = (area <= K_EPSILON && area >= -1.f * K_EPSILON);
+	const bool zinv = fmax3f(fn.z[0], fn.z[1], fn.z[2]) < K_EPSILON;
+	if ((o.cull_back_faces && area < 0.f) || zero_area || zinv) return false;
+	const float xmin = fmin3f(fn.x[0], fn.x[1], fn.x[2]) - o.blur, xmax = fmax3f(fn.x[0], fn.x[1], fn.x[2]) + o.blur;
+	const float ymin = fmin3f(fn.y[0], fn.y[1], fn.y[2]) - o.blur, ymax = fmax3f(fn.y[0], fn.y[1], fn.y[2]) + o.blur;
+	if (!(xmax >= xmin) || !(ymax >= ymin)) return false;
+	int u0, u1, v0, v1;
+	pixel_span(xmin, xmax, o.W, o.H, &u0, &u1);
+	pixel_span(ymin, ymax, o.H, o.W, &v0, &v1);
+	if (u0 > u1 || v0 > v1) return false;
+	tx0 = u0 / TILE;
+	tx1 = u1 / TILE;
+	ty0 = v0 / TILE;
+	ty1 = v1 / TILE;
+	return true;
+}
+
+__global__ void k_tile_count(const float* __restrict__ face_ndc, const uint8_t* __restrict__ mask, int64_t F, RasterOptions o, int tiles_x,
+                             int* __restrict__ counts) {
+	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (f >= F || (mask && !mask[f])) return;
+	int tx0, tx1, ty0, ty1;
+	if (!face_tile_range(load_face_ndc(face_ndc, f), o, tx0, tx1, ty0, ty1)) return;
+	for (int ty = ty0; ty <= ty1; ty++)
+		for (int tx = tx0; tx <= tx1; tx++) atomicAdd(counts + ty * tiles_x + tx, 1);
+}
+
+__global__ void k_tile_fill(const float* __restrict__ face_ndc, const uint8_t* __restrict__ mask, int64_t F, RasterOptions o, int tiles_x,
+                            const int* __restrict__ offsets, int* __restrict__ cursor, int32_t* __restrict__ lists) {
+	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (f >= F || (mask && !mask[f])) return;
+	int tx0, tx1, ty0, ty1;
+	if (!face_tile_range(load_face_ndc(face_ndc, f), o, tx0, tx1, ty0, ty1)) return;
+	for (int ty = ty0; ty <= ty1; ty++)
+		for (int tx = tx0; tx <= tx1; tx++) {
+			const int t = ty * tiles_x + tx;
+			lists[offsets[t] + atomicAdd(cursor + t, 1)] = static_cast<int32_t>(f);
+		}
+}
+
+// per-tile insertion sort of the (short) face list so the per-pixel walk visits faces in ascending order
+__global__ void k_tile_sort(const int* __restrict__ offsets, int tiles, int32_t* __restrict__ lists) {
+	const int t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= tiles) return;
+	int32_t* l = lists + offsets[t];
+	const int n = offsets[t + 1] - offsets[t];
+	for (int i = 1; i < n; i++) {
+		int32_t x = l[i];
+		int j = i - 1;
+		while (j >= 0 && l[j] > x) {
+			l[j + 1] = l[j];
+			j--;
+		}
+		l[j + 1] = x;
+	}
+}
+
+struct QEntry {
+	float depth, dist, b0, b1, b2;
+	int32_t face;
+};
+
+__global__ __launch_bounds__(256) void k_tile_raster(const float* __restrict__ face_ndc, RasterOptions o, int tiles_x, int K,
+                                                     const int* __restrict__ offsets, const int32_t* __restrict__ lists,
+                                                     int64_t* __restrict__ out_face, float* __restrict__ out_depth, float* __restrict__ out_bary,
+                                                     float* __restrict__ out_dist) {
+	const int tile = blockIdx.x;
+	const int u = (tile % tiles_x) * TILE + (threadIdx.x % TILE), v = (tile / tiles_x) * TILE + (threadIdx.x / TILE);
+	if (u >= o.W || v >= o.H) return;
+	const float px = pixel_to_ndc(u, o.W, o.H), py = pixel_to_ndc(v, o.H, o.W);
+	QEntry q[MAX_FACES_PER_PIXEL];
+	int qs = 0, qat = -1;
+	float qmax = -1000.f;
+	for (int i = offsets[tile]; i < offsets[tile + 1]; i++) {
+		const int32_t f = lists[i];
+		RasterHit h;
+		if (!face_test(load_face_ndc(face_ndc, f), px, py, o.blur, o.perspective, o.clip_barycentric, o.cull_back_faces, h)) continue;
+		const QEntry e{h.depth, h.dist, h.b0, h.b1, h.b2, f};
+		if (qs < K) {
+			q[qs] = e;
+			if (e.depth > qmax) {
+				qmax = e.depth;
+				qat = qs;
+			}
+			qs++;
+		} else if (e.depth < qmax) {
+			q[qat] = e;
+			qmax = e.depth;
+			for (int j = 0; j < K; j++)
+				if (q[j].depth > qmax) {
+					qmax = q[j].depth;
+					qat = j;
+				}
+		}
+	}
+	// sort by (depth, face): RayFaceIntersection.h:42-45
+	for (int i = 1; i < qs; i++) {
+		QEntry x = q[i];
+		int j = i - 1;
+		while (j >= 0 && (q[j].depth > x.depth || (q[j].depth == x.depth && q[j].face > x.face))) {
+			q[j + 1] = q[j];
+			j--;
+		}
+		q[j + 1] = x;
+	}
+	const int64_t p = static_cast<int64_t>(v) * o.W + u;
+	for (int i = 0; i < K; i++) {
+		const int64_t o_ = p * K + i;
+		if (i < qs) {
+			out_face[o_] = q[i].face;
+			out_depth[o_] = q[i].depth;
+			out_dist[o_] = q[i].dist;
+			out_bary[3 * o_] = q[i].b0;
+			out_bary[3 * o_ + 1] = q[i].b1;
+			out_bary[3 * o_ + 2] = q[i].b2;
+		} else {
+			out_face[o_] = -1;
+			out_depth[o_] = -1.f;
+			out_dist[o_] = -1.f;
+			out_bary[3 * o_] = out_bary[3 * o_ + 1] = out_bary[3 * o_ + 2] = -1.f;
+		}
+	}
+}
+
+nnrt_status launch_raster_multi(const float* face_ndc, const uint8_t* mask, int64_t F, const RasterOptions& o, int faces_per_pixel,
+                                int64_t* out_face, float* out_depth, float* out_bary, float* out_dist, hipStream_t stream) {
+	const int tiles_x = static_cast<int>(ceil_div(o.W, TILE)), tiles_y = static_cast<int>(ceil_div(o.H, TILE));
+	const int tiles = tiles_x * tiles_y;
+	int *counts = nullptr, *offsets = nullptr, *cursor = nullptr;
+	int32_t* lists = nullptr;
+	void* tmp = nullptr;
+	size_t tmp_bytes = 0;
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&counts), sizeof(int) * (tiles + 1), stream));
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&offsets), sizeof(int) * (tiles + 1), stream));
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&cursor), sizeof(int) * tiles, stream));
+	NNRT_HIP(hipMemsetAsync(counts, 0, sizeof(int) * (tiles + 1), stream));
+	NNRT_HIP(hipMemsetAsync(cursor, 0, sizeof(int) * tiles, stream));
+	const unsigned fg = static_cast<unsigned>(ceil_div(F > 0 ? F : 1, 256));
+	if (F > 0) k_tile_count<<<fg, 256, 0, stream>>>(face_ndc, mask, F, o, tiles_x, counts);
+	NNRT_LAUNCH_CHECK();
+	NNRT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts, offsets, tiles + 1, stream));
+	NNRT_HIP(hipMallocAsync(&tmp, tmp_bytes, stream));
+	NNRT_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, counts, offsets, tiles + 1, stream));
+	int total = 0;
+	NNRT_HIP(hipMemcpyAsync(&total, offsets + tiles, sizeof(int), hipMemcpyDeviceToHost, stream));
+	NNRT_HIP(hipStreamSynchronize(stream));
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&lists), sizeof(int32_t) * (total > 0 ? total : 1), stream));
+	if (F > 0) k_tile_fill<<<fg, 256, 0, stream>>>(face_ndc, mask, F, o, tiles_x, offsets, cursor, lists);
+	NNRT_LAUNCH_CHECK();
+	k_tile_sort<<<static_cast<unsigned>(ceil_div(tiles, 64)), 64, 0, stream>>>(offsets, tiles, lists);
+	NNRT_LAUNCH_CHECK();
+	k_tile_raster<<<tiles, TILE * TILE, 0, stream>>>(face_ndc, o, tiles_x, faces_per_pixel, offsets, lists, out_face, out_depth, out_bary,
+	                                                   out_dist);
+	NNRT_LAUNCH_CHECK();
+	NNRT_HIP(hipFreeAsync(counts, stream));
+	NNRT_HIP(hipFreeAsync(offsets, stream));
+	NNRT_HIP(hipFreeAsync(cursor, stream));
+	NNRT_HIP(hipFreeAsync(lists, stream));
+	NNRT_HIP(hipFreeAsync(tmp, stream));
+	return NNRT_OK;
+}
+
+} // namespace nnrt

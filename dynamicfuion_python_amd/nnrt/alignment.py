@@ -1,0 +1,113 @@
+"""nnrt.alignment: DeformableMeshToImageFitter (cpp/alignment/DeformableMeshToImageFitter.h:34-91) and IterationMode
+(cpp/alignment/IterationMode.h:24-28) -- absent from the reference's bindings, added here as SURVEY 8(b) specifies."""
+from __future__ import annotations
+
+import ctypes
+import enum
+
+import numpy as np
+import torch
+
+from .. import _native as N
+from ._tensors import to_device, to_host_f64
+from .geometry import HierarchicalGraphWarpField, TriangleMesh
+
+
+class IterationMode(enum.IntEnum):
+    ALL = 0
+    TRANSLATION_ONLY = 1
+    ROTATION_ONLY = 2
+
+
+class DeformableMeshToImageFitter:
+    def __init__(self, max_iteration_count: int = 100, iteration_mode_sequence=(IterationMode.ALL,), minimal_update_threshold: float = 1e-6,
+                 use_perspective_correction: bool = True, max_depth: float = 10.0, use_tukey_penalty_for_data_term: bool = False,
+                 tukey_penalty_cutoff_cm: float = 0.01, preconditioning_dampening_factor: float = 0.0, arap_term_weight: float = 200.0,
+                 use_huber_penalty_for_arap_term: bool = False, huber_penalty_constant: float = 1e-4, device: int = 0,
+                 use_hip_graph: bool = True):
+        p = N.FitterParams()
+        N.lib().nnrt_fitter_default_params(ctypes.byref(p))
+        modes = list(iteration_mode_sequence)
+        p.max_iteration_count = int(max_iteration_count)
+        p.iteration_mode_count = len(modes)
+        for i, m in enumerate(modes):
+            p.iteration_modes[i] = int(m)
+        p.minimal_update_threshold = float(minimal_update_threshold)
+        p.use_perspective_correction = int(use_perspective_correction)
+        p.max_depth = float(max_depth)
+        p.use_tukey_penalty_for_data_term = int(use_tukey_penalty_for_data_term)
+        p.tukey_penalty_cutoff_cm = float(tukey_penalty_cutoff_cm)
+        p.preconditioning_dampening_factor = float(preconditioning_dampening_factor)
+        p.arap_term_weight = float(arap_term_weight)
+        p.use_huber_penalty_for_arap_term = int(use_huber_penalty_for_arap_term)
+        p.huber_penalty_constant = float(huber_penalty_constant)
+        p.use_hip_graph = int(use_hip_graph)
+        h = ctypes.c_void_p()
+        N.check(N.lib().nnrt_fitter_create(ctypes.byref(p), int(device), ctypes.byref(h)))
+        self._h = h
+        self.params = p
+        self.device = torch.device("cuda", device)
+        self.modes = modes
+        self._frame = None
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                N.lib().nnrt_fitter_destroy(h)
+            except Exception:   # interpreter shutdown
+                pass
+            self._h = None
+
+    # ---- split API (once-per-frame prepare + GN iterations) ----
+    def prepare(self, warp_field: HierarchicalGraphWarpField, canonical_mesh: TriangleMesh, reference_depth_image,
+                reference_image_mask, intrinsic_matrix, extrinsic_matrix=None, depth_scale: float = 1.0, stream=None):
+        N.require_gpu()
+        dev = self.device
+        p, n, f = canonical_mesh.on_device(dev)
+        d = to_device(reference_depth_image, torch.float32, dev)
+        if d.dim() == 3:
+            d = d[..., 0].contiguous()
+        H, W = d.shape
+        m = None if reference_image_mask is None else to_device(reference_image_mask, torch.uint8, dev).reshape(H, W)
+        K = to_host_f64(intrinsic_matrix)
+        E = None if extrinsic_matrix is None else to_host_f64(extrinsic_matrix)
+        self._frame = (p, n, f, d, m, K, E, H, W)   # keep device inputs alive for the duration of the frame
+        self._node_count = warp_field.node_count
+        N.check(N.lib().nnrt_fitter_prepare(self._h, warp_field.handle, N.ptr(p), N.ptr(n), p.shape[0], N.ptr(f), f.shape[0], N.ptr(d), N.ptr(m),
+                                            H, W, N.ptr(K), N.ptr(E), float(depth_scale), N.stream_ptr(stream)))
+
+    def iterate(self, warp_field: HierarchicalGraphWarpField, first_iteration: int = 0, count: int = 1, stream=None):
+        N.check(N.lib().nnrt_fitter_iterate(self._h, warp_field.handle, int(first_iteration), int(count), N.stream_ptr(stream)))
+
+    def check(self, stream=None):
+        N.check(N.lib().nnrt_fitter_check(self._h, N.stream_ptr(stream)))
+
+    def fit_to_image(self, warp_field: HierarchicalGraphWarpField, canonical_mesh: TriangleMesh, reference_color_image,
+                     reference_depth_image, reference_image_mask, intrinsic_matrix, extrinsic_matrix=None, depth_scale: float = 1.0):
+        """FitToImage(warp_field, mesh, color, depth, mask, K, E, depth_scale) (DeformableMeshToImageFitter.cpp:278-314).
+        The color image is unused by the reference's fitter as well. Mutates the warp field."""
+        self.prepare(warp_field, canonical_mesh, reference_depth_image, reference_image_mask, intrinsic_matrix, extrinsic_matrix, depth_scale)
+        self.iterate(warp_field, 0, self.params.max_iteration_count)
+        self.check()
+
+    def diagnostics(self, stream=None) -> dict:
+        """Residuals, residual mask, rasterized face per pixel, motion updates, negative gradient and data-term Hessian
+        blocks of the most recent iteration (host numpy)."""
+        _, _, _, _, _, _, _, H, W = self._frame
+        P = H * W
+        s = 6   # upper bound (3-dof modes fill the first N*3 / N*9 entries)
+        nodes = self._node_count
+        out = dict(residuals=np.empty(P, np.float32), residual_mask=np.empty(P, np.uint8), pixel_faces=np.empty(P, np.int32),
+                   updates=np.empty(nodes * s, np.float32), gradient=np.empty(nodes * s, np.float32),
+                   hessian=np.empty(nodes * s * s, np.float32))
+        N.check(N.lib().nnrt_fitter_get_diagnostics(self._h, N.ptr(out["residuals"]), N.ptr(out["residual_mask"]), N.ptr(out["pixel_faces"]),
+                                                    N.ptr(out["updates"]), N.ptr(out["gradient"]), N.ptr(out["hessian"]), N.stream_ptr(stream)))
+        out["residual_mask"] = out["residual_mask"].astype(bool)
+        return out
+
+    def anchors(self, vertex_count: int, anchor_count: int, stream=None):
+        a = np.empty((vertex_count, anchor_count), np.int32)
+        w = np.empty((vertex_count, anchor_count), np.float32)
+        N.check(N.lib().nnrt_fitter_get_anchors(self._h, N.ptr(a), N.ptr(w), N.stream_ptr(stream)))
+        return a, w

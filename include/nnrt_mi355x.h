@@ -1,0 +1,178 @@
+/*
+ * nnrt_mi355x.h -- C-ABI of the MI355X-native DeformableMeshToImageFitter hot path.
+ *
+ * Drop-in boundary for henry123-boy/Dynamicfuion_python's dense non-rigid tracker. Every entry point replaces a
+ * reference interface, cited per function (paths relative to the reference repository root). Plain pointers and
+ * sizes only: arrays marked d_ are DEVICE pointers (hipMalloc'd or torch.cuda tensors on the same device), h_ arrays
+ * are HOST pointers. All functions return 0 on success and a non-zero nnrt_status otherwise, with a message retrievable
+ * through nnrt_last_error() (thread-local). No exceptions cross the ABI. A `stream` argument is a hipStream_t (NULL =
+ * the legacy default stream). Handles are not thread-safe: use one handle per host thread.
+ *
+ * Layout conventions follow the reference tensors: float32 row-major, vertex/face/node-major; rotations [N,3,3]
+ * row-major; triangle indices int64 [F,3]; intrinsics/extrinsics float64 [3,3]/[4,4] on the host.
+ */
+#ifndef NNRT_MI355X_H
+#define NNRT_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t nnrt_status;
+enum {
+	NNRT_OK = 0,
+	NNRT_ERROR_ARGUMENT = 1,
+	NNRT_ERROR_HIP = 2,
+	NNRT_ERROR_NOT_POSITIVE_DEFINITE = 3,   /* reference: NNRT_LAPACK_CHECK potrf failure -> RuntimeError */
+	NNRT_ERROR_UNSUPPORTED = 4,
+	NNRT_ERROR_CAPACITY = 5
+};
+
+/* iteration modes: cpp/alignment/IterationMode.h:24-28 */
+enum { NNRT_ITERATION_ALL = 0, NNRT_ITERATION_TRANSLATION_ONLY = 1, NNRT_ITERATION_ROTATION_ONLY = 2 };
+/* warp-node coverage: cpp/geometry/WarpNodeCoverageComputationMethod.h */
+enum { NNRT_FIXED_NODE_COVERAGE = 0, NNRT_MINIMAL_K_NEIGHBOR_NODE_DISTANCE = 1 };
+
+typedef struct nnrt_warp_field nnrt_warp_field;
+typedef struct nnrt_fitter nnrt_fitter;
+
+const char* nnrt_last_error(void);
+/* HIP runtime version the library was built against and the number of visible devices (-1 on error). */
+int32_t nnrt_runtime_version(void);
+int32_t nnrt_device_count(void);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * Warp field -- replaces nnrt::geometry::HierarchicalGraphWarpField (cpp/geometry/HierarchicalGraphWarpField.h:37-97,
+ * cpp/geometry/HierarchicalGraphWarpField.cpp:37-313) and the exported GraphWarpField accessors
+ * (cpp/pybind/geometry/geometry.cpp:278-320). Node state lives on the device in virtual (hierarchy) order.
+ * h_layer_radii may be NULL (default radius (i+1) * node_coverage, HierarchicalGraphWarpField.h:46-47).
+ * ------------------------------------------------------------------------------------------------------------- */
+nnrt_status nnrt_warp_field_create(const float* h_nodes, int32_t node_count, float node_coverage, int32_t threshold_nodes_by_distance,
+                                   int32_t anchor_count, int32_t minimum_valid_anchor_count, int32_t coverage_method,
+                                   int32_t layer_count, int32_t max_vertex_degree, const float* h_layer_radii, int32_t device,
+                                   nnrt_warp_field** out);
+void nnrt_warp_field_destroy(nnrt_warp_field* warp_field);
+int32_t nnrt_warp_field_node_count(const nnrt_warp_field* warp_field);
+int32_t nnrt_warp_field_edge_count(const nnrt_warp_field* warp_field);
+/* layer sizes (fine -> coarse) into h_counts[layer_count]; returns layer_count */
+int32_t nnrt_warp_field_layer_counts(const nnrt_warp_field* warp_field, int32_t* h_counts);
+/* HierarchicalGraphWarpField::GetVirtualNodeIndices (:206-208): h_out[N] int64 (virtual -> original) */
+nnrt_status nnrt_warp_field_get_virtual_node_indices(const nnrt_warp_field* warp_field, int64_t* h_out);
+/* GetEdges / GetEdgeLayerIndices (:201-228): h_edges[E,2] int32 virtual indices, h_edge_layers[E] int8 (either may be NULL) */
+nnrt_status nnrt_warp_field_get_edges(const nnrt_warp_field* warp_field, int32_t* h_edges, int8_t* h_edge_layers);
+/* GetNodePositions/Rotations/Translations(use_virtual_ordering) (:210-224) and Set/Translate/Rotate counterparts. */
+nnrt_status nnrt_warp_field_get_node_positions(const nnrt_warp_field* warp_field, float* h_out, int32_t virtual_order);
+nnrt_status nnrt_warp_field_get_node_rotations(const nnrt_warp_field* warp_field, float* h_out, int32_t virtual_order);
+nnrt_status nnrt_warp_field_get_node_translations(const nnrt_warp_field* warp_field, float* h_out, int32_t virtual_order);
+nnrt_status nnrt_warp_field_set_node_rotations(nnrt_warp_field* warp_field, const float* h_in, int32_t virtual_order);
+nnrt_status nnrt_warp_field_set_node_translations(nnrt_warp_field* warp_field, const float* h_in, int32_t virtual_order);
+/* node coverage weights (MINIMAL_K_NEIGHBOR_NODE_DISTANCE, WarpField.cpp:249-263), virtual order */
+nnrt_status nnrt_warp_field_get_node_coverage_weights(const nnrt_warp_field* warp_field, float* h_out);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * Fitter -- replaces nnrt::alignment::DeformableMeshToImageFitter (cpp/alignment/DeformableMeshToImageFitter.h:34-91,
+ * .cpp:56-448). Parameters mirror the constructor (.h:34-46).
+ * ------------------------------------------------------------------------------------------------------------- */
+typedef struct nnrt_fitter_params {
+	int32_t max_iteration_count;            /* 100 */
+	int32_t iteration_mode_count;           /* 1 */
+	int32_t iteration_modes[16];            /* {NNRT_ITERATION_ALL} */
+	float minimal_update_threshold;         /* 1e-6 (never effective in the reference: A14) */
+	int32_t use_perspective_correction;     /* 1 */
+	float max_depth;                        /* 10 */
+	int32_t use_tukey_penalty_for_data_term;/* 0 */
+	float tukey_penalty_cutoff_cm;          /* 0.01 */
+	float preconditioning_dampening_factor; /* 0 ; must be in [0, 1] */
+	float arap_term_weight;                 /* 200 */
+	int32_t use_huber_penalty_for_arap_term;/* 0 */
+	float huber_penalty_constant;           /* 1e-4 */
+	int32_t use_hip_graph;                  /* 1: capture one GN iteration per mode into a hipGraph and replay it */
+} nnrt_fitter_params;
+
+void nnrt_fitter_default_params(nnrt_fitter_params* params);
+nnrt_status nnrt_fitter_create(const nnrt_fitter_params* params, int32_t device, nnrt_fitter** out);
+void nnrt_fitter_destroy(nnrt_fitter* fitter);
+
+/* FitToImage(warp_field, canonical_mesh, color, depth, mask, K, E, depth_scale) (DeformableMeshToImageFitter.cpp:278-314).
+ * d_depth: float32 [H,W] metric depth * depth_scale; d_mask: uint8 [H,W] or NULL; h_K: float64[9]; h_E: float64[16] or
+ * NULL (identity). Mutates the warp field's rotations/translations in place. */
+nnrt_status nnrt_fitter_fit_to_image(nnrt_fitter* fitter, nnrt_warp_field* warp_field, const float* d_vertices, const float* d_normals,
+                                     int64_t vertex_count, const int64_t* d_faces, int64_t face_count, const float* d_depth,
+                                     const uint8_t* d_mask, int32_t height, int32_t width, const double* h_K, const double* h_E,
+                                     float depth_scale, void* stream);
+/* The same call split in two for benchmarking / streaming use: prepare() runs the once-per-frame setup of
+ * FitToImage (:96-106: anchors, NDC intrinsics, face<->anchor association, reference point cloud); iterate() runs
+ * `count` GN iterations (loop body :111-275) starting at iteration index `first_iteration` (selects the mode). */
+nnrt_status nnrt_fitter_prepare(nnrt_fitter* fitter, nnrt_warp_field* warp_field, const float* d_vertices, const float* d_normals,
+                                int64_t vertex_count, const int64_t* d_faces, int64_t face_count, const float* d_depth,
+                                const uint8_t* d_mask, int32_t height, int32_t width, const double* h_K, const double* h_E,
+                                float depth_scale, void* stream);
+nnrt_status nnrt_fitter_iterate(nnrt_fitter* fitter, nnrt_warp_field* warp_field, int32_t first_iteration, int32_t count, void* stream);
+/* Reports (and clears) a failure recorded on the device by earlier iterate() calls (e.g. a non-positive-definite block,
+ * which the reference raises from potrf). Synchronizes `stream`. */
+nnrt_status nnrt_fitter_check(nnrt_fitter* fitter, void* stream);
+/* Diagnostics of the most recent iteration, copied to the host (any pointer may be NULL): residuals [H*W] float32,
+ * residual mask [H*W] uint8, rasterized face per pixel [H*W] int32 (-1 = none), motion updates [N*s] (s = 6 for ALL,
+ * 3 otherwise), negative gradient [N*s], data-term Hessian blocks [N*s*s]. Synchronizes `stream`. */
+nnrt_status nnrt_fitter_get_diagnostics(nnrt_fitter* fitter, float* h_residuals, uint8_t* h_residual_mask, int32_t* h_pixel_faces,
+                                        float* h_updates, float* h_negative_gradient, float* h_hessian_blocks, void* stream);
+/* Once-per-frame outputs of prepare(): anchors [V,K] int32 and weights [V,K] float32 (device -> host). */
+nnrt_status nnrt_fitter_get_anchors(nnrt_fitter* fitter, int32_t* h_anchors, float* h_weights, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * Stage entry points (parity surface; all device pointers, all asynchronous on `stream`)
+ * ------------------------------------------------------------------------------------------------------------- */
+/* nnrt.geometry.functional.compute_anchors_and_weights_euclidean_{fixed,variable}_node_weight
+ * (cpp/pybind/geometry/functional/functional.cpp:52-90 -> WarpAnchorComputationImpl.h:42-140).
+ * d_node_coverage_weights == NULL -> fixed coverage. */
+nnrt_status nnrt_compute_anchors_and_weights(const float* d_points, int64_t point_count, const float* d_nodes, int32_t node_count,
+                                             int32_t anchor_count, float node_coverage, const float* d_node_coverage_weights,
+                                             int32_t minimum_valid_anchor_count, int32_t* d_anchors, float* d_weights, void* stream);
+/* WarpTriangleMeshUsingSuppliedAnchors (cpp/geometry/functional/Warping.cpp:222-264). h_E may be NULL. */
+nnrt_status nnrt_warp_mesh(const float* d_vertices, const float* d_normals, int64_t vertex_count, const float* d_nodes,
+                           const float* d_rotations, const float* d_translations, int32_t node_count, const int32_t* d_anchors,
+                           const float* d_weights, int32_t anchor_count, const double* h_E, float* d_out_vertices,
+                           float* d_out_normals, void* stream);
+/* nnrt.rendering.functional.get_mesh_ndc_face_vertices_and_clip_mask (cpp/rendering/functional/ExtractFaceVertices.cpp:56-85).
+ * d_face_ndc [F,3,3], d_clip_mask [F] uint8 (1 = keep). */
+nnrt_status nnrt_get_mesh_ndc_face_vertices_and_clip_mask(const float* d_vertices, const int64_t* d_faces, int64_t face_count,
+                                                          const double* h_K, int32_t height, int32_t width, float near_clip,
+                                                          float far_clip, float* d_face_ndc, uint8_t* d_clip_mask, void* stream);
+/* nnrt.rendering.rasterize_ndc_triangles (cpp/pybind/rendering/rendering.cpp:36-43 -> RasterizeNdcTriangles.cpp:33-129).
+ * Outputs fragments: face [H,W,Kf] int64 (-1), depth [H,W,Kf], barycentrics [H,W,Kf,3], signed distance [H,W,Kf]
+ * (-1 fill). d_clip_mask may be NULL. bin_size / max_faces_per_bin are accepted for signature parity; the MI355X
+ * rasterizer does not need coarse bins (faces_per_pixel == 1: per-face scatter with a (depth, face) 64-bit atomic
+ * minimum; faces_per_pixel > 1: tile-binned per-pixel queues). */
+nnrt_status nnrt_rasterize_ndc_triangles(const float* d_face_ndc, const uint8_t* d_clip_mask, int64_t face_count, int32_t height,
+                                         int32_t width, float blur_radius_pixels, int32_t faces_per_pixel, int32_t bin_size,
+                                         int32_t max_faces_per_bin, int32_t perspective_correct_barycentric_coordinates,
+                                         int32_t clip_barycentric_coordinates, int32_t cull_back_faces, int64_t* d_pixel_faces,
+                                         float* d_pixel_depths, float* d_pixel_barycentrics, float* d_pixel_face_distances,
+                                         void* stream);
+/* nnrt.rendering.functional.interpolate_vertex_attributes (InterpolateFaceAttributesImpl.h:30-75): [H,W,Kf,C] */
+nnrt_status nnrt_interpolate_face_attributes(const int64_t* d_pixel_faces, const float* d_barycentrics, int64_t pixel_count,
+                                             int32_t faces_per_pixel, const float* d_face_attributes, int32_t channels,
+                                             float* d_out, void* stream);
+/* nnrt.geometry.functional.unproject_raster_depth_without_filtering (PerspectiveProjectionImpl.h:60-146), float32 depth */
+nnrt_status nnrt_unproject_depth(const float* d_depth, int32_t height, int32_t width, const double* h_K, float depth_scale,
+                                 float depth_max, float* d_points, uint8_t* d_mask, void* stream);
+/* nnrt.core.linalg AxisAngleVectorsToMatricesRodrigues (cpp/core/linalg/RodriguesImpl.h:66-88) */
+nnrt_status nnrt_axis_angle_to_matrices_rodrigues(const float* d_vectors, int32_t count, float* d_matrices, void* stream);
+/* SolveBlockDiagonalCholesky (cpp/core/linalg/SolveBlockDiagonalCholesky.cpp): x_i = A_i^-1 b_i, block size 3 or 6 */
+nnrt_status nnrt_solve_block_diagonal_cholesky(const float* d_blocks, const float* d_b, int32_t block_count, int32_t block_size,
+                                               float* d_x, void* stream);
+/* SolveBlockSparseArrowheadCholesky (cpp/core/linalg/SolveBlockSparseArrowheadCholesky.cpp:30-95), 6x6 blocks:
+ * d_diagonal_blocks [N,6,6], d_wing_blocks [E,6,6] at block coordinates d_wing_coordinates [E,2] (row < arrow_base
+ * <= column for stem-to-corner blocks; row >= arrow_base for corner off-diagonal blocks), b [6N]. */
+nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diagonal_blocks, const float* d_wing_blocks,
+                                                       const int32_t* d_wing_coordinates, int32_t wing_block_count,
+                                                       int32_t diagonal_block_count, int32_t arrow_base_block_index,
+                                                       const float* d_b, float* d_x, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NNRT_MI355X_H */

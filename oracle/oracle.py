@@ -1,0 +1,397 @@
+"""ctypes wrapper over oracle/libnnrt_oracle.so -- TEST INFRASTRUCTURE ONLY.
+
+The CPU restatement of the reference hot path (see nnrt_oracle.cpp header). Only tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg may import this module; the product package never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libnnrt_oracle.so")
+_lib = None
+
+MODE = {"ALL": 0, "TRANSLATION_ONLY": 1, "ROTATION_ONLY": 2}
+
+
+def build(force: bool = False) -> str:
+    src = os.path.join(_HERE, "nnrt_oracle.cpp")
+    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE, "libnnrt_oracle.so"])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+        _lib.orc_last_error.restype = ctypes.c_char_p
+    return _lib
+
+
+def _p(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _i64(a):
+    return np.ascontiguousarray(a, dtype=np.int64)
+
+
+def _i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def _u8(a):
+    return np.ascontiguousarray(a, dtype=np.uint8)
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError(f"oracle error {rc}: {lib().orc_last_error().decode()}")
+
+
+def set_num_threads(n: int):
+    lib().orc_set_num_threads(ctypes.c_int(n))
+
+
+def num_threads() -> int:
+    return lib().orc_num_threads()
+
+
+def compute_anchors(points, nodes, anchor_count=4, coverage=0.05, node_weights=None, minimum_valid_anchor_count=0):
+    points, nodes = _f32(points), _f32(nodes)
+    V, N = len(points), len(nodes)
+    anchors = np.empty((V, anchor_count), np.int32)
+    weights = np.empty((V, anchor_count), np.float32)
+    nw = None if node_weights is None else _f32(node_weights)
+    lib().orc_compute_anchors(_p(points), ctypes.c_int64(V), _p(nodes), ctypes.c_int(N), ctypes.c_int(anchor_count),
+                              ctypes.c_float(coverage), _p(nw), ctypes.c_int(minimum_valid_anchor_count), _p(anchors), _p(weights))
+    return anchors, weights
+
+
+def node_coverage_weights(nodes, coverage):
+    nodes = _f32(nodes)
+    out = np.empty(len(nodes), np.float32)
+    lib().orc_node_coverage_weights(_p(nodes), ctypes.c_int(len(nodes)), ctypes.c_float(coverage), _p(out))
+    return out
+
+
+def build_hierarchy(nodes, coverage, layer_count, max_degree=4, radii=None):
+    nodes = _f32(nodes)
+    N = len(nodes)
+    vidx = np.empty(N, np.int64)
+    counts = np.empty(layer_count, np.int32)
+    cap = N * max_degree
+    edges = np.empty((cap, 2), np.int32)
+    elayers = np.empty(cap, np.int8)
+    r = None if radii is None else _f32(radii)
+    ne = lib().orc_build_hierarchy(_p(nodes), ctypes.c_int(N), ctypes.c_float(coverage), ctypes.c_int(layer_count),
+                                   ctypes.c_int(max_degree), _p(r), _p(vidx), _p(counts), _p(edges), _p(elayers), ctypes.c_int(cap))
+    if ne < 0:
+        raise RuntimeError(lib().orc_last_error().decode())
+    return vidx, counts, edges[:ne].copy(), elayers[:ne].copy()
+
+
+def warp_mesh(points, normals, nodes, rotations, translations, anchors, weights, extrinsics=None):
+    points, normals, nodes = _f32(points), _f32(normals), _f32(nodes)
+    rotations, translations, anchors, weights = _f32(rotations), _f32(translations), _i32(anchors), _f32(weights)
+    V = len(points)
+    op = np.empty((V, 3), np.float32)
+    on = np.empty((V, 3), np.float32)
+    E = None if extrinsics is None else _f64(extrinsics)
+    lib().orc_warp_mesh(_p(points), _p(normals), ctypes.c_int64(V), _p(nodes), _p(rotations), _p(translations), _p(anchors),
+                        _p(weights), ctypes.c_int(anchors.shape[1]), _p(E), _p(op), _p(on))
+    return op, on
+
+
+def intrinsics_to_ndc(K, H, W):
+    K = _f64(K)
+    ndc = np.empty(9, np.float64)
+    rng = np.empty(4, np.float32)
+    lib().orc_intrinsics_to_ndc(_p(K), ctypes.c_int(H), ctypes.c_int(W), _p(ndc), _p(rng))
+    return ndc.reshape(3, 3), rng
+
+
+def extract_face_ndc(verts, faces, K, H, W, near=0.0, far=float("inf")):
+    verts, faces, K = _f32(verts), _i64(faces), _f64(K)
+    F = len(faces)
+    out = np.empty((F, 3, 3), np.float32)
+    mask = np.empty(F, np.uint8)
+    lib().orc_extract_face_ndc(_p(verts), _p(faces), ctypes.c_int64(F), _p(K), ctypes.c_int(H), ctypes.c_int(W),
+                               ctypes.c_float(near), ctypes.c_float(far), _p(out), _p(mask))
+    return out, mask.astype(bool)
+
+
+def rasterize(face_ndc, mask, H, W, blur_radius_pixels=0.0, faces_per_pixel=8, bin_size=-1, max_faces_per_bin=-1,
+              perspective_correct=False, clip_barycentric=False, cull_back_faces=True):
+    face_ndc = _f32(face_ndc)
+    F = len(face_ndc)
+    m = None if mask is None else _u8(mask)
+    Kf = faces_per_pixel
+    fi = np.empty((H, W, Kf), np.int64)
+    dep = np.empty((H, W, Kf), np.float32)
+    bary = np.empty((H, W, Kf, 3), np.float32)
+    dist = np.empty((H, W, Kf), np.float32)
+    _check(lib().orc_rasterize(_p(face_ndc), _p(m), ctypes.c_int64(F), ctypes.c_int(H), ctypes.c_int(W),
+                               ctypes.c_float(blur_radius_pixels), ctypes.c_int(Kf), ctypes.c_int(bin_size),
+                               ctypes.c_int(max_faces_per_bin), ctypes.c_int(int(perspective_correct)),
+                               ctypes.c_int(int(clip_barycentric)), ctypes.c_int(int(cull_back_faces)),
+                               _p(fi), _p(dep), _p(bary), _p(dist)))
+    return fi, dep, bary, dist
+
+
+def rasterize_k1_fast(face_ndc, mask, H, W, blur_radius_pixels=0.0, perspective_correct=False, cull_back_faces=True):
+    face_ndc = _f32(face_ndc)
+    F = len(face_ndc)
+    m = None if mask is None else _u8(mask)
+    fi = np.empty((H, W, 1), np.int64)
+    dep = np.empty((H, W, 1), np.float32)
+    bary = np.empty((H, W, 1, 3), np.float32)
+    dist = np.empty((H, W, 1), np.float32)
+    _check(lib().orc_rasterize_k1_fast(_p(face_ndc), _p(m), ctypes.c_int64(F), ctypes.c_int(H), ctypes.c_int(W),
+                                       ctypes.c_float(blur_radius_pixels), ctypes.c_int(int(perspective_correct)),
+                                       ctypes.c_int(int(cull_back_faces)), _p(fi), _p(dep), _p(bary), _p(dist)))
+    return fi, dep, bary, dist
+
+
+def interpolate_face_attributes(pixel_faces, bary, face_attrs):
+    pixel_faces, bary, face_attrs = _i64(pixel_faces), _f32(bary), _f32(face_attrs)
+    H, W, Kf = pixel_faces.shape
+    C = face_attrs.shape[2]
+    out = np.empty((H, W, Kf, C), np.float32)
+    lib().orc_interpolate_face_attributes(_p(pixel_faces), _p(bary), ctypes.c_int64(H * W), ctypes.c_int(Kf), _p(face_attrs),
+                                          ctypes.c_int(C), _p(out))
+    return out
+
+
+def unproject(depth, K, depth_scale=1.0, depth_max=10.0):
+    depth, K = _f32(depth), _f64(K)
+    H, W = depth.shape[:2]
+    pts = np.empty((H * W, 3), np.float32)
+    mask = np.empty(H * W, np.uint8)
+    lib().orc_unproject(_p(depth), ctypes.c_int(H), ctypes.c_int(W), _p(K), ctypes.c_float(depth_scale), ctypes.c_float(depth_max),
+                        _p(pts), _p(mask))
+    return pts, mask.astype(bool)
+
+
+def warped_surface_jacobians(points, normals, nodes, rotations, anchors, weights):
+    points, normals, nodes, rotations, anchors, weights = _f32(points), _f32(normals), _f32(nodes), _f32(rotations), _i32(anchors), _f32(weights)
+    V, K = anchors.shape
+    vj = np.empty((V, K, 4), np.float32)
+    nj = np.empty((V, K, 3), np.float32)
+    lib().orc_warped_surface_jacobians(_p(points), _p(normals), ctypes.c_int64(V), _p(nodes), _p(rotations), _p(anchors), _p(weights),
+                                       ctypes.c_int(K), _p(vj), _p(nj))
+    return vj, nj
+
+
+def rasterized_surface_jacobians(verts, normals, faces, pixel_faces, pixel_bary, K, perspective_correct=True):
+    verts, normals, faces, pixel_faces, pixel_bary, K = _f32(verts), _f32(normals), _i64(faces), _i64(pixel_faces), _f32(pixel_bary), _f64(K)
+    H, W, Kf = pixel_faces.shape
+    vj = np.empty((H, W, 3, 9), np.float32)
+    nj = np.empty((H, W, 3, 10), np.float32)
+    lib().orc_rasterized_surface_jacobians(_p(verts), _p(normals), _p(faces), _p(pixel_faces), _p(pixel_bary), ctypes.c_int(H),
+                                           ctypes.c_int(W), ctypes.c_int(Kf), _p(K), ctypes.c_int(int(perspective_correct)), _p(vj), _p(nj))
+    return vj, nj
+
+
+def associate_faces_with_anchors(faces, anchors):
+    faces, anchors = _i64(faces), _i32(anchors)
+    F, K = len(faces), anchors.shape[1]
+    nodes = np.empty((F, 3 * K), np.int32)
+    slots = np.empty((F, 3 * K, 3), np.int32)
+    counts = np.empty(F, np.int32)
+    lib().orc_associate_faces_with_anchors(_p(faces), ctypes.c_int64(F), _p(anchors), ctypes.c_int(K), _p(nodes), _p(slots), _p(counts))
+    return nodes, slots, counts
+
+
+def pixel_vertex_anchor_jacobians(rast_vj, rast_nj, warped_vj, warped_nj, point_map_vectors, rasterized_normals, residual_mask,
+                                  pixel_faces, faces, face_nodes, face_slots, face_counts, use_tukey=False, tukey_cutoff=0.01, mode="ALL"):
+    m = MODE[mode]
+    rast_vj, rast_nj, warped_vj = _f32(rast_vj), _f32(rast_nj), _f32(warped_vj)
+    warped_nj = _f32(warped_nj) if warped_nj is not None else np.zeros(1, np.float32)
+    pmv, rn, rm = _f32(point_map_vectors), _f32(rasterized_normals), _u8(residual_mask)
+    pixel_faces, faces = _i64(pixel_faces), _i64(faces)
+    face_nodes, face_slots, face_counts = _i32(face_nodes), _i32(face_slots), _i32(face_counts)
+    P = rm.size
+    K = face_nodes.shape[1] // 3
+    Kf = pixel_faces.shape[-1]
+    s = 6 if m == 0 else 3
+    pj = np.empty((P, 3 * K, s), np.float32)
+    pc = np.empty(P, np.int32)
+    lib().orc_pixel_vertex_anchor_jacobians(_p(rast_vj), _p(rast_nj), _p(warped_vj), _p(warped_nj), ctypes.c_int(K), _p(pmv), _p(rn), _p(rm),
+                                            _p(pixel_faces), ctypes.c_int(Kf), _p(faces), _p(face_nodes), _p(face_slots), _p(face_counts),
+                                            ctypes.c_int64(P), ctypes.c_int(int(use_tukey)), ctypes.c_float(tukey_cutoff), ctypes.c_int(m),
+                                            _p(pj), _p(pc))
+    return pj, pc
+
+
+def data_hessian_gradient(pixel_jacobians, pixel_counts, pixel_faces, face_nodes, residuals, residual_mask, node_count, mode="ALL"):
+    m = MODE[mode]
+    s = 6 if m == 0 else 3
+    pj, pc, pf, fn = _f32(pixel_jacobians), _i32(pixel_counts), _i64(pixel_faces), _i32(face_nodes)
+    r, rm = _f32(residuals), _u8(residual_mask)
+    P = rm.size
+    K = fn.shape[1] // 3
+    Kf = pf.shape[-1]
+    H = np.empty((node_count, s, s), np.float32)
+    g = np.empty(node_count * s, np.float32)
+    lib().orc_data_hessian_gradient(_p(pj), _p(pc), _p(pf), ctypes.c_int(Kf), _p(fn), ctypes.c_int(K), _p(r), _p(rm), ctypes.c_int64(P),
+                                    ctypes.c_int(node_count), ctypes.c_int(m), _p(H), _p(g))
+    return H, g
+
+
+def arap_residuals(edges, edge_layers, radii, node_weights, nodes, rotations, translations, weight, use_huber=False, huber=1e-4):
+    edges = _i32(edges)
+    E = len(edges)
+    out = np.empty(E * 3, np.float32)
+    el = None if edge_layers is None else np.ascontiguousarray(edge_layers, np.int8)
+    rd = None if radii is None else _f32(radii)
+    nw = None if node_weights is None else _f32(node_weights)
+    nodes, rotations, translations = _f32(nodes), _f32(rotations), _f32(translations)
+    _check(lib().orc_arap_residuals(_p(edges), ctypes.c_int(E), _p(el), _p(rd), _p(nw), _p(nodes), _p(rotations),
+                                    _p(translations), ctypes.c_float(weight), ctypes.c_int(int(use_huber)), ctypes.c_float(huber),
+                                    _p(out)))
+    return out
+
+
+def arap_edge_jacobians(edges, edge_layers, radii, node_weights, nodes, rotations, weight):
+    edges = _i32(edges)
+    E = len(edges)
+    out = np.empty((E, 5), np.float32)
+    el = None if edge_layers is None else np.ascontiguousarray(edge_layers, np.int8)
+    rd = None if radii is None else _f32(radii)
+    nw = None if node_weights is None else _f32(node_weights)
+    nodes, rotations = _f32(nodes), _f32(rotations)
+    lib().orc_arap_edge_jacobians(_p(edges), ctypes.c_int(E), _p(el), _p(rd), _p(nw), _p(nodes), _p(rotations),
+                                  ctypes.c_float(weight), _p(out))
+    return out
+
+
+def arap_hessian(edges, edge_jacobians, node_count):
+    edges, ej = _i32(edges), _f32(edge_jacobians)
+    E = len(edges)
+    diag = np.empty((node_count, 6, 6), np.float32)
+    wing = np.empty((E, 6, 6), np.float32)
+    lib().orc_arap_hessian(_p(edges), ctypes.c_int(E), _p(ej), ctypes.c_int(node_count), _p(diag), _p(wing))
+    return diag, wing
+
+
+def arap_gradient(edges, edge_jacobians, residuals, g):
+    g = _f32(g).copy()
+    edges, edge_jacobians, residuals = _i32(edges), _f32(edge_jacobians), _f32(residuals)
+    lib().orc_arap_gradient(_p(edges), ctypes.c_int(len(edges)), _p(edge_jacobians), _p(residuals), _p(g))
+    return g
+
+
+def solve_block_diagonal(H, g, lm=0.0):
+    H, g = _f32(H), _f32(g)
+    N, s = H.shape[0], H.shape[1]
+    x = np.empty(N * s, np.float32)
+    rc = lib().orc_solve_block_diagonal(_p(H), _p(g), ctypes.c_int(N), ctypes.c_int(s), ctypes.c_float(lm), _p(x))
+    return x, rc
+
+
+def solve_arrowhead(diag, wing, edges, n0, g):
+    diag, wing, edges, g = _f32(diag), _f32(wing), _i32(edges), _f32(g)
+    N = diag.shape[0]
+    x = np.empty(N * 6, np.float32)
+    _check(lib().orc_solve_arrowhead(_p(diag), _p(wing), _p(edges), ctypes.c_int(len(edges)), ctypes.c_int(N), ctypes.c_int(n0), _p(g), _p(x)))
+    return x
+
+
+def rodrigues(w):
+    w = _f32(w).reshape(-1, 3)
+    R = np.empty((len(w), 3, 3), np.float32)
+    lib().orc_rodrigues(_p(w), ctypes.c_int(len(w)), _p(R))
+    return R
+
+
+class _Params(ctypes.Structure):
+    _fields_ = [("max_iterations", ctypes.c_int), ("mode_count", ctypes.c_int), ("modes", ctypes.c_int * 16),
+                ("use_perspective_correction", ctypes.c_int), ("max_depth", ctypes.c_float), ("use_tukey", ctypes.c_int),
+                ("tukey_cutoff", ctypes.c_float), ("lm_factor", ctypes.c_float), ("arap_weight", ctypes.c_float),
+                ("use_huber", ctypes.c_int), ("huber_delta", ctypes.c_float)]
+
+
+class _WarpField(ctypes.Structure):
+    _fields_ = [("N", ctypes.c_int), ("K", ctypes.c_int), ("coverage", ctypes.c_float), ("coverage_method", ctypes.c_int),
+                ("min_valid_anchors", ctypes.c_int), ("nodes", ctypes.c_void_p), ("rotations", ctypes.c_void_p),
+                ("translations", ctypes.c_void_p), ("node_weights", ctypes.c_void_p), ("E", ctypes.c_int), ("edges", ctypes.c_void_p),
+                ("edge_layers", ctypes.c_void_p), ("radii", ctypes.c_void_p), ("first_layer_count", ctypes.c_int)]
+
+
+class _Outputs(ctypes.Structure):
+    _fields_ = [("residuals", ctypes.c_void_p), ("residual_mask", ctypes.c_void_p), ("pixel_faces", ctypes.c_void_p),
+                ("updates", ctypes.c_void_p), ("gradient", ctypes.c_void_p), ("hessian_diag", ctypes.c_void_p),
+                ("stage_seconds", ctypes.c_void_p)]
+
+
+def fit(*, nodes, rotations, translations, mesh_points, mesh_normals, faces, ref_points, ref_mask, H, W, K, extrinsics=None,
+        max_iterations=1, modes=("ALL",), use_perspective_correction=True, max_depth=10.0, use_tukey=False, tukey_cutoff=0.01,
+        lm_factor=0.0, arap_weight=200.0, use_huber=False, huber_delta=1e-4, anchor_count=4, coverage=0.05, coverage_method=0,
+        node_weights=None, min_valid_anchors=0, edges=None, edge_layers=None, radii=None, first_layer_count=None, fast_raster=True):
+    """Full FitToImage on the CPU restatement (virtual node order). Returns (R, t, diagnostics of the last iteration)."""
+    nodes = _f32(nodes)
+    R = _f32(rotations).copy()
+    t = _f32(translations).copy()
+    N = len(nodes)
+    prm = _Params()
+    prm.max_iterations = max_iterations
+    prm.mode_count = len(modes)
+    for i, m in enumerate(modes):
+        prm.modes[i] = MODE[m]
+    prm.use_perspective_correction = int(use_perspective_correction)
+    prm.max_depth = max_depth
+    prm.use_tukey = int(use_tukey)
+    prm.tukey_cutoff = tukey_cutoff
+    prm.lm_factor = lm_factor
+    prm.arap_weight = arap_weight
+    prm.use_huber = int(use_huber)
+    prm.huber_delta = huber_delta
+    keep = []
+
+    def ptr(a):
+        keep.append(a)
+        return a.ctypes.data
+
+    wf = _WarpField()
+    wf.N, wf.K, wf.coverage, wf.coverage_method, wf.min_valid_anchors = N, anchor_count, coverage, coverage_method, min_valid_anchors
+    wf.nodes, wf.rotations, wf.translations = ptr(nodes), ptr(R), ptr(t)
+    wf.node_weights = ptr(_f32(node_weights)) if node_weights is not None else None
+    if edges is not None and len(edges) > 0:
+        wf.E = len(edges)
+        wf.edges = ptr(_i32(edges))
+        wf.edge_layers = ptr(np.ascontiguousarray(edge_layers, np.int8))
+        wf.radii = ptr(_f32(radii))
+        wf.first_layer_count = first_layer_count
+    else:
+        wf.E = 0
+    P = H * W
+    s = 6 if modes[(max_iterations - 1) % len(modes)] == "ALL" else 3
+    diag = dict(residuals=np.zeros(P, np.float32), residual_mask=np.zeros(P, np.uint8), pixel_faces=np.zeros(P, np.int64),
+                updates=np.zeros(N * s, np.float32), gradient=np.zeros(N * s, np.float32), hessian_diag=np.zeros(N * s * s, np.float32),
+                stage_seconds=np.zeros(8, np.float64))
+    outs = _Outputs(*[ptr(diag[k]) for k in ("residuals", "residual_mask", "pixel_faces", "updates", "gradient", "hessian_diag",
+                                               "stage_seconds")])
+    E = None if extrinsics is None else ptr(_f64(extrinsics))
+    rc = lib().orc_fit(ctypes.byref(prm), ctypes.byref(wf), ctypes.c_void_p(ptr(_f32(mesh_points))),
+                       ctypes.c_void_p(ptr(_f32(mesh_normals))), ctypes.c_int64(len(mesh_points)),
+                       ctypes.c_void_p(ptr(_i64(faces))), ctypes.c_int64(len(faces)), ctypes.c_void_p(ptr(_f32(ref_points))),
+                       ctypes.c_void_p(ptr(_u8(ref_mask))), ctypes.c_int(H), ctypes.c_int(W),
+                       ctypes.c_void_p(ptr(_f64(K))), ctypes.c_void_p(E), ctypes.c_int(int(fast_raster)), ctypes.byref(outs))
+    _check(rc)
+    diag["residual_mask"] = diag["residual_mask"].astype(bool)
+    return R, t, diag
