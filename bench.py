@@ -1,0 +1,274 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Gauss-Newton iterations/s of DeformableMeshToImageFitter (BASELINE.json metric) on MI355X.
+
+Workload (BASELINE.json configs[1]): one 640x480 synthetic depth frame, a 1500-node warp graph
+(50x30, node coverage 0.03, 4 anchors, block-diagonal solve), a 321x241 grid mesh (77,361 vertices, 153,600
+triangles). The target depth is the mesh rendered under a smooth ground-truth motion; random-free, seed = rank.
+
+A step = restore the identity warp (R = I, t = 0) + one full GN iteration (warp, rasterize, residuals, Jacobians,
+JtJ / Jt r, LM block solve, Rodrigues update) replayed from a hipGraph. The reference's own block-diagonal GN diverges
+on multi-node scenes after 2-3 iterations (SURVEY.md / DESIGN.md section "Divergence"), so every step starts from the
+same state: each timed iteration does the work of the first iteration of a frame, with nothing cached between steps.
+
+N > 1: one process per GPU (torchrun), each fitting its own independent sequence (seed = rank) -- replicas, no
+collective in the data path; the only collectives are the barrier and the max-over-ranks of the elapsed time.
+
+Also reported: the dominant kernel's roofline (k_fit_pixels, HIP-event timed on the fitter's work stream) and the
+CPU baseline (the oracle/ C++ restatement, OpenMP, on a bounded sample of the same workload, rank 0, N = 1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM": 8 TB/s spec)
+DEFAULT_CONFIG = "C2"
+ROOFLINE_KERNEL = "k_fit_pixels"
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# distributed helpers (GPU-free; covered by tests/test_distributed_cpu.py with gloo)
+# ---------------------------------------------------------------------------------------------------------------------
+def dist_env():
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device if device is not None else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def aggregate(steps: int, elapsed_s: float, world: int) -> dict:
+    """Whole-job throughput: every rank runs `steps` iterations; the job takes the slowest rank's time."""
+    return dict(value=world * steps / elapsed_s, ms_per_step=1000.0 * elapsed_s / steps)
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# algorithmic bytes (DESIGN.md "Kernels and rooflines")
+# ---------------------------------------------------------------------------------------------------------------------
+def fit_pixels_bytes(P: int, F: int, V: int, N: int, anchor_count: int, nacc: int = 27) -> int:
+    """Compulsory HBM bytes of one k_fit_pixels launch: per pixel the raster key (8 B read + 8 B reset), the reference
+    depth (4 B), residual (4 B), residual mask (1 B), rasterized face (4 B); every face record once (int4, 16 B); per
+    vertex its warped position + normal (2 x float4), anchors (4 B x K) and warped Jacobians (2 x float4 x K); per node
+    the accumulator row (nacc floats, read + write)."""
+    per_pixel = 8 + 8 + 4 + 4 + 1 + 4
+    per_vertex = 16 + 16 + anchor_count * (4 + 16 + 16)
+    return P * per_pixel + F * 16 + V * per_vertex + N * nacc * 4 * 2
+
+
+def iteration_bytes(P: int, F: int, V: int, N: int, anchor_count: int) -> int:
+    """Compulsory bytes of the whole iteration (all kernels): warp (read canonical mesh 24 B/vertex, anchors+weights,
+    node state; write float4 position/normal + Jacobians), raster scatter (face record + warped vertices, one 8 B
+    atomicMin per covered pixel ~ P), k_fit_pixels (above), solve (accumulator + node state)."""
+    warp = V * (24 + anchor_count * 8 + 32 + anchor_count * 32) + N * 64
+    scatter = F * 16 + V * 16 + P * 8
+    solve = N * (27 * 4 * 2 + 64 * 2)
+    return warp + scatter + fit_pixels_bytes(P, F, V, N, anchor_count) + solve
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--config", default=DEFAULT_CONFIG, help="synthetic workload (dynamicfuion_python_amd.synthetic.CONFIGS)")
+    ap.add_argument("--timed-steps", type=int, default=100, help="eager per-stage HIP-event timing steps (roofline)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU-baseline sample (loop-body seconds)")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="OpenMP threads for the CPU baseline (the box's CPU share)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
+                    help="PMC-derived HBM bytes per launch of the roofline kernel (tools/pmc_traffic.py output)")
+    return ap.parse_args(argv)
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def render_target(sc, G, Rr):
+    """Target depth = the canonical mesh warped by the ground-truth motion and rasterized (on the GPU, through the same
+    C-ABI entry points the fitter exposes); pixels without geometry -> 0."""
+    mesh = G.TriangleMesh(sc.points, sc.normals, sc.faces)
+    a, w = G.compute_anchors_and_weights_euclidean_fixed_node_weight(sc.points, sc.nodes, 4, 0, sc.coverage)
+    warped = G.warp_triangle_mesh(mesh, sc.nodes, sc.gt_rotations, sc.gt_translations, a, w)
+    fndc, fm = Rr.get_mesh_ndc_face_vertices_and_clip_mask(warped, sc.K, (sc.H, sc.W), 0.0, 10.0)
+    _, dep, _, _ = Rr.rasterize_ndc_triangles(fndc, fm, (sc.H, sc.W), 0.5, 1, -1, -1, True, False, True)
+    d = dep[..., 0]
+    return (d * (d > 0)).contiguous()
+
+
+def load_traffic(path: str, workload: str):
+    try:
+        with open(path) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if t.get("workload") != workload or t.get("kernel") != ROOFLINE_KERNEL:
+        return None, None
+    return t.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+
+
+def cpu_baseline(sc, depth_host, threads: int, budget_s: float):
+    """The oracle (C++/OpenMP restatement of the reference CPU path; test infrastructure, used here only as the
+    reported baseline) running the same step: 1 GN iteration from the identity warp. Timed = loop body S1-S12
+    (DeformableMeshToImageFitter.cpp:111-275), once-per-frame setup excluded, as in the GPU step."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    O.set_num_threads(threads)
+    refp, refm = O.unproject(depth_host, sc.K, 1.0, 10.0)
+    N = len(sc.nodes)
+    R0 = np.tile(np.eye(3, dtype=np.float32), (N, 1, 1))
+    t0 = np.zeros((N, 3), np.float32)
+    body = solve = 0.0
+    iters = 0
+    wall0 = time.perf_counter()
+    while body < budget_s and time.perf_counter() - wall0 < 3 * budget_s:
+        _, _, dg = O.fit(nodes=sc.nodes, rotations=R0, translations=t0, mesh_points=sc.points, mesh_normals=sc.normals, faces=sc.faces,
+                         ref_points=refp, ref_mask=refm, H=sc.H, W=sc.W, K=sc.K, max_iterations=1, lm_factor=0.001, coverage=sc.coverage)
+        if iters > 0:   # first call warms caches / page-ins
+            body += dg["stage_seconds"][7]
+            solve += dg["stage_seconds"][5]
+        iters += 1
+    n = max(iters - 1, 1)
+    return dict(value=n / body if body > 0 else None, unit="GN iters/s", cores=O.num_threads(), kind="port",
+                ms_per_solve=1000.0 * solve / n,
+                sample=f"{sc.name}: {n} single GN iterations from the identity warp (loop body timed, setup excluded), "
+                       f"oracle/ C++ OpenMP restatement, fast K=1 raster")
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    rank, local_rank, world = dist_env()
+    import torch
+    import torch.distributed as dist
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a HIP device (the MI355X path has no CPU fallback)")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group(backend="nccl", device_id=dev)
+
+    from dynamicfuion_python_amd import _native as NV
+    from dynamicfuion_python_amd import synthetic as S
+    from dynamicfuion_python_amd.nnrt import alignment as A
+    from dynamicfuion_python_amd.nnrt import geometry as G
+    from dynamicfuion_python_amd.nnrt import rendering as Rr
+
+    sc = S.make_scene(args.config, seed=rank)
+    if sc.layer_count > 1:
+        raise SystemExit("bench.py drives the block-diagonal configs (C1/C2/C3); ARAP configs are parity-test cases")
+    P, F, V, Nn = sc.H * sc.W, len(sc.faces), len(sc.points), len(sc.nodes)
+    workload = (f"{sc.name}: {sc.W}x{sc.H} depth, {Nn}-node graph, {V}-vertex/{F}-triangle mesh, block-diagonal LM solve, "
+                f"1 GN iteration per step from the identity warp")
+    log(f"rank {rank}/{world} on {torch.cuda.get_device_name(dev)}: {workload}")
+
+    depth = render_target(sc, G, Rr)
+    wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE, 1)
+    ft = A.DeformableMeshToImageFitter(1, [A.IterationMode.ALL], preconditioning_dampening_factor=0.001, use_hip_graph=True)
+    mesh = G.TriangleMesh(sc.points, sc.normals, sc.faces)
+    ft.prepare(wf, mesh, depth, None, sc.K)
+
+    lib = NV.lib()
+    stream = torch.cuda.current_stream(dev)
+    s_ptr = NV.stream_ptr(stream)
+    wf_h, ft_h = wf.handle, ft._h
+
+    def step():
+        st = lib.nnrt_warp_field_reset_motion(wf_h, s_ptr)
+        st |= lib.nnrt_fitter_iterate(ft_h, wf_h, 0, 1, s_ptr)
+        return st
+
+    # warmup (first call captures the iteration graph)
+    for _ in range(args.warmup):
+        if step():
+            NV.check(1)
+    torch.cuda.synchronize(dev)
+    ft.check()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    bad = 0
+    for _ in range(args.steps):
+        bad |= step()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    if bad:
+        NV.check(bad)
+    ft.check()   # solver failure flag (potrf) -> raises
+    elapsed_max = max_over_ranks(elapsed, dev)
+    agg = aggregate(args.steps, elapsed_max, world)
+
+    # per-stage device time (eager launches, HIP events on the fitter's work stream), same step
+    stages = dict(warp=0.0, raster=0.0, pixels=0.0, arap=0.0, solve=0.0)
+    for _ in range(args.timed_steps):
+        wf.reset_motion()
+        r = ft.iterate_timed(wf, 0, 1)
+        for k in stages:
+            stages[k] += r[k] / args.timed_steps
+    ft.check()
+
+    # sanity: the measured iteration produced a finite, non-zero update (parity itself is tests/test_gpu_parity.py)
+    dg = ft.diagnostics()
+    if not (np.isfinite(dg["updates"]).all() and np.abs(dg["updates"]).max() > 0):
+        raise SystemExit("non-finite or empty GN update in the timed configuration")
+
+    kbytes = fit_pixels_bytes(P, F, V, Nn, 4)
+    k_ms = stages["pixels"]
+    achieved = kbytes / (k_ms * 1e-3) / 1e9
+    traffic, traffic_src = load_traffic(args.traffic_file, workload)
+
+    out = {
+        "metric": "GN iters/sec (640x480, 1.5k-node graph)" if args.config == "C2" else f"GN iters/sec ({args.config})",
+        "value": agg["value"],
+        "unit": "GN iters/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": agg["ms_per_step"],
+        "ms_per_solve": stages["solve"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (smooth grid mesh + GT node motion rendered to depth; seed = rank)",
+        "config": {"workload": workload, "config": args.config, "frame": [sc.H, sc.W], "nodes": Nn, "vertices": V, "triangles": F,
+                   "anchors": 4, "iteration_mode": "ALL", "lm_damping": 0.001, "hip_graph": True,
+                   "parallelism": f"replicas{world}" if world > 1 else "single"},
+        "stage_ms": {k: round(v, 5) for k, v in stages.items()},
+        "roofline": {"kernel": ROOFLINE_KERNEL, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "algorithmic_bytes": kbytes, "kernel_ms": k_ms,
+                     "traffic_source": traffic_src,
+                     "iteration_algorithmic_bytes": iteration_bytes(P, F, V, Nn, 4),
+                     "iteration_frac": iteration_bytes(P, F, V, Nn, 4) / (agg["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log(f"GPU: {agg['value']:.1f} it/s; running the CPU baseline sample (~{args.cpu_seconds:.0f} s)")
+        out["cpu_baseline"] = cpu_baseline(sc, depth.cpu().numpy(), args.cpu_threads, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -55,6 +55,7 @@ _SIGNATURES = {
     "nnrt_warp_field_set_node_rotations": (c_int32, [c_void_p, c_void_p, c_int32]),
     "nnrt_warp_field_set_node_translations": (c_int32, [c_void_p, c_void_p, c_int32]),
     "nnrt_warp_field_get_node_coverage_weights": (c_int32, [c_void_p, c_void_p]),
+    "nnrt_warp_field_reset_motion": (c_int32, [c_void_p, c_void_p]),
     "nnrt_fitter_default_params": (None, [c_void_p]),
     "nnrt_fitter_create": (c_int32, [c_void_p, c_int32, ctypes.POINTER(c_void_p)]),
     "nnrt_fitter_destroy": (None, [c_void_p]),
@@ -63,6 +64,7 @@ _SIGNATURES = {
     "nnrt_fitter_prepare": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                       c_int32, c_int32, c_void_p, c_void_p, c_float, c_void_p]),
     "nnrt_fitter_iterate": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
+    "nnrt_fitter_iterate_timed": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     "nnrt_fitter_check": (c_int32, [c_void_p, c_void_p]),
     "nnrt_fitter_get_diagnostics": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "nnrt_fitter_get_anchors": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -115,6 +117,12 @@ def check(status: int):
 def require_gpu():
     if not torch.cuda.is_available():
         raise RuntimeError("no HIP device is visible: the MI355X path has no CPU fallback")
+
+
+def current_device() -> int:
+    """torch's current HIP device (one process per GPU: torch.cuda.set_device(LOCAL_RANK) selects it)."""
+    require_gpu()
+    return torch.cuda.current_device()
 
 
 def ptr(t) -> c_void_p:

@@ -283,6 +283,22 @@ nnrt_status nnrt_warp_field_set_node_translations(nnrt_warp_field* wf, const flo
 nnrt_status nnrt_warp_field_set_node_rotations(nnrt_warp_field* wf, const float* h_in, int32_t virtual_order) {
 	return wf_set(wf, h_in, virtual_order, 6, 9);
 }
+__global__ void k_reset_motion(float* state, int N) {
+	const int n = blockIdx.x * blockDim.x + threadIdx.x;
+	if (n >= N) return;
+	float* s = state + static_cast<int64_t>(n) * NODE_STRIDE;
+	for (int c = 3; c < 15; c++) s[c] = 0.f;
+	s[6] = s[10] = s[14] = 1.f;
+}
+
+nnrt_status nnrt_warp_field_reset_motion(nnrt_warp_field* wf, void* stream) {
+	NNRT_CHECK_ARG(wf, "null pointer");
+	DeviceGuard guard(wf->device);
+	k_reset_motion<<<static_cast<unsigned>(ceil_div(wf->N, 256)), 256, 0, static_cast<hipStream_t>(stream)>>>(wf->state.ptr, wf->N);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
 nnrt_status nnrt_warp_field_get_node_coverage_weights(const nnrt_warp_field* wf, float* h_out) {
 	NNRT_CHECK_ARG(wf && h_out, "null pointer");
 	std::memcpy(h_out, wf->weights_virtual.data(), sizeof(float) * wf->N);
@@ -358,14 +374,21 @@ __global__ void k_faces_to_int4(const int64_t* __restrict__ faces, int64_t F, in
 	out[f] = make_int4(static_cast<int>(faces[3 * f]), static_cast<int>(faces[3 * f + 1]), static_cast<int>(faces[3 * f + 2]), 0);
 }
 
-nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mode, hipStream_t s) {
+nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mode, hipStream_t s, hipEvent_t* marks = nullptr) {
 	nnrt_status st;
+	auto mark = [&](int i) -> nnrt_status {
+		if (marks) NNRT_HIP(hipEventRecord(marks[i], s));
+		return NNRT_OK;
+	};
+	if ((st = mark(0))) return st;
 	const bool with_jacobians = true;
 	if ((st = launch_warp_mesh(ft->mesh_p.ptr, ft->mesh_n.ptr, ft->V, wf->state.ptr, ft->anchors.ptr, ft->weights.ptr, ft->K, ft->extr,
 	                           ft->wpos.ptr, ft->wnrm.ptr, with_jacobians ? ft->jv.ptr : nullptr, ft->jn.ptr, s)))
 		return st;
+	if ((st = mark(1))) return st;
 	RasterOptions ro{ft->H, ft->W, 0.5f / (static_cast<float>(fminf(ft->H, ft->W)) / 2.0f), ft->p.use_perspective_correction, 0, 1};
 	if ((st = launch_raster_scatter_mesh(ft->wpos.ptr, ft->faces4.ptr, ft->F, ft->ndc, 0.0f, 10.0f, ro, ft->keys.ptr, s))) return st;
+	if ((st = mark(2))) return st;
 	FitPixelArgs fa{};
 	fa.H = ft->H;
 	fa.W = ft->W;
@@ -392,6 +415,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 	fa.pixel_face = ft->pixel_face.ptr;
 	fa.acc = ft->acc.ptr;
 	if ((st = launch_fit_pixels(mode, fa, s))) return st;
+	if ((st = mark(3))) return st;
 	if (ft->E > 0) {
 		ArapArgs aa{};
 		aa.E = ft->E;
@@ -411,11 +435,13 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 		aa.edge_residuals = ft->edge_residuals.ptr;
 		aa.error_flag = ft->error_flag.ptr;
 		if ((st = launch_arap_edges(aa, s))) return st;
+		if ((st = mark(4))) return st;
 		const float lm = ft->p.preconditioning_dampening_factor;
 		if ((st = launch_arrowhead_iteration(ft->aw, ft->acc.ptr, lm, wf->edges.ptr, ft->wing.ptr, wf->state.ptr, ft->arap_acc.ptr,
 		                                     ft->updates.ptr, ft->gradient.ptr, ft->hessian.ptr, ft->error_flag.ptr, s)))
 			return st;
 	} else {
+		if ((st = mark(4))) return st;
 		SolveArgs sa{};
 		sa.N = ft->N;
 		sa.lm = ft->p.preconditioning_dampening_factor;
@@ -427,7 +453,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 		sa.error_flag = ft->error_flag.ptr;
 		if ((st = launch_solve_update(mode, sa, s))) return st;
 	}
-	return NNRT_OK;
+	return mark(5);
 }
 
 } // namespace
@@ -647,6 +673,43 @@ nnrt_status nnrt_fitter_iterate(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t fi
 	NNRT_HIP(hipEventRecord(ft->ev_out, s));
 	NNRT_HIP(hipStreamWaitEvent(us, ft->ev_out, 0));
 	return NNRT_OK;
+}
+
+nnrt_status nnrt_fitter_iterate_timed(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_iteration, int32_t count, float* h_stage_ms,
+                                      void* stream) {
+	NNRT_CHECK_ARG(ft && wf && h_stage_ms && count > 0, "invalid arguments");
+	if (!ft->prepared || ft->wf != wf) {
+		set_error("nnrt_fitter_prepare must be called with this warp field before nnrt_fitter_iterate_timed");
+		return NNRT_ERROR_ARGUMENT;
+	}
+	DeviceGuard guard(ft->device);
+	hipStream_t us = static_cast<hipStream_t>(stream);
+	NNRT_HIP(hipEventRecord(ft->ev_in, us));
+	NNRT_HIP(hipStreamWaitEvent(ft->work, ft->ev_in, 0));
+	std::vector<hipEvent_t> ev(static_cast<size_t>(count) * 6, nullptr);
+	for (auto& e : ev) NNRT_HIP(hipEventCreate(&e));
+	nnrt_status st = NNRT_OK;
+	for (int i = 0; i < count && !st; i++) {
+		const int it = first_iteration + i;
+		const int mode = ft->p.iteration_modes[it % ft->p.iteration_mode_count];
+		ft->last_mode = mode;
+		st = enqueue_iteration(ft, wf, mode, ft->work, &ev[static_cast<size_t>(i) * 6]);
+	}
+	if (!st) {
+		NNRT_HIP(hipStreamSynchronize(ft->work));
+		for (int k = 0; k < 5; k++) h_stage_ms[k] = 0.f;
+		for (int i = 0; i < count; i++)
+			for (int k = 0; k < 5; k++) {
+				float ms = 0.f;
+				NNRT_HIP(hipEventElapsedTime(&ms, ev[static_cast<size_t>(i) * 6 + k], ev[static_cast<size_t>(i) * 6 + k + 1]));
+				h_stage_ms[k] += ms / count;
+			}
+	}
+	for (auto& e : ev)
+		if (e) hipEventDestroy(e);
+	NNRT_HIP(hipEventRecord(ft->ev_out, ft->work));
+	NNRT_HIP(hipStreamWaitEvent(us, ft->ev_out, 0));
+	return st;
 }
 
 nnrt_status nnrt_fitter_check(nnrt_fitter* ft, void* stream) {

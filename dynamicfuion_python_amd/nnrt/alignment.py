@@ -23,8 +23,9 @@ class DeformableMeshToImageFitter:
     def __init__(self, max_iteration_count: int = 100, iteration_mode_sequence=(IterationMode.ALL,), minimal_update_threshold: float = 1e-6,
                  use_perspective_correction: bool = True, max_depth: float = 10.0, use_tukey_penalty_for_data_term: bool = False,
                  tukey_penalty_cutoff_cm: float = 0.01, preconditioning_dampening_factor: float = 0.0, arap_term_weight: float = 200.0,
-                 use_huber_penalty_for_arap_term: bool = False, huber_penalty_constant: float = 1e-4, device: int = 0,
+                 use_huber_penalty_for_arap_term: bool = False, huber_penalty_constant: float = 1e-4, device: int | None = None,
                  use_hip_graph: bool = True):
+        device = N.current_device() if device is None else int(device)
         p = N.FitterParams()
         N.lib().nnrt_fitter_default_params(ctypes.byref(p))
         modes = list(iteration_mode_sequence)
@@ -79,6 +80,12 @@ class DeformableMeshToImageFitter:
 
     def iterate(self, warp_field: HierarchicalGraphWarpField, first_iteration: int = 0, count: int = 1, stream=None):
         N.check(N.lib().nnrt_fitter_iterate(self._h, warp_field.handle, int(first_iteration), int(count), N.stream_ptr(stream)))
+
+    def iterate_timed(self, warp_field: HierarchicalGraphWarpField, first_iteration: int = 0, count: int = 1, stream=None) -> dict:
+        """Eager iterations with HIP events between stages; returns average device ms per iteration per stage."""
+        ms = np.zeros(5, np.float32)
+        N.check(N.lib().nnrt_fitter_iterate_timed(self._h, warp_field.handle, int(first_iteration), int(count), N.ptr(ms), N.stream_ptr(stream)))
+        return dict(warp=float(ms[0]), raster=float(ms[1]), pixels=float(ms[2]), arap=float(ms[3]), solve=float(ms[4]))
 
     def check(self, stream=None):
         N.check(N.lib().nnrt_fitter_check(self._h, N.stream_ptr(stream)))

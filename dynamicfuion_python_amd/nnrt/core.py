@@ -12,7 +12,7 @@ from ._tensors import to_device
 def _axis_angle_vectors_to_matrices_rodrigues(vectors) -> torch.Tensor:
     """AxisAngleVectorsToMatricesRodrigues (cpp/core/linalg/RodriguesImpl.h:66-88); |w| = 0 -> NaN as in the reference (A7)."""
     N.require_gpu()
-    dev = vectors.device if isinstance(vectors, torch.Tensor) and vectors.is_cuda else torch.device("cuda", 0)
+    dev = vectors.device if isinstance(vectors, torch.Tensor) and vectors.is_cuda else torch.device("cuda", N.current_device())
     v = to_device(vectors, torch.float32, dev).reshape(-1, 3)
     out = torch.empty((v.shape[0], 3, 3), dtype=torch.float32, device=dev)
     N.check(N.lib().nnrt_axis_angle_to_matrices_rodrigues(N.ptr(v), v.shape[0], N.ptr(out), N.stream_ptr()))
@@ -22,7 +22,7 @@ def _axis_angle_vectors_to_matrices_rodrigues(vectors) -> torch.Tensor:
 def _solve_block_diagonal_cholesky(blocks, b) -> torch.Tensor:
     """SolveBlockDiagonalCholesky (cpp/core/linalg/SolveBlockDiagonalCholesky.cpp): x_i = A_i^-1 b_i."""
     N.require_gpu()
-    dev = torch.device("cuda", 0)
+    dev = torch.device("cuda", N.current_device())
     A = to_device(blocks, torch.float32, dev)
     n, s = A.shape[0], A.shape[1]
     bb = to_device(b, torch.float32, dev).reshape(-1)
@@ -34,7 +34,7 @@ def _solve_block_diagonal_cholesky(blocks, b) -> torch.Tensor:
 def _solve_block_sparse_arrowhead_cholesky(diagonal_blocks, upper_wing_blocks, upper_wing_block_coordinates, arrow_base_block_index, b):
     """SolveBlockSparseArrowheadCholesky (cpp/core/linalg/SolveBlockSparseArrowheadCholesky.cpp:30-95), uncapped."""
     N.require_gpu()
-    dev = torch.device("cuda", 0)
+    dev = torch.device("cuda", N.current_device())
     D = to_device(diagonal_blocks, torch.float32, dev)
     Wb = to_device(upper_wing_blocks, torch.float32, dev)
     C = to_device(upper_wing_block_coordinates, torch.int32, dev)

@@ -39,7 +39,8 @@ class HierarchicalGraphWarpField:
     def __init__(self, nodes, node_coverage: float = 0.05, threshold_nodes_by_distance: bool = False, anchor_count: int = 4,
                  minimum_valid_anchor_count: int = 0,
                  warp_node_coverage_computation_method=WarpNodeCoverageComputationMethod.MINIMAL_K_NEIGHBOR_NODE_DISTANCE,
-                 layer_count: int = 4, max_vertex_degree: int = 4, layer_decimation_radii=None, device: int = 0):
+                 layer_count: int = 4, max_vertex_degree: int = 4, layer_decimation_radii=None, device: int | None = None):
+        device = N.current_device() if device is None else int(device)
         nodes_np = np.ascontiguousarray(nodes.detach().cpu().numpy() if isinstance(nodes, torch.Tensor) else nodes, dtype=np.float32)
         radii = None if layer_decimation_radii is None else np.ascontiguousarray(layer_decimation_radii, dtype=np.float32)
         h = ctypes.c_void_p()
@@ -95,6 +96,10 @@ class HierarchicalGraphWarpField:
         R = self.get_node_rotations(use_virtual_ordering)
         self.set_node_rotations(np.einsum("nij,njk->nik", R, np.asarray(deltas, np.float32)), use_virtual_ordering)
 
+    def reset_motion(self, stream=None):
+        """R = I, t = 0 for every node (device side, asynchronous on `stream`)."""
+        N.check(N.lib().nnrt_warp_field_reset_motion(self._h, N.stream_ptr(stream)))
+
     def get_virtual_node_indices(self) -> np.ndarray:
         out = np.empty(self.node_count, np.int64)
         N.check(N.lib().nnrt_warp_field_get_virtual_node_indices(self._h, N.ptr(out)))
@@ -138,8 +143,7 @@ def GraphWarpField(nodes, node_coverage=0.05, threshold_nodes_by_distance=False,
 # nnrt.geometry.functional
 # ----------------------------------------------------------------------------------------------------------------
 def _dev():
-    N.require_gpu()
-    return torch.device("cuda", 0)
+    return torch.device("cuda", N.current_device())
 
 
 def _anchors(points, nodes, anchor_count, coverage, node_weights, minimum_valid_anchor_count):

@@ -10,8 +10,7 @@ from ._tensors import to_device, to_host_f64
 
 
 def _dev():
-    N.require_gpu()
-    return torch.device("cuda", 0)
+    return torch.device("cuda", N.current_device())
 
 
 def rasterize_ndc_triangles(ndc_face_vertices, clipped_faces_mask, image_size, blur_radius_pixels=0.0, faces_per_pixel=8, bin_size=-1,

@@ -68,6 +68,8 @@ nnrt_status nnrt_warp_field_get_node_rotations(const nnrt_warp_field* warp_field
 nnrt_status nnrt_warp_field_get_node_translations(const nnrt_warp_field* warp_field, float* h_out, int32_t virtual_order);
 nnrt_status nnrt_warp_field_set_node_rotations(nnrt_warp_field* warp_field, const float* h_in, int32_t virtual_order);
 nnrt_status nnrt_warp_field_set_node_translations(nnrt_warp_field* warp_field, const float* h_in, int32_t virtual_order);
+/* Resets every node to the identity motion (R = I, t = 0; WarpField::ResetRotations, WarpField.cpp:151-156) on `stream`. */
+nnrt_status nnrt_warp_field_reset_motion(nnrt_warp_field* warp_field, void* stream);
 /* node coverage weights (MINIMAL_K_NEIGHBOR_NODE_DISTANCE, WarpField.cpp:249-263), virtual order */
 nnrt_status nnrt_warp_field_get_node_coverage_weights(const nnrt_warp_field* warp_field, float* h_out);
 
@@ -110,6 +112,11 @@ nnrt_status nnrt_fitter_prepare(nnrt_fitter* fitter, nnrt_warp_field* warp_field
                                 const uint8_t* d_mask, int32_t height, int32_t width, const double* h_K, const double* h_E,
                                 float depth_scale, void* stream);
 nnrt_status nnrt_fitter_iterate(nnrt_fitter* fitter, nnrt_warp_field* warp_field, int32_t first_iteration, int32_t count, void* stream);
+/* iterate() without graphs, with HIP events between the stages of every iteration; h_stage_ms[5] receives the average
+ * per-iteration device time of: 0 warp (+warped Jacobians), 1 raster scatter, 2 fused pixel kernel, 3 ARAP edges,
+ * 4 linear solve + update ("ms/solve"). Synchronizes `stream`. */
+nnrt_status nnrt_fitter_iterate_timed(nnrt_fitter* fitter, nnrt_warp_field* warp_field, int32_t first_iteration, int32_t count,
+                                      float* h_stage_ms, void* stream);
 /* Reports (and clears) a failure recorded on the device by earlier iterate() calls (e.g. a non-positive-definite block,
  * which the reference raises from potrf). Synchronizes `stream`. */
 nnrt_status nnrt_fitter_check(nnrt_fitter* fitter, void* stream);

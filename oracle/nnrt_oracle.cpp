@@ -604,6 +604,12 @@ ORC_API int orc_rasterize_k1_fast(const float* face_ndc, const uint8_t* mask, in
 	std::vector<Hit> best(P);
 	for (int64_t i = 0; i < P; i++) { best[i].face = -1; best[i].depth = 0.f; }
 	const float rx = GetNdcRange(W, H), ry = GetNdcRange(H, W);
+	// row bands per thread: every thread scans all faces but only writes its own rows (the winner per pixel is the
+	// strict minimum under HitLess, so the result does not depend on the partition)
+#pragma omp parallel
+	{
+	const int nt = omp_get_num_threads(), tid = omp_get_thread_num();
+	const int band_lo = static_cast<int>(static_cast<int64_t>(H) * tid / nt), band_hi = static_cast<int>(static_cast<int64_t>(H) * (tid + 1) / nt) - 1;
 	for (int64_t f = 0; f < F; f++) {
 		if (mask && !mask[f]) continue;
 		const float* fv = face_ndc + 9 * f;
@@ -617,7 +623,8 @@ ORC_API int orc_rasterize_k1_fast(const float* face_ndc, const uint8_t* mask, in
 		double vlo = std::floor((static_cast<double>(ymin) + ry / 2.0) * H / ry - 0.5) - 1;
 		double vhi = std::ceil((static_cast<double>(ymax) + ry / 2.0) * H / ry - 0.5) + 1;
 		int u0 = static_cast<int>(std::max(0.0, ulo)), u1 = static_cast<int>(std::min<double>(W - 1, uhi));
-		int v0 = static_cast<int>(std::max(0.0, vlo)), v1 = static_cast<int>(std::min<double>(H - 1, vhi));
+		int v0 = static_cast<int>(std::max<double>(band_lo, vlo)), v1 = static_cast<int>(std::min<double>(band_hi, vhi));
+		if (v0 > v1) continue;
 		for (int v = v0; v <= v1; v++) {
 			float py = PixelToNdc(v, H, W);
 			for (int u = u0; u <= u1; u++) {
@@ -628,6 +635,7 @@ ORC_API int orc_rasterize_k1_fast(const float* face_ndc, const uint8_t* mask, in
 				if (b.face == -1 || HitLess(h, b)) b = h;
 			}
 		}
+	}
 	}
 	for (int64_t i = 0; i < P; i++) {
 		if (best[i].face == -1) { out_face[i] = -1; out_depth[i] = -1.f; out_dist[i] = -1.f; out_bary[3 * i] = out_bary[3 * i + 1] = out_bary[3 * i + 2] = -1.f; continue; }

@@ -1,0 +1,109 @@
+"""Shared test helpers (fixture loaders, scene rendering through the CPU oracle)."""
+import os
+import struct
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+FIXTURES = os.path.join(GOLDEN, "reference_fixtures")
+
+
+def rel_err(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    den = np.abs(b).max()
+    return float(np.abs(a - b).max() / (den if den > 0 else 1.0))
+
+
+def subdivide_midpoint(V, F, n):
+    """Open3D TriangleMesh::SubdivideMidpoint face/vertex order (used by the reference's GenerateXyPlane,
+    cpp/tests/test_utils/geometry.cpp:25-64)."""
+    V = [tuple(v) for v in V]
+    F = [tuple(f) for f in F]
+    for _ in range(n):
+        edge = {}
+
+        def mid(a, b):
+            k = (min(a, b), max(a, b))
+            if k not in edge:
+                V.append(tuple((np.array(V[a], np.float64) + np.array(V[b], np.float64)) / 2))
+                edge[k] = len(V) - 1
+            return edge[k]
+
+        NF = []
+        for (a, b, c) in F:
+            ab, bc, ca = mid(a, b), mid(b, c), mid(c, a)
+            NF += [(a, ab, ca), (ab, b, bc), (bc, c, ca), (ab, bc, ca)]
+        F = NF
+    return np.array(V, np.float32), np.array(F, np.int64)
+
+
+def xy_plane(side, center, subdivisions):
+    h = side / 2
+    V = np.array([[-h, -h, 0], [-h, h, 0], [h, -h, 0], [h, h, 0]], np.float32) + np.asarray(center, np.float32)
+    F = np.array([[0, 1, 2], [2, 1, 3]], np.int64)
+    V, F = subdivide_midpoint(V, F, subdivisions)
+    N = np.tile(np.array([[0, 0, -1]], np.float32), (len(V), 1))
+    return V, N, F
+
+
+def read_ply(path):
+    """Binary little-endian PLY (Blender export: x y z nx ny nz s t; faces as uchar count + uint indices). Quads are
+    fan-triangulated (0,1,2),(0,2,3)."""
+    with open(path, "rb") as f:
+        data = f.read()
+    head_end = data.index(b"end_header\n") + len(b"end_header\n")
+    header = data[:head_end].decode().splitlines()
+    nv = int([l for l in header if l.startswith("element vertex")][0].split()[-1])
+    nf = int([l for l in header if l.startswith("element face")][0].split()[-1])
+    props = [l.split()[-1] for l in header if l.startswith("property float")]
+    body = data[head_end:]
+    vert = np.frombuffer(body[: nv * 4 * len(props)], dtype="<f4").reshape(nv, len(props))
+    off = nv * 4 * len(props)
+    faces = []
+    for _ in range(nf):
+        c = body[off]
+        off += 1
+        idx = struct.unpack("<" + "I" * c, body[off: off + 4 * c])
+        off += 4 * c
+        for k in range(1, c - 1):
+            faces.append((idx[0], idx[k], idx[k + 1]))
+    P = vert[:, [props.index("x"), props.index("y"), props.index("z")]].astype(np.float32)
+    N = vert[:, [props.index("nx"), props.index("ny"), props.index("nz")]].astype(np.float32)
+    return P, N, np.array(faces, np.int64)
+
+
+def transform_mesh(P, N, T):
+    T = np.asarray(T, np.float64)
+    P2 = (P.astype(np.float64) @ T[:3, :3].T + T[:3, 3]).astype(np.float32)
+    N2 = (N.astype(np.float64) @ T[:3, :3].T).astype(np.float32)
+    return P2, N2
+
+
+def render_target_oracle(O, points, normals, faces, nodes, R, t, K, H, W, coverage, anchor_count=4, blur=0.5):
+    """Target depth = rasterized depth of the mesh warped by (R, t), -1 -> 0 (test_deformable_mesh_fitter_one_node.cpp:94-101)."""
+    a, w = O.compute_anchors(points, nodes, anchor_count, coverage)
+    wp, wn = O.warp_mesh(points, normals, nodes, R, t, a, w)
+    fndc, fm = O.extract_face_ndc(wp, faces, K, H, W, 0.0, 10.0)
+    fi, dep, bary, dist = O.rasterize_k1_fast(fndc, fm, H, W, blur, True, True)
+    return np.where(dep[..., 0] > 0, dep[..., 0], 0).astype(np.float32)
+
+
+def scene_target(O, sc):
+    return render_target_oracle(O, sc.points, sc.normals, sc.faces, sc.nodes, sc.gt_rotations, sc.gt_translations, sc.K, sc.H, sc.W,
+                                sc.coverage)
+
+
+def oracle_fit_scene(O, sc, depth, iterations=1, lm=0.001, modes=("ALL",), **kw):
+    refp, refm = O.unproject(depth, sc.K, 1.0, 10.0)
+    N = len(sc.nodes)
+    R0 = np.tile(np.eye(3, dtype=np.float32), (N, 1, 1))
+    t0 = np.zeros((N, 3), np.float32)
+    h = sc.hierarchy
+    hk = {}
+    if h:
+        hk = dict(edges=h["edges"], edge_layers=h["edge_layers"], radii=h["radii"], first_layer_count=int(h["layer_counts"][0]))
+    hk.update(kw)
+    return O.fit(nodes=sc.nodes, rotations=R0, translations=t0, mesh_points=sc.points, mesh_normals=sc.normals, faces=sc.faces,
+                 ref_points=refp, ref_mask=refm, H=sc.H, W=sc.W, K=sc.K, max_iterations=iterations, lm_factor=lm, modes=modes,
+                 coverage=sc.coverage, **hk)

@@ -1,0 +1,363 @@
+"""GPU parity tests: every HIP stage and the fused GN iteration against the CPU oracle on the same seeded inputs.
+
+Tolerances: integer/index outputs (anchors, rasterized faces, masks) must be identical; the raster and warp stages are
+bit-identical by construction (same float expression order, -ffp-contract=off, transcendentals rounded once from
+double on both sides). Float reductions (JtJ / Jt r) are summed with atomics in a different order than the oracle, so
+they are compared at <= 1e-5 relative (Hessian) and the solved updates at <= 1e-4 relative (north_star tolerance).
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from _util import FIXTURES, oracle_fit_scene, read_ply, rel_err, scene_target, transform_mesh, xy_plane  # noqa: E402
+from golden import kat_literals as L  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def nn():
+    if not torch.cuda.is_available():
+        pytest.fail("no HIP device visible for a -m gpu test")
+    from dynamicfuion_python_amd import _native
+    _native.lib()
+    from dynamicfuion_python_amd import nnrt
+    return nnrt
+
+
+@pytest.fixture(scope="module")
+def S():
+    from dynamicfuion_python_amd import synthetic
+    return synthetic
+
+
+def _np(t):
+    return t.detach().cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t)
+
+
+def _scene(S, O, name, seed=0):
+    return S.make_scene(name, seed=seed, hierarchy_builder=lambda n, c, l: O.build_hierarchy(n, c, l))
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# stages
+# ---------------------------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["S1", "C1"])
+def test_anchors_bit_exact(nn, S, oracle_mod, name):
+    sc = _scene(S, oracle_mod, name)
+    a_o, w_o = oracle_mod.compute_anchors(sc.points, sc.nodes, 4, sc.coverage)
+    a_g, w_g = nn.geometry.functional.compute_anchors_and_weights_euclidean_fixed_node_weight(sc.points, sc.nodes, 4, 0, sc.coverage)
+    assert np.array_equal(a_o, _np(a_g))
+    assert np.array_equal(w_o, _np(w_g))
+
+
+def test_anchors_variable_coverage_and_threshold(nn, S, oracle_mod):
+    sc = _scene(S, oracle_mod, "S1")
+    cw = oracle_mod.node_coverage_weights(sc.nodes, sc.coverage)
+    a_o, w_o = oracle_mod.compute_anchors(sc.points, sc.nodes, 4, 0.0, node_weights=cw)
+    a_g, w_g = nn.geometry.functional.compute_anchors_and_weights_euclidean_variable_node_weight(sc.points, sc.nodes, cw, 4, 0)
+    assert np.array_equal(a_o, _np(a_g)) and np.array_equal(w_o, _np(w_g))
+    a_o, w_o = oracle_mod.compute_anchors(sc.points, sc.nodes, 4, 0.1, minimum_valid_anchor_count=2)
+    a_g, w_g = nn.geometry.functional.compute_anchors_and_weights_euclidean_fixed_node_weight(sc.points, sc.nodes, 4, 2, 0.1)
+    assert np.array_equal(a_o, _np(a_g)) and np.array_equal(w_o, _np(w_g))
+
+
+@pytest.mark.parametrize("extrinsic", [False, True])
+def test_warp_bit_exact(nn, S, oracle_mod, extrinsic):
+    sc = _scene(S, oracle_mod, "C1")
+    a, w = oracle_mod.compute_anchors(sc.points, sc.nodes, 4, sc.coverage)
+    E = None
+    if extrinsic:
+        E = np.eye(4)
+        E[:3, :3] = S.rodrigues_np(np.array([[0.01, -0.02, 0.03]], np.float32))[0]
+        E[:3, 3] = [0.01, -0.005, 0.02]
+    wp_o, wn_o = oracle_mod.warp_mesh(sc.points, sc.normals, sc.nodes, sc.gt_rotations, sc.gt_translations, a, w, E)
+    m = nn.geometry.functional.warp_triangle_mesh(nn.geometry.TriangleMesh(sc.points, sc.normals, sc.faces), sc.nodes, sc.gt_rotations,
+                                                  sc.gt_translations, a, w, E)
+    assert np.array_equal(wp_o, _np(m.vertex_positions))
+    assert np.array_equal(wn_o, _np(m.vertex_normals))
+
+
+def test_ndc_extraction_bit_exact_and_fixture(nn, S, oracle_mod):
+    V, N, F = xy_plane(1.2615, (0, 0, 1), 4)
+    K = np.array([[580., 0., 320.], [0., 580., 240.], [0., 0., 1.]])
+    ndc_g, m_g = nn.rendering.functional.get_mesh_ndc_face_vertices_and_clip_mask(nn.geometry.TriangleMesh(V, N, F), K, (480, 640), 0.0, 2.0)
+    gt = np.load(os.path.join(FIXTURES, "extracted_face_vertices.npy"))
+    gm = np.load(os.path.join(FIXTURES, "extracted_face_mask.npy"))
+    assert np.array_equal(_np(m_g), gm)
+    assert np.allclose(_np(ndc_g)[gm], gt[gm], atol=1e-5)
+    sc = _scene(S, oracle_mod, "C1")
+    ndc_o, m_o = oracle_mod.extract_face_ndc(sc.points, sc.faces, sc.K, sc.H, sc.W, 0.0, 10.0)
+    ndc_g, m_g = nn.rendering.functional.get_mesh_ndc_face_vertices_and_clip_mask(nn.geometry.TriangleMesh(sc.points, sc.normals, sc.faces),
+                                                                                   sc.K, (sc.H, sc.W), 0.0, 10.0)
+    assert np.array_equal(m_o, _np(m_g)) and np.array_equal(ndc_o, _np(ndc_g))
+
+
+def _warped_face_ndc(oracle_mod, sc):
+    a, w = oracle_mod.compute_anchors(sc.points, sc.nodes, 4, sc.coverage)
+    wp, wn = oracle_mod.warp_mesh(sc.points, sc.normals, sc.nodes, sc.gt_rotations, sc.gt_translations, a, w)
+    fndc, fm = oracle_mod.extract_face_ndc(wp, sc.faces, sc.K, sc.H, sc.W, 0.0, 10.0)
+    return wp, wn, fndc, fm
+
+
+@pytest.mark.parametrize("name,blur,persp,clip", [("S1", 0.5, True, False), ("S1", 0.0, False, False), ("S1", 0.5, True, True),
+                                                  ("C1", 0.5, True, False)])
+def test_rasterize_k1_bit_exact(nn, S, oracle_mod, name, blur, persp, clip):
+    sc = _scene(S, oracle_mod, name)
+    _, _, fndc, fm = _warped_face_ndc(oracle_mod, sc)
+    ref = oracle_mod.rasterize(fndc, fm, sc.H, sc.W, blur, 1, -1, -1, persp, clip, True)
+    got = nn.rendering.rasterize_ndc_triangles(fndc, fm, (sc.H, sc.W), blur, 1, -1, -1, persp, clip, True)
+    for r, g in zip(ref, got):
+        assert np.array_equal(r, _np(g))
+
+
+@pytest.mark.parametrize("k", [2, 4, 8])
+def test_rasterize_multi_face_bit_exact(nn, S, oracle_mod, k):
+    sc = _scene(S, oracle_mod, "S1")
+    _, _, fndc, fm = _warped_face_ndc(oracle_mod, sc)
+    ref = oracle_mod.rasterize(fndc, fm, sc.H, sc.W, 0.5, k, -1, -1, True, False, True)
+    got = nn.rendering.rasterize_ndc_triangles(fndc, fm, (sc.H, sc.W), 0.5, k, -1, -1, True, False, True)
+    for r, g in zip(ref, got):
+        assert np.array_equal(r, _np(g))
+
+
+def test_rasterize_edge_cases(nn, oracle_mod):
+    H = W = 32
+    # empty face set, all faces clipped, degenerate (zero-area) and back-facing triangles
+    empty = np.zeros((0, 3, 3), np.float32)
+    fi, dep, _, _ = nn.rendering.rasterize_ndc_triangles(empty, None, (H, W), 0.5, 1, -1, -1, True, False, True)
+    assert (_np(fi) == -1).all() and (_np(dep) == -1).all()
+    tri = np.array([[[-0.5, -0.5, 1.0], [-0.5, 0.5, 1.0], [0.5, -0.5, 1.0]],     # front
+                    [[0.5, -0.5, 1.0], [-0.5, 0.5, 1.0], [-0.5, -0.5, 1.0]],     # back-facing
+                    [[0.0, 0.0, 1.0], [0.0, 0.0, 1.0], [0.1, 0.1, 1.0]]], np.float32)  # degenerate
+    mask = np.array([1, 1, 1], np.uint8)
+    for cull in (True, False):
+        ref = oracle_mod.rasterize(tri, mask, H, W, 0.5, 1, -1, -1, True, False, cull)
+        got = nn.rendering.rasterize_ndc_triangles(tri, mask, (H, W), 0.5, 1, -1, -1, True, False, cull)
+        for r, g in zip(ref, got):
+            assert np.array_equal(r, _np(g))
+    ref = oracle_mod.rasterize(tri, np.zeros(3, np.uint8), H, W, 0.5, 1, -1, -1, True, False, True)
+    assert (ref[0] == -1).all()
+    got = nn.rendering.rasterize_ndc_triangles(tri, np.zeros(3, np.uint8), (H, W), 0.5, 1, -1, -1, True, False, True)
+    assert (_np(got[0]) == -1).all()
+    with pytest.raises(RuntimeError):
+        nn.rendering.rasterize_ndc_triangles(tri, mask, (H, W), 0.5, 9, -1, -1, True, False, True)
+
+
+def test_interpolate_and_unproject(nn, S, oracle_mod):
+    sc = _scene(S, oracle_mod, "S1")
+    wp, wn, fndc, fm = _warped_face_ndc(oracle_mod, sc)
+    fi, dep, bary, _ = oracle_mod.rasterize(fndc, fm, sc.H, sc.W, 0.5, 1, -1, -1, True, False, True)
+    attrs = wn[sc.faces]
+    r = oracle_mod.interpolate_face_attributes(fi, bary, attrs)
+    g = nn.rendering.functional.interpolate_vertex_attributes(fi, bary, attrs)
+    assert np.array_equal(r, _np(g))
+    depth = np.where(dep[..., 0] > 0, dep[..., 0], 0).astype(np.float32) * 1000.0
+    p_o, m_o = oracle_mod.unproject(depth, sc.K, 1000.0, 10.0)
+    p_g, m_g = nn.geometry.functional.unproject_raster_depth_without_filtering(depth, sc.K, 1000.0, 10.0)
+    assert np.array_equal(p_o, _np(p_g)) and np.array_equal(m_o, _np(m_g))
+
+
+def test_rodrigues_and_block_cholesky_kats(nn, oracle_mod):
+    R = nn.core.linalg.AxisAngleVectorsToMatricesRodrigues(L.RODRIGUES_AXIS_ANGLE)
+    assert np.allclose(_np(R), L.RODRIGUES_EXPECTED, rtol=1e-3, atol=1e-7)
+    assert np.array_equal(_np(R), oracle_mod.rodrigues(L.RODRIGUES_AXIS_ANGLE))
+    for col in range(2):
+        x = nn.core.linalg.SolveBlockDiagonalCholesky(L.CHOLESKY_A, L.CHOLESKY_B[:, col])
+        assert np.allclose(_np(x), L.CHOLESKY_X[:, col], atol=2e-5, rtol=1e-4)
+    with pytest.raises(RuntimeError):
+        nn.core.linalg.SolveBlockDiagonalCholesky(-L.CHOLESKY_A, L.CHOLESKY_B[:, 0])
+
+
+@pytest.mark.parametrize("n0,n1,degree", [(40, 6, 4), (300, 30, 4), (1, 1, 1)])
+def test_arrowhead_solver_vs_oracle(nn, oracle_mod, n0, n1, degree):
+    rng = np.random.default_rng(n0)
+    N = n0 + n1
+    edges = []
+    for i in range(n0):
+        for j in rng.choice(n1, size=min(degree, n1), replace=False):
+            edges.append((i, n0 + int(j)))
+    edges = np.array(edges, np.int32)
+    wing = rng.normal(0, 0.3, (len(edges), 6, 6)).astype(np.float32)
+    diag = np.empty((N, 6, 6), np.float32)
+    for i in range(N):
+        A = rng.normal(size=(6, 6))
+        diag[i] = (A @ A.T + 6 * np.eye(6) * (1 + degree)).astype(np.float32)
+    for e, (i, j) in enumerate(edges):   # keep the full matrix diagonally dominant (SPD)
+        diag[j] += np.eye(6, dtype=np.float32) * 6 * degree
+    b = rng.normal(size=6 * N).astype(np.float32)
+    x_o = oracle_mod.solve_arrowhead(diag, wing, edges, n0, b)
+    x_g = _np(nn.core.linalg.SolveBlockSparseArrowheadCholesky(diag, wing, edges, n0, b))
+    assert rel_err(x_g, x_o) < 1e-4
+    # residual check against the assembled dense matrix (float64)
+    Hd = np.zeros((6 * N, 6 * N))
+    for i in range(N):
+        Hd[6 * i:6 * i + 6, 6 * i:6 * i + 6] = diag[i]
+    for e, (i, j) in enumerate(edges):
+        Hd[6 * i:6 * i + 6, 6 * j:6 * j + 6] = wing[e]
+        Hd[6 * j:6 * j + 6, 6 * i:6 * i + 6] = wing[e].T
+    assert np.abs(Hd @ x_g - b).max() < 1e-3 * np.abs(b).max()
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# fused GN iteration
+# ---------------------------------------------------------------------------------------------------------------------
+def _gpu_fit(nn, sc, depth, iterations=1, lm=0.001, modes=None, tukey=False, coverage_method=0, graph=True, extrinsics=None, **fkw):
+    G, A = nn.geometry, nn.alignment
+    modes = modes or [A.IterationMode.ALL]
+    wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod(coverage_method),
+                                      sc.layer_count)
+    ft = A.DeformableMeshToImageFitter(iterations, modes, preconditioning_dampening_factor=lm, use_tukey_penalty_for_data_term=tukey,
+                                       use_hip_graph=graph, **fkw)
+    ft.fit_to_image(wf, G.TriangleMesh(sc.points, sc.normals, sc.faces), None, depth, None, sc.K, extrinsics, 1.0)
+    return wf, ft, ft.diagnostics()
+
+
+def _compare_iteration(dg_o, dg_g, s, N):
+    assert np.array_equal(dg_o["pixel_faces"].astype(np.int64), dg_g["pixel_faces"].astype(np.int64))
+    assert np.array_equal(dg_o["residual_mask"], dg_g["residual_mask"])
+    assert np.allclose(dg_o["residuals"], dg_g["residuals"], rtol=0, atol=1e-6)
+    assert rel_err(dg_g["hessian"][: N * s * s], dg_o["hessian_diag"]) < 1e-5
+    assert rel_err(dg_g["gradient"][: N * s], dg_o["gradient"]) < 1e-4
+    assert rel_err(dg_g["updates"][: N * s], dg_o["updates"]) < 1e-4
+
+
+@pytest.mark.parametrize("name", ["S1", "C1", "C2"])
+def test_fit_one_iteration_parity(nn, S, oracle_mod, name):
+    sc = _scene(S, oracle_mod, name)
+    depth = scene_target(oracle_mod, sc)
+    R_o, t_o, dg_o = oracle_fit_scene(oracle_mod, sc, depth, 1)
+    wf, ft, dg_g = _gpu_fit(nn, sc, depth, 1)
+    _compare_iteration(dg_o, dg_g, 6, len(sc.nodes))
+    assert rel_err(wf.get_node_translations(True), t_o) < 1e-4
+    assert rel_err(wf.get_node_rotations(True) - np.eye(3), R_o - np.eye(3)) < 1e-4
+
+
+@pytest.mark.parametrize("mode", ["TRANSLATION_ONLY", "ROTATION_ONLY"])
+def test_fit_single_mode_parity(nn, S, oracle_mod, mode):
+    sc = _scene(S, oracle_mod, "S1")
+    depth = scene_target(oracle_mod, sc)
+    _, _, dg_o = oracle_fit_scene(oracle_mod, sc, depth, 1, modes=(mode,))
+    _, _, dg_g = _gpu_fit(nn, sc, depth, 1, modes=[nn.alignment.IterationMode[mode]])
+    _compare_iteration(dg_o, dg_g, 3, len(sc.nodes))
+
+
+def test_fit_tukey_and_variable_coverage_parity(nn, S, oracle_mod):
+    sc = _scene(S, oracle_mod, "S1")
+    depth = scene_target(oracle_mod, sc)
+    _, _, dg_o = oracle_fit_scene(oracle_mod, sc, depth, 1, use_tukey=True, tukey_cutoff=0.01)
+    _, _, dg_g = _gpu_fit(nn, sc, depth, 1, tukey=True, tukey_penalty_cutoff_cm=0.01)
+    _compare_iteration(dg_o, dg_g, 6, len(sc.nodes))
+    cw = oracle_mod.node_coverage_weights(sc.nodes, sc.coverage)
+    _, _, dg_o = oracle_fit_scene(oracle_mod, sc, depth, 1, coverage_method=1, node_weights=cw)
+    _, _, dg_g = _gpu_fit(nn, sc, depth, 1, coverage_method=1)
+    _compare_iteration(dg_o, dg_g, 6, len(sc.nodes))
+
+
+def test_fit_multi_iteration_parity(nn, S, oracle_mod):
+    sc = _scene(S, oracle_mod, "S1")
+    depth = scene_target(oracle_mod, sc)
+    R_o, t_o, _ = oracle_fit_scene(oracle_mod, sc, depth, 3)
+    wf, _, _ = _gpu_fit(nn, sc, depth, 3)
+    # the GN map is sensitive (block-diagonal Jacobi steps, A17): reduction-order differences grow per iteration
+    assert rel_err(wf.get_node_translations(True), t_o) < 1e-3
+    assert rel_err(wf.get_node_rotations(True) - np.eye(3), R_o - np.eye(3)) < 1e-3
+
+
+@pytest.mark.parametrize("name", ["S1_ARAP", "C1_ARAP"])
+def test_fit_arap_parity(nn, S, oracle_mod, name):
+    sc = _scene(S, oracle_mod, name)
+    wf = nn.geometry.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, nn.geometry.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE,
+                                                sc.layer_count)
+    assert np.array_equal(wf.get_virtual_node_indices(), np.arange(len(sc.nodes)))
+    assert np.array_equal(wf.get_edges(), sc.hierarchy["edges"])
+    depth = scene_target(oracle_mod, sc)
+    R_o, t_o, dg_o = oracle_fit_scene(oracle_mod, sc, depth, 1)
+    wf, _, dg_g = _gpu_fit(nn, sc, depth, 1)
+    _compare_iteration(dg_o, dg_g, 6, len(sc.nodes))
+    assert rel_err(wf.get_node_translations(True), t_o) < 1e-4
+
+
+def test_hip_graph_matches_eager(nn, S, oracle_mod):
+    sc = _scene(S, oracle_mod, "S1")
+    depth = scene_target(oracle_mod, sc)
+    wf1, _, d1 = _gpu_fit(nn, sc, depth, 2, graph=True)
+    wf2, _, d2 = _gpu_fit(nn, sc, depth, 2, graph=False)
+    assert np.array_equal(d1["pixel_faces"], d2["pixel_faces"])
+    assert rel_err(wf1.get_node_translations(), wf2.get_node_translations()) < 1e-4
+
+
+def test_fit_with_extrinsics_parity(nn, S, oracle_mod):
+    sc = _scene(S, oracle_mod, "S1")
+    depth = scene_target(oracle_mod, sc)
+    E = np.eye(4)
+    E[:3, 3] = [0.002, -0.001, 0.003]
+    _, _, dg_o = oracle_fit_scene(oracle_mod, sc, depth, 1, extrinsics=E)
+    _, _, dg_g = _gpu_fit(nn, sc, depth, 1, extrinsics=E)
+    _compare_iteration(dg_o, dg_g, 6, len(sc.nodes))
+
+
+def test_25_node_plane_fixture_parity(nn, oracle_mod):
+    # cpp/tests/test_deformable_mesh_fitter_advanced.cpp:55-143 scene (parity of the first iteration GPU vs oracle)
+    T = np.array([[-1, 0, 0, 0], [0, 1, 0, 0], [0, 0, -1, 1.2], [0, 0, 0, 1.]])
+    Ps, Ns, Fs = read_ply(os.path.join(FIXTURES, "plane_skin_25_nodes_source.ply"))
+    Pt, Nt, Ft = read_ply(os.path.join(FIXTURES, "plane_skin_25_nodes_target.ply"))
+    Ps, Ns = transform_mesh(Ps, Ns, T)
+    Pt, Nt = transform_mesh(Pt, Nt, T)
+    nodes = np.load(os.path.join(FIXTURES, "nodes_25-node_plane.npy")).astype(np.float32)
+    nodes = (nodes.astype(np.float64) @ T[:3, :3].T + T[:3, 3]).astype(np.float32)
+    K = np.array([[100.0, 0, 50], [0, 100.0, 50], [0, 0, 1]])
+    fndc, fm = oracle_mod.extract_face_ndc(Pt, Ft, K, 100, 100, 0.0, 10.0)
+    fi, dep, _, _ = oracle_mod.rasterize(fndc, fm, 100, 100, 0.0, 1, -1, -1, True, False, True)
+    fi_g, dep_g, _, _ = nn.rendering.rasterize_ndc_triangles(fndc, fm, (100, 100), 0.0, 1, -1, -1, True, False, True)
+    assert np.array_equal(fi, _np(fi_g)) and np.array_equal(dep, _np(dep_g))
+    depth = np.where(dep[..., 0] > 0, dep[..., 0], 0).astype(np.float32)
+    refp, refm = oracle_mod.unproject(depth, K, 1.0, 10.0)
+    weights = oracle_mod.node_coverage_weights(nodes, 0.1)
+    I = np.tile(np.eye(3, dtype=np.float32), (25, 1, 1))
+    R_o, t_o, dg_o = oracle_mod.fit(nodes=nodes, rotations=I, translations=np.zeros((25, 3), np.float32), mesh_points=Ps, mesh_normals=Ns,
+                                    faces=Fs, ref_points=refp, ref_mask=refm, H=100, W=100, K=K, max_iterations=1, lm_factor=0.001,
+                                    coverage=0.1, coverage_method=1, node_weights=weights)
+    G, A = nn.geometry, nn.alignment
+    wf = G.HierarchicalGraphWarpField(nodes, 0.1, False, 4, 0, G.WarpNodeCoverageComputationMethod.MINIMAL_K_NEIGHBOR_NODE_DISTANCE, 1)
+    assert np.array_equal(wf.get_node_coverage_weights(), weights)
+    ft = A.DeformableMeshToImageFitter(1, [A.IterationMode.ALL], 1e-6, True, 10.0, False, 0.01, 0.001)
+    ft.fit_to_image(wf, G.TriangleMesh(Ps, Ns, Fs), None, depth, depth > 0, K, np.eye(4), 1.0)
+    _compare_iteration(dg_o, ft.diagnostics(), 6, 25)
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# full-size properties and error behaviour
+# ---------------------------------------------------------------------------------------------------------------------
+def test_c3_raster_parity_and_iteration_properties(nn, S, oracle_mod):
+    sc = _scene(S, oracle_mod, "C3")
+    _, _, fndc, fm = _warped_face_ndc(oracle_mod, sc)
+    ref = oracle_mod.rasterize_k1_fast(fndc, fm, sc.H, sc.W, 0.5, True, True)
+    got = nn.rendering.rasterize_ndc_triangles(fndc, fm, (sc.H, sc.W), 0.5, 1, -1, -1, True, False, True)
+    for r, g in zip(ref, got):
+        assert np.array_equal(r, _np(g))
+    depth = np.where(ref[1][..., 0] > 0, ref[1][..., 0], 0).astype(np.float32)
+    wf, ft, dg = _gpu_fit(nn, sc, depth, 1)
+    N = len(sc.nodes)
+    Hb = dg["hessian"].reshape(N, 6, 6)
+    assert np.allclose(Hb, Hb.transpose(0, 2, 1))
+    assert (np.linalg.eigvalsh(Hb.astype(np.float64)) > -1e-3 * np.abs(Hb).max()).all()
+    assert np.array_equal(dg["residual_mask"], (dg["pixel_faces"] >= 0) & (depth.reshape(-1) > 0))
+    assert np.isfinite(dg["updates"]).all()
+
+
+def test_errors_fail_loudly(nn, S, oracle_mod):
+    A, G = nn.alignment, nn.geometry
+    with pytest.raises(RuntimeError):
+        A.DeformableMeshToImageFitter(1, [A.IterationMode.ALL], preconditioning_dampening_factor=2.0)
+    with pytest.raises(RuntimeError):
+        G.HierarchicalGraphWarpField(np.zeros((2, 3), np.float32), 0.1, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE, 1)
+    # a node far from the mesh gets no pixels: with LM = 0 its 6x6 block is zero -> potrf failure (reference raises)
+    sc = _scene(S, oracle_mod, "S1")
+    depth = scene_target(oracle_mod, sc)
+    sc.nodes = np.concatenate([sc.nodes, np.array([[5.0, 5.0, 5.0]], np.float32)])
+    with pytest.raises(RuntimeError, match="positive-definite"):
+        _gpu_fit(nn, sc, depth, 1, lm=0.0)

@@ -1,0 +1,112 @@
+"""CPU checks of the drop-in boundary: the HIP library loads without a GPU, exports every function that
+include/nnrt_mi355x.h declares, the Python binding table matches the header, and the host-side argument checks fail
+loudly (no compute is launched here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "nnrt_mi355x.h")
+
+
+def _declared():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(nnrt_[a-z0-9_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def native():
+    from dynamicfuion_python_amd import _native
+    if not os.path.exists(_native.LIB_PATH):
+        _native.build()
+    return _native
+
+
+def test_header_declares_entry_points():
+    names = _declared()
+    assert len(names) >= 30
+    for must in ("nnrt_fitter_fit_to_image", "nnrt_fitter_prepare", "nnrt_fitter_iterate", "nnrt_warp_field_create",
+                 "nnrt_rasterize_ndc_triangles", "nnrt_solve_block_sparse_arrowhead_cholesky"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(native):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", native.LIB_PATH], text=True)
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    missing = [n for n in _declared() if n not in exported]
+    assert not missing, f"declared in include/nnrt_mi355x.h but not exported: {missing}"
+    # every exported nnrt_ symbol is declared (no undocumented ABI)
+    extra = sorted(n for n in exported if n.startswith("nnrt_") and n not in _declared())
+    assert not extra, f"exported but not declared: {extra}"
+
+
+def test_binding_table_matches_header(native):
+    assert sorted(native.exported_symbols()) == _declared()
+
+
+def test_library_loads_without_gpu(native):
+    lib = native.lib()   # dlopen + binds every signature; must not need a device
+    for name in _declared():
+        assert getattr(lib, name) is not None
+    assert lib.nnrt_runtime_version() > 0
+
+
+def test_default_params_mirror_reference_constructor(native):
+    p = native.FitterParams()
+    native.lib().nnrt_fitter_default_params(ctypes.byref(p))
+    # DeformableMeshToImageFitter.h:34-46 defaults
+    assert p.max_iteration_count == 100
+    assert p.iteration_mode_count == 1 and p.iteration_modes[0] == 0
+    assert p.minimal_update_threshold == pytest.approx(1e-6)
+    assert p.use_perspective_correction == 1
+    assert p.max_depth == pytest.approx(10.0)
+    assert p.use_tukey_penalty_for_data_term == 0
+    assert p.tukey_penalty_cutoff_cm == pytest.approx(0.01)
+    assert p.preconditioning_dampening_factor == 0.0
+    assert p.arap_term_weight == pytest.approx(200.0)
+    assert p.use_huber_penalty_for_arap_term == 0
+    assert p.huber_penalty_constant == pytest.approx(1e-4)
+    assert p.use_hip_graph == 1
+
+
+def test_struct_layout_matches_header(native):
+    # 12 scalars + 16-int mode array, all 4-byte fields
+    assert ctypes.sizeof(native.FitterParams) == 4 * (12 + 16)
+
+
+def test_argument_errors_are_reported(native):
+    lib = native.lib()
+    out = ctypes.c_void_p()
+    nodes = np.zeros((2, 3), np.float32)
+    # anchor_count > node_count -> error (WarpField.cpp:57-61), before any device work
+    st = lib.nnrt_warp_field_create(native.ptr(nodes), 2, 0.05, 0, 4, 0, 1, 1, 4, None, 0, ctypes.byref(out))
+    assert st == 1
+    assert b"Anchor count" in lib.nnrt_last_error()
+    st = lib.nnrt_warp_field_create(None, 2, 0.05, 0, 4, 0, 1, 1, 4, None, 0, ctypes.byref(out))
+    assert st == 1
+    p = native.FitterParams()
+    lib.nnrt_fitter_default_params(ctypes.byref(p))
+    p.preconditioning_dampening_factor = 2.0   # must be in [0, 1] (DeformableMeshToImageFitter.cpp:79-82)
+    st = lib.nnrt_fitter_create(ctypes.byref(p), 0, ctypes.byref(out))
+    assert st == 1
+    with pytest.raises(native.NnrtError):
+        native.check(st)
+
+
+def test_no_cpu_fallback(native, monkeypatch):
+    import torch
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: False)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        native.require_gpu()
+
+
+def test_missing_library_fails_loudly(native, monkeypatch, tmp_path):
+    monkeypatch.setattr(native, "_lib", None)
+    monkeypatch.setattr(native, "LIB_PATH", str(tmp_path / "absent.so"))
+    with pytest.raises(RuntimeError, match="missing"):
+        native.lib()
