@@ -106,17 +106,17 @@ nnrt_status launch_arap_edges(const ArapArgs& args, hipStream_t stream) {
 }
 
 // ---- acc (data) + arap_acc -> full diagonal blocks (+LM) and rhs = negative gradient ----
-__global__ void k_arrow_prepare(int N, float lm, float* __restrict__ acc, float* __restrict__ arap_acc, float* __restrict__ diag,
+__global__ void k_arrow_prepare(int N, float lm, double* __restrict__ acc, float* __restrict__ arap_acc, float* __restrict__ diag,
                                 float* __restrict__ rhs, float* __restrict__ gradient_out, float* __restrict__ hessian_out) {
 	const int n = blockIdx.x * blockDim.x + threadIdx.x;
 	if (n >= N) return;
-	float* ad = acc + static_cast<int64_t>(n) * ACC_STRIDE;
+	double* ad = acc + static_cast<int64_t>(n) * ACC_STRIDE;
 	float* aa = arap_acc + static_cast<int64_t>(n) * ACC_STRIDE;
 	float* d = diag + static_cast<int64_t>(n) * 36;
 	int q = 0;
 	for (int r = 0; r < 6; r++)
 		for (int c = r; c < 6; c++) {
-			const float hd = ad[q];
+			const float hd = static_cast<float>(ad[q]);
 			const float v = aa[q] + hd;
 			if (hessian_out) {
 				hessian_out[static_cast<int64_t>(n) * 36 + 6 * r + c] = hd;
@@ -129,12 +129,12 @@ __global__ void k_arrow_prepare(int N, float lm, float* __restrict__ acc, float*
 	if (lm > 0.f)
 		for (int i = 0; i < 6; i++) d[7 * i] += lm;
 	for (int c = 0; c < 6; c++) {
-		const float g = (0.f - ad[21 + c]) - aa[21 + c];
+		const float g = (0.f - static_cast<float>(ad[21 + c])) - aa[21 + c];
 		rhs[6 * n + c] = g;
 		gradient_out[6 * n + c] = g;
 	}
 	for (int k = 0; k < 27; k++) {
-		ad[k] = 0.f;
+		ad[k] = 0.0;
 		aa[k] = 0.f;
 	}
 }
@@ -422,10 +422,10 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 	return NNRT_OK;
 }
 
-nnrt_status launch_arrowhead_iteration(const ArrowheadWorkspace& ws, const float* acc, float lm, const int32_t* edges, const float* wing,
+nnrt_status launch_arrowhead_iteration(const ArrowheadWorkspace& ws, const double* acc, float lm, const int32_t* edges, const float* wing,
                                        float* node_state, float* arap_acc, float* updates_out, float* gradient_out, float* hessian_out,
                                        int* error_flag, hipStream_t stream) {
-	k_arrow_prepare<<<static_cast<unsigned>(ceil_div(ws.N, 256)), 256, 0, stream>>>(ws.N, lm, const_cast<float*>(acc), arap_acc, ws.diag,
+	k_arrow_prepare<<<static_cast<unsigned>(ceil_div(ws.N, 256)), 256, 0, stream>>>(ws.N, lm, const_cast<double*>(acc), arap_acc, ws.diag,
 	                                                                               ws.rhs, gradient_out, hessian_out);
 	NNRT_LAUNCH_CHECK();
 	nnrt_status st = arrowhead_solve_core(ws, edges, wing, error_flag, stream);

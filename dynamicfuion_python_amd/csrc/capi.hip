@@ -336,7 +336,8 @@ struct nnrt_fitter {
 	DeviceBuffer<float> residuals;
 	DeviceBuffer<uint8_t> residual_mask;
 	DeviceBuffer<int32_t> pixel_face;
-	DeviceBuffer<float> acc, arap_acc;
+	DeviceBuffer<double> acc;       // [N, ACC_STRIDE] data term (fp64)
+	DeviceBuffer<float> arap_acc;
 	DeviceBuffer<float> updates, gradient, hessian;
 	DeviceBuffer<int> error_flag;
 	// ARAP / arrowhead
@@ -506,7 +507,8 @@ void nnrt_fitter_destroy(nnrt_fitter* ft) {
 	DeviceGuard guard(ft->device);
 	hipStreamSynchronize(ft->work);
 	ft->drop_graphs();
-	for (auto* b : {&ft->mesh_p, &ft->mesh_n, &ft->weights, &ft->ref_depth, &ft->residuals, &ft->acc, &ft->arap_acc, &ft->updates, &ft->gradient,
+	ft->acc.release();
+	for (auto* b : {&ft->mesh_p, &ft->mesh_n, &ft->weights, &ft->ref_depth, &ft->residuals, &ft->arap_acc, &ft->updates, &ft->gradient,
 	                &ft->hessian, &ft->wing, &ft->edge_residuals, &ft->a_diag, &ft->a_dinv, &ft->a_dinvb, &ft->a_schur, &ft->a_rhs, &ft->a_x})
 		b->release();
 	ft->faces4.release();
@@ -627,7 +629,7 @@ nnrt_status nnrt_fitter_prepare(nnrt_fitter* ft, nnrt_warp_field* wf, const floa
 	                                                                            ft->ref_depth.ptr);
 	NNRT_LAUNCH_CHECK();
 	NNRT_HIP(hipMemsetAsync(ft->keys.ptr, 0xff, sizeof(uint64_t) * P, s));
-	NNRT_HIP(hipMemsetAsync(ft->acc.ptr, 0, sizeof(float) * N * ACC_STRIDE, s));
+	NNRT_HIP(hipMemsetAsync(ft->acc.ptr, 0, sizeof(double) * N * ACC_STRIDE, s));
 	NNRT_HIP(hipMemsetAsync(ft->arap_acc.ptr, 0, sizeof(float) * N * ACC_STRIDE, s));
 	NNRT_HIP(hipEventRecord(ft->ev_out, s));
 	NNRT_HIP(hipStreamWaitEvent(us, ft->ev_out, 0));

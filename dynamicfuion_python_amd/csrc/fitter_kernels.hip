@@ -4,16 +4,19 @@
 // (ComputeDepthResiduals :331-390), rasterized-surface Jacobians (RasterizedSurfaceJacobiansImpl.h:114-200),
 // pixel->node Jacobians (PixelVertexAnchorJacobiansImpl.h:179-363) and the block-diagonal data JtJ / Jt r reduction
 // (DeformableMeshToImageFitterImpl.h:199-456). The reference materialises [P,12,6] pixel Jacobians, [P,3,19] rasterized
-// Jacobians and [N,4000] node lists (capped: A4) and reduces each node serially; here each 16x16-pixel workgroup reduces
-// its pixels' per-node contributions (21 JtJ entries + 6 Jt r) in an LDS hash table and flushes them to HBM with one
-// float atomic per (node, entry) -- no intermediate tensors, no cap.
+// Jacobians and [N,4000] node lists (capped: A4) and reduces each node serially. Here every 64-lane wavefront owns an
+// 8x8 pixel block; it walks the distinct nodes its pixels touch (wave-uniform loop driven by a ballot), each lane builds
+// its pixel's 6-dof Jacobian for that node, and the 27 products (21 JtJ upper-triangle entries + 6 J r) are summed over
+// the wave with a transposing butterfly (32 values -> one per lane in 6 exchange steps) and added to the node's fp64
+// accumulator row with one atomic per entry. Products are rounded to float exactly as the reference forms them and
+// summed in double, so the data term equals the exactly-summed reference data term (see DESIGN.md "Numerics") -- no
+// intermediate tensors, no node-list cap, no LDS.
 #include "fitter_kernels.hpp"
 
 namespace nnrt {
 
 constexpr int PIX_TILE = 16;
 constexpr int PIX_BLOCK = PIX_TILE * PIX_TILE;
-constexpr int LDS_SLOTS = 128;
 
 template <int MODE>
 struct ModeTraits;
@@ -30,29 +33,35 @@ struct ModeTraits<NNRT_ITERATION_ROTATION_ONLY> {
 	static constexpr int S = 3, NH = 6, NACC = 9;
 };
 
-__device__ inline int lds_find_slot(int* keys, int node) {
-	const unsigned h = (static_cast<unsigned>(node) * 2654435761u) >> (32 - 7);
-	for (int probe = 0; probe < LDS_SLOTS; probe++) {
-		const int s = (h + probe) & (LDS_SLOTS - 1);
-		const int k = __hip_atomic_load(keys + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-		if (k == node) return s;
-		if (k == -1) {
-			const int prev = atomicCAS(keys + s, -1, node);
-			if (prev == -1 || prev == node) return s;
+// Sum 32 per-lane values over the 64-lane wavefront. Each exchange step halves the values a lane holds: lanes with the
+// step's bit set keep the upper half and send the lower half to their partner (and vice versa), so 32 + 1 shuffles
+// replace 32 x 6. On return lane l (and l + 32) holds the wave total of value index transpose_index(l).
+__device__ inline int transpose_index(int lane) {
+	return ((lane & 1) << 4) | ((lane & 2) << 2) | (lane & 4) | ((lane & 8) >> 2) | ((lane & 16) >> 4);
+}
+
+__device__ inline double wave_transpose_reduce32(double (&v)[32], int lane) {
+#pragma unroll
+	for (int step = 0; step < 5; step++) {
+		const int d = 1 << step;
+		const int half = 16 >> step;
+		const bool upper = (lane & d) != 0;
+#pragma unroll
+		for (int j = 0; j < half; j++) {
+			const double lo = v[j], hi = v[j + half];
+			const double send = upper ? lo : hi;
+			const double keep = upper ? hi : lo;
+			v[j] = keep + __shfl_xor(send, d);
 		}
 	}
-	return -1;
+	return v[0] + __shfl_xor(v[0], 32);
 }
 
 template <int MODE>
 __global__ __launch_bounds__(PIX_BLOCK) void k_fit_pixels(FitPixelArgs a) {
 	using T = ModeTraits<MODE>;
 	constexpr int S = T::S;
-	__shared__ int s_keys[LDS_SLOTS];
-	__shared__ float s_acc[LDS_SLOTS * ACC_STRIDE];
-	for (int i = threadIdx.x; i < LDS_SLOTS; i += PIX_BLOCK) s_keys[i] = -1;
-	for (int i = threadIdx.x; i < LDS_SLOTS * ACC_STRIDE; i += PIX_BLOCK) s_acc[i] = 0.f;
-	__syncthreads();
+	static_assert(T::NACC <= 32, "accumulator row must fit the 32-value wave reduction");
 
 	// XCD-aware tile order: consecutive workgroups are dealt round-robin over the 8 XCDs, so give each XCD a contiguous
 	// band of tiles (neighbouring tiles share vertices, anchors and nodes -> L2 reuse within the XCD).
@@ -61,10 +70,26 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_fit_pixels(FitPixelArgs a) {
 	const int b = blockIdx.x;
 	const int tile = (b % 8) * per_xcd + b / 8;
 	const int tu = tile % a.tiles_x, tv = tile / a.tiles_x;
-	const int u = tu * PIX_TILE + static_cast<int>(threadIdx.x % PIX_TILE);
-	const int v = tv * PIX_TILE + static_cast<int>(threadIdx.x / PIX_TILE);
+	// wave w of the workgroup owns the 8x8 quadrant (w & 1, w >> 1): compact pixel sets touch the fewest nodes
+	const int lane = static_cast<int>(threadIdx.x & 63), wave = static_cast<int>(threadIdx.x >> 6);
+	const int u = tu * PIX_TILE + (wave & 1) * 8 + (lane & 7);
+	const int v = tv * PIX_TILE + (wave >> 1) * 8 + (lane >> 3);
 	const bool in_image = tile < tiles && u < a.W && v < a.H;
 	const int64_t p = static_cast<int64_t>(v) * a.W + u;
+
+	// per-lane inputs of the wave-level node loop below
+	uint32_t pending = 0;   // bit 8*fv + k: anchor k of face vertex fv still to be reduced
+	int vid[3] = {0, 0, 0};
+	int anc[3][MAX_ANCHORS];
+	float dr_dV[9];
+	float rn[3] = {0.f, 0.f, 0.f}, rho[3] = {0.f, 0.f, 0.f};
+	float r_used = 0.f;
+#pragma unroll
+	for (int c = 0; c < 9; c++) dr_dV[c] = 0.f;
+#pragma unroll
+	for (int fv = 0; fv < 3; fv++)
+#pragma unroll
+		for (int k = 0; k < MAX_ANCHORS; k++) anc[fv][k] = -1;
 
 	if (in_image) {
 		const uint64_t key = a.keys[p];
@@ -73,7 +98,6 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_fit_pixels(FitPixelArgs a) {
 		RasterHit h{0.f, 0.f, 0.f, 0.f, 0.f};
 		f3 V3[3], N3[3];
 		FaceNdc fn;
-		int vid[3] = {0, 0, 0};
 		const float px = pixel_to_ndc(u, a.W, a.H), py = pixel_to_ndc(v, a.H, a.W);
 		if (key != EMPTY_KEY) {
 			face = static_cast<int32_t>(key & 0xffffffffu);
@@ -151,7 +175,9 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_fit_pixels(FitPixelArgs a) {
 		}
 		if (contributes) {
 			// ---- rasterized surface Jacobians (RasterizedSurfaceJacobiansImpl.h:114-200) ----
-			const float rho[3] = {h.b0, h.b1, h.b2};
+			rho[0] = h.b0;
+			rho[1] = h.b1;
+			rho[2] = h.b2;
 			float A, sa[3], drho[3] = {0.f, 0.f, 0.f};
 			A = spa_cw(fn.x[0], fn.y[0], fn.x[1], fn.y[1], fn.x[2], fn.y[2]) + K_EPSILON;
 			if (a.perspective) {
@@ -231,10 +257,12 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_fit_pixels(FitPixelArgs a) {
 					for (int c = 0; c < 9; c++) J[r][c] = J2[r][c];
 			}
 			// dr/dV = dr/dwl * dwl/dV + dr/dnl * dnl/dV ; dr/dN = dr/dnl (rho (x) I)
-			float dr_dV[9];
 			const float Vr[3][3] = {{V3[0].x, V3[0].y, V3[0].z}, {V3[1].x, V3[1].y, V3[1].z}, {V3[2].x, V3[2].y, V3[2].z}};
 			const float Nr[3][3] = {{N3[0].x, N3[0].y, N3[0].z}, {N3[1].x, N3[1].y, N3[1].z}, {N3[2].x, N3[2].y, N3[2].z}};
-			const float rw[3] = {dr_dwl.x, dr_dwl.y, dr_dwl.z}, rn[3] = {dr_dnl.x, dr_dnl.y, dr_dnl.z};
+			const float rw[3] = {dr_dwl.x, dr_dwl.y, dr_dwl.z};
+			rn[0] = dr_dnl.x;
+			rn[1] = dr_dnl.y;
+			rn[2] = dr_dnl.z;
 #pragma unroll
 			for (int c = 0; c < 9; c++) {
 				float w_rc[3], n_rc[3];
@@ -248,98 +276,101 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_fit_pixels(FitPixelArgs a) {
 				const float y = (rn[0] * n_rc[0] + rn[1] * n_rc[1]) + rn[2] * n_rc[2];
 				dr_dV[c] = x + y;
 			}
-			// ---- pixel -> node Jacobians (PixelVertexAnchorJacobiansImpl.h:229-363), merged per unique node ----
+			// anchors of the face's vertices (PixelVertexAnchorJacobiansImpl.h:229-363 via the face-node association)
 			const int KA = a.anchor_count;
-			int anc[3][MAX_ANCHORS];
 #pragma unroll
 			for (int fv = 0; fv < 3; fv++)
 #pragma unroll
-				for (int k = 0; k < MAX_ANCHORS; k++) anc[fv][k] = (k < KA) ? a.anchors[static_cast<int64_t>(vid[fv]) * KA + k] : -1;
-			const float r_used = residual;
+				for (int k = 0; k < MAX_ANCHORS; k++) {
+					const int n = (k < KA) ? a.anchors[static_cast<int64_t>(vid[fv]) * KA + k] : -1;
+					anc[fv][k] = n;
+					if (n >= 0) pending |= 1u << (8 * fv + k);
+				}
+			r_used = residual;
+		}
+	}
+
+	// ---- wave-level reduction over the distinct nodes of this wave's pixels ----
+	// Per node, a pixel's Jacobian sums the contributions of every face vertex anchored to it (fv ascending, the
+	// reference's association keeps the LAST matching anchor slot of a vertex: AssociateFacesWithAnchors), then JJ^T
+	// and J r are added to the node's accumulator row.
+	const int KA = a.anchor_count;
+	while (true) {
+		const uint64_t active = __ballot(pending != 0u);
+		if (active == 0) break;
+		const int leader = __ffsll(static_cast<unsigned long long>(active)) - 1;
+		int mine = -1;
 #pragma unroll
-			for (int fv0 = 0; fv0 < 3; fv0++) {
+		for (int fv = 2; fv >= 0; fv--)
 #pragma unroll
-				for (int k0 = 0; k0 < MAX_ANCHORS; k0++) {
-					const int node = anc[fv0][k0];
-					if (node < 0) continue;
-					// first occurrence only (the reference keeps one face-anchor per unique node, in first-appearance order)
-					bool seen = false;
+			for (int k = MAX_ANCHORS - 1; k >= 0; k--)
+				if ((pending >> (8 * fv + k)) & 1u) mine = anc[fv][k];
+		const int node = __shfl(mine, leader);
+		float jr[3] = {0.f, 0.f, 0.f}, jt[3] = {0.f, 0.f, 0.f};
+		bool has = false;
 #pragma unroll
-					for (int fv1 = 0; fv1 <= fv0; fv1++)
+		for (int fv = 0; fv < 3; fv++) {
+			int kk = -1;
 #pragma unroll
-						for (int k1 = 0; k1 < MAX_ANCHORS; k1++)
-							if ((fv1 < fv0 || k1 < k0) && anc[fv1][k1] == node) seen = true;
-					if (seen) continue;
-					float jr[3] = {0.f, 0.f, 0.f}, jt[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-					for (int fv = fv0; fv < 3; fv++) {
-#pragma unroll
-						for (int k = 0; k < MAX_ANCHORS; k++) {
-							if (anc[fv][k] != node) continue;
-							const int64_t vk = static_cast<int64_t>(vid[fv]) * KA + k;
-							const float4 jv = a.jv[vk];
-							const f3 dv = make3(dr_dV[3 * fv], dr_dV[3 * fv + 1], dr_dV[3 * fv + 2]);
-							if (MODE != NNRT_ITERATION_ROTATION_ONLY) {
-								jt[0] += dv.x * jv.w;
-								jt[1] += dv.y * jv.w;
-								jt[2] += dv.z * jv.w;
-							}
-							if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) {
-								const float4 jn = a.jn[vk];
-								const f3 dn = make3(rn[0] * rho[fv], rn[1] * rho[fv], rn[2] * rho[fv]);
-								const f3 t1 = row_times_skew(dv, make3(jv.x, jv.y, jv.z));
-								const f3 t2 = row_times_skew(dn, make3(jn.x, jn.y, jn.z));
-								jr[0] += t1.x + t2.x;
-								jr[1] += t1.y + t2.y;
-								jr[2] += t1.z + t2.z;
-							}
-						}
-					}
-					float Jn[S];
-					if (MODE == NNRT_ITERATION_ALL) {
-						Jn[0] = jr[0];
-						Jn[1] = jr[1];
-						Jn[2] = jr[2];
-						Jn[3 % S] = jt[0];
-						Jn[4 % S] = jt[1];
-						Jn[5 % S] = jt[2];
-					} else if (MODE == NNRT_ITERATION_TRANSLATION_ONLY) {
-						Jn[0] = jt[0];
-						Jn[1] = jt[1];
-						Jn[2] = jt[2];
-					} else {
-						Jn[0] = jr[0];
-						Jn[1] = jr[1];
-						Jn[2] = jr[2];
-					}
-					// ---- accumulate JJ^T (upper triangle) and J r into the workgroup's LDS table ----
-					float vals[T::NACC];
-					int e = 0;
-#pragma unroll
-					for (int c0 = 0; c0 < S; c0++)
-#pragma unroll
-						for (int c1 = c0; c1 < S; c1++) vals[e++] = Jn[c0] * Jn[c1];
-#pragma unroll
-					for (int c = 0; c < S; c++) vals[T::NH + c] = Jn[c] * r_used;
-					const int slot = lds_find_slot(s_keys, node);
-					if (slot >= 0) {
-						float* dst = s_acc + slot * ACC_STRIDE;
-#pragma unroll
-						for (int k = 0; k < T::NACC; k++) atomicAdd(dst + k, vals[k]);
-					} else {   // table full: fall back to global atomics (correct, slower)
-						float* dst = a.acc + static_cast<int64_t>(node) * ACC_STRIDE;
-#pragma unroll
-						for (int k = 0; k < T::NACC; k++) atomicAdd(dst + k, vals[k]);
-					}
+			for (int k = 0; k < MAX_ANCHORS; k++) {
+				const uint32_t bit = 1u << (8 * fv + k);
+				if ((pending & bit) && anc[fv][k] == node) {
+					pending &= ~bit;
+					kk = k;
+				}
+			}
+			if (kk >= 0) {
+				has = true;
+				const int64_t vk = static_cast<int64_t>(vid[fv]) * KA + kk;
+				const float4 jv = a.jv[vk];
+				const f3 dv = make3(dr_dV[3 * fv], dr_dV[3 * fv + 1], dr_dV[3 * fv + 2]);
+				if (MODE != NNRT_ITERATION_ROTATION_ONLY) {
+					jt[0] += dv.x * jv.w;
+					jt[1] += dv.y * jv.w;
+					jt[2] += dv.z * jv.w;
+				}
+				if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) {
+					const float4 jn = a.jn[vk];
+					const f3 dn = make3(rn[0] * rho[fv], rn[1] * rho[fv], rn[2] * rho[fv]);
+					const f3 t1 = row_times_skew(dv, make3(jv.x, jv.y, jv.z));
+					const f3 t2 = row_times_skew(dn, make3(jn.x, jn.y, jn.z));
+					jr[0] += t1.x + t2.x;
+					jr[1] += t1.y + t2.y;
+					jr[2] += t1.z + t2.z;
 				}
 			}
 		}
-	}
-	__syncthreads();
-	for (int i = threadIdx.x; i < LDS_SLOTS * T::NACC; i += PIX_BLOCK) {
-		const int s = i / T::NACC, k = i % T::NACC;
-		const int node = s_keys[s];
-		if (node >= 0) atomicAdd(a.acc + static_cast<int64_t>(node) * ACC_STRIDE + k, s_acc[s * ACC_STRIDE + k]);
+		float Jn[S];
+		if (MODE == NNRT_ITERATION_ALL) {
+			Jn[0] = jr[0];
+			Jn[1] = jr[1];
+			Jn[2] = jr[2];
+			Jn[3 % S] = jt[0];
+			Jn[4 % S] = jt[1];
+			Jn[5 % S] = jt[2];
+		} else if (MODE == NNRT_ITERATION_TRANSLATION_ONLY) {
+			Jn[0] = jt[0];
+			Jn[1] = jt[1];
+			Jn[2] = jt[2];
+		} else {
+			Jn[0] = jr[0];
+			Jn[1] = jr[1];
+			Jn[2] = jr[2];
+		}
+		// products rounded to float as the reference forms them, summed in double
+		double vals[32];
+		int e = 0;
+#pragma unroll
+		for (int c0 = 0; c0 < S; c0++)
+#pragma unroll
+			for (int c1 = c0; c1 < S; c1++) vals[e++] = has ? static_cast<double>(Jn[c0] * Jn[c1]) : 0.0;
+#pragma unroll
+		for (int c = 0; c < S; c++) vals[T::NH + c] = has ? static_cast<double>(Jn[c] * r_used) : 0.0;
+#pragma unroll
+		for (int c = T::NACC; c < 32; c++) vals[c] = 0.0;
+		const double total = wave_transpose_reduce32(vals, lane);
+		const int idx = transpose_index(lane);
+		if (lane < 32 && idx < T::NACC) atomicAdd(a.acc + static_cast<int64_t>(node) * ACC_STRIDE + idx, total);
 	}
 }
 
@@ -392,21 +423,22 @@ __global__ void k_solve_update(SolveArgs a) {
 	constexpr int S = T::S;
 	const int n = blockIdx.x * blockDim.x + threadIdx.x;
 	if (n >= a.N) return;
-	float* acc = a.acc + static_cast<int64_t>(n) * ACC_STRIDE;
+	double* acc = a.acc + static_cast<int64_t>(n) * ACC_STRIDE;
 	float H[S][S], g[S];
 	int e = 0;
 #pragma unroll
 	for (int c0 = 0; c0 < S; c0++)
 #pragma unroll
 		for (int c1 = c0; c1 < S; c1++) {
-			H[c0][c1] = acc[e];
-			H[c1][c0] = acc[e];
+			const float hv = static_cast<float>(acc[e]);
+			H[c0][c1] = hv;
+			H[c1][c0] = hv;
 			e++;
 		}
 #pragma unroll
-	for (int c = 0; c < S; c++) g[c] = 0.f - acc[T::NH + c];
+	for (int c = 0; c < S; c++) g[c] = 0.f - static_cast<float>(acc[T::NH + c]);
 #pragma unroll
-	for (int k = 0; k < T::NACC; k++) acc[k] = 0.f;
+	for (int k = 0; k < T::NACC; k++) acc[k] = 0.0;
 	if (a.hessian_out) {
 #pragma unroll
 		for (int r = 0; r < S; r++)

@@ -28,13 +28,13 @@ struct FitPixelArgs {
 	float* residuals;       // [P]
 	uint8_t* residual_mask; // [P]
 	int32_t* pixel_face;    // [P]
-	float* acc;             // [N, ACC_STRIDE]
+	double* acc;            // [N, ACC_STRIDE] fp64 data-term accumulator (21 JtJ + 6 J r)
 };
 
 struct SolveArgs {
 	int N;
 	float lm;
-	float* acc;
+	double* acc;
 	float* node_state;
 	float* updates_out;     // [N*s]
 	float* gradient_out;    // [N*s]
@@ -76,7 +76,7 @@ struct ArrowheadWorkspace {
 	int* edge_list = nullptr;   // [E]
 };
 // acc -> diagonal blocks (+lm) + rhs ; arrowhead solve ; update node state
-nnrt_status launch_arrowhead_iteration(const ArrowheadWorkspace& ws, const float* acc, float lm, const int32_t* edges, const float* wing,
+nnrt_status launch_arrowhead_iteration(const ArrowheadWorkspace& ws, const double* acc, float lm, const int32_t* edges, const float* wing,
                                        float* node_state, float* acc_mut, float* updates_out, float* gradient_out, float* hessian_out,
                                        int* error_flag, hipStream_t stream);
 nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* edges, const float* wing, int* error_flag, hipStream_t stream);

@@ -911,6 +911,13 @@ ORC_API void orc_pixel_vertex_anchor_jacobians(const float* rast_vj, const float
 	}
 }
 
+// Summation precision of the data-term JtJ / Jt r. The reference sums the float products serially in float
+// (DeformableMeshToImageFitterImpl.h:199-456); on ill-conditioned node blocks that rounding alone moves the solved
+// update by up to ~4e-4 relative (C2), so the checker sums the same float products in double (default, = the exactly
+// summed reference data term) and keeps the float-serial order available to measure that noise.
+static int g_acc_double = 1;
+ORC_API void orc_set_accumulate_double(int on) { g_acc_double = on; }
+
 // DeformableMeshToImageFitterImpl.h:199-456 : block-diagonal data JtJ and -Jt r, node lists in ascending (pixel, slot) order.
 // out_H [N, s, s], out_g [N*s]
 ORC_API void orc_data_hessian_gradient(const float* pixel_jacobians, const int32_t* pixel_counts, const int64_t* pixel_faces, int Kf,
@@ -939,21 +946,29 @@ ORC_API void orc_data_hessian_gradient(const float* pixel_jacobians, const int32
 		for (int c0 = 0; c0 < s; c0++) {
 			for (int c1 = c0; c1 < s; c1++) {
 				float acc = 0.0f;
+				double accd = 0.0;
 				for (int64_t e = offsets[n]; e < offsets[n + 1]; e++) {
 					const float* J = pixel_jacobians + addr[e] * s;
-					acc += J[c0] * J[c1];
+					if (g_acc_double) accd += static_cast<double>(J[c0] * J[c1]);
+					else acc += J[c0] * J[c1];
 				}
+				if (g_acc_double) acc = static_cast<float>(accd);
 				out_H[n * s * s + c0 * s + c1] = acc;
 				out_H[n * s * s + c1 * s + c0] = acc;
 			}
 		}
 		float gsum[6] = {0, 0, 0, 0, 0, 0};
+		double gsumd[6] = {0, 0, 0, 0, 0, 0};
 		for (int64_t e = offsets[n]; e < offsets[n + 1]; e++) {
 			int64_t p = addr[e] / M;
 			if (!residual_mask[p]) continue;
 			const float* J = pixel_jacobians + addr[e] * s;
-			for (int c = 0; c < s; c++) gsum[c] += J[c] * residuals[p];
+			for (int c = 0; c < s; c++) {
+				if (g_acc_double) gsumd[c] += static_cast<double>(J[c] * residuals[p]);
+				else gsum[c] += J[c] * residuals[p];
+			}
 		}
+		if (g_acc_double) for (int c = 0; c < s; c++) gsum[c] = static_cast<float>(gsumd[c]);
 		for (int c = 0; c < s; c++) out_g[n * s + c] = 0.f - gsum[c];
 	}
 }

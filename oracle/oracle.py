@@ -67,6 +67,11 @@ def set_num_threads(n: int):
     lib().orc_set_num_threads(ctypes.c_int(n))
 
 
+def set_accumulate_double(on: bool):
+    """Data-term JtJ / Jt r summation: double (default, exact-sum checker) or the reference's float-serial order."""
+    lib().orc_set_accumulate_double(ctypes.c_int(int(on)))
+
+
 def num_threads() -> int:
     return lib().orc_num_threads()
 

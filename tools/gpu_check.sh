@@ -4,7 +4,7 @@
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
-STAGES=${STAGES:-"smoke tests bench prof"}
+STAGES=${STAGES:-"smoke tests bench prof pmc"}
 step() {   # name seconds cmd...
 	local name=$1 t=$2
 	shift 2
@@ -21,7 +21,9 @@ for s in $STAGES; do
 		smoke) step smoke 400 python -u -c "import __graft_entry__ as g; g.smoke()"; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
 		tests) step gpu_tests 900 python -u -m pytest tests -m gpu -q --maxfail=20 -p no:cacheprovider; rc=$?; fatal $rc && exit $rc ;;
 		bench) step bench 600 python -u bench.py; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
-		prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o r01 -- python3 bench.py --steps 300 --warmup 30 --timed-steps 100 --no-cpu-baseline; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+		prof) step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 300 --warmup 30 --timed-steps 100 --no-cpu-baseline; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
+		pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 20 --warmup 5 --timed-steps 20 --no-cpu-baseline; rc=$?; [ $rc -eq 0 ] || exit $rc
+		     step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 20 --warmup 5 --timed-steps 20 --no-cpu-baseline; rc=$?; [ $rc -eq 0 ] || exit $rc ;;
 	esac
 done
 exit 0
