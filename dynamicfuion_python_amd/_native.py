@@ -13,7 +13,7 @@ import subprocess
 import torch  # noqa: F401  (loads the HIP runtime shared with the library)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnnrt_mi355x.so")
+LIB_PATH = os.environ.get("NNRT_LIB_PATH") or os.path.join(_HERE, "libnnrt_mi355x.so")   # override: development timing builds
 CSRC = os.path.join(_HERE, "csrc")
 
 _lib = None

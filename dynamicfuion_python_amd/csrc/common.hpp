@@ -125,7 +125,10 @@ __device__ inline float point_segment_sq(float px, float py, float ax, float ay,
 	return dx * dx + dy * dy;
 }
 
-// returns true if accepted. `box_checked`: caller already evaluated the bounding-box test identically.
+// Ray-face test of one pixel centre (RayFaceIntersection.h:162-255 semantics). Returns true if accepted.
+// DIST = false skips the point-to-edge distance: valid only where the caller knows the distance test passes (a face
+// whose box diagonal is far below the blur radius, or a winner re-resolved after a full test); h.dist is then unset.
+template <bool DIST = true>
 __device__ inline bool face_test(const FaceNdc& f, float px, float py, float blur, bool persp, bool clip, bool cull, RasterHit& h) {
 	const float area = spa_cw(f.x[0], f.y[0], f.x[1], f.y[1], f.x[2], f.y[2]);
 	const bool back = area < 0.f;
@@ -162,12 +165,14 @@ __device__ inline bool face_test(const FaceNdc& f, float px, float py, float blu
 	}
 	const float depth = c0 * f.z[0] + c1 * f.z[1] + c2 * f.z[2];
 	if (depth < 0.f) return false;
-	const float d = fmin3f(point_segment_sq(px, py, f.x[0], f.y[0], f.x[1], f.y[1]), point_segment_sq(px, py, f.x[0], f.y[0], f.x[2], f.y[2]),
-	                       point_segment_sq(px, py, f.x[1], f.y[1], f.x[2], f.y[2]));
-	const bool inside = b0 > 0.f && b1 > 0.f && b2 > 0.f;
-	if (!inside && d >= blur) return false;
+	if constexpr (DIST) {
+		const float d = fmin3f(point_segment_sq(px, py, f.x[0], f.y[0], f.x[1], f.y[1]), point_segment_sq(px, py, f.x[0], f.y[0], f.x[2], f.y[2]),
+		                       point_segment_sq(px, py, f.x[1], f.y[1], f.x[2], f.y[2]));
+		const bool inside = b0 > 0.f && b1 > 0.f && b2 > 0.f;
+		if (!inside && d >= blur) return false;
+		h.dist = inside ? -d : d;
+	}
 	h.depth = depth;
-	h.dist = inside ? -d : d;
 	h.b0 = c0;
 	h.b1 = c1;
 	h.b2 = c2;

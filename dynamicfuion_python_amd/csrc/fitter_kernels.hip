@@ -7,8 +7,8 @@
 // Jacobians and [N,4000] node lists (capped: A4) and reduces each node serially. Here every 64-lane wavefront owns an
 // 8x8 pixel block; it walks the distinct nodes its pixels touch (wave-uniform loop driven by a ballot), each lane builds
 // its pixel's 6-dof Jacobian for that node, and the 27 products (21 JtJ upper-triangle entries + 6 J r) are summed over
-// the wave with a transposing butterfly (32 values -> one per lane in 6 exchange steps) and added to the node's fp64
-// accumulator row with one atomic per entry. Products are rounded to float exactly as the reference forms them and
+// the wave in double with a transposing butterfly (permlane swaps + DPP, no LDS) and added to the node's fp64
+// accumulator row with one 27-lane atomic. Products are rounded to float exactly as the reference forms them and
 // summed in double, so the data term equals the exactly-summed reference data term (see DESIGN.md "Numerics") -- no
 // intermediate tensors, no node-list cap, no LDS.
 #include "fitter_kernels.hpp"
@@ -33,31 +33,81 @@ struct ModeTraits<NNRT_ITERATION_ROTATION_ONLY> {
 	static constexpr int S = 3, NH = 6, NACC = 9;
 };
 
-// Sum 32 per-lane values over the 64-lane wavefront. Each exchange step halves the values a lane holds: lanes with the
-// step's bit set keep the upper half and send the lower half to their partner (and vice versa), so 32 + 1 shuffles
-// replace 32 x 6. On return lane l (and l + 32) holds the wave total of value index transpose_index(l).
-__device__ inline int transpose_index(int lane) {
-	return ((lane & 1) << 4) | ((lane & 2) << 2) | (lane & 4) | ((lane & 8) >> 2) | ((lane & 16) >> 4);
+// ---- wavefront reduction helpers ----
+template <int CTRL>
+__device__ inline float dpp_f32(float x) {
+	return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ inline double dpp_f64(double x) {
+	const uint64_t u = __builtin_bit_cast(uint64_t, x);
+	const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(u & 0xffffffffu), CTRL, 0xf, 0xf, false);
+	const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(u >> 32), CTRL, 0xf, 0xf, false);
+	return __builtin_bit_cast(double, (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) | static_cast<uint32_t>(lo));
+}
+template <int CTRL, typename R>
+__device__ inline R dpp_move(R x) {
+	if constexpr (sizeof(R) == 4) return dpp_f32<CTRL>(x);
+	else return dpp_f64<CTRL>(x);
 }
 
-__device__ inline double wave_transpose_reduce32(double (&v)[32], int lane) {
-#pragma unroll
-	for (int step = 0; step < 5; step++) {
-		const int d = 1 << step;
-		const int half = 16 >> step;
-		const bool upper = (lane & d) != 0;
-#pragma unroll
-		for (int j = 0; j < half; j++) {
-			const double lo = v[j], hi = v[j + half];
-			const double send = upper ? lo : hi;
-			const double keep = upper ? hi : lo;
-			v[j] = keep + __shfl_xor(send, d);
-		}
+// ---- wave sum of 32 per-lane values (transposing butterfly) ----
+// Each exchange step halves the values a lane holds: lanes with the step's bit set keep the upper half of the values,
+// the others the lower half, each adding its partner's copy. The two cross-row steps go first through gfx950's
+// v_permlane32_swap / v_permlane16_swap
+// swap(lo, hi) exchanges the upper half of `lo` with the lower half of `hi` (32 lanes, or the odd/even 16-lane rows),
+// so after one add the lanes with the step's bit clear hold lo(l) + lo(l ^ d) and the others hi(l ^ d) + hi(l):
+// a whole transposing step costs one swap per dword and one add, no selects. Rows then finish with DPP (8, 4, 2) and a
+// quad_perm add (1). On return lanes 2i and 2i + 1 hold the wave total of value index i.
+template <bool ROW16>
+__device__ inline uint2 permlane_swap_u32(uint32_t lo, uint32_t hi) {
+	if constexpr (ROW16) {
+		const auto r = __builtin_amdgcn_permlane16_swap(lo, hi, false, false);
+		return make_uint2(r[0], r[1]);
+	} else {
+		const auto r = __builtin_amdgcn_permlane32_swap(lo, hi, false, false);
+		return make_uint2(r[0], r[1]);
 	}
-	return v[0] + __shfl_xor(v[0], 32);
+}
+template <bool ROW16, typename R>
+__device__ inline R swap_add(R lo, R hi) {
+	if constexpr (sizeof(R) == 4) {
+		const uint2 r = permlane_swap_u32<ROW16>(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
+		return __builtin_bit_cast(R, r.x) + __builtin_bit_cast(R, r.y);
+	} else {
+		const uint64_t a = __builtin_bit_cast(uint64_t, lo), b = __builtin_bit_cast(uint64_t, hi);
+		const uint2 l = permlane_swap_u32<ROW16>(static_cast<uint32_t>(a), static_cast<uint32_t>(b));
+		const uint2 h = permlane_swap_u32<ROW16>(static_cast<uint32_t>(a >> 32), static_cast<uint32_t>(b >> 32));
+		const R x = __builtin_bit_cast(R, (static_cast<uint64_t>(h.x) << 32) | l.x);
+		const R y = __builtin_bit_cast(R, (static_cast<uint64_t>(h.y) << 32) | l.y);
+		return x + y;
+	}
 }
 
-template <int MODE>
+template <int D, int HALF, typename R>
+__device__ inline void butterfly_row_step(R (&v)[32], bool upper) {
+#pragma unroll
+	for (int j = 0; j < HALF; j++) {
+		const R lo = v[j], hi = v[j + HALF];
+		const R from_above = dpp_move<0x100 + D>(lo);   // row_shl:D
+		const R from_below = dpp_move<0x110 + D>(hi);   // row_shr:D
+		v[j] = upper ? (hi + from_below) : (lo + from_above);
+	}
+}
+
+template <typename R>
+__device__ inline R wave_reduce32_swap(R (&v)[32], int lane) {
+#pragma unroll
+	for (int j = 0; j < 16; j++) v[j] = swap_add<false>(v[j], v[j + 16]);
+#pragma unroll
+	for (int j = 0; j < 8; j++) v[j] = swap_add<true>(v[j], v[j + 8]);
+	butterfly_row_step<8, 4>(v, (lane & 8) != 0);
+	butterfly_row_step<4, 2>(v, (lane & 4) != 0);
+	butterfly_row_step<2, 1>(v, (lane & 2) != 0);
+	return v[0] + dpp_move<0xB1>(v[0]);   // quad_perm [1,0,3,2]: lanes 2i, 2i+1 exchange
+}
+
+template <int MODE, int MAXK>
 __global__ __launch_bounds__(PIX_BLOCK) void k_fit_pixels(FitPixelArgs a) {
 	using T = ModeTraits<MODE>;
 	constexpr int S = T::S;
@@ -80,7 +130,7 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_fit_pixels(FitPixelArgs a) {
 	// per-lane inputs of the wave-level node loop below
 	uint32_t pending = 0;   // bit 8*fv + k: anchor k of face vertex fv still to be reduced
 	int vid[3] = {0, 0, 0};
-	int anc[3][MAX_ANCHORS];
+	int anc[3][MAXK];
 	float dr_dV[9];
 	float rn[3] = {0.f, 0.f, 0.f}, rho[3] = {0.f, 0.f, 0.f};
 	float r_used = 0.f;
@@ -89,7 +139,7 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_fit_pixels(FitPixelArgs a) {
 #pragma unroll
 	for (int fv = 0; fv < 3; fv++)
 #pragma unroll
-		for (int k = 0; k < MAX_ANCHORS; k++) anc[fv][k] = -1;
+		for (int k = 0; k < MAXK; k++) anc[fv][k] = -1;
 
 	if (in_image) {
 		const uint64_t key = a.keys[p];
@@ -114,7 +164,8 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_fit_pixels(FitPixelArgs a) {
 				a.ndc.ndc.project(V3[i].x, V3[i].y, V3[i].z, &fn.x[i], &fn.y[i]);
 				fn.z[i] = V3[i].z;
 			}
-			if (!face_test(fn, px, py, a.blur, a.perspective, false, true, h)) face = -1;
+			// the scatter accepted this face for this pixel after the full test; re-resolving needs no distance test
+			if (!face_test<false>(fn, px, py, a.blur, a.perspective, false, true, h)) face = -1;
 		}
 		// ---- ComputeDepthResiduals (:331-390) ----
 		const float depth = face >= 0 ? h.depth : -1.f;
@@ -281,7 +332,7 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_fit_pixels(FitPixelArgs a) {
 #pragma unroll
 			for (int fv = 0; fv < 3; fv++)
 #pragma unroll
-				for (int k = 0; k < MAX_ANCHORS; k++) {
+				for (int k = 0; k < MAXK; k++) {
 					const int n = (k < KA) ? a.anchors[static_cast<int64_t>(vid[fv]) * KA + k] : -1;
 					anc[fv][k] = n;
 					if (n >= 0) pending |= 1u << (8 * fv + k);
@@ -303,16 +354,15 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_fit_pixels(FitPixelArgs a) {
 #pragma unroll
 		for (int fv = 2; fv >= 0; fv--)
 #pragma unroll
-			for (int k = MAX_ANCHORS - 1; k >= 0; k--)
+			for (int k = MAXK - 1; k >= 0; k--)
 				if ((pending >> (8 * fv + k)) & 1u) mine = anc[fv][k];
 		const int node = __shfl(mine, leader);
 		float jr[3] = {0.f, 0.f, 0.f}, jt[3] = {0.f, 0.f, 0.f};
-		bool has = false;
 #pragma unroll
 		for (int fv = 0; fv < 3; fv++) {
 			int kk = -1;
 #pragma unroll
-			for (int k = 0; k < MAX_ANCHORS; k++) {
+			for (int k = 0; k < MAXK; k++) {
 				const uint32_t bit = 1u << (8 * fv + k);
 				if ((pending & bit) && anc[fv][k] == node) {
 					pending &= ~bit;
@@ -320,7 +370,6 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_fit_pixels(FitPixelArgs a) {
 				}
 			}
 			if (kk >= 0) {
-				has = true;
 				const int64_t vk = static_cast<int64_t>(vid[fv]) * KA + kk;
 				const float4 jv = a.jv[vk];
 				const f3 dv = make3(dr_dV[3 * fv], dr_dV[3 * fv + 1], dr_dV[3 * fv + 2]);
@@ -357,30 +406,42 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_fit_pixels(FitPixelArgs a) {
 			Jn[1] = jr[1];
 			Jn[2] = jr[2];
 		}
-		// products rounded to float as the reference forms them, summed in double
+		// products rounded to float as the reference forms them (lanes without the node hold Jn = 0 -> 0 products),
+		// summed in double over the wave and across waves
 		double vals[32];
 		int e = 0;
 #pragma unroll
 		for (int c0 = 0; c0 < S; c0++)
 #pragma unroll
-			for (int c1 = c0; c1 < S; c1++) vals[e++] = has ? static_cast<double>(Jn[c0] * Jn[c1]) : 0.0;
+			for (int c1 = c0; c1 < S; c1++) vals[e++] = static_cast<double>(Jn[c0] * Jn[c1]);
 #pragma unroll
-		for (int c = 0; c < S; c++) vals[T::NH + c] = has ? static_cast<double>(Jn[c] * r_used) : 0.0;
+		for (int c = 0; c < S; c++) vals[T::NH + c] = static_cast<double>(Jn[c] * r_used);
 #pragma unroll
 		for (int c = T::NACC; c < 32; c++) vals[c] = 0.0;
-		const double total = wave_transpose_reduce32(vals, lane);
-		const int idx = transpose_index(lane);
-		if (lane < 32 && idx < T::NACC) atomicAdd(a.acc + static_cast<int64_t>(node) * ACC_STRIDE + idx, total);
+		const double total = wave_reduce32_swap(vals, lane);
+		const int idx = (lane & 1) ? 32 : (lane >> 1);   // lanes 2i, 2i+1 hold entry i
+		if (idx < T::NACC) atomicAdd(a.acc + static_cast<int64_t>(node) * ACC_STRIDE + idx, total);
 	}
 }
 
 nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t stream) {
 	const int tiles = args.tiles_x * args.tiles_y;
 	const unsigned grid = static_cast<unsigned>(((tiles + 7) / 8) * 8);
+	// anchor slots per vertex: the common 4-anchor configuration gets its own instantiation (half the slot logic)
+	const bool k4 = args.anchor_count <= 4;
 	switch (mode) {
-		case NNRT_ITERATION_ALL: k_fit_pixels<NNRT_ITERATION_ALL><<<grid, PIX_BLOCK, 0, stream>>>(args); break;
-		case NNRT_ITERATION_TRANSLATION_ONLY: k_fit_pixels<NNRT_ITERATION_TRANSLATION_ONLY><<<grid, PIX_BLOCK, 0, stream>>>(args); break;
-		case NNRT_ITERATION_ROTATION_ONLY: k_fit_pixels<NNRT_ITERATION_ROTATION_ONLY><<<grid, PIX_BLOCK, 0, stream>>>(args); break;
+		case NNRT_ITERATION_ALL:
+			if (k4) k_fit_pixels<NNRT_ITERATION_ALL, 4><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			else k_fit_pixels<NNRT_ITERATION_ALL, MAX_ANCHORS><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			break;
+		case NNRT_ITERATION_TRANSLATION_ONLY:
+			if (k4) k_fit_pixels<NNRT_ITERATION_TRANSLATION_ONLY, 4><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			else k_fit_pixels<NNRT_ITERATION_TRANSLATION_ONLY, MAX_ANCHORS><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			break;
+		case NNRT_ITERATION_ROTATION_ONLY:
+			if (k4) k_fit_pixels<NNRT_ITERATION_ROTATION_ONLY, 4><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			else k_fit_pixels<NNRT_ITERATION_ROTATION_ONLY, MAX_ANCHORS><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			break;
 		default: set_error("unknown iteration mode"); return NNRT_ERROR_ARGUMENT;
 	}
 	NNRT_LAUNCH_CHECK();

@@ -193,10 +193,95 @@ __global__ __launch_bounds__(256) void k_warp_mesh(const float* __restrict__ poi
 	out_n[v] = make_float4(wn.x, wn.y, wn.z, 0.f);
 }
 
+// K <= 4: one lane per (vertex, anchor slot) -- 4x the waves of a lane-per-vertex launch, so the node-state gathers of
+// neighbouring lanes are in flight together; Jv/Jn rows are stored coalesced (lane = slot). The quad's slot-0 lane sums
+// the slot contributions in slot order (DPP quad broadcasts), the reference's serial accumulation order.
+template <int CTRL>
+__device__ inline float quad_bcast(float x) {
+	return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
+}
+
+__global__ __launch_bounds__(256) void k_warp_mesh_quad(const float* __restrict__ points, const float* __restrict__ normals, int64_t V,
+                                                        const float* __restrict__ node_state, const int32_t* __restrict__ anchors,
+                                                        const float* __restrict__ weights, int K, WarpExtrinsics E, float4* __restrict__ out_p,
+                                                        float4* __restrict__ out_n, float4* __restrict__ jv, float4* __restrict__ jn) {
+	const int64_t tid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	const int64_t v = tid >> 2;
+	const int k = static_cast<int>(tid & 3);
+	const bool vertex_ok = v < V;
+	const bool slot_ok = vertex_ok && k < K;
+	f3 cp = make3(0.f, 0.f, 0.f), cn = make3(0.f, 0.f, 0.f);   // this slot's contribution
+	bool valid = false;
+	if (slot_ok) {
+		const f3 p = make3(points[3 * v], points[3 * v + 1], points[3 * v + 2]);
+		const f3 n = make3(normals[3 * v], normals[3 * v + 1], normals[3 * v + 2]);
+		f3 pc = p, nc = n;
+		if (!E.identity) {
+			pc = make3(((p.x * E.m[0] + p.y * E.m[1]) + p.z * E.m[2]) + E.m[3], ((p.x * E.m[4] + p.y * E.m[5]) + p.z * E.m[6]) + E.m[7],
+			           ((p.x * E.m[8] + p.y * E.m[9]) + p.z * E.m[10]) + E.m[11]);
+			nc = make3((n.x * E.m[0] + n.y * E.m[1]) + n.z * E.m[2], (n.x * E.m[4] + n.y * E.m[5]) + n.z * E.m[6],
+			           (n.x * E.m[8] + n.y * E.m[9]) + n.z * E.m[10]);
+		}
+		const int32_t a = anchors[v * K + k];
+		float4 ojv = make_float4(0.f, 0.f, 0.f, 0.f), ojn = make_float4(0.f, 0.f, 0.f, 0.f);
+		if (a != -1) {
+			valid = true;
+			const float w = weights[v * K + k];
+			const float4* ns = reinterpret_cast<const float4*>(node_state + static_cast<int64_t>(a) * NODE_STRIDE);
+			const float4 s0 = ns[0], s1 = ns[1], s2 = ns[2], s3 = ns[3];   // g, t, R (row-major), pad
+			const f3 g = make3(s0.x, s0.y, s0.z);
+			const f3 t = make3(s0.w, s1.x, s1.y);
+			const float R[9] = {s1.z, s1.w, s2.x, s2.y, s2.z, s2.w, s3.x, s3.y, s3.z};
+			const f3 Rd = matvec3(R, sub3(pc, g));
+			cp = make3(w * ((g.x + Rd.x) + t.x), w * ((g.y + Rd.y) + t.y), w * ((g.z + Rd.z) + t.z));
+			const f3 Rn = matvec3(R, nc);
+			cn = make3(w * Rn.x, w * Rn.y, w * Rn.z);
+			if (jv) {
+				const f3 Rj = E.identity ? Rd : matvec3(R, sub3(p, g));
+				const f3 Rnj = E.identity ? Rn : matvec3(R, n);
+				ojv = make_float4(-w * Rj.x, -w * Rj.y, -w * Rj.z, w);
+				ojn = make_float4(-w * Rnj.x, -w * Rnj.y, -w * Rnj.z, 0.f);
+			}
+		}
+		if (jv) {
+			jv[v * K + k] = ojv;
+			jn[v * K + k] = ojn;
+		}
+	}
+	// serial slot-order sum on the quad's first lane: ((0 + c0) + c1) + c2) + c3, skipping invalid anchors
+	const float vf = valid ? 1.f : 0.f;
+	float c[4][7];
+	const float mine[7] = {cp.x, cp.y, cp.z, cn.x, cn.y, cn.z, vf};
+#pragma unroll
+	for (int i = 0; i < 7; i++) {
+		c[0][i] = quad_bcast<0x00>(mine[i]);
+		c[1][i] = quad_bcast<0x55>(mine[i]);
+		c[2][i] = quad_bcast<0xAA>(mine[i]);
+		c[3][i] = quad_bcast<0xFF>(mine[i]);
+	}
+	if (vertex_ok && k == 0) {
+		float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			if (q >= K || c[q][6] == 0.f) continue;
+#pragma unroll
+			for (int i = 0; i < 6; i++) acc[i] += c[q][i];
+		}
+		out_p[v] = make_float4(acc[0], acc[1], acc[2], 0.f);
+		out_n[v] = make_float4(acc[3], acc[4], acc[5], 0.f);
+	}
+}
+
 nnrt_status launch_warp_mesh(const float* points, const float* normals, int64_t V, const float* node_state, const int32_t* anchors,
                              const float* weights, int K, const WarpExtrinsics& E, float4* out_p, float4* out_n, float4* jv, float4* jn,
                              hipStream_t stream) {
 	if (V == 0) return NNRT_OK;
+	if (K <= 4) {
+		k_warp_mesh_quad<<<static_cast<unsigned>(ceil_div(4 * V, 256)), 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E,
+		                                                                                 out_p, out_n, jv, jn);
+		NNRT_LAUNCH_CHECK();
+		return NNRT_OK;
+	}
 	k_warp_mesh<<<static_cast<unsigned>(ceil_div(V, 256)), 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p,
 	                                                                          out_n, jv, jn);
 	NNRT_LAUNCH_CHECK();

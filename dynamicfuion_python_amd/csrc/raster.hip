@@ -26,45 +26,114 @@ __device__ inline FaceNdc load_face_ndc(const float* face_ndc, int64_t f) {
 	return r;
 }
 
-// scatter all pixels of the face's box; returns nothing, updates keys
-__device__ inline void scatter_face(const FaceNdc& fn, int32_t face, const RasterOptions& o, uint64_t* keys) {
+// Exact pixel range of a face: the pixels whose centres pass face_test's bounding-box check (box widened by the blur
+// radius). Returns false for faces face_test rejects for every pixel (culled, zero-area, behind the camera, off-image).
+__device__ inline bool face_pixel_range(const FaceNdc& fn, const RasterOptions& o, int& u0, int& u1, int& v0, int& v1) {
 	const float area = spa_cw(fn.x[0], fn.y[0], fn.x[1], fn.y[1], fn.x[2], fn.y[2]);
 	const bool back = area < 0.f;
 	const bool zero_area = (area <= K_EPSILON && area >= -1.f * K_EPSILON);
 	const bool zinv = fmax3f(fn.z[0], fn.z[1], fn.z[2]) < K_EPSILON;
-	if ((o.cull_back_faces && back) || zero_area || zinv) return;   // rejected for every pixel by face_test
+	if ((o.cull_back_faces && back) || zero_area || zinv) return false;
 	const float xmin = fmin3f(fn.x[0], fn.x[1], fn.x[2]) - o.blur;
 	const float xmax = fmax3f(fn.x[0], fn.x[1], fn.x[2]) + o.blur;
 	const float ymin = fmin3f(fn.y[0], fn.y[1], fn.y[2]) - o.blur;
 	const float ymax = fmax3f(fn.y[0], fn.y[1], fn.y[2]) + o.blur;
-	if (!(xmax >= xmin) || !(ymax >= ymin)) return;
-	int u0, u1, v0, v1;
+	if (!(xmax >= xmin) || !(ymax >= ymin)) return false;
 	pixel_span(xmin, xmax, o.W, o.H, &u0, &u1);
 	pixel_span(ymin, ymax, o.H, o.W, &v0, &v1);
-	for (int v = v0; v <= v1; v++) {
-		const float py = pixel_to_ndc(v, o.H, o.W);
-		for (int u = u0; u <= u1; u++) {
-			const float px = pixel_to_ndc(u, o.W, o.H);
-			RasterHit h;
-			if (!face_test(fn, px, py, o.blur, o.perspective, o.clip_barycentric, o.cull_back_faces, h)) continue;
-			atomicMin(reinterpret_cast<unsigned long long*>(keys + static_cast<int64_t>(v) * o.W + u),
-			          static_cast<unsigned long long>(raster_key(h.depth, face)));
+	// pixel_to_ndc is monotone: trim the one-pixel widening so only pixels inside the box remain
+	while (u0 <= u1 && pixel_to_ndc(u0, o.W, o.H) < xmin) u0++;
+	while (u1 >= u0 && pixel_to_ndc(u1, o.W, o.H) > xmax) u1--;
+	while (v0 <= v1 && pixel_to_ndc(v0, o.H, o.W) < ymin) v0++;
+	while (v1 >= v0 && pixel_to_ndc(v1, o.H, o.W) > ymax) v1--;
+	return u0 <= u1 && v0 <= v1;
+}
+
+// One workgroup = 256 consecutive faces. Consecutive faces of a mesh are spatially coherent, so their pixel boxes share a
+// small bounding rectangle: the workgroup resolves its faces' (depth, face) minima in LDS with 64-bit LDS atomics and
+// then merges the rectangle into the image with one global atomicMin per touched pixel, row-contiguous across lanes
+// (memory-side global atomics cost one 64-B request per scattered lane: MI355X_MICROARCH.md "Global float atomics").
+// Workgroups whose rectangle exceeds the LDS tile fall back to per-pixel global atomics. Result = min over all faces of
+// the key, i.e. identical to a direct scatter.
+constexpr int SCATTER_BLOCK = 256;
+constexpr int SCATTER_LDS_KEYS = 4096;   // 32 KiB
+
+__device__ inline void scatter_block(const FaceNdc& fn, bool ok, int32_t face, const RasterOptions& o, uint64_t* keys) {
+	__shared__ uint64_t s_keys[SCATTER_LDS_KEYS];
+	__shared__ int s_box[4];
+	int u0 = 0, u1 = -1, v0 = 0, v1 = -1;
+	if (ok) ok = face_pixel_range(fn, o, u0, u1, v0, v1);
+	if (threadIdx.x == 0) {
+		s_box[0] = 0x7fffffff;
+		s_box[1] = -1;
+		s_box[2] = 0x7fffffff;
+		s_box[3] = -1;
+	}
+	__syncthreads();
+	if (ok) {
+		atomicMin(&s_box[0], u0);
+		atomicMax(&s_box[1], u1);
+		atomicMin(&s_box[2], v0);
+		atomicMax(&s_box[3], v1);
+	}
+	__syncthreads();
+	const int bu0 = s_box[0], bv0 = s_box[2];
+	const int bw = s_box[1] - bu0 + 1, bh = s_box[3] - bv0 + 1;
+	if (bw <= 0 || bh <= 0) return;   // uniform: no face of this workgroup covers a pixel
+	const bool staged = bw * bh <= SCATTER_LDS_KEYS;
+	if (staged) {
+		for (int i = threadIdx.x; i < bw * bh; i += SCATTER_BLOCK) s_keys[i] = EMPTY_KEY;
+		__syncthreads();
+	}
+	// A13: the blur radius is compared against SQUARED NDC distances, so for a face whose blur-widened box has a squared
+	// diagonal well below the radius every pixel in the box passes the distance test: skip computing it.
+	bool near_all = false;
+	if (ok) {
+		const float w = (fmax3f(fn.x[0], fn.x[1], fn.x[2]) - fmin3f(fn.x[0], fn.x[1], fn.x[2])) + 2.f * o.blur;
+		const float hh = (fmax3f(fn.y[0], fn.y[1], fn.y[2]) - fmin3f(fn.y[0], fn.y[1], fn.y[2])) + 2.f * o.blur;
+		near_all = (w * w + hh * hh) < 0.5f * o.blur;
+	}
+	if (ok) {
+		for (int v = v0; v <= v1; v++) {
+			const float py = pixel_to_ndc(v, o.H, o.W);
+			for (int u = u0; u <= u1; u++) {
+				const float px = pixel_to_ndc(u, o.W, o.H);
+				RasterHit h;
+				const bool hit = near_all ? face_test<false>(fn, px, py, o.blur, o.perspective, o.clip_barycentric, o.cull_back_faces, h)
+				                          : face_test<true>(fn, px, py, o.blur, o.perspective, o.clip_barycentric, o.cull_back_faces, h);
+				if (!hit) continue;
+				const unsigned long long key = raster_key(h.depth, face);
+				if (staged)
+					__hip_atomic_fetch_min(reinterpret_cast<unsigned long long*>(s_keys + (v - bv0) * bw + (u - bu0)), key, __ATOMIC_RELAXED,
+					                       __HIP_MEMORY_SCOPE_WORKGROUP);
+				else
+					atomicMin(reinterpret_cast<unsigned long long*>(keys + static_cast<int64_t>(v) * o.W + u), key);
+			}
 		}
+	}
+	if (!staged) return;
+	__syncthreads();
+	for (int i = threadIdx.x; i < bw * bh; i += SCATTER_BLOCK) {
+		const uint64_t k = s_keys[i];
+		if (k == EMPTY_KEY) continue;
+		const int64_t p = static_cast<int64_t>(bv0 + i / bw) * o.W + bu0 + i % bw;
+		atomicMin(reinterpret_cast<unsigned long long*>(keys + p), static_cast<unsigned long long>(k));
 	}
 }
 
-__global__ __launch_bounds__(256) void k_raster_scatter_ndc(const float* __restrict__ face_ndc, const uint8_t* __restrict__ mask, int64_t F,
-                                                            RasterOptions o, uint64_t* __restrict__ keys) {
+__global__ __launch_bounds__(SCATTER_BLOCK) void k_raster_scatter_ndc(const float* __restrict__ face_ndc, const uint8_t* __restrict__ mask,
+                                                                      int64_t F, RasterOptions o, uint64_t* __restrict__ keys) {
 	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-	if (f >= F) return;
-	if (mask && !mask[f]) return;
-	scatter_face(load_face_ndc(face_ndc, f), static_cast<int32_t>(f), o, keys);
+	FaceNdc fn{};
+	bool ok = f < F && !(mask && !mask[f]);
+	if (ok) fn = load_face_ndc(face_ndc, f);
+	scatter_block(fn, ok, static_cast<int32_t>(f), o, keys);
 }
 
 nnrt_status launch_raster_scatter_ndc(const float* face_ndc, const uint8_t* mask, int64_t F, const RasterOptions& o, uint64_t* keys,
                                       hipStream_t stream) {
 	if (F == 0) return NNRT_OK;
-	k_raster_scatter_ndc<<<static_cast<unsigned>(ceil_div(F, 256)), 256, 0, stream>>>(face_ndc, mask, F, o, keys);
+	k_raster_scatter_ndc<<<static_cast<unsigned>(ceil_div(F, SCATTER_BLOCK)), SCATTER_BLOCK, 0, stream>>>(face_ndc, mask, F, o, keys);
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;
 }
@@ -92,20 +161,19 @@ __device__ inline bool project_mesh_face(const float4* __restrict__ wpos, int4 f
 	return inlier;
 }
 
-__global__ __launch_bounds__(256) void k_raster_scatter_mesh(const float4* __restrict__ wpos, const int4* __restrict__ faces4, int64_t F,
-                                                             NdcSetup s, float near_clip, float far_clip, RasterOptions o,
-                                                             uint64_t* __restrict__ keys) {
+__global__ __launch_bounds__(SCATTER_BLOCK) void k_raster_scatter_mesh(const float4* __restrict__ wpos, const int4* __restrict__ faces4,
+                                                                       int64_t F, NdcSetup s, float near_clip, float far_clip, RasterOptions o,
+                                                                       uint64_t* __restrict__ keys) {
 	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-	if (f >= F) return;
-	FaceNdc fn;
-	if (!project_mesh_face(wpos, faces4[f], s, near_clip, far_clip, fn)) return;
-	scatter_face(fn, static_cast<int32_t>(f), o, keys);
+	FaceNdc fn{};
+	const bool ok = f < F && project_mesh_face(wpos, faces4[f], s, near_clip, far_clip, fn);
+	scatter_block(fn, ok, static_cast<int32_t>(f), o, keys);
 }
 
 nnrt_status launch_raster_scatter_mesh(const float4* wpos, const int4* faces4, int64_t F, const NdcSetup& s, float near_clip, float far_clip,
                                        const RasterOptions& o, uint64_t* keys, hipStream_t stream) {
 	if (F == 0) return NNRT_OK;
-	k_raster_scatter_mesh<<<static_cast<unsigned>(ceil_div(F, 256)), 256, 0, stream>>>(wpos, faces4, F, s, near_clip, far_clip, o, keys);
+	k_raster_scatter_mesh<<<static_cast<unsigned>(ceil_div(F, SCATTER_BLOCK)), SCATTER_BLOCK, 0, stream>>>(wpos, faces4, F, s, near_clip, far_clip, o, keys);
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;
 }
