@@ -63,6 +63,10 @@ _SIGNATURES = {
                                            c_int32, c_int32, c_void_p, c_void_p, c_float, c_void_p]),
     "nnrt_fitter_prepare": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                       c_int32, c_int32, c_void_p, c_void_p, c_float, c_void_p]),
+    "nnrt_fitter_prepare_point_cloud": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
+                                                  c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
+    "nnrt_fitter_fit_to_point_cloud": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
+                                                 c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
     "nnrt_fitter_iterate": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "nnrt_fitter_iterate_timed": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     "nnrt_fitter_check": (c_int32, [c_void_p, c_void_p]),

@@ -331,7 +331,7 @@ struct nnrt_fitter {
 	DeviceBuffer<int32_t> anchors;
 	DeviceBuffer<float> weights;
 	DeviceBuffer<float4> wpos, wnrm, jv, jn;
-	DeviceBuffer<float> ref_depth;
+	DeviceBuffer<float4> ref_points;   // [P] reference point (x, y, z, valid)
 	DeviceBuffer<uint64_t> keys;
 	DeviceBuffer<float> residuals;
 	DeviceBuffer<uint8_t> residual_mask;
@@ -360,13 +360,26 @@ struct nnrt_fitter {
 
 namespace {
 
-__global__ void k_prepare_reference(const float* __restrict__ depth, const uint8_t* __restrict__ mask, int64_t P, float scale, float max_depth,
-                                    float* __restrict__ out) {
+// depth overload (DeformableMeshToImageFitter.cpp:278-314): UnprojectDepthImageWithoutFiltering with the pixel intrinsics
+// (PerspectiveProjectionImpl.h:60-146): d = depth / scale, valid iff 0 < d < max_depth (AND the optional image mask)
+__global__ void k_prepare_reference_depth(const float* __restrict__ depth, const uint8_t* __restrict__ mask, int H, int W, float scale,
+                                          float max_depth, Camera pix, float4* __restrict__ out) {
 	const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-	if (i >= P) return;
+	if (i >= static_cast<int64_t>(H) * W) return;
+	const int u = static_cast<int>(i % W), v = static_cast<int>(i / W);
 	const float d = depth[i] / scale;
 	const bool valid = d > 0 && d < max_depth && (mask == nullptr || mask[i] != 0);
-	out[i] = valid ? d : 0.f;
+	out[i] = valid ? make_float4((static_cast<float>(u) - pix.cx) * d / pix.fx, (static_cast<float>(v) - pix.cy) * d / pix.fy, d, 1.f)
+	               : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// point-cloud overload (:85-95): organized reference points [P,3] and their mask
+__global__ void k_prepare_reference_points(const float* __restrict__ points, const uint8_t* __restrict__ mask, int64_t P,
+                                           float4* __restrict__ out) {
+	const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (i >= P) return;
+	const bool valid = mask == nullptr || mask[i] != 0;
+	out[i] = valid ? make_float4(points[3 * i], points[3 * i + 1], points[3 * i + 2], 1.f) : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 __global__ void k_faces_to_int4(const int64_t* __restrict__ faces, int64_t F, int4* __restrict__ out) {
@@ -410,7 +423,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 	fa.anchors = ft->anchors.ptr;
 	fa.jv = ft->jv.ptr;
 	fa.jn = ft->jn.ptr;
-	fa.ref_depth = ft->ref_depth.ptr;
+	fa.ref_points = ft->ref_points.ptr;
 	fa.residuals = ft->residuals.ptr;
 	fa.residual_mask = ft->residual_mask.ptr;
 	fa.pixel_face = ft->pixel_face.ptr;
@@ -508,7 +521,8 @@ void nnrt_fitter_destroy(nnrt_fitter* ft) {
 	hipStreamSynchronize(ft->work);
 	ft->drop_graphs();
 	ft->acc.release();
-	for (auto* b : {&ft->mesh_p, &ft->mesh_n, &ft->weights, &ft->ref_depth, &ft->residuals, &ft->arap_acc, &ft->updates, &ft->gradient,
+	ft->ref_points.release();
+	for (auto* b : {&ft->mesh_p, &ft->mesh_n, &ft->weights, &ft->residuals, &ft->arap_acc, &ft->updates, &ft->gradient,
 	                &ft->hessian, &ft->wing, &ft->edge_residuals, &ft->a_diag, &ft->a_dinv, &ft->a_dinvb, &ft->a_schur, &ft->a_rhs, &ft->a_x})
 		b->release();
 	ft->faces4.release();
@@ -529,13 +543,22 @@ void nnrt_fitter_destroy(nnrt_fitter* ft) {
 	delete ft;
 }
 
-nnrt_status nnrt_fitter_prepare(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_vertices, const float* d_normals, int64_t V,
-                                const int64_t* d_faces, int64_t F, const float* d_depth, const uint8_t* d_mask, int32_t H, int32_t W,
-                                const double* h_K, const double* h_E, float depth_scale, void* stream) {
-	NNRT_CHECK_ARG(ft && wf && d_vertices && d_normals && d_faces && d_depth && h_K, "null pointer");
+namespace {
+// reference input of one frame: either a depth image (+ scale) or an organized point cloud, with an optional mask
+struct FrameReference {
+	const float* depth = nullptr;
+	const float* points = nullptr;
+	const uint8_t* mask = nullptr;
+	float depth_scale = 1.f;
+};
+
+nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_vertices, const float* d_normals, int64_t V,
+                          const int64_t* d_faces, int64_t F, const FrameReference& ref, int32_t H, int32_t W, const double* h_K,
+                          const double* h_E, void* stream) {
+	NNRT_CHECK_ARG(ft && wf && d_vertices && d_normals && d_faces && (ref.depth || ref.points) && h_K, "null pointer");
 	NNRT_CHECK_ARG(V > 0 && F > 0 && H > 0 && W > 0, "empty mesh or image");
 	NNRT_CHECK_ARG(V < (int64_t(1) << 31) && F < (int64_t(1) << 31), "mesh too large for int32 indexing");
-	NNRT_CHECK_ARG(depth_scale > 0.f, "depth_scale must be positive");
+	NNRT_CHECK_ARG(ref.depth_scale > 0.f, "depth_scale must be positive");
 	DeviceGuard guard(ft->device);
 	hipStream_t us = static_cast<hipStream_t>(stream);
 	const int64_t P = static_cast<int64_t>(H) * W;
@@ -553,7 +576,7 @@ nnrt_status nnrt_fitter_prepare(nnrt_fitter* ft, nnrt_warp_field* wf, const floa
 	if ((st = ft->mesh_p.ensure(3 * V)) || (st = ft->mesh_n.ensure(3 * V)) || (st = ft->faces4.ensure(F)) ||
 	    (st = ft->anchors.ensure(static_cast<size_t>(V) * K)) || (st = ft->weights.ensure(static_cast<size_t>(V) * K)) ||
 	    (st = ft->wpos.ensure(V)) || (st = ft->wnrm.ensure(V)) || (st = ft->jv.ensure(static_cast<size_t>(V) * K)) ||
-	    (st = ft->jn.ensure(static_cast<size_t>(V) * K)) || (st = ft->ref_depth.ensure(P)) || (st = ft->keys.ensure(P)) ||
+	    (st = ft->jn.ensure(static_cast<size_t>(V) * K)) || (st = ft->ref_points.ensure(P)) || (st = ft->keys.ensure(P)) ||
 	    (st = ft->residuals.ensure(P)) || (st = ft->residual_mask.ensure(P)) || (st = ft->pixel_face.ensure(P)) ||
 	    (st = ft->acc.ensure(static_cast<size_t>(N) * ACC_STRIDE)) || (st = ft->arap_acc.ensure(static_cast<size_t>(N) * ACC_STRIDE)) ||
 	    (st = ft->updates.ensure(static_cast<size_t>(N) * 6)) || (st = ft->gradient.ensure(static_cast<size_t>(N) * 6)) ||
@@ -625,8 +648,11 @@ nnrt_status nnrt_fitter_prepare(nnrt_fitter* ft, nnrt_warp_field* wf, const floa
 	                                 wf->threshold ? wf->minimum_valid : 0, ft->anchors.ptr, ft->weights.ptr, s)))
 		return st;
 	// reference point cloud (:289-306): depth / scale with 0 < d < max_depth, AND the user mask; stored as depth (0 = masked)
-	k_prepare_reference<<<static_cast<unsigned>(ceil_div(P, 256)), 256, 0, s>>>(d_depth, d_mask, P, depth_scale, ft->p.max_depth,
-	                                                                            ft->ref_depth.ptr);
+	if (ref.depth)
+		k_prepare_reference_depth<<<static_cast<unsigned>(ceil_div(P, 256)), 256, 0, s>>>(ref.depth, ref.mask, H, W, ref.depth_scale,
+		                                                                                  ft->p.max_depth, ft->pix, ft->ref_points.ptr);
+	else
+		k_prepare_reference_points<<<static_cast<unsigned>(ceil_div(P, 256)), 256, 0, s>>>(ref.points, ref.mask, P, ft->ref_points.ptr);
 	NNRT_LAUNCH_CHECK();
 	NNRT_HIP(hipMemsetAsync(ft->keys.ptr, 0xff, sizeof(uint64_t) * P, s));
 	NNRT_HIP(hipMemsetAsync(ft->acc.ptr, 0, sizeof(double) * N * ACC_STRIDE, s));
@@ -636,6 +662,28 @@ nnrt_status nnrt_fitter_prepare(nnrt_fitter* ft, nnrt_warp_field* wf, const floa
 	ft->prepared = true;
 	return NNRT_OK;
 }
+} // namespace
+
+nnrt_status nnrt_fitter_prepare(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_vertices, const float* d_normals, int64_t V,
+                                const int64_t* d_faces, int64_t F, const float* d_depth, const uint8_t* d_mask, int32_t H, int32_t W,
+                                const double* h_K, const double* h_E, float depth_scale, void* stream) {
+	FrameReference ref;
+	ref.depth = d_depth;
+	ref.mask = d_mask;
+	ref.depth_scale = depth_scale;
+	NNRT_CHECK_ARG(d_depth, "null depth image");
+	return prepare_frame(ft, wf, d_vertices, d_normals, V, d_faces, F, ref, H, W, h_K, h_E, stream);
+}
+
+nnrt_status nnrt_fitter_prepare_point_cloud(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_vertices, const float* d_normals,
+                                            int64_t V, const int64_t* d_faces, int64_t F, const float* d_points, const uint8_t* d_point_mask,
+                                            int32_t H, int32_t W, const double* h_K, const double* h_E, void* stream) {
+	FrameReference ref;
+	ref.points = d_points;
+	ref.mask = d_point_mask;
+	NNRT_CHECK_ARG(d_points, "null reference point cloud");
+	return prepare_frame(ft, wf, d_vertices, d_normals, V, d_faces, F, ref, H, W, h_K, h_E, stream);
+}
 
 nnrt_status nnrt_fitter_iterate(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_iteration, int32_t count, void* stream) {
 	NNRT_CHECK_ARG(ft && wf, "null pointer");
@@ -644,10 +692,9 @@ nnrt_status nnrt_fitter_iterate(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t fi
 		return NNRT_ERROR_ARGUMENT;
 	}
 	DeviceGuard guard(ft->device);
+	// Iterations run on the caller's stream (no cross-stream handshake per call). Graphs are captured once per
+	// iteration mode on the fitter's private stream (capture needs a non-legacy stream) and replayed on the caller's.
 	hipStream_t us = static_cast<hipStream_t>(stream);
-	NNRT_HIP(hipEventRecord(ft->ev_in, us));
-	NNRT_HIP(hipStreamWaitEvent(ft->work, ft->ev_in, 0));
-	hipStream_t s = ft->work;
 	nnrt_status st;
 	for (int it = first_iteration; it < first_iteration + count; it++) {
 		const int mode = ft->p.iteration_modes[it % ft->p.iteration_mode_count];
@@ -655,9 +702,9 @@ nnrt_status nnrt_fitter_iterate(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t fi
 		if (ft->p.use_hip_graph) {
 			if (!ft->graph[mode]) {
 				hipGraph_t g = nullptr;
-				NNRT_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-				st = enqueue_iteration(ft, wf, mode, s);
-				hipError_t ce = hipStreamEndCapture(s, &g);
+				NNRT_HIP(hipStreamBeginCapture(ft->work, hipStreamCaptureModeThreadLocal));
+				st = enqueue_iteration(ft, wf, mode, ft->work);
+				hipError_t ce = hipStreamEndCapture(ft->work, &g);
 				if (st) {
 					if (g) hipGraphDestroy(g);
 					return st;
@@ -667,13 +714,11 @@ nnrt_status nnrt_fitter_iterate(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t fi
 				hipGraphDestroy(g);
 				NNRT_HIP(ie);
 			}
-			NNRT_HIP(hipGraphLaunch(ft->graph[mode], s));
+			NNRT_HIP(hipGraphLaunch(ft->graph[mode], us));
 		} else {
-			if ((st = enqueue_iteration(ft, wf, mode, s))) return st;
+			if ((st = enqueue_iteration(ft, wf, mode, us))) return st;
 		}
 	}
-	NNRT_HIP(hipEventRecord(ft->ev_out, s));
-	NNRT_HIP(hipStreamWaitEvent(us, ft->ev_out, 0));
 	return NNRT_OK;
 }
 
@@ -740,6 +785,15 @@ nnrt_status nnrt_fitter_fit_to_image(nnrt_fitter* ft, nnrt_warp_field* wf, const
 	nnrt_status st = nnrt_fitter_prepare(ft, wf, d_vertices, d_normals, V, d_faces, F, d_depth, d_mask, H, W, h_K, h_E, depth_scale, stream);
 	if (st) return st;
 	// A14: the reference never updates `maximum_update`, so the loop always runs max_iteration_count iterations
+	if ((st = nnrt_fitter_iterate(ft, wf, 0, ft->p.max_iteration_count, stream))) return st;
+	return nnrt_fitter_check(ft, stream);
+}
+
+nnrt_status nnrt_fitter_fit_to_point_cloud(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_vertices, const float* d_normals, int64_t V,
+                                           const int64_t* d_faces, int64_t F, const float* d_points, const uint8_t* d_point_mask, int32_t H,
+                                           int32_t W, const double* h_K, const double* h_E, void* stream) {
+	nnrt_status st = nnrt_fitter_prepare_point_cloud(ft, wf, d_vertices, d_normals, V, d_faces, F, d_points, d_point_mask, H, W, h_K, h_E, stream);
+	if (st) return st;
 	if ((st = nnrt_fitter_iterate(ft, wf, 0, ft->p.max_iteration_count, stream))) return st;
 	return nnrt_fitter_check(ft, stream);
 }

@@ -192,10 +192,9 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_fit_pixels(FitPixelArgs a) {
 		if (rendered_valid) {
 			prast = make3((static_cast<float>(u) - a.pix.cx) * depth / a.pix.fx, (static_cast<float>(v) - a.pix.cy) * depth / a.pix.fy, depth);
 		}
-		const float dref = a.ref_depth[p];
-		f3 q = make3(0.f, 0.f, 0.f);
-		const bool ref_valid = dref > 0.f;
-		if (ref_valid) q = make3((static_cast<float>(u) - a.pix.cx) * dref / a.pix.fx, (static_cast<float>(v) - a.pix.cy) * dref / a.pix.fy, dref);
+		const float4 qr = a.ref_points[p];
+		const bool ref_valid = qr.w != 0.f;
+		const f3 q = make3(qr.x, qr.y, qr.z);
 		const bool mask = ref_valid && rendered_valid;
 		const f3 d = sub3(prast, q);   // point map vector w_l - o_l
 		float dist = dot3(nl, d);

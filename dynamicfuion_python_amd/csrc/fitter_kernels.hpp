@@ -24,7 +24,7 @@ struct FitPixelArgs {
 	const int32_t* anchors; // [V,K]
 	const float4* jv;       // [V,K] (-w R (v-g), w)
 	const float4* jn;       // [V,K] (-w R n, 0)
-	const float* ref_depth; // [P] reference depth / scale, 0 where the reference point is masked out
+	const float4* ref_points; // [P] reference point (x, y, z, valid)
 	float* residuals;       // [P]
 	uint8_t* residual_mask; // [P]
 	int32_t* pixel_face;    // [P]

@@ -78,6 +78,25 @@ class DeformableMeshToImageFitter:
         N.check(N.lib().nnrt_fitter_prepare(self._h, warp_field.handle, N.ptr(p), N.ptr(n), p.shape[0], N.ptr(f), f.shape[0], N.ptr(d), N.ptr(m),
                                             H, W, N.ptr(K), N.ptr(E), float(depth_scale), N.stream_ptr(stream)))
 
+    def prepare_point_cloud(self, warp_field: HierarchicalGraphWarpField, canonical_mesh: TriangleMesh, reference_point_cloud,
+                            reference_point_mask, intrinsic_matrix, extrinsic_matrix, rendering_image_size, stream=None):
+        """Once-per-frame setup of the point-cloud overload (DeformableMeshToImageFitter.cpp:85-106): organized reference
+        points [H*W,3] (or [H,W,3]) and their mask, rendered at rendering_image_size = (H, W)."""
+        N.require_gpu()
+        dev = self.device
+        p, n, f = canonical_mesh.on_device(dev)
+        H, W = int(rendering_image_size[0]), int(rendering_image_size[1])
+        q = to_device(reference_point_cloud, torch.float32, dev).reshape(-1, 3).contiguous()
+        if q.shape[0] != H * W:
+            raise ValueError(f"reference point cloud has {q.shape[0]} points, expected an organized cloud of {H}x{W}")
+        m = None if reference_point_mask is None else to_device(reference_point_mask, torch.uint8, dev).reshape(-1).contiguous()
+        K = to_host_f64(intrinsic_matrix)
+        E = None if extrinsic_matrix is None else to_host_f64(extrinsic_matrix)
+        self._frame = (p, n, f, q, m, K, E, H, W)
+        self._node_count = warp_field.node_count
+        N.check(N.lib().nnrt_fitter_prepare_point_cloud(self._h, warp_field.handle, N.ptr(p), N.ptr(n), p.shape[0], N.ptr(f), f.shape[0],
+                                                        N.ptr(q), N.ptr(m), H, W, N.ptr(K), N.ptr(E), N.stream_ptr(stream)))
+
     def iterate(self, warp_field: HierarchicalGraphWarpField, first_iteration: int = 0, count: int = 1, stream=None):
         N.check(N.lib().nnrt_fitter_iterate(self._h, warp_field.handle, int(first_iteration), int(count), N.stream_ptr(stream)))
 
@@ -90,11 +109,28 @@ class DeformableMeshToImageFitter:
     def check(self, stream=None):
         N.check(N.lib().nnrt_fitter_check(self._h, N.stream_ptr(stream)))
 
-    def fit_to_image(self, warp_field: HierarchicalGraphWarpField, canonical_mesh: TriangleMesh, reference_color_image,
-                     reference_depth_image, reference_image_mask, intrinsic_matrix, extrinsic_matrix=None, depth_scale: float = 1.0):
-        """FitToImage(warp_field, mesh, color, depth, mask, K, E, depth_scale) (DeformableMeshToImageFitter.cpp:278-314).
-        The color image is unused by the reference's fitter as well. Mutates the warp field."""
-        self.prepare(warp_field, canonical_mesh, reference_depth_image, reference_image_mask, intrinsic_matrix, extrinsic_matrix, depth_scale)
+    def fit_to_image(self, warp_field: HierarchicalGraphWarpField, canonical_mesh: TriangleMesh, *args):
+        """The three FitToImage overloads (DeformableMeshToImageFitter.h:58-90); all mutate the warp field in place:
+
+        * (warp_field, mesh, rgbd_image, reference_image_mask, K, E, depth_scale) -- rgbd_image has .color / .depth
+          (DeformableMeshToImageFitter.cpp:316-329);
+        * (warp_field, mesh, color, depth, reference_image_mask, K, E, depth_scale) (:278-314);
+        * (warp_field, mesh, color, reference_point_cloud, reference_point_mask, K, E, rendering_image_size) (:85-276).
+
+        The colour image is unused, as in the reference. A14: all max_iteration_count iterations run."""
+        if len(args) == 5 and hasattr(args[0], "depth"):
+            rgbd, mask, K, E, scale = args
+            self.prepare(warp_field, canonical_mesh, rgbd.depth, mask, K, E, scale)
+        elif len(args) == 6 and isinstance(args[5], (tuple, list, torch.Size)):
+            _color, points, mask, K, E, size = args
+            self.prepare_point_cloud(warp_field, canonical_mesh, points, mask, K, E, size)
+        elif len(args) in (5, 6):
+            _color, depth, mask, K = args[:4]
+            E = args[4] if len(args) > 4 else None
+            scale = args[5] if len(args) > 5 else 1.0
+            self.prepare(warp_field, canonical_mesh, depth, mask, K, E, scale)
+        else:
+            raise TypeError("fit_to_image: no overload matches the arguments (see DeformableMeshToImageFitter.h:58-90)")
         self.iterate(warp_field, 0, self.params.max_iteration_count)
         self.check()
 

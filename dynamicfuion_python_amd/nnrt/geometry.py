@@ -33,6 +33,13 @@ class TriangleMesh:
                 to_device(self.triangle_indices, torch.int64, device))
 
 
+@dataclass
+class RGBDImage:
+    """Stand-in for open3d.t.geometry.RGBDImage: colour [H,W,3] (unused by the fitter) and depth [H,W]."""
+    color: object
+    depth: object
+
+
 class HierarchicalGraphWarpField:
     """Device-resident warp field with a regularization hierarchy (virtual node order = fine-to-coarse layers)."""
 

@@ -112,13 +112,13 @@ class Scene:
     points: np.ndarray            # [V,3]
     normals: np.ndarray           # [V,3]
     faces: np.ndarray             # [F,3] int64
-    nodes: np.ndarray             # [N,3], virtual order (identity permutation)
+    nodes: np.ndarray             # [N,3] (original order; hierarchy["virtual_indices"] maps virtual -> original)
     coverage: float
     layer_count: int
     iterations: int
     gt_rotations: np.ndarray      # [N,3,3]
     gt_translations: np.ndarray   # [N,3]
-    hierarchy: dict = field(default_factory=dict)   # edges, edge_layers, radii, layer_counts (layer_count > 1)
+    hierarchy: dict = field(default_factory=dict)   # edges, edge_layers, radii, layer_counts, virtual_indices (layers > 1)
 
 
 def make_scene(name: str = "C2", seed: int = 0, hierarchy_builder=None) -> Scene:
@@ -132,14 +132,17 @@ def make_scene(name: str = "C2", seed: int = 0, hierarchy_builder=None) -> Scene
     hier = {}
     if layers > 1:
         if hierarchy_builder is None:
-            raise ValueError("multi-layer scenes need a hierarchy_builder to pre-sort nodes into virtual order")
-        for attempt in range(8):
+            raise ValueError("multi-layer scenes need a hierarchy_builder (virtual order and edges)")
+        # Pre-sort the nodes toward virtual order (identity permutation) where the hierarchy allows it. The median-grid
+        # subsample keeps each cell's medoid with ties going to the earlier node, so a two-member cell flips its medoid
+        # whenever the order changes; such scenes keep a non-identity virtual order (virtual_indices).
+        for attempt in range(4):
             vidx, counts, edges, elayers = hierarchy_builder(nodes, cov, layers)
             if np.array_equal(vidx, np.arange(len(nodes))):
                 break
-            nodes, uv, w, t = nodes[vidx], uv[vidx], w[vidx], t[vidx]
-        else:
-            raise RuntimeError("could not pre-sort nodes into an identity virtual order")
+            if attempt < 3:
+                nodes, uv, w, t = nodes[vidx], uv[vidx], w[vidx], t[vidx]
+        vidx, counts, edges, elayers = hierarchy_builder(nodes, cov, layers)
         radii = np.array([cov * (i + 1) for i in range(layers)], np.float32)
-        hier = dict(edges=edges, edge_layers=elayers, radii=radii, layer_counts=counts)
+        hier = dict(edges=edges, edge_layers=elayers, radii=radii, layer_counts=counts, virtual_indices=np.asarray(vidx, np.int64))
     return Scene(name, H, W, K, points, normals, faces, nodes, cov, layers, iters, rodrigues_np(w), t, hier)

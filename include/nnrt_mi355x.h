@@ -111,6 +111,18 @@ nnrt_status nnrt_fitter_prepare(nnrt_fitter* fitter, nnrt_warp_field* warp_field
                                 int64_t vertex_count, const int64_t* d_faces, int64_t face_count, const float* d_depth,
                                 const uint8_t* d_mask, int32_t height, int32_t width, const double* h_K, const double* h_E,
                                 float depth_scale, void* stream);
+/* FitToImage(warp_field, canonical_mesh, color, reference_point_cloud, reference_point_mask, K, E, rendering_image_size)
+ * (DeformableMeshToImageFitter.cpp:85-276, the overload the depth variant forwards to): d_points float32 [H*W,3]
+ * organized reference points, d_point_mask uint8 [H*W] or NULL (all valid), (height, width) = rendering image size. */
+nnrt_status nnrt_fitter_prepare_point_cloud(nnrt_fitter* fitter, nnrt_warp_field* warp_field, const float* d_vertices,
+                                            const float* d_normals, int64_t vertex_count, const int64_t* d_faces, int64_t face_count,
+                                            const float* d_points, const uint8_t* d_point_mask, int32_t height, int32_t width,
+                                            const double* h_K, const double* h_E, void* stream);
+nnrt_status nnrt_fitter_fit_to_point_cloud(nnrt_fitter* fitter, nnrt_warp_field* warp_field, const float* d_vertices,
+                                           const float* d_normals, int64_t vertex_count, const int64_t* d_faces, int64_t face_count,
+                                           const float* d_points, const uint8_t* d_point_mask, int32_t height, int32_t width,
+                                           const double* h_K, const double* h_E, void* stream);
+/* Iterations are enqueued on `stream` itself (graphs: captured once per iteration mode, replayed on `stream`). */
 nnrt_status nnrt_fitter_iterate(nnrt_fitter* fitter, nnrt_warp_field* warp_field, int32_t first_iteration, int32_t count, void* stream);
 /* iterate() without graphs, with HIP events between the stages of every iteration; h_stage_ms[5] receives the average
  * per-iteration device time of: 0 warp (+warped Jacobians), 1 raster scatter, 2 fused pixel kernel, 3 ARAP edges,

@@ -101,9 +101,12 @@ def oracle_fit_scene(O, sc, depth, iterations=1, lm=0.001, modes=("ALL",), **kw)
     t0 = np.zeros((N, 3), np.float32)
     h = sc.hierarchy
     hk = {}
+    nodes = sc.nodes
     if h:
+        # the fit runs in virtual node order (outputs are virtual-ordered too)
+        nodes = sc.nodes[h["virtual_indices"]]
         hk = dict(edges=h["edges"], edge_layers=h["edge_layers"], radii=h["radii"], first_layer_count=int(h["layer_counts"][0]))
     hk.update(kw)
-    return O.fit(nodes=sc.nodes, rotations=R0, translations=t0, mesh_points=sc.points, mesh_normals=sc.normals, faces=sc.faces,
+    return O.fit(nodes=nodes, rotations=R0, translations=t0, mesh_points=sc.points, mesh_normals=sc.normals, faces=sc.faces,
                  ref_points=refp, ref_mask=refm, H=sc.H, W=sc.W, K=sc.K, max_iterations=iterations, lm_factor=lm, modes=modes,
                  coverage=sc.coverage, **hk)

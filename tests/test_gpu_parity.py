@@ -2,8 +2,9 @@
 
 Tolerances: integer/index outputs (anchors, rasterized faces, masks) must be identical; the raster and warp stages are
 bit-identical by construction (same float expression order, -ffp-contract=off, transcendentals rounded once from
-double on both sides). Float reductions (JtJ / Jt r) are summed with atomics in a different order than the oracle, so
-they are compared at <= 1e-5 relative (Hessian) and the solved updates at <= 1e-4 relative (north_star tolerance).
+double on both sides). The data-term JtJ / Jt r sums are exact on both sides (float products summed in double: GPU
+wave/atomic order vs the oracle's serial order differ only in double rounding), so Hessian and gradient blocks are
+compared at <= 1e-6 relative and the solved updates / node motion at <= 1e-4 relative (north_star tolerance).
 """
 import os
 
@@ -220,8 +221,8 @@ def _compare_iteration(dg_o, dg_g, s, N):
     assert np.array_equal(dg_o["pixel_faces"].astype(np.int64), dg_g["pixel_faces"].astype(np.int64))
     assert np.array_equal(dg_o["residual_mask"], dg_g["residual_mask"])
     assert np.allclose(dg_o["residuals"], dg_g["residuals"], rtol=0, atol=1e-6)
-    assert rel_err(dg_g["hessian"][: N * s * s], dg_o["hessian_diag"]) < 1e-5
-    assert rel_err(dg_g["gradient"][: N * s], dg_o["gradient"]) < 1e-4
+    assert rel_err(dg_g["hessian"][: N * s * s], dg_o["hessian_diag"]) < 1e-6
+    assert rel_err(dg_g["gradient"][: N * s], dg_o["gradient"]) < 1e-6
     assert rel_err(dg_g["updates"][: N * s], dg_o["updates"]) < 1e-4
 
 
@@ -267,12 +268,13 @@ def test_fit_multi_iteration_parity(nn, S, oracle_mod):
     assert rel_err(wf.get_node_rotations(True) - np.eye(3), R_o - np.eye(3)) < 1e-3
 
 
-@pytest.mark.parametrize("name", ["S1_ARAP", "C1_ARAP"])
+@pytest.mark.parametrize("name", ["S1_ARAP", "C1_ARAP", "C2_ARAP", "C5"])
 def test_fit_arap_parity(nn, S, oracle_mod, name):
+    """layer_count 2 + ARAP: arrowhead (stem blocks + dense Schur corner) solve."""
     sc = _scene(S, oracle_mod, name)
     wf = nn.geometry.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, nn.geometry.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE,
                                                 sc.layer_count)
-    assert np.array_equal(wf.get_virtual_node_indices(), np.arange(len(sc.nodes)))
+    assert np.array_equal(wf.get_virtual_node_indices(), sc.hierarchy["virtual_indices"])
     assert np.array_equal(wf.get_edges(), sc.hierarchy["edges"])
     depth = scene_target(oracle_mod, sc)
     R_o, t_o, dg_o = oracle_fit_scene(oracle_mod, sc, depth, 1)
@@ -368,3 +370,43 @@ def test_errors_fail_loudly(nn, S, oracle_mod):
     sc.nodes = np.concatenate([sc.nodes, np.array([[5.0, 5.0, 5.0]], np.float32)])
     with pytest.raises(RuntimeError, match="positive-definite"):
         _gpu_fit(nn, sc, depth, 1, lm=0.0)
+
+
+def test_fit_point_cloud_overload_parity(nn, S, oracle_mod):
+    """FitToImage(warp_field, mesh, color, reference_point_cloud, mask, K, E, rendering_image_size)
+    (DeformableMeshToImageFitter.cpp:85-276) with a reference cloud that is NOT an unprojected depth image."""
+    sc = _scene(S, oracle_mod, "S1")
+    depth = scene_target(oracle_mod, sc)
+    refp, refm = oracle_mod.unproject(depth, sc.K, 1.0, 10.0)
+    rng = np.random.default_rng(3)
+    pts = (refp + rng.normal(scale=1e-3, size=refp.shape)).astype(np.float32)
+    mask = (refm.astype(bool) & (rng.random(len(refm)) > 0.1)).astype(np.uint8)
+    N = len(sc.nodes)
+    R_o, t_o, dg_o = oracle_mod.fit(nodes=sc.nodes, rotations=np.tile(np.eye(3, dtype=np.float32), (N, 1, 1)),
+                                    translations=np.zeros((N, 3), np.float32), mesh_points=sc.points, mesh_normals=sc.normals,
+                                    faces=sc.faces, ref_points=pts, ref_mask=mask, H=sc.H, W=sc.W, K=sc.K, max_iterations=1,
+                                    lm_factor=0.001, coverage=sc.coverage)
+    G, A = nn.geometry, nn.alignment
+    wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE, 1)
+    ft = A.DeformableMeshToImageFitter(1, [A.IterationMode.ALL], preconditioning_dampening_factor=0.001)
+    ft.fit_to_image(wf, G.TriangleMesh(sc.points, sc.normals, sc.faces), None, pts, mask, sc.K, None, (sc.H, sc.W))
+    _compare_iteration(dg_o, ft.diagnostics(), 6, N)
+    assert rel_err(wf.get_node_translations(True), t_o) < 1e-4
+
+
+def test_fit_rgbd_overload_matches_depth_overload(nn, S, oracle_mod):
+    sc = _scene(S, oracle_mod, "S1")
+    depth = scene_target(oracle_mod, sc)
+    G, A = nn.geometry, nn.alignment
+    mesh = G.TriangleMesh(sc.points, sc.normals, sc.faces)
+    out = []
+    for use_rgbd in (False, True):
+        wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE, 1)
+        ft = A.DeformableMeshToImageFitter(1, [A.IterationMode.ALL], preconditioning_dampening_factor=0.001)
+        if use_rgbd:
+            ft.fit_to_image(wf, mesh, G.RGBDImage(None, depth * 1000.0), None, sc.K, None, 1000.0)
+        else:
+            ft.fit_to_image(wf, mesh, None, depth, None, sc.K, None, 1.0)
+        out.append(ft.diagnostics())
+    assert np.array_equal(out[0]["pixel_faces"], out[1]["pixel_faces"])
+    assert rel_err(out[1]["updates"], out[0]["updates"]) < 1e-4
