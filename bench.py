@@ -55,26 +55,54 @@ def aggregate(steps: int, elapsed_s: float, world: int) -> dict:
 
 
 # ---------------------------------------------------------------------------------------------------------------------
-# algorithmic bytes (DESIGN.md "Kernels and rooflines")
+# algorithmic bytes: SURVEY.md 8(d) "Algorithmic bytes per GN iteration" (compulsory traffic at the reference's stage
+# boundaries, fp32 values, int32 indices, 1-byte masks), mode ALL, no ARAP rows for the block-diagonal configs.
+# P pixels, V vertices, F faces, N nodes, K anchors, E pixel-node associations (counted from the run).
 # ---------------------------------------------------------------------------------------------------------------------
-def fit_pixels_bytes(P: int, F: int, V: int, N: int, anchor_count: int, nacc: int = 27) -> int:
-    """Compulsory HBM bytes of one k_fit_pixels launch: per pixel the raster key (8 B read + 8 B reset), the reference
-    depth (4 B), residual (4 B), residual mask (1 B), rasterized face (4 B); every face record once (int4, 16 B); per
-    vertex its warped position + normal (2 x float4), anchors (4 B x K) and warped Jacobians (2 x float4 x K); per node
-    the accumulator row (nacc floats, read + write)."""
-    per_pixel = 8 + 8 + 4 + 4 + 1 + 4
-    per_vertex = 16 + 16 + anchor_count * (4 + 16 + 16)
-    return P * per_pixel + F * 16 + V * per_vertex + N * nacc * 4 * 2
+def stage_bytes(P: int, F: int, V: int, N: int, K: int, E: int) -> dict:
+    return {
+        "warp": V * (48 + 8 * K) + 60 * N,
+        "ndc": F * (12 + 36 + 37),
+        "raster": F * 72 + P * 24,
+        "residual": P * 58 + F * 36,
+        "warped_jacobians": V * (24 + 8 * K + 28 * K),
+        "rasterized_jacobians": P * 244 + F * 72,
+        "pixel_anchor_jacobians": P * 257 + P * 72 * K + 4 * E,
+        "jtj_jtr": E * 28 + P * 5 + 168 * N,
+        "solve": 144 * N + 48 * N,   # block-diagonal: n0 = N, no wing blocks, no dense corner
+    }
 
 
-def iteration_bytes(P: int, F: int, V: int, N: int, anchor_count: int) -> int:
-    """Compulsory bytes of the whole iteration (all kernels): warp (read canonical mesh 24 B/vertex, anchors+weights,
-    node state; write float4 position/normal + Jacobians), raster scatter (face record + warped vertices, one 8 B
-    atomicMin per covered pixel ~ P), k_fit_pixels (above), solve (accumulator + node state)."""
-    warp = V * (24 + anchor_count * 8 + 32 + anchor_count * 32) + N * 64
-    scatter = F * 16 + V * 16 + P * 8
-    solve = N * (27 * 4 * 2 + 64 * 2)
-    return warp + scatter + fit_pixels_bytes(P, F, V, N, anchor_count) + solve
+# stages fused into each kernel of one GN iteration
+KERNEL_STAGES = {
+    "k_warp_mesh": ("warp", "warped_jacobians"),
+    "k_raster_scatter_mesh": ("ndc", "raster"),
+    "k_fit_pixels": ("residual", "rasterized_jacobians", "pixel_anchor_jacobians", "jtj_jtr"),
+    "k_solve_update": ("solve",),
+}
+
+
+def kernel_bytes(kernel: str, sb: dict) -> int:
+    return sum(sb[k] for k in KERNEL_STAGES[kernel])
+
+
+def fused_compulsory_bytes(P: int, F: int, V: int, N: int, K: int) -> int:
+    """What k_fit_pixels itself must move: per pixel the raster key (8 B read + 8 B reset), the reference
+    point (float4), residual, mask and face (9 B); each face record once (int4); per vertex warped position + normal
+    (2 x float4), anchors (4 B x K) and warped Jacobians (2 x float4 x K); per node the fp64 accumulator row (27 x 8 B
+    read-modify-write)."""
+    return P * (16 + 16 + 9) + F * 16 + V * (32 + K * 36) + N * 27 * 8 * 2
+
+
+def count_associations(pixel_faces, residual_mask, faces, anchors) -> int:
+    """E = sum over pixels with a residual of the unique anchor nodes of the rasterized face's vertices."""
+    import numpy as np
+    sel = residual_mask.astype(bool) & (pixel_faces >= 0)
+    f = pixel_faces[sel].astype(np.int64)
+    nodes = anchors[faces[f]].reshape(len(f), -1)
+    nodes = np.sort(nodes, axis=1)
+    uniq = (nodes >= 0) & np.concatenate([np.ones((len(f), 1), bool), nodes[:, 1:] != nodes[:, :-1]], axis=1)
+    return int(uniq.sum())
 
 
 # ---------------------------------------------------------------------------------------------------------------------
@@ -230,9 +258,13 @@ def main(argv=None):
     if not (np.isfinite(dg["updates"]).all() and np.abs(dg["updates"]).max() > 0):
         raise SystemExit("non-finite or empty GN update in the timed configuration")
 
-    kbytes = fit_pixels_bytes(P, F, V, Nn, 4)
+    anchors, _ = ft.anchors(V, 4)
+    E = count_associations(dg["pixel_faces"], dg["residual_mask"], sc.faces, anchors)
+    sb = stage_bytes(P, F, V, Nn, 4, E)
+    kbytes = kernel_bytes(ROOFLINE_KERNEL, sb)
     k_ms = stages["pixels"]
     achieved = kbytes / (k_ms * 1e-3) / 1e9
+    it_bytes = sum(sb.values())
     traffic, traffic_src = load_traffic(args.traffic_file, workload)
 
     out = {
@@ -255,9 +287,11 @@ def main(argv=None):
         "stage_ms": {k: round(v, 5) for k, v in stages.items()},
         "roofline": {"kernel": ROOFLINE_KERNEL, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "algorithmic_bytes": kbytes, "kernel_ms": k_ms,
-                     "traffic_source": traffic_src,
-                     "iteration_algorithmic_bytes": iteration_bytes(P, F, V, Nn, 4),
-                     "iteration_frac": iteration_bytes(P, F, V, Nn, 4) / (agg["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                     "bytes_formula": "SURVEY.md 8(d): residual + rasterized Jacobians + pixel-anchor Jacobians + JtJ/Jtr rows",
+                     "associations_E": E, "traffic_source": traffic_src,
+                     "fused_compulsory_bytes": fused_compulsory_bytes(P, F, V, Nn, 4),
+                     "iteration_algorithmic_bytes": it_bytes,
+                     "iteration_frac": it_bytes / (agg["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

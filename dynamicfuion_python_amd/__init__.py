@@ -7,4 +7,4 @@ Layout:
   alignment/       mirror of alignment/render_based/RenderingAlignmentOptimizer (the reference's Python API slot)
   synthetic.py     synthetic scenes for the BASELINE configs (C1-C5)
 """
-__all__ = ["nnrt", "synthetic"]
+__all__ = ["nnrt", "alignment", "synthetic"]

@@ -59,6 +59,7 @@ class HierarchicalGraphWarpField:
         self.node_count = len(nodes_np)
         self.anchor_count = anchor_count
         self.node_coverage = node_coverage
+        self.minimum_valid_anchor_count = minimum_valid_anchor_count
         self.warp_node_coverage_computation_method = WarpNodeCoverageComputationMethod(warp_node_coverage_computation_method)
 
     def __del__(self):
@@ -103,6 +104,31 @@ class HierarchicalGraphWarpField:
         R = self.get_node_rotations(use_virtual_ordering)
         self.set_node_rotations(np.einsum("nij,njk->nik", R, np.asarray(deltas, np.float32)), use_virtual_ordering)
 
+    def reset_rotations(self):
+        """WarpField::ResetRotations (cpp/geometry/WarpField.cpp:151-156): identity rotations, translations kept."""
+        self.set_node_rotations(np.tile(np.eye(3, dtype=np.float32), (self.node_count, 1, 1)))
+
+    def get_warped_nodes(self) -> np.ndarray:
+        """WarpField::GetWarpedNodes: node positions + translations (original order)."""
+        return self.get_node_positions() + self.get_node_translations()
+
+    def warp_mesh(self, input_mesh: "TriangleMesh", anchors=None, anchor_weights=None, disable_neighbor_thresholding: bool = True,
+                  extrinsics=None) -> "TriangleMesh":
+        """GraphWarpField.warp_mesh, both overloads (cpp/pybind/geometry/geometry.cpp:293-302 -> WarpField.cpp:129-144):
+        anchors are computed over the original-order nodes unless supplied."""
+        nodes = self.get_node_positions()
+        if anchors is None:
+            p, _, _ = input_mesh.on_device(_dev())
+            min_valid = 0 if disable_neighbor_thresholding else self.minimum_valid_anchor_count
+            if self.warp_node_coverage_computation_method == WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE:
+                anchors, anchor_weights = _anchors(p, nodes, self.anchor_count, self.node_coverage, None, min_valid)
+            else:
+                weights = np.empty(self.node_count, np.float32)
+                weights[self.get_virtual_node_indices()] = self.get_node_coverage_weights()
+                anchors, anchor_weights = _anchors(p, nodes, self.anchor_count, 0.0, weights, min_valid)
+        return warp_triangle_mesh(input_mesh, nodes, self.get_node_rotations(), self.get_node_translations(), anchors, anchor_weights,
+                                  extrinsics)
+
     def reset_motion(self, stream=None):
         """R = I, t = 0 for every node (device side, asynchronous on `stream`)."""
         N.check(N.lib().nnrt_warp_field_reset_motion(self._h, N.stream_ptr(stream)))
@@ -140,7 +166,7 @@ class HierarchicalGraphWarpField:
 
 
 def GraphWarpField(nodes, node_coverage=0.05, threshold_nodes_by_distance=False, anchor_count=4, minimum_valid_anchor_count=0,
-                   device: int = 0):
+                   device: int | None = None):
     """GraphWarpField (= WarpField, cpp/pybind/geometry/geometry.cpp:278-320): a single-layer field (no edges)."""
     return HierarchicalGraphWarpField(nodes, node_coverage, threshold_nodes_by_distance, anchor_count, minimum_valid_anchor_count,
                                       WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE, layer_count=1, device=device)

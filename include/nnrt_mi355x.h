@@ -68,7 +68,7 @@ nnrt_status nnrt_warp_field_get_node_rotations(const nnrt_warp_field* warp_field
 nnrt_status nnrt_warp_field_get_node_translations(const nnrt_warp_field* warp_field, float* h_out, int32_t virtual_order);
 nnrt_status nnrt_warp_field_set_node_rotations(nnrt_warp_field* warp_field, const float* h_in, int32_t virtual_order);
 nnrt_status nnrt_warp_field_set_node_translations(nnrt_warp_field* warp_field, const float* h_in, int32_t virtual_order);
-/* Resets every node to the identity motion (R = I, t = 0; WarpField::ResetRotations, WarpField.cpp:151-156) on `stream`. */
+/* Resets every node to the identity motion on `stream`: R = I (as WarpField::ResetRotations, WarpField.cpp:151-156) and t = 0. */
 nnrt_status nnrt_warp_field_reset_motion(nnrt_warp_field* warp_field, void* stream);
 /* node coverage weights (MINIMAL_K_NEIGHBOR_NODE_DISTANCE, WarpField.cpp:249-263), virtual order */
 nnrt_status nnrt_warp_field_get_node_coverage_weights(const nnrt_warp_field* warp_field, float* h_out);

@@ -63,7 +63,20 @@ def test_single_process_helpers():
 
 
 def test_algorithmic_bytes_c2():
-    # C2: 640x480, 153,600 triangles, 77,361 vertices, 1500 nodes, 4 anchors
-    b = bench.fit_pixels_bytes(640 * 480, 153600, 77361, 1500, 4)
-    assert b == 307200 * 29 + 153600 * 16 + 77361 * 176 + 1500 * 216
-    assert bench.iteration_bytes(640 * 480, 153600, 77361, 1500, 4) > b
+    # SURVEY.md 8(d) worked example: C2 (P = 307,200, V = 77,361, F = 153,600, K = 4, E ~ 1.4 M, N = 1500) ~ 374 MB
+    sb = bench.stage_bytes(640 * 480, 153600, 77361, 1500, 4, 1_400_000)
+    total = sum(sb.values())
+    assert 330e6 < total < 400e6
+    assert sb["pixel_anchor_jacobians"] == 307200 * 257 + 307200 * 72 * 4 + 4 * 1_400_000
+    k = bench.kernel_bytes("k_fit_pixels", sb)
+    assert k == sb["residual"] + sb["rasterized_jacobians"] + sb["pixel_anchor_jacobians"] + sb["jtj_jtr"]
+
+
+def test_association_count():
+    import numpy as np
+    faces = np.array([[0, 1, 2], [1, 2, 3]])
+    anchors = np.array([[0, 1, 2, 3], [0, 1, 2, 4], [0, 5, -1, -1], [6, 6, 7, 8]], np.int32)
+    pixel_faces = np.array([0, 1, -1, 0])
+    mask = np.array([1, 1, 1, 0])
+    # pixel 0: face 0 -> {0,1,2,3,4,5} = 6 ; pixel 1: face 1 -> {0,1,2,4,5,6,7,8} = 8 ; pixel 2: no face ; pixel 3: masked
+    assert bench.count_associations(pixel_faces, mask, faces, anchors) == 14

@@ -410,3 +410,42 @@ def test_fit_rgbd_overload_matches_depth_overload(nn, S, oracle_mod):
         out.append(ft.diagnostics())
     assert np.array_equal(out[0]["pixel_faces"], out[1]["pixel_faces"])
     assert rel_err(out[1]["updates"], out[0]["updates"]) < 1e-4
+
+
+def test_rendering_alignment_optimizer_slot(nn, S, oracle_mod):
+    """alignment.render_based.RenderingAlignmentOptimizer.optimize_graph over the fitter (point-cloud overload)."""
+    from dynamicfuion_python_amd.alignment.render_based import (PenaltyFunction, RenderingAlignmentOptimizer,
+                                                                 RenderingAlignmentParameters)
+    sc = _scene(S, oracle_mod, "S1")
+    depth = scene_target(oracle_mod, sc)
+    refp, refm = oracle_mod.unproject(depth, sc.K, 1.0, 10.0)
+    N = len(sc.nodes)
+    _, t_o, dg_o = oracle_mod.fit(nodes=sc.nodes, rotations=np.tile(np.eye(3, dtype=np.float32), (N, 1, 1)),
+                                  translations=np.zeros((N, 3), np.float32), mesh_points=sc.points, mesh_normals=sc.normals,
+                                  faces=sc.faces, ref_points=refp, ref_mask=refm, H=sc.H, W=sc.W, K=sc.K, max_iterations=1,
+                                  lm_factor=0.001, coverage=sc.coverage)
+    G = nn.geometry
+    graph = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE, 1)
+    params = RenderingAlignmentParameters(data_term_penalty_function=PenaltyFunction.SQUARE, max_iteration_count=1)
+    opt = RenderingAlignmentOptimizer((sc.H, sc.W), None, sc.K, params)
+    pts = np.where(refm[:, None].astype(bool), refp, 0).reshape(sc.H, sc.W, 3)
+    opt.optimize_graph(graph, G.TriangleMesh(sc.points, sc.normals, sc.faces), pts, None)
+    assert rel_err(graph.get_node_translations(True), t_o) < 1e-4
+
+
+def test_graph_warp_field_warp_mesh(nn, S, oracle_mod):
+    """GraphWarpField.warp_mesh (cpp/pybind/geometry/geometry.cpp:293-302): anchors over the field's nodes + blend warp."""
+    sc = _scene(S, oracle_mod, "S1")
+    G = nn.geometry
+    wf = G.GraphWarpField(sc.nodes, sc.coverage, False, 4, 0)
+    wf.set_node_rotations(sc.gt_rotations)
+    wf.set_node_translations(sc.gt_translations)
+    out = wf.warp_mesh(G.TriangleMesh(sc.points, sc.normals, sc.faces))
+    a, w = oracle_mod.compute_anchors(sc.points, sc.nodes, 4, sc.coverage)
+    wp, wn = oracle_mod.warp_mesh(sc.points, sc.normals, sc.nodes, sc.gt_rotations, sc.gt_translations, a, w)
+    assert np.array_equal(_np(out.vertex_positions), wp)
+    assert np.array_equal(_np(out.vertex_normals), wn)
+    assert np.allclose(wf.get_warped_nodes(), sc.nodes + sc.gt_translations)
+    wf.reset_rotations()
+    assert np.array_equal(wf.get_node_rotations(), np.tile(np.eye(3, dtype=np.float32), (len(sc.nodes), 1, 1)))
+    assert np.array_equal(wf.get_node_translations(), sc.gt_translations)
