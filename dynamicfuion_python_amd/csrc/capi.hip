@@ -332,6 +332,7 @@ struct nnrt_fitter {
 	DeviceBuffer<float> weights;
 	DeviceBuffer<float4> wpos, wnrm, jv, jn;
 	DeviceBuffer<float4> ref_points;   // [P] reference point (x, y, z, valid)
+	DeviceBuffer<float4> records;      // [P, 4] pixel Jacobian records
 	DeviceBuffer<uint64_t> keys;
 	DeviceBuffer<float> residuals;
 	DeviceBuffer<uint8_t> residual_mask;
@@ -424,6 +425,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 	fa.jv = ft->jv.ptr;
 	fa.jn = ft->jn.ptr;
 	fa.ref_points = ft->ref_points.ptr;
+	fa.records = ft->records.ptr;
 	fa.residuals = ft->residuals.ptr;
 	fa.residual_mask = ft->residual_mask.ptr;
 	fa.pixel_face = ft->pixel_face.ptr;
@@ -522,6 +524,7 @@ void nnrt_fitter_destroy(nnrt_fitter* ft) {
 	ft->drop_graphs();
 	ft->acc.release();
 	ft->ref_points.release();
+	ft->records.release();
 	for (auto* b : {&ft->mesh_p, &ft->mesh_n, &ft->weights, &ft->residuals, &ft->arap_acc, &ft->updates, &ft->gradient,
 	                &ft->hessian, &ft->wing, &ft->edge_residuals, &ft->a_diag, &ft->a_dinv, &ft->a_dinvb, &ft->a_schur, &ft->a_rhs, &ft->a_x})
 		b->release();
@@ -576,7 +579,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	if ((st = ft->mesh_p.ensure(3 * V)) || (st = ft->mesh_n.ensure(3 * V)) || (st = ft->faces4.ensure(F)) ||
 	    (st = ft->anchors.ensure(static_cast<size_t>(V) * K)) || (st = ft->weights.ensure(static_cast<size_t>(V) * K)) ||
 	    (st = ft->wpos.ensure(V)) || (st = ft->wnrm.ensure(V)) || (st = ft->jv.ensure(static_cast<size_t>(V) * K)) ||
-	    (st = ft->jn.ensure(static_cast<size_t>(V) * K)) || (st = ft->ref_points.ensure(P)) || (st = ft->keys.ensure(P)) ||
+	    (st = ft->jn.ensure(static_cast<size_t>(V) * K)) || (st = ft->ref_points.ensure(P)) || (st = ft->records.ensure(4 * P)) || (st = ft->keys.ensure(P)) ||
 	    (st = ft->residuals.ensure(P)) || (st = ft->residual_mask.ensure(P)) || (st = ft->pixel_face.ensure(P)) ||
 	    (st = ft->acc.ensure(static_cast<size_t>(N) * ACC_STRIDE)) || (st = ft->arap_acc.ensure(static_cast<size_t>(N) * ACC_STRIDE)) ||
 	    (st = ft->updates.ensure(static_cast<size_t>(N) * 6)) || (st = ft->gradient.ensure(static_cast<size_t>(N) * 6)) ||

@@ -80,6 +80,26 @@ __host__ __device__ inline float pixel_to_ndc(int i, int d1, int d2) {
 	return -offset + (range * static_cast<float>(i) + offset) / static_cast<float>(d1);
 }
 
+// ---- correctly rounded division through a shared reciprocal (Markstein) ----
+// y = RN(1/b) from the double quotient (double rounding is innocuous for a float reciprocal), q = RN(a*y),
+// r = a - b*q exact by FMA, RN(q + r*y) = RN(a/b) for normal-range operands (Markstein's theorem); other operands fall
+// back to the division. Bit-identical to a/b with -fhip-fp32-correctly-rounded-divide-sqrt, at 3 instructions per
+// quotient once the reciprocal of a shared denominator is known.
+__device__ inline float rcp_rn(float b) { return static_cast<float>(1.0 / static_cast<double>(b)); }
+__device__ inline float div_rn(float a, float b, float y) {
+	const float aa = fabsf(a), ab = fabsf(b);
+	if (!(aa > 1e-30f && aa < 1e30f && ab > 1e-30f && ab < 1e30f)) return a / b;
+	const float q = a * y;
+	const float r = fmaf(-b, q, a);
+	return fmaf(r, y, q);
+}
+// pixel_to_ndc with the reciprocal of d1 precomputed (rcp_rn(d1))
+__device__ inline float pixel_to_ndc_r(int i, int d1, int d2, float inv_d1) {
+	float range = ndc_range(d1, d2);
+	const float offset = (range / 2.0f);
+	return -offset + div_rn(range * static_cast<float>(i) + offset, static_cast<float>(d1), inv_d1);
+}
+
 // Open3D TransformIndexer::Project with float intrinsics
 struct Camera {
 	float fx, fy, cx, cy;
@@ -128,8 +148,13 @@ __device__ inline float point_segment_sq(float px, float py, float ax, float ay,
 // Ray-face test of one pixel centre (RayFaceIntersection.h:162-255 semantics). Returns true if accepted.
 // DIST = false skips the point-to-edge distance: valid only where the caller knows the distance test passes (a face
 // whose box diagonal is far below the blur radius, or a winner re-resolved after a full test); h.dist is then unset.
+__device__ inline float face_area_cw(const FaceNdc& f) { return spa_cw(f.x[0], f.y[0], f.x[1], f.y[1], f.x[2], f.y[2]); }
+// reciprocal of the barycentric denominator (area + K_EPSILON) of a face, for face_test's shared-reciprocal division
+__device__ inline float face_inv_area(const FaceNdc& f) { return rcp_rn(face_area_cw(f) + K_EPSILON); }
+
 template <bool DIST = true>
-__device__ inline bool face_test(const FaceNdc& f, float px, float py, float blur, bool persp, bool clip, bool cull, RasterHit& h) {
+__device__ inline bool face_test(const FaceNdc& f, float px, float py, float blur, bool persp, bool clip, bool cull, RasterHit& h,
+                                 float inv_area) {
 	const float area = spa_cw(f.x[0], f.y[0], f.x[1], f.y[1], f.x[2], f.y[2]);
 	const bool back = area < 0.f;
 	const bool zero_area = (area <= K_EPSILON && area >= -1.f * K_EPSILON);
@@ -140,9 +165,9 @@ __device__ inline bool face_test(const FaceNdc& f, float px, float py, float blu
 	const bool zinv = fmax3f(f.z[0], f.z[1], f.z[2]) < K_EPSILON;
 	if ((px > xmax || px < xmin || py > ymax || py < ymin || zinv) || (cull && back) || zero_area) return false;
 	const float A = area + K_EPSILON;
-	float b0 = spa_cw(px, py, f.x[1], f.y[1], f.x[2], f.y[2]) / A;
-	float b1 = spa_cw(px, py, f.x[2], f.y[2], f.x[0], f.y[0]) / A;
-	float b2 = spa_cw(px, py, f.x[0], f.y[0], f.x[1], f.y[1]) / A;
+	float b0 = div_rn(spa_cw(px, py, f.x[1], f.y[1], f.x[2], f.y[2]), A, inv_area);
+	float b1 = div_rn(spa_cw(px, py, f.x[2], f.y[2], f.x[0], f.y[0]), A, inv_area);
+	float b2 = div_rn(spa_cw(px, py, f.x[0], f.y[0], f.x[1], f.y[1]), A, inv_area);
 	if (persp) {
 		const float n0 = b0 * f.z[1] * f.z[2], n1 = f.z[0] * b1 * f.z[2], n2 = f.z[0] * f.z[1] * b2;
 		const float den = fmaxf(n0 + n1 + n2, K_EPSILON);
@@ -177,6 +202,10 @@ __device__ inline bool face_test(const FaceNdc& f, float px, float py, float blu
 	h.b1 = c1;
 	h.b2 = c2;
 	return true;
+}
+template <bool DIST = true>
+__device__ inline bool face_test(const FaceNdc& f, float px, float py, float blur, bool persp, bool clip, bool cull, RasterHit& h) {
+	return face_test<DIST>(f, px, py, blur, persp, clip, cull, h, face_inv_area(f));
 }
 
 // 64-bit (depth, face) key: non-negative float depth bits are order-preserving; ties resolve to the lower face index

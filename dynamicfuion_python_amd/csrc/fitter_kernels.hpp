@@ -29,6 +29,7 @@ struct FitPixelArgs {
 	uint8_t* residual_mask; // [P]
 	int32_t* pixel_face;    // [P]
 	double* acc;            // [N, ACC_STRIDE] fp64 data-term accumulator (21 JtJ + 6 J r)
+	float4* records;        // [P, 4] per-pixel Jacobian record (pass 1 -> pass 2)
 };
 
 struct SolveArgs {

@@ -26,6 +26,24 @@ __device__ inline FaceNdc load_face_ndc(const float* face_ndc, int64_t f) {
 	return r;
 }
 
+// Conservative pixel index range of [lo, hi] along one image axis, in float (two pixels of margin absorb the rounding
+// of the estimate; face_pixel_range trims it exactly). Empty for NaN / off-image bounds.
+__device__ inline void pixel_span_f(float lo, float hi, int dim, int other, int* first, int* last) {
+	const float r = ndc_range(dim, other);
+	const float s = static_cast<float>(dim) / r;
+	float a = floorf((lo + 0.5f * r) * s - 0.5f) - 2.f;
+	float b = ceilf((hi + 0.5f * r) * s - 0.5f) + 2.f;
+	if (!(a <= static_cast<float>(dim - 1)) || !(b >= 0.f)) {
+		*first = 1;
+		*last = 0;
+		return;
+	}
+	a = fmaxf(a, 0.f);
+	b = fminf(b, static_cast<float>(dim - 1));
+	*first = static_cast<int>(a);
+	*last = static_cast<int>(b);
+}
+
 // Exact pixel range of a face: the pixels whose centres pass face_test's bounding-box check (box widened by the blur
 // radius). Returns false for faces face_test rejects for every pixel (culled, zero-area, behind the camera, off-image).
 __device__ inline bool face_pixel_range(const FaceNdc& fn, const RasterOptions& o, int& u0, int& u1, int& v0, int& v1) {
@@ -39,30 +57,58 @@ __device__ inline bool face_pixel_range(const FaceNdc& fn, const RasterOptions& 
 	const float ymin = fmin3f(fn.y[0], fn.y[1], fn.y[2]) - o.blur;
 	const float ymax = fmax3f(fn.y[0], fn.y[1], fn.y[2]) + o.blur;
 	if (!(xmax >= xmin) || !(ymax >= ymin)) return false;
-	pixel_span(xmin, xmax, o.W, o.H, &u0, &u1);
-	pixel_span(ymin, ymax, o.H, o.W, &v0, &v1);
-	// pixel_to_ndc is monotone: trim the one-pixel widening so only pixels inside the box remain
-	while (u0 <= u1 && pixel_to_ndc(u0, o.W, o.H) < xmin) u0++;
-	while (u1 >= u0 && pixel_to_ndc(u1, o.W, o.H) > xmax) u1--;
-	while (v0 <= v1 && pixel_to_ndc(v0, o.H, o.W) < ymin) v0++;
-	while (v1 >= v0 && pixel_to_ndc(v1, o.H, o.W) > ymax) v1--;
+	pixel_span_f(xmin, xmax, o.W, o.H, &u0, &u1);
+	pixel_span_f(ymin, ymax, o.H, o.W, &v0, &v1);
+	// pixel_to_ndc is monotone: trim the widening so only pixels inside the box remain
+	const float inv_w = rcp_rn(static_cast<float>(o.W)), inv_h = rcp_rn(static_cast<float>(o.H));
+	while (u0 <= u1 && pixel_to_ndc_r(u0, o.W, o.H, inv_w) < xmin) u0++;
+	while (u1 >= u0 && pixel_to_ndc_r(u1, o.W, o.H, inv_w) > xmax) u1--;
+	while (v0 <= v1 && pixel_to_ndc_r(v0, o.H, o.W, inv_h) < ymin) v0++;
+	while (v1 >= v0 && pixel_to_ndc_r(v1, o.H, o.W, inv_h) > ymax) v1--;
 	return u0 <= u1 && v0 <= v1;
 }
 
-// One workgroup = 256 consecutive faces. Consecutive faces of a mesh are spatially coherent, so their pixel boxes share a
-// small bounding rectangle: the workgroup resolves its faces' (depth, face) minima in LDS with 64-bit LDS atomics and
-// then merges the rectangle into the image with one global atomicMin per touched pixel, row-contiguous across lanes
-// (memory-side global atomics cost one 64-B request per scattered lane: MI355X_MICROARCH.md "Global float atomics").
-// Workgroups whose rectangle exceeds the LDS tile fall back to per-pixel global atomics. Result = min over all faces of
-// the key, i.e. identical to a direct scatter.
+// One workgroup = 64 consecutive faces, 4 lanes per face (the lanes of a quad split the face's pixel tests, so a launch
+// has 4x the waves of a lane-per-face launch and each lane a quarter of the serial test loop). Consecutive faces of a
+// mesh are spatially coherent, so their pixel boxes share a small bounding rectangle: the workgroup resolves its
+// faces' (depth, face) minima in LDS with 64-bit LDS atomics and then merges the rectangle into the image with one
+// global atomicMin per touched pixel, row-contiguous across lanes (memory-side global atomics cost one 64-B request
+// per scattered lane: MI355X_MICROARCH.md "Global float atomics"). Workgroups whose rectangle exceeds the LDS tile fall
+// back to per-pixel global atomics. Result = min over all faces of the key, i.e. identical to a direct scatter.
 constexpr int SCATTER_BLOCK = 256;
+#ifndef NNRT_FIT_VARIANT
+#define NNRT_FIT_VARIANT 0
+#endif
+#if NNRT_FIT_VARIANT == 21
+constexpr int SCATTER_LANES_PER_FACE = 1;
+#elif NNRT_FIT_VARIANT == 22
+constexpr int SCATTER_LANES_PER_FACE = 2;
+#else
+constexpr int SCATTER_LANES_PER_FACE = 1;
+#endif
+constexpr int SCATTER_FACES_PER_BLOCK = SCATTER_BLOCK / SCATTER_LANES_PER_FACE;
 constexpr int SCATTER_LDS_KEYS = 4096;   // 32 KiB
+
+#if NNRT_FIT_VARIANT == 30
+__device__ unsigned long long g_raster_stamps[1 << 18];
+#define RSTAMP(i)                                                                                                             \
+	do {                                                                                                                    \
+		if ((threadIdx.x & 63) == 0) g_raster_stamps[(blockIdx.x * (SCATTER_BLOCK / 64) + threadIdx.x / 64) * 8 + (i)] =        \
+		                                 __builtin_amdgcn_s_memrealtime();                                                    \
+	} while (0)
+extern "C" int nnrt_dev_raster_stamps(unsigned long long* host, int n) {
+	return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_raster_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
+}
+#else
+#define RSTAMP(i) do {} while (0)
+#endif
 
 __device__ inline void scatter_block(const FaceNdc& fn, bool ok, int32_t face, const RasterOptions& o, uint64_t* keys) {
 	__shared__ uint64_t s_keys[SCATTER_LDS_KEYS];
 	__shared__ int s_box[4];
 	int u0 = 0, u1 = -1, v0 = 0, v1 = -1;
 	if (ok) ok = face_pixel_range(fn, o, u0, u1, v0, v1);
+	RSTAMP(1);
 	if (threadIdx.x == 0) {
 		s_box[0] = 0x7fffffff;
 		s_box[1] = -1;
@@ -70,13 +116,25 @@ __device__ inline void scatter_block(const FaceNdc& fn, bool ok, int32_t face, c
 		s_box[3] = -1;
 	}
 	__syncthreads();
-	if (ok) {
-		atomicMin(&s_box[0], u0);
-		atomicMax(&s_box[1], u1);
-		atomicMin(&s_box[2], v0);
-		atomicMax(&s_box[3], v1);
+	{
+		// wave-level min/max first: one LDS atomic per wave instead of 64 same-address atomics per wave
+		int bu0 = ok ? u0 : 0x7fffffff, bu1 = ok ? u1 : -1, bv0 = ok ? v0 : 0x7fffffff, bv1 = ok ? v1 : -1;
+#pragma unroll
+		for (int d = 32; d >= 1; d >>= 1) {
+			bu0 = min(bu0, __shfl_xor(bu0, d));
+			bu1 = max(bu1, __shfl_xor(bu1, d));
+			bv0 = min(bv0, __shfl_xor(bv0, d));
+			bv1 = max(bv1, __shfl_xor(bv1, d));
+		}
+		if ((threadIdx.x & 63) == 0 && bu1 >= 0) {
+			atomicMin(&s_box[0], bu0);
+			atomicMax(&s_box[1], bu1);
+			atomicMin(&s_box[2], bv0);
+			atomicMax(&s_box[3], bv1);
+		}
 	}
 	__syncthreads();
+	RSTAMP(2);
 	const int bu0 = s_box[0], bv0 = s_box[2];
 	const int bw = s_box[1] - bu0 + 1, bh = s_box[3] - bv0 + 1;
 	if (bw <= 0 || bh <= 0) return;   // uniform: no face of this workgroup covers a pixel
@@ -85,6 +143,7 @@ __device__ inline void scatter_block(const FaceNdc& fn, bool ok, int32_t face, c
 		for (int i = threadIdx.x; i < bw * bh; i += SCATTER_BLOCK) s_keys[i] = EMPTY_KEY;
 		__syncthreads();
 	}
+	RSTAMP(3);
 	// A13: the blur radius is compared against SQUARED NDC distances, so for a face whose blur-widened box has a squared
 	// diagonal well below the radius every pixel in the box passes the distance test: skip computing it.
 	bool near_all = false;
@@ -94,13 +153,19 @@ __device__ inline void scatter_block(const FaceNdc& fn, bool ok, int32_t face, c
 		near_all = (w * w + hh * hh) < 0.5f * o.blur;
 	}
 	if (ok) {
-		for (int v = v0; v <= v1; v++) {
-			const float py = pixel_to_ndc(v, o.H, o.W);
-			for (int u = u0; u <= u1; u++) {
-				const float px = pixel_to_ndc(u, o.W, o.H);
+		const float inv_w = rcp_rn(static_cast<float>(o.W)), inv_h = rcp_rn(static_cast<float>(o.H));
+		const float inv_area = face_inv_area(fn);
+		const int sub = static_cast<int>(threadIdx.x % SCATTER_LANES_PER_FACE);
+		const int span_u = u1 - u0 + 1;
+		const int count = span_u * (v1 - v0 + 1);
+		for (int i = sub; i < count; i += SCATTER_LANES_PER_FACE) {
+			const int v = v0 + i / span_u, u = u0 + i % span_u;
+			{
+				const float py = pixel_to_ndc_r(v, o.H, o.W, inv_h);
+				const float px = pixel_to_ndc_r(u, o.W, o.H, inv_w);
 				RasterHit h;
-				const bool hit = near_all ? face_test<false>(fn, px, py, o.blur, o.perspective, o.clip_barycentric, o.cull_back_faces, h)
-				                          : face_test<true>(fn, px, py, o.blur, o.perspective, o.clip_barycentric, o.cull_back_faces, h);
+				const bool hit = near_all ? face_test<false>(fn, px, py, o.blur, o.perspective, o.clip_barycentric, o.cull_back_faces, h, inv_area)
+				                          : face_test<true>(fn, px, py, o.blur, o.perspective, o.clip_barycentric, o.cull_back_faces, h, inv_area);
 				if (!hit) continue;
 				const unsigned long long key = raster_key(h.depth, face);
 				if (staged)
@@ -111,19 +176,22 @@ __device__ inline void scatter_block(const FaceNdc& fn, bool ok, int32_t face, c
 			}
 		}
 	}
+	RSTAMP(4);
 	if (!staged) return;
 	__syncthreads();
+	RSTAMP(5);
 	for (int i = threadIdx.x; i < bw * bh; i += SCATTER_BLOCK) {
 		const uint64_t k = s_keys[i];
 		if (k == EMPTY_KEY) continue;
 		const int64_t p = static_cast<int64_t>(bv0 + i / bw) * o.W + bu0 + i % bw;
 		atomicMin(reinterpret_cast<unsigned long long*>(keys + p), static_cast<unsigned long long>(k));
 	}
+	RSTAMP(6);
 }
 
 __global__ __launch_bounds__(SCATTER_BLOCK) void k_raster_scatter_ndc(const float* __restrict__ face_ndc, const uint8_t* __restrict__ mask,
                                                                       int64_t F, RasterOptions o, uint64_t* __restrict__ keys) {
-	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	const int64_t f = static_cast<int64_t>(blockIdx.x) * SCATTER_FACES_PER_BLOCK + threadIdx.x / SCATTER_LANES_PER_FACE;
 	FaceNdc fn{};
 	bool ok = f < F && !(mask && !mask[f]);
 	if (ok) fn = load_face_ndc(face_ndc, f);
@@ -133,7 +201,7 @@ __global__ __launch_bounds__(SCATTER_BLOCK) void k_raster_scatter_ndc(const floa
 nnrt_status launch_raster_scatter_ndc(const float* face_ndc, const uint8_t* mask, int64_t F, const RasterOptions& o, uint64_t* keys,
                                       hipStream_t stream) {
 	if (F == 0) return NNRT_OK;
-	k_raster_scatter_ndc<<<static_cast<unsigned>(ceil_div(F, SCATTER_BLOCK)), SCATTER_BLOCK, 0, stream>>>(face_ndc, mask, F, o, keys);
+	k_raster_scatter_ndc<<<static_cast<unsigned>(ceil_div(F, SCATTER_FACES_PER_BLOCK)), SCATTER_BLOCK, 0, stream>>>(face_ndc, mask, F, o, keys);
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;
 }
@@ -164,7 +232,8 @@ __device__ inline bool project_mesh_face(const float4* __restrict__ wpos, int4 f
 __global__ __launch_bounds__(SCATTER_BLOCK) void k_raster_scatter_mesh(const float4* __restrict__ wpos, const int4* __restrict__ faces4,
                                                                        int64_t F, NdcSetup s, float near_clip, float far_clip, RasterOptions o,
                                                                        uint64_t* __restrict__ keys) {
-	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	RSTAMP(0);
+	const int64_t f = static_cast<int64_t>(blockIdx.x) * SCATTER_FACES_PER_BLOCK + threadIdx.x / SCATTER_LANES_PER_FACE;
 	FaceNdc fn{};
 	const bool ok = f < F && project_mesh_face(wpos, faces4[f], s, near_clip, far_clip, fn);
 	scatter_block(fn, ok, static_cast<int32_t>(f), o, keys);
@@ -173,7 +242,7 @@ __global__ __launch_bounds__(SCATTER_BLOCK) void k_raster_scatter_mesh(const flo
 nnrt_status launch_raster_scatter_mesh(const float4* wpos, const int4* faces4, int64_t F, const NdcSetup& s, float near_clip, float far_clip,
                                        const RasterOptions& o, uint64_t* keys, hipStream_t stream) {
 	if (F == 0) return NNRT_OK;
-	k_raster_scatter_mesh<<<static_cast<unsigned>(ceil_div(F, SCATTER_BLOCK)), SCATTER_BLOCK, 0, stream>>>(wpos, faces4, F, s, near_clip, far_clip, o, keys);
+	k_raster_scatter_mesh<<<static_cast<unsigned>(ceil_div(F, SCATTER_FACES_PER_BLOCK)), SCATTER_BLOCK, 0, stream>>>(wpos, faces4, F, s, near_clip, far_clip, o, keys);
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;
 }
