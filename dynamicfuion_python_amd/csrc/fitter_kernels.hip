@@ -1,16 +1,16 @@
 // GN iteration kernels for gfx950 (DeformableMeshToImageFitter.cpp:111-275).
 //
-// k_fit_pixels fuses, per pixel, stages S3b-S10 of the reference loop: raster resolve, depth residual
-// (ComputeDepthResiduals :331-390), rasterized-surface Jacobians (RasterizedSurfaceJacobiansImpl.h:114-200),
-// pixel->node Jacobians (PixelVertexAnchorJacobiansImpl.h:179-363) and the block-diagonal data JtJ / Jt r reduction
-// (DeformableMeshToImageFitterImpl.h:199-456). The reference materialises [P,12,6] pixel Jacobians, [P,3,19] rasterized
-// Jacobians and [N,4000] node lists (capped: A4) and reduces each node serially. Here every 64-lane wavefront owns an
-// 8x8 pixel block; it walks the distinct nodes its pixels touch (wave-uniform loop driven by a ballot), each lane builds
-// its pixel's 6-dof Jacobian for that node, and the 27 products (21 JtJ upper-triangle entries + 6 J r) are summed over
-// the wave in double with a transposing butterfly (permlane swaps + DPP, no LDS) and added to the node's fp64
-// accumulator row with one 27-lane atomic. Products are rounded to float exactly as the reference forms them and
-// summed in double, so the data term equals the exactly-summed reference data term (see DESIGN.md "Numerics") -- no
-// intermediate tensors, no node-list cap, no LDS.
+// The reference materialises [P,12,6] pixel Jacobians, [P,3,19] rasterized Jacobians and [N,4000] node lists
+// (capped: A4) and reduces each node serially. Here the data term takes two passes over the pixels:
+//  * k_pixel_jacobians (pass 1, one lane per pixel): raster resolve, depth residual (ComputeDepthResiduals :331-390)
+//    and the rasterized-surface chain (RasterizedSurfaceJacobiansImpl.h:114-284) folded with dr/dw_l, dr/dn_l into a
+//    16-float record per contributing pixel (dr/dV 9, dr/dn_l 3, rho 3, r).
+//  * k_node_reduce_grouped (pass 2, one wave per 8x8 pixels): groups the block's (pixel, node) associations by node
+//    (AssociateFacesWithAnchorsImpl.h semantics), forms each association's node Jacobian
+//    (PixelVertexAnchorJacobiansImpl.h:179-363) and sums JJᵀ and J r per node (DeformableMeshToImageFitterImpl.h:199-456)
+//    into fp64 accumulator rows.
+// Products are rounded to float exactly as the reference forms them and summed in double, so the data term equals the
+// exactly-summed reference data term (see DESIGN.md "Numerics"); no node-list cap.
 #include "fitter_kernels.hpp"
 
 #ifndef NNRT_FIT_VARIANT
@@ -18,6 +18,7 @@
 #endif
 
 #if NNRT_FIT_VARIANT == 30
+#define FIT_STAMPS 1
 __device__ unsigned long long g_fit_stamps[2][1 << 17];
 #define FSTAMP(k, i)                                                                                                          \
 	do {                                                                                                                    \
@@ -27,8 +28,16 @@ extern "C" int nnrt_dev_fit_stamps(int k, unsigned long long* host, int n) {
 	return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fit_stamps), sizeof(unsigned long long) * n, sizeof(unsigned long long) * (1 << 17) * k) ==
 	               hipSuccess ? 0 : 1;
 }
+#define FSTAMP_AT(k, i, t)                                                                                                    \
+	do {                                                                                                                    \
+		if ((threadIdx.x & 63) == 0) g_fit_stamps[k][(blockIdx.x * 4 + threadIdx.x / 64) * 8 + (i)] = (t);                \
+	} while (0)
+#define FCLOCK() __builtin_amdgcn_s_memrealtime()
 #else
+#define FIT_STAMPS 0
 #define FSTAMP(k, i) do {} while (0)
+#define FSTAMP_AT(k, i, t) do {} while (0)
+#define FCLOCK() 0ull
 #endif
 
 namespace nnrt {
@@ -50,80 +59,6 @@ template <>
 struct ModeTraits<NNRT_ITERATION_ROTATION_ONLY> {
 	static constexpr int S = 3, NH = 6, NACC = 9;
 };
-
-// ---- wavefront reduction helpers ----
-template <int CTRL>
-__device__ inline float dpp_f32(float x) {
-	return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
-}
-template <int CTRL>
-__device__ inline double dpp_f64(double x) {
-	const uint64_t u = __builtin_bit_cast(uint64_t, x);
-	const int lo = __builtin_amdgcn_update_dpp(0, static_cast<int>(u & 0xffffffffu), CTRL, 0xf, 0xf, false);
-	const int hi = __builtin_amdgcn_update_dpp(0, static_cast<int>(u >> 32), CTRL, 0xf, 0xf, false);
-	return __builtin_bit_cast(double, (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) | static_cast<uint32_t>(lo));
-}
-template <int CTRL, typename R>
-__device__ inline R dpp_move(R x) {
-	if constexpr (sizeof(R) == 4) return dpp_f32<CTRL>(x);
-	else return dpp_f64<CTRL>(x);
-}
-
-// ---- wave sum of 32 per-lane values (transposing butterfly) ----
-// Each exchange step halves the values a lane holds: lanes with the step's bit set keep the upper half of the values,
-// the others the lower half, each adding its partner's copy. The two cross-row steps go first through gfx950's
-// v_permlane32_swap / v_permlane16_swap
-// swap(lo, hi) exchanges the upper half of `lo` with the lower half of `hi` (32 lanes, or the odd/even 16-lane rows),
-// so after one add the lanes with the step's bit clear hold lo(l) + lo(l ^ d) and the others hi(l ^ d) + hi(l):
-// a whole transposing step costs one swap per dword and one add, no selects. Rows then finish with DPP (8, 4, 2) and a
-// quad_perm add (1). On return lanes 2i and 2i + 1 hold the wave total of value index i.
-template <bool ROW16>
-__device__ inline uint2 permlane_swap_u32(uint32_t lo, uint32_t hi) {
-	if constexpr (ROW16) {
-		const auto r = __builtin_amdgcn_permlane16_swap(lo, hi, false, false);
-		return make_uint2(r[0], r[1]);
-	} else {
-		const auto r = __builtin_amdgcn_permlane32_swap(lo, hi, false, false);
-		return make_uint2(r[0], r[1]);
-	}
-}
-template <bool ROW16, typename R>
-__device__ inline R swap_add(R lo, R hi) {
-	if constexpr (sizeof(R) == 4) {
-		const uint2 r = permlane_swap_u32<ROW16>(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
-		return __builtin_bit_cast(R, r.x) + __builtin_bit_cast(R, r.y);
-	} else {
-		const uint64_t a = __builtin_bit_cast(uint64_t, lo), b = __builtin_bit_cast(uint64_t, hi);
-		const uint2 l = permlane_swap_u32<ROW16>(static_cast<uint32_t>(a), static_cast<uint32_t>(b));
-		const uint2 h = permlane_swap_u32<ROW16>(static_cast<uint32_t>(a >> 32), static_cast<uint32_t>(b >> 32));
-		const R x = __builtin_bit_cast(R, (static_cast<uint64_t>(h.x) << 32) | l.x);
-		const R y = __builtin_bit_cast(R, (static_cast<uint64_t>(h.y) << 32) | l.y);
-		return x + y;
-	}
-}
-
-template <int D, int HALF, typename R>
-__device__ inline void butterfly_row_step(R (&v)[32], bool upper) {
-#pragma unroll
-	for (int j = 0; j < HALF; j++) {
-		const R lo = v[j], hi = v[j + HALF];
-		const R from_above = dpp_move<0x100 + D>(lo);   // row_shl:D
-		const R from_below = dpp_move<0x110 + D>(hi);   // row_shr:D
-		v[j] = upper ? (hi + from_below) : (lo + from_above);
-	}
-}
-
-template <typename R>
-__device__ inline R wave_reduce32_swap(R (&v)[32], int lane) {
-#pragma unroll
-	for (int j = 0; j < 16; j++) v[j] = swap_add<false>(v[j], v[j + 16]);
-#pragma unroll
-	for (int j = 0; j < 8; j++) v[j] = swap_add<true>(v[j], v[j + 8]);
-	butterfly_row_step<8, 4>(v, (lane & 8) != 0);
-	butterfly_row_step<4, 2>(v, (lane & 4) != 0);
-	butterfly_row_step<2, 1>(v, (lane & 2) != 0);
-	return v[0] + dpp_move<0xB1>(v[0]);   // quad_perm [1,0,3,2]: lanes 2i, 2i+1 exchange
-}
 
 // ---- pass 1: per pixel (S3b-S9) -----------------------------------------------------------------------------------
 // Resolves the raster winner, writes the residual / mask / face outputs and, for pixels that contribute to the data
@@ -360,431 +295,307 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_pixel_jacobians(FitPixelArgs a) {
 	FSTAMP(0, 2);
 }
 
-// ---- pass 2: per node (S10) ------------------------------------------------------------------------------------
-// 8x8 pixels per wave. For each distinct node of the wave's pixels (wave-uniform loop driven by a ballot), every lane
-// forms its pixel's 6-dof Jacobian for that node from the pass-1 record and the face vertices' warped-Jacobian rows;
-// JJᵀ and J r are summed over the wave and added to the node's fp64 accumulator row.
+// ---- pass 2, node-grouped per wave --------------------------------------------------------------------------------
+// 8x8 pixels per wave (the K1 mapping); the wave's (pixel, node) associations are processed in chunks of NG_CAP.
+// (1) Group: a wave-uniform loop over anchor slots picks the next pending node (readlane of the first lane holding
+//     it in that slot); every lane matches it against its remaining slots with scalar wave masks (per face vertex the
+//     LAST matching slot: AssociateFacesWithAnchors) and the matching lanes file one association (pixel, vertex-anchor
+//     row per face vertex) at consecutive LDS positions (mbcnt) -- no LDS atomics, no hash. A node that does not fit
+//     the chunk is split: its first lanes are filed, the rest stay pending.
+// (2) Jacobians: one association per lane (no idle lanes); J (S floats) and r overwrite the association's slot.
+// (3) Sums: the wave splits into 64 / GROUP lane groups; lane e of a group owns accumulator entry e (JJᵀ upper
+//     triangle, then J r) and walks its group's share of the chunk adding the float product J[c0] * J[c1] in double;
+//     at a node change the group adds its totals to the node's fp64 row (one 27-lane atomic). No cross-lane reduction.
+// Chunks are software-pipelined over two LDS buffers: the jv / jn row gathers of chunk c + 1 are in flight while
+// chunk c is summed, and chunk c + 1 is grouped while chunk c's gathers land. Pixel records are staged in LDS.
+constexpr int NG_CAP = 52;     // associations per chunk (one lane each in (2))
+constexpr int NG_BATCH = 8;    // associations per group read ahead in (3)
+// Slot buffers are component-major (word c of slot i at c * NG_STRIDE + i; odd stride: the words one lane group reads
+// in (3) fall in distinct LDS banks). Words: (1) pixel lane, jv/jn row per face vertex (-1: none), node at word 7;
+// (2) J[0..S-1], r at word S.
+constexpr int NG_STRIDE = 59;
+constexpr int ng_read_end(int g) {   // one past the last slot (3) reads for any chunk size, with g lane groups
+	int m = 0;
+	for (int count = 1; count <= NG_CAP; count++) {
+		const int steps = (count + g - 1) / g;
+		const int end = (g - 1) * count / g + (steps + NG_BATCH - 1) / NG_BATCH * NG_BATCH;
+		m = end > m ? end : m;
+	}
+	return m;
+}
+constexpr int NG_ROWS = 8;     // pixel rows per wave (8 x NG_ROWS pixels)
+
+__device__ inline void ng_flush(double* dst, double v) { atomicAdd(dst, v); }
+
 template <int MODE, int MAXK>
-__global__ __launch_bounds__(PIX_BLOCK) void k_node_reduce(FitPixelArgs a) {
+__global__ __launch_bounds__(PIX_BLOCK, 5) void k_node_reduce_grouped(FitPixelArgs a) {
 	using T = ModeTraits<MODE>;
 	constexpr int S = T::S;
-	static_assert(T::NACC <= 32, "accumulator row must fit the 32-value wave reduction");
+	constexpr int NSLOT = 3 * MAXK;
+	constexpr int GROUP = T::NACC > 16 ? 32 : 16;
+	constexpr int G = 64 / GROUP;
+	static_assert(T::NACC <= GROUP && ng_read_end(G) <= NG_STRIDE && (NG_STRIDE & 1), "slot layout");
+	__shared__ float s_rec[PIX_BLOCK / 64][16 * 64];                 // component-major pixel records
+	__shared__ float s_slots[PIX_BLOCK / 64][2][8 * NG_STRIDE];
 
-	// XCD-aware tile order: consecutive workgroups are dealt round-robin over the 8 XCDs, so give each XCD a contiguous
-	// band of tiles (neighbouring tiles share vertices, anchors and nodes -> L2 reuse within the XCD).
-	const int tiles = a.tiles_x * a.tiles_y;
+	// tiles of 16 x (2 NG_ROWS) pixels, one 8 x NG_ROWS block per wave
+	const int tiles_y = (a.H + 2 * NG_ROWS - 1) / (2 * NG_ROWS);
+	const int tiles = a.tiles_x * tiles_y;
 	const int per_xcd = (tiles + 7) / 8;
 	const int b = blockIdx.x;
 	const int tile = (b % 8) * per_xcd + b / 8;
 	const int tu = tile % a.tiles_x, tv = tile / a.tiles_x;
-	// wave w of the workgroup owns the 8x8 quadrant (w & 1, w >> 1): compact pixel sets touch the fewest nodes
 	const int lane = static_cast<int>(threadIdx.x & 63), wave = static_cast<int>(threadIdx.x >> 6);
-	const int u = tu * PIX_TILE + (wave & 1) * 8 + (lane & 7);
-	const int v = tv * PIX_TILE + (wave >> 1) * 8 + (lane >> 3);
-	const bool in_image = tile < tiles && u < a.W && v < a.H;
-	const int64_t p = static_cast<int64_t>(v) * a.W + u;
+	const int u = tu * PIX_TILE + (wave & 1) * 8 + (lane & 7), v = tv * 2 * NG_ROWS + (wave >> 1) * NG_ROWS + (lane >> 3);
+	const bool in_image = tile < tiles && (lane >> 3) < NG_ROWS && u < a.W && v < a.H;
+	float* recs = s_rec[wave];
+	const int KA = a.anchor_count;
 
-	// per-lane inputs of the wave-level node loop below
-	uint32_t pending = 0;   // bit 8*fv + k: anchor k of face vertex fv still to be reduced
+	int anc[NSLOT];
 	int vid[3] = {0, 0, 0};
-	int anc[3][MAXK];
-	float dr_dV[9];
-	float rn[3] = {0.f, 0.f, 0.f}, rho[3] = {0.f, 0.f, 0.f};
-	float r_used = 0.f;
-#if NNRT_FIT_VARIANT == 16 || NNRT_FIT_VARIANT == 17
-	float cj[3][MAXK][S];   // per anchor slot: this pixel's contribution to the slot node's Jacobian
 #pragma unroll
-	for (int fv = 0; fv < 3; fv++)
-#pragma unroll
-		for (int k = 0; k < MAXK; k++)
-#pragma unroll
-			for (int c = 0; c < S; c++) cj[fv][k][c] = 0.f;
-#endif
-#pragma unroll
-	for (int c = 0; c < 9; c++) dr_dV[c] = 0.f;
-#pragma unroll
-	for (int fv = 0; fv < 3; fv++)
-#pragma unroll
-		for (int k = 0; k < MAXK; k++) anc[fv][k] = -1;
-
-	FSTAMP(1, 0);
+	for (int t = 0; t < NSLOT; t++) anc[t] = -1;
+	[[maybe_unused]] const unsigned long long t_start = FCLOCK();
+	unsigned long long t_jac = 0, t_sum = 0;
 	if (in_image) {
+		const int64_t p = static_cast<int64_t>(v) * a.W + u;
 		const uint64_t key = a.keys[p];
 		a.keys[p] = EMPTY_KEY;   // ready for the next iteration's scatter
 		if (key != EMPTY_KEY) {
+			const float4* rec = a.records + 4 * p;
+			const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2], q3 = rec[3];
 			const int face = static_cast<int>(key & 0xffffffffu);
 			const int4 fi = a.faces4[face];
 			vid[0] = fi.x;
 			vid[1] = fi.y;
 			vid[2] = fi.z;
-			const int KA = a.anchor_count;
 #pragma unroll
 			for (int fv = 0; fv < 3; fv++)
 #pragma unroll
-				for (int k = 0; k < MAXK; k++) {
-					const int n = (k < KA) ? a.anchors[static_cast<int64_t>(vid[fv]) * KA + k] : -1;
-					anc[fv][k] = n;
-					if (n >= 0) pending |= 1u << (8 * fv + k);
+				for (int k = 0; k < MAXK; k++) anc[fv * MAXK + k] = (k < KA) ? a.anchors[static_cast<int64_t>(vid[fv]) * KA + k] : -1;
+			const float q[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+#pragma unroll
+			for (int w = 0; w < 16; w++) recs[w * 64 + lane] = q[w];
+		}
+	}
+	if (FIT_STAMPS && __ballot(anc[NSLOT - 1] == 123456789) == 777ull) a.acc[0] = 0;   // stamp after the prologue loads
+	const unsigned long long t_loaded = FCLOCK();
+
+	// accumulator entry of this lane within its group
+	const int grp = lane / GROUP, e = lane % GROUP;
+	const bool e_valid = e < T::NACC;
+	int c0 = 0, c1 = 0;
+	{
+		int idx = 0;
+#pragma unroll
+		for (int r0 = 0; r0 < S; r0++)
+#pragma unroll
+			for (int r1 = r0; r1 < S; r1++) {
+				if (idx == e) {
+					c0 = r0;
+					c1 = r1;
 				}
-			const float4* rec = a.records + 4 * p;
-			const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
-			dr_dV[0] = r0.x;
-			dr_dV[1] = r0.y;
-			dr_dV[2] = r0.z;
-			dr_dV[3] = r0.w;
-			dr_dV[4] = r1.x;
-			dr_dV[5] = r1.y;
-			dr_dV[6] = r1.z;
-			dr_dV[7] = r1.w;
-			dr_dV[8] = r2.x;
-			rn[0] = r2.y;
-			rn[1] = r2.z;
-			rn[2] = r2.w;
-			rho[0] = r3.x;
-			rho[1] = r3.y;
-			rho[2] = r3.z;
-			r_used = r3.w;
-#if NNRT_FIT_VARIANT == 16 || NNRT_FIT_VARIANT == 17
-			pending = 0;
+				idx++;
+			}
+#pragma unroll
+		for (int r0 = 0; r0 < S; r0++)
+			if (T::NH + r0 == e) {
+				c0 = r0;
+				c1 = S;
+			}
+	}
+	double acc = 0.0;
+	int cur = -1;
+
+	// (1) file up to NG_CAP associations into `slots`; returns the count (0: nothing pending)
+	const uint64_t lanes_below = (1ull << lane) - 1ull;
+	uint64_t pend[NSLOT];   // lanes whose slot t is still to be filed (wave masks: scalar registers)
+#pragma unroll
+	for (int t = 0; t < NSLOT; t++) pend[t] = __ballot(anc[t] >= 0);
+	auto group = [&](float* slots) -> int {
+		int filed = 0;
+#pragma unroll
+		for (int s = 0; s < NSLOT; s++) {
+			while (filed < NG_CAP && pend[s] != 0) {
+				const int leader = __ffsll(static_cast<unsigned long long>(pend[s])) - 1;
+				const int X = __builtin_amdgcn_readlane(anc[s], leader);
+				uint64_t hs[NSLOT];
+				uint64_t M = 0;
+#pragma unroll
+				for (int t = s; t < NSLOT; t++) {   // slots before s are exhausted wave-wide
+					hs[t] = __ballot(anc[t] == X) & pend[t];
+					M |= hs[t];
+				}
+				// lanes beyond the chunk's room stay pending (split node)
+				const int rank = __popcll(M & lanes_below);
+				const uint64_t keep = __ballot(__builtin_amdgcn_inverse_ballot_w64(M) && rank < NG_CAP - filed);
+				int kf[3] = {-1, -1, -1};
+#pragma unroll
+				for (int t = s; t < NSLOT; t++) {
+					const uint64_t h = hs[t] & keep;
+					pend[t] &= ~h;
+					if (__builtin_amdgcn_inverse_ballot_w64(h)) kf[t / MAXK] = t % MAXK;   // per face vertex the LAST match
+				}
+				if (__builtin_amdgcn_inverse_ballot_w64(keep)) {
+					const int pos = filed + rank;
+					slots[pos] = __builtin_bit_cast(float, lane);
+#pragma unroll
+					for (int fv = 0; fv < 3; fv++)
+						slots[(1 + fv) * NG_STRIDE + pos] = __builtin_bit_cast(float, kf[fv] >= 0 ? vid[fv] * KA + kf[fv] : -1);
+					slots[7 * NG_STRIDE + pos] = __builtin_bit_cast(float, X);
+				}
+				filed += __popcll(keep);
+			}
+		}
+		return filed;
+	};
+
+	// (2a) gather: association `lane` of a filed chunk -> its jv / jn rows (in flight until (2b))
+	int4 d = make_int4(0, -1, -1, -1);
+	float4 jv[3], jn[3];
+	auto gather = [&](const float* slots, int count) {
+		d = make_int4(0, -1, -1, -1);
+		if (lane < count)
+			d = make_int4(__builtin_bit_cast(int, slots[lane]), __builtin_bit_cast(int, slots[NG_STRIDE + lane]),
+			              __builtin_bit_cast(int, slots[2 * NG_STRIDE + lane]), __builtin_bit_cast(int, slots[3 * NG_STRIDE + lane]));
+		const int rows[3] = {d.y, d.z, d.w};
+#pragma unroll
+		for (int fv = 0; fv < 3; fv++) {
+			jv[fv] = make_float4(0.f, 0.f, 0.f, 0.f);
+			jn[fv] = make_float4(0.f, 0.f, 0.f, 0.f);
+			if (rows[fv] >= 0) {
+				jv[fv] = a.jv[rows[fv]];
+				if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) jn[fv] = a.jn[rows[fv]];
+			}
+		}
+	};
+	// (2b) J and r of association `lane` into its slot
+	auto jacobians = [&](float* slots, int count) {
+		if (lane < count) {
+			const int l = d.x;
+			const int rows[3] = {d.y, d.z, d.w};
+			float q[16];
+#pragma unroll
+			for (int w = 0; w < 16; w++) q[w] = recs[w * 64 + l];
+			const float dr_dV[9] = {q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7], q[8]};
+			const float rn[3] = {q[9], q[10], q[11]};
+			const float rho[3] = {q[12], q[13], q[14]};
+			float jr[3] = {0.f, 0.f, 0.f}, jt[3] = {0.f, 0.f, 0.f};
 #pragma unroll
 			for (int fv = 0; fv < 3; fv++) {
+				if (rows[fv] < 0) continue;
 				const f3 dv = make3(dr_dV[3 * fv], dr_dV[3 * fv + 1], dr_dV[3 * fv + 2]);
-				const f3 dn = make3(rn[0] * rho[fv], rn[1] * rho[fv], rn[2] * rho[fv]);
+				if (MODE != NNRT_ITERATION_ROTATION_ONLY) {
+					jt[0] += dv.x * jv[fv].w;
+					jt[1] += dv.y * jv[fv].w;
+					jt[2] += dv.z * jv[fv].w;
+				}
+				if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) {
+					const f3 dn = make3(rn[0] * rho[fv], rn[1] * rho[fv], rn[2] * rho[fv]);
+					const f3 t1 = row_times_skew(dv, make3(jv[fv].x, jv[fv].y, jv[fv].z));
+					const f3 t2 = row_times_skew(dn, make3(jn[fv].x, jn[fv].y, jn[fv].z));
+					jr[0] += t1.x + t2.x;
+					jr[1] += t1.y + t2.y;
+					jr[2] += t1.z + t2.z;
+				}
+			}
+			float J[8];
+			if (MODE == NNRT_ITERATION_ALL) {
+				J[0] = jr[0];
+				J[1] = jr[1];
+				J[2] = jr[2];
+				J[3] = jt[0];
+				J[4] = jt[1];
+				J[5] = jt[2];
+			} else if (MODE == NNRT_ITERATION_TRANSLATION_ONLY) {
+				J[0] = jt[0];
+				J[1] = jt[1];
+				J[2] = jt[2];
+			} else {
+				J[0] = jr[0];
+				J[1] = jr[1];
+				J[2] = jr[2];
+			}
+			J[S] = q[15];
 #pragma unroll
-				for (int k = 0; k < MAXK; k++) {
-					bool later_duplicate = false;
+			for (int c = 0; c <= S; c++) slots[c * NG_STRIDE + lane] = J[c];
+		}
+	};
+	// (3) exact sums of the chunk's products per node
+	auto sums = [&](const float* slots, int count) {
+		const int lo = (grp * count) / G, hi = ((grp + 1) * count) / G;
+		const int steps = (count + G - 1) / G;
+		for (int j = 0; j < steps; j += NG_BATCH) {
+			// every LDS read of the batch is issued before the dependent double adds (slots past `hi` are another
+			// group's or padding and are masked)
+			const float* base = slots + (lo + j);
+			int nodes[NG_BATCH];
+			float prod[NG_BATCH];
+			bool same = true;
 #pragma unroll
-					for (int k2 = k + 1; k2 < MAXK; k2++) later_duplicate |= anc[fv][k2] == anc[fv][k];
-					if (anc[fv][k] < 0 || later_duplicate) continue;
-					pending |= 1u << (8 * fv + k);
-					const int64_t vk = static_cast<int64_t>(vid[fv]) * KA + k;
-					const float4 jv = a.jv[vk];
-					float* c = cj[fv][k];
-					if (MODE == NNRT_ITERATION_TRANSLATION_ONLY) {
-						c[0] = dv.x * jv.w;
-						c[1] = dv.y * jv.w;
-						c[2] = dv.z * jv.w;
-					} else {
-						const float4 jn = a.jn[vk];
-						const f3 t1 = row_times_skew(dv, make3(jv.x, jv.y, jv.z));
-						const f3 t2 = row_times_skew(dn, make3(jn.x, jn.y, jn.z));
-						c[0] = t1.x + t2.x;
-						c[1] = t1.y + t2.y;
-						c[2] = t1.z + t2.z;
-						if (MODE == NNRT_ITERATION_ALL) {
-							c[3 % S] = dv.x * jv.w;
-							c[4 % S] = dv.y * jv.w;
-							c[5 % S] = dv.z * jv.w;
-						}
+			for (int q = 0; q < NG_BATCH; q++) {
+				const bool valid = lo + j + q < hi;
+				nodes[q] = __builtin_bit_cast(int, base[7 * NG_STRIDE + q]);
+				const float x = base[c0 * NG_STRIDE + q] * base[c1 * NG_STRIDE + q];
+				prod[q] = valid ? x : 0.f;
+				same &= !valid || nodes[q] == cur;
+			}
+			if (__all(same)) {
+				// independent partial sums: the double adds of a batch do not wait on one another
+				double part[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+				for (int q = 0; q < NG_BATCH; q++) part[q & 3] += static_cast<double>(prod[q]);
+				acc += (part[0] + part[1]) + (part[2] + part[3]);
+			} else {
+#pragma unroll
+				for (int q = 0; q < NG_BATCH; q++) {
+					if (lo + j + q < hi && nodes[q] != cur) {
+						if (cur >= 0 && e_valid) ng_flush(a.acc + static_cast<int64_t>(cur) * ACC_STRIDE + e, acc);
+						acc = 0.0;
+						cur = nodes[q];
 					}
+					acc += static_cast<double>(prod[q]);
 				}
 			}
-#endif
 		}
-	}
+	};
+	auto wave_sync = [&]() {
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+	};
 
-	// ---- wave-level reduction over the distinct nodes of this wave's pixels ----
-	// Per node, a pixel's Jacobian sums the contributions of every face vertex anchored to it (fv ascending, the
-	// reference's association keeps the LAST matching anchor slot of a vertex: AssociateFacesWithAnchors), then JJ^T
-	// and J r are added to the node's accumulator row.
-	if (__ballot(r_used == 1.2345f) == 777ull) a.acc[0] = 0;   // anchors the stamp after the prologue loads
-	FSTAMP(1, 1);
-	const int KA = a.anchor_count;
-	// this lane's Jacobian with respect to `node` (zero if none of its face's vertices is anchored to it); clears the
-	// node's pending slots. Contributions are summed in face-vertex order, the reference's per-node accumulation order.
-	// Slots of this lane anchored to `node`: per face vertex the LAST matching anchor slot (AssociateFacesWithAnchors),
-	// -1 if none; clears them from `pending`.
-	auto node_slots = [&](int node, int (&kk)[3]) {
-#pragma unroll
-		for (int fv = 0; fv < 3; fv++) {
-			kk[fv] = -1;
-#pragma unroll
-			for (int k = 0; k < MAXK; k++) {
-				const uint32_t bit = 1u << (8 * fv + k);
-				if ((pending & bit) && anc[fv][k] == node) {
-					pending &= ~bit;
-					kk[fv] = k;
-				}
-			}
-		}
-	};
-	struct SlotData {
-		float4 jv[3], jn[3];
-	};
-	auto load_slots = [&](const int (&kk)[3], SlotData& d) {
-#pragma unroll
-		for (int fv = 0; fv < 3; fv++) {
-			d.jv[fv] = make_float4(0.f, 0.f, 0.f, 0.f);
-			d.jn[fv] = make_float4(0.f, 0.f, 0.f, 0.f);
-			if (kk[fv] >= 0) {
-				const int64_t vk = static_cast<int64_t>(vid[fv]) * KA + kk[fv];
-				d.jv[fv] = a.jv[vk];
-				if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) d.jn[fv] = a.jn[vk];
-			}
-		}
-	};
-	// this lane's Jacobian with respect to the node whose slots are kk: contributions summed in face-vertex order,
-	// the reference's per-node accumulation order; zero if no vertex of the lane's face is anchored to the node
-	auto slot_jacobian = [&](const int (&kk)[3], const SlotData& d, float (&Jn)[S]) {
-		float jr[3] = {0.f, 0.f, 0.f}, jt[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-		for (int fv = 0; fv < 3; fv++) {
-			if (kk[fv] < 0) continue;
-			const float4 jv = d.jv[fv];
-			const f3 dv = make3(dr_dV[3 * fv], dr_dV[3 * fv + 1], dr_dV[3 * fv + 2]);
-			if (MODE != NNRT_ITERATION_ROTATION_ONLY) {
-				jt[0] += dv.x * jv.w;
-				jt[1] += dv.y * jv.w;
-				jt[2] += dv.z * jv.w;
-			}
-			if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) {
-				const float4 jn = d.jn[fv];
-				const f3 dn = make3(rn[0] * rho[fv], rn[1] * rho[fv], rn[2] * rho[fv]);
-				const f3 t1 = row_times_skew(dv, make3(jv.x, jv.y, jv.z));
-				const f3 t2 = row_times_skew(dn, make3(jn.x, jn.y, jn.z));
-				jr[0] += t1.x + t2.x;
-				jr[1] += t1.y + t2.y;
-				jr[2] += t1.z + t2.z;
-			}
-		}
-		if (MODE == NNRT_ITERATION_ALL) {
-			Jn[0] = jr[0];
-			Jn[1] = jr[1];
-			Jn[2] = jr[2];
-			Jn[3 % S] = jt[0];
-			Jn[4 % S] = jt[1];
-			Jn[5 % S] = jt[2];
-		} else if (MODE == NNRT_ITERATION_TRANSLATION_ONLY) {
-			Jn[0] = jt[0];
-			Jn[1] = jt[1];
-			Jn[2] = jt[2];
-		} else {
-			Jn[0] = jr[0];
-			Jn[1] = jr[1];
-			Jn[2] = jr[2];
-		}
-	};
-	auto node_jacobian = [&](int node, float (&Jn)[S]) {
-		int kk[3];
-		SlotData d;
-		node_slots(node, kk);
-		load_slots(kk, d);
-		slot_jacobian(kk, d, Jn);
-	};
-	// wave-uniform: the first pending node of the first lane that still has one (-1 when the wave is done)
-	auto next_node = [&]() -> int {
-		const uint64_t active = __ballot(pending != 0u);
-		if (active == 0) return -1;
-		const int leader = __ffsll(static_cast<unsigned long long>(active)) - 1;
-		int mine = -1;
-#pragma unroll
-		for (int fv = 2; fv >= 0; fv--)
-#pragma unroll
-			for (int k = MAXK - 1; k >= 0; k--)
-				if ((pending >> (8 * fv + k)) & 1u) mine = anc[fv][k];
-		return __shfl(mine, leader);
-	};
-#if NNRT_FIT_VARIANT == 16 || NNRT_FIT_VARIANT == 17
-	// Jacobian for `node` from the precomputed slot contributions (rotation part first for mode ALL, as cj is laid out)
-	auto pre_jacobian = [&](int node, float (&Jn)[S]) {
-		float Jv[S];
-#pragma unroll
-		for (int c = 0; c < S; c++) Jv[c] = 0.f;
-#pragma unroll
-		for (int fv = 0; fv < 3; fv++)
-#pragma unroll
-			for (int k = 0; k < MAXK; k++) {
-				const uint32_t bit = 1u << (8 * fv + k);
-				const bool m = (pending & bit) && anc[fv][k] == node;
-				if (m) pending &= ~bit;
-#pragma unroll
-				for (int c = 0; c < S; c++) Jv[c] = m ? Jv[c] + cj[fv][k][c] : Jv[c];
-			}
-#pragma unroll
-		for (int c = 0; c < S; c++) Jn[c] = Jv[c];
-	};
-#endif
-#if NNRT_FIT_VARIANT == 19
-	if (__ballot(pending != 0u) == 12345ull) a.acc[0] = r_used + dr_dV[0] + rn[0] + rho[0] + anc[0][0];   // keep loads live
-	pending = 0;
-#endif
-#if NNRT_FIT_VARIANT == 16
-	constexpr int XS16 = 17;
-	__shared__ double s_x16[PIX_BLOCK / 64][64 * XS16];
-	double* xw16 = s_x16[wave];
+	int cb = 0, count = 0;   // buffer and size of the chunk in flight (gathered, not yet reduced)
 	while (true) {
-		const int nodeA = next_node();
-		if (nodeA < 0) break;
-		float JA[S], JB[S];
-		pre_jacobian(nodeA, JA);
-		const int nodeB = next_node();
-#pragma unroll
-		for (int c = 0; c < S; c++) JB[c] = 0.f;
-		if (nodeB >= 0) pre_jacobian(nodeB, JB);
-		double* row = xw16 + lane * XS16;
-#pragma unroll
-		for (int c = 0; c < 8; c++) {
-			row[c] = c < S ? static_cast<double>(JA[c < S ? c : 0]) : (c == S ? static_cast<double>(r_used) : 0.0);
-			row[8 + c] = c < S ? static_cast<double>(JB[c < S ? c : 0]) : (c == S ? static_cast<double>(r_used) : 0.0);
-		}
-		__builtin_amdgcn_wave_barrier();
-		typedef double d4 __attribute__((ext_vector_type(4)));
-		d4 C = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-		for (int m = 0; m < 16; m++) {
-			const double x = xw16[(4 * m + (lane >> 4)) * XS16 + (lane & 15)];
-			C = __builtin_amdgcn_mfma_f64_16x16x4f64(x, x, C, 0, 0, 0);
-		}
-		__builtin_amdgcn_wave_barrier();
-		const int col = lane & 15;
-#pragma unroll
-		for (int i = 0; i < 4; i++) {
-			const int rw = (lane >> 4) + 4 * i;
-			if ((rw >> 3) != (col >> 3)) continue;
-			const int node = (rw >> 3) ? nodeB : nodeA;
-			const int r0 = rw & 7, c0 = col & 7;
-			int idx = -1;
-			if (r0 < S && c0 < S && r0 <= c0) idx = r0 * S - (r0 * (r0 - 1)) / 2 + (c0 - r0);
-			else if (r0 < S && c0 == S) idx = T::NH + r0;
-			if (idx >= 0 && node >= 0) atomicAdd(a.acc + static_cast<int64_t>(node) * ACC_STRIDE + idx, C[i]);
-		}
+		float* nxt = s_slots[wave][cb ^ 1];
+		float* cur_slots = s_slots[wave][cb];
+		const int next = group(nxt);
+		wave_sync();
+		const unsigned long long tc0 = FCLOCK();
+		if (count > 0) jacobians(cur_slots, count);
+		if (next > 0) gather(nxt, next);
+		wave_sync();
+		const unsigned long long tc1 = FCLOCK();
+		if (count > 0) sums(cur_slots, count);
+		wave_sync();
+		if (FIT_STAMPS && __ballot(acc == 1.2345) == 777ull) a.acc[0] = 0;
+		const unsigned long long tc2 = FCLOCK();
+		t_jac += tc1 - tc0;
+		t_sum += tc2 - tc1;
+		if (next == 0) break;
+		cb ^= 1;
+		count = next;
 	}
-#elif NNRT_FIT_VARIANT == 17
-	while (true) {
-		const int node = next_node();
-		if (node < 0) break;
-		float Jn[S];
-		pre_jacobian(node, Jn);
-		double vals[32];
-		int e = 0;
-#pragma unroll
-		for (int c0 = 0; c0 < S; c0++)
-#pragma unroll
-			for (int c1 = c0; c1 < S; c1++) vals[e++] = static_cast<double>(Jn[c0] * Jn[c1]);
-#pragma unroll
-		for (int c = 0; c < S; c++) vals[T::NH + c] = static_cast<double>(Jn[c] * r_used);
-#pragma unroll
-		for (int c = T::NACC; c < 32; c++) vals[c] = 0.0;
-		const double total = wave_reduce32_swap(vals, lane);
-		const int idx = (lane & 1) ? 32 : (lane >> 1);
-		if (idx < T::NACC) atomicAdd(a.acc + static_cast<int64_t>(node) * ACC_STRIDE + idx, total);
+	if (cur >= 0 && e_valid) ng_flush(a.acc + static_cast<int64_t>(cur) * ACC_STRIDE + e, acc);
+	if (FIT_STAMPS) {
+		const unsigned long long t_end = FCLOCK();
+		[[maybe_unused]] const unsigned long long t_group = t_end - t_loaded - t_jac - t_sum;
+		FSTAMP_AT(1, 0, t_start);
+		FSTAMP_AT(1, 1, t_loaded);
+		FSTAMP_AT(1, 2, t_loaded + t_group);
+		FSTAMP_AT(1, 3, t_loaded + t_group + t_jac);
+		FSTAMP_AT(1, 4, t_end);
 	}
-#elif NNRT_FIT_VARIANT == 11
-	// ---- node pairs through the FP64 matrix core ----
-	// X (64 pixels x 16) = [J_A, r, 0 | J_B, r, 0] per lane, staged in LDS; XᵀX over the wave's 64 pixels by 16
-	// v_mfma_f64_16x16x4_f64 (products of float Jacobian entries are exact in double, sums in double). Diagonal 8x8
-	// blocks hold JJᵀ (rows/cols < S) and J r (column S) of node A and node B.
-	constexpr int XS = 17;   // row stride in doubles (136 B: b64-aligned, spreads the rows over the LDS banks)
-	__shared__ double s_x[PIX_BLOCK / 64][64 * XS];
-	double* xw = s_x[wave];
-	while (true) {
-		const int nodeA = next_node();
-		if (nodeA < 0) break;
-		// both nodes' slot searches first, then all their loads in flight together
-		int kkA[3], kkB[3] = {-1, -1, -1};
-		node_slots(nodeA, kkA);
-		const int nodeB = next_node();
-		if (nodeB >= 0) node_slots(nodeB, kkB);
-		SlotData dA, dB;
-		load_slots(kkA, dA);
-		load_slots(kkB, dB);
-		float JA[S], JB[S];
-		slot_jacobian(kkA, dA, JA);
-		slot_jacobian(kkB, dB, JB);
-		double* row = xw + lane * XS;
-#pragma unroll
-		for (int c = 0; c < 8; c++) {
-			row[c] = c < S ? static_cast<double>(JA[c < S ? c : 0]) : (c == S ? static_cast<double>(r_used) : 0.0);
-			row[8 + c] = c < S ? static_cast<double>(JB[c < S ? c : 0]) : (c == S ? static_cast<double>(r_used) : 0.0);
-		}
-		__builtin_amdgcn_wave_barrier();
-		typedef double d4 __attribute__((ext_vector_type(4)));
-		d4 C = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-		for (int m = 0; m < 16; m++) {
-			const double x = xw[(4 * m + (lane >> 4)) * XS + (lane & 15)];
-			C = __builtin_amdgcn_mfma_f64_16x16x4f64(x, x, C, 0, 0, 0);
-		}
-		__builtin_amdgcn_wave_barrier();
-		// lane holds C[row = (lane >> 4) + 4 i][col = lane & 15], i = 0..3
-		const int col = lane & 15;
-#pragma unroll
-		for (int i = 0; i < 4; i++) {
-			const int rw = (lane >> 4) + 4 * i;
-			if ((rw >> 3) != (col >> 3)) continue;
-			const int node = (rw >> 3) ? nodeB : nodeA;
-			const int r0 = rw & 7, c0 = col & 7;
-			int idx = -1;
-			if (r0 < S && c0 < S && r0 <= c0) idx = r0 * S - (r0 * (r0 - 1)) / 2 + (c0 - r0);
-			else if (r0 < S && c0 == S) idx = T::NH + r0;
-			if (idx >= 0 && node >= 0) atomicAdd(a.acc + static_cast<int64_t>(node) * ACC_STRIDE + idx, C[i]);
-		}
-	}
-#elif NNRT_FIT_VARIANT == 13
-	// software-pipelined: the next node's slot loads are in flight while the current node is reduced
-	int nodeA = next_node();
-	int kkA[3] = {-1, -1, -1};
-	SlotData dA;
-	if (nodeA >= 0) {
-		node_slots(nodeA, kkA);
-		load_slots(kkA, dA);
-	}
-	while (nodeA >= 0) {
-		const int nodeB = next_node();
-		int kkB[3] = {-1, -1, -1};
-		SlotData dB;
-		if (nodeB >= 0) {
-			node_slots(nodeB, kkB);
-			load_slots(kkB, dB);
-		}
-		float Jn[S];
-		slot_jacobian(kkA, dA, Jn);
-		double vals[32];
-		int e = 0;
-#pragma unroll
-		for (int c0 = 0; c0 < S; c0++)
-#pragma unroll
-			for (int c1 = c0; c1 < S; c1++) vals[e++] = static_cast<double>(Jn[c0] * Jn[c1]);
-#pragma unroll
-		for (int c = 0; c < S; c++) vals[T::NH + c] = static_cast<double>(Jn[c] * r_used);
-#pragma unroll
-		for (int c = T::NACC; c < 32; c++) vals[c] = 0.0;
-		const double total = wave_reduce32_swap(vals, lane);
-		const int idx = (lane & 1) ? 32 : (lane >> 1);
-		if (idx < T::NACC) atomicAdd(a.acc + static_cast<int64_t>(nodeA) * ACC_STRIDE + idx, total);
-		nodeA = nodeB;
-#pragma unroll
-		for (int fv = 0; fv < 3; fv++) kkA[fv] = kkB[fv];
-		dA = dB;
-	}
-#else
-	while (true) {
-		const int node = next_node();
-		if (node < 0) break;
-		float Jn[S];
-		node_jacobian(node, Jn);
-		// products rounded to float as the reference forms them (lanes without the node hold Jn = 0 -> 0 products),
-		// summed in double over the wave and across waves
-		double vals[32];
-		int e = 0;
-#pragma unroll
-		for (int c0 = 0; c0 < S; c0++)
-#pragma unroll
-			for (int c1 = c0; c1 < S; c1++) vals[e++] = static_cast<double>(Jn[c0] * Jn[c1]);
-#pragma unroll
-		for (int c = 0; c < S; c++) vals[T::NH + c] = static_cast<double>(Jn[c] * r_used);
-#pragma unroll
-		for (int c = T::NACC; c < 32; c++) vals[c] = 0.0;
-		const double total = wave_reduce32_swap(vals, lane);
-		const int idx = (lane & 1) ? 32 : (lane >> 1);   // lanes 2i, 2i+1 hold entry i
-#if NNRT_FIT_VARIANT == 18
-		if (idx < T::NACC && total == 1234.5) a.acc[idx] = total;
-#else
-		if (idx < T::NACC) atomicAdd(a.acc + static_cast<int64_t>(node) * ACC_STRIDE + idx, total);
-#endif
-	}
-#endif
-	FSTAMP(1, 2);
 }
 
 nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t stream) {
@@ -799,20 +610,20 @@ nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t st
 	NNRT_LAUNCH_CHECK();
 	// anchor slots per vertex: the common 4-anchor configuration gets its own instantiation (half the slot logic)
 	const bool k4 = args.anchor_count <= 4;
+	const unsigned grid_ng = static_cast<unsigned>(((args.tiles_x * ((args.H + 2 * NG_ROWS - 1) / (2 * NG_ROWS)) + 7) / 8) * 8);
 	switch (mode) {
 		case NNRT_ITERATION_ALL:
-			if (k4) k_node_reduce<NNRT_ITERATION_ALL, 4><<<grid, PIX_BLOCK, 0, stream>>>(args);
-			else k_node_reduce<NNRT_ITERATION_ALL, MAX_ANCHORS><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			if (k4) k_node_reduce_grouped<NNRT_ITERATION_ALL, 4><<<grid_ng, PIX_BLOCK, 0, stream>>>(args);
+			else k_node_reduce_grouped<NNRT_ITERATION_ALL, MAX_ANCHORS><<<grid_ng, PIX_BLOCK, 0, stream>>>(args);
 			break;
 		case NNRT_ITERATION_TRANSLATION_ONLY:
-			if (k4) k_node_reduce<NNRT_ITERATION_TRANSLATION_ONLY, 4><<<grid, PIX_BLOCK, 0, stream>>>(args);
-			else k_node_reduce<NNRT_ITERATION_TRANSLATION_ONLY, MAX_ANCHORS><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			if (k4) k_node_reduce_grouped<NNRT_ITERATION_TRANSLATION_ONLY, 4><<<grid_ng, PIX_BLOCK, 0, stream>>>(args);
+			else k_node_reduce_grouped<NNRT_ITERATION_TRANSLATION_ONLY, MAX_ANCHORS><<<grid_ng, PIX_BLOCK, 0, stream>>>(args);
 			break;
-		case NNRT_ITERATION_ROTATION_ONLY:
-			if (k4) k_node_reduce<NNRT_ITERATION_ROTATION_ONLY, 4><<<grid, PIX_BLOCK, 0, stream>>>(args);
-			else k_node_reduce<NNRT_ITERATION_ROTATION_ONLY, MAX_ANCHORS><<<grid, PIX_BLOCK, 0, stream>>>(args);
+		default:
+			if (k4) k_node_reduce_grouped<NNRT_ITERATION_ROTATION_ONLY, 4><<<grid_ng, PIX_BLOCK, 0, stream>>>(args);
+			else k_node_reduce_grouped<NNRT_ITERATION_ROTATION_ONLY, MAX_ANCHORS><<<grid_ng, PIX_BLOCK, 0, stream>>>(args);
 			break;
-		default: set_error("unknown iteration mode"); return NNRT_ERROR_ARGUMENT;
 	}
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;

@@ -9,7 +9,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ["NNRT_LIB_PATH"] = os.path.join(ROOT, "dynamicfuion_python_amd", "csrc", "variants", "libnnrt_v30.so")
+VARIANT = os.environ.get("STAMP_VARIANT", "30")
+os.environ["NNRT_LIB_PATH"] = os.path.join(ROOT, "dynamicfuion_python_amd", "csrc", "variants", f"libnnrt_v{VARIANT}.so")
 
 
 def report(name, st, nwaves, phases):
@@ -26,6 +27,11 @@ def report(name, st, nwaves, phases):
     life = rel[:, -1] - rel[:, 0]
     print(f"{name}: waves {ok.sum()}/{nwaves} kernel span {span:.1f} us, wave lifetime mean {life.mean():.1f} max {life.max():.1f} us, "
           f"start spread p50 {np.percentile(rel[:, 0], 50):.1f} p90 {np.percentile(rel[:, 0], 90):.1f} max {rel[:, 0].max():.1f} us")
+    blk = np.nonzero(ok)[0] // 4
+    xcd = blk % 8
+    ends = [rel[xcd == x, -1].max() if (xcd == x).any() else 0 for x in range(8)]
+    print("    per-XCD last wave end (us): " + " ".join(f"{e:.1f}" for e in ends))
+    print("    lifetime percentiles p10/p50/p90/p99: " + " ".join(f"{np.percentile(life, q):.1f}" for q in (10, 50, 90, 99)))
     d = np.diff(rel, axis=1)
     for i, ph in enumerate(phases):
         print(f"    {ph:28s} mean {d[:, i].mean():7.2f} us  p90 {np.percentile(d[:, i], 90):7.2f}")
@@ -63,7 +69,7 @@ def main():
     assert lib.nnrt_dev_fit_stamps(0, buf.ctypes.data, nw * 8) == 0
     report("k_pixel_jacobians", buf, nw, ["key/face/wpos loads+resolve", "residual+Jacobians+record"])
     assert lib.nnrt_dev_fit_stamps(1, buf.ctypes.data, nw * 8) == 0
-    report("k_node_reduce", buf, nw, ["prologue loads", "node passes"])
+    report("k_node_reduce_grouped", buf, nw, ["key/face/anchor loads", "grouping (+ final flush)", "Jacobians (sum)", "exact sums (sum)"])
 
 
 if __name__ == "__main__":
