@@ -11,10 +11,12 @@ on multi-node scenes after 2-3 iterations (SURVEY.md / DESIGN.md section "Diverg
 same state: each timed iteration does the work of the first iteration of a frame, with nothing cached between steps.
 
 N > 1: one process per GPU (torchrun), each fitting its own independent sequence (seed = rank) -- replicas, no
-collective in the data path; the only collectives are the barrier and the max-over-ranks of the elapsed time.
+collective in the data path; the only collectives are the barrier, the max-over-ranks of the elapsed time and the
+end-of-run all-gather of per-rank results.
 
-Also reported: the dominant kernel's roofline (k_fit_pixels, HIP-event timed on the fitter's work stream) and the
-CPU baseline (the oracle/ C++ restatement, OpenMP, on a bounded sample of the same workload, rank 0, N = 1).
+Also reported: the dominant kernel's roofline (k_node_reduce_grouped, HIP-event timed on the fitter's work stream; every
+other kernel of the iteration under "kernels"), the once-per-frame setup time, and the CPU baseline (the oracle/ C++
+restatement, OpenMP, on a bounded sample of the same workload, rank 0, N = 1; also at 1 thread).
 """
 from __future__ import annotations
 
@@ -29,7 +31,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM": 8 TB/s spec)
 DEFAULT_CONFIG = "C2"
-ROOFLINE_KERNEL = "k_fit_pixels"
+ROOFLINE_KERNEL = "k_node_reduce_grouped"
 
 
 # ---------------------------------------------------------------------------------------------------------------------
@@ -73,25 +75,28 @@ def stage_bytes(P: int, F: int, V: int, N: int, K: int, E: int) -> dict:
     }
 
 
-# stages fused into each kernel of one GN iteration
+# stages fused into each kernel of one GN iteration (block-diagonal configs)
 KERNEL_STAGES = {
-    "k_warp_mesh": ("warp", "warped_jacobians"),
+    "k_warp_mesh_quad": ("warp", "warped_jacobians"),
     "k_raster_scatter_mesh": ("ndc", "raster"),
-    "k_fit_pixels": ("residual", "rasterized_jacobians", "pixel_anchor_jacobians", "jtj_jtr"),
+    "k_pixel_jacobians": ("residual", "rasterized_jacobians"),
+    "k_node_reduce_grouped": ("pixel_anchor_jacobians", "jtj_jtr"),
     "k_solve_update": ("solve",),
 }
+# nnrt_fitter_iterate_timed stage -> the kernel it times
+STAGE_KERNEL = {"warp": "k_warp_mesh_quad", "raster": "k_raster_scatter_mesh", "pixel_jacobians": "k_pixel_jacobians",
+                "node_reduce": "k_node_reduce_grouped", "solve": "k_solve_update"}
 
 
 def kernel_bytes(kernel: str, sb: dict) -> int:
     return sum(sb[k] for k in KERNEL_STAGES[kernel])
 
 
-def fused_compulsory_bytes(P: int, F: int, V: int, N: int, K: int) -> int:
-    """What k_fit_pixels itself must move: per pixel the raster key (8 B read + 8 B reset), the reference
-    point (float4), residual, mask and face (9 B); each face record once (int4); per vertex warped position + normal
-    (2 x float4), anchors (4 B x K) and warped Jacobians (2 x float4 x K); per node the fp64 accumulator row (27 x 8 B
-    read-modify-write)."""
-    return P * (16 + 16 + 9) + F * 16 + V * (32 + K * 36) + N * 27 * 8 * 2
+def node_pass_compulsory_bytes(P: int, P_c: int, F: int, V: int, N: int, K: int) -> int:
+    """What k_node_reduce_grouped itself must move: per pixel the pass-1 key (8 B read + 8 B reset); per
+    contributing pixel its 64-B Jacobian record; each face record once (int4); per vertex its anchors (4 B x K) and
+    warped-Jacobian rows (2 x float4 x K); per node the fp64 accumulator row (27 x 8 B read-modify-write)."""
+    return P * 16 + P_c * 64 + F * 16 + V * K * (4 + 32) + N * 27 * 8 * 2
 
 
 def count_associations(pixel_faces, residual_mask, faces, anchors) -> int:
@@ -143,19 +148,46 @@ def load_traffic(path: str, workload: str):
             t = json.load(f)
     except (OSError, ValueError):
         return None, None
-    if t.get("workload") != workload or t.get("kernel") != ROOFLINE_KERNEL:
+    if t.get("workload") != workload or ROOFLINE_KERNEL not in t.get("kernels", {}):
         return None, None
-    return t.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    return t["kernels"][ROOFLINE_KERNEL].get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
 
 
-def cpu_baseline(sc, depth_host, threads: int, budget_s: float):
+def host_cpu():
+    """CPU model, sockets and logical CPUs of this host (/proc/cpuinfo; os.cpu_count() is the whole machine)."""
+    model, sockets = None, set()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and model is None:
+                    model = v
+                elif k == "physical id":
+                    sockets.add(v)
+    except OSError:
+        pass
+    return dict(model=model, sockets=len(sockets) or None, logical_cpus=os.cpu_count())
+
+
+def cpu_baseline(sc, depth_host, threads: int, budget_s: float, single_thread_s: float = 4.0):
     """The oracle (C++/OpenMP restatement of the reference CPU path; test infrastructure, used here only as the
     reported baseline) running the same step: 1 GN iteration from the identity warp. Timed = loop body S1-S12
-    (DeformableMeshToImageFitter.cpp:111-275), once-per-frame setup excluded, as in the GPU step."""
+    (DeformableMeshToImageFitter.cpp:111-275), once-per-frame setup excluded, as in the GPU step. Run with `threads`
+    OpenMP threads (the headline) and again with 1 thread on a smaller sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    O.set_num_threads(threads)
     refp, refm = O.unproject(depth_host, sc.K, 1.0, 10.0)
+    res = _cpu_sample(O, sc, refp, refm, threads, budget_s)
+    one = _cpu_sample(O, sc, refp, refm, 1, single_thread_s)
+    res["single_thread"] = dict(value=one["value"], unit=one["unit"], cores=1, ms_per_solve=one["ms_per_solve"],
+                                sample=one["sample"])
+    res["host"] = host_cpu()
+    return res
+
+
+def _cpu_sample(O, sc, refp, refm, threads: int, budget_s: float):
+    O.set_num_threads(threads)
     N = len(sc.nodes)
     R0 = np.tile(np.eye(3, dtype=np.float32), (N, 1, 1))
     t0 = np.zeros((N, 3), np.float32)
@@ -245,7 +277,7 @@ def main(argv=None):
     agg = aggregate(args.steps, elapsed_max, world)
 
     # per-stage device time (eager launches, HIP events on the fitter's work stream), same step
-    stages = dict(warp=0.0, raster=0.0, pixels=0.0, arap=0.0, solve=0.0)
+    stages = {k: 0.0 for k in A.TIMED_STAGES}
     for _ in range(args.timed_steps):
         wf.reset_motion()
         r = ft.iterate_timed(wf, 0, 1)
@@ -260,12 +292,34 @@ def main(argv=None):
 
     anchors, _ = ft.anchors(V, 4)
     E = count_associations(dg["pixel_faces"], dg["residual_mask"], sc.faces, anchors)
+    P_c = int(dg["residual_mask"].sum())
     sb = stage_bytes(P, F, V, Nn, 4, E)
-    kbytes = kernel_bytes(ROOFLINE_KERNEL, sb)
-    k_ms = stages["pixels"]
+    kernels = {}
+    for stage, kname in STAGE_KERNEL.items():
+        kb = kernel_bytes(kname, sb)
+        ms = stages[stage]
+        kernels[kname] = dict(ms=round(ms, 5), algorithmic_bytes=kb, frac=kb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS if ms > 0 else None)
+    kbytes = kernels[ROOFLINE_KERNEL]["algorithmic_bytes"]
+    k_ms = stages["node_reduce"]
     achieved = kbytes / (k_ms * 1e-3) / 1e9
     it_bytes = sum(sb.values())
     traffic, traffic_src = load_traffic(args.traffic_file, workload)
+
+    # once-per-frame setup (DeformableMeshToImageFitter.cpp:96-106: anchors, reference point cloud, buffers), timed
+    # on a repeated prepare() of the same frame
+    torch.cuda.synchronize(dev)
+    t_setup = time.perf_counter()
+    ft.prepare(wf, mesh, depth, None, sc.K)
+    torch.cuda.synchronize(dev)
+    setup_ms = (time.perf_counter() - t_setup) * 1000.0
+
+    # end-of-run exchange of per-rank results: iterations/s, seconds, final |update|
+    per_rank = None
+    if world > 1:
+        mine = torch.tensor([args.steps / elapsed, elapsed, float(np.linalg.norm(dg["updates"]))], dtype=torch.float64, device=dev)
+        got = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(got, mine)
+        per_rank = [dict(rank=i, iters_per_s=float(g[0]), seconds=float(g[1]), update_norm=float(g[2])) for i, g in enumerate(got)]
 
     out = {
         "metric": "GN iters/sec (640x480, 1.5k-node graph)" if args.config == "C2" else f"GN iters/sec ({args.config})",
@@ -284,14 +338,17 @@ def main(argv=None):
         "config": {"workload": workload, "config": args.config, "frame": [sc.H, sc.W], "nodes": Nn, "vertices": V, "triangles": F,
                    "anchors": 4, "iteration_mode": "ALL", "lm_damping": 0.001, "hip_graph": True,
                    "parallelism": f"replicas{world}" if world > 1 else "single"},
+        "setup_ms": round(setup_ms, 3),
         "stage_ms": {k: round(v, 5) for k, v in stages.items()},
         "roofline": {"kernel": ROOFLINE_KERNEL, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "algorithmic_bytes": kbytes, "kernel_ms": k_ms,
-                     "bytes_formula": "SURVEY.md 8(d): residual + rasterized Jacobians + pixel-anchor Jacobians + JtJ/Jtr rows",
-                     "associations_E": E, "traffic_source": traffic_src,
-                     "fused_compulsory_bytes": fused_compulsory_bytes(P, F, V, Nn, 4),
+                     "bytes_formula": "SURVEY.md 8(d): pixel-anchor Jacobians + JtJ/Jtr rows (P*257 + P*72K + 4E + E*28 + P*5 + 168N)",
+                     "associations_E": E, "contributing_pixels": P_c, "traffic_source": traffic_src,
+                     "compulsory_bytes": node_pass_compulsory_bytes(P, P_c, F, V, Nn, 4),
                      "iteration_algorithmic_bytes": it_bytes,
                      "iteration_frac": it_bytes / (agg["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS},
+        "kernels": kernels,
+        "per_rank": per_rank,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -430,8 +430,8 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 	fa.residual_mask = ft->residual_mask.ptr;
 	fa.pixel_face = ft->pixel_face.ptr;
 	fa.acc = ft->acc.ptr;
-	if ((st = launch_fit_pixels(mode, fa, s))) return st;
-	if ((st = mark(3))) return st;
+	if ((st = launch_fit_pixels(mode, fa, s, marks ? marks[3] : nullptr))) return st;
+	if ((st = mark(4))) return st;
 	if (ft->E > 0) {
 		ArapArgs aa{};
 		aa.E = ft->E;
@@ -451,13 +451,13 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 		aa.edge_residuals = ft->edge_residuals.ptr;
 		aa.error_flag = ft->error_flag.ptr;
 		if ((st = launch_arap_edges(aa, s))) return st;
-		if ((st = mark(4))) return st;
+		if ((st = mark(5))) return st;
 		const float lm = ft->p.preconditioning_dampening_factor;
 		if ((st = launch_arrowhead_iteration(ft->aw, ft->acc.ptr, lm, wf->edges.ptr, ft->wing.ptr, wf->state.ptr, ft->arap_acc.ptr,
 		                                     ft->updates.ptr, ft->gradient.ptr, ft->hessian.ptr, ft->error_flag.ptr, s)))
 			return st;
 	} else {
-		if ((st = mark(4))) return st;
+		if ((st = mark(5))) return st;
 		SolveArgs sa{};
 		sa.N = ft->N;
 		sa.lm = ft->p.preconditioning_dampening_factor;
@@ -469,7 +469,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 		sa.error_flag = ft->error_flag.ptr;
 		if ((st = launch_solve_update(mode, sa, s))) return st;
 	}
-	return mark(5);
+	return mark(6);
 }
 
 } // namespace
@@ -736,22 +736,23 @@ nnrt_status nnrt_fitter_iterate_timed(nnrt_fitter* ft, nnrt_warp_field* wf, int3
 	hipStream_t us = static_cast<hipStream_t>(stream);
 	NNRT_HIP(hipEventRecord(ft->ev_in, us));
 	NNRT_HIP(hipStreamWaitEvent(ft->work, ft->ev_in, 0));
-	std::vector<hipEvent_t> ev(static_cast<size_t>(count) * 6, nullptr);
+	constexpr int NS = NNRT_TIMED_STAGES;
+	std::vector<hipEvent_t> ev(static_cast<size_t>(count) * (NS + 1), nullptr);
 	for (auto& e : ev) NNRT_HIP(hipEventCreate(&e));
 	nnrt_status st = NNRT_OK;
 	for (int i = 0; i < count && !st; i++) {
 		const int it = first_iteration + i;
 		const int mode = ft->p.iteration_modes[it % ft->p.iteration_mode_count];
 		ft->last_mode = mode;
-		st = enqueue_iteration(ft, wf, mode, ft->work, &ev[static_cast<size_t>(i) * 6]);
+		st = enqueue_iteration(ft, wf, mode, ft->work, &ev[static_cast<size_t>(i) * (NS + 1)]);
 	}
 	if (!st) {
 		NNRT_HIP(hipStreamSynchronize(ft->work));
-		for (int k = 0; k < 5; k++) h_stage_ms[k] = 0.f;
+		for (int k = 0; k < NS; k++) h_stage_ms[k] = 0.f;
 		for (int i = 0; i < count; i++)
-			for (int k = 0; k < 5; k++) {
+			for (int k = 0; k < NS; k++) {
 				float ms = 0.f;
-				NNRT_HIP(hipEventElapsedTime(&ms, ev[static_cast<size_t>(i) * 6 + k], ev[static_cast<size_t>(i) * 6 + k + 1]));
+				NNRT_HIP(hipEventElapsedTime(&ms, ev[static_cast<size_t>(i) * (NS + 1) + k], ev[static_cast<size_t>(i) * (NS + 1) + k + 1]));
 				h_stage_ms[k] += ms / count;
 			}
 	}

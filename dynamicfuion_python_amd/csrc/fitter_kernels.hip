@@ -598,7 +598,7 @@ __global__ __launch_bounds__(PIX_BLOCK, 5) void k_node_reduce_grouped(FitPixelAr
 	}
 }
 
-nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t stream) {
+nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t stream, hipEvent_t between) {
 	const int tiles = args.tiles_x * args.tiles_y;
 	const unsigned grid = static_cast<unsigned>(((tiles + 7) / 8) * 8);
 	switch (mode) {
@@ -608,6 +608,10 @@ nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t st
 		default: set_error("unknown iteration mode"); return NNRT_ERROR_ARGUMENT;
 	}
 	NNRT_LAUNCH_CHECK();
+	if (between && hipEventRecord(between, stream) != hipSuccess) {
+		set_error("hipEventRecord failed");
+		return NNRT_ERROR_HIP;
+	}
 	// anchor slots per vertex: the common 4-anchor configuration gets its own instantiation (half the slot logic)
 	const bool k4 = args.anchor_count <= 4;
 	const unsigned grid_ng = static_cast<unsigned>(((args.tiles_x * ((args.H + 2 * NG_ROWS - 1) / (2 * NG_ROWS)) + 7) / 8) * 8);

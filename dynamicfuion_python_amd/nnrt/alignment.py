@@ -12,6 +12,9 @@ from .. import _native as N
 from ._tensors import to_device, to_host_f64
 from .geometry import HierarchicalGraphWarpField, TriangleMesh
 
+# nnrt_fitter_iterate_timed stage order (include/nnrt_mi355x.h, NNRT_TIMED_STAGES)
+TIMED_STAGES = ("warp", "raster", "pixel_jacobians", "node_reduce", "arap", "solve")
+
 
 class IterationMode(enum.IntEnum):
     ALL = 0
@@ -102,9 +105,9 @@ class DeformableMeshToImageFitter:
 
     def iterate_timed(self, warp_field: HierarchicalGraphWarpField, first_iteration: int = 0, count: int = 1, stream=None) -> dict:
         """Eager iterations with HIP events between stages; returns average device ms per iteration per stage."""
-        ms = np.zeros(5, np.float32)
+        ms = np.zeros(len(TIMED_STAGES), np.float32)
         N.check(N.lib().nnrt_fitter_iterate_timed(self._h, warp_field.handle, int(first_iteration), int(count), N.ptr(ms), N.stream_ptr(stream)))
-        return dict(warp=float(ms[0]), raster=float(ms[1]), pixels=float(ms[2]), arap=float(ms[3]), solve=float(ms[4]))
+        return {name: float(v) for name, v in zip(TIMED_STAGES, ms)}
 
     def check(self, stream=None):
         N.check(N.lib().nnrt_fitter_check(self._h, N.stream_ptr(stream)))

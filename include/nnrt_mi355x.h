@@ -124,9 +124,11 @@ nnrt_status nnrt_fitter_fit_to_point_cloud(nnrt_fitter* fitter, nnrt_warp_field*
                                            const double* h_K, const double* h_E, void* stream);
 /* Iterations are enqueued on `stream` itself (graphs: captured once per iteration mode, replayed on `stream`). */
 nnrt_status nnrt_fitter_iterate(nnrt_fitter* fitter, nnrt_warp_field* warp_field, int32_t first_iteration, int32_t count, void* stream);
-/* iterate() without graphs, with HIP events between the stages of every iteration; h_stage_ms[5] receives the average
- * per-iteration device time of: 0 warp (+warped Jacobians), 1 raster scatter, 2 fused pixel kernel, 3 ARAP edges,
- * 4 linear solve + update ("ms/solve"). Synchronizes `stream`. */
+/* iterate() without graphs, with HIP events between the stages of every iteration; h_stage_ms[NNRT_TIMED_STAGES]
+ * receives the average per-iteration device time of: 0 warp (+warped Jacobians), 1 raster scatter, 2 pixel pass
+ * (residuals + rasterized Jacobians, k_pixel_jacobians), 3 node pass (node Jacobians + JtJ / Jt r,
+ * k_node_reduce_grouped), 4 ARAP edges, 5 linear solve + update ("ms/solve"). Synchronizes `stream`. */
+#define NNRT_TIMED_STAGES 6
 nnrt_status nnrt_fitter_iterate_timed(nnrt_fitter* fitter, nnrt_warp_field* warp_field, int32_t first_iteration, int32_t count,
                                       float* h_stage_ms, void* stream);
 /* Reports (and clears) a failure recorded on the device by earlier iterate() calls (e.g. a non-positive-definite block,

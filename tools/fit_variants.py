@@ -25,7 +25,7 @@ def child(config, steps):
     wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE, 1)
     ft = A.DeformableMeshToImageFitter(1, [A.IterationMode.ALL], preconditioning_dampening_factor=0.001)
     ft.prepare(wf, G.TriangleMesh(sc.points, sc.normals, sc.faces), depth, None, sc.K)
-    acc = dict(warp=0.0, raster=0.0, pixels=0.0, arap=0.0, solve=0.0)
+    acc = {k: 0.0 for k in A.TIMED_STAGES}
     for i in range(steps + 5):
         wf.reset_motion()
         r = ft.iterate_timed(wf, 0, 1)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""HBM traffic per launch of one kernel from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; csv output).
+"""HBM traffic per launch of the GN-iteration kernels from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; csv).
 
 gfx950 corrections (MI355X_MICROARCH.md "HBM"): FETCH_SIZE counts KiB at half the bytes of a wide coalesced read
 (128-B requests tallied at 64 B) -> doubled; WRITE_SIZE counts KiB exactly. traffic = (2 * FETCH_SIZE + WRITE_SIZE) *
@@ -24,19 +24,22 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fetch", default="gpurun_out/pmc_fetch/**/*counter_collection.csv")
     ap.add_argument("--write", default="gpurun_out/pmc_write/**/*counter_collection.csv")
-    ap.add_argument("--kernel", default="k_fit_pixels<0>")
+    ap.add_argument("--kernels", nargs="+", default=["k_node_reduce_grouped<0, 4>", "k_pixel_jacobians<0>", "k_raster_scatter_mesh",
+                                                      "k_warp_mesh_quad", "k_solve_update<0>"])
     ap.add_argument("--workload", required=True, help="bench.py config.workload string the passes ran")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
-    f = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
-    w = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
-    if not f or not w:
-        raise SystemExit(f"no dispatches of {a.kernel}: fetch {len(f)} write {len(w)}")
-    fetch_kib = sum(f) / len(f)
-    write_kib = sum(w) / len(w)
-    out = {"kernel": "k_fit_pixels", "kernel_symbol": a.kernel, "workload": a.workload, "dispatches": [len(f), len(w)],
-           "fetch_size_kib": fetch_kib, "write_size_kib": write_kib,
-           "hbm_bytes_per_launch": (2 * fetch_kib + write_kib) * 1024.0,
+    kernels = {}
+    for sym in a.kernels:
+        f = per_dispatch(a.fetch, "FETCH_SIZE", sym)
+        w = per_dispatch(a.write, "WRITE_SIZE", sym)
+        if not f or not w:
+            raise SystemExit(f"no dispatches of {sym}: fetch {len(f)} write {len(w)}")
+        fetch_kib = sum(f) / len(f)
+        write_kib = sum(w) / len(w)
+        kernels[sym.split("<")[0]] = {"kernel_symbol": sym, "dispatches": [len(f), len(w)], "fetch_size_kib": fetch_kib,
+                                      "write_size_kib": write_kib, "hbm_bytes_per_launch": (2 * fetch_kib + write_kib) * 1024.0}
+    out = {"workload": a.workload, "kernels": kernels,
            "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count correction)"}
     text = json.dumps(out, indent=1)
     print(text)
