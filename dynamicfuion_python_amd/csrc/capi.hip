@@ -81,6 +81,17 @@ struct DeviceBuffer {
 	}
 };
 
+template <typename T>
+nnrt_status upload(DeviceBuffer<T>& buf, const std::vector<T>& host) {
+	nnrt_status st = buf.ensure(host.size());
+	if (st) return st;
+	if (!host.empty() && hipMemcpy(buf.ptr, host.data(), sizeof(T) * host.size(), hipMemcpyHostToDevice) != hipSuccess) {
+		set_error("hipMemcpy failed");
+		return NNRT_ERROR_HIP;
+	}
+	return NNRT_OK;
+}
+
 struct DeviceGuard {
 	int prev = -1;
 	explicit DeviceGuard(int device) {
@@ -342,8 +353,9 @@ struct nnrt_fitter {
 	DeviceBuffer<float> updates, gradient, hessian;
 	DeviceBuffer<int> error_flag;
 	// ARAP / arrowhead
-	DeviceBuffer<float> wing, edge_residuals, a_diag, a_dinv, a_dinvb, a_schur, a_rhs, a_x;
-	DeviceBuffer<int> a_offsets, a_list;
+	DeviceBuffer<float> wing, edge_residuals, a_diag, a_dinv, a_dinvb, a_schur, a_linv, a_cb, a_rhs, a_x;
+	DeviceBuffer<int> a_offsets, a_list, a_tgt_off, a_rhs_off, a_rhs_edges;
+	DeviceBuffer<int2> a_tgt_ab, a_pairs;
 	ArrowheadWorkspace aw;
 	int n0 = 0;
 	int last_mode = 0;
@@ -526,7 +538,7 @@ void nnrt_fitter_destroy(nnrt_fitter* ft) {
 	ft->ref_points.release();
 	ft->records.release();
 	for (auto* b : {&ft->mesh_p, &ft->mesh_n, &ft->weights, &ft->residuals, &ft->arap_acc, &ft->updates, &ft->gradient,
-	                &ft->hessian, &ft->wing, &ft->edge_residuals, &ft->a_diag, &ft->a_dinv, &ft->a_dinvb, &ft->a_schur, &ft->a_rhs, &ft->a_x})
+	                &ft->hessian, &ft->wing, &ft->edge_residuals, &ft->a_diag, &ft->a_dinv, &ft->a_dinvb, &ft->a_schur, &ft->a_linv, &ft->a_cb, &ft->a_rhs, &ft->a_x})
 		b->release();
 	ft->faces4.release();
 	ft->anchors.release();
@@ -540,6 +552,11 @@ void nnrt_fitter_destroy(nnrt_fitter* ft) {
 	ft->error_flag.release();
 	ft->a_offsets.release();
 	ft->a_list.release();
+	ft->a_tgt_off.release();
+	ft->a_rhs_off.release();
+	ft->a_rhs_edges.release();
+	ft->a_tgt_ab.release();
+	ft->a_pairs.release();
 	if (ft->ev_in) hipEventDestroy(ft->ev_in);
 	if (ft->ev_out) hipEventDestroy(ft->ev_out);
 	if (ft->work) hipStreamDestroy(ft->work);
@@ -589,10 +606,11 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	ft->E = E;
 	ft->n0 = wf->h.layer_counts.empty() ? N : wf->h.layer_counts[0];
 	if (E > 0) {
-		const int n0 = ft->n0, m = 6 * (N - n0);
+		const int n0 = ft->n0, m = 6 * (N - n0), ld = corner_ld(m);
 		if ((st = ft->wing.ensure(static_cast<size_t>(E) * 36)) || (st = ft->edge_residuals.ensure(3 * static_cast<size_t>(E))) ||
 		    (st = ft->a_diag.ensure(static_cast<size_t>(N) * 36)) || (st = ft->a_dinv.ensure(static_cast<size_t>(n0) * 36)) ||
-		    (st = ft->a_dinvb.ensure(static_cast<size_t>(E) * 36)) || (st = ft->a_schur.ensure(static_cast<size_t>(m) * m)) ||
+		    (st = ft->a_dinvb.ensure(static_cast<size_t>(E) * 36)) || (st = ft->a_schur.ensure(static_cast<size_t>(ld) * ld)) ||
+		    (st = ft->a_linv.ensure(static_cast<size_t>(ld) * CORNER_NB)) || (st = ft->a_cb.ensure(static_cast<size_t>(ld))) ||
 		    (st = ft->a_rhs.ensure(6 * static_cast<size_t>(N))) || (st = ft->a_x.ensure(6 * static_cast<size_t>(N))) ||
 		    (st = ft->a_offsets.ensure(n0 + 1)) || (st = ft->a_list.ensure(E)))
 			return st;
@@ -610,10 +628,23 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 		}
 		NNRT_HIP(hipMemcpy(ft->a_offsets.ptr, counts.data(), sizeof(int) * (n0 + 1), hipMemcpyHostToDevice));
 		NNRT_HIP(hipMemcpy(ft->a_list.ptr, list.data(), sizeof(int) * E, hipMemcpyHostToDevice));
+		const StemSchurLists sl = build_stem_schur_lists(wf->h.edges.data(), E, n0, N);
+		if ((st = upload(ft->a_tgt_off, sl.tgt_off)) || (st = upload(ft->a_tgt_ab, sl.tgt_ab)) || (st = upload(ft->a_pairs, sl.pairs)) ||
+		    (st = upload(ft->a_rhs_off, sl.rhs_off)) || (st = upload(ft->a_rhs_edges, sl.rhs_edges)))
+			return st;
+		ft->aw.targets = static_cast<int>(sl.tgt_ab.size());
+		ft->aw.tgt_off = ft->a_tgt_off.ptr;
+		ft->aw.tgt_ab = ft->a_tgt_ab.ptr;
+		ft->aw.pairs = ft->a_pairs.ptr;
+		ft->aw.rhs_off = ft->a_rhs_off.ptr;
+		ft->aw.rhs_edges = ft->a_rhs_edges.ptr;
 		ft->aw.N = N;
 		ft->aw.n0 = n0;
 		ft->aw.E = E;
 		ft->aw.m = m;
+		ft->aw.ld = ld;
+		ft->aw.linv = ft->a_linv.ptr;
+		ft->aw.cb = ft->a_cb.ptr;
 		ft->aw.diag = ft->a_diag.ptr;
 		ft->aw.dinv = ft->a_dinv.ptr;
 		ft->aw.dinv_b = ft->a_dinvb.ptr;
@@ -959,16 +990,32 @@ nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, cons
 	ws.n0 = n0;
 	ws.E = E;
 	ws.m = 6 * (N - n0);
+	ws.ld = corner_ld(ws.m);
 	int* flag = nullptr;
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.dinv), sizeof(float) * 36 * std::max(n0, 1), s));
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.dinv_b), sizeof(float) * 36 * std::max(E, 1), s));
-	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.schur), sizeof(float) * std::max<int64_t>(static_cast<int64_t>(ws.m) * ws.m, 1), s));
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.schur), sizeof(float) * std::max<int64_t>(static_cast<int64_t>(ws.ld) * ws.ld, 1), s));
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.linv), sizeof(float) * std::max<int64_t>(static_cast<int64_t>(ws.ld) * CORNER_NB, 1), s));
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.cb), sizeof(float) * std::max(ws.ld, 1), s));
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.edge_offsets), sizeof(int) * (n0 + 1), s));
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.edge_list), sizeof(int) * std::max(E, 1), s));
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&flag), sizeof(int), s));
 	NNRT_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
 	NNRT_HIP(hipMemcpyAsync(ws.edge_offsets, counts.data(), sizeof(int) * (n0 + 1), hipMemcpyHostToDevice, s));
 	NNRT_HIP(hipMemcpyAsync(ws.edge_list, list.data(), sizeof(int) * std::max(E, 1), hipMemcpyHostToDevice, s));
+	const StemSchurLists sl = build_stem_schur_lists(coords.data(), E, n0, N);
+	ws.targets = static_cast<int>(sl.tgt_ab.size());
+	auto dev_copy = [&](const auto& v, auto** out) -> hipError_t {
+		using T = typename std::decay_t<decltype(v)>::value_type;
+		hipError_t e = hipMallocAsync(reinterpret_cast<void**>(out), sizeof(T) * std::max<size_t>(v.size(), 1), s);
+		if (e == hipSuccess && !v.empty()) e = hipMemcpyAsync(*out, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, s);
+		return e;
+	};
+	NNRT_HIP(dev_copy(sl.tgt_off, &ws.tgt_off));
+	NNRT_HIP(dev_copy(sl.tgt_ab, &ws.tgt_ab));
+	NNRT_HIP(dev_copy(sl.pairs, &ws.pairs));
+	NNRT_HIP(dev_copy(sl.rhs_off, &ws.rhs_off));
+	NNRT_HIP(dev_copy(sl.rhs_edges, &ws.rhs_edges));
 	ws.diag = const_cast<float*>(d_diag);
 	ws.rhs = const_cast<float*>(d_b);
 	ws.x = d_x;
@@ -978,7 +1025,9 @@ nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, cons
 		NNRT_HIP(hipMemcpyAsync(&host_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
 		NNRT_HIP(hipStreamSynchronize(s));
 	}
-	for (void* p : {static_cast<void*>(ws.dinv), static_cast<void*>(ws.dinv_b), static_cast<void*>(ws.schur), static_cast<void*>(ws.edge_offsets),
+	for (void* p : {static_cast<void*>(ws.dinv), static_cast<void*>(ws.dinv_b), static_cast<void*>(ws.schur), static_cast<void*>(ws.linv),
+	                static_cast<void*>(ws.cb), static_cast<void*>(ws.tgt_off), static_cast<void*>(ws.tgt_ab), static_cast<void*>(ws.pairs),
+	                static_cast<void*>(ws.rhs_off), static_cast<void*>(ws.rhs_edges), static_cast<void*>(ws.edge_offsets),
 	                static_cast<void*>(ws.edge_list), static_cast<void*>(flag)})
 		hipFreeAsync(p, s);
 	if (st) return st;

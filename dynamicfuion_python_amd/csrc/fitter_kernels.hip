@@ -308,35 +308,28 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_pixel_jacobians(FitPixelArgs a) {
 //     at a node change the group adds its totals to the node's fp64 row (one 27-lane atomic). No cross-lane reduction.
 // Chunks are software-pipelined over two LDS buffers: the jv / jn row gathers of chunk c + 1 are in flight while
 // chunk c is summed, and chunk c + 1 is grouped while chunk c's gathers land. Pixel records are staged in LDS.
-constexpr int NG_CAP = 52;     // associations per chunk (one lane each in (2))
-constexpr int NG_BATCH = 8;    // associations per group read ahead in (3)
+constexpr int NG_CAP = 48;     // associations per chunk (one lane each in (2)); lane group g of (3) owns slots
+                               // [g * NG_CAP / G, (g + 1) * NG_CAP / G), zero-padded past the chunk's count
 // Slot buffers are component-major (word c of slot i at c * NG_STRIDE + i; odd stride: the words one lane group reads
 // in (3) fall in distinct LDS banks). Words: (1) pixel lane, jv/jn row per face vertex (-1: none), node at word 7;
-// (2) J[0..S-1], r at word S.
-constexpr int NG_STRIDE = 59;
-constexpr int ng_read_end(int g) {   // one past the last slot (3) reads for any chunk size, with g lane groups
-	int m = 0;
-	for (int count = 1; count <= NG_CAP; count++) {
-		const int steps = (count + g - 1) / g;
-		const int end = (g - 1) * count / g + (steps + NG_BATCH - 1) / NG_BATCH * NG_BATCH;
-		m = end > m ? end : m;
-	}
-	return m;
-}
+// (2) J[0..S-1], r at word S (zeros past the count, whose node word repeats the chunk's last node).
+constexpr int NG_STRIDE = 49;
 constexpr int NG_ROWS = 8;     // pixel rows per wave (8 x NG_ROWS pixels)
 
 __device__ inline void ng_flush(double* dst, double v) { atomicAdd(dst, v); }
 
 template <int MODE, int MAXK>
-__global__ __launch_bounds__(PIX_BLOCK, 5) void k_node_reduce_grouped(FitPixelArgs a) {
+__global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_grouped(FitPixelArgs a) {
 	using T = ModeTraits<MODE>;
 	constexpr int S = T::S;
 	constexpr int NSLOT = 3 * MAXK;
 	constexpr int GROUP = T::NACC > 16 ? 32 : 16;
 	constexpr int G = 64 / GROUP;
-	static_assert(T::NACC <= GROUP && ng_read_end(G) <= NG_STRIDE && (NG_STRIDE & 1), "slot layout");
-	__shared__ float s_rec[PIX_BLOCK / 64][16 * 64];                 // component-major pixel records
+	constexpr int SEG = NG_CAP / G;
+	constexpr int NG_BATCH = SEG % 8 == 0 ? 8 : 6;   // associations per group read ahead in (3)
+	static_assert(T::NACC <= GROUP && NG_CAP % G == 0 && SEG % NG_BATCH == 0 && NG_STRIDE >= NG_CAP && (NG_STRIDE & 1), "slot layout");
 	__shared__ float s_slots[PIX_BLOCK / 64][2][8 * NG_STRIDE];
+	__shared__ float s_rec[PIX_BLOCK / 64][16 * 64];                 // component-major pixel records
 
 	// tiles of 16 x (2 NG_ROWS) pixels, one 8 x NG_ROWS block per wave
 	const int tiles_y = (a.H + 2 * NG_ROWS - 1) / (2 * NG_ROWS);
@@ -471,6 +464,12 @@ __global__ __launch_bounds__(PIX_BLOCK, 5) void k_node_reduce_grouped(FitPixelAr
 	};
 	// (2b) J and r of association `lane` into its slot
 	auto jacobians = [&](float* slots, int count) {
+		if (lane >= count && lane < NG_CAP) {   // padding: zero products, continuing the chunk's last node
+			const float last = slots[7 * NG_STRIDE + count - 1];
+#pragma unroll
+			for (int c = 0; c <= S; c++) slots[c * NG_STRIDE + lane] = 0.f;
+			slots[7 * NG_STRIDE + lane] = last;
+		}
 		if (lane < count) {
 			const int l = d.x;
 			const int rows[3] = {d.y, d.z, d.w};
@@ -523,22 +522,19 @@ __global__ __launch_bounds__(PIX_BLOCK, 5) void k_node_reduce_grouped(FitPixelAr
 	};
 	// (3) exact sums of the chunk's products per node
 	auto sums = [&](const float* slots, int count) {
-		const int lo = (grp * count) / G, hi = ((grp + 1) * count) / G;
-		const int steps = (count + G - 1) / G;
-		for (int j = 0; j < steps; j += NG_BATCH) {
-			// every LDS read of the batch is issued before the dependent double adds (slots past `hi` are another
-			// group's or padding and are masked)
-			const float* base = slots + (lo + j);
+		(void)count;
+#pragma unroll
+		for (int j = 0; j < SEG; j += NG_BATCH) {
+			// every LDS read of the batch is issued before the dependent double adds
+			const float* base = slots + grp * SEG + j;
 			int nodes[NG_BATCH];
 			float prod[NG_BATCH];
 			bool same = true;
 #pragma unroll
 			for (int q = 0; q < NG_BATCH; q++) {
-				const bool valid = lo + j + q < hi;
 				nodes[q] = __builtin_bit_cast(int, base[7 * NG_STRIDE + q]);
-				const float x = base[c0 * NG_STRIDE + q] * base[c1 * NG_STRIDE + q];
-				prod[q] = valid ? x : 0.f;
-				same &= !valid || nodes[q] == cur;
+				prod[q] = base[c0 * NG_STRIDE + q] * base[c1 * NG_STRIDE + q];
+				same &= nodes[q] == cur;
 			}
 			if (__all(same)) {
 				// independent partial sums: the double adds of a batch do not wait on one another
@@ -549,7 +545,7 @@ __global__ __launch_bounds__(PIX_BLOCK, 5) void k_node_reduce_grouped(FitPixelAr
 			} else {
 #pragma unroll
 				for (int q = 0; q < NG_BATCH; q++) {
-					if (lo + j + q < hi && nodes[q] != cur) {
+					if (nodes[q] != cur) {
 						if (cur >= 0 && e_valid) ng_flush(a.acc + static_cast<int64_t>(cur) * ACC_STRIDE + e, acc);
 						acc = 0.0;
 						cur = nodes[q];

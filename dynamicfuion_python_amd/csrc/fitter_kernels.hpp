@@ -1,6 +1,8 @@
 // Argument blocks of the GN-iteration kernels (passed by value; stable pointers so iterations can be hipGraph-captured).
 #pragma once
 
+#include <vector>
+
 #include "kernels.hpp"
 
 namespace nnrt {
@@ -66,17 +68,37 @@ struct ArapArgs {
 };
 nnrt_status launch_arap_edges(const ArapArgs& args, hipStream_t stream);
 
+constexpr int CORNER_NB = 64;   // dense-corner Cholesky block size (the corner is padded to a multiple with identity)
+inline int corner_ld(int m) { return (m + CORNER_NB - 1) / CORNER_NB * CORNER_NB; }
+
 struct ArrowheadWorkspace {
 	int N = 0, n0 = 0, E = 0, m = 0;
+	int ld = 0;                 // corner_ld(m): padded corner size and row stride of `schur`
 	float* diag = nullptr;      // [N,36] full diagonal blocks (with LM)
 	float* dinv = nullptr;      // [n0,36]
 	float* dinv_b = nullptr;    // [E,36]
-	float* schur = nullptr;     // [m,m]
+	float* schur = nullptr;     // [ld,ld] Schur complement of the stem (lower triangle factored in place)
+	float* linv = nullptr;      // [ld/64, 64, 64] inverses of the corner's diagonal Cholesky blocks
+	float* cb = nullptr;        // [ld] corner right-hand side / solution (zero padded)
 	float* rhs = nullptr;       // [6N] negative gradient
 	float* x = nullptr;         // [6N]
 	int* edge_offsets = nullptr;// [n0+1] CSR of stem edges by source node (edges grouped by source)
 	int* edge_list = nullptr;   // [E]
+	// Schur update S -= B^T D^-1 B grouped by target block (lower block triangle), and b_C -= B^T D^-1 b_D by corner
+	// node: each target is written by one owner, no atomics (build_stem_schur_lists)
+	int targets = 0;
+	int* tgt_off = nullptr;     // [targets+1] CSR into `pairs`
+	int2* tgt_ab = nullptr;     // [targets] (a, b) corner block coordinates, a >= b
+	int2* pairs = nullptr;      // (e1, e2): stem edges i->a, i->b of one stem node i
+	int* rhs_off = nullptr;     // [N - n0 + 1] CSR into `rhs_edges` by corner node
+	int* rhs_edges = nullptr;   // stem edges into each corner node
 };
+struct StemSchurLists {
+	std::vector<int> tgt_off, rhs_off, rhs_edges;
+	std::vector<int2> tgt_ab, pairs;
+};
+// host: group the stem's edge pairs by Schur target block (edges [E,2] host, virtual order; stem = first n0 nodes)
+StemSchurLists build_stem_schur_lists(const int32_t* edges, int E, int n0, int N);
 // acc -> diagonal blocks (+lm) + rhs ; arrowhead solve ; update node state
 nnrt_status launch_arrowhead_iteration(const ArrowheadWorkspace& ws, const double* acc, float lm, const int32_t* edges, const float* wing,
                                        float* node_state, float* acc_mut, float* updates_out, float* gradient_out, float* hessian_out,

@@ -121,6 +121,14 @@ class Scene:
     hierarchy: dict = field(default_factory=dict)   # edges, edge_layers, radii, layer_counts, virtual_indices (layers > 1)
 
 
+def native_hierarchy_builder(nodes, coverage, layer_count):
+    """hierarchy_builder over this package's own warp field (HierarchicalGraphWarpField.cpp:74-199 semantics, built
+    by the native library; needs the HIP device): (virtual_indices, layer_counts, edges, edge_layers)."""
+    from .nnrt import geometry as G
+    wf = G.HierarchicalGraphWarpField(nodes, coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE, layer_count)
+    return wf.get_virtual_node_indices(), wf.get_layer_node_counts(), wf.get_edges(), wf.get_edge_layer_indices()
+
+
 def make_scene(name: str = "C2", seed: int = 0, hierarchy_builder=None) -> Scene:
     """hierarchy_builder(nodes, coverage, layer_count) -> (virtual_indices, layer_counts, edges, edge_layers) is used
     to pre-sort the nodes into virtual order (identity permutation) for multi-layer configs."""

@@ -20,9 +20,10 @@ def child(config, steps):
     from dynamicfuion_python_amd.nnrt import geometry as G
     from dynamicfuion_python_amd.nnrt import rendering as Rr
     torch.cuda.set_device(0)
-    sc = S.make_scene(config)
+    sc = S.make_scene(config, hierarchy_builder=S.native_hierarchy_builder)
     depth = bench.render_target(sc, G, Rr)
-    wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE, 1)
+    wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE,
+                                      sc.layer_count)
     ft = A.DeformableMeshToImageFitter(1, [A.IterationMode.ALL], preconditioning_dampening_factor=0.001)
     ft.prepare(wf, G.TriangleMesh(sc.points, sc.normals, sc.faces), depth, None, sc.K)
     acc = {k: 0.0 for k in A.TIMED_STAGES}
