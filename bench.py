@@ -30,6 +30,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM": 8 TB/s spec)
+MFMA_F32_PEAK_TFS = 157.3   # dense f32-input MFMA peak (MI355X_MICROARCH.md MFMA table, "F32 (f32 in)")
 DEFAULT_CONFIG = "C2"
 ROOFLINE_KERNEL = "k_node_reduce_grouped"
 
@@ -86,6 +87,18 @@ KERNEL_STAGES = {
 # nnrt_fitter_iterate_timed stage -> the kernel it times
 STAGE_KERNEL = {"warp": "k_warp_mesh_quad", "raster": "k_raster_scatter_mesh", "pixel_jacobians": "k_pixel_jacobians",
                 "node_reduce": "k_node_reduce_grouped", "solve": "k_solve_update"}
+
+
+def arap_stage_bytes(N: int, n0: int, Ee: int) -> dict:
+    """SURVEY.md 8(d) ARAP and arrowhead-solve rows (E_e edges, n0 stem nodes, n1 = N - n0 corner nodes)."""
+    n1 = N - n0
+    return {"arap": Ee * (8 + 20 + 144 + 12) + 288 * N, "solve": 144 * (n0 + 3 * Ee) + 3 * 4 * (6 * n1) ** 2 + 48 * N}
+
+
+def corner_flops(n1: int, n_rhs: int = 1) -> float:
+    """dense corner Cholesky + solve, (6 n1)^3 / 3 + 2 (6 n1)^2 (1 + n_rhs)."""
+    m = 6 * n1
+    return m ** 3 / 3.0 + 2.0 * m * m * (1 + n_rhs)
 
 
 def kernel_bytes(kernel: str, sb: dict) -> int:
@@ -228,16 +241,17 @@ def main(argv=None):
     from dynamicfuion_python_amd.nnrt import geometry as G
     from dynamicfuion_python_amd.nnrt import rendering as Rr
 
-    sc = S.make_scene(args.config, seed=rank)
-    if sc.layer_count > 1:
-        raise SystemExit("bench.py drives the block-diagonal configs (C1/C2/C3); ARAP configs are parity-test cases")
+    sc = S.make_scene(args.config, seed=rank, hierarchy_builder=S.native_hierarchy_builder)
+    arap = sc.layer_count > 1
     P, F, V, Nn = sc.H * sc.W, len(sc.faces), len(sc.points), len(sc.nodes)
-    workload = (f"{sc.name}: {sc.W}x{sc.H} depth, {Nn}-node graph, {V}-vertex/{F}-triangle mesh, block-diagonal LM solve, "
+    solve_kind = f"{sc.layer_count}-layer ARAP arrowhead LM solve" if arap else "block-diagonal LM solve"
+    workload = (f"{sc.name}: {sc.W}x{sc.H} depth, {Nn}-node graph, {V}-vertex/{F}-triangle mesh, {solve_kind}, "
                 f"1 GN iteration per step from the identity warp")
     log(f"rank {rank}/{world} on {torch.cuda.get_device_name(dev)}: {workload}")
 
     depth = render_target(sc, G, Rr)
-    wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE, 1)
+    wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE,
+                                      sc.layer_count)
     ft = A.DeformableMeshToImageFitter(1, [A.IterationMode.ALL], preconditioning_dampening_factor=0.001, use_hip_graph=True)
     mesh = G.TriangleMesh(sc.points, sc.normals, sc.faces)
     ft.prepare(wf, mesh, depth, None, sc.K)
@@ -296,9 +310,26 @@ def main(argv=None):
     sb = stage_bytes(P, F, V, Nn, 4, E)
     kernels = {}
     for stage, kname in STAGE_KERNEL.items():
+        if arap and stage == "solve":
+            continue
         kb = kernel_bytes(kname, sb)
         ms = stages[stage]
         kernels[kname] = dict(ms=round(ms, 5), algorithmic_bytes=kb, frac=kb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS if ms > 0 else None)
+    corner = None
+    if arap:
+        counts = wf.get_layer_node_counts()
+        n0 = int(counts[0])
+        Ee = len(wf.get_edges())
+        ab = arap_stage_bytes(Nn, n0, Ee)
+        sb.update(ab)
+        kernels["k_arap_edges"] = dict(ms=round(stages["arap"], 5), algorithmic_bytes=ab["arap"],
+                                       frac=ab["arap"] / (stages["arap"] * 1e-3) / 1e9 / HBM_PEAK_GBS)
+        fl = corner_flops(Nn - n0)
+        corner = dict(kernel="arrowhead solve stage (stem Schur update + dense corner Cholesky + substitutions + update)",
+                      bound="mfma", achieved=fl / (stages["solve"] * 1e-3) / 1e12, peak=MFMA_F32_PEAK_TFS, unit="TFLOP/s",
+                      frac=fl / (stages["solve"] * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS, traffic=None, flops=fl, kernel_ms=stages["solve"],
+                      n0=n0, n1=Nn - n0, corner_size=6 * (Nn - n0), edges=Ee,
+                      flops_formula="SURVEY.md 8(d): (6 n1)^3 / 3 + 2 (6 n1)^2 (1 + n_rhs), n_rhs = 1")
     kbytes = kernels[ROOFLINE_KERNEL]["algorithmic_bytes"]
     k_ms = stages["node_reduce"]
     achieved = kbytes / (k_ms * 1e-3) / 1e9
@@ -348,10 +379,14 @@ def main(argv=None):
                      "iteration_algorithmic_bytes": it_bytes,
                      "iteration_frac": it_bytes / (agg["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS},
         "kernels": kernels,
+        "hbm_roofline": None,
         "per_rank": per_rank,
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if corner is not None:   # ARAP configs: the dense corner (MFMA-bound) is the dominant stage; the HBM one moves aside
+        out["hbm_roofline"] = out["roofline"]
+        out["roofline"] = corner
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not arap:
         log(f"GPU: {agg['value']:.1f} it/s; running the CPU baseline sample (~{args.cpu_seconds:.0f} s)")
         out["cpu_baseline"] = cpu_baseline(sc, depth.cpu().numpy(), args.cpu_threads, args.cpu_seconds)
     if rank == 0:
