@@ -421,6 +421,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 	fa.W = ft->W;
 	fa.tiles_x = static_cast<int>(ceil_div(ft->W, 16));
 	fa.tiles_y = static_cast<int>(ceil_div(ft->H, 16));
+	fa.tile_row0 = 0;
 	fa.pix = ft->pix;
 	fa.ndc = ft->ndc;
 	fa.blur = ro.blur;
@@ -522,6 +523,7 @@ nnrt_status nnrt_fitter_create(const nnrt_fitter_params* params, int32_t device,
 	NNRT_HIP(hipStreamCreateWithFlags(&ft->work, hipStreamNonBlocking));
 	NNRT_HIP(hipEventCreateWithFlags(&ft->ev_in, hipEventDisableTiming));
 	NNRT_HIP(hipEventCreateWithFlags(&ft->ev_out, hipEventDisableTiming));
+
 	nnrt_status st = ft->error_flag.ensure(1);
 	if (st) return st;
 	NNRT_HIP(hipMemset(ft->error_flag.ptr, 0, sizeof(int)));
@@ -559,6 +561,7 @@ void nnrt_fitter_destroy(nnrt_fitter* ft) {
 	ft->a_pairs.release();
 	if (ft->ev_in) hipEventDestroy(ft->ev_in);
 	if (ft->ev_out) hipEventDestroy(ft->ev_out);
+
 	if (ft->work) hipStreamDestroy(ft->work);
 	delete ft;
 }

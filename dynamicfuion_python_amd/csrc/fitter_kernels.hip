@@ -65,7 +65,7 @@ struct ModeTraits<NNRT_ITERATION_ROTATION_ONLY> {
 // term, the compact per-pixel Jacobian record [dr/dV (9), dr/dn_l (3), rho (3), r] (4 x float4). The raster key is
 // replaced by the contributing face (or EMPTY) for pass 2, which resets it.
 template <int MODE>
-__global__ __launch_bounds__(PIX_BLOCK) void k_pixel_jacobians(FitPixelArgs a) {
+__global__ __launch_bounds__(PIX_BLOCK, NNRT_FIT_VARIANT == 60 || NNRT_FIT_VARIANT == 61 ? 5 : 1) void k_pixel_jacobians(FitPixelArgs a) {
 
 	// XCD-aware tile order: consecutive workgroups are dealt round-robin over the 8 XCDs, so give each XCD a contiguous
 	// band of tiles (neighbouring tiles share vertices, anchors and nodes -> L2 reuse within the XCD).
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_pixel_jacobians(FitPixelArgs a) {
 	const int per_xcd = (tiles + 7) / 8;
 	const int b = blockIdx.x;
 	const int tile = (b % 8) * per_xcd + b / 8;
-	const int tu = tile % a.tiles_x, tv = tile / a.tiles_x;
+	const int tu = tile % a.tiles_x, tv = a.tile_row0 + tile / a.tiles_x;
 	// wave w of the workgroup owns the 8x8 quadrant (w & 1, w >> 1): compact pixel sets touch the fewest nodes
 	const int lane = static_cast<int>(threadIdx.x & 63), wave = static_cast<int>(threadIdx.x >> 6);
 	const int u = tu * PIX_TILE + (wave & 1) * 8 + (lane & 7);
@@ -238,6 +238,18 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_pixel_jacobians(FitPixelArgs a) {
 			rn[0] = dr_dnl.x;
 			rn[1] = dr_dnl.y;
 			rn[2] = dr_dnl.z;
+#if NNRT_FIT_VARIANT == 60 || NNRT_FIT_VARIANT == 62
+			// the face vertices are re-read (L1/L2) for the per-vertex chain instead of being held through the
+			// Jacobian set-up above: 18 fewer live registers there (occupancy), same values
+			asm volatile("" ::: "memory");
+#pragma unroll
+			for (int i = 0; i < 3; i++) {
+				const float4 wp = a.wpos[vid[i]];
+				const float4 wn = a.wnrm[vid[i]];
+				V3[i] = make3(wp.x, wp.y, wp.z);
+				N3[i] = make3(wn.x, wn.y, wn.z);
+			}
+#endif
 #pragma unroll
 			for (int i = 0; i < 3; i++) {
 				const float z = V3[i].z;
@@ -315,6 +327,7 @@ constexpr int NG_CAP = 48;     // associations per chunk (one lane each in (2));
 // (2) J[0..S-1], r at word S (zeros past the count, whose node word repeats the chunk's last node).
 constexpr int NG_STRIDE = 49;
 constexpr int NG_ROWS = 8;     // pixel rows per wave (8 x NG_ROWS pixels)
+static_assert(2 * NG_ROWS == PIX_TILE, "pass 2 walks the pass-1 tiles");
 
 __device__ inline void ng_flush(double* dst, double v) { atomicAdd(dst, v); }
 
@@ -331,13 +344,12 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 	__shared__ float s_slots[PIX_BLOCK / 64][2][8 * NG_STRIDE];
 	__shared__ float s_rec[PIX_BLOCK / 64][16 * 64];                 // component-major pixel records
 
-	// tiles of 16 x (2 NG_ROWS) pixels, one 8 x NG_ROWS block per wave
-	const int tiles_y = (a.H + 2 * NG_ROWS - 1) / (2 * NG_ROWS);
-	const int tiles = a.tiles_x * tiles_y;
+	// tiles of 16 x 16 pixels (the pass-1 tiles), one 8 x 8 block per wave
+	const int tiles = a.tiles_x * a.tiles_y;
 	const int per_xcd = (tiles + 7) / 8;
 	const int b = blockIdx.x;
 	const int tile = (b % 8) * per_xcd + b / 8;
-	const int tu = tile % a.tiles_x, tv = tile / a.tiles_x;
+	const int tu = tile % a.tiles_x, tv = a.tile_row0 + tile / a.tiles_x;
 	const int lane = static_cast<int>(threadIdx.x & 63), wave = static_cast<int>(threadIdx.x >> 6);
 	const int u = tu * PIX_TILE + (wave & 1) * 8 + (lane & 7), v = tv * 2 * NG_ROWS + (wave >> 1) * NG_ROWS + (lane >> 3);
 	const bool in_image = tile < tiles && (lane >> 3) < NG_ROWS && u < a.W && v < a.H;
@@ -594,9 +606,8 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 	}
 }
 
-nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t stream, hipEvent_t between) {
-	const int tiles = args.tiles_x * args.tiles_y;
-	const unsigned grid = static_cast<unsigned>(((tiles + 7) / 8) * 8);
+static nnrt_status launch_pixel_pass(int mode, const FitPixelArgs& args, hipStream_t stream) {
+	const unsigned grid = static_cast<unsigned>(((args.tiles_x * args.tiles_y + 7) / 8) * 8);
 	switch (mode) {
 		case NNRT_ITERATION_ALL: k_pixel_jacobians<NNRT_ITERATION_ALL><<<grid, PIX_BLOCK, 0, stream>>>(args); break;
 		case NNRT_ITERATION_TRANSLATION_ONLY: k_pixel_jacobians<NNRT_ITERATION_TRANSLATION_ONLY><<<grid, PIX_BLOCK, 0, stream>>>(args); break;
@@ -604,29 +615,44 @@ nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t st
 		default: set_error("unknown iteration mode"); return NNRT_ERROR_ARGUMENT;
 	}
 	NNRT_LAUNCH_CHECK();
-	if (between && hipEventRecord(between, stream) != hipSuccess) {
-		set_error("hipEventRecord failed");
-		return NNRT_ERROR_HIP;
-	}
+	return NNRT_OK;
+}
+
+static nnrt_status launch_node_pass(int mode, const FitPixelArgs& args, hipStream_t stream) {
+	const unsigned grid = static_cast<unsigned>(((args.tiles_x * args.tiles_y + 7) / 8) * 8);
 	// anchor slots per vertex: the common 4-anchor configuration gets its own instantiation (half the slot logic)
 	const bool k4 = args.anchor_count <= 4;
-	const unsigned grid_ng = static_cast<unsigned>(((args.tiles_x * ((args.H + 2 * NG_ROWS - 1) / (2 * NG_ROWS)) + 7) / 8) * 8);
 	switch (mode) {
 		case NNRT_ITERATION_ALL:
-			if (k4) k_node_reduce_grouped<NNRT_ITERATION_ALL, 4><<<grid_ng, PIX_BLOCK, 0, stream>>>(args);
-			else k_node_reduce_grouped<NNRT_ITERATION_ALL, MAX_ANCHORS><<<grid_ng, PIX_BLOCK, 0, stream>>>(args);
+			if (k4) k_node_reduce_grouped<NNRT_ITERATION_ALL, 4><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			else k_node_reduce_grouped<NNRT_ITERATION_ALL, MAX_ANCHORS><<<grid, PIX_BLOCK, 0, stream>>>(args);
 			break;
 		case NNRT_ITERATION_TRANSLATION_ONLY:
-			if (k4) k_node_reduce_grouped<NNRT_ITERATION_TRANSLATION_ONLY, 4><<<grid_ng, PIX_BLOCK, 0, stream>>>(args);
-			else k_node_reduce_grouped<NNRT_ITERATION_TRANSLATION_ONLY, MAX_ANCHORS><<<grid_ng, PIX_BLOCK, 0, stream>>>(args);
+			if (k4) k_node_reduce_grouped<NNRT_ITERATION_TRANSLATION_ONLY, 4><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			else k_node_reduce_grouped<NNRT_ITERATION_TRANSLATION_ONLY, MAX_ANCHORS><<<grid, PIX_BLOCK, 0, stream>>>(args);
 			break;
 		default:
-			if (k4) k_node_reduce_grouped<NNRT_ITERATION_ROTATION_ONLY, 4><<<grid_ng, PIX_BLOCK, 0, stream>>>(args);
-			else k_node_reduce_grouped<NNRT_ITERATION_ROTATION_ONLY, MAX_ANCHORS><<<grid_ng, PIX_BLOCK, 0, stream>>>(args);
+			if (k4) k_node_reduce_grouped<NNRT_ITERATION_ROTATION_ONLY, 4><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			else k_node_reduce_grouped<NNRT_ITERATION_ROTATION_ONLY, MAX_ANCHORS><<<grid, PIX_BLOCK, 0, stream>>>(args);
 			break;
 	}
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;
+}
+
+#define NNRT_EV(call)                                                                                                   \
+	do {                                                                                                                \
+		if ((call) != hipSuccess) {                                                                                     \
+			set_error("event record/wait failed");                                                                      \
+			return NNRT_ERROR_HIP;                                                                                      \
+		}                                                                                                               \
+	} while (0)
+
+nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t stream, hipEvent_t between) {
+	nnrt_status st = launch_pixel_pass(mode, args, stream);
+	if (st) return st;
+	if (between) NNRT_EV(hipEventRecord(between, stream));
+	return launch_node_pass(mode, args, stream);
 }
 
 // =====================================================================================================================

@@ -10,7 +10,8 @@ namespace nnrt {
 constexpr int ACC_STRIDE = 28;   // per node: 21 JtJ upper-triangle entries + 6 Jt r (+1 pad); 3-dof modes use 6 + 3
 
 struct FitPixelArgs {
-	int H, W, tiles_x, tiles_y;
+	int H, W, tiles_x, tiles_y;   // tiles of 16 x 16 pixels; this launch covers tile rows [tile_row0, tile_row0 + tiles_y)
+	int tile_row0;
 	Camera pix;             // pixel-space intrinsics (float)
 	NdcSetup ndc;
 	float blur;             // NDC units
