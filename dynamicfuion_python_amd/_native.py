@@ -83,6 +83,9 @@ _SIGNATURES = {
     "nnrt_interpolate_face_attributes": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_int32, c_void_p, c_void_p]),
     "nnrt_unproject_depth": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p]),
     "nnrt_axis_angle_to_matrices_rodrigues": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
+    "nnrt_compute_triangle_normals": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
+    "nnrt_compute_vertex_normals": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
+    "nnrt_compute_ordered_point_cloud_normals": (c_int32, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p]),
     "nnrt_solve_block_diagonal_cholesky": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     "nnrt_solve_block_sparse_arrowhead_cholesky": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p,
                                                              c_void_p, c_void_p]),

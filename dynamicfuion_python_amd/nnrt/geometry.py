@@ -27,6 +27,7 @@ class TriangleMesh:
     vertex_positions: object
     vertex_normals: object
     triangle_indices: object
+    triangle_normals: object = None
 
     def on_device(self, device: torch.device):
         return (to_device(self.vertex_positions, torch.float32, device), to_device(self.vertex_normals, torch.float32, device),
@@ -239,7 +240,53 @@ def compute_point_to_plane_distances(normals1, vertices1, vertices2) -> torch.Te
     return (n[:, 0] * d[:, 0] + n[:, 1] * d[:, 1]) + n[:, 2] * d[:, 2]
 
 
+def _mesh_vf(mesh: TriangleMesh, dev):
+    if mesh.vertex_positions is None or mesh.triangle_indices is None:
+        raise RuntimeError("Mesh needs to have both vertex positions and triangle indices to compute normals.")
+    return to_device(mesh.vertex_positions, torch.float32, dev), to_device(mesh.triangle_indices, torch.int64, dev)
+
+
+def compute_triangle_normals(mesh: TriangleMesh, normalized: bool = True):
+    """ComputeTriangleNormals (cpp/geometry/functional/NormalsOperations.cpp:36-46): sets mesh.triangle_normals [F,3]."""
+    dev = _dev()
+    p, f = _mesh_vf(mesh, dev)
+    out = torch.empty((f.shape[0], 3), dtype=torch.float32, device=dev)
+    N.check(N.lib().nnrt_compute_triangle_normals(N.ptr(p), p.shape[0], N.ptr(f), f.shape[0], int(bool(normalized)), N.ptr(out),
+                                                  N.stream_ptr()))
+    mesh.triangle_normals = out
+    return out
+
+
+def compute_vertex_normals(mesh: TriangleMesh, normalized: bool = True):
+    """ComputeVertexNormals (NormalsOperations.cpp:52-66): sum of the unnormalized incident triangle normals (ascending
+    face order), optionally normalized; sets mesh.vertex_normals [V,3]."""
+    dev = _dev()
+    p, f = _mesh_vf(mesh, dev)
+    out = torch.empty((p.shape[0], 3), dtype=torch.float32, device=dev)
+    N.check(N.lib().nnrt_compute_vertex_normals(N.ptr(p), p.shape[0], N.ptr(f), f.shape[0], int(bool(normalized)), N.ptr(out),
+                                                N.stream_ptr()))
+    mesh.vertex_normals = out
+    return out
+
+
+def compute_ordered_point_cloud_normals(point_cloud, source_image_size) -> torch.Tensor:
+    """ComputeOrderedPointCloudNormals (NormalsOperations.cpp:74-95): organized point cloud ([H*W,3] positions, or an
+    object with `point_positions`) -> [H*W,3] normals facing the camera, zero on the image border."""
+    if len(source_image_size) != 2:
+        raise RuntimeError(f"Source image size must have two dimensions. Got {len(source_image_size)}.")
+    dev = _dev()
+    pts = getattr(point_cloud, "point_positions", point_cloud)
+    q = to_device(pts, torch.float32, dev).reshape(-1, 3)
+    H, W = int(source_image_size[0]), int(source_image_size[1])
+    out = torch.empty_like(q)
+    N.check(N.lib().nnrt_compute_ordered_point_cloud_normals(N.ptr(q), q.shape[0], H, W, N.ptr(out), N.stream_ptr()))
+    return out
+
+
 functional = types.SimpleNamespace(
+    compute_triangle_normals=compute_triangle_normals,
+    compute_vertex_normals=compute_vertex_normals,
+    compute_ordered_point_cloud_normals=compute_ordered_point_cloud_normals,
     compute_anchors_and_weights_euclidean_fixed_node_weight=compute_anchors_and_weights_euclidean_fixed_node_weight,
     compute_anchors_and_weights_euclidean_variable_node_weight=compute_anchors_and_weights_euclidean_variable_node_weight,
     warp_triangle_mesh=warp_triangle_mesh,

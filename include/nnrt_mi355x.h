@@ -179,6 +179,20 @@ nnrt_status nnrt_interpolate_face_attributes(const int64_t* d_pixel_faces, const
 /* nnrt.geometry.functional.unproject_raster_depth_without_filtering (PerspectiveProjectionImpl.h:60-146), float32 depth */
 nnrt_status nnrt_unproject_depth(const float* d_depth, int32_t height, int32_t width, const double* h_K, float depth_scale,
                                  float depth_max, float* d_points, uint8_t* d_mask, void* stream);
+/* nnrt.geometry.functional.compute_triangle_normals(mesh, normalized=True) (cpp/geometry/functional/NormalsOperations.cpp:36-46,
+ * kernel NormalsOperationsImpl.h:39-68): d_out [F,3] = (v1 - v0) x (v2 - v0), optionally normalized (zero stays zero,
+ * NaN -> (0,0,1)) */
+nnrt_status nnrt_compute_triangle_normals(const float* d_vertices, int64_t vertex_count, const int64_t* d_faces, int64_t face_count,
+                                          int32_t normalized, float* d_out, void* stream);
+/* nnrt.geometry.functional.compute_vertex_normals(mesh, normalized=True) (NormalsOperations.cpp:52-66, kernel :95-166): sum of the
+ * unnormalized incident triangle normals, in ascending face order (the reference's serial order; its CUDA path uses
+ * unordered atomics), optionally normalized. Synchronizes `stream`. */
+nnrt_status nnrt_compute_vertex_normals(const float* d_vertices, int64_t vertex_count, const int64_t* d_faces, int64_t face_count,
+                                        int32_t normalized, float* d_out, void* stream);
+/* nnrt.geometry.functional.compute_ordered_point_cloud_normals(point_cloud, source_image_size) (NormalsOperations.cpp:74-95,
+ * kernel NormalsOperationsImpl.h:170-214): organized [H*W,3] points -> [H*W,3] normals facing the camera, 0 on the border */
+nnrt_status nnrt_compute_ordered_point_cloud_normals(const float* d_points, int64_t point_count, int32_t height, int32_t width, float* d_out,
+                                                     void* stream);
 /* nnrt.core.linalg AxisAngleVectorsToMatricesRodrigues (cpp/core/linalg/RodriguesImpl.h:66-88) */
 nnrt_status nnrt_axis_angle_to_matrices_rodrigues(const float* d_vectors, int32_t count, float* d_matrices, void* stream);
 /* SolveBlockDiagonalCholesky (cpp/core/linalg/SolveBlockDiagonalCholesky.cpp): x_i = A_i^-1 b_i, block size 3 or 6 */

@@ -317,6 +317,61 @@ def solve_arrowhead(diag, wing, edges, n0, g):
     return x
 
 
+# ---- normals (cpp/geometry/functional/kernel/NormalsOperationsImpl.h) : float32 numpy, one IEEE op at a time ----
+def _normalize_eigen(v):
+    """Eigen normalize(): divide by sqrt of the squared norm when positive (zero rows stay zero)."""
+    v = np.asarray(v, np.float32)
+    n2 = (v[:, 0] * v[:, 0] + v[:, 1] * v[:, 1]) + v[:, 2] * v[:, 2]
+    out = v.copy()
+    pos = n2 > 0
+    n = np.sqrt(n2[pos])
+    out[pos] = v[pos] / n[:, None]
+    return out
+
+
+def triangle_normals(verts, faces, normalized=True):
+    """ComputeTriangleNormals (:39-68) (+ NormalizeVectors3d :75-93: NaN -> (0, 0, 1))."""
+    v = np.asarray(verts, np.float32)
+    f = np.asarray(faces, np.int64)
+    a = v[f[:, 1]] - v[f[:, 0]]
+    b = v[f[:, 2]] - v[f[:, 0]]
+    n = np.stack([a[:, 1] * b[:, 2] - a[:, 2] * b[:, 1], a[:, 2] * b[:, 0] - a[:, 0] * b[:, 2], a[:, 0] * b[:, 1] - a[:, 1] * b[:, 0]], 1)
+    if normalized:
+        n = _normalize_eigen(n)
+        n[np.isnan(n[:, 0])] = (0.0, 0.0, 1.0)
+    return n.astype(np.float32)
+
+
+def vertex_normals(verts, faces, normalized=True):
+    """ComputeVertexNormals (:95-166): unnormalized triangle normals added per vertex in ascending face order (the
+    reference's serial order), optionally normalized."""
+    v = np.asarray(verts, np.float32)
+    f = np.asarray(faces, np.int64)
+    tn = triangle_normals(v, f, normalized=False)
+    out = np.zeros((len(v), 3), np.float32)
+    np.add.at(out, f.reshape(-1), np.repeat(tn, 3, axis=0))
+    if normalized:
+        out = _normalize_eigen(out)
+        out[np.isnan(out[:, 0])] = (0.0, 0.0, 1.0)
+    return out
+
+
+def ordered_point_cloud_normals(points, H, W):
+    """ComputeOrderedPointCloudNormals (:170-214): normalize((right - left) x (top - bottom)), flipped so n.z <= 0,
+    zero on the image border."""
+    p = np.asarray(points, np.float32).reshape(H, W, 3)
+    out = np.zeros((H, W, 3), np.float32)
+    dh = p[1:-1, 2:] - p[1:-1, :-2]
+    dv = p[:-2, 1:-1] - p[2:, 1:-1]
+    n = np.stack([dh[..., 1] * dv[..., 2] - dh[..., 2] * dv[..., 1], dh[..., 2] * dv[..., 0] - dh[..., 0] * dv[..., 2],
+                  dh[..., 0] * dv[..., 1] - dh[..., 1] * dv[..., 0]], -1).reshape(-1, 3)
+    n = _normalize_eigen(n)
+    flip = n[:, 2] > 0
+    n[flip] = -n[flip]
+    out[1:-1, 1:-1] = n.reshape(H - 2, W - 2, 3)
+    return out.reshape(-1, 3)
+
+
 def rodrigues(w):
     w = _f32(w).reshape(-1, 3)
     R = np.empty((len(w), 3, 3), np.float32)

@@ -449,3 +449,27 @@ def test_graph_warp_field_warp_mesh(nn, S, oracle_mod):
     wf.reset_rotations()
     assert np.array_equal(wf.get_node_rotations(), np.tile(np.eye(3, dtype=np.float32), (len(sc.nodes), 1, 1)))
     assert np.array_equal(wf.get_node_translations(), sc.gt_translations)
+
+
+@pytest.mark.parametrize("name", ["S1", "C1"])
+def test_normals_bit_exact(nn, S, oracle_mod, name):
+    """compute_triangle_normals / compute_vertex_normals / compute_ordered_point_cloud_normals (NormalsOperationsImpl.h)
+    against the oracle restatement: identical bits (vertex sums in ascending face order on both sides)."""
+    sc = _scene(S, oracle_mod, name)
+    G = nn.geometry
+    mesh = G.TriangleMesh(sc.points, None, sc.faces)
+    for normalized in (False, True):
+        tn = _np(G.functional.compute_triangle_normals(mesh, normalized))
+        assert np.array_equal(tn, oracle_mod.triangle_normals(sc.points, sc.faces, normalized))
+        vn = _np(G.functional.compute_vertex_normals(mesh, normalized))
+        assert np.array_equal(vn, oracle_mod.vertex_normals(sc.points, sc.faces, normalized))
+    assert np.array_equal(_np(mesh.vertex_normals), vn)
+    depth = scene_target(oracle_mod, sc)
+    pts, _ = nn.geometry.functional.unproject_raster_depth_without_filtering(depth, sc.K, 1.0, 10.0)
+    on = _np(G.functional.compute_ordered_point_cloud_normals(pts, (sc.H, sc.W)))
+    assert np.array_equal(on, oracle_mod.ordered_point_cloud_normals(_np(pts), sc.H, sc.W))
+    with pytest.raises(RuntimeError):
+        G.functional.compute_ordered_point_cloud_normals(pts[:-1], (sc.H, sc.W))
+    bad = G.TriangleMesh(sc.points, None, np.array([[0, 1, len(sc.points)]], np.int64))
+    with pytest.raises(RuntimeError):
+        G.functional.compute_vertex_normals(bad)

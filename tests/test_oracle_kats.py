@@ -192,3 +192,24 @@ def test_reference_float_order_noise_is_below_summation_bound(oracle_mod):
     assert rel_err(f["gradient"], d["gradient"]) < 1e-5
     assert rel_err(f["updates"], d["updates"]) < 1e-4
     assert np.array_equal(f["residuals"], d["residuals"])
+
+
+def test_normals_restatement_properties(oracle_mod):
+    """Normals restatement (NormalsOperationsImpl.h): a flat z = const grid facing the camera gives (0, 0, -1) ordered
+    normals inside and zeros on the border; vertex normals of a two-triangle quad are the sum of its face normals."""
+    O = oracle_mod
+    H, W = 6, 7
+    ys, xs = np.mgrid[0:H, 0:W].astype(np.float32)
+    pts = np.stack([xs * 0.01, ys * 0.01, np.full_like(xs, 1.5)], -1).reshape(-1, 3)
+    n = O.ordered_point_cloud_normals(pts, H, W).reshape(H, W, 3)
+    assert np.all(n[0] == 0) and np.all(n[-1] == 0) and np.all(n[:, 0] == 0) and np.all(n[:, -1] == 0)
+    assert np.allclose(n[1:-1, 1:-1], (0.0, 0.0, -1.0))
+    v = np.array([[0, 0, 0], [1, 0, 0], [1, 1, 0], [0, 1, 0]], np.float32)
+    f = np.array([[0, 1, 2], [0, 2, 3]], np.int64)
+    tn = O.triangle_normals(v, f, normalized=False)
+    assert np.array_equal(tn, np.array([[0, 0, 1], [0, 0, 1]], np.float32))
+    vn = O.vertex_normals(v, f, normalized=False)
+    assert np.array_equal(vn, np.array([[0, 0, 2], [0, 0, 1], [0, 0, 2], [0, 0, 1]], np.float32))
+    assert np.array_equal(O.vertex_normals(v, f)[:, 2], np.ones(4, np.float32))
+    z = O.triangle_normals(np.zeros((3, 3), np.float32), np.array([[0, 1, 2]]), normalized=True)
+    assert np.array_equal(z, np.zeros((1, 3), np.float32))   # Eigen normalize leaves zero vectors at zero
