@@ -395,10 +395,18 @@ __global__ void k_prepare_reference_points(const float* __restrict__ points, con
 	out[i] = valid ? make_float4(points[3 * i], points[3 * i + 1], points[3 * i + 2], 1.f) : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
-__global__ void k_faces_to_int4(const int64_t* __restrict__ faces, int64_t F, int4* __restrict__ out) {
+// faces -> int4; an index outside [0, V) becomes the degenerate face (0, 0, 0) (never rasterized, never gathered out of
+// bounds) and sets error bit 4, which nnrt_fitter_check reports
+__global__ void k_faces_to_int4(const int64_t* __restrict__ faces, int64_t F, int64_t V, int4* __restrict__ out, int* error_flag) {
 	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
 	if (f >= F) return;
-	out[f] = make_int4(static_cast<int>(faces[3 * f]), static_cast<int>(faces[3 * f + 1]), static_cast<int>(faces[3 * f + 2]), 0);
+	const int64_t i0 = faces[3 * f], i1 = faces[3 * f + 1], i2 = faces[3 * f + 2];
+	if (i0 < 0 || i0 >= V || i1 < 0 || i1 >= V || i2 < 0 || i2 >= V) {
+		atomicOr(error_flag, 4);
+		out[f] = make_int4(0, 0, 0, 0);
+		return;
+	}
+	out[f] = make_int4(static_cast<int>(i0), static_cast<int>(i1), static_cast<int>(i2), 0);
 }
 
 nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mode, hipStream_t s, hipEvent_t* marks = nullptr) {
@@ -677,7 +685,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	hipStream_t s = ft->work;
 	NNRT_HIP(hipMemcpyAsync(ft->mesh_p.ptr, d_vertices, sizeof(float) * 3 * V, hipMemcpyDeviceToDevice, s));
 	NNRT_HIP(hipMemcpyAsync(ft->mesh_n.ptr, d_normals, sizeof(float) * 3 * V, hipMemcpyDeviceToDevice, s));
-	k_faces_to_int4<<<static_cast<unsigned>(ceil_div(F, 256)), 256, 0, s>>>(d_faces, F, ft->faces4.ptr);
+	k_faces_to_int4<<<static_cast<unsigned>(ceil_div(F, 256)), 256, 0, s>>>(d_faces, F, V, ft->faces4.ptr, ft->error_flag.ptr);
 	NNRT_LAUNCH_CHECK();
 	// once per frame (:96-106): anchors & weights on the canonical mesh in virtual node order
 	if ((st = launch_compute_anchors(ft->mesh_p.ptr, V, wf->node_positions.ptr, N, K, wf->coverage,
@@ -813,6 +821,10 @@ nnrt_status nnrt_fitter_check(nnrt_fitter* ft, void* stream) {
 	if (flag & 2) {
 		set_error("fixed-coverage ARAP residual indexes edge_layer_indices[node_j] out of bounds (reference quirk A3)");
 		return NNRT_ERROR_UNSUPPORTED;
+	}
+	if (flag & 4) {
+		set_error("mesh triangle index out of range (faces must index [0, vertex_count))");
+		return NNRT_ERROR_ARGUMENT;
 	}
 	return NNRT_OK;
 }

@@ -28,10 +28,16 @@ __device__ inline f3 triangle_normal(const float* verts, const int64_t* faces, i
 	return make3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 
-__global__ void k_triangle_normals(const float* __restrict__ verts, const int64_t* __restrict__ faces, int64_t F, int normalized,
-                                   float* __restrict__ out) {
+__global__ void k_triangle_normals(const float* __restrict__ verts, int64_t V, const int64_t* __restrict__ faces, int64_t F, int normalized,
+                                   float* __restrict__ out, int* error_flag) {
 	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
 	if (f >= F) return;
+	const int64_t i0 = faces[3 * f], i1 = faces[3 * f + 1], i2 = faces[3 * f + 2];
+	if (i0 < 0 || i0 >= V || i1 < 0 || i1 >= V || i2 < 0 || i2 >= V) {   // no gather outside the vertex array
+		atomicOr(error_flag, 1);
+		out[3 * f] = out[3 * f + 1] = out[3 * f + 2] = __builtin_nanf("");
+		return;
+	}
 	f3 n = triangle_normal(verts, faces, f);
 	if (normalized) n = normalize_like_eigen(n);
 	out[3 * f] = n.x;
@@ -78,7 +84,7 @@ __global__ void k_vertex_face_fill(const int64_t* __restrict__ faces, int64_t F,
                                    int* __restrict__ list) {
 	const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
 	if (i >= 3 * F) return;
-	const int64_t v = faces[i];
+	const int64_t v = faces[i];   // indices were validated by k_vertex_face_count before this launch
 	const int slot = atomicAdd(cursor + v, 1);
 	list[offsets[v] + slot] = static_cast<int>(i / 3);
 }
@@ -143,12 +149,26 @@ extern "C" {
 
 nnrt_status nnrt_compute_triangle_normals(const float* d_vertices, int64_t vertex_count, const int64_t* d_faces, int64_t face_count,
                                           int32_t normalized, float* d_out, void* stream) {
-	(void) vertex_count;
 	if (face_count == 0) return NNRT_OK;
-	NNRT_CHECK_ARG(d_vertices && d_faces && d_out && face_count > 0, "invalid arguments");
-	k_triangle_normals<<<static_cast<unsigned>(ceil_div(face_count, 256)), 256, 0, static_cast<hipStream_t>(stream)>>>(d_vertices, d_faces,
-	                                                                                                                  face_count, normalized, d_out);
-	NNRT_LAUNCH_CHECK();
+	NNRT_CHECK_ARG(d_vertices && d_faces && d_out && face_count > 0 && vertex_count >= 0, "invalid arguments");
+	hipStream_t s = static_cast<hipStream_t>(stream);
+	int* flag = nullptr;
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&flag), sizeof(int), s));
+	NNRT_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
+	k_triangle_normals<<<static_cast<unsigned>(ceil_div(face_count, 256)), 256, 0, s>>>(d_vertices, vertex_count, d_faces, face_count, normalized,
+	                                                                                    d_out, flag);
+	hipError_t le = hipGetLastError();
+	int host_flag = 0;
+	hipError_t ce = hipMemcpyAsync(&host_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s);
+	hipError_t se = hipStreamSynchronize(s);
+	hipFreeAsync(flag, s);
+	NNRT_HIP(le);
+	NNRT_HIP(ce);
+	NNRT_HIP(se);
+	if (host_flag) {
+		set_error("triangle index out of range");
+		return NNRT_ERROR_ARGUMENT;
+	}
 	return NNRT_OK;
 }
 
@@ -166,22 +186,29 @@ nnrt_status nnrt_compute_vertex_normals(const float* d_vertices, int64_t vertex_
 	NNRT_HIP(hipMemsetAsync(count, 0, sizeof(int) * V, s));
 	NNRT_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
 	if (n3 > 0) k_vertex_face_count<<<static_cast<unsigned>(ceil_div(n3, 256)), 256, 0, s>>>(d_faces, face_count, V, count, flag);
+	{   // validate every index before anything gathers through the faces (the fill and the sums index by them)
+		hipError_t le = hipGetLastError();
+		int host_flag = 0;
+		hipError_t ce = hipMemcpyAsync(&host_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s);
+		hipError_t se = hipStreamSynchronize(s);
+		if (le != hipSuccess || ce != hipSuccess || se != hipSuccess || host_flag) {
+			for (void* p : {static_cast<void*>(count), static_cast<void*>(offsets), static_cast<void*>(list), static_cast<void*>(flag)}) hipFreeAsync(p, s);
+			NNRT_HIP(le);
+			NNRT_HIP(ce);
+			NNRT_HIP(se);
+			set_error("triangle index out of range");
+			return NNRT_ERROR_ARGUMENT;
+		}
+	}
 	k_exclusive_scan<<<1, 1024, 0, s>>>(count, V, offsets);
 	NNRT_HIP(hipMemsetAsync(count, 0, sizeof(int) * V, s));
 	if (n3 > 0) k_vertex_face_fill<<<static_cast<unsigned>(ceil_div(n3, 256)), 256, 0, s>>>(d_faces, face_count, offsets, count, list);
 	k_vertex_normals<<<static_cast<unsigned>(ceil_div(V, 256)), 256, 0, s>>>(d_vertices, d_faces, V, offsets, list, normalized, d_out);
 	hipError_t le = hipGetLastError();
-	int host_flag = 0;
-	hipError_t ce = hipMemcpyAsync(&host_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s);
 	hipError_t se = hipStreamSynchronize(s);
 	for (void* p : {static_cast<void*>(count), static_cast<void*>(offsets), static_cast<void*>(list), static_cast<void*>(flag)}) hipFreeAsync(p, s);
 	NNRT_HIP(le);
-	NNRT_HIP(ce);
 	NNRT_HIP(se);
-	if (host_flag) {
-		set_error("triangle index out of range");
-		return NNRT_ERROR_ARGUMENT;
-	}
 	return NNRT_OK;
 }
 

@@ -370,6 +370,11 @@ def test_errors_fail_loudly(nn, S, oracle_mod):
     sc.nodes = np.concatenate([sc.nodes, np.array([[5.0, 5.0, 5.0]], np.float32)])
     with pytest.raises(RuntimeError, match="positive-definite"):
         _gpu_fit(nn, sc, depth, 1, lm=0.0)
+    # a triangle index outside the vertex array is rejected (validated on the device, nothing gathered out of bounds)
+    sc = _scene(S, oracle_mod, "S1")
+    sc.faces = np.concatenate([sc.faces, np.array([[0, 1, len(sc.points)]], sc.faces.dtype)])
+    with pytest.raises(RuntimeError, match="index out of range"):
+        _gpu_fit(nn, sc, depth, 1, lm=0.001)
 
 
 def test_fit_point_cloud_overload_parity(nn, S, oracle_mod):
@@ -473,3 +478,7 @@ def test_normals_bit_exact(nn, S, oracle_mod, name):
     bad = G.TriangleMesh(sc.points, None, np.array([[0, 1, len(sc.points)]], np.int64))
     with pytest.raises(RuntimeError):
         G.functional.compute_vertex_normals(bad)
+    with pytest.raises(RuntimeError):
+        G.functional.compute_triangle_normals(bad)
+    # the library stays usable after a rejected call (nothing gathered outside the vertex array)
+    assert np.array_equal(_np(G.functional.compute_triangle_normals(mesh, True)), oracle_mod.triangle_normals(sc.points, sc.faces, True))
