@@ -300,17 +300,91 @@ StemSchurLists build_stem_schur_lists(const int32_t* edges, int E, int n0, int N
 }
 
 // ---- dense corner: blocked right-looking Cholesky of S (ld x ld, row-major, lower triangle) and S x = b -------------
-// SolveBlockSparseArrowheadCholesky.cpp:30-95 factors the Schur complement with a dense potrf. Here, per 64-column
-// block k: k_chol_diag factors the diagonal block in LDS and inverts it (L_kk^-1 kept for the panel and the
-// substitutions), k_chol_panel forms L_Ik = A_Ik L_kk^-T for every block row below (one workgroup per block row), and
-// k_chol_update applies A_IJ -= L_Ik L_Jk^T to every lower tile of the trailing matrix (one workgroup per tile). The
-// substitutions are block-parallel matrix-vector products with the stored inverses.
-constexpr int CT = 256;   // threads per workgroup of the corner kernels (64 x 64 tiles: 4 x 4 outputs per thread)
-#if NNRT_FIT_VARIANT == 30
+// SolveBlockSparseArrowheadCholesky.cpp:30-95 factors the Schur complement with a dense potrf. Here ONE launch per
+// 64-column block k (k_chol_step), whose workgroups play two roles:
+//   panel   (block rows I >= k, dealt first): apply the previous block's update to the two tiles this row needs,
+//           A_kk -= L_k,k-1 L_k,k-1^T and A_Ik -= L_I,k-1 L_k,k-1^T (f32 MFMA, v_mfma_f32_32x32x2_f32, one 32 x 32
+//           quadrant per wave, into LDS); then one wave holds both tiles (lane = row) in registers and runs the 64
+//           column eliminations of A_kk, applying each to its panel row as it goes (one packed FMA per column pair):
+//           L_kk and L_Ik = A_Ik L_kk^-T come out of one pass with no inverse. The right-hand side rides along as the
+//           panel row of the diagonal workgroup (lane 0): y_k = L_kk^-1 b_k.
+//   trailing (tiles k < J <= I): A_IJ -= L_I,k-1 L_J,k-1^T on the MFMA, and b_J -= L_J,k-1 y_k-1 by the diagonal tiles.
+// Every operand of launch k was finished by launch k - 1, so consecutive launches are the only synchronisation.
+// After the factorization k_chol_diag_inverse inverts every L_kk in parallel (once) and the block back substitution
+// L^T x = y runs one launch per block row (k_chol_back_step), each a pair of matrix-vector products.
+constexpr int CT = 256;   // threads per workgroup of the corner kernels
+constexpr int CS4 = CORNER_NB + 4;   // LDS row stride of the staged tiles (16-B aligned rows for ds_read_b128)
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ inline float lane_bcast(float v, int src) {
+	return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
+}
+
+// 32 x 32 quadrant (qr, qc) of X Y^T for X, Y 64 x 64 row-major tiles at row stride ld (lane l feeds
+// A[i = l & 31][k'] = X[32 qr + i][32 (l >> 5) + s] and B[k'][j] = Y[32 qc + j][32 (l >> 5) + s] to MFMA step s, so the 32
+// steps x 2 lane halves cover the 64-wide k range; each lane reads 32 contiguous floats). C/D map: column l & 31, row
+// (v & 3) + 8 (v >> 2) + 4 (l >> 5).
+__device__ inline f32x16 quadrant_xyt(const float* X, const float* Y, int64_t ld, int qr, int qc, int lane) {
+	const int half = lane >> 5, l32 = lane & 31;
+	const float4* x4 = reinterpret_cast<const float4*>(X + (32 * qr + l32) * ld + 32 * half);
+	const float4* y4 = reinterpret_cast<const float4*>(Y + (32 * qc + l32) * ld + 32 * half);
+	float4 vx[8], vy[8];
+#pragma unroll
+	for (int q = 0; q < 8; q++) {
+		vx[q] = x4[q];
+		vy[q] = y4[q];
+	}
+	f32x16 acc = {};
+#pragma unroll
+	for (int q = 0; q < 8; q++) {
+		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].x, vy[q].x, acc, 0, 0, 0);
+		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].y, vy[q].y, acc, 0, 0, 0);
+		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].z, vy[q].z, acc, 0, 0, 0);
+		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].w, vy[q].w, acc, 0, 0, 0);
+	}
+	return acc;
+}
+
+__device__ inline int quad_row(int v, int lane) { return (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5); }
+
+// s_t[r][c] = T[r][c] - (X Y^T)[r][c] for the workgroup's quadrant of a 64 x 64 tile T (global, row stride ld)
+__device__ inline void stage_updated_tile(const float* T, const float* X, const float* Y, int64_t ld, int wave, int lane, float* s_t) {
+	const int qr = wave >> 1, qc = wave & 1;
+	float tv[16];
+#pragma unroll
+	for (int v = 0; v < 16; v++) tv[v] = T[(32 * qr + quad_row(v, lane)) * ld + 32 * qc + (lane & 31)];
+	const f32x16 acc = quadrant_xyt(X, Y, ld, qr, qc, lane);
+#pragma unroll
+	for (int v = 0; v < 16; v++) s_t[(32 * qr + quad_row(v, lane)) * CS4 + 32 * qc + (lane & 31)] = tv[v] - acc[v];
+}
+
+// b_J -= L_J y for a 64 x 64 tile L (row stride ld) and the 64-vector y: 4 threads per row, 16 columns each
+__device__ inline float rhs_row_update(const float* L, int64_t ld, const float* y, int t) {
+	const int r = t >> 2, q4 = t & 3;
+	const float* Lr = L + r * ld + 16 * q4;
+	const float* yq = y + 16 * q4;
+	float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+	for (int c = 0; c < 16; c += 2) {
+		s0 += Lr[c] * yq[c];
+		s1 += Lr[c + 1] * yq[c + 1];
+	}
+	float s = s0 + s1;
+	s += __shfl_xor(s, 1);
+	s += __shfl_xor(s, 2);
+	return s;
+}
+
+#if NNRT_FIT_VARIANT == 30   // development: s_memrealtime phase stamps of the diagonal workgroup (tools/chol_stamps.py)
 __device__ unsigned long long g_chol_stamps[64][8];
 #define CSTAMP(i) \
 	do { \
-		if (threadIdx.x == 0 && k < 64) g_chol_stamps[k][i] = __builtin_amdgcn_s_memrealtime(); \
+		if (blockIdx.x == 0 && threadIdx.x == 0 && k < 64) { \
+			g_chol_stamps[k][i] = __builtin_amdgcn_s_memrealtime(); \
+			g_chol_stamps[k][4 + i] = __builtin_amdgcn_s_memtime(); \
+		} \
 	} while (0)
 extern "C" int nnrt_dev_chol_stamps(unsigned long long* host) {
 	return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_chol_stamps), sizeof(g_chol_stamps)) == hipSuccess ? 0 : 1;
@@ -319,266 +393,180 @@ extern "C" int nnrt_dev_chol_stamps(unsigned long long* host) {
 #define CSTAMP(i) do {} while (0)
 #endif
 
-// The 64 x 64 diagonal block is factored in four 16-column steps inside one workgroup: wave 0 factors the 16 x 16
-// diagonal sub-block in registers (lane = row, static register indices, pivots and columns broadcast with readlane) and
-// inverts it; the rows below are solved against that inverse and the trailing lower triangle updated by all threads.
-// L^-1 of the whole block is then assembled block row by block row from the four 16 x 16 inverses.
-constexpr int CS = CORNER_NB + 1;   // LDS row stride
-
-// 16 x 16 lower Cholesky + inverse of the sub-block at (o, o) of s (row stride CS), lanes 0..15 of one wave
-__device__ inline float lane_bcast(float v, int src) {
-	return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
-}
-
-// 16 x 16 lower Cholesky + inverse of the sub-block at (o, o) of s (row stride CS), lanes 0..15 of one wave. The
-// column chain is latency-bound (one wave): hardware square root / reciprocal, independent partial sums.
-__device__ inline bool potrf16_inv16(float* s, int o, float* x16, int lane) {
-	float a[16];
-	const int r = lane & 15;
-#pragma unroll
-	for (int c = 0; c < 16; c++) a[c] = s[(o + r) * CS + o + c];
-	bool ok = true;
-	float inv_diag[16];
-#pragma unroll
-	for (int j = 0; j < 16; j++) {
-		float d = lane_bcast(a[j], j);
-		if (!(d > 0.f)) {
-			ok = false;
-			d = 1.f;
-		}
-		const float ip = __builtin_amdgcn_rsqf(d);   // 1 / sqrt(d)
-		inv_diag[j] = ip;
-		const float l = r > j ? a[j] * ip : (r == j ? d * ip : 0.f);
-		a[j] = l;
-#pragma unroll
-		for (int c = j + 1; c < 16; c++) a[c] -= l * lane_bcast(l, c);
-	}
-	// inverse, lane = column: x_i = (delta_ir - sum_{k<i} L_ik x_k) / L_ii with L_ik broadcast from lane i
-	float x[16];
-#pragma unroll
-	for (int i = 0; i < 16; i++) {
-		float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-		for (int q = 0; q < i; q++) {
-			if (q & 1) s1 += lane_bcast(a[q], i) * x[q];
-			else s0 += lane_bcast(a[q], i) * x[q];
-		}
-		x[i] = ((r == i ? 1.f : 0.f) - (s0 + s1)) * inv_diag[i];
-	}
-	if (lane < 16) {
-#pragma unroll
-		for (int c = 0; c < 16; c++) {
-			s[(o + r) * CS + o + c] = c <= r ? a[c] : 0.f;
-			x16[c * 17 + r] = x[c];   // x16[i][col]
-		}
-	}
-	return ok;
-}
-
-__global__ __launch_bounds__(CT) void k_chol_diag(float* __restrict__ A, int ld, int k, float* __restrict__ linv, float* __restrict__ b,
-                                                  int* error_flag) {
-	__shared__ float s_a[CORNER_NB * CS];          // the block, then L
-	__shared__ float s_x[CORNER_NB * CS];          // L^-1 (and scratch)
-	__shared__ float s_x16[4][16 * 17];            // inverses of the 16 x 16 diagonal sub-blocks
-	__shared__ float s_b[CORNER_NB];
-	__shared__ int s_fail;
+__global__ __launch_bounds__(CT) void k_chol_step(float* __restrict__ A, int ld, int k, int T, float* __restrict__ b, int* error_flag) {
+	__shared__ float s_d[CORNER_NB * CS4];   // A_kk after the previous block's update
+	__shared__ float s_p[CORNER_NB * CS4];   // A_Ik after the previous block's update (panel workgroups below the diagonal)
+	__shared__ float s_b[CORNER_NB];         // b_k after the previous block's update (diagonal workgroup)
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-	const int64_t o = static_cast<int64_t>(k) * CORNER_NB;
+	const int64_t LD = ld;
+	const int npanel = T - k;
+	const int64_t ok0 = static_cast<int64_t>(k) * CORNER_NB, op = ok0 - CORNER_NB;   // column offsets of blocks k and k - 1
+	if (static_cast<int>(blockIdx.x) >= npanel) {
+		// ---- trailing tile (I, J), k < J <= I: the previous block's update ----
+		int r = static_cast<int>(blockIdx.x) - npanel, ii = 0;
+		while (r > ii) {   // row ii holds ii + 1 tiles
+			r -= ii + 1;
+			ii++;
+		}
+		const int64_t rI = static_cast<int64_t>(k + 1 + ii) * CORNER_NB, rJ = static_cast<int64_t>(k + 1 + r) * CORNER_NB;
+		const int qr = wave >> 1, qc = wave & 1;
+		float* C = A + rI * LD + rJ + 32 * qc + (lane & 31);
+		float cv[16];
+#pragma unroll
+		for (int v = 0; v < 16; v++) cv[v] = C[(32 * qr + quad_row(v, lane)) * LD];
+		const f32x16 acc = quadrant_xyt(A + rI * LD + op, A + rJ * LD + op, LD, qr, qc, lane);
+#pragma unroll
+		for (int v = 0; v < 16; v++) C[(32 * qr + quad_row(v, lane)) * LD] = cv[v] - acc[v];
+		if (rI == rJ) {
+			const float s = rhs_row_update(A + rJ * LD + op, LD, b + op, t);
+			if ((t & 3) == 0) b[rJ + (t >> 2)] -= s;
+		}
+		return;
+	}
+	// ---- panel row I = k + blockIdx.x ----
 	CSTAMP(0);
-	for (int e = t; e < CORNER_NB * CORNER_NB; e += CT) s_a[(e / CORNER_NB) * CS + e % CORNER_NB] = A[(o + e / CORNER_NB) * ld + o + e % CORNER_NB];
-	if (t < CORNER_NB) s_b[t] = b[o + t];
-	if (t == 0) s_fail = 0;
+	const bool diag = blockIdx.x == 0;
+	const int64_t rI = ok0 + static_cast<int64_t>(blockIdx.x) * CORNER_NB;
+	if (k > 0) {
+		stage_updated_tile(A + ok0 * LD + ok0, A + ok0 * LD + op, A + ok0 * LD + op, LD, wave, lane, s_d);
+		if (!diag) {
+			stage_updated_tile(A + rI * LD + ok0, A + rI * LD + op, A + ok0 * LD + op, LD, wave, lane, s_p);
+		} else {
+			const float s = rhs_row_update(A + ok0 * LD + op, LD, b + op, t);
+			if ((t & 3) == 0) s_b[t >> 2] = b[ok0 + (t >> 2)] - s;
+		}
+	} else {
+		for (int e = t; e < CORNER_NB * CORNER_NB; e += CT) {
+			const int rr = e / CORNER_NB, cc = e % CORNER_NB;
+			s_d[rr * CS4 + cc] = A[(ok0 + rr) * LD + ok0 + cc];
+			if (!diag) s_p[rr * CS4 + cc] = A[(rI + rr) * LD + ok0 + cc];
+		}
+		if (diag && t < CORNER_NB) s_b[t] = b[ok0 + t];
+	}
 	__syncthreads();
 	CSTAMP(1);
-	for (int p = 0; p < 4; p++) {
-		const int o16 = 16 * p;
-		if (wave == 0) {
-			if (!potrf16_inv16(s_a, o16, s_x16[p], lane) && lane == 0) s_fail = 1;
-		}
-		__syncthreads();
-		if (p == 0) CSTAMP(5);
-		const int rows = CORNER_NB - o16 - 16;
-		if (rows > 0) {
-			// panel rows below: L_r = A_r X16^T (X16 lower) into scratch, then back into s_a
-			for (int e = t; e < rows * 16; e += CT) {
-				const int rr = o16 + 16 + e / 16, c = e % 16;
-				float acc = 0.f;
+	if (wave != 0) return;
+	// ap[c] = (A_kk[lane][c], A_Ik[lane][c]): both rows see the same column operations, so one packed FMA
+	// (v_pk_fma_f32) updates the pair
+	f32x2 ap[CORNER_NB];
 #pragma unroll
-				for (int q = 0; q < 16; q++) acc += s_a[rr * CS + o16 + q] * s_x16[p][c * 17 + q];
-				s_x[rr * CS + c] = acc;
-			}
-			__syncthreads();
-			for (int e = t; e < rows * 16; e += CT) {
-				const int rr = o16 + 16 + e / 16, c = e % 16;
-				s_a[rr * CS + o16 + c] = s_x[rr * CS + c];
-			}
-			__syncthreads();
-			if (p == 0) CSTAMP(6);
-			// trailing lower triangle: A_rc -= sum_q L_rq L_cq
-			for (int e = t; e < rows * rows; e += CT) {
-				const int rr = o16 + 16 + e / rows, cc = o16 + 16 + e % rows;
-				if (cc > rr) continue;
-				float acc = 0.f;
-#pragma unroll
-				for (int q = 0; q < 16; q++) acc += s_a[rr * CS + o16 + q] * s_a[cc * CS + o16 + q];
-				s_a[rr * CS + cc] -= acc;
-			}
-			__syncthreads();
-			if (p == 0) CSTAMP(7);
-		}
+	for (int q = 0; q < CORNER_NB / 4; q++) {
+		const float4 va = *reinterpret_cast<const float4*>(s_d + lane * CS4 + 4 * q);
+		float4 vp;
+		if (diag)   // the augmented row: b_k on lane 0, zero elsewhere
+			vp = lane == 0 ? *reinterpret_cast<const float4*>(s_b + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+		else
+			vp = *reinterpret_cast<const float4*>(s_p + lane * CS4 + 4 * q);
+		ap[4 * q] = f32x2{va.x, vp.x};
+		ap[4 * q + 1] = f32x2{va.y, vp.y};
+		ap[4 * q + 2] = f32x2{va.z, vp.z};
+		ap[4 * q + 3] = f32x2{va.w, vp.w};
 	}
+	// Column eliminations in blocks of four: the four columns are factored among themselves, then applied to every
+	// later column c with four packed FMAs whose multipliers L_c,jb..jb+3 are read from lane c by readlane (scalar
+	// operands: nothing on the elimination path waits on LDS). Every element sees its updates in ascending column order.
+	__shared__ float4 s_l4[2][CORNER_NB];   // s_l4[.][c] = (L_c,jb .. L_c,jb+3)
 	CSTAMP(2);
-	// L^-1: diagonal blocks X_II = inverse of L_II; block row I: X_IJ = -X_II (sum_{J<=K<I} L_IK X_KJ), J < I
-	for (int e = t; e < CORNER_NB * CORNER_NB; e += CT) {
-		const int r = e / CORNER_NB, c = e % CORNER_NB;
-		s_x[r * CS + c] = (r / 16 == c / 16) ? s_x16[r / 16][(r % 16) * 17 + c % 16] : 0.f;
-	}
-	__syncthreads();
-	for (int I = 1; I < 4; I++) {
-		// tmp_IJ = sum_{K=J}^{I-1} L_IK X_KJ for every J < I (16 x 16 I values; at most 3 per thread, static slots)
-		const int n = 16 * 16 * I;
-		float tmp[3];
+	int bad = 0;
+#pragma clang loop unroll(full)
+	for (int jb = 0; jb < CORNER_NB; jb += 4) {
+		float lx[4];
+		f32x2 nl[4];
 #pragma unroll
-		for (int it = 0; it < 3; it++) {
-			const int e = t + it * CT;
-			tmp[it] = 0.f;
-			if (e < n) {
-				const int r = e / (16 * I), cg = e % (16 * I);
-				const int J = cg / 16;
-				float acc = 0.f;
-				for (int q = 16 * J; q < 16 * I; q++) acc += s_a[(16 * I + r) * CS + q] * s_x[q * CS + cg];
-				tmp[it] = acc;
+		for (int q = 0; q < 4; q++) {
+			const int j = jb + q;
+			float piv = lane_bcast(ap[j].x, j);   // A_jj after the first j eliminations
+			bad |= !(piv > 0.f);
+			piv = piv > 0.f ? piv : 1.f;
+			const float rs = __builtin_amdgcn_rsqf(piv);
+			const f32x2 l = ap[j] * rs;   // (L_rj for rows r >= j of the diagonal block, panel / rhs entry)
+			ap[j] = l;
+			lx[q] = l.x;
+			nl[q] = -l;
+#pragma unroll
+			for (int q2 = q + 1; q2 < 4; q2++) {
+				const float lc = lane_bcast(l.x, jb + q2);
+				ap[jb + q2] = __builtin_elementwise_fma(nl[q], f32x2{lc, lc}, ap[jb + q2]);
 			}
 		}
-		__syncthreads();
+		// next block's columns first (readlane: on the pivot chain), the rest from a wave-uniform 16-B LDS broadcast
+		// whose latency hides behind them
+		float4* row = &s_l4[(jb >> 2) & 1][0];
+		if (jb + 8 < CORNER_NB) row[lane] = make_float4(lx[0], lx[1], lx[2], lx[3]);
 #pragma unroll
-		for (int it = 0; it < 3; it++) {
-			const int e = t + it * CT;
-			if (e < n) s_x[(16 * I + e / (16 * I)) * CS + e % (16 * I)] = tmp[it];   // staged: block row I, columns < 16 I
-		}
-		__syncthreads();
+		for (int q = 0; q < 4; q++)   // q outer: consecutive FMAs are independent
 #pragma unroll
-		for (int it = 0; it < 3; it++) {
-			const int e = t + it * CT;
-			if (e < n) {
-				const int r = e / (16 * I), cg = e % (16 * I);
-				float acc = 0.f;
-#pragma unroll
-				for (int q = 0; q < 16; q++) acc += s_x16[I][r * 17 + q] * s_x[(16 * I + q) * CS + cg];
-				tmp[it] = -acc;
+			for (int c = jb + 4; c < CORNER_NB && c < jb + 8; c++) {
+				const float lc = lane_bcast(lx[q], c);   // L_c,jb+q, c > jb + 3
+				ap[c] = __builtin_elementwise_fma(nl[q], f32x2{lc, lc}, ap[c]);
 			}
-		}
-		__syncthreads();
 #pragma unroll
-		for (int it = 0; it < 3; it++) {
-			const int e = t + it * CT;
-			if (e < n) s_x[(16 * I + e / (16 * I)) * CS + e % (16 * I)] = tmp[it];
+		for (int c0 = jb + 8; c0 < CORNER_NB; c0 += 8) {   // chunks of 8 columns: 8 broadcasts in flight
+			float4 L4[8];
+#pragma unroll
+			for (int u = 0; u < 8; u++)
+				if (c0 + u < CORNER_NB) L4[u] = row[c0 + u];
+#pragma unroll
+			for (int u = 0; u < 8; u++)
+				if (c0 + u < CORNER_NB) ap[c0 + u] = __builtin_elementwise_fma(nl[0], f32x2{L4[u].x, L4[u].x}, ap[c0 + u]);
+#pragma unroll
+			for (int u = 0; u < 8; u++)
+				if (c0 + u < CORNER_NB) ap[c0 + u] = __builtin_elementwise_fma(nl[1], f32x2{L4[u].y, L4[u].y}, ap[c0 + u]);
+#pragma unroll
+			for (int u = 0; u < 8; u++)
+				if (c0 + u < CORNER_NB) ap[c0 + u] = __builtin_elementwise_fma(nl[2], f32x2{L4[u].z, L4[u].z}, ap[c0 + u]);
+#pragma unroll
+			for (int u = 0; u < 8; u++)
+				if (c0 + u < CORNER_NB) ap[c0 + u] = __builtin_elementwise_fma(nl[3], f32x2{L4[u].w, L4[u].w}, ap[c0 + u]);
 		}
-		__syncthreads();
 	}
+	const bool ok = !bad;
 	CSTAMP(3);
-	float* Li = linv + static_cast<int64_t>(k) * CORNER_NB * CORNER_NB;
-	for (int e = t; e < CORNER_NB * CORNER_NB; e += CT) {
-		const int r = e / CORNER_NB, c = e % CORNER_NB;
-		A[(o + r) * ld + o + c] = c <= r ? s_a[r * CS + c] : 0.f;
-		Li[e] = s_x[r * CS + c];
-	}
-	// forward substitution of the augmented column: y_k = L_kk^-1 b_k (b_k already carries every earlier block's update)
-	if (t < CORNER_NB) {
-		float y = 0.f;
-		for (int c = 0; c <= t; c++) y += s_x[t * CS + c] * s_b[c];
-		b[o + t] = y;
-	}
-	__syncthreads();
-	CSTAMP(4);
-	if (s_fail && t == 0) atomicOr(error_flag, 1);
-}
-
-// 64 x 64 x 64 tile product in LDS: thread (ty, tx) owns rows 4 ty.., columns 4 tx.. of C = X Y^T
-__device__ inline void tile_xyt(const float (*X)[CORNER_NB + 1], const float (*Y)[CORNER_NB + 1], int ty, int tx, float (&c)[4][4]) {
+	if (diag) {
+		float4* wa = reinterpret_cast<float4*>(A + (ok0 + lane) * LD + ok0);
 #pragma unroll
-	for (int r = 0; r < 4; r++)
+		for (int q = 0; q < CORNER_NB / 4; q++)
+			wa[q] = make_float4(4 * q <= lane ? ap[4 * q].x : 0.f, 4 * q + 1 <= lane ? ap[4 * q + 1].x : 0.f,
+			                    4 * q + 2 <= lane ? ap[4 * q + 2].x : 0.f, 4 * q + 3 <= lane ? ap[4 * q + 3].x : 0.f);
+		if (lane == 0) {
+			float4* wb = reinterpret_cast<float4*>(b + ok0);
 #pragma unroll
-		for (int q = 0; q < 4; q++) c[r][q] = 0.f;
-	for (int kk = 0; kk < CORNER_NB; kk++) {
-		float x[4], y[4];
+			for (int q = 0; q < CORNER_NB / 4; q++) wb[q] = make_float4(ap[4 * q].y, ap[4 * q + 1].y, ap[4 * q + 2].y, ap[4 * q + 3].y);
+			if (!ok) atomicOr(error_flag, 1);
+		}
+	} else {
+		float4* wp = reinterpret_cast<float4*>(A + (rI + lane) * LD + ok0);
 #pragma unroll
-		for (int r = 0; r < 4; r++) x[r] = X[4 * ty + r][kk];
-#pragma unroll
-		for (int q = 0; q < 4; q++) y[q] = Y[4 * tx + q][kk];
-#pragma unroll
-		for (int r = 0; r < 4; r++)
-#pragma unroll
-			for (int q = 0; q < 4; q++) c[r][q] += x[r] * y[q];
+		for (int q = 0; q < CORNER_NB / 4; q++) wp[q] = make_float4(ap[4 * q].y, ap[4 * q + 1].y, ap[4 * q + 2].y, ap[4 * q + 3].y);
 	}
 }
 
-// L_Ik = A_Ik L_kk^-T for block rows I = k + 1 + blockIdx.x
-__global__ __launch_bounds__(CT) void k_chol_panel(float* __restrict__ A, int ld, int k, const float* __restrict__ linv, float* __restrict__ b) {
-	__shared__ float s_x[CORNER_NB][CORNER_NB + 1];
-	__shared__ float s_y[CORNER_NB][CORNER_NB + 1];
-	const int t = threadIdx.x;
-	const int64_t rI = static_cast<int64_t>(k + 1 + blockIdx.x) * CORNER_NB, ck = static_cast<int64_t>(k) * CORNER_NB;
-	const float* Li = linv + static_cast<int64_t>(k) * CORNER_NB * CORNER_NB;
-	for (int e = t; e < CORNER_NB * CORNER_NB; e += CT) {
-		s_x[e / CORNER_NB][e % CORNER_NB] = A[(rI + e / CORNER_NB) * ld + ck + e % CORNER_NB];
-		s_y[e / CORNER_NB][e % CORNER_NB] = Li[e];
-	}
+// L_kk^-1 for every diagonal block (one wave each): lane c solves L x = e_c by right-looking substitution with the
+// columns of L_kk broadcast from LDS (stored transposed so each column is contiguous)
+__global__ __launch_bounds__(64) void k_chol_diag_inverse(const float* __restrict__ A, int ld, float* __restrict__ linv) {
+	__shared__ float s_lt[CORNER_NB][CORNER_NB + 4];   // s_lt[c][r] = L[r][c]
+	const int lane = threadIdx.x, k = blockIdx.x;
+	const int64_t o = static_cast<int64_t>(k) * CORNER_NB;
+	for (int r = 0; r < CORNER_NB; r++) s_lt[lane][r] = A[(o + r) * ld + o + lane];
 	__syncthreads();
-	const int ty = t / 16, tx = t % 16;
-	float c[4][4];
-	tile_xyt(s_x, s_y, ty, tx, c);
+	float z[CORNER_NB];
 #pragma unroll
-	for (int r = 0; r < 4; r++)
+	for (int r = 0; r < CORNER_NB; r++) z[r] = r == lane ? 1.f : 0.f;
 #pragma unroll
-		for (int q = 0; q < 4; q++) A[(rI + 4 * ty + r) * ld + ck + 4 * tx + q] = c[r][q];
-	// augmented column: b_I -= L_Ik y_k (rows 4 ty + r; the 16 threads of a row group share the sum through LDS)
-	__syncthreads();
-	float* s_part = &s_x[0][0];   // [64][16]
+	for (int i = 0; i < CORNER_NB; i++) {
+		const float xi = z[i] / s_lt[i][i];
+		z[i] = xi;
 #pragma unroll
-	for (int r = 0; r < 4; r++) {
-		float acc = 0.f;
-#pragma unroll
-		for (int q = 0; q < 4; q++) acc += c[r][q] * b[ck + 4 * tx + q];
-		s_part[(4 * ty + r) * 16 + tx] = acc;
+		for (int r = i + 1; r < CORNER_NB; r++) z[r] -= s_lt[i][r] * xi;
 	}
-	__syncthreads();
-	if (t < CORNER_NB) {
-		float acc = 0.f;
-		for (int q = 0; q < 16; q++) acc += s_part[t * 16 + q];
-		b[rI + t] -= acc;
-	}
-}
-
-// A_IJ -= L_Ik L_Jk^T for the lower tiles k < J <= I of the trailing matrix (blockIdx.x enumerates them row by row)
-__global__ __launch_bounds__(CT) void k_chol_update(float* __restrict__ A, int ld, int k) {
-	__shared__ float s_x[CORNER_NB][CORNER_NB + 1];
-	__shared__ float s_y[CORNER_NB][CORNER_NB + 1];
-	int b = static_cast<int>(blockIdx.x), ii = 0;
-	while (b > ii) {   // row ii holds ii + 1 tiles
-		b -= ii + 1;
-		ii++;
-	}
-	const int I = k + 1 + ii, J = k + 1 + b;
-	const int t = threadIdx.x;
-	const int64_t ck = static_cast<int64_t>(k) * CORNER_NB, rI = static_cast<int64_t>(I) * CORNER_NB, rJ = static_cast<int64_t>(J) * CORNER_NB;
-	for (int e = t; e < CORNER_NB * CORNER_NB; e += CT) {
-		s_x[e / CORNER_NB][e % CORNER_NB] = A[(rI + e / CORNER_NB) * ld + ck + e % CORNER_NB];
-		s_y[e / CORNER_NB][e % CORNER_NB] = A[(rJ + e / CORNER_NB) * ld + ck + e % CORNER_NB];
-	}
-	__syncthreads();
-	const int ty = t / 16, tx = t % 16;
-	float c[4][4];
-	tile_xyt(s_x, s_y, ty, tx, c);
+	float* Li = linv + static_cast<int64_t>(k) * CORNER_NB * CORNER_NB;   // Li[r][c] = (L_kk^-1)_rc
 #pragma unroll
-	for (int r = 0; r < 4; r++)
-#pragma unroll
-		for (int q = 0; q < 4; q++) A[(rI + 4 * ty + r) * ld + rJ + 4 * tx + q] -= c[r][q];
+	for (int r = 0; r < CORNER_NB; r++) Li[r * CORNER_NB + lane] = z[r];
 }
 
 // back substitution L^T x = y in place, right-looking over block rows: launch k (from the last block) has
-// workgroup i < k form x_k = L_kk^-T y_k (each workgroup redundantly, 64 x 64) and apply y_i -= L_ki^T x_k; workgroup
-// k itself stores x_k. Block rows are read coalesced (L_ki is row block k).
+// workgroup i < k form x_k = L_kk^-T y_k (each workgroup redundantly) and apply y_i -= L_ki^T x_k; workgroup k itself
+// stores x_k. The operands that do not depend on y (L_kk^-1 and the L_ki tile) are loaded before y_k.
 __global__ __launch_bounds__(CT) void k_chol_back_step(const float* __restrict__ A, int ld, int k, const float* __restrict__ linv,
                                                        float* __restrict__ b) {
 	__shared__ float s_y[CORNER_NB], s_x[CORNER_NB];
@@ -586,13 +574,20 @@ __global__ __launch_bounds__(CT) void k_chol_back_step(const float* __restrict__
 	const int t = threadIdx.x, c = t % CORNER_NB, seg = t / CORNER_NB;
 	const int i = static_cast<int>(blockIdx.x);   // target block (i == k: store x_k)
 	const int64_t ck = static_cast<int64_t>(k) * CORNER_NB, ci = static_cast<int64_t>(i) * CORNER_NB;
+	const float* Li = linv + static_cast<int64_t>(k) * CORNER_NB * CORNER_NB;
+	float li[16], lk[16];
+#pragma unroll
+	for (int q = 0; q < 16; q++) li[q] = Li[(seg * 16 + q) * CORNER_NB + c];
+	if (i != k) {
+#pragma unroll
+		for (int q = 0; q < 16; q++) lk[q] = A[(ck + seg * 16 + q) * ld + ci + c];
+	}
 	if (t < CORNER_NB) s_y[t] = b[ck + t];
 	__syncthreads();
 	// x_k[c] = sum_q Linv[q][c] y_q
-	const float* Li = linv + static_cast<int64_t>(k) * CORNER_NB * CORNER_NB;
 	float acc = 0.f;
 #pragma unroll
-	for (int q = seg * 16; q < seg * 16 + 16; q++) acc += Li[q * CORNER_NB + c] * s_y[q];
+	for (int q = 0; q < 16; q++) acc += li[q] * s_y[seg * 16 + q];
 	s_part[seg][c] = acc;
 	__syncthreads();
 	if (t < CORNER_NB) s_x[t] = (s_part[0][t] + s_part[1][t]) + (s_part[2][t] + s_part[3][t]);
@@ -604,7 +599,7 @@ __global__ __launch_bounds__(CT) void k_chol_back_step(const float* __restrict__
 	// y_i[c] -= sum_r L[k-block row r][i-block col c] x_k[r]
 	acc = 0.f;
 #pragma unroll
-	for (int r = seg * 16; r < seg * 16 + 16; r++) acc += A[(ck + r) * ld + ci + c] * s_x[r];
+	for (int q = 0; q < 16; q++) acc += lk[q] * s_x[seg * 16 + q];
 	__syncthreads();
 	s_part[seg][c] = acc;
 	__syncthreads();
@@ -618,17 +613,14 @@ __global__ void k_corner_out(int m, const float* __restrict__ cb, float* __restr
 
 nnrt_status corner_cholesky_solve(float* A, int ld, float* linv, float* cb, int* error_flag, hipStream_t stream) {
 	const int T = ld / CORNER_NB;
-	for (int k = 0; k < T; k++) {   // factor [S | b]: the forward substitution rides along as an augmented column
-		k_chol_diag<<<1, CT, 0, stream>>>(A, ld, k, linv, cb, error_flag);
+	for (int k = 0; k < T; k++) {   // factor [S | b]: the forward substitution rides along as an augmented row
+		const int panel = T - k, below = T - 1 - k;
+		const int trailing = k > 0 ? below * (below + 1) / 2 : 0;
+		k_chol_step<<<panel + trailing, CT, 0, stream>>>(A, ld, k, T, cb, error_flag);
 		NNRT_LAUNCH_CHECK();
-		const int below = T - 1 - k;
-		if (below > 0) {
-			k_chol_panel<<<below, CT, 0, stream>>>(A, ld, k, linv, cb);
-			NNRT_LAUNCH_CHECK();
-			k_chol_update<<<below * (below + 1) / 2, CT, 0, stream>>>(A, ld, k);
-			NNRT_LAUNCH_CHECK();
-		}
 	}
+	k_chol_diag_inverse<<<T, 64, 0, stream>>>(A, ld, linv);
+	NNRT_LAUNCH_CHECK();
 	for (int k = T - 1; k >= 0; k--) {
 		k_chol_back_step<<<k + 1, CT, 0, stream>>>(A, ld, k, linv, cb);
 		NNRT_LAUNCH_CHECK();

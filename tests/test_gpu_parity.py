@@ -173,7 +173,7 @@ def test_rodrigues_and_block_cholesky_kats(nn, oracle_mod):
         nn.core.linalg.SolveBlockDiagonalCholesky(-L.CHOLESKY_A, L.CHOLESKY_B[:, 0])
 
 
-@pytest.mark.parametrize("n0,n1,degree", [(40, 6, 4), (300, 30, 4), (1, 1, 1)])
+@pytest.mark.parametrize("n0,n1,degree", [(40, 6, 4), (300, 30, 4), (1, 1, 1), (2000, 200, 4)])
 def test_arrowhead_solver_vs_oracle(nn, oracle_mod, n0, n1, degree):
     rng = np.random.default_rng(n0)
     N = n0 + n1

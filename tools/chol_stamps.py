@@ -34,18 +34,16 @@ def main():
     lib.nnrt_dev_chol_stamps.argtypes = [ctypes.c_void_p]
     buf = np.zeros((64, 8), np.uint64)
     assert lib.nnrt_dev_chol_stamps(buf.ctypes.data) == 0
-    rows = buf[(buf[:, 4] > 0)].astype(np.int64)
-    d = np.diff(rows[:, :5], axis=1) * 10 / 1000.0
-    names = ["global loads", "potrf", "scale + L^-1", "store + y_k"]
-    print(f"k_chol_diag: {len(rows)} blocks")
+    rows = buf[(buf[:, 3] > 0)].astype(np.int64)
+    d = np.diff(rows[:, :4], axis=1) * 10 / 1000.0
+    names = ["stage (update tiles)", "registers", "elimination"]
+    print(f"k_chol_step diagonal workgroup: {len(rows)} blocks")
     for i, n in enumerate(names):
         print(f"    {n:16s} mean {d[:, i].mean():8.2f} us  max {d[:, i].max():8.2f}")
-    sub = rows[:, [1, 5, 6, 7]]
-    if (sub > 0).all():
-        ds = np.diff(sub, axis=1) * 10 / 1000.0
-        for i, n in enumerate(["p=0 potrf16+inv16", "p=0 panel", "p=0 trailing"]):
-            print(f"    {n:16s} mean {ds[:, i].mean():8.2f} us")
-
+    clk = (rows[:, 7] - rows[:, 4]) / ((rows[:, 3] - rows[:, 0]) * 10e-9) / 1e9
+    print(f"    s_memtime rate over the workgroup's span: mean {clk.mean():.3f} GHz (min {clk.min():.3f}, max {clk.max():.3f})")
+    for k in (0, 1, len(rows) // 2, len(rows) - 1):
+        print(f"    k={k}: " + " ".join(f"{x:7.2f}" for x in d[k]))
 
 if __name__ == "__main__":
     main()
