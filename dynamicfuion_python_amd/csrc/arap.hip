@@ -46,6 +46,7 @@ __global__ void k_arap_edges(ArapArgs a) {
 	} else {
 		if (j >= a.E) {   // reference indexes edge_layer_indices[node_j] (A3); out of bounds there
 			atomicOr(a.error_flag, 2);
+			for (int q = 0; q < EDGE_TERMS; q++) a.edge_jr[static_cast<int64_t>(e) * EDGE_TERMS + q] = 0.f;
 			return;
 		}
 		w_res = a.radii[a.edge_layers[j]];
@@ -65,22 +66,6 @@ __global__ void k_arap_edges(ArapArgs a) {
 	const float j5[5] = {s * Rd.x, s * Rd.y, s * Rd.z, a.lambda * w_jac, -a.lambda * w_jac};
 	float dEi[3][6];
 	edge_block_i(j5, dEi);
-	// diagonal contributions (ComputeBlockSums of dEi^T dEi / dEj^T dEj)
-	float* acc_i = a.acc + static_cast<int64_t>(i) * ACC_STRIDE;
-	float* acc_j = a.acc + static_cast<int64_t>(j) * ACC_STRIDE;
-	int q = 0;
-#pragma unroll
-	for (int r0 = 0; r0 < 6; r0++)
-#pragma unroll
-		for (int c0 = r0; c0 < 6; c0++) {
-			const float v = (dEi[0][r0] * dEi[0][c0] + dEi[1][r0] * dEi[1][c0]) + dEi[2][r0] * dEi[2][c0];
-			atomicAdd(acc_i + q, v);
-			q++;
-		}
-	const float bb = (j5[4] * j5[4] + 0.f * 0.f) + 0.f * 0.f;
-	atomicAdd(acc_j + 15, bb);   // (3,3) in the upper-triangle enumeration
-	atomicAdd(acc_j + 18, bb);   // (4,4)
-	atomicAdd(acc_j + 20, bb);   // (5,5)
 	// wing block dEi^T dEj: dEj = [0 | b I]
 	float* wb = a.wing + static_cast<int64_t>(e) * 36;
 #pragma unroll
@@ -94,14 +79,25 @@ __global__ void k_arap_edges(ArapArgs a) {
 			}
 			wb[6 * r0 + c0] = v;
 		}
-	// J^T e (the accumulator stores +J^T r; the solve negates)
+	// the edge's contributions to its two nodes' diagonal blocks and gradients, summed per node by k_arrow_prepare (no
+	// atomics; every node sums its incident edges in ascending edge order): source i: dEi^T dEi (21 upper-triangle
+	// entries, ComputeBlockSums) + J_i^T e (6); target j: b^2 on the translation diagonal + b e (3)
+	float* src = a.edge_jr + static_cast<int64_t>(e) * EDGE_TERMS;
+	int q = 0;
+#pragma unroll
+	for (int r0 = 0; r0 < 6; r0++)
+#pragma unroll
+		for (int c0 = r0; c0 < 6; c0++) src[q++] = (dEi[0][r0] * dEi[0][c0] + dEi[1][r0] * dEi[1][c0]) + dEi[2][r0] * dEi[2][c0];
 	const float skT[3][3] = {{0.f, j5[2], -j5[1]}, {-j5[2], 0.f, j5[0]}, {j5[1], -j5[0], 0.f}};
 #pragma unroll
 	for (int c = 0; c < 3; c++) {
-		atomicAdd(acc_i + 21 + c, (skT[c][0] * r[0] + skT[c][1] * r[1]) + skT[c][2] * r[2]);
-		atomicAdd(acc_i + 24 + c, j5[3] * r[c]);
-		atomicAdd(acc_j + 24 + c, j5[4] * r[c]);
+		src[21 + c] = (skT[c][0] * r[0] + skT[c][1] * r[1]) + skT[c][2] * r[2];
+		src[24 + c] = j5[3] * r[c];
 	}
+	src[27] = (j5[4] * j5[4] + 0.f * 0.f) + 0.f * 0.f;   // target j: dEj = [0 | b I]
+#pragma unroll
+	for (int c = 0; c < 3; c++) src[28 + c] = j5[4] * r[c];
+	src[31] = 0.f;
 }
 
 nnrt_status launch_arap_edges(const ArapArgs& args, hipStream_t stream) {
@@ -111,37 +107,63 @@ nnrt_status launch_arap_edges(const ArapArgs& args, hipStream_t stream) {
 	return NNRT_OK;
 }
 
-// ---- acc (data) + arap_acc -> full diagonal blocks (+LM) and rhs = negative gradient ----
-__global__ void k_arrow_prepare(int N, float lm, double* __restrict__ acc, float* __restrict__ arap_acc, float* __restrict__ diag,
-                                float* __restrict__ rhs, float* __restrict__ gradient_out, float* __restrict__ hessian_out) {
-	const int n = blockIdx.x * blockDim.x + threadIdx.x;
-	if (n >= N) return;
-	double* ad = acc + static_cast<int64_t>(n) * ACC_STRIDE;
-	float* aa = arap_acc + static_cast<int64_t>(n) * ACC_STRIDE;
-	float* d = diag + static_cast<int64_t>(n) * 36;
-	int q = 0;
-	for (int r = 0; r < 6; r++)
-		for (int c = r; c < 6; c++) {
-			const float hd = static_cast<float>(ad[q]);
-			const float v = aa[q] + hd;
-			if (hessian_out) {
-				hessian_out[static_cast<int64_t>(n) * 36 + 6 * r + c] = hd;
-				hessian_out[static_cast<int64_t>(n) * 36 + 6 * c + r] = hd;
-			}
-			d[6 * r + c] = v;
-			d[6 * c + r] = v;
-			q++;
+// ---- data acc + ARAP edge terms -> full diagonal blocks (+LM) and rhs = negative gradient ----
+// 32 lanes per node: lane q < 21 owns upper-triangle entry q of the 6x6 block, lanes 21..26 the gradient. The ARAP
+// terms (ComputeBlockSums of dEi^T dEi / dEj^T dEj and J^T e, ArapHessianImpl.h / DeformableMeshToImageFitterImpl.h)
+// are gathered from the node's incident edges (CSR, ascending edge order; entry = 2 e + (node is the edge's target)).
+__global__ __launch_bounds__(256) void k_arrow_prepare(int N, float lm, double* __restrict__ acc, const int* __restrict__ inc_off,
+                                                       const int* __restrict__ inc_list, const float* __restrict__ edge_terms, float* __restrict__ diag,
+                                                       float* __restrict__ rhs, float* __restrict__ gradient_out, float* __restrict__ hessian_out) {
+	const int n = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 5);
+	const int q = static_cast<int>(threadIdx.x & 31);
+	if (n >= N) return;   // uniform per 32-lane node group
+	// the term this lane sums from a source incidence / a target incidence (-1: none)
+	const int q_src = q < 27 ? q : -1;
+	const int q_tgt = (q == 15 || q == 18 || q == 20) ? 27 : (q >= 24 && q < 27) ? 28 + (q - 24) : -1;
+	float arap = 0.f;
+	const int beg = inc_off[n], end = inc_off[n + 1];
+	for (int u0 = beg; u0 < end; u0 += 32) {
+		const int nu = end - u0 < 32 ? end - u0 : 32;
+		const int mine = q < nu ? inc_list[u0 + q] : 0;   // one incidence per lane, broadcast below
+		float v[32];
+#pragma unroll
+		for (int u = 0; u < 32; u++) {
+			const int code = __shfl(mine, u, 32);
+			const int col = (code & 1) ? q_tgt : q_src;
+			v[u] = (u < nu && col >= 0) ? edge_terms[static_cast<int64_t>(code >> 1) * EDGE_TERMS + col] : 0.f;
 		}
-	if (lm > 0.f)
-		for (int i = 0; i < 6; i++) d[7 * i] += lm;
-	for (int c = 0; c < 6; c++) {
-		const float g = (0.f - static_cast<float>(ad[21 + c])) - aa[21 + c];
-		rhs[6 * n + c] = g;
-		gradient_out[6 * n + c] = g;
+#pragma unroll
+		for (int u = 0; u < 32; u++)
+			if (u < nu) arap += v[u];
 	}
-	for (int k = 0; k < 27; k++) {
-		ad[k] = 0.0;
-		aa[k] = 0.f;
+	if (q >= 27) return;
+	int r0 = 0, c0 = 0;   // upper-triangle enumeration of entry q (q < 21)
+	{
+		int qq = q;
+		while (r0 < 6 && qq >= 6 - r0) {
+			qq -= 6 - r0;
+			r0++;
+		}
+		c0 = r0 + qq;
+	}
+	double* ad = acc + static_cast<int64_t>(n) * ACC_STRIDE;
+	const double hq = ad[q];
+	ad[q] = 0.0;
+	if (q < 21) {
+		const float hd = static_cast<float>(hq);
+		float v = arap + hd;
+		if (r0 == c0 && lm > 0.f) v += lm;
+		float* d = diag + static_cast<int64_t>(n) * 36;
+		d[6 * r0 + c0] = v;
+		d[6 * c0 + r0] = v;
+		if (hessian_out) {
+			hessian_out[static_cast<int64_t>(n) * 36 + 6 * r0 + c0] = hd;
+			hessian_out[static_cast<int64_t>(n) * 36 + 6 * c0 + r0] = hd;
+		}
+	} else {
+		const float g = (0.f - static_cast<float>(hq)) - arap;
+		rhs[6 * static_cast<int64_t>(n) + q - 21] = g;
+		gradient_out[6 * static_cast<int64_t>(n) + q - 21] = g;
 	}
 }
 
@@ -218,42 +240,137 @@ __global__ __launch_bounds__(64) void k_arrow_stem(int n0, const float* __restri
 }
 
 // ---- Schur update S_ab -= sum over stem nodes i adjacent to a and b of B_ia^T D_i^-1 B_ib (one wave per target) ----
-__global__ void k_stem_schur(int targets, int ld, const int* __restrict__ tgt_off, const int2* __restrict__ tgt_ab, const int2* __restrict__ pairs,
-                             const float* __restrict__ wing, const float* __restrict__ dinv_b, float* __restrict__ S) {
+// Lane (r, c) < 36 owns entry (r, c) of the 6x6 target block. The target's pair list is loaded once, one pair per lane,
+// and broadcast by shuffle, so the wing / D^-1 B loads of eight pairs are in flight together (no dependent index load
+// per pair). Pairs are summed in list order.
+__global__ __launch_bounds__(256) void k_stem_schur(int targets, int ld, const int* __restrict__ tgt_off, const int2* __restrict__ tgt_ab,
+                                                    const int2* __restrict__ pairs, const float* __restrict__ wing, const float* __restrict__ dinv_b,
+                                                    float* __restrict__ S) {
 	const int w = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
 	const int lane = static_cast<int>(threadIdx.x & 63);
-	if (w >= targets || lane >= 36) return;
-	const int r = lane / 6, c = lane % 6;
+	if (w >= targets) return;
+	const int r = lane < 36 ? lane / 6 : 0, c = lane < 36 ? lane % 6 : 0;
+	const int beg = tgt_off[w], end = tgt_off[w + 1];
 	float acc = 0.f;
-	for (int p = tgt_off[w]; p < tgt_off[w + 1]; p++) {
-		const int2 e = pairs[p];
-		const float* B1 = wing + static_cast<int64_t>(e.x) * 36;
-		const float* Y2 = dinv_b + static_cast<int64_t>(e.y) * 36;
-		float s = 0.f;
-		for (int k = 0; k < 6; k++) s += B1[6 * k + r] * Y2[6 * k + c];
-		acc += s;
+	for (int p0 = beg; p0 < end; p0 += 64) {
+		const int np = end - p0 < 64 ? end - p0 : 64;
+		const int2 mine = lane < np ? pairs[p0 + lane] : make_int2(0, 0);
+		for (int u0 = 0; u0 < np; u0 += 8) {
+			float b1[8][6], y2[8][6];
+#pragma unroll
+			for (int u = 0; u < 8; u++) {
+				const int e1 = __shfl(mine.x, u0 + u), e2 = __shfl(mine.y, u0 + u);
+				const bool live = u0 + u < np;
+				const float* B1 = wing + static_cast<int64_t>(live ? e1 : 0) * 36;
+				const float* Y2 = dinv_b + static_cast<int64_t>(live ? e2 : 0) * 36;
+#pragma unroll
+				for (int k = 0; k < 6; k++) {
+					b1[u][k] = live ? B1[6 * k + r] : 0.f;
+					y2[u][k] = live ? Y2[6 * k + c] : 0.f;
+				}
+			}
+#pragma unroll
+			for (int u = 0; u < 8; u++) {
+				if (u0 + u < np) {
+					float sum = 0.f;
+#pragma unroll
+					for (int k = 0; k < 6; k++) sum += b1[u][k] * y2[u][k];
+					acc += sum;
+				}
+			}
+		}
 	}
-	const int2 ab = tgt_ab[w];
-	S[static_cast<int64_t>(6 * ab.x + r) * ld + 6 * ab.y + c] -= acc;
+	if (lane < 36) {
+		const int2 ab = tgt_ab[w];
+		S[static_cast<int64_t>(6 * ab.x + r) * ld + 6 * ab.y + c] -= acc;
+	}
 }
 
-// ---- b_C -= sum over stem edges i->a of (D_i^-1 B_ia)^T b_i (one thread per corner entry) ----
-__global__ void k_stem_rhs(int m, const int* __restrict__ rhs_off, const int* __restrict__ rhs_edges, const int32_t* __restrict__ edges,
-                           const float* __restrict__ dinv_b, const float* __restrict__ rhs, float* __restrict__ cb) {
-	const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-	if (idx >= m) return;
-	const int a = idx / 6, c = idx % 6;
+// ---- fitter form of the Schur update: the ARAP wing blocks dEi^T dEj (dEj = [0 | b I]) are zero outside their last
+// three columns, so B_ia^T D_i^-1 B_ib is zero outside its lower-right 3x3 block and only those 9 entries change
+// (the others would subtract exact zeros). 7 pair slots x 9 entries per wave; slots reduced in order at the end.
+__global__ __launch_bounds__(256) void k_stem_schur_t3(int targets, int ld, const int* __restrict__ tgt_off, const int2* __restrict__ tgt_ab,
+                                                       const int2* __restrict__ pairs, const float* __restrict__ wing,
+                                                       const float* __restrict__ dinv_b, float* __restrict__ S) {
+	__shared__ float s_part[4][7][9];
+	const int w = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
+	const int lane = static_cast<int>(threadIdx.x & 63), wl = static_cast<int>(threadIdx.x >> 6);
+	if (w >= targets) return;
+	const int slot = lane < 63 ? lane / 9 : 6, ent = lane < 63 ? lane % 9 : 0;
+	const int r = 3 + ent / 3, c = 3 + ent % 3;
+	const int beg = tgt_off[w], end = tgt_off[w + 1];
 	float acc = 0.f;
-	for (int q = rhs_off[a]; q < rhs_off[a + 1]; q++) {
+	for (int p0 = beg; p0 < end; p0 += 14) {
+		float b1[2][6], y2[2][6];
+		bool live[2];
+#pragma unroll
+		for (int h = 0; h < 2; h++) {
+			const int p = p0 + 7 * h + slot;
+			live[h] = lane < 63 && p < end;
+			const int2 e = live[h] ? pairs[p] : make_int2(0, 0);
+			const float* B1 = wing + static_cast<int64_t>(e.x) * 36;
+			const float* Y2 = dinv_b + static_cast<int64_t>(e.y) * 36;
+#pragma unroll
+			for (int k = 0; k < 6; k++) {
+				b1[h][k] = live[h] ? B1[6 * k + r] : 0.f;
+				y2[h][k] = live[h] ? Y2[6 * k + c] : 0.f;
+			}
+		}
+#pragma unroll
+		for (int h = 0; h < 2; h++)
+			if (live[h]) {
+				float sum = 0.f;
+#pragma unroll
+				for (int k = 0; k < 6; k++) sum += b1[h][k] * y2[h][k];
+				acc += sum;
+			}
+	}
+	if (lane < 63) s_part[wl][slot][ent] = acc;
+	__builtin_amdgcn_wave_barrier();   // LDS is in order within the wave; keep the compiler from moving the reads up
+	if (lane < 9) {
+		float t = 0.f;
+#pragma unroll
+		for (int sl = 0; sl < 7; sl++) t += s_part[wl][sl][lane];
+		const int2 ab = tgt_ab[w];
+		S[static_cast<int64_t>(6 * ab.x + 3 + lane / 3) * ld + 6 * ab.y + 3 + lane % 3] -= t;
+	}
+}
+
+// ---- b_C -= sum over stem edges i->a of (D_i^-1 B_ia)^T b_i (one wave per corner node; lanes over its edges) ----
+__global__ __launch_bounds__(256) void k_stem_rhs(int nc, const int* __restrict__ rhs_off, const int* __restrict__ rhs_edges,
+                                                  const int32_t* __restrict__ edges, const float* __restrict__ dinv_b, const float* __restrict__ rhs,
+                                                  float* __restrict__ cb) {
+	const int a = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
+	const int lane = static_cast<int>(threadIdx.x & 63);
+	if (a >= nc) return;
+	float s[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+	for (int q = rhs_off[a] + lane; q < rhs_off[a + 1]; q += 64) {
 		const int e = rhs_edges[q];
 		const int i = edges[2 * e];
 		const float* Y = dinv_b + static_cast<int64_t>(e) * 36;
 		const float* g = rhs + 6 * static_cast<int64_t>(i);
-		float s = 0.f;
-		for (int k = 0; k < 6; k++) s += Y[6 * k + c] * g[k];
-		acc += s;
+		float gk[6];
+#pragma unroll
+		for (int k = 0; k < 6; k++) gk[k] = g[k];
+#pragma unroll
+		for (int c = 0; c < 6; c++) {
+			float t = 0.f;
+#pragma unroll
+			for (int k = 0; k < 6; k++) t += Y[6 * k + c] * gk[k];
+			s[c] += t;
+		}
 	}
-	cb[idx] -= acc;
+#pragma unroll
+	for (int c = 0; c < 6; c++) {
+#pragma unroll
+		for (int off = 32; off > 0; off >>= 1) s[c] += __shfl_xor(s[c], off);
+	}
+	if (lane < 6) {
+		float v = s[0];
+#pragma unroll
+		for (int c = 1; c < 6; c++) v = lane == c ? s[c] : v;
+		cb[6 * static_cast<int64_t>(a) + lane] -= v;
+	}
 }
 
 StemSchurLists build_stem_schur_lists(const int32_t* edges, int E, int n0, int N) {
@@ -310,8 +427,7 @@ StemSchurLists build_stem_schur_lists(const int32_t* edges, int E, int n0, int N
 //           panel row of the diagonal workgroup (lane 0): y_k = L_kk^-1 b_k.
 //   trailing (tiles k < J <= I): A_IJ -= L_I,k-1 L_J,k-1^T on the MFMA, and b_J -= L_J,k-1 y_k-1 by the diagonal tiles.
 // Every operand of launch k was finished by launch k - 1, so consecutive launches are the only synchronisation.
-// After the factorization k_chol_diag_inverse inverts every L_kk in parallel (once) and the block back substitution
-// L^T x = y runs one launch per block row (k_chol_back_step), each a pair of matrix-vector products.
+// The block back substitution L^T x = y then runs BACK_G block rows per launch (k_chol_back_group).
 constexpr int CT = 256;   // threads per workgroup of the corner kernels
 constexpr int CS4 = CORNER_NB + 4;   // LDS row stride of the staged tiles (16-B aligned rows for ds_read_b128)
 
@@ -541,66 +657,87 @@ __global__ __launch_bounds__(CT) void k_chol_step(float* __restrict__ A, int ld,
 	}
 }
 
-// L_kk^-1 for every diagonal block (one wave each): lane c solves L x = e_c by right-looking substitution with the
-// columns of L_kk broadcast from LDS (stored transposed so each column is contiguous)
-__global__ __launch_bounds__(64) void k_chol_diag_inverse(const float* __restrict__ A, int ld, float* __restrict__ linv) {
-	__shared__ float s_lt[CORNER_NB][CORNER_NB + 4];   // s_lt[c][r] = L[r][c]
-	const int lane = threadIdx.x, k = blockIdx.x;
-	const int64_t o = static_cast<int64_t>(k) * CORNER_NB;
-	for (int r = 0; r < CORNER_NB; r++) s_lt[lane][r] = A[(o + r) * ld + o + lane];
-	__syncthreads();
-	float z[CORNER_NB];
-#pragma unroll
-	for (int r = 0; r < CORNER_NB; r++) z[r] = r == lane ? 1.f : 0.f;
-#pragma unroll
-	for (int i = 0; i < CORNER_NB; i++) {
-		const float xi = z[i] / s_lt[i][i];
-		z[i] = xi;
-#pragma unroll
-		for (int r = i + 1; r < CORNER_NB; r++) z[r] -= s_lt[i][r] * xi;
-	}
-	float* Li = linv + static_cast<int64_t>(k) * CORNER_NB * CORNER_NB;   // Li[r][c] = (L_kk^-1)_rc
-#pragma unroll
-	for (int r = 0; r < CORNER_NB; r++) Li[r * CORNER_NB + lane] = z[r];
-}
+// ---- block back substitution L^T x = y, BACK_G block rows per launch (from the last block up) ----------------------
+// Launch for blocks k0, k0 - 1, .., kl (g = k0 - block): wave g holds L_{k0-g,k0-g} by columns in registers; as soon as
+// x_{k0-g2} is known every later wave subtracts L_{k0-g2,k0-g}^T x_{k0-g2} from its z (coupling tiles staged in LDS by
+// the whole workgroup), and wave g, once its z is complete, solves L^T x = z by column-oriented substitution (x_i broadcast by readlane; lane = column, so column i of L^T is the lanes'
+// register i). Every workgroup forms the group's x redundantly; workgroup i < kl then applies y_i -= sum L_ki^T x_k
+// (its tiles prefetched meanwhile) and the group's own workgroups store x.
+constexpr int BACK_G = 4;
 
-// back substitution L^T x = y in place, right-looking over block rows: launch k (from the last block) has
-// workgroup i < k form x_k = L_kk^-T y_k (each workgroup redundantly) and apply y_i -= L_ki^T x_k; workgroup k itself
-// stores x_k. The operands that do not depend on y (L_kk^-1 and the L_ki tile) are loaded before y_k.
-__global__ __launch_bounds__(CT) void k_chol_back_step(const float* __restrict__ A, int ld, int k, const float* __restrict__ linv,
-                                                       float* __restrict__ b) {
-	__shared__ float s_y[CORNER_NB], s_x[CORNER_NB];
+__global__ __launch_bounds__(CT) void k_chol_back_group(const float* __restrict__ A, int ld, int k0, int kl, float* __restrict__ b) {
+	__shared__ float s_cpl[BACK_G * (BACK_G - 1) / 2][CORNER_NB][CORNER_NB + 1];   // [g(g-1)/2 + g2][r][c] = L_{k0-g2,k0-g}[r][c]
+	__shared__ __attribute__((aligned(16))) float s_x[BACK_G][CORNER_NB];
 	__shared__ float s_part[4][CORNER_NB];
-	const int t = threadIdx.x, c = t % CORNER_NB, seg = t / CORNER_NB;
-	const int i = static_cast<int>(blockIdx.x);   // target block (i == k: store x_k)
-	const int64_t ck = static_cast<int64_t>(k) * CORNER_NB, ci = static_cast<int64_t>(i) * CORNER_NB;
-	const float* Li = linv + static_cast<int64_t>(k) * CORNER_NB * CORNER_NB;
-	float li[16], lk[16];
+	const int t = threadIdx.x, c = t % CORNER_NB, seg = t / CORNER_NB, wave = t >> 6, lane = t & 63;
+	const int i = static_cast<int>(blockIdx.x);   // target block (i >= kl: a block of the group, store its x)
+	const int64_t LD = ld, ci = static_cast<int64_t>(i) * CORNER_NB;
+	const int G = k0 - kl + 1;
+	float lk[BACK_G][16];
+	if (i < kl) {   // L_ki (rows of block k, columns of block i) for the target update
 #pragma unroll
-	for (int q = 0; q < 16; q++) li[q] = Li[(seg * 16 + q) * CORNER_NB + c];
-	if (i != k) {
+		for (int g = 0; g < BACK_G; g++)
+			if (g < G) {
+				const int64_t ck = static_cast<int64_t>(k0 - g) * CORNER_NB;
 #pragma unroll
-		for (int q = 0; q < 16; q++) lk[q] = A[(ck + seg * 16 + q) * ld + ci + c];
+				for (int q = 0; q < 16; q++) lk[g][q] = A[(ck + seg * 16 + q) * LD + ci + c];
+			}
 	}
-	if (t < CORNER_NB) s_y[t] = b[ck + t];
-	__syncthreads();
-	// x_k[c] = sum_q Linv[q][c] y_q
-	float acc = 0.f;
+	for (int g = 1; g < G; g++)
+		for (int g2 = 0; g2 < g; g2++) {
+			const int64_t rr = static_cast<int64_t>(k0 - g2) * CORNER_NB, cc = static_cast<int64_t>(k0 - g) * CORNER_NB;
+			float(*dst)[CORNER_NB + 1] = s_cpl[g * (g - 1) / 2 + g2];
 #pragma unroll
-	for (int q = 0; q < 16; q++) acc += li[q] * s_y[seg * 16 + q];
-	s_part[seg][c] = acc;
+			for (int q = 0; q < 16; q++) dst[seg * 16 + q][c] = A[(rr + seg * 16 + q) * LD + cc + c];
+		}
+	float col[CORNER_NB];   // wave g: col[r] = L_kk[r][lane], k = k0 - g
+	float inv_d = 1.f, z = 0.f;
+	if (wave < G) {
+		const int64_t ok = static_cast<int64_t>(k0 - wave) * CORNER_NB;
+#pragma unroll
+		for (int r = 0; r < CORNER_NB; r++) col[r] = A[(ok + r) * LD + ok + lane];
+		inv_d = 1.f / A[(ok + lane) * LD + ok + lane];
+		z = b[ok + lane];
+	}
+	for (int g = 0; g < G; g++) {
+		__syncthreads();   // x_{g-1} and the staged coupling tiles are visible
+		if (g > 0 && wave >= g && wave < G) {   // every later block applies the newest x at once (off the chain)
+			const float(*cp)[CORNER_NB + 1] = s_cpl[wave * (wave - 1) / 2 + g - 1];
+			const float4* xv = reinterpret_cast<const float4*>(s_x[g - 1]);
+			float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+			for (int r4 = 0; r4 < CORNER_NB / 4; r4++) {
+				const float4 x4 = xv[r4];
+				s0 += cp[4 * r4][lane] * x4.x;
+				s1 += cp[4 * r4 + 1][lane] * x4.y;
+				s0 += cp[4 * r4 + 2][lane] * x4.z;
+				s1 += cp[4 * r4 + 3][lane] * x4.w;
+			}
+			z -= s0 + s1;
+		}
+		if (wave == g) {
+			float x = 0.f;
+#pragma unroll
+			for (int r = CORNER_NB - 1; r >= 0; r--) {
+				const float xr = lane_bcast(z, r) * lane_bcast(inv_d, r);   // x_r = z_r / L_rr
+				x = lane == r ? xr : x;
+				z -= col[r] * xr;   // z_c -= L_rc x_r (only c < r matter)
+			}
+			s_x[g][lane] = x;
+		}
+	}
 	__syncthreads();
-	if (t < CORNER_NB) s_x[t] = (s_part[0][t] + s_part[1][t]) + (s_part[2][t] + s_part[3][t]);
-	__syncthreads();
-	if (i == k) {
-		if (t < CORNER_NB) b[ck + t] = s_x[t];
+	if (i >= kl) {
+		if (t < CORNER_NB) b[ci + t] = s_x[k0 - i][t];
 		return;
 	}
-	// y_i[c] -= sum_r L[k-block row r][i-block col c] x_k[r]
-	acc = 0.f;
+	float acc = 0.f;
 #pragma unroll
-	for (int q = 0; q < 16; q++) acc += lk[q] * s_x[seg * 16 + q];
-	__syncthreads();
+	for (int g = 0; g < BACK_G; g++)
+		if (g < G) {
+#pragma unroll
+			for (int q = 0; q < 16; q++) acc += lk[g][q] * s_x[g][seg * 16 + q];
+		}
 	s_part[seg][c] = acc;
 	__syncthreads();
 	if (t < CORNER_NB) b[ci + t] -= (s_part[0][t] + s_part[1][t]) + (s_part[2][t] + s_part[3][t]);
@@ -611,7 +748,7 @@ __global__ void k_corner_out(int m, const float* __restrict__ cb, float* __restr
 	if (i < m) x[i] = cb[i];
 }
 
-nnrt_status corner_cholesky_solve(float* A, int ld, float* linv, float* cb, int* error_flag, hipStream_t stream) {
+nnrt_status corner_cholesky_solve(float* A, int ld, float* cb, int* error_flag, hipStream_t stream) {
 	const int T = ld / CORNER_NB;
 	for (int k = 0; k < T; k++) {   // factor [S | b]: the forward substitution rides along as an augmented row
 		const int panel = T - k, below = T - 1 - k;
@@ -619,10 +756,9 @@ nnrt_status corner_cholesky_solve(float* A, int ld, float* linv, float* cb, int*
 		k_chol_step<<<panel + trailing, CT, 0, stream>>>(A, ld, k, T, cb, error_flag);
 		NNRT_LAUNCH_CHECK();
 	}
-	k_chol_diag_inverse<<<T, 64, 0, stream>>>(A, ld, linv);
-	NNRT_LAUNCH_CHECK();
-	for (int k = T - 1; k >= 0; k--) {
-		k_chol_back_step<<<k + 1, CT, 0, stream>>>(A, ld, k, linv, cb);
+	for (int k0 = T - 1; k0 >= 0; k0 -= BACK_G) {
+		const int kl = k0 - BACK_G + 1 > 0 ? k0 - BACK_G + 1 : 0;
+		k_chol_back_group<<<k0 + 1, CT, 0, stream>>>(A, ld, k0, kl, cb);
 		NNRT_LAUNCH_CHECK();
 	}
 	return NNRT_OK;
@@ -673,7 +809,8 @@ __global__ void k_arrow_update(int N, const float* __restrict__ x, float* __rest
 		for (int c = 0; c < 3; c++) ns[6 + 3 * r + c] = (R[3 * r] * dR[c] + R[3 * r + 1] * dR[3 + c]) + R[3 * r + 2] * dR[6 + c];
 }
 
-nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* edges, const float* wing, int* error_flag, hipStream_t stream) {
+nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* edges, const float* wing, int* error_flag, hipStream_t stream,
+                                 bool arap_wings) {
 	const int m = ws.m, ld = ws.ld;
 	if (m > 0) {
 		k_arrow_corner_init<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ld) * ld, 256)), 256, 0, stream>>>(ws.n0, m, ld, ws.diag,
@@ -689,15 +826,20 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 		                                                                           ws.dinv_b, error_flag);
 		NNRT_LAUNCH_CHECK();
 		if (m > 0 && ws.targets > 0) {
-			k_stem_schur<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ws.targets) * 64, 256)), 256, 0, stream>>>(
-			    ws.targets, ld, ws.tgt_off, ws.tgt_ab, ws.pairs, wing, ws.dinv_b, ws.schur);
+			if (arap_wings)
+				k_stem_schur_t3<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ws.targets) * 64, 256)), 256, 0, stream>>>(
+				    ws.targets, ld, ws.tgt_off, ws.tgt_ab, ws.pairs, wing, ws.dinv_b, ws.schur);
+			else
+				k_stem_schur<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ws.targets) * 64, 256)), 256, 0, stream>>>(
+				    ws.targets, ld, ws.tgt_off, ws.tgt_ab, ws.pairs, wing, ws.dinv_b, ws.schur);
 			NNRT_LAUNCH_CHECK();
-			k_stem_rhs<<<static_cast<unsigned>(ceil_div(m, 256)), 256, 0, stream>>>(m, ws.rhs_off, ws.rhs_edges, edges, ws.dinv_b, ws.rhs, ws.cb);
+			k_stem_rhs<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(m / 6) * 64, 256)), 256, 0, stream>>>(m / 6, ws.rhs_off, ws.rhs_edges,
+			                                                                                                         edges, ws.dinv_b, ws.rhs, ws.cb);
 			NNRT_LAUNCH_CHECK();
 		}
 	}
 	if (m > 0) {
-		nnrt_status st = corner_cholesky_solve(ws.schur, ld, ws.linv, ws.cb, error_flag, stream);
+		nnrt_status st = corner_cholesky_solve(ws.schur, ld, ws.cb, error_flag, stream);
 		if (st) return st;
 		k_corner_out<<<static_cast<unsigned>(ceil_div(m, 256)), 256, 0, stream>>>(m, ws.cb, ws.x + 6 * static_cast<int64_t>(ws.n0));
 		NNRT_LAUNCH_CHECK();
@@ -711,12 +853,12 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 }
 
 nnrt_status launch_arrowhead_iteration(const ArrowheadWorkspace& ws, const double* acc, float lm, const int32_t* edges, const float* wing,
-                                       float* node_state, float* arap_acc, float* updates_out, float* gradient_out, float* hessian_out,
+                                       float* node_state, const float* edge_jr, float* updates_out, float* gradient_out, float* hessian_out,
                                        int* error_flag, hipStream_t stream) {
-	k_arrow_prepare<<<static_cast<unsigned>(ceil_div(ws.N, 256)), 256, 0, stream>>>(ws.N, lm, const_cast<double*>(acc), arap_acc, ws.diag,
-	                                                                               ws.rhs, gradient_out, hessian_out);
+	k_arrow_prepare<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ws.N) * 32, 256)), 256, 0, stream>>>(
+	    ws.N, lm, const_cast<double*>(acc), ws.inc_off, ws.inc_list, edge_jr, ws.diag, ws.rhs, gradient_out, hessian_out);
 	NNRT_LAUNCH_CHECK();
-	nnrt_status st = arrowhead_solve_core(ws, edges, wing, error_flag, stream);
+	nnrt_status st = arrowhead_solve_core(ws, edges, wing, error_flag, stream, true);
 	if (st) return st;
 	k_arrow_update<<<static_cast<unsigned>(ceil_div(ws.N, 256)), 256, 0, stream>>>(ws.N, ws.x, node_state, updates_out);
 	NNRT_LAUNCH_CHECK();

@@ -349,12 +349,12 @@ struct nnrt_fitter {
 	DeviceBuffer<uint8_t> residual_mask;
 	DeviceBuffer<int32_t> pixel_face;
 	DeviceBuffer<double> acc;       // [N, ACC_STRIDE] data term (fp64)
-	DeviceBuffer<float> arap_acc;
+	DeviceBuffer<float> edge_jr;   // [E,8] ARAP edge Jacobian + residual
 	DeviceBuffer<float> updates, gradient, hessian;
 	DeviceBuffer<int> error_flag;
 	// ARAP / arrowhead
-	DeviceBuffer<float> wing, edge_residuals, a_diag, a_dinv, a_dinvb, a_schur, a_linv, a_cb, a_rhs, a_x;
-	DeviceBuffer<int> a_offsets, a_list, a_tgt_off, a_rhs_off, a_rhs_edges;
+	DeviceBuffer<float> wing, edge_residuals, a_diag, a_dinv, a_dinvb, a_schur, a_cb, a_rhs, a_x;
+	DeviceBuffer<int> a_offsets, a_list, a_tgt_off, a_rhs_off, a_rhs_edges, a_inc_off, a_inc_list;
 	DeviceBuffer<int2> a_tgt_ab, a_pairs;
 	ArrowheadWorkspace aw;
 	int n0 = 0;
@@ -467,14 +467,14 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 		aa.radii = wf->radii.ptr;
 		aa.node_weights = wf->node_weights.ptr;
 		aa.node_state = wf->state.ptr;
-		aa.acc = ft->arap_acc.ptr;
+		aa.edge_jr = ft->edge_jr.ptr;
 		aa.wing = ft->wing.ptr;
 		aa.edge_residuals = ft->edge_residuals.ptr;
 		aa.error_flag = ft->error_flag.ptr;
 		if ((st = launch_arap_edges(aa, s))) return st;
 		if ((st = mark(5))) return st;
 		const float lm = ft->p.preconditioning_dampening_factor;
-		if ((st = launch_arrowhead_iteration(ft->aw, ft->acc.ptr, lm, wf->edges.ptr, ft->wing.ptr, wf->state.ptr, ft->arap_acc.ptr,
+		if ((st = launch_arrowhead_iteration(ft->aw, ft->acc.ptr, lm, wf->edges.ptr, ft->wing.ptr, wf->state.ptr, ft->edge_jr.ptr,
 		                                     ft->updates.ptr, ft->gradient.ptr, ft->hessian.ptr, ft->error_flag.ptr, s)))
 			return st;
 	} else {
@@ -547,8 +547,8 @@ void nnrt_fitter_destroy(nnrt_fitter* ft) {
 	ft->acc.release();
 	ft->ref_points.release();
 	ft->records.release();
-	for (auto* b : {&ft->mesh_p, &ft->mesh_n, &ft->weights, &ft->residuals, &ft->arap_acc, &ft->updates, &ft->gradient,
-	                &ft->hessian, &ft->wing, &ft->edge_residuals, &ft->a_diag, &ft->a_dinv, &ft->a_dinvb, &ft->a_schur, &ft->a_linv, &ft->a_cb, &ft->a_rhs, &ft->a_x})
+	for (auto* b : {&ft->mesh_p, &ft->mesh_n, &ft->weights, &ft->residuals, &ft->edge_jr, &ft->updates, &ft->gradient,
+	                &ft->hessian, &ft->wing, &ft->edge_residuals, &ft->a_diag, &ft->a_dinv, &ft->a_dinvb, &ft->a_schur, &ft->a_cb, &ft->a_rhs, &ft->a_x})
 		b->release();
 	ft->faces4.release();
 	ft->anchors.release();
@@ -567,6 +567,8 @@ void nnrt_fitter_destroy(nnrt_fitter* ft) {
 	ft->a_rhs_edges.release();
 	ft->a_tgt_ab.release();
 	ft->a_pairs.release();
+	ft->a_inc_off.release();
+	ft->a_inc_list.release();
 	if (ft->ev_in) hipEventDestroy(ft->ev_in);
 	if (ft->ev_out) hipEventDestroy(ft->ev_out);
 
@@ -609,7 +611,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	    (st = ft->wpos.ensure(V)) || (st = ft->wnrm.ensure(V)) || (st = ft->jv.ensure(static_cast<size_t>(V) * K)) ||
 	    (st = ft->jn.ensure(static_cast<size_t>(V) * K)) || (st = ft->ref_points.ensure(P)) || (st = ft->records.ensure(4 * P)) || (st = ft->keys.ensure(P)) ||
 	    (st = ft->residuals.ensure(P)) || (st = ft->residual_mask.ensure(P)) || (st = ft->pixel_face.ensure(P)) ||
-	    (st = ft->acc.ensure(static_cast<size_t>(N) * ACC_STRIDE)) || (st = ft->arap_acc.ensure(static_cast<size_t>(N) * ACC_STRIDE)) ||
+	    (st = ft->acc.ensure(static_cast<size_t>(N) * ACC_STRIDE)) ||
 	    (st = ft->updates.ensure(static_cast<size_t>(N) * 6)) || (st = ft->gradient.ensure(static_cast<size_t>(N) * 6)) ||
 	    (st = ft->hessian.ensure(static_cast<size_t>(N) * 36)))
 		return st;
@@ -621,7 +623,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 		if ((st = ft->wing.ensure(static_cast<size_t>(E) * 36)) || (st = ft->edge_residuals.ensure(3 * static_cast<size_t>(E))) ||
 		    (st = ft->a_diag.ensure(static_cast<size_t>(N) * 36)) || (st = ft->a_dinv.ensure(static_cast<size_t>(n0) * 36)) ||
 		    (st = ft->a_dinvb.ensure(static_cast<size_t>(E) * 36)) || (st = ft->a_schur.ensure(static_cast<size_t>(ld) * ld)) ||
-		    (st = ft->a_linv.ensure(static_cast<size_t>(ld) * CORNER_NB)) || (st = ft->a_cb.ensure(static_cast<size_t>(ld))) ||
+		    (st = ft->edge_jr.ensure(static_cast<size_t>(E) * EDGE_TERMS)) || (st = ft->a_cb.ensure(static_cast<size_t>(ld))) ||
 		    (st = ft->a_rhs.ensure(6 * static_cast<size_t>(N))) || (st = ft->a_x.ensure(6 * static_cast<size_t>(N))) ||
 		    (st = ft->a_offsets.ensure(n0 + 1)) || (st = ft->a_list.ensure(E)))
 			return st;
@@ -639,6 +641,23 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 		}
 		NNRT_HIP(hipMemcpy(ft->a_offsets.ptr, counts.data(), sizeof(int) * (n0 + 1), hipMemcpyHostToDevice));
 		NNRT_HIP(hipMemcpy(ft->a_list.ptr, list.data(), sizeof(int) * E, hipMemcpyHostToDevice));
+		// CSR of edge incidences by node (source: 2 e, target: 2 e + 1), ascending e per node
+		std::vector<int> inc_off(static_cast<size_t>(N) + 1, 0), inc_list(2 * static_cast<size_t>(E));
+		for (int e = 0; e < E; e++) {
+			inc_off[static_cast<size_t>(wf->h.edges[2 * e]) + 1]++;
+			inc_off[static_cast<size_t>(wf->h.edges[2 * e + 1]) + 1]++;
+		}
+		for (int n = 0; n < N; n++) inc_off[static_cast<size_t>(n) + 1] += inc_off[static_cast<size_t>(n)];
+		{
+			std::vector<int> fill_inc(inc_off.begin(), inc_off.end() - 1);
+			for (int e = 0; e < E; e++) {
+				inc_list[static_cast<size_t>(fill_inc[static_cast<size_t>(wf->h.edges[2 * e])]++)] = 2 * e;
+				inc_list[static_cast<size_t>(fill_inc[static_cast<size_t>(wf->h.edges[2 * e + 1])]++)] = 2 * e + 1;
+			}
+		}
+		if ((st = upload(ft->a_inc_off, inc_off)) || (st = upload(ft->a_inc_list, inc_list))) return st;
+		ft->aw.inc_off = ft->a_inc_off.ptr;
+		ft->aw.inc_list = ft->a_inc_list.ptr;
 		const StemSchurLists sl = build_stem_schur_lists(wf->h.edges.data(), E, n0, N);
 		if ((st = upload(ft->a_tgt_off, sl.tgt_off)) || (st = upload(ft->a_tgt_ab, sl.tgt_ab)) || (st = upload(ft->a_pairs, sl.pairs)) ||
 		    (st = upload(ft->a_rhs_off, sl.rhs_off)) || (st = upload(ft->a_rhs_edges, sl.rhs_edges)))
@@ -654,7 +673,6 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 		ft->aw.E = E;
 		ft->aw.m = m;
 		ft->aw.ld = ld;
-		ft->aw.linv = ft->a_linv.ptr;
 		ft->aw.cb = ft->a_cb.ptr;
 		ft->aw.diag = ft->a_diag.ptr;
 		ft->aw.dinv = ft->a_dinv.ptr;
@@ -701,7 +719,6 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	NNRT_LAUNCH_CHECK();
 	NNRT_HIP(hipMemsetAsync(ft->keys.ptr, 0xff, sizeof(uint64_t) * P, s));
 	NNRT_HIP(hipMemsetAsync(ft->acc.ptr, 0, sizeof(double) * N * ACC_STRIDE, s));
-	NNRT_HIP(hipMemsetAsync(ft->arap_acc.ptr, 0, sizeof(float) * N * ACC_STRIDE, s));
 	NNRT_HIP(hipEventRecord(ft->ev_out, s));
 	NNRT_HIP(hipStreamWaitEvent(us, ft->ev_out, 0));
 	ft->prepared = true;
@@ -1010,7 +1027,6 @@ nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, cons
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.dinv), sizeof(float) * 36 * std::max(n0, 1), s));
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.dinv_b), sizeof(float) * 36 * std::max(E, 1), s));
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.schur), sizeof(float) * std::max<int64_t>(static_cast<int64_t>(ws.ld) * ws.ld, 1), s));
-	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.linv), sizeof(float) * std::max<int64_t>(static_cast<int64_t>(ws.ld) * CORNER_NB, 1), s));
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.cb), sizeof(float) * std::max(ws.ld, 1), s));
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.edge_offsets), sizeof(int) * (n0 + 1), s));
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.edge_list), sizeof(int) * std::max(E, 1), s));
@@ -1040,7 +1056,7 @@ nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, cons
 		NNRT_HIP(hipMemcpyAsync(&host_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
 		NNRT_HIP(hipStreamSynchronize(s));
 	}
-	for (void* p : {static_cast<void*>(ws.dinv), static_cast<void*>(ws.dinv_b), static_cast<void*>(ws.schur), static_cast<void*>(ws.linv),
+	for (void* p : {static_cast<void*>(ws.dinv), static_cast<void*>(ws.dinv_b), static_cast<void*>(ws.schur),
 	                static_cast<void*>(ws.cb), static_cast<void*>(ws.tgt_off), static_cast<void*>(ws.tgt_ab), static_cast<void*>(ws.pairs),
 	                static_cast<void*>(ws.rhs_off), static_cast<void*>(ws.rhs_edges), static_cast<void*>(ws.edge_offsets),
 	                static_cast<void*>(ws.edge_list), static_cast<void*>(flag)})

@@ -62,13 +62,14 @@ struct ArapArgs {
 	const float* radii;             // [layers]
 	const float* node_weights;      // [N] (variable coverage)
 	const float* node_state;        // [N,16]
-	float* acc;                     // [N, ACC_STRIDE]: ARAP diagonal JtJ and -(-J^T e) added (acc stores +J^T r)
+	float* edge_jr;                 // [E,EDGE_TERMS]: the edge's diagonal-block / gradient terms for its two nodes
 	float* wing;                    // [E,36]: dEi^T dEj
 	float* edge_residuals;          // [3E]
 	int* error_flag;
 };
 nnrt_status launch_arap_edges(const ArapArgs& args, hipStream_t stream);
 
+constexpr int EDGE_TERMS = 32;  // per ARAP edge: 21 + 6 source terms, 1 + 3 target terms, 1 pad
 constexpr int CORNER_NB = 64;   // dense-corner Cholesky block size (the corner is padded to a multiple with identity)
 inline int corner_ld(int m) { return (m + CORNER_NB - 1) / CORNER_NB * CORNER_NB; }
 
@@ -79,12 +80,13 @@ struct ArrowheadWorkspace {
 	float* dinv = nullptr;      // [n0,36]
 	float* dinv_b = nullptr;    // [E,36]
 	float* schur = nullptr;     // [ld,ld] Schur complement of the stem (lower triangle factored in place)
-	float* linv = nullptr;      // [ld/64, 64, 64] inverses of the corner's diagonal Cholesky blocks
 	float* cb = nullptr;        // [ld] corner right-hand side / solution (zero padded)
 	float* rhs = nullptr;       // [6N] negative gradient
 	float* x = nullptr;         // [6N]
 	int* edge_offsets = nullptr;// [n0+1] CSR of stem edges by source node (edges grouped by source)
 	int* edge_list = nullptr;   // [E]
+	int* inc_off = nullptr;     // [N+1] CSR of edge incidences by node (fitter only: k_arrow_prepare)
+	int* inc_list = nullptr;    // [2E] 2 e + (node is the edge's target), ascending e per node
 	// Schur update S -= B^T D^-1 B grouped by target block (lower block triangle), and b_C -= B^T D^-1 b_D by corner
 	// node: each target is written by one owner, no atomics (build_stem_schur_lists)
 	int targets = 0;
@@ -102,8 +104,10 @@ struct StemSchurLists {
 StemSchurLists build_stem_schur_lists(const int32_t* edges, int E, int n0, int N);
 // acc -> diagonal blocks (+lm) + rhs ; arrowhead solve ; update node state
 nnrt_status launch_arrowhead_iteration(const ArrowheadWorkspace& ws, const double* acc, float lm, const int32_t* edges, const float* wing,
-                                       float* node_state, float* acc_mut, float* updates_out, float* gradient_out, float* hessian_out,
+                                       float* node_state, const float* edge_jr, float* updates_out, float* gradient_out, float* hessian_out,
                                        int* error_flag, hipStream_t stream);
-nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* edges, const float* wing, int* error_flag, hipStream_t stream);
+// arap_wings: the wing blocks have the ARAP structure dEi^T [0 | b I] (zero outside their last three columns)
+nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* edges, const float* wing, int* error_flag, hipStream_t stream,
+                                 bool arap_wings = false);
 
 } // namespace nnrt
