@@ -6,7 +6,9 @@ Workload (BASELINE.json configs[1]): one 640x480 synthetic de
 triangles). The target depth is the mesh rendered under a smooth ground-truth motion; random-free, seed = rank.
 
 A step = restore the identity warp (R = I, t = 0) + one full GN iteration (warp, rasterize, residuals, Jacobians,
-JtJ / Jt r, LM block solve, Rodrigues update) replayed from a hipGraph. The reference's own block-diagonal GN diverges
+JtJ / Jt r, LM block solve, Rodrigues update); --graph-steps (default 10, C2's GN iterations per frame) steps are
+captured as one hipGraph and replayed as one launch, the way FitToImage replays its iteration loop (the timed step count
+is rounded up to a whole number of launches). The reference's own block-diagonal GN diverges
 on multi-node scenes after 2-3 iterations (SURVEY.md / DESIGN.md section "Divergence"), so every step starts from the
 same state: each timed iteration does the work of the first iteration of a frame, with nothing cached between steps.
 
@@ -131,6 +133,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default=DEFAULT_CONFIG, help="synthetic workload (dynamicfuion_python_amd.synthetic.CONFIGS)")
     ap.add_argument("--timed-steps", type=int, default=100, help="eager per-stage HIP-event timing steps (roofline)")
+    ap.add_argument("--graph-steps", type=int, default=10, help="steps per captured graph launch (C2: 10 GN iterations per frame)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU-baseline sample (loop-body seconds)")
     ap.add_argument("--cpu-threads", type=int, default=16, help="OpenMP threads for the CPU baseline (the box's CPU share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -261,14 +264,16 @@ def main(argv=None):
     s_ptr = NV.stream_ptr(stream)
     wf_h, ft_h = wf.handle, ft._h
 
-    def step():
-        st = lib.nnrt_warp_field_reset_motion(wf_h, s_ptr)
-        st |= lib.nnrt_fitter_iterate(ft_h, wf_h, 0, 1, s_ptr)
-        return st
+    # One launch = GRAPH_STEPS steps: a hipGraph of GRAPH_STEPS x (reset to the identity warp + one GN iteration), the
+    # way FitToImage replays its iteration loop (C2: 10 GN iterations per frame) as one captured graph.
+    per_launch = max(1, min(args.graph_steps, args.steps))
+
+    def step(n):
+        return lib.nnrt_fitter_iterate_from_identity(ft_h, wf_h, 0, n, s_ptr)
 
     # warmup (first call captures the iteration graph)
-    for _ in range(args.warmup):
-        if step():
+    for _ in range(max(1, args.warmup // per_launch)):
+        if step(per_launch):
             NV.check(1)
     torch.cuda.synchronize(dev)
     ft.check()
@@ -278,8 +283,10 @@ def main(argv=None):
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     bad = 0
-    for _ in range(args.steps):
-        bad |= step()
+    launches = -(-args.steps // per_launch)
+    args.steps = launches * per_launch   # whole graphs only: the timed step count is rounded up to a multiple
+    for _ in range(launches):
+        bad |= step(per_launch)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -367,7 +374,7 @@ def main(argv=None):
         "dtype": "f32",
         "data": "synthetic (smooth grid mesh + GT node motion rendered to depth; seed = rank)",
         "config": {"workload": workload, "config": args.config, "frame": [sc.H, sc.W], "nodes": Nn, "vertices": V, "triangles": F,
-                   "anchors": 4, "iteration_mode": "ALL", "lm_damping": 0.001, "hip_graph": True,
+                   "anchors": 4, "iteration_mode": "ALL", "lm_damping": 0.001, "hip_graph": True, "steps_per_graph": per_launch,
                    "parallelism": f"replicas{world}" if world > 1 else "single"},
         "setup_ms": round(setup_ms, 3),
         "stage_ms": {k: round(v, 5) for k, v in stages.items()},

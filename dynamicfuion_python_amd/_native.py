@@ -68,6 +68,7 @@ _SIGNATURES = {
     "nnrt_fitter_fit_to_point_cloud": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                                  c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
     "nnrt_fitter_iterate": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
+    "nnrt_fitter_iterate_from_identity": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "nnrt_fitter_iterate_timed": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     "nnrt_fitter_check": (c_int32, [c_void_p, c_void_p]),
     "nnrt_fitter_get_diagnostics": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -359,15 +359,19 @@ struct nnrt_fitter {
 	ArrowheadWorkspace aw;
 	int n0 = 0;
 	int last_mode = 0;
-	// graphs (one per iteration mode)
-	hipGraphExec_t graph[3] = {nullptr, nullptr, nullptr};
+	// graphs: one per iteration sequence (the modes of the `count` iterations of an iterate() call, and whether each
+	// restarts from the identity warp), captured once and replayed as ONE launch; the most recent few are kept
+	struct SeqGraph {
+		std::vector<int> modes;
+		int reset = 0;
+		hipGraphExec_t exec = nullptr;
+	};
+	std::vector<SeqGraph> graphs;
 
 	void drop_graphs() {
-		for (auto& g : graph)
-			if (g) {
-				hipGraphExecDestroy(g);
-				g = nullptr;
-			}
+		for (auto& g : graphs)
+			if (g.exec) hipGraphExecDestroy(g.exec);
+		graphs.clear();
 	}
 };
 
@@ -747,41 +751,85 @@ nnrt_status nnrt_fitter_prepare_point_cloud(nnrt_fitter* ft, nnrt_warp_field* wf
 	return prepare_frame(ft, wf, d_vertices, d_normals, V, d_faces, F, ref, H, W, h_K, h_E, stream);
 }
 
+namespace {
+constexpr int MAX_GRAPH_ITERATIONS = 64;   // iterations per captured sequence graph (longer runs replay several)
+constexpr size_t MAX_CACHED_GRAPHS = 4;
+
+nnrt_status iterate_impl(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_iteration, int32_t count, int reset, hipStream_t us) {
+	nnrt_status st;
+	if (!ft->p.use_hip_graph) {
+		for (int it = first_iteration; it < first_iteration + count; it++) {
+			const int mode = ft->p.iteration_modes[it % ft->p.iteration_mode_count];
+			ft->last_mode = mode;
+			if (reset) {
+				k_reset_motion<<<static_cast<unsigned>(ceil_div(wf->N, 256)), 256, 0, us>>>(wf->state.ptr, wf->N);
+				NNRT_LAUNCH_CHECK();
+			}
+			if ((st = enqueue_iteration(ft, wf, mode, us))) return st;
+		}
+		return NNRT_OK;
+	}
+	// Graphs are captured on the fitter's private stream (capture needs a non-legacy stream) and replayed on the
+	// caller's: a whole run of iterations is one launch.
+	for (int it0 = first_iteration; it0 < first_iteration + count; it0 += MAX_GRAPH_ITERATIONS) {
+		const int n = std::min(MAX_GRAPH_ITERATIONS, first_iteration + count - it0);
+		std::vector<int> modes(static_cast<size_t>(n));
+		for (int i = 0; i < n; i++) modes[static_cast<size_t>(i)] = ft->p.iteration_modes[(it0 + i) % ft->p.iteration_mode_count];
+		ft->last_mode = modes.back();
+		hipGraphExec_t exec = nullptr;
+		for (auto& g : ft->graphs)
+			if (g.reset == reset && g.modes == modes) exec = g.exec;
+		if (!exec) {
+			hipGraph_t g = nullptr;
+			NNRT_HIP(hipStreamBeginCapture(ft->work, hipStreamCaptureModeThreadLocal));
+			st = NNRT_OK;
+			for (int i = 0; i < n && !st; i++) {
+				if (reset) {
+					k_reset_motion<<<static_cast<unsigned>(ceil_div(wf->N, 256)), 256, 0, ft->work>>>(wf->state.ptr, wf->N);
+					if (hipGetLastError() != hipSuccess) st = NNRT_ERROR_HIP;
+				}
+				if (!st) st = enqueue_iteration(ft, wf, modes[static_cast<size_t>(i)], ft->work);
+			}
+			hipError_t ce = hipStreamEndCapture(ft->work, &g);
+			if (st) {
+				if (g) hipGraphDestroy(g);
+				if (st == NNRT_ERROR_HIP) set_error("kernel launch failed during graph capture");
+				return st;
+			}
+			NNRT_HIP(ce);
+			hipError_t ie = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+			hipGraphDestroy(g);
+			NNRT_HIP(ie);
+			if (ft->graphs.size() >= MAX_CACHED_GRAPHS) {
+				hipGraphExecDestroy(ft->graphs.front().exec);
+				ft->graphs.erase(ft->graphs.begin());
+			}
+			ft->graphs.push_back({modes, reset, exec});
+		}
+		NNRT_HIP(hipGraphLaunch(exec, us));
+	}
+	return NNRT_OK;
+}
+} // namespace
+
 nnrt_status nnrt_fitter_iterate(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_iteration, int32_t count, void* stream) {
-	NNRT_CHECK_ARG(ft && wf, "null pointer");
+	NNRT_CHECK_ARG(ft && wf && count >= 0, "invalid arguments");
 	if (!ft->prepared || ft->wf != wf) {
 		set_error("nnrt_fitter_prepare must be called with this warp field before nnrt_fitter_iterate");
 		return NNRT_ERROR_ARGUMENT;
 	}
 	DeviceGuard guard(ft->device);
-	// Iterations run on the caller's stream (no cross-stream handshake per call). Graphs are captured once per
-	// iteration mode on the fitter's private stream (capture needs a non-legacy stream) and replayed on the caller's.
-	hipStream_t us = static_cast<hipStream_t>(stream);
-	nnrt_status st;
-	for (int it = first_iteration; it < first_iteration + count; it++) {
-		const int mode = ft->p.iteration_modes[it % ft->p.iteration_mode_count];
-		ft->last_mode = mode;
-		if (ft->p.use_hip_graph) {
-			if (!ft->graph[mode]) {
-				hipGraph_t g = nullptr;
-				NNRT_HIP(hipStreamBeginCapture(ft->work, hipStreamCaptureModeThreadLocal));
-				st = enqueue_iteration(ft, wf, mode, ft->work);
-				hipError_t ce = hipStreamEndCapture(ft->work, &g);
-				if (st) {
-					if (g) hipGraphDestroy(g);
-					return st;
-				}
-				NNRT_HIP(ce);
-				hipError_t ie = hipGraphInstantiate(&ft->graph[mode], g, nullptr, nullptr, 0);
-				hipGraphDestroy(g);
-				NNRT_HIP(ie);
-			}
-			NNRT_HIP(hipGraphLaunch(ft->graph[mode], us));
-		} else {
-			if ((st = enqueue_iteration(ft, wf, mode, us))) return st;
-		}
+	return iterate_impl(ft, wf, first_iteration, count, 0, static_cast<hipStream_t>(stream));
+}
+
+nnrt_status nnrt_fitter_iterate_from_identity(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_iteration, int32_t count, void* stream) {
+	NNRT_CHECK_ARG(ft && wf && count >= 0, "invalid arguments");
+	if (!ft->prepared || ft->wf != wf) {
+		set_error("nnrt_fitter_prepare must be called with this warp field before nnrt_fitter_iterate_from_identity");
+		return NNRT_ERROR_ARGUMENT;
 	}
-	return NNRT_OK;
+	DeviceGuard guard(ft->device);
+	return iterate_impl(ft, wf, first_iteration, count, 1, static_cast<hipStream_t>(stream));
 }
 
 nnrt_status nnrt_fitter_iterate_timed(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_iteration, int32_t count, float* h_stage_ms,

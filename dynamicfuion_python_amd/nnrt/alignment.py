@@ -103,6 +103,12 @@ class DeformableMeshToImageFitter:
     def iterate(self, warp_field: HierarchicalGraphWarpField, first_iteration: int = 0, count: int = 1, stream=None):
         N.check(N.lib().nnrt_fitter_iterate(self._h, warp_field.handle, int(first_iteration), int(count), N.stream_ptr(stream)))
 
+    def iterate_from_identity(self, warp_field: HierarchicalGraphWarpField, first_iteration: int = 0, count: int = 1, stream=None):
+        """iterate() with the warp field's motion reset to the identity before every iteration (benchmark form: each
+        iteration is the first GN iteration of the prepared frame); graph-captured like iterate()."""
+        N.check(N.lib().nnrt_fitter_iterate_from_identity(self._h, warp_field.handle, int(first_iteration), int(count),
+                                                           N.stream_ptr(stream)))
+
     def iterate_timed(self, warp_field: HierarchicalGraphWarpField, first_iteration: int = 0, count: int = 1, stream=None) -> dict:
         """Eager iterations with HIP events between stages; returns average device ms per iteration per stage."""
         ms = np.zeros(len(TIMED_STAGES), np.float32)

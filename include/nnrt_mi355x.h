@@ -122,8 +122,14 @@ nnrt_status nnrt_fitter_fit_to_point_cloud(nnrt_fitter* fitter, nnrt_warp_field*
                                            const float* d_normals, int64_t vertex_count, const int64_t* d_faces, int64_t face_count,
                                            const float* d_points, const uint8_t* d_point_mask, int32_t height, int32_t width,
                                            const double* h_K, const double* h_E, void* stream);
-/* Iterations are enqueued on `stream` itself (graphs: captured once per iteration mode, replayed on `stream`). */
+/* Iterations are enqueued on `stream` itself. With use_hip_graph the `count` iterations (up to 64 per launch) are
+ * captured once as one graph per mode sequence and replayed on `stream` as a single launch. */
 nnrt_status nnrt_fitter_iterate(nnrt_fitter* fitter, nnrt_warp_field* warp_field, int32_t first_iteration, int32_t count, void* stream);
+/* Benchmark / diagnostic form of iterate(): every iteration first resets the warp field's motion to the identity
+ * (R = I, t = 0, as nnrt_warp_field_reset_motion), so each is the first GN iteration of the prepared frame. Same
+ * graph behaviour as iterate() (the resets are captured with the iterations). */
+nnrt_status nnrt_fitter_iterate_from_identity(nnrt_fitter* fitter, nnrt_warp_field* warp_field, int32_t first_iteration, int32_t count,
+                                              void* stream);
 /* iterate() without graphs, with HIP events between the stages of every iteration; h_stage_ms[NNRT_TIMED_STAGES]
  * receives the average per-iteration device time of: 0 warp (+warped Jacobians), 1 raster scatter, 2 pixel pass
  * (residuals + rasterized Jacobians, k_pixel_jacobians), 3 node pass (node Jacobians + JtJ / Jt r,

@@ -299,6 +299,31 @@ def test_hip_graph_matches_eager(nn, S, oracle_mod):
     assert rel_err(wf1.get_node_translations(), wf2.get_node_translations()) < 1e-4
 
 
+def test_sequence_graph_and_iterate_from_identity(nn, S, oracle_mod):
+    """A mixed-mode run of iterations captured as one graph matches eager launches, and iterate_from_identity(count)
+    leaves the state of ONE iteration from the identity warp (every iteration restarts from it)."""
+    A, G = nn.alignment, nn.geometry
+    sc = _scene(S, oracle_mod, "S1")
+    depth = scene_target(oracle_mod, sc)
+    modes = [A.IterationMode.TRANSLATION_ONLY, A.IterationMode.ROTATION_ONLY, A.IterationMode.ALL]
+    wf1, _, d1 = _gpu_fit(nn, sc, depth, 3, modes=modes, graph=True)
+    wf2, _, d2 = _gpu_fit(nn, sc, depth, 3, modes=modes, graph=False)
+    assert (d1["pixel_faces"] == d2["pixel_faces"]).mean() > 0.999
+    assert rel_err(wf1.get_node_translations(), wf2.get_node_translations()) < 1e-4
+    assert rel_err(wf1.get_node_rotations(), wf2.get_node_rotations()) < 1e-4
+    _, _, d_one = _gpu_fit(nn, sc, depth, 1, graph=False)
+    wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE,
+                                      sc.layer_count)
+    ft = A.DeformableMeshToImageFitter(1, [A.IterationMode.ALL], preconditioning_dampening_factor=0.001, use_hip_graph=True)
+    ft.prepare(wf, G.TriangleMesh(sc.points, sc.normals, sc.faces), depth, None, sc.K)
+    for count in (3, 5, 3):   # replays of cached graphs of different lengths
+        ft.iterate_from_identity(wf, 0, count)
+    ft.check()
+    dg = ft.diagnostics()
+    assert np.array_equal(dg["pixel_faces"], d_one["pixel_faces"])
+    assert rel_err(dg["updates"], d_one["updates"]) < 1e-6
+
+
 def test_fit_with_extrinsics_parity(nn, S, oracle_mod):
     sc = _scene(S, oracle_mod, "S1")
     depth = scene_target(oracle_mod, sc)
