@@ -7,10 +7,18 @@ namespace nnrt {
 // =====================================================================================================================
 // Anchors: brute-force K-NN in ascending node order with replace-the-current-maximum insertion
 // (cpp/core/kernel/KnnUtilities.h:64-117) + Gaussian weights (WarpUtilities.h:34-247, WarpAnchorComputationImpl.h:42-140).
-// One thread per point; node positions are staged through LDS in chunks shared by the workgroup.
+// One lane per point, one wave per workgroup. Nodes are loaded 64 at a time (one per lane, a batch ahead) and
+// broadcast by readlane (SGPR operands, no LDS); squared distances of a group of ANCHOR_UNROLL nodes are formed with packed f32
+// (the reference's (dx dx + dy dy) + dz dz, no contraction); only the group's nodes that some lane has below its
+// current maximum at the group's start run the insertion (maxd only decreases, so every other node would have been
+// skipped by the serial loop too), in node order, exactly as the serial loop.
 // =====================================================================================================================
-constexpr int ANCHOR_BLOCK = 256;
-constexpr int ANCHOR_CHUNK = 2048;
+constexpr int ANCHOR_BLOCK = 64;
+constexpr int ANCHOR_UNROLL = 8;
+
+__device__ inline float lane_read(float v, int src) {
+	return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
+}
 
 template <int K>
 __global__ __launch_bounds__(ANCHOR_BLOCK) void k_compute_anchors(const float* __restrict__ points, int64_t point_count,
@@ -18,7 +26,7 @@ __global__ __launch_bounds__(ANCHOR_BLOCK) void k_compute_anchors(const float* _
                                                                     float coverage_squared, const float* __restrict__ node_weights,
                                                                     int minimum_valid, int32_t* __restrict__ anchors,
                                                                     float* __restrict__ weights) {
-	__shared__ float s_nodes[ANCHOR_CHUNK * 3];
+	typedef float f2 __attribute__((ext_vector_type(2)));
 	const int64_t i = static_cast<int64_t>(blockIdx.x) * ANCHOR_BLOCK + threadIdx.x;
 	const bool active = i < point_count;
 	float px = 0.f, py = 0.f, pz = 0.f;
@@ -35,35 +43,72 @@ __global__ __launch_bounds__(ANCHOR_BLOCK) void k_compute_anchors(const float* _
 		d2[k] = INFINITY;
 	}
 	int max_at = 0;
-	float maxd = INFINITY;
-	for (int base = 0; base < node_count; base += ANCHOR_CHUNK) {
-		const int count = min(ANCHOR_CHUNK, node_count - base);
-		__syncthreads();
-		for (int j = threadIdx.x; j < count * 3; j += ANCHOR_BLOCK) s_nodes[j] = nodes[3 * static_cast<int64_t>(base) + j];
-		__syncthreads();
-		if (!active) continue;
-		for (int j = 0; j < count; j++) {
-			const float dx = s_nodes[3 * j] - px, dy = s_nodes[3 * j + 1] - py, dz = s_nodes[3 * j + 2] - pz;
-			const float sq = (dx * dx + dy * dy) + dz * dz;
-			if (sq < maxd) {
+	float maxd = active ? INFINITY : -INFINITY;   // inactive lanes never insert
+	auto insert = [&](float sq, int j) {
+		if (sq < maxd) {
 #pragma unroll
-				for (int k = 0; k < K; k++) {
-					if (k == max_at) {
-						d2[k] = sq;
-						idx[k] = base + j;
-					}
+			for (int k = 0; k < K; k++) {
+				if (k == max_at) {
+					d2[k] = sq;
+					idx[k] = j;
 				}
-				max_at = 0;
-				maxd = d2[0];
+			}
+			max_at = 0;
+			maxd = d2[0];
 #pragma unroll
-				for (int k = 1; k < K; k++) {
-					if (d2[k] > maxd) {
-						max_at = k;
-						maxd = d2[k];
-					}
+			for (int k = 1; k < K; k++) {
+				if (d2[k] > maxd) {
+					max_at = k;
+					maxd = d2[k];
 				}
 			}
 		}
+	};
+	const f2 PX = {px, px}, PY = {py, py}, PZ = {pz, pz};
+	// batches of 64 nodes: lane l loads node base + l (coalesced, one batch ahead); the batch's coordinates are then
+	// broadcast to the wave by readlane (SGPR operands)
+	const int full = node_count - node_count % 64;
+	float bx = 0.f, by = 0.f, bz = 0.f;
+	const int lane = static_cast<int>(threadIdx.x & 63);
+	if (full > 0) {
+		bx = nodes[3 * lane];
+		by = nodes[3 * lane + 1];
+		bz = nodes[3 * lane + 2];
+	}
+	for (int base = 0; base < full; base += 64) {
+		const float cx = bx, cy = by, cz = bz;
+		if (base + 64 < full) {
+			const int64_t j = base + 64 + lane;
+			bx = nodes[3 * j];
+			by = nodes[3 * j + 1];
+			bz = nodes[3 * j + 2];
+		}
+#pragma unroll
+		for (int g = 0; g < 64; g += ANCHOR_UNROLL) {
+			float sq[ANCHOR_UNROLL];
+#pragma unroll
+			for (int q = 0; q < ANCHOR_UNROLL; q += 2) {
+				const f2 dx = f2{lane_read(cx, g + q), lane_read(cx, g + q + 1)} - PX;
+				const f2 dy = f2{lane_read(cy, g + q), lane_read(cy, g + q + 1)} - PY;
+				const f2 dz = f2{lane_read(cz, g + q), lane_read(cz, g + q + 1)} - PZ;
+				const f2 s2 = (dx * dx + dy * dy) + dz * dz;
+				sq[q] = s2.x;
+				sq[q + 1] = s2.y;
+			}
+			// the group runs the (divergent, node-ordered) insertions only if some lane has one of its distances below its
+			// maximum at the group's start (maxd only decreases, so otherwise the serial loop would skip all of them)
+			float m = sq[0];
+#pragma unroll
+			for (int q = 1; q < ANCHOR_UNROLL; q++) m = fminf(m, sq[q]);
+			if (__any(m < maxd)) {
+#pragma unroll
+				for (int q = 0; q < ANCHOR_UNROLL; q++) insert(sq[q], base + g + q);
+			}
+		}
+	}
+	for (int j = full; j < node_count; j++) {
+		const float dx = nodes[3 * j] - px, dy = nodes[3 * j + 1] - py, dz = nodes[3 * j + 2] - pz;
+		insert((dx * dx + dy * dy) + dz * dz, j);
 	}
 	if (!active) return;
 	float w[K];

@@ -46,11 +46,11 @@ def _scene(S, O, name, seed=0):
 # ---------------------------------------------------------------------------------------------------------------------
 # stages
 # ---------------------------------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("name", ["S1", "C1"])
-def test_anchors_bit_exact(nn, S, oracle_mod, name):
+@pytest.mark.parametrize("name,k", [("S1", 4), ("C1", 4), ("C2", 4), ("C1", 1), ("C1", 3), ("C1", 8)])
+def test_anchors_bit_exact(nn, S, oracle_mod, name, k):
     sc = _scene(S, oracle_mod, name)
-    a_o, w_o = oracle_mod.compute_anchors(sc.points, sc.nodes, 4, sc.coverage)
-    a_g, w_g = nn.geometry.functional.compute_anchors_and_weights_euclidean_fixed_node_weight(sc.points, sc.nodes, 4, 0, sc.coverage)
+    a_o, w_o = oracle_mod.compute_anchors(sc.points, sc.nodes, k, sc.coverage)
+    a_g, w_g = nn.geometry.functional.compute_anchors_and_weights_euclidean_fixed_node_weight(sc.points, sc.nodes, k, 0, sc.coverage)
     assert np.array_equal(a_o, _np(a_g))
     assert np.array_equal(w_o, _np(w_g))
 
