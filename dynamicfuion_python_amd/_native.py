@@ -90,6 +90,32 @@ _SIGNATURES = {
     "nnrt_solve_block_diagonal_cholesky": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     "nnrt_solve_block_sparse_arrowhead_cholesky": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p,
                                                              c_void_p, c_void_p]),
+    # TSDF voxel block grid
+    "nnrt_voxel_grid_create": (c_int32, [c_float, c_int32, c_int64, c_int32, c_int32, c_int32, ctypes.POINTER(c_void_p)]),
+    "nnrt_voxel_grid_destroy": (None, [c_void_p]),
+    "nnrt_voxel_grid_get_info": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "nnrt_voxel_grid_activate": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "nnrt_voxel_grid_get_block_coordinates": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "nnrt_voxel_grid_unique_block_coordinates": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_float,
+                                                           c_float, c_float, c_void_p, c_void_p]),
+    "nnrt_voxel_grid_copy_result_coordinates": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "nnrt_voxel_grid_integrate": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32, c_int32,
+                                            c_void_p, c_void_p, c_void_p, c_float, c_float, c_float, c_void_p]),
+    "nnrt_voxel_grid_integrate_non_rigid": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p,
+                                                      c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float, c_float,
+                                                      c_void_p, c_void_p]),
+    "nnrt_voxel_grid_extract_voxel_values_and_coordinates": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "nnrt_voxel_grid_extract_voxel_values_at": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "nnrt_voxel_grid_copy_result_rows": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "nnrt_voxel_grid_warped_block_boxes": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "nnrt_boxes_intersecting_surface_mask": (c_int32, [c_void_p, c_int64, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_float, c_float,
+                                                       c_int32, c_float, c_void_p, c_void_p]),
+    "nnrt_voxel_grid_find_blocks_intersecting_truncation_region": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p,
+                                                                             c_void_p, c_float, c_float, c_float, c_void_p, c_void_p]),
+    "nnrt_voxel_grid_activate_sleeve_blocks": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "nnrt_voxel_grid_extract_triangle_mesh": (c_int32, [c_void_p, c_float, c_void_p, c_void_p, c_void_p]),
+    "nnrt_voxel_grid_copy_mesh": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "nnrt_marching_cubes_table": (c_int32, [c_void_p, c_void_p]),
 }
 
 

@@ -133,6 +133,22 @@ struct nnrt_warp_field {
 	int E() const { return static_cast<int>(h.edge_layers.size()); }
 };
 
+namespace nnrt {
+WarpFieldView warp_field_view(const void* handle) {
+	const nnrt_warp_field* wf = static_cast<const nnrt_warp_field*>(handle);
+	WarpFieldView v{};
+	v.N = wf->N;
+	v.anchor_count = wf->anchor_count;
+	v.minimum_valid = wf->minimum_valid;
+	v.fixed_coverage = wf->coverage_method == NNRT_MINIMAL_K_NEIGHBOR_NODE_DISTANCE ? 0 : 1;
+	v.coverage = wf->coverage;
+	v.state = wf->state.ptr;
+	v.node_weights = wf->node_weights.ptr;
+	v.device = wf->device;
+	return v;
+}
+} // namespace nnrt
+
 namespace {
 nnrt_status wf_download_state(const nnrt_warp_field* wf, std::vector<float>& host) {
 	host.resize(static_cast<size_t>(wf->N) * NODE_STRIDE);

@@ -43,6 +43,16 @@ nnrt_status launch_raster_scatter_mesh(const float4* wpos, const int4* faces4, i
 nnrt_status launch_raster_multi(const float* face_ndc, const uint8_t* mask, int64_t F, const RasterOptions& o, int faces_per_pixel,
                                 int64_t* out_face, float* out_depth, float* out_bary, float* out_dist, hipStream_t stream);
 
+// read-only device view of a warp field (capi.hip owns the handle; the TSDF kernels warp voxels with it)
+struct WarpFieldView {
+	int N, anchor_count, minimum_valid, fixed_coverage;
+	float coverage;                 // node coverage (fixed-coverage weights use coverage^2)
+	const float* state;             // [N,16] virtual order: g(3) t(3) R(9, row-major) pad
+	const float* node_weights;      // [N] squared coverage per node (variable coverage)
+	int device;
+};
+WarpFieldView warp_field_view(const void* warp_field_handle);
+
 // float transcendentals evaluated in double and rounded once: bit-identical with the host restatement (oracle/) and
 // within 1 ulp of the reference's expf/sinf/cosf
 __host__ __device__ inline float exp_cr(float x) { return static_cast<float>(exp(static_cast<double>(x))); }

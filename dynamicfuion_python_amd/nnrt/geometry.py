@@ -28,6 +28,7 @@ class TriangleMesh:
     vertex_normals: object
     triangle_indices: object
     triangle_normals: object = None
+    vertex_colors: object = None
 
     def on_device(self, device: torch.device):
         return (to_device(self.vertex_positions, torch.float32, device), to_device(self.vertex_normals, torch.float32, device),
@@ -293,3 +294,6 @@ functional = types.SimpleNamespace(
     unproject_raster_depth_without_filtering=unproject_raster_depth_without_filtering,
     compute_point_to_plane_distances=compute_point_to_plane_distances,
 )
+
+
+from .voxel_grid import NonRigidSurfaceVoxelBlockGrid, VoxelBlockGrid  # noqa: E402,F401

@@ -212,6 +212,87 @@ nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diagonal_b
                                                        int32_t diagonal_block_count, int32_t arrow_base_block_index,
                                                        const float* d_b, float* d_x, void* stream);
 
+/* ---- TSDF voxel block grid (NonRigidSurfaceVoxelBlockGrid, cpp/geometry/NonRigidSurfaceVoxelBlockGrid.h:30-65 over
+ * VoxelBlockGrid, cpp/geometry/VoxelBlockGrid.h; Python: nnrt.geometry.NonRigidSurfaceVoxelBlockGrid, pybind
+ * cpp/pybind/geometry/geometry.cpp:61-275). Attributes tsdf (float32), weight (float32 | uint16), color (none |
+ * float32 | uint16 | uint8, 3 channels). Block coordinates are int32 [n,3]; images are device arrays: depth [H,W]
+ * uint16 or float32, color [Hc,Wc,3] uint8 (uint16 depth) or float32 (float32 depth, [0,1]); intrinsics double[9],
+ * extrinsics double[16] (NULL: identity). Functions producing a variable-size result return its size and keep it in
+ * the grid until the matching copy_* call (the grid owns the workspace). ---- */
+typedef struct nnrt_voxel_grid nnrt_voxel_grid;
+#define NNRT_DTYPE_NONE -1
+#define NNRT_DTYPE_FLOAT32 0
+#define NNRT_DTYPE_UINT16 1
+#define NNRT_DTYPE_UINT8 2
+/* VoxelBlockGrid(attr_names, attr_dtypes, attr_channels, voxel_size, block_resolution, block_count, device)
+ * (VoxelBlockGrid.h:52-58); storage grows (x2) past block_count as Open3D's hash map does. */
+nnrt_status nnrt_voxel_grid_create(float voxel_size, int32_t block_resolution, int64_t block_count, int32_t weight_dtype,
+                                   int32_t color_dtype, int32_t device, nnrt_voxel_grid** out);
+void nnrt_voxel_grid_destroy(nnrt_voxel_grid* grid);
+nnrt_status nnrt_voxel_grid_get_info(const nnrt_voxel_grid* grid, int64_t* h_active_blocks, int64_t* h_capacity, float* h_voxel_size,
+                                     int32_t* h_block_resolution);
+/* hashmap().activate(block_coords) (Open3D HashMap::Activate); new blocks start at zero */
+nnrt_status nnrt_voxel_grid_activate(nnrt_voxel_grid* grid, const int32_t* d_block_coords, int64_t count, void* stream);
+/* active block coordinates [active,3] in buffer order (ExtractVoxelBlockCoordinates before its metric scaling,
+ * NonRigidSurfaceVoxelBlockGrid.cpp:186-191) */
+nnrt_status nnrt_voxel_grid_get_block_coordinates(const nnrt_voxel_grid* grid, int32_t* d_out, void* stream);
+/* GetUniqueBlockCoordinates(depth, intrinsic, extrinsic, depth_scale, depth_max, trunc_voxel_multiplier)
+ * (VoxelBlockGrid.cpp:237-270, Open3D DepthTouch); result -> nnrt_voxel_grid_copy_result_coordinates */
+nnrt_status nnrt_voxel_grid_unique_block_coordinates(nnrt_voxel_grid* grid, const void* d_depth, int32_t depth_dtype, int32_t height,
+                                                     int32_t width, const double* h_K, const double* h_E, float depth_scale,
+                                                     float depth_max, float trunc_voxel_multiplier, int64_t* h_count, void* stream);
+nnrt_status nnrt_voxel_grid_copy_result_coordinates(const nnrt_voxel_grid* grid, int32_t* d_out, void* stream);
+/* Integrate(block_coords, depth, color, depth_intrinsic, color_intrinsic, extrinsic, depth_scale, depth_max,
+ * trunc_voxel_multiplier) (VoxelBlockGrid.cpp:317-350, Open3D voxel_grid::Integrate); d_color may be NULL */
+nnrt_status nnrt_voxel_grid_integrate(nnrt_voxel_grid* grid, const int32_t* d_block_coords, int64_t count, const void* d_depth,
+                                      int32_t depth_dtype, int32_t height, int32_t width, const void* d_color, int32_t color_height,
+                                      int32_t color_width, const double* h_depth_K, const double* h_color_K, const double* h_E,
+                                      float depth_scale, float depth_max, float trunc_voxel_multiplier, void* stream);
+/* IntegrateNonRigid(block_coords, warp_field, depth, color, depth_normals, depth_intrinsics, color_intrinsics,
+ * extrinsics, depth_scale, depth_max, truncation_voxel_multiplier) -> cos_voxel_ray_to_normal [H,W]
+ * (NonRigidSurfaceVoxelBlockGrid.cpp:33-66, NonRigidSurfaceVoxelBlockGridImpl.h:52-229); d_depth_normals [H,W,3] */
+nnrt_status nnrt_voxel_grid_integrate_non_rigid(nnrt_voxel_grid* grid, const int32_t* d_block_coords, int64_t count,
+                                                const nnrt_warp_field* warp_field, const void* d_depth, int32_t depth_dtype,
+                                                int32_t height, int32_t width, const void* d_color, int32_t color_height,
+                                                int32_t color_width, const float* d_depth_normals, const double* h_depth_K,
+                                                const double* h_color_K, const double* h_E, float depth_scale, float depth_max,
+                                                float trunc_voxel_multiplier, float* d_cos_out, void* stream);
+/* ExtractVoxelValuesAndCoordinates (NonRigidSurfaceVoxelBlockGrid.cpp:168-184): d_out [active * res^3, C], rows
+ * (x, y, z, tsdf, weight[, r, g, b]), C = 5 or 8 (h_channels) */
+nnrt_status nnrt_voxel_grid_extract_voxel_values_and_coordinates(const nnrt_voxel_grid* grid, float* d_out, int32_t* h_channels,
+                                                                 void* stream);
+/* ExtractVoxelValuesAt(query_voxel_coordinates) (NonRigidSurfaceVoxelBlockGrid.cpp:193-224): rows of the queries whose
+ * block is active -> nnrt_voxel_grid_copy_result_rows */
+nnrt_status nnrt_voxel_grid_extract_voxel_values_at(nnrt_voxel_grid* grid, const int32_t* d_query, int64_t count, int64_t* h_rows,
+                                                    int32_t* h_channels, void* stream);
+nnrt_status nnrt_voxel_grid_copy_result_rows(const nnrt_voxel_grid* grid, float* d_out, void* stream);
+/* GetBoundingBoxesOfWarpedBlocks(block_keys, warp_field, extrinsics) (NonRigidSurfaceVoxelBlockGrid.cpp:113-124):
+ * d_boxes [n,6] (min xyz, max xyz) */
+nnrt_status nnrt_voxel_grid_warped_block_boxes(const nnrt_voxel_grid* grid, const int32_t* d_block_keys, int64_t count,
+                                               const nnrt_warp_field* warp_field, const double* h_E, float* d_boxes, void* stream);
+/* GetAxisAlignedBoxesInterceptingSurfaceMask (NonRigidSurfaceVoxelBlockGridImpl.h:359-437): d_mask [n] uint8 */
+nnrt_status nnrt_boxes_intersecting_surface_mask(const float* d_boxes, int64_t count, const void* d_depth, int32_t depth_dtype,
+                                                 int32_t height, int32_t width, const double* h_K, float depth_scale, float depth_max,
+                                                 int32_t stride, float truncation_distance, uint8_t* d_mask, void* stream);
+/* FindBlocksIntersectingTruncationRegion(depth, warp_field, intrinsics, extrinsics, depth_scale, depth_max,
+ * truncation_voxel_multiplier) (NonRigidSurfaceVoxelBlockGrid.cpp:141-166) -> nnrt_voxel_grid_copy_result_coordinates */
+nnrt_status nnrt_voxel_grid_find_blocks_intersecting_truncation_region(nnrt_voxel_grid* grid, const void* d_depth, int32_t depth_dtype,
+                                                                       int32_t height, int32_t width, const nnrt_warp_field* warp_field,
+                                                                       const double* h_K, const double* h_E, float depth_scale,
+                                                                       float depth_max, float trunc_voxel_multiplier, int64_t* h_count,
+                                                                       void* stream);
+/* ActivateSleeveBlocks() (NonRigidSurfaceVoxelBlockGrid.cpp:98-109): returns the inactive-neighbour count */
+nnrt_status nnrt_voxel_grid_activate_sleeve_blocks(nnrt_voxel_grid* grid, int64_t* h_count, void* stream);
+/* ExtractTriangleMesh(weight_threshold, estimated_vertex_number) (VoxelBlockGrid.cpp:461-497, Open3D marching cubes)
+ * -> counts; then nnrt_voxel_grid_copy_mesh: vertices [V,3], normals [V,3], colors [V,3] in [0,1] (may be NULL),
+ * triangles int64 [T,3] */
+nnrt_status nnrt_voxel_grid_extract_triangle_mesh(nnrt_voxel_grid* grid, float weight_threshold, int64_t* h_vertex_count,
+                                                  int64_t* h_triangle_count, void* stream);
+nnrt_status nnrt_voxel_grid_copy_mesh(const nnrt_voxel_grid* grid, float* d_vertices, float* d_normals, float* d_colors,
+                                      int64_t* d_triangles, void* stream);
+/* the generated marching-cubes tables (host): tri [256][31] int8 edge triples (-1 terminated), edge mask [256] */
+nnrt_status nnrt_marching_cubes_table(int8_t* h_tri, uint16_t* h_edge_mask);
+
 #ifdef __cplusplus
 }
 #endif

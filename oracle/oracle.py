@@ -19,8 +19,8 @@ MODE = {"ALL": 0, "TRANSLATION_ONLY": 1, "ROTATION_ONLY": 2}
 
 
 def build(force: bool = False) -> str:
-    src = os.path.join(_HERE, "nnrt_oracle.cpp")
-    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("nnrt_oracle.cpp", "tsdf_oracle.cpp")]
+    if force or not os.path.exists(_LIB_PATH) or any(os.path.getmtime(_LIB_PATH) < os.path.getmtime(f) for f in srcs):
         subprocess.check_call(["make", "-s", "-C", _HERE, "libnnrt_oracle.so"])
     return _LIB_PATH
 
@@ -455,3 +455,136 @@ def fit(*, nodes, rotations, translations, mesh_points, mesh_normals, faces, ref
     _check(rc)
     diag["residual_mask"] = diag["residual_mask"].astype(bool)
     return R, t, diag
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# TSDF voxel block grid restatement (tsdf_oracle.cpp)
+# ---------------------------------------------------------------------------------------------------------------------
+DT = {"none": -1, "float32": 0, "uint16": 1, "uint8": 2}
+
+
+def _depth_arg(depth):
+    d = np.ascontiguousarray(depth)
+    if d.dtype == np.uint16:
+        return d, 1
+    return np.ascontiguousarray(d, dtype=np.float32), 0
+
+
+class OracleGrid:
+    """CPU restatement of NonRigidSurfaceVoxelBlockGrid (test infrastructure only)."""
+
+    def __init__(self, voxel_size, block_resolution, weight_dtype="float32", color_dtype="none"):
+        L = lib()
+        L.orc_grid_create.restype = ctypes.c_void_p
+        L.orc_grid_create.argtypes = [ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        for name in ("orc_grid_block_count", "orc_grid_touch", "orc_grid_values_at", "orc_grid_inactive_neighbors"):
+            getattr(L, name).restype = ctypes.c_int64
+        self.h = ctypes.c_void_p(L.orc_grid_create(float(voxel_size), int(block_resolution), DT[weight_dtype], DT[color_dtype]))
+        self.res = int(block_resolution)
+        self.voxel = float(voxel_size)
+        self.color = color_dtype != "none"
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_grid_destroy(self.h)
+
+    def block_count(self):
+        return lib().orc_grid_block_count(self.h)
+
+    def block_coords(self):
+        out = np.zeros((self.block_count(), 3), np.int32)
+        lib().orc_grid_block_coords(self.h, _p(out))
+        return out
+
+    def activate(self, coords):
+        c = _i32(coords).reshape(-1, 3)
+        lib().orc_grid_activate(self.h, _p(c), ctypes.c_int64(len(c)))
+
+    def touch(self, depth, K, E, scale, dmax, trunc_mult):
+        d, dt = _depth_arg(depth)
+        cap = (d.shape[0] // 4) * (d.shape[1] // 4) * 4 + 1
+        out = np.zeros((cap, 3), np.int32)
+        n = lib().orc_grid_touch(self.h, _p(d), dt, d.shape[0], d.shape[1], _p(_f64(K)), _p(None if E is None else _f64(E)),
+                                 ctypes.c_float(scale), ctypes.c_float(dmax), ctypes.c_float(trunc_mult), _p(out), ctypes.c_int64(cap))
+        return out[:n]
+
+    def integrate(self, coords, depth, color, Kd, Kc, E, scale, dmax, trunc_mult):
+        c = _i32(coords).reshape(-1, 3)
+        d, dt = _depth_arg(depth)
+        col = None if color is None else np.ascontiguousarray(color, dtype=np.uint8 if dt == 1 else np.float32)
+        Hc, Wc = (0, 0) if col is None else col.shape[:2]
+        lib().orc_grid_integrate(self.h, _p(c), ctypes.c_int64(len(c)), _p(d), dt, d.shape[0], d.shape[1], _p(col), Hc, Wc, _p(_f64(Kd)),
+                                 _p(_f64(Kc)), _p(None if E is None else _f64(E)), ctypes.c_float(scale), ctypes.c_float(dmax),
+                                 ctypes.c_float(trunc_mult))
+
+    def integrate_non_rigid(self, coords, nodes, R, t, coverage, K, min_valid, depth, color, normals, Kd, Kc, E, scale, dmax, trunc_mult,
+                            node_coverage_sq=None, apply_oblique_test=True):
+        c = _i32(coords).reshape(-1, 3)
+        d, dt = _depth_arg(depth)
+        col = None if color is None else np.ascontiguousarray(color, dtype=np.uint8 if dt == 1 else np.float32)
+        Hc, Wc = (0, 0) if col is None else col.shape[:2]
+        cos = np.zeros(d.shape[:2], np.float32)
+        nodes, R, t, nrm = _f32(nodes), _f32(R), _f32(t), _f32(normals)
+        c2 = None if node_coverage_sq is None else _f32(node_coverage_sq)
+        lib().orc_grid_integrate_non_rigid(self.h, _p(c), ctypes.c_int64(len(c)), _p(nodes), _p(R), _p(t), _p(c2), len(nodes),
+                                           ctypes.c_float(coverage), int(K), int(min_valid), _p(d), dt, d.shape[0], d.shape[1], _p(col), Hc,
+                                           Wc, _p(nrm), _p(_f64(Kd)), _p(_f64(Kc)), _p(None if E is None else _f64(E)), ctypes.c_float(scale),
+                                           ctypes.c_float(dmax), ctypes.c_float(trunc_mult), _p(cos), int(bool(apply_oblique_test)))
+        return cos
+
+    def channels(self):
+        return 8 if self.color else 5
+
+    def values_at(self, query):
+        q = _i32(query).reshape(-1, 3)
+        out = np.zeros((len(q), self.channels()), np.float32)
+        n = lib().orc_grid_values_at(self.h, _p(q), ctypes.c_int64(len(q)), _p(out))
+        return out[:n]
+
+    def values_all(self):
+        out = np.zeros((self.block_count() * self.res ** 3, self.channels()), np.float32)
+        lib().orc_grid_values_all(self.h, _p(out))
+        return out
+
+    def inactive_neighbors(self):
+        cap = 27 * self.block_count() + 1
+        out = np.zeros((cap, 3), np.int32)
+        n = lib().orc_grid_inactive_neighbors(self.h, _p(out), ctypes.c_int64(cap))
+        return out[:n]
+
+    def mesh(self, weight_threshold):
+        nv, nt = ctypes.c_int64(), ctypes.c_int64()
+        z = np.zeros((1, 3), np.float32)
+        lib().orc_grid_mesh(self.h, ctypes.c_float(weight_threshold), _p(z), _p(z), _p(z), _p(np.zeros((1, 3), np.int64)), ctypes.c_int64(0),
+                            ctypes.c_int64(0), ctypes.byref(nv), ctypes.byref(nt))
+        V = np.zeros((max(nv.value, 1), 3), np.float32)
+        Nn = np.zeros_like(V)
+        C = np.zeros_like(V)
+        T = np.zeros((max(nt.value, 1), 3), np.int64)
+        lib().orc_grid_mesh(self.h, ctypes.c_float(weight_threshold), _p(V), _p(Nn), _p(C), _p(T), ctypes.c_int64(nv.value),
+                            ctypes.c_int64(nt.value), ctypes.byref(nv), ctypes.byref(nt))
+        return V[:nv.value], Nn[:nv.value], C[:nv.value], T[:nt.value]
+
+    def find_blocks_intersecting_truncation_region(self, depth, nodes, R, t, coverage, K, min_valid, Kd, E, scale, dmax, trunc_mult):
+        cand = self.inactive_neighbors()
+        boxes = warped_block_boxes(cand, self.res * self.voxel, nodes, R, t, coverage, K, min_valid, E)
+        mask = boxes_mask(boxes, depth, Kd, scale, dmax, 4, self.voxel * trunc_mult)
+        return cand[mask.astype(bool)]
+
+
+def warped_block_boxes(keys, side, nodes, R, t, coverage, K, min_valid, E):
+    k = _i32(keys).reshape(-1, 3)
+    nodes, R, t = _f32(nodes), _f32(R), _f32(t)
+    out = np.zeros((len(k), 6), np.float32)
+    lib().orc_warped_block_boxes(_p(k), ctypes.c_int64(len(k)), ctypes.c_float(side), _p(nodes), _p(R), _p(t), len(nodes),
+                                 ctypes.c_float(coverage), int(K), int(min_valid), _p(None if E is None else _f64(E)), _p(out))
+    return out
+
+
+def boxes_mask(boxes, depth, K, scale, dmax, stride, trunc):
+    b = _f32(boxes).reshape(-1, 6)
+    d, dt = _depth_arg(depth)
+    out = np.zeros(len(b), np.uint8)
+    lib().orc_boxes_mask(_p(b), ctypes.c_int64(len(b)), _p(d), dt, d.shape[0], d.shape[1], _p(_f64(K)), ctypes.c_float(scale),
+                         ctypes.c_float(dmax), int(stride), ctypes.c_float(trunc), _p(out))
+    return out
