@@ -463,7 +463,7 @@ constexpr int NR_BLOCK = 256;
 constexpr int NR_CAND = 2048;
 __global__ __launch_bounds__(NR_BLOCK) void k_integrate_non_rigid(GridView g, int64_t nb, WarpFieldView wf, ImageView im, const float* __restrict__ normals,
                                                                   Xform depth_x, Xform color_x, float sdf_trunc, float color_multiplier,
-                                                                  float range, float* __restrict__ cos_out) {
+                                                                  float range, uint64_t* __restrict__ cos_key) {
 	__shared__ int s_cand[NR_CAND];
 	__shared__ int s_count;
 	__shared__ int s_wave_counts[NR_BLOCK / 64];
@@ -565,9 +565,12 @@ __global__ __launch_bounds__(NR_BLOCK) void k_integrate_non_rigid(GridView g, in
 		}
 		const int64_t pix = static_cast<int64_t>(vr) * im.W + ui;
 		const float cosine = (vx * normals[3 * pix] + vy * normals[3 * pix + 1]) + vz * normals[3 * pix + 2];
-		cos_out[pix] = cosine;
-		if (psdf <= -sdf_trunc || cosine > 0.5f) continue;
 		const int64_t lin = static_cast<int64_t>(b) * g.res3 + vi;
+		// the reference's plain store races between voxels that project to one pixel; here the voxel with the highest
+		// linear index wins (the serial loop's last writer)
+		atomicMax(reinterpret_cast<unsigned long long*>(cos_key + pix),
+		          (static_cast<unsigned long long>(lin + 1) << 32) | __builtin_bit_cast(uint32_t, cosine));
+		if (psdf <= -sdf_trunc || cosine > 0.5f) continue;
 		const float tsdf_n = (psdf < sdf_trunc ? psdf : sdf_trunc) / sdf_trunc;
 		const float weight = read_store(g.weight, g.weight_type, lin);
 		const float inv_wsum = 1.0f / (weight + 1);
@@ -586,6 +589,13 @@ __global__ __launch_bounds__(NR_BLOCK) void k_integrate_non_rigid(GridView g, in
 			}
 		}
 	}
+}
+
+__global__ void k_cos_resolve(const uint64_t* __restrict__ key, int64_t n, float* __restrict__ cos_out) {
+	const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	const uint64_t k = key[i];
+	cos_out[i] = k ? __builtin_bit_cast(float, static_cast<uint32_t>(k & 0xffffffffu)) : 0.f;
 }
 
 // ---------------------------------------------------------------------------------------------------------------------
@@ -1400,8 +1410,11 @@ nnrt_status nnrt_voxel_grid_integrate_non_rigid(nnrt_voxel_grid* vg, const int32
 	if ((st = activate_coords(vg, d_block_coords, count, s))) return st;
 	const WarpFieldView wv = warp_field_view(wf);
 	NNRT_CHECK_ARG(wv.anchor_count >= 1 && wv.anchor_count <= TSDF_MAX_ANCHORS, "anchor_count must be in [1, 8]");
-	NNRT_HIP(hipMemsetAsync(d_cos_out, 0, sizeof(float) * static_cast<size_t>(height) * width, s));   // Tensor::Zeros (:72)
+	const int64_t P = static_cast<int64_t>(height) * width;
+	NNRT_HIP(hipMemsetAsync(d_cos_out, 0, sizeof(float) * P, s));   // Tensor::Zeros (:72)
 	if (vg->active == 0) return NNRT_OK;
+	if ((st = vg->s_packed.ensure(P))) return st;
+	NNRT_HIP(hipMemsetAsync(vg->s_packed.ptr, 0, sizeof(uint64_t) * P, s));
 	float range = 2.f * wv.coverage;   // nodes farther than 2 c are never valid anchors
 	if (!wv.fixed_coverage) {
 		std::vector<float> w(static_cast<size_t>(wv.N));
@@ -1413,7 +1426,8 @@ nnrt_status nnrt_voxel_grid_integrate_non_rigid(nnrt_voxel_grid* vg, const int32
 	const ImageView im = make_image(d_depth, depth_dtype, height, width, d_color, color_height, color_width, depth_scale, depth_max);
 	k_integrate_non_rigid<<<static_cast<unsigned>(vg->active), NR_BLOCK, 0, s>>>(
 	    vg->view(), vg->active, wv, im, d_depth_normals, make_xform(h_depth_K, h_E), make_xform(h_color_K ? h_color_K : h_depth_K, nullptr),
-	    vg->voxel_size * trunc_voxel_multiplier, color_multiplier(depth_dtype), range, d_cos_out);
+	    vg->voxel_size * trunc_voxel_multiplier, color_multiplier(depth_dtype), range, vg->s_packed.ptr);
+	k_cos_resolve<<<grid_of(P), 256, 0, s>>>(vg->s_packed.ptr, P, d_cos_out);
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;
 }

@@ -426,7 +426,7 @@ ORC_API void orc_grid_integrate_non_rigid(void* h, const int32_t* coords, int64_
 			}
 			const int64_t pix = static_cast<int64_t>(vr) * W + ui;
 			const float cosine = (vd[0] * normals[3 * pix] + vd[1] * normals[3 * pix + 1]) + vd[2] * normals[3 * pix + 2];
-			cos_out[pix] = cosine;
+			cos_out[pix] = cosine;   // racy in the reference; the serial last writer (highest voxel index) here and on the GPU
 			if (psdf <= -trunc || (apply_oblique_test && cosine > 0.5f)) continue;
 			const int64_t lin = static_cast<int64_t>(b) * g->res3 + vi;
 			const float tn = (psdf < trunc ? psdf : trunc) / trunc;

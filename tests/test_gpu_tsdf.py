@@ -41,7 +41,8 @@ def test_boxes_and_mask_kats(nn):
     wf = _wf(G, L.VBG_BOX_NODES, R, np.tile(L.VBG_BOX_TRANSLATION, (4, 1)), L.VBG_BOX_COVERAGE, threshold=False, min_valid=0)
     boxes = _np(grid.get_bounding_boxes_of_warped_blocks(L.VBG_BOX_KEYS, wf, np.eye(4)))
     assert np.allclose(boxes, L.VBG_BOX_EXPECTED)
-    mask = _np(G.voxel_grid.get_axis_aligned_boxes_intersecting_surface_mask(L.VBG_MASK_BOXES, L.VBG_MASK_DEPTH, L.VBG_MASK_K, 1.0, 100.0,
+    from dynamicfuion_python_amd.nnrt import voxel_grid as VG
+    mask = _np(VG.get_axis_aligned_boxes_intersecting_surface_mask(L.VBG_MASK_BOXES, L.VBG_MASK_DEPTH, L.VBG_MASK_K, 1.0, 100.0,
                                                                              1, 0.5))
     assert np.array_equal(mask, L.VBG_MASK_EXPECTED)
 
