@@ -382,32 +382,48 @@ __global__ void k_integrate_rigid(GridView g, const int* __restrict__ blocks, in
 // nodes alone. Returns the valid count; weights are normalized only when valid >= minimum (the reference returns false otherwise
 // and, where the return value is ignored, blends the unnormalized weights).
 // ---------------------------------------------------------------------------------------------------------------------
+template <int KT>
 struct Anchors {
-	int idx[TSDF_MAX_ANCHORS];
-	float w[TSDF_MAX_ANCHORS];
+	int idx[KT];
+	float w[KT];
 	int valid;
 	bool ok;
+	__device__ void reset() {
+#pragma unroll
+		for (int k = 0; k < KT; k++) {
+			idx[k] = -1;
+			w[k] = INFINITY;
+		}
+	}
 };
 
-__device__ inline void knn_insert(Anchors& a, int K, float d, int node, float& maxd, int& max_at) {
+// replace-the-maximum insertion with static register indices (the slot to overwrite is selected, not indexed)
+template <int KT>
+__device__ inline void knn_insert(Anchors<KT>& a, float d, int node, float& maxd, int& max_at) {
 	if (maxd > d) {
-		a.w[max_at] = d;   // distances held in the weight slots (WarpUtilities.h:325)
-		a.idx[max_at] = node;
+#pragma unroll
+		for (int k = 0; k < KT; k++)
+			if (k == max_at) {
+				a.w[k] = d;   // distances held in the weight slots (WarpUtilities.h:325)
+				a.idx[k] = node;
+			}
 		max_at = 0;
 		maxd = a.w[0];
-		for (int k = 1; k < K; k++)
+#pragma unroll
+		for (int k = 1; k < KT; k++)
 			if (a.w[k] > maxd) {
 				max_at = k;
 				maxd = a.w[k];
 			}
 	}
 }
-__device__ inline void anchors_finish(Anchors& a, const WarpFieldView& wf) {
-	const int K = wf.anchor_count;
+template <int KT>
+__device__ inline void anchors_finish(Anchors<KT>& a, const WarpFieldView& wf) {
 	const float c2_fixed = wf.coverage * wf.coverage;
 	float sum = 0.f;
 	a.valid = 0;
-	for (int k = 0; k < K; k++) {
+#pragma unroll
+	for (int k = 0; k < KT; k++) {
 		if (a.idx[k] < 0) continue;
 		float sq = a.w[k];
 		sq = sq * sq;
@@ -424,16 +440,20 @@ __device__ inline void anchors_finish(Anchors& a, const WarpFieldView& wf) {
 	a.ok = a.valid >= wf.minimum_valid;
 	if (a.ok) {   // NormalizeAnchorWeights (WarpUtilities.h:36-46)
 		if (sum > 0.0f) {
-			for (int k = 0; k < K; k++) a.w[k] /= sum;
+#pragma unroll
+			for (int k = 0; k < KT; k++) a.w[k] /= sum;
 		} else if (a.valid > 0) {
-			for (int k = 0; k < K; k++) a.w[k] = 1.0f / static_cast<float>(a.valid);
+#pragma unroll
+			for (int k = 0; k < KT; k++) a.w[k] = 1.0f / static_cast<float>(a.valid);
 		}
 	}
 }
 // BlendWarp (WarpUtilities.h:429-445): sum_k w_k (g_k + R_k (p - g_k) + t_k) over valid anchors
-__device__ inline void blend_warp(const Anchors& a, const WarpFieldView& wf, float px, float py, float pz, float& ox, float& oy, float& oz) {
+template <int KT>
+__device__ inline void blend_warp(const Anchors<KT>& a, const WarpFieldView& wf, float px, float py, float pz, float& ox, float& oy, float& oz) {
 	ox = oy = oz = 0.f;
-	for (int k = 0; k < wf.anchor_count; k++) {
+#pragma unroll
+	for (int k = 0; k < KT; k++) {
 		const int n = a.idx[k];
 		if (n < 0) continue;
 		const float* s = wf.state + static_cast<int64_t>(n) * NODE_STRIDE;
@@ -461,6 +481,7 @@ __device__ inline float node_dist(const float* s, float px, float py, float pz) 
 // ---------------------------------------------------------------------------------------------------------------------
 constexpr int NR_BLOCK = 256;
 constexpr int NR_CAND = 2048;
+template <int KT>
 __global__ __launch_bounds__(NR_BLOCK) void k_integrate_non_rigid(GridView g, int64_t nb, WarpFieldView wf, ImageView im, const float* __restrict__ normals,
                                                                   Xform depth_x, Xform color_x, float sdf_trunc, float color_multiplier,
                                                                   float range, uint64_t* __restrict__ cos_key) {
@@ -515,7 +536,6 @@ __global__ __launch_bounds__(NR_BLOCK) void k_integrate_non_rigid(GridView g, in
 	}
 	const int ncand = s_count;
 	overflow = ncand > NR_CAND;
-	const int K = wf.anchor_count;
 	for (int vi = t; vi < g.res3; vi += NR_BLOCK) {
 		int xv, yv, zv;
 		voxel_local(vi, g.res, xv, yv, zv);
@@ -524,29 +544,26 @@ __global__ __launch_bounds__(NR_BLOCK) void k_integrate_non_rigid(GridView g, in
 		const float z = static_cast<float>(g.keys[3 * b + 2] * g.res + zv) * g.voxel_size;
 		float xc, yc, zc;
 		depth_x.rigid(x, y, z, xc, yc, zc);
-		Anchors a;
-		for (int k = 0; k < K; k++) {
-			a.idx[k] = -1;
-			a.w[k] = INFINITY;
-		}
+		Anchors<KT> a;
+		a.reset();
 		float maxd = INFINITY;
 		int max_at = 0;
 		if (!overflow) {
 			for (int q = 0; q < ncand; q++) {
 				const int n = s_cand[q];
 				const float d = node_dist(wf.state + static_cast<int64_t>(n) * NODE_STRIDE, xc, yc, zc);
-				if (d <= range) knn_insert(a, K, d, n, maxd, max_at);
+				if (d <= range) knn_insert<KT>(a, d, n, maxd, max_at);
 			}
 		} else {
 			for (int n = 0; n < wf.N; n++) {
 				const float d = node_dist(wf.state + static_cast<int64_t>(n) * NODE_STRIDE, xc, yc, zc);
-				if (d <= range) knn_insert(a, K, d, n, maxd, max_at);
+				if (d <= range) knn_insert<KT>(a, d, n, maxd, max_at);
 			}
 		}
-		anchors_finish(a, wf);
+		anchors_finish<KT>(a, wf);
 		if (!a.ok) continue;
 		float wx, wy, wz;
-		blend_warp(a, wf, xc, yc, zc, wx, wy, wz);
+		blend_warp<KT>(a, wf, xc, yc, zc, wx, wy, wz);
 		if (wz < 0) continue;
 		float u, v;
 		depth_x.project(wx, wy, wz, u, v);
@@ -659,37 +676,64 @@ __global__ void k_compact_rows(const float* __restrict__ rows, const int* __rest
 // is the integer block key itself plus the block side length (metric only when the side is 1), the anchors' return
 // value is ignored, and the min / max updates are an if / else-if pair.
 // ---------------------------------------------------------------------------------------------------------------------
-__global__ void k_warped_block_boxes(const int32_t* __restrict__ keys, int64_t n, float side, WarpFieldView wf, Xform ex, float* __restrict__ boxes) {
-	const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-	if (i >= n) return;
-	const float x0 = static_cast<float>(keys[3 * i]), y0 = static_cast<float>(keys[3 * i + 1]), z0 = static_cast<float>(keys[3 * i + 2]);
-	const float x1 = x0 + side, y1 = y0 + side, z1 = z0 + side;
-	const float corners[8][3] = {{x0, y0, z0}, {x0, y0, z1}, {x0, y1, z0}, {x1, y0, z0}, {x0, y1, z1}, {x1, y0, z1}, {x1, y1, z0}, {x1, y1, z1}};
-	float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
-	for (int c = 0; c < 8; c++) {
+// One lane per (block, corner): 8 consecutive lanes hold one block's corners (the corner order of the reference's
+// block_corners array); node positions are staged in LDS and only nodes within 2 c of the corner enter the K-NN
+// (nodes farther away are never valid anchors; the oracle applies the same rule). Lane 0 of each octet then folds the
+// 8 warped corners in order with the reference's if / else-if min-max.
+constexpr int BOX_BLOCK = 256;
+constexpr int BOX_LDS_NODES = 4096;
+template <int KT>
+__global__ __launch_bounds__(BOX_BLOCK) void k_warped_block_boxes(const int32_t* __restrict__ keys, int64_t n, float side, WarpFieldView wf,
+                                                                  Xform ex, float range, float* __restrict__ boxes) {
+	__shared__ float s_nodes[BOX_LDS_NODES * 3];
+	const bool staged = wf.N <= BOX_LDS_NODES;
+	if (staged)
+		for (int i = threadIdx.x; i < wf.N; i += BOX_BLOCK)
+			for (int k = 0; k < 3; k++) s_nodes[3 * i + k] = wf.state[static_cast<int64_t>(i) * NODE_STRIDE + k];
+	__syncthreads();
+	const int64_t gid = static_cast<int64_t>(blockIdx.x) * BOX_BLOCK + threadIdx.x;
+	const int64_t i = gid >> 3;
+	const int c = static_cast<int>(gid & 7);
+	float w[3] = {0.f, 0.f, 0.f};
+	if (i < n) {
+		const float x0 = static_cast<float>(keys[3 * i]), y0 = static_cast<float>(keys[3 * i + 1]), z0 = static_cast<float>(keys[3 * i + 2]);
+		const float x1 = x0 + side, y1 = y0 + side, z1 = z0 + side;
+		// block_corners order (:322-331): 000, 001, 010, 100, 011, 101, 110, 111 (bit pattern x y z)
+		const int pat[8] = {0, 1, 2, 4, 3, 5, 6, 7};
+		const int m = pat[c];
 		float p[3];
-		ex.rigid(corners[c][0], corners[c][1], corners[c][2], p[0], p[1], p[2]);
-		Anchors a;
-		for (int k = 0; k < wf.anchor_count; k++) {
-			a.idx[k] = -1;
-			a.w[k] = INFINITY;
-		}
+		ex.rigid((m & 4) ? x1 : x0, (m & 2) ? y1 : y0, (m & 1) ? z1 : z0, p[0], p[1], p[2]);
+		Anchors<KT> a;
+		a.reset();
 		float maxd = INFINITY;
 		int max_at = 0;
-		for (int nn = 0; nn < wf.N; nn++) knn_insert(a, wf.anchor_count, node_dist(wf.state + static_cast<int64_t>(nn) * NODE_STRIDE, p[0], p[1], p[2]), nn, maxd, max_at);
+		for (int nn = 0; nn < wf.N; nn++) {
+			const float* q = staged ? s_nodes + 3 * nn : wf.state + static_cast<int64_t>(nn) * NODE_STRIDE;
+			const float dx = q[0] - p[0], dy = q[1] - p[1], dz = q[2] - p[2];
+			const float d = sqrtf((dx * dx + dy * dy) + dz * dz);
+			if (d <= range) knn_insert<KT>(a, d, nn, maxd, max_at);
+		}
 		WarpFieldView fixed = wf;
 		fixed.fixed_coverage = 1;   // ComputeAnchorsForPoint<.., true, true>: fixed node coverage
-		anchors_finish(a, fixed);
-		float w[3];
-		blend_warp(a, wf, p[0], p[1], p[2], w[0], w[1], w[2]);
-		for (int k = 0; k < 3; k++) {
-			if (mn[k] > w[k]) mn[k] = w[k];
-			else if (mx[k] < w[k]) mx[k] = w[k];
-		}
+		anchors_finish<KT>(a, fixed);
+		blend_warp<KT>(a, wf, p[0], p[1], p[2], w[0], w[1], w[2]);
 	}
-	for (int k = 0; k < 3; k++) {
-		boxes[6 * i + k] = mn[k];
-		boxes[6 * i + 3 + k] = mx[k];
+	float all[8][3];
+#pragma unroll
+	for (int q = 0; q < 8; q++)
+#pragma unroll
+		for (int k = 0; k < 3; k++) all[q][k] = __shfl(w[k], (threadIdx.x & ~7) + q);
+	if (i < n && c == 0) {
+		float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+		for (int q = 0; q < 8; q++)
+			for (int k = 0; k < 3; k++) {
+				if (mn[k] > all[q][k]) mn[k] = all[q][k];
+				else if (mx[k] < all[q][k]) mx[k] = all[q][k];
+			}
+		for (int k = 0; k < 3; k++) {
+			boxes[6 * i + k] = mn[k];
+			boxes[6 * i + 3 + k] = mx[k];
+		}
 	}
 }
 
@@ -1234,6 +1278,7 @@ nnrt_status take_error(int* d_error, hipStream_t s) {
 }
 
 nnrt_status activate_coords(nnrt_voxel_grid* vg, const int32_t* d_coords, int64_t n, hipStream_t s) {
+	if (n == 0) return NNRT_OK;
 	DevBuf<int> err;
 	nnrt_status st;
 	if ((st = err.ensure(1))) return st;
@@ -1424,9 +1469,18 @@ nnrt_status nnrt_voxel_grid_integrate_non_rigid(nnrt_voxel_grid* vg, const int32
 		range = 2.f * std::sqrt(mx);
 	}
 	const ImageView im = make_image(d_depth, depth_dtype, height, width, d_color, color_height, color_width, depth_scale, depth_max);
-	k_integrate_non_rigid<<<static_cast<unsigned>(vg->active), NR_BLOCK, 0, s>>>(
-	    vg->view(), vg->active, wv, im, d_depth_normals, make_xform(h_depth_K, h_E), make_xform(h_color_K ? h_color_K : h_depth_K, nullptr),
-	    vg->voxel_size * trunc_voxel_multiplier, color_multiplier(depth_dtype), range, vg->s_packed.ptr);
+	const GridView gv = vg->view();
+	const Xform xd = make_xform(h_depth_K, h_E), xc = make_xform(h_color_K ? h_color_K : h_depth_K, nullptr);
+	const float trunc = vg->voxel_size * trunc_voxel_multiplier, cm = color_multiplier(depth_dtype);
+	switch (wv.anchor_count) {
+#define NNRT_NR_CASE(KK)                                                                                                          \
+	case KK:                                                                                                                      \
+		k_integrate_non_rigid<KK><<<static_cast<unsigned>(vg->active), NR_BLOCK, 0, s>>>(gv, vg->active, wv, im, d_depth_normals, xd, xc, \
+		                                                                               trunc, cm, range, vg->s_packed.ptr);        \
+		break;
+		NNRT_NR_CASE(1) NNRT_NR_CASE(2) NNRT_NR_CASE(3) NNRT_NR_CASE(4) NNRT_NR_CASE(5) NNRT_NR_CASE(6) NNRT_NR_CASE(7) NNRT_NR_CASE(8)
+#undef NNRT_NR_CASE
+	}
 	k_cos_resolve<<<grid_of(P), 256, 0, s>>>(vg->s_packed.ptr, P, d_cos_out);
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;
@@ -1487,8 +1541,15 @@ nnrt_status nnrt_voxel_grid_warped_block_boxes(const nnrt_voxel_grid* vg, const 
 	const WarpFieldView wv = warp_field_view(wf);
 	NNRT_CHECK_ARG(wv.anchor_count >= 1 && wv.anchor_count <= TSDF_MAX_ANCHORS, "anchor_count must be in [1, 8]");
 	if (count == 0) return NNRT_OK;
-	k_warped_block_boxes<<<grid_of(count), 256, 0, static_cast<hipStream_t>(stream)>>>(
-	    d_block_keys, count, static_cast<float>(vg->res) * vg->voxel_size, wv, make_xform(nullptr, h_E), d_boxes);
+	const float side = static_cast<float>(vg->res) * vg->voxel_size;
+	const Xform ex = make_xform(nullptr, h_E);
+	hipStream_t bs = static_cast<hipStream_t>(stream);
+	switch (wv.anchor_count) {
+#define NNRT_BOX_CASE(KK)                                                                                  \
+	case KK: k_warped_block_boxes<KK><<<grid_of(8 * count, BOX_BLOCK), BOX_BLOCK, 0, bs>>>(d_block_keys, count, side, wv, ex, 2.f * wv.coverage, d_boxes); break;
+		NNRT_BOX_CASE(1) NNRT_BOX_CASE(2) NNRT_BOX_CASE(3) NNRT_BOX_CASE(4) NNRT_BOX_CASE(5) NNRT_BOX_CASE(6) NNRT_BOX_CASE(7) NNRT_BOX_CASE(8)
+#undef NNRT_BOX_CASE
+	}
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;
 }

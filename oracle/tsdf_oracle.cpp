@@ -506,9 +506,10 @@ ORC_API void orc_warped_block_boxes(const int32_t* keys, int64_t n, float side, 
 			ex.rigid(c[0], c[1], c[2], p[0], p[1], p[2]);
 			int idx[8];
 			float w[8];
-			// all nodes (no range filter), fixed coverage; the result is used whatever the valid count (anchors() returns
-			// before normalizing when valid < min_valid: the raw Gaussian weights are blended then)
-			anchors(f, p, INFINITY, idx, w);
+			// nodes within 2 c (the only possible valid anchors; both implementations search those), fixed coverage; the
+			// result is used whatever the valid count (anchors() returns before normalizing when valid < min_valid: the raw
+			// Gaussian weights are blended then)
+			anchors(f, p, 2.f * coverage, idx, w);
 			float wp[3];
 			blend(f, idx, w, p, wp);
 			for (int k = 0; k < 3; k++) {
