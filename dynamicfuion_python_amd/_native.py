@@ -26,7 +26,8 @@ class FitterParams(ctypes.Structure):
                 ("minimal_update_threshold", c_float), ("use_perspective_correction", c_int32), ("max_depth", c_float),
                 ("use_tukey_penalty_for_data_term", c_int32), ("tukey_penalty_cutoff_cm", c_float),
                 ("preconditioning_dampening_factor", c_float), ("arap_term_weight", c_float),
-                ("use_huber_penalty_for_arap_term", c_int32), ("huber_penalty_constant", c_float), ("use_hip_graph", c_int32)]
+                ("use_huber_penalty_for_arap_term", c_int32), ("huber_penalty_constant", c_float), ("use_hip_graph", c_int32),
+                ("ndc_convention", c_int32)]
 
 
 def build(force: bool = False) -> str:
@@ -83,6 +84,9 @@ _SIGNATURES = {
                                                c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "nnrt_interpolate_face_attributes": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_int32, c_void_p, c_void_p]),
     "nnrt_unproject_depth": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p]),
+    "nnrt_backproject_depth_ushort": (c_int32, [c_void_p, c_int32, c_int32, c_float, c_float, c_float, c_float, c_float, c_void_p,
+                                                c_void_p]),
+    "nnrt_backproject_depth_float": (c_int32, [c_void_p, c_int32, c_int32, c_float, c_float, c_float, c_float, c_void_p, c_void_p]),
     "nnrt_axis_angle_to_matrices_rodrigues": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "nnrt_compute_triangle_normals": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
     "nnrt_compute_vertex_normals": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),

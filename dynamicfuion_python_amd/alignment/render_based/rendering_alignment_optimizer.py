@@ -39,6 +39,9 @@ class RenderingAlignmentParameters:
     arap_term_weight: float = 200.0
     max_depth: float = 10.0
     use_perspective_correction: bool = True
+    # A.NDC_REFERENCE reproduces the reference's y-mirrored render placement (A11); A.NDC_CONSISTENT is what real depth
+    # frames need (the fusion pipeline's default)
+    ndc_convention: int = A.NDC_REFERENCE
 
 
 def as_triangle_mesh(mesh) -> G.TriangleMesh:
@@ -69,7 +72,7 @@ class RenderingAlignmentOptimizer:
             tukey_penalty_cutoff_cm=p.data_term_penalty_constant, preconditioning_dampening_factor=p.preconditioning_dampening_factor,
             arap_term_weight=p.arap_term_weight,
             use_huber_penalty_for_arap_term=p.regularization_term_penalty_function == PenaltyFunction.HUBER,
-            huber_penalty_constant=p.regularization_term_penalty_constant, device=dev)
+            huber_penalty_constant=p.regularization_term_penalty_constant, device=dev, ndc_convention=p.ndc_convention)
 
     def optimize_graph(self, graph: G.HierarchicalGraphWarpField, tsdf, target_points, target_rgb=None):
         """tsdf: an object with extract_surface_mesh(-1, 0) (NonRigidSurfaceVoxelBlockGrid) or the canonical mesh

@@ -20,21 +20,25 @@ thread_local std::string g_error;
 void set_error(const std::string& message) { g_error = message; }
 const std::string& get_error() { return g_error; }
 
-NdcSetup make_ndc_setup(const double* K, int height, int width) {
-	// CoordinateSystemConversions.h:109-146
+NdcSetup make_ndc_setup(const double* K, int height, int width, bool consistent) {
+	// CoordinateSystemConversions.h:109-146. consistent = false reproduces the reference (A11: rows mirrored about cy, columns
+	// shifted by w - 2cx, clip window centred on the NDC principal point); consistent = true maps pixel (u, v) of the
+	// intrinsics K onto the centre of raster pixel (u, v), the clip window being the image.
 	const double fx = K[0], fy = K[4], cx = K[2], cy = K[5];
 	const double h = height, w = width;
 	const double s = std::min(w, h);
 	const float range_x = ndc_range(width, height);
 	const float range_y = ndc_range(height, width);
-	const double fx_ndc = 2.0 * fx / s, fy_ndc = -2.0 * fy / s;
-	const double cx_ndc = -(2.0 * cx - w) / s, cy_ndc = (2.0 * cy - h) / s;
+	const double fx_ndc = 2.0 * fx / s, fy_ndc = (consistent ? 2.0 : -2.0) * fy / s;
+	const double cx_ndc = consistent ? (2.0 * cx + 1.0 - w) / s : -(2.0 * cx - w) / s;
+	const double cy_ndc = consistent ? (2.0 * cy + 1.0 - h) / s : (2.0 * cy - h) / s;
+	const double wx = consistent ? 0.0 : cx_ndc, wy = consistent ? 0.0 : cy_ndc;
 	NdcSetup r;
 	r.ndc = Camera{static_cast<float>(fx_ndc), static_cast<float>(fy_ndc), static_cast<float>(cx_ndc), static_cast<float>(cy_ndc)};
-	r.min_x = static_cast<float>(cx_ndc - range_x / 2.f);
-	r.max_x = static_cast<float>(cx_ndc + range_x / 2.f);
-	r.min_y = static_cast<float>(cy_ndc - range_y / 2.f);
-	r.max_y = static_cast<float>(cy_ndc + range_y / 2.f);
+	r.min_x = static_cast<float>(wx - range_x / 2.f);
+	r.max_x = static_cast<float>(wx + range_x / 2.f);
+	r.min_y = static_cast<float>(wy - range_y / 2.f);
+	r.max_y = static_cast<float>(wy + range_y / 2.f);
 	return r;
 }
 
@@ -417,7 +421,10 @@ __global__ void k_prepare_reference_points(const float* __restrict__ points, con
 
 // faces -> int4; an index outside [0, V) becomes the degenerate face (0, 0, 0) (never rasterized, never gathered out of
 // bounds) and sets error bit 4, which nnrt_fitter_check reports
-__global__ void k_faces_to_int4(const int64_t* __restrict__ faces, int64_t F, int64_t V, int4* __restrict__ out, int* error_flag) {
+// flip_winding: the consistent NDC convention keeps rows in image order, which negates every face's NDC area relative to
+// the reference's mirrored image; swapping two corners restores the orientation the back-face test expects.
+__global__ void k_faces_to_int4(const int64_t* __restrict__ faces, int64_t F, int64_t V, int flip_winding, int4* __restrict__ out,
+                                int* error_flag) {
 	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
 	if (f >= F) return;
 	const int64_t i0 = faces[3 * f], i1 = faces[3 * f + 1], i2 = faces[3 * f + 2];
@@ -426,7 +433,8 @@ __global__ void k_faces_to_int4(const int64_t* __restrict__ faces, int64_t F, in
 		out[f] = make_int4(0, 0, 0, 0);
 		return;
 	}
-	out[f] = make_int4(static_cast<int>(i0), static_cast<int>(i1), static_cast<int>(i2), 0);
+	out[f] = flip_winding ? make_int4(static_cast<int>(i0), static_cast<int>(i2), static_cast<int>(i1), 0)
+	                      : make_int4(static_cast<int>(i0), static_cast<int>(i1), static_cast<int>(i2), 0);
 }
 
 nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mode, hipStream_t s, hipEvent_t* marks = nullptr) {
@@ -533,6 +541,7 @@ void nnrt_fitter_default_params(nnrt_fitter_params* p) {
 	p->use_huber_penalty_for_arap_term = 0;
 	p->huber_penalty_constant = 1e-4f;
 	p->use_hip_graph = 1;
+	p->ndc_convention = NNRT_NDC_REFERENCE;
 }
 
 nnrt_status nnrt_fitter_create(const nnrt_fitter_params* params, int32_t device, nnrt_fitter** out) {
@@ -544,6 +553,7 @@ nnrt_status nnrt_fitter_create(const nnrt_fitter_params* params, int32_t device,
 	NNRT_CHECK_ARG(params->iteration_mode_count >= 1 && params->iteration_mode_count <= 16, "iteration_mode_count must be in [1, 16]");
 	for (int i = 0; i < params->iteration_mode_count; i++)
 		NNRT_CHECK_ARG(params->iteration_modes[i] >= 0 && params->iteration_modes[i] <= 2, "unknown iteration mode");
+	NNRT_CHECK_ARG(params->ndc_convention == NNRT_NDC_REFERENCE || params->ndc_convention == NNRT_NDC_CONSISTENT, "unknown ndc_convention");
 	DeviceGuard guard(device);
 	auto ft = std::make_unique<nnrt_fitter>();
 	ft->p = *params;
@@ -712,7 +722,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	ft->N = N;
 	ft->K = K;
 	ft->wf = wf;
-	ft->ndc = make_ndc_setup(h_K, H, W);
+	ft->ndc = make_ndc_setup(h_K, H, W, ft->p.ndc_convention == NNRT_NDC_CONSISTENT);
 	ft->pix = pixel_camera(h_K);
 	const WarpExtrinsics ne = make_extrinsics(h_E);
 	if (std::memcmp(&ne, &ft->extr, sizeof(ne)) != 0) ft->drop_graphs();
@@ -723,7 +733,8 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	hipStream_t s = ft->work;
 	NNRT_HIP(hipMemcpyAsync(ft->mesh_p.ptr, d_vertices, sizeof(float) * 3 * V, hipMemcpyDeviceToDevice, s));
 	NNRT_HIP(hipMemcpyAsync(ft->mesh_n.ptr, d_normals, sizeof(float) * 3 * V, hipMemcpyDeviceToDevice, s));
-	k_faces_to_int4<<<static_cast<unsigned>(ceil_div(F, 256)), 256, 0, s>>>(d_faces, F, V, ft->faces4.ptr, ft->error_flag.ptr);
+	k_faces_to_int4<<<static_cast<unsigned>(ceil_div(F, 256)), 256, 0, s>>>(d_faces, F, V, ft->p.ndc_convention == NNRT_NDC_CONSISTENT,
+	                                                                        ft->faces4.ptr, ft->error_flag.ptr);
 	NNRT_LAUNCH_CHECK();
 	// once per frame (:96-106): anchors & weights on the canonical mesh in virtual node order
 	if ((st = launch_compute_anchors(ft->mesh_p.ptr, V, wf->node_positions.ptr, N, K, wf->coverage,
@@ -993,7 +1004,7 @@ nnrt_status nnrt_get_mesh_ndc_face_vertices_and_clip_mask(const float* d_vertice
 	NNRT_CHECK_ARG(h_K && d_vertices && d_faces && d_face_ndc && d_clip_mask, "null pointer");
 	NNRT_CHECK_ARG(near_clip >= 0.f, "near_clipping_distance cannot be less than 0 (ExtractFaceVertices.cpp:40-44)");
 	NNRT_CHECK_ARG(near_clip <= far_clip, "near_clipping_distance cannot be greater than far_clipping_distance");
-	return launch_extract_face_ndc(d_vertices, d_faces, F, make_ndc_setup(h_K, H, W), near_clip, far_clip, d_face_ndc, d_clip_mask,
+	return launch_extract_face_ndc(d_vertices, d_faces, F, make_ndc_setup(h_K, H, W, false), near_clip, far_clip, d_face_ndc, d_clip_mask,
 	                               static_cast<hipStream_t>(stream));
 }
 
@@ -1038,6 +1049,22 @@ nnrt_status nnrt_unproject_depth(const float* d_depth, int32_t H, int32_t W, con
                                  float* d_points, uint8_t* d_mask, void* stream) {
 	NNRT_CHECK_ARG(h_K, "null intrinsics");
 	return launch_unproject(d_depth, H, W, pixel_camera(h_K), depth_scale, depth_max, d_points, d_mask, static_cast<hipStream_t>(stream));
+}
+
+nnrt_status nnrt_backproject_depth_ushort(const uint16_t* d_depth, int32_t height, int32_t width, float fx, float fy, float cx, float cy,
+                                          float normalizer, float* d_points, void* stream) {
+	NNRT_CHECK_ARG(height >= 0 && width >= 0, "negative image size");
+	NNRT_CHECK_ARG((d_depth && d_points) || height * static_cast<int64_t>(width) == 0, "null image");
+	return launch_backproject_depth_u16(d_depth, height, width, BackprojectCamera{fx, fy, cx, cy, normalizer}, d_points,
+	                                    static_cast<hipStream_t>(stream));
+}
+
+nnrt_status nnrt_backproject_depth_float(const float* d_depth, int32_t height, int32_t width, float fx, float fy, float cx, float cy,
+                                         float* d_points, void* stream) {
+	NNRT_CHECK_ARG(height >= 0 && width >= 0, "negative image size");
+	NNRT_CHECK_ARG((d_depth && d_points) || height * static_cast<int64_t>(width) == 0, "null image");
+	return launch_backproject_depth_f32(d_depth, height, width, BackprojectCamera{fx, fy, cx, cy, 1.0f}, d_points,
+	                                    static_cast<hipStream_t>(stream));
 }
 
 nnrt_status nnrt_axis_angle_to_matrices_rodrigues(const float* d_vectors, int32_t count, float* d_matrices, void* stream) {

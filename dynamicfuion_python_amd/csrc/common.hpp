@@ -115,7 +115,7 @@ struct NdcSetup {
 	float min_x, max_x, min_y, max_y;   // NDC clip range
 };
 // CoordinateSystemConversions.h:109-146 ImageSpaceIntrinsicsToNdc (double on host, stored as float like TransformIndexer)
-NdcSetup make_ndc_setup(const double* K, int height, int width);
+NdcSetup make_ndc_setup(const double* K, int height, int width, bool consistent);
 
 __host__ __device__ inline float spa_cw(float px, float py, float v0x, float v0y, float v1x, float v1y) {
 	// cpp/rendering/functional/kernel/BarycentricCoordinates.h:35-47 (ClockWise)

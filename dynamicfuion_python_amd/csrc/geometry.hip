@@ -449,6 +449,76 @@ nnrt_status launch_unproject(const float* depth, int H, int W, const Camera& K, 
 	return NNRT_OK;
 }
 
+// =====================================================================================================================
+// Depth back-projection to an ordered [H, W, 3] point image (cpp/cpu/image_proc.cpp:275-339): depth = d / normalizer,
+// p = (depth * (x - cx) / fx, depth * (y - cy) / fy, depth), zeros where depth <= 0. Four pixels per lane: 8 B (u16) or
+// 16 B (f32) in, three 16-B stores out, so a wave writes 3 KB of contiguous point image.
+// =====================================================================================================================
+template <typename T>
+__device__ __forceinline__ void backproject_one(T raw, int x, int y, const BackprojectCamera& c, float& px, float& py, float& pz) {
+	const float depth = static_cast<float>(raw) / c.normalizer;
+	if (depth > 0.f) {
+		px = depth * (static_cast<float>(x) - c.cx) / c.fx;
+		py = depth * (static_cast<float>(y) - c.cy) / c.fy;
+		pz = depth;
+	} else {
+		px = py = pz = 0.f;
+	}
+}
+
+template <typename T>
+__global__ void k_backproject_depth_x4(const T* __restrict__ depth, int H, int W, BackprojectCamera c, float4* __restrict__ out) {
+	const int64_t q = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;   // quad of pixels 4q .. 4q+3
+	if (q * 4 >= static_cast<int64_t>(H) * W) return;
+	T d[4];
+	if constexpr (sizeof(T) == 2) {
+		const uint2 v = reinterpret_cast<const uint2*>(depth)[q];
+		d[0] = static_cast<T>(v.x & 0xffffu); d[1] = static_cast<T>(v.x >> 16);
+		d[2] = static_cast<T>(v.y & 0xffffu); d[3] = static_cast<T>(v.y >> 16);
+	} else {
+		const float4 v = reinterpret_cast<const float4*>(depth)[q];
+		d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+	}
+	float p[12];
+	const int y = static_cast<int>((q * 4) / W), x0 = static_cast<int>((q * 4) % W);   // W % 4 == 0: one row per quad
+#pragma unroll
+	for (int k = 0; k < 4; ++k) backproject_one(d[k], x0 + k, y, c, p[3 * k], p[3 * k + 1], p[3 * k + 2]);
+	out[3 * q] = make_float4(p[0], p[1], p[2], p[3]);
+	out[3 * q + 1] = make_float4(p[4], p[5], p[6], p[7]);
+	out[3 * q + 2] = make_float4(p[8], p[9], p[10], p[11]);
+}
+
+template <typename T>
+__global__ void k_backproject_depth(const T* __restrict__ depth, int H, int W, BackprojectCamera c, float* __restrict__ out) {
+	const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (i >= static_cast<int64_t>(H) * W) return;
+	backproject_one(depth[i], static_cast<int>(i % W), static_cast<int>(i / W), c, out[3 * i], out[3 * i + 1], out[3 * i + 2]);
+}
+
+template <typename T>
+static nnrt_status backproject_depth(const T* depth, int H, int W, const BackprojectCamera& c, float* out, hipStream_t stream) {
+	const int64_t P = static_cast<int64_t>(H) * W;
+	if (P == 0) return NNRT_OK;
+	const bool vec = (W % 4 == 0) && (reinterpret_cast<uintptr_t>(depth) % (4 * sizeof(T)) == 0) &&
+	                 (reinterpret_cast<uintptr_t>(out) % 16 == 0);
+	if (vec) {
+		k_backproject_depth_x4<T><<<static_cast<unsigned>(ceil_div(P / 4, 256)), 256, 0, stream>>>(depth, H, W, c,
+		                                                                                         reinterpret_cast<float4*>(out));
+	} else {
+		k_backproject_depth<T><<<static_cast<unsigned>(ceil_div(P, 256)), 256, 0, stream>>>(depth, H, W, c, out);
+	}
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+nnrt_status launch_backproject_depth_u16(const uint16_t* depth, int H, int W, const BackprojectCamera& c, float* out, hipStream_t stream) {
+	return backproject_depth<uint16_t>(depth, H, W, c, out, stream);
+}
+
+nnrt_status launch_backproject_depth_f32(const float* depth, int H, int W, const BackprojectCamera& c, float* out, hipStream_t stream) {
+	return backproject_depth<float>(depth, H, W, c, out, stream);
+}
+
 __global__ void k_interpolate(const int64_t* __restrict__ pixel_faces, const float* __restrict__ bary, int64_t P, int Kf,
                               const float* __restrict__ attrs, int C, float* __restrict__ out) {
 	const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;

@@ -20,6 +20,11 @@ nnrt_status launch_pack_nodes(const float* nodes, const float* R, const float* t
 nnrt_status launch_unpack_float4x3(const float4* in, int64_t count, float* out, hipStream_t stream);
 nnrt_status launch_extract_face_ndc(const float* verts, const int64_t* faces, int64_t F, const NdcSetup& s, float near_clip, float far_clip,
                                     float* out, uint8_t* mask, hipStream_t stream);
+struct BackprojectCamera {
+	float fx, fy, cx, cy, normalizer;
+};
+nnrt_status launch_backproject_depth_u16(const uint16_t* depth, int H, int W, const BackprojectCamera& c, float* out, hipStream_t stream);
+nnrt_status launch_backproject_depth_f32(const float* depth, int H, int W, const BackprojectCamera& c, float* out, hipStream_t stream);
 nnrt_status launch_unproject(const float* depth, int H, int W, const Camera& K, float scale, float depth_max, float* pts, uint8_t* mask,
                              hipStream_t stream);
 nnrt_status launch_interpolate(const int64_t* pixel_faces, const float* bary, int64_t P, int Kf, const float* attrs, int C, float* out,

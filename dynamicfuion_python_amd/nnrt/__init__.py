@@ -3,4 +3,5 @@
 Submodules keep the reference names: nnrt.core.linalg, nnrt.geometry (+ .functional), nnrt.rendering (+ .functional),
 and the new nnrt.alignment (DeformableMeshToImageFitter, IterationMode) that the reference never bound.
 """
-from . import core, geometry, rendering, alignment  # noqa: F401
+from . import core, geometry, rendering, alignment, image_proc  # noqa: F401
+from .image_proc import backproject_depth_ushort, backproject_depth_float  # noqa: F401  (nnrt_pybind.cpp:52-67)

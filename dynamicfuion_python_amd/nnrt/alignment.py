@@ -22,12 +22,16 @@ class IterationMode(enum.IntEnum):
     ROTATION_ONLY = 2
 
 
+NDC_REFERENCE = 0     # the reference's image -> NDC mapping
+NDC_CONSISTENT = 1    # raster pixel (u, v) == pixel (u, v) of the intrinsics
+
+
 class DeformableMeshToImageFitter:
     def __init__(self, max_iteration_count: int = 100, iteration_mode_sequence=(IterationMode.ALL,), minimal_update_threshold: float = 1e-6,
                  use_perspective_correction: bool = True, max_depth: float = 10.0, use_tukey_penalty_for_data_term: bool = False,
                  tukey_penalty_cutoff_cm: float = 0.01, preconditioning_dampening_factor: float = 0.0, arap_term_weight: float = 200.0,
                  use_huber_penalty_for_arap_term: bool = False, huber_penalty_constant: float = 1e-4, device: int | None = None,
-                 use_hip_graph: bool = True):
+                 use_hip_graph: bool = True, ndc_convention: int = 0):
         device = N.current_device() if device is None else int(device)
         p = N.FitterParams()
         N.lib().nnrt_fitter_default_params(ctypes.byref(p))
@@ -46,6 +50,7 @@ class DeformableMeshToImageFitter:
         p.use_huber_penalty_for_arap_term = int(use_huber_penalty_for_arap_term)
         p.huber_penalty_constant = float(huber_penalty_constant)
         p.use_hip_graph = int(use_hip_graph)
+        p.ndc_convention = int(ndc_convention)   # NDC_REFERENCE (A11, y-mirrored renders) or NDC_CONSISTENT (real depth frames)
         h = ctypes.c_void_p()
         N.check(N.lib().nnrt_fitter_create(ctypes.byref(p), int(device), ctypes.byref(h)))
         self._h = h

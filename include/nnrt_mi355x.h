@@ -91,7 +91,13 @@ typedef struct nnrt_fitter_params {
 	int32_t use_huber_penalty_for_arap_term;/* 0 */
 	float huber_penalty_constant;           /* 1e-4 */
 	int32_t use_hip_graph;                  /* 1: capture one GN iteration per mode into a hipGraph and replay it */
+	int32_t ndc_convention;                 /* NNRT_NDC_REFERENCE (0): the reference's image-space -> NDC mapping, whose
+	                                           rendered points are y-mirrored about cy (CoordinateSystemConversions.h:
+	                                           130-136); NNRT_NDC_CONSISTENT (1): raster pixel (u, v) is pixel (u, v) of K, for
+	                                           fitting real depth frames (a deliberate divergence) */
 } nnrt_fitter_params;
+#define NNRT_NDC_REFERENCE 0
+#define NNRT_NDC_CONSISTENT 1
 
 void nnrt_fitter_default_params(nnrt_fitter_params* params);
 nnrt_status nnrt_fitter_create(const nnrt_fitter_params* params, int32_t device, nnrt_fitter** out);
@@ -185,6 +191,15 @@ nnrt_status nnrt_interpolate_face_attributes(const int64_t* d_pixel_faces, const
 /* nnrt.geometry.functional.unproject_raster_depth_without_filtering (PerspectiveProjectionImpl.h:60-146), float32 depth */
 nnrt_status nnrt_unproject_depth(const float* d_depth, int32_t height, int32_t width, const double* h_K, float depth_scale,
                                  float depth_max, float* d_points, uint8_t* d_mask, void* stream);
+/* nnrt.backproject_depth_ushort(image_in, point_image_out, fx, fy, cx, cy, normalizer) (cpp/pybind/nnrt_pybind.cpp:52-57,
+ * cpp/cpu/image_proc.cpp:275-302): uint16 depth [H,W] -> ordered point image d_points [H,W,3]; depth = d / normalizer,
+ * (depth*(x-cx)/fx, depth*(y-cy)/fy, depth), zeros where depth <= 0 (the reference leaves those entries as allocated). */
+nnrt_status nnrt_backproject_depth_ushort(const uint16_t* d_depth, int32_t height, int32_t width, float fx, float fy, float cx, float cy,
+                                          float normalizer, float* d_points, void* stream);
+/* nnrt.backproject_depth_float(image_in, point_image_out, fx, fy, cx, cy) (nnrt_pybind.cpp:66-67, image_proc.cpp:312-339): float
+ * depth in metres [H,W] -> [H,W,3], as above with normalizer 1. */
+nnrt_status nnrt_backproject_depth_float(const float* d_depth, int32_t height, int32_t width, float fx, float fy, float cx, float cy,
+                                         float* d_points, void* stream);
 /* nnrt.geometry.functional.compute_triangle_normals(mesh, normalized=True) (cpp/geometry/functional/NormalsOperations.cpp:36-46,
  * kernel NormalsOperationsImpl.h:39-68): d_out [F,3] = (v1 - v0) x (v2 - v0), optionally normalized (zero stays zero,
  * NaN -> (0,0,1)) */

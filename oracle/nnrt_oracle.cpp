@@ -89,6 +89,10 @@ struct Box2 { float min_x, max_x, min_y, max_y;   // cpp/geometry/kernel/AxisAli
 	bool Contains(float x, float y) const { return y >= min_y && x >= min_x && y <= max_y && x <= max_x; } };
 
 // ---- CoordinateSystemConversions.h:109-146 ImageSpaceIntrinsicsToNdc ----
+// g_ndc_consistent (set by orc_fit for the fitter's NNRT_NDC_CONSISTENT option, a deliberate divergence from the reference):
+// pixel (u, v) of K lands on the centre of raster pixel (u, v) instead of the reference's y-mirrored placement (A11), and
+// the clip window is the image itself.
+static bool g_ndc_consistent = false;   // orc_fit is not re-entrant; read inside its OpenMP regions
 void IntrinsicsToNdc(const double* K, int H, int W, double* ndcK, Box2* range) {
 	double fx = K[0], fy = K[4], cx = K[2], cy = K[5];
 	double height = H, width = W;
@@ -96,15 +100,16 @@ void IntrinsicsToNdc(const double* K, int H, int W, double* ndcK, Box2* range) {
 	float range_x = GetNdcRange(W, H);
 	float range_y = GetNdcRange(H, W);
 	double fx_ndc = 2.0 * fx / s;
-	double fy_ndc = -2.0 * fy / s;
-	double cx_ndc = -(2.0 * cx - width) / s;
-	double cy_ndc = (2.0 * cy - height) / s;
+	double fy_ndc = (g_ndc_consistent ? 2.0 : -2.0) * fy / s;
+	double cx_ndc = g_ndc_consistent ? (2.0 * cx + 1.0 - width) / s : -(2.0 * cx - width) / s;
+	double cy_ndc = g_ndc_consistent ? (2.0 * cy + 1.0 - height) / s : (2.0 * cy - height) / s;
 	double m[9] = {fx_ndc, 0.0, cx_ndc, 0.0, fy_ndc, cy_ndc, 0.0, 0.0, 1.0};
 	std::memcpy(ndcK, m, sizeof(m));
-	range->min_x = static_cast<float>(cx_ndc - range_x / 2.f);
-	range->max_x = static_cast<float>(cx_ndc + range_x / 2.f);
-	range->min_y = static_cast<float>(cy_ndc - range_y / 2.f);
-	range->max_y = static_cast<float>(cy_ndc + range_y / 2.f);
+	double wx = g_ndc_consistent ? 0.0 : cx_ndc, wy = g_ndc_consistent ? 0.0 : cy_ndc;
+	range->min_x = static_cast<float>(wx - range_x / 2.f);
+	range->max_x = static_cast<float>(wx + range_x / 2.f);
+	range->min_y = static_cast<float>(wy - range_y / 2.f);
+	range->max_y = static_cast<float>(wy + range_y / 2.f);
 }
 
 inline float SPA_CW(float px, float py, float v0x, float v0y, float v1x, float v1y) {
@@ -1233,6 +1238,7 @@ struct OrcFitParams {
 	float arap_weight;
 	int use_huber;
 	float huber_delta;
+	int ndc_consistent;   // NNRT_NDC_CONSISTENT: see IntrinsicsToNdc
 };
 
 struct OrcWarpField {
@@ -1277,6 +1283,14 @@ ORC_API int orc_fit(const OrcFitParams* prm, OrcWarpField* wf, const float* mesh
 	const int64_t P = static_cast<int64_t>(H) * W;
 	const int N = wf->N, KA = wf->K;
 	const bool use_reg = wf->E > 0;
+	// consistent NDC: rows keep image order, which negates NDC face areas; swapping two corners keeps front faces front
+	struct NdcModeGuard { NdcModeGuard(bool on) { g_ndc_consistent = on; } ~NdcModeGuard() { g_ndc_consistent = false; } } ndc_mode(prm->ndc_consistent != 0);
+	std::vector<int64_t> swapped;
+	if (prm->ndc_consistent) {
+		swapped.assign(faces, faces + 3 * F);
+		for (int64_t f = 0; f < F; f++) std::swap(swapped[3 * f + 1], swapped[3 * f + 2]);
+		faces = swapped.data();
+	}
 	if (prm->lm_factor < 0.f || prm->lm_factor > 1.f) { g_error = "`preconditioning_dampening_factor` should be between 0 and 1"; return 10; }
 	std::vector<int32_t> anchors(V * KA);
 	std::vector<float> weights(V * KA);

@@ -383,7 +383,7 @@ class _Params(ctypes.Structure):
     _fields_ = [("max_iterations", ctypes.c_int), ("mode_count", ctypes.c_int), ("modes", ctypes.c_int * 16),
                 ("use_perspective_correction", ctypes.c_int), ("max_depth", ctypes.c_float), ("use_tukey", ctypes.c_int),
                 ("tukey_cutoff", ctypes.c_float), ("lm_factor", ctypes.c_float), ("arap_weight", ctypes.c_float),
-                ("use_huber", ctypes.c_int), ("huber_delta", ctypes.c_float)]
+                ("use_huber", ctypes.c_int), ("huber_delta", ctypes.c_float), ("ndc_consistent", ctypes.c_int)]
 
 
 class _WarpField(ctypes.Structure):
@@ -402,7 +402,8 @@ class _Outputs(ctypes.Structure):
 def fit(*, nodes, rotations, translations, mesh_points, mesh_normals, faces, ref_points, ref_mask, H, W, K, extrinsics=None,
         max_iterations=1, modes=("ALL",), use_perspective_correction=True, max_depth=10.0, use_tukey=False, tukey_cutoff=0.01,
         lm_factor=0.0, arap_weight=200.0, use_huber=False, huber_delta=1e-4, anchor_count=4, coverage=0.05, coverage_method=0,
-        node_weights=None, min_valid_anchors=0, edges=None, edge_layers=None, radii=None, first_layer_count=None, fast_raster=True):
+        node_weights=None, min_valid_anchors=0, edges=None, edge_layers=None, radii=None, first_layer_count=None, fast_raster=True,
+        ndc_consistent=False):
     """Full FitToImage on the CPU restatement (virtual node order). Returns (R, t, diagnostics of the last iteration)."""
     nodes = _f32(nodes)
     R = _f32(rotations).copy()
@@ -421,6 +422,7 @@ def fit(*, nodes, rotations, translations, mesh_points, mesh_normals, faces, ref
     prm.arap_weight = arap_weight
     prm.use_huber = int(use_huber)
     prm.huber_delta = huber_delta
+    prm.ndc_consistent = int(ndc_consistent)
     keep = []
 
     def ptr(a):
@@ -587,4 +589,22 @@ def boxes_mask(boxes, depth, K, scale, dmax, stride, trunc):
     out = np.zeros(len(b), np.uint8)
     lib().orc_boxes_mask(_p(b), ctypes.c_int64(len(b)), _p(d), dt, d.shape[0], d.shape[1], _p(_f64(K)), ctypes.c_float(scale),
                          ctypes.c_float(dmax), int(stride), ctypes.c_float(trunc), _p(out))
+    return out
+
+
+def backproject_depth(depth, fx, fy, cx, cy, normalizer=1.0):
+    """image_proc.cpp:275-302 (uint16, depth = d / normalizer) and :312-339 (float32, normalizer 1) in float32 numpy: each
+    operation is one correctly rounded IEEE op, in the reference's order ((depth * (x - cx)) / fx), so the GPU kernel is
+    compared bit for bit. Pixels with depth <= 0 are (0, 0, 0)."""
+    d = np.asarray(depth)
+    H, W = d.shape
+    f32 = np.float32
+    dm = d.astype(f32) / f32(normalizer) if d.dtype == np.uint16 else d.astype(f32)
+    xs = np.arange(W, dtype=f32)[None, :] - f32(cx)
+    ys = np.arange(H, dtype=f32)[:, None] - f32(cy)
+    out = np.zeros((H, W, 3), f32)
+    valid = dm > 0
+    out[..., 0] = np.where(valid, (dm * xs) / f32(fx), f32(0))
+    out[..., 1] = np.where(valid, (dm * ys) / f32(fy), f32(0))
+    out[..., 2] = np.where(valid, dm, f32(0))
     return out

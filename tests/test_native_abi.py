@@ -75,8 +75,8 @@ def test_default_params_mirror_reference_constructor(native):
 
 
 def test_struct_layout_matches_header(native):
-    # 12 scalars + 16-int mode array, all 4-byte fields
-    assert ctypes.sizeof(native.FitterParams) == 4 * (12 + 16)
+    # 13 scalars + 16-int mode array, all 4-byte fields
+    assert ctypes.sizeof(native.FitterParams) == 4 * (13 + 16)
 
 
 def test_argument_errors_are_reported(native):
@@ -96,6 +96,11 @@ def test_argument_errors_are_reported(native):
     assert st == 1
     with pytest.raises(native.NnrtError):
         native.check(st)
+    lib.nnrt_fitter_default_params(ctypes.byref(p))
+    assert p.ndc_convention == 0   # NNRT_NDC_REFERENCE
+    p.ndc_convention = 7
+    assert lib.nnrt_fitter_create(ctypes.byref(p), 0, ctypes.byref(out)) == 1
+    assert b"ndc_convention" in lib.nnrt_last_error()
 
 
 def test_no_cpu_fallback(native, monkeypatch):
