@@ -437,7 +437,10 @@ __global__ void k_faces_to_int4(const int64_t* __restrict__ faces, int64_t F, in
 	                      : make_int4(static_cast<int>(i0), static_cast<int>(i1), static_cast<int>(i2), 0);
 }
 
-nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mode, hipStream_t s, hipEvent_t* marks = nullptr) {
+// from_identity: the warp and the update treat every node's motion as R = I, t = 0 without reading it (only on the
+// block-diagonal path with <= 4 anchors, see fold_reset); the result equals a reset followed by the iteration.
+nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mode, hipStream_t s, hipEvent_t* marks = nullptr,
+                              bool from_identity = false) {
 	nnrt_status st;
 	auto mark = [&](int i) -> nnrt_status {
 		if (marks) NNRT_HIP(hipEventRecord(marks[i], s));
@@ -446,7 +449,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 	if ((st = mark(0))) return st;
 	const bool with_jacobians = true;
 	if ((st = launch_warp_mesh(ft->mesh_p.ptr, ft->mesh_n.ptr, ft->V, wf->state.ptr, ft->anchors.ptr, ft->weights.ptr, ft->K, ft->extr,
-	                           ft->wpos.ptr, ft->wnrm.ptr, with_jacobians ? ft->jv.ptr : nullptr, ft->jn.ptr, s)))
+	                           ft->wpos.ptr, ft->wnrm.ptr, with_jacobians ? ft->jv.ptr : nullptr, ft->jn.ptr, s, from_identity)))
 		return st;
 	if ((st = mark(1))) return st;
 	RasterOptions ro{ft->H, ft->W, 0.5f / (static_cast<float>(fminf(ft->H, ft->W)) / 2.0f), ft->p.use_perspective_correction, 0, 1};
@@ -516,7 +519,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 		sa.gradient_out = ft->gradient.ptr;
 		sa.hessian_out = ft->hessian.ptr;
 		sa.error_flag = ft->error_flag.ptr;
-		if ((st = launch_solve_update(mode, sa, s))) return st;
+		if ((st = launch_solve_update(mode, sa, s, from_identity))) return st;
 	}
 	return mark(6);
 }
@@ -782,17 +785,21 @@ namespace {
 constexpr int MAX_GRAPH_ITERATIONS = 64;   // iterations per captured sequence graph (longer runs replay several)
 constexpr size_t MAX_CACHED_GRAPHS = 4;
 
+// reset folded into the iteration's warp / update kernels where they support it (no ARAP state reads, <= 4 anchors)
+bool fold_reset(const nnrt_fitter* ft) { return ft->E == 0 && ft->K <= 4; }
+
 nnrt_status iterate_impl(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_iteration, int32_t count, int reset, hipStream_t us) {
 	nnrt_status st;
+	const bool folded = reset && fold_reset(ft);
 	if (!ft->p.use_hip_graph) {
 		for (int it = first_iteration; it < first_iteration + count; it++) {
 			const int mode = ft->p.iteration_modes[it % ft->p.iteration_mode_count];
 			ft->last_mode = mode;
-			if (reset) {
+			if (reset && !folded) {
 				k_reset_motion<<<static_cast<unsigned>(ceil_div(wf->N, 256)), 256, 0, us>>>(wf->state.ptr, wf->N);
 				NNRT_LAUNCH_CHECK();
 			}
-			if ((st = enqueue_iteration(ft, wf, mode, us))) return st;
+			if ((st = enqueue_iteration(ft, wf, mode, us, nullptr, folded))) return st;
 		}
 		return NNRT_OK;
 	}
@@ -811,11 +818,11 @@ nnrt_status iterate_impl(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_ite
 			NNRT_HIP(hipStreamBeginCapture(ft->work, hipStreamCaptureModeThreadLocal));
 			st = NNRT_OK;
 			for (int i = 0; i < n && !st; i++) {
-				if (reset) {
+				if (reset && !folded) {
 					k_reset_motion<<<static_cast<unsigned>(ceil_div(wf->N, 256)), 256, 0, ft->work>>>(wf->state.ptr, wf->N);
 					if (hipGetLastError() != hipSuccess) st = NNRT_ERROR_HIP;
 				}
-				if (!st) st = enqueue_iteration(ft, wf, modes[static_cast<size_t>(i)], ft->work);
+				if (!st) st = enqueue_iteration(ft, wf, modes[static_cast<size_t>(i)], ft->work, nullptr, folded);
 			}
 			hipError_t ce = hipStreamEndCapture(ft->work, &g);
 			if (st) {

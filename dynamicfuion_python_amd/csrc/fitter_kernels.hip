@@ -660,37 +660,56 @@ nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t st
 // (potrf + 2 trsm per block), RodriguesImpl.h:66-88, HierarchicalGraphWarpField::TranslateNodes/RotateNodes (:261-282:
 // t += dt, R <- R * dR). One thread per node; consumes and re-zeroes the accumulator row.
 // =====================================================================================================================
+// old = the node's (t, R) as loaded at kernel start (stride-15 state row, entries 3..14)
 template <int MODE>
-__device__ inline void apply_update(float* ns, const float* x) {
+__device__ inline void apply_update(float* ns, const float* old, const float* x) {
 	if (MODE == NNRT_ITERATION_ALL) {
-		ns[3] += x[3];
-		ns[4] += x[4];
-		ns[5] += x[5];
+		ns[3] = old[0] + x[3];
+		ns[4] = old[1] + x[4];
+		ns[5] = old[2] + x[5];
 	} else if (MODE == NNRT_ITERATION_TRANSLATION_ONLY) {
-		ns[3] += x[0];
-		ns[4] += x[1];
-		ns[5] += x[2];
+		ns[3] = old[0] + x[0];
+		ns[4] = old[1] + x[1];
+		ns[5] = old[2] + x[2];
+	} else {
+		ns[3] = old[0];
+		ns[4] = old[1];
+		ns[5] = old[2];
 	}
 	if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) {
 		float dR[9], R[9], o[9];
 		rodrigues_device(x[0], x[1], x[2], dR);
 #pragma unroll
-		for (int i = 0; i < 9; i++) R[i] = ns[6 + i];
+		for (int i = 0; i < 9; i++) R[i] = old[3 + i];
 #pragma unroll
 		for (int r = 0; r < 3; r++)
 #pragma unroll
 			for (int c = 0; c < 3; c++) o[3 * r + c] = (R[3 * r] * dR[c] + R[3 * r + 1] * dR[3 + c]) + R[3 * r + 2] * dR[6 + c];
 #pragma unroll
 		for (int i = 0; i < 9; i++) ns[6 + i] = o[i];
+	} else {
+#pragma unroll
+		for (int i = 0; i < 9; i++) ns[6 + i] = old[3 + i];
 	}
 }
 
-template <int MODE>
-__global__ void k_solve_update(SolveArgs a) {
+// IDENTITY: the node's motion before the update is R = I, t = 0 (iterate-from-identity) and is not read. Otherwise the
+// (t, R) row is loaded up front so its latency overlaps the accumulator loads.
+template <int MODE, bool IDENTITY>
+__global__ __launch_bounds__(64) void k_solve_update(SolveArgs a) {
 	using T = ModeTraits<MODE>;
 	constexpr int S = T::S;
 	const int n = blockIdx.x * blockDim.x + threadIdx.x;
 	if (n >= a.N) return;
+	float* ns = a.node_state + static_cast<int64_t>(n) * NODE_STRIDE;
+	float old[12];
+	if constexpr (IDENTITY) {
+#pragma unroll
+		for (int i = 0; i < 12; i++) old[i] = (i == 3 || i == 7 || i == 11) ? 1.f : 0.f;
+	} else {
+#pragma unroll
+		for (int i = 0; i < 12; i++) old[i] = __builtin_nontemporal_load(ns + 3 + i);
+	}
 	double* acc = a.acc + static_cast<int64_t>(n) * ACC_STRIDE;
 	float H[S][S], g[S];
 	int e = 0;
@@ -731,17 +750,24 @@ __global__ void k_solve_update(SolveArgs a) {
 	}
 #pragma unroll
 	for (int c = 0; c < S; c++) a.updates_out[static_cast<int64_t>(n) * S + c] = x[c];
-	apply_update<MODE>(a.node_state + static_cast<int64_t>(n) * NODE_STRIDE, x);
+	apply_update<MODE>(ns, old, x);
 }
 
-nnrt_status launch_solve_update(int mode, const SolveArgs& args, hipStream_t stream) {
-	const unsigned grid = static_cast<unsigned>(ceil_div(args.N, 256));
+template <bool IDENTITY>
+static nnrt_status solve_update_mode(int mode, const SolveArgs& args, hipStream_t stream) {
+	const unsigned grid = static_cast<unsigned>(ceil_div(args.N, 64));   // one wave per workgroup: more CUs take part
 	switch (mode) {
-		case NNRT_ITERATION_ALL: k_solve_update<NNRT_ITERATION_ALL><<<grid, 256, 0, stream>>>(args); break;
-		case NNRT_ITERATION_TRANSLATION_ONLY: k_solve_update<NNRT_ITERATION_TRANSLATION_ONLY><<<grid, 256, 0, stream>>>(args); break;
-		case NNRT_ITERATION_ROTATION_ONLY: k_solve_update<NNRT_ITERATION_ROTATION_ONLY><<<grid, 256, 0, stream>>>(args); break;
+		case NNRT_ITERATION_ALL: k_solve_update<NNRT_ITERATION_ALL, IDENTITY><<<grid, 64, 0, stream>>>(args); break;
+		case NNRT_ITERATION_TRANSLATION_ONLY: k_solve_update<NNRT_ITERATION_TRANSLATION_ONLY, IDENTITY><<<grid, 64, 0, stream>>>(args); break;
+		case NNRT_ITERATION_ROTATION_ONLY: k_solve_update<NNRT_ITERATION_ROTATION_ONLY, IDENTITY><<<grid, 64, 0, stream>>>(args); break;
 		default: set_error("unknown iteration mode"); return NNRT_ERROR_ARGUMENT;
 	}
+	return NNRT_OK;
+}
+
+nnrt_status launch_solve_update(int mode, const SolveArgs& args, hipStream_t stream, bool from_identity) {
+	const nnrt_status st = from_identity ? solve_update_mode<true>(mode, args, stream) : solve_update_mode<false>(mode, args, stream);
+	if (st) return st;
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;
 }

@@ -48,7 +48,7 @@ struct SolveArgs {
 
 // pass 1 (k_pixel_jacobians) then pass 2 (k_node_reduce_grouped); `between` (optional) is recorded between them
 nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t stream, hipEvent_t between = nullptr);
-nnrt_status launch_solve_update(int mode, const SolveArgs& args, hipStream_t stream);
+nnrt_status launch_solve_update(int mode, const SolveArgs& args, hipStream_t stream, bool from_identity = false);
 
 // ARAP (regularized, mode ALL) path
 struct ArapArgs {

@@ -246,6 +246,9 @@ __device__ inline float quad_bcast(float x) {
 	return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xf, 0xf, false));
 }
 
+// IDENTITY: every node at R = I, t = 0 without reading them (iterate-from-identity, the benchmark protocol); the
+// arithmetic is the same as with the identity loaded from memory.
+template <bool IDENTITY>
 __global__ __launch_bounds__(256) void k_warp_mesh_quad(const float* __restrict__ points, const float* __restrict__ normals, int64_t V,
                                                         const float* __restrict__ node_state, const int32_t* __restrict__ anchors,
                                                         const float* __restrict__ weights, int K, WarpExtrinsics E, float4* __restrict__ out_p,
@@ -273,10 +276,22 @@ __global__ __launch_bounds__(256) void k_warp_mesh_quad(const float* __restrict_
 			valid = true;
 			const float w = weights[v * K + k];
 			const float4* ns = reinterpret_cast<const float4*>(node_state + static_cast<int64_t>(a) * NODE_STRIDE);
-			const float4 s0 = ns[0], s1 = ns[1], s2 = ns[2], s3 = ns[3];   // g, t, R (row-major), pad
-			const f3 g = make3(s0.x, s0.y, s0.z);
-			const f3 t = make3(s0.w, s1.x, s1.y);
-			const float R[9] = {s1.z, s1.w, s2.x, s2.y, s2.z, s2.w, s3.x, s3.y, s3.z};
+			f3 g, t;
+			float R[9];
+			if constexpr (IDENTITY) {
+				const float4 s0 = ns[0];
+				g = make3(s0.x, s0.y, s0.z);
+				t = make3(0.f, 0.f, 0.f);
+#pragma unroll
+				for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.f : 0.f;
+			} else {
+				const float4 s0 = ns[0], s1 = ns[1], s2 = ns[2], s3 = ns[3];   // g, t, R (row-major), pad
+				g = make3(s0.x, s0.y, s0.z);
+				t = make3(s0.w, s1.x, s1.y);
+				const float Rl[9] = {s1.z, s1.w, s2.x, s2.y, s2.z, s2.w, s3.x, s3.y, s3.z};
+#pragma unroll
+				for (int i = 0; i < 9; i++) R[i] = Rl[i];
+			}
 			const f3 Rd = matvec3(R, sub3(pc, g));
 			cp = make3(w * ((g.x + Rd.x) + t.x), w * ((g.y + Rd.y) + t.y), w * ((g.z + Rd.z) + t.z));
 			const f3 Rn = matvec3(R, nc);
@@ -319,13 +334,20 @@ __global__ __launch_bounds__(256) void k_warp_mesh_quad(const float* __restrict_
 
 nnrt_status launch_warp_mesh(const float* points, const float* normals, int64_t V, const float* node_state, const int32_t* anchors,
                              const float* weights, int K, const WarpExtrinsics& E, float4* out_p, float4* out_n, float4* jv, float4* jn,
-                             hipStream_t stream) {
+                             hipStream_t stream, bool from_identity) {
 	if (V == 0) return NNRT_OK;
 	if (K <= 4) {
-		k_warp_mesh_quad<<<static_cast<unsigned>(ceil_div(4 * V, 256)), 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E,
-		                                                                                 out_p, out_n, jv, jn);
+		const unsigned grid = static_cast<unsigned>(ceil_div(4 * V, 256));
+		if (from_identity)
+			k_warp_mesh_quad<true><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n, jv, jn);
+		else
+			k_warp_mesh_quad<false><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n, jv, jn);
 		NNRT_LAUNCH_CHECK();
 		return NNRT_OK;
+	}
+	if (from_identity) {
+		set_error("launch_warp_mesh: from_identity needs K <= 4");
+		return NNRT_ERROR_ARGUMENT;
 	}
 	k_warp_mesh<<<static_cast<unsigned>(ceil_div(V, 256)), 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p,
 	                                                                          out_n, jv, jn);

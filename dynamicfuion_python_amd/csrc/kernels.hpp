@@ -15,7 +15,7 @@ nnrt_status launch_compute_anchors(const float* points, int64_t V, const float* 
                                    const float* node_weights, int minimum_valid, int32_t* anchors, float* weights, hipStream_t stream);
 nnrt_status launch_warp_mesh(const float* points, const float* normals, int64_t V, const float* node_state, const int32_t* anchors,
                              const float* weights, int K, const WarpExtrinsics& E, float4* out_p, float4* out_n, float4* jv, float4* jn,
-                             hipStream_t stream);
+                             hipStream_t stream, bool from_identity = false);
 nnrt_status launch_pack_nodes(const float* nodes, const float* R, const float* t, int N, float* state, hipStream_t stream);
 nnrt_status launch_unpack_float4x3(const float4* in, int64_t count, float* out, hipStream_t stream);
 nnrt_status launch_extract_face_ndc(const float* verts, const int64_t* faces, int64_t F, const NdcSetup& s, float near_clip, float far_clip,

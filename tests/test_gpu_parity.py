@@ -322,6 +322,35 @@ def test_sequence_graph_and_iterate_from_identity(nn, S, oracle_mod):
     dg = ft.diagnostics()
     assert np.array_equal(dg["pixel_faces"], d_one["pixel_faces"])
     assert rel_err(dg["updates"], d_one["updates"]) < 1e-6
+    # the identity start is folded into the warp / update kernels on this path (no reset launch): the final state is
+    # one iteration's, for every mode, graph-captured or eager
+    for mode in (A.IterationMode.ALL, A.IterationMode.TRANSLATION_ONLY, A.IterationMode.ROTATION_ONLY):
+        wf_one, _, _ = _gpu_fit(nn, sc, depth, 1, modes=[mode], graph=False)
+        for graph in (True, False):
+            wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE,
+                                              sc.layer_count)
+            wf.set_node_translations(np.full((len(sc.nodes), 3), 0.5, np.float32))   # overwritten by the identity start
+            ft = A.DeformableMeshToImageFitter(1, [mode], preconditioning_dampening_factor=0.001, use_hip_graph=graph)
+            ft.prepare(wf, G.TriangleMesh(sc.points, sc.normals, sc.faces), depth, None, sc.K)
+            ft.iterate_from_identity(wf, 0, 2)
+            ft.check()
+            assert rel_err(wf.get_node_translations(), wf_one.get_node_translations()) < 1e-6
+            assert rel_err(wf.get_node_rotations() - np.eye(3), wf_one.get_node_rotations() - np.eye(3)) < 1e-6
+
+
+def test_iterate_from_identity_with_arap(nn, S, oracle_mod):
+    """ARAP path (the reset stays a separate launch there): iterate_from_identity(3) == one iteration."""
+    A, G = nn.alignment, nn.geometry
+    sc = _scene(S, oracle_mod, "C1_ARAP")
+    depth = scene_target(oracle_mod, sc)
+    wf_one, _, _ = _gpu_fit(nn, sc, depth, 1)
+    wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE,
+                                      sc.layer_count)
+    ft = A.DeformableMeshToImageFitter(1, [A.IterationMode.ALL], preconditioning_dampening_factor=0.001)
+    ft.prepare(wf, G.TriangleMesh(sc.points, sc.normals, sc.faces), depth, None, sc.K)
+    ft.iterate_from_identity(wf, 0, 3)
+    ft.check()
+    assert rel_err(wf.get_node_translations(), wf_one.get_node_translations()) < 1e-4
 
 
 def test_fit_with_extrinsics_parity(nn, S, oracle_mod):
