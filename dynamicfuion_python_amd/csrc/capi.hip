@@ -204,10 +204,11 @@ nnrt_status nnrt_warp_field_create(const float* h_nodes, int32_t node_count, flo
 	wf->minimum_valid = minimum_valid_anchor_count;
 	wf->coverage_method = coverage_method;
 	wf->nodes_original.assign(h_nodes, h_nodes + 3 * static_cast<size_t>(node_count));
-	nnrt_status st = build_hierarchy(h_nodes, node_count, node_coverage, layer_count, max_vertex_degree, h_layer_radii, wf->h);
+	HierarchyOps& ops = device_hierarchy_ops();
+	nnrt_status st = build_hierarchy(h_nodes, node_count, node_coverage, layer_count, max_vertex_degree, h_layer_radii, ops, wf->h);
 	if (st) return st;
 	std::vector<float> weights_original;
-	node_coverage_weights(h_nodes, node_count, node_coverage, weights_original);
+	if ((st = ops.coverage_weights(h_nodes, node_count, node_coverage, weights_original))) return st;
 	std::vector<float> state(static_cast<size_t>(node_count) * NODE_STRIDE, 0.f), pos(3 * static_cast<size_t>(node_count));
 	wf->weights_virtual.resize(node_count);
 	for (int v = 0; v < node_count; v++) {

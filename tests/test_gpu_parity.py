@@ -536,3 +536,52 @@ def test_normals_bit_exact(nn, S, oracle_mod, name):
         G.functional.compute_triangle_normals(bad)
     # the library stays usable after a rejected call (nothing gathered outside the vertex array)
     assert np.array_equal(_np(G.functional.compute_triangle_normals(mesh, True)), oracle_mod.triangle_normals(sc.points, sc.faces, True))
+
+
+# ---- warp-field construction on the GPU (hierarchy.hip): medoid subsampling, K-NN edges, coverage weights ------------
+
+def test_hierarchy_kat_gpu(nn):
+    """cpp/tests/test_graph_warp_field.cpp:30-340 through the device construction (3 layers, radii 0.25/0.5/1.0)."""
+    G = nn.geometry
+    wf = G.HierarchicalGraphWarpField(L.HIERARCHY_NODES, 0.25, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE, 3, 4,
+                                      [0.25, 0.5, 1.0])
+    vidx, edges = wf.get_virtual_node_indices(), wf.get_edges()
+    assert list(wf.get_layer_node_counts()) == [19, 10, 4]
+    assert sorted(vidx[:19].tolist()) == L.HIERARCHY_LAYER0
+    assert sorted(vidx[19:29].tolist()) == L.HIERARCHY_LAYER1
+    assert sorted(vidx[29:].tolist()) == L.HIERARCHY_LAYER2
+    assert edges[:, 0].tolist() == L.HIERARCHY_EDGE_SOURCES
+    assert sorted((int(vidx[i]), int(vidx[j])) for i, j in edges) == sorted(L.HIERARCHY_EDGES_ORIGINAL)
+
+
+def _grid_nodes(n, seed, jitter=1e-3):
+    rng = np.random.default_rng(seed)
+    side = int(np.sqrt(n))
+    i = np.arange(n)
+    nodes = np.stack([(i % side) * 0.025 + rng.uniform(-jitter, jitter, n), (i // side) * 0.025, 1.5 + 0.01 * rng.uniform(-1, 1, n)], 1)
+    return nodes.astype(np.float32)
+
+
+@pytest.mark.parametrize("n,layers,degree,kind", [(1500, 2, 4, "grid"), (5000, 2, 4, "grid"), (3000, 4, 4, "random"),
+                                                   (2000, 3, 6, "random"), (700, 2, 1, "duplicates")])
+def test_hierarchy_and_coverage_bit_exact(nn, oracle_mod, n, layers, degree, kind):
+    """Device construction == the sequential restatement: layer membership, virtual order, edges, edge layers, coverage
+    weights (exact float equality: same per-cell summation order, correctly rounded sqrt)."""
+    if kind == "grid":
+        nodes = _grid_nodes(n, 1)
+    elif kind == "random":
+        nodes = np.random.default_rng(n).uniform(-0.5, 0.5, (n, 3)).astype(np.float32)
+    else:   # exact duplicates and equal distances: medoid ties and K-NN ties resolved by index
+        base = np.random.default_rng(3).integers(0, 6, (n // 2, 3)).astype(np.float32) * 0.04
+        nodes = np.concatenate([base, base])
+    coverage = 0.03 if kind == "grid" else 0.05
+    G = nn.geometry
+    vidx_o, counts_o, edges_o, el_o = oracle_mod.build_hierarchy(nodes, coverage, layers, degree)
+    wf = G.HierarchicalGraphWarpField(nodes, coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.MINIMAL_K_NEIGHBOR_NODE_DISTANCE, layers,
+                                      degree)
+    assert np.array_equal(wf.get_layer_node_counts(), counts_o)
+    assert np.array_equal(wf.get_virtual_node_indices(), vidx_o)
+    assert np.array_equal(wf.get_edges(), edges_o)
+    assert np.array_equal(wf.get_edge_layer_indices(), el_o)
+    w_o = oracle_mod.node_coverage_weights(nodes, coverage)
+    assert np.array_equal(wf.get_node_coverage_weights(), w_o[vidx_o])
