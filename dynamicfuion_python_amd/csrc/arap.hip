@@ -586,22 +586,39 @@ __global__ __launch_bounds__(CT) void k_chol_step(float* __restrict__ A, int ld,
 	int bad = 0;
 #pragma clang loop unroll(full)
 	for (int jb = 0; jb < CORNER_NB; jb += 4) {
+		// The 4 x 4 diagonal sub-block is read once (10 independent readlanes) and factored wave-uniformly; every lane
+		// then runs the same operations on its own row with the uniform multipliers. The uniform values are exactly
+		// the ones lanes jb..jb+3 compute (same operations, same order), so the pivot chain has no readlane round trip
+		// per column.
+		float M[4][4], Lu[4][4], rsv[4];
+#pragma unroll
+		for (int q = 0; q < 4; q++)
+#pragma unroll
+			for (int i = q; i < 4; i++) M[i][q] = lane_bcast(ap[jb + q].x, jb + i);
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			float piv = M[q][q];   // A_jj after the first j eliminations
+			bad |= !(piv > 0.f);
+			piv = piv > 0.f ? piv : 1.f;
+			rsv[q] = __builtin_amdgcn_rsqf(piv);
+#pragma unroll
+			for (int i = q; i < 4; i++) Lu[i][q] = M[i][q] * rsv[q];
+#pragma unroll
+			for (int q2 = q + 1; q2 < 4; q2++)
+#pragma unroll
+				for (int i = q2; i < 4; i++) M[i][q2] = __builtin_fmaf(-Lu[i][q], Lu[q2][q], M[i][q2]);
+		}
 		float lx[4];
 		f32x2 nl[4];
 #pragma unroll
 		for (int q = 0; q < 4; q++) {
-			const int j = jb + q;
-			float piv = lane_bcast(ap[j].x, j);   // A_jj after the first j eliminations
-			bad |= !(piv > 0.f);
-			piv = piv > 0.f ? piv : 1.f;
-			const float rs = __builtin_amdgcn_rsqf(piv);
-			const f32x2 l = ap[j] * rs;   // (L_rj for rows r >= j of the diagonal block, panel / rhs entry)
-			ap[j] = l;
+			const f32x2 l = ap[jb + q] * rsv[q];   // (L_rj for rows r >= j of the diagonal block, panel / rhs entry)
+			ap[jb + q] = l;
 			lx[q] = l.x;
 			nl[q] = -l;
 #pragma unroll
 			for (int q2 = q + 1; q2 < 4; q2++) {
-				const float lc = lane_bcast(l.x, jb + q2);
+				const float lc = Lu[q2][q];
 				ap[jb + q2] = __builtin_elementwise_fma(nl[q], f32x2{lc, lc}, ap[jb + q2]);
 			}
 		}

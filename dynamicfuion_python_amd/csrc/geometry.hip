@@ -265,43 +265,14 @@ __global__ __launch_bounds__(256) void k_warp_mesh_quad(const float* __restrict_
 		const f3 n = make3(normals[3 * v], normals[3 * v + 1], normals[3 * v + 2]);
 		f3 pc = p, nc = n;
 		if (!E.identity) {
-			pc = make3(((p.x * E.m[0] + p.y * E.m[1]) + p.z * E.m[2]) + E.m[3], ((p.x * E.m[4] + p.y * E.m[5]) + p.z * E.m[6]) + E.m[7],
-			           ((p.x * E.m[8] + p.y * E.m[9]) + p.z * E.m[10]) + E.m[11]);
-			nc = make3((n.x * E.m[0] + n.y * E.m[1]) + n.z * E.m[2], (n.x * E.m[4] + n.y * E.m[5]) + n.z * E.m[6],
-			           (n.x * E.m[8] + n.y * E.m[9]) + n.z * E.m[10]);
+			pc = apply_extrinsics_point(E, p);
+			nc = apply_extrinsics_normal(E, n);
 		}
 		const int32_t a = anchors[v * K + k];
 		float4 ojv = make_float4(0.f, 0.f, 0.f, 0.f), ojn = make_float4(0.f, 0.f, 0.f, 0.f);
 		if (a != -1) {
 			valid = true;
-			const float w = weights[v * K + k];
-			const float4* ns = reinterpret_cast<const float4*>(node_state + static_cast<int64_t>(a) * NODE_STRIDE);
-			f3 g, t;
-			float R[9];
-			if constexpr (IDENTITY) {
-				const float4 s0 = ns[0];
-				g = make3(s0.x, s0.y, s0.z);
-				t = make3(0.f, 0.f, 0.f);
-#pragma unroll
-				for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.f : 0.f;
-			} else {
-				const float4 s0 = ns[0], s1 = ns[1], s2 = ns[2], s3 = ns[3];   // g, t, R (row-major), pad
-				g = make3(s0.x, s0.y, s0.z);
-				t = make3(s0.w, s1.x, s1.y);
-				const float Rl[9] = {s1.z, s1.w, s2.x, s2.y, s2.z, s2.w, s3.x, s3.y, s3.z};
-#pragma unroll
-				for (int i = 0; i < 9; i++) R[i] = Rl[i];
-			}
-			const f3 Rd = matvec3(R, sub3(pc, g));
-			cp = make3(w * ((g.x + Rd.x) + t.x), w * ((g.y + Rd.y) + t.y), w * ((g.z + Rd.z) + t.z));
-			const f3 Rn = matvec3(R, nc);
-			cn = make3(w * Rn.x, w * Rn.y, w * Rn.z);
-			if (jv) {
-				const f3 Rj = E.identity ? Rd : matvec3(R, sub3(p, g));
-				const f3 Rnj = E.identity ? Rn : matvec3(R, n);
-				ojv = make_float4(-w * Rj.x, -w * Rj.y, -w * Rj.z, w);
-				ojn = make_float4(-w * Rnj.x, -w * Rnj.y, -w * Rnj.z, 0.f);
-			}
+			warp_slot<IDENTITY>(node_state, a, weights[v * K + k], p, n, pc, nc, E.identity, cp, cn, ojv, ojn);
 		}
 		if (jv) {
 			jv[v * K + k] = ojv;

@@ -11,6 +11,48 @@ struct WarpExtrinsics {
 };
 WarpExtrinsics make_extrinsics(const double* E);
 
+// One (vertex, anchor) term of the blended warp (WarpUtilities.h:448-467) and its Jacobian rows
+// (WarpedSurfaceJacobiansImpl.h:33-158): cp = w (g + R (pc - g) + t), cn = w R nc, jv = (-w R (p - g), w), jn = (-w R n, 0).
+// p / n: the vertex as stored; pc / nc: after the extrinsics. IDENTITY: R = I, t = 0 without reading them. Shared by
+// the warp kernels.
+template <bool IDENTITY>
+__device__ inline void warp_slot(const float* __restrict__ node_state, int32_t a, float w, f3 p, f3 n, f3 pc, f3 nc, int extr_identity, f3& cp,
+                                 f3& cn, float4& ojv, float4& ojn) {
+	const float4* ns = reinterpret_cast<const float4*>(node_state + static_cast<int64_t>(a) * NODE_STRIDE);
+	f3 g, t;
+	float R[9];
+	if constexpr (IDENTITY) {
+		const float4 s0 = ns[0];
+		g = make3(s0.x, s0.y, s0.z);
+		t = make3(0.f, 0.f, 0.f);
+#pragma unroll
+		for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.f : 0.f;
+	} else {
+		const float4 s0 = ns[0], s1 = ns[1], s2 = ns[2], s3 = ns[3];   // g, t, R (row-major), pad
+		g = make3(s0.x, s0.y, s0.z);
+		t = make3(s0.w, s1.x, s1.y);
+		const float Rl[9] = {s1.z, s1.w, s2.x, s2.y, s2.z, s2.w, s3.x, s3.y, s3.z};
+#pragma unroll
+		for (int i = 0; i < 9; i++) R[i] = Rl[i];
+	}
+	const f3 Rd = matvec3(R, sub3(pc, g));
+	cp = make3(w * ((g.x + Rd.x) + t.x), w * ((g.y + Rd.y) + t.y), w * ((g.z + Rd.z) + t.z));
+	const f3 Rn = matvec3(R, nc);
+	cn = make3(w * Rn.x, w * Rn.y, w * Rn.z);
+	const f3 Rj = extr_identity ? Rd : matvec3(R, sub3(p, g));
+	const f3 Rnj = extr_identity ? Rn : matvec3(R, n);
+	ojv = make_float4(-w * Rj.x, -w * Rj.y, -w * Rj.z, w);
+	ojn = make_float4(-w * Rnj.x, -w * Rnj.y, -w * Rnj.z, 0.f);
+}
+
+__device__ inline f3 apply_extrinsics_point(const WarpExtrinsics& E, f3 p) {
+	return make3(((p.x * E.m[0] + p.y * E.m[1]) + p.z * E.m[2]) + E.m[3], ((p.x * E.m[4] + p.y * E.m[5]) + p.z * E.m[6]) + E.m[7],
+	             ((p.x * E.m[8] + p.y * E.m[9]) + p.z * E.m[10]) + E.m[11]);
+}
+__device__ inline f3 apply_extrinsics_normal(const WarpExtrinsics& E, f3 n) {
+	return make3((n.x * E.m[0] + n.y * E.m[1]) + n.z * E.m[2], (n.x * E.m[4] + n.y * E.m[5]) + n.z * E.m[6], (n.x * E.m[8] + n.y * E.m[9]) + n.z * E.m[10]);
+}
+
 nnrt_status launch_compute_anchors(const float* points, int64_t V, const float* nodes, int N, int K, float coverage,
                                    const float* node_weights, int minimum_valid, int32_t* anchors, float* weights, hipStream_t stream);
 nnrt_status launch_warp_mesh(const float* points, const float* normals, int64_t V, const float* node_state, const int32_t* anchors,
