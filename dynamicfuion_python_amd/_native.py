@@ -120,7 +120,23 @@ _SIGNATURES = {
     "nnrt_voxel_grid_extract_triangle_mesh": (c_int32, [c_void_p, c_float, c_void_p, c_void_p, c_void_p]),
     "nnrt_voxel_grid_copy_mesh": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "nnrt_marching_cubes_table": (c_int32, [c_void_p, c_void_p]),
+    # include/nnrt_dlpack.h
+    "nnrt_warp_field_create_dlpack": (c_int32, [c_void_p, c_float, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_int32,
+                                                c_void_p]),
+    "nnrt_fitter_fit_to_image_dlpack": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                  c_float, c_void_p]),
 }
+
+
+def dlpack(x):
+    """(capsule, DLManagedTensor*) for a torch tensor or numpy array. The tensor is lent, not consumed: keep the capsule
+    alive for the duration of the call; its destructor releases the tensor afterwards."""
+    import torch
+    cap = torch.utils.dlpack.to_dlpack(x) if isinstance(x, torch.Tensor) else x.__dlpack__()
+    get = ctypes.pythonapi.PyCapsule_GetPointer
+    get.restype = ctypes.c_void_p
+    get.argtypes = [ctypes.py_object, ctypes.c_char_p]
+    return cap, get(cap, b"dltensor")
 
 
 def exported_symbols():

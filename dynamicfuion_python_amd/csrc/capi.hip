@@ -11,6 +11,7 @@
 
 #include "fitter_kernels.hpp"
 #include "warp_field.hpp"
+#include "nnrt_dlpack.h"
 
 namespace nnrt {
 
@@ -1166,6 +1167,109 @@ nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, cons
 		return NNRT_ERROR_NOT_POSITIVE_DEFINITE;
 	}
 	return NNRT_OK;
+}
+
+// ---- DLPack entry points (include/nnrt_dlpack.h): validate, then forward to the pointer entry points ----------------
+namespace {
+enum class Mem { device, host };
+// dtypes: list of (code, bits); dims: -1 = any extent (returned through `dims_out`)
+nnrt_status dl_check(const DLManagedTensor* mt, const char* name, std::initializer_list<std::pair<int, int>> dtypes, int ndim,
+                     std::initializer_list<int64_t> dims, Mem mem, int device, const void** data, int64_t* dims_out) {
+	if (!mt) {
+		set_error(std::string("invalid argument: ") + name + ": null tensor");
+		return NNRT_ERROR_ARGUMENT;
+	}
+	const DLTensor& t = mt->dl_tensor;
+	bool dtype_ok = false;
+	for (const auto& d : dtypes) dtype_ok |= t.dtype.code == d.first && t.dtype.bits == d.second && t.dtype.lanes == 1;
+	if (!dtype_ok) {
+		set_error(std::string("invalid argument: ") + name + ": unsupported dtype (code " + std::to_string(t.dtype.code) + ", bits " +
+		          std::to_string(t.dtype.bits) + ")");
+		return NNRT_ERROR_ARGUMENT;
+	}
+	if (t.ndim != ndim) {
+		set_error(std::string("invalid argument: ") + name + ": expected " + std::to_string(ndim) + " dimensions, got " + std::to_string(t.ndim));
+		return NNRT_ERROR_ARGUMENT;
+	}
+	int k = 0;
+	for (int64_t want : dims) {
+		if (want >= 0 && t.shape[k] != want) {
+			set_error(std::string("invalid argument: ") + name + ": dimension " + std::to_string(k) + " is " + std::to_string(t.shape[k]) +
+			          ", expected " + std::to_string(want));
+			return NNRT_ERROR_ARGUMENT;
+		}
+		dims_out[k] = t.shape[k];
+		k++;
+	}
+	if (t.strides) {   // compact row-major only
+		int64_t expect = 1;
+		for (int d = ndim - 1; d >= 0; d--) {
+			if (t.shape[d] > 1 && t.strides[d] != expect) {
+				set_error(std::string("invalid argument: ") + name + ": not a compact row-major tensor");
+				return NNRT_ERROR_ARGUMENT;
+			}
+			expect *= t.shape[d];
+		}
+	}
+	const bool on_device = t.device.device_type == kDLROCM;
+	const bool on_host = t.device.device_type == kDLCPU || t.device.device_type == kDLROCMHost;
+	if (mem == Mem::device && !(on_device && t.device.device_id == device)) {
+		set_error(std::string("invalid argument: ") + name + ": must be a ROCm device tensor on device " + std::to_string(device));
+		return NNRT_ERROR_ARGUMENT;
+	}
+	if (mem == Mem::host && !on_host) {
+		set_error(std::string("invalid argument: ") + name + ": must be a host (CPU) tensor");
+		return NNRT_ERROR_ARGUMENT;
+	}
+	*data = static_cast<const char*>(t.data) + t.byte_offset;
+	return NNRT_OK;
+}
+constexpr std::pair<int, int> F32{kDLFloat, 32}, F64{kDLFloat, 64}, I64{kDLInt, 64}, U8{kDLUInt, 8}, B8{kDLBool, 8};
+} // namespace
+
+nnrt_status nnrt_warp_field_create_dlpack(const DLManagedTensor* nodes, float node_coverage, int32_t threshold_nodes_by_distance,
+                                          int32_t anchor_count, int32_t minimum_valid_anchor_count, int32_t coverage_method,
+                                          int32_t layer_count, int32_t max_vertex_degree, const float* h_layer_radii, int32_t device,
+                                          nnrt_warp_field** out) {
+	NNRT_CHECK_ARG(nodes != nullptr, "nodes: null tensor");
+	const bool on_device = nodes->dl_tensor.device.device_type == kDLROCM;
+	const void* data = nullptr;
+	int64_t dims[2];
+	nnrt_status st = dl_check(nodes, "nodes", {F32}, 2, {-1, 3}, on_device ? Mem::device : Mem::host,
+	                          on_device ? nodes->dl_tensor.device.device_id : device, &data, dims);
+	if (st) return st;
+	NNRT_CHECK_ARG(dims[0] <= INT32_MAX, "nodes: too many nodes");
+	std::vector<float> host;
+	const float* h_nodes = static_cast<const float*>(data);
+	if (on_device) {
+		DeviceGuard guard(nodes->dl_tensor.device.device_id);
+		host.resize(3 * static_cast<size_t>(dims[0]));
+		NNRT_HIP(hipMemcpy(host.data(), data, sizeof(float) * host.size(), hipMemcpyDeviceToHost));
+		h_nodes = host.data();
+	}
+	return nnrt_warp_field_create(h_nodes, static_cast<int32_t>(dims[0]), node_coverage, threshold_nodes_by_distance, anchor_count,
+	                              minimum_valid_anchor_count, coverage_method, layer_count, max_vertex_degree, h_layer_radii, device, out);
+}
+
+nnrt_status nnrt_fitter_fit_to_image_dlpack(nnrt_fitter* ft, nnrt_warp_field* wf, const DLManagedTensor* vertices, const DLManagedTensor* normals,
+                                            const DLManagedTensor* faces, const DLManagedTensor* depth, const DLManagedTensor* mask,
+                                            const DLManagedTensor* K, const DLManagedTensor* E, float depth_scale, void* stream) {
+	NNRT_CHECK_ARG(ft && wf, "null handle");
+	const int dev = wf->device;
+	const void *pv, *pn, *pf, *pd, *pm = nullptr, *pk, *pe;
+	int64_t dv[2], dn[2], df[2], dd[2], dm[2], dk[2], de[2];
+	nnrt_status st;
+	if ((st = dl_check(vertices, "vertices", {F32}, 2, {-1, 3}, Mem::device, dev, &pv, dv))) return st;
+	if ((st = dl_check(normals, "normals", {F32}, 2, {dv[0], 3}, Mem::device, dev, &pn, dn))) return st;
+	if ((st = dl_check(faces, "faces", {I64}, 2, {-1, 3}, Mem::device, dev, &pf, df))) return st;
+	if ((st = dl_check(depth, "depth", {F32}, 2, {-1, -1}, Mem::device, dev, &pd, dd))) return st;
+	if (mask && (st = dl_check(mask, "mask", {B8, U8}, 2, {dd[0], dd[1]}, Mem::device, dev, &pm, dm))) return st;
+	if ((st = dl_check(K, "K", {F64}, 2, {3, 3}, Mem::host, dev, &pk, dk))) return st;
+	if ((st = dl_check(E, "E", {F64}, 2, {4, 4}, Mem::host, dev, &pe, de))) return st;
+	NNRT_CHECK_ARG(dd[0] <= INT32_MAX && dd[1] <= INT32_MAX, "depth: image too large");
+	return nnrt_fitter_fit_to_image(ft, wf, static_cast<const float*>(pv), static_cast<const float*>(pn), dv[0], static_cast<const int64_t*>(pf),
+	                                df[0], static_cast<const float*>(pd), static_cast<const uint8_t*>(pm), static_cast<int32_t>(dd[0]),
+	                                static_cast<int32_t>(dd[1]), static_cast<const double*>(pk), static_cast<const double*>(pe), depth_scale, stream);
 }
 
 } // extern "C"

@@ -585,3 +585,42 @@ def test_hierarchy_and_coverage_bit_exact(nn, oracle_mod, n, layers, degree, kin
     assert np.array_equal(wf.get_edge_layer_indices(), el_o)
     w_o = oracle_mod.node_coverage_weights(nodes, coverage)
     assert np.array_equal(wf.get_node_coverage_weights(), w_o[vidx_o])
+
+
+def test_dlpack_fit_matches_pointer_fit(nn, S, oracle_mod):
+    """include/nnrt_dlpack.h: torch-ROCm tensors lent through DLPack run the same fit as the pointer entry point (same
+    kernels, same inputs -> identical node motion); device / dtype mismatches are argument errors."""
+    import ctypes
+    from dynamicfuion_python_amd import _native
+    sc = _scene(S, oracle_mod, "S1")
+    depth = scene_target(oracle_mod, sc)
+    wf_p, _, _ = _gpu_fit(nn, sc, depth, 2, graph=False)
+    G, A = nn.geometry, nn.alignment
+    lib = _native.lib()
+    h = ctypes.c_void_p()
+    caps = []
+
+    def dl(x):
+        cap, ptr = _native.dlpack(x)
+        caps.append(cap)
+        return ptr
+
+    nodes_dev = torch.as_tensor(sc.nodes, device="cuda")
+    assert lib.nnrt_warp_field_create_dlpack(dl(nodes_dev), sc.coverage, 0, 4, 0, 0, sc.layer_count, 4, None, 0, ctypes.byref(h)) == 0
+    wf_d = G.HierarchicalGraphWarpField.__new__(G.HierarchicalGraphWarpField)
+    wf_d._h, wf_d.device, wf_d.node_count, wf_d.anchor_count = h, 0, len(sc.nodes), 4
+    ft = A.DeformableMeshToImageFitter(2, [A.IterationMode.ALL], preconditioning_dampening_factor=0.001, use_hip_graph=False)
+    dev = lambda a: torch.as_tensor(np.ascontiguousarray(a), device="cuda")  # noqa: E731
+    verts, nrms, faces = dev(sc.points.astype(np.float32)), dev(sc.normals.astype(np.float32)), dev(sc.faces.astype(np.int64))
+    dep = dev(depth.astype(np.float32))
+    K, E = np.ascontiguousarray(sc.K, np.float64), np.eye(4)
+    st = lib.nnrt_fitter_fit_to_image_dlpack(ft._h, h, dl(verts), dl(nrms), dl(faces), dl(dep), None, dl(K), dl(E), 1.0, None)
+    assert st == 0, lib.nnrt_last_error()
+    torch.cuda.synchronize()
+    assert np.array_equal(wf_d.get_node_translations(True), wf_p.get_node_translations(True))
+    assert np.array_equal(wf_d.get_node_rotations(True), wf_p.get_node_rotations(True))
+    # mismatches: int32 faces, host-resident vertices
+    st = lib.nnrt_fitter_fit_to_image_dlpack(ft._h, h, dl(verts), dl(nrms), dl(faces.to(torch.int32)), dl(dep), None, dl(K), dl(E), 1.0, None)
+    assert st == 1 and b"faces: unsupported dtype" in lib.nnrt_last_error()
+    st = lib.nnrt_fitter_fit_to_image_dlpack(ft._h, h, dl(verts.cpu()), dl(nrms), dl(faces), dl(dep), None, dl(K), dl(E), 1.0, None)
+    assert st == 1 and b"vertices: must be a ROCm device tensor" in lib.nnrt_last_error()

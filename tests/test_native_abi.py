@@ -10,13 +10,15 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "nnrt_mi355x.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("nnrt_mi355x.h", "nnrt_dlpack.h")]
 
 
 def _declared():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(nnrt_[a-z0-9_]+)\s*\(", text)))
+    names = set()
+    for header in HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", open(header).read(), flags=re.S)
+        names |= set(re.findall(r"\b(nnrt_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)
 
 
 @pytest.fixture(scope="module")
@@ -31,7 +33,8 @@ def test_header_declares_entry_points():
     names = _declared()
     assert len(names) >= 30
     for must in ("nnrt_fitter_fit_to_image", "nnrt_fitter_prepare", "nnrt_fitter_iterate", "nnrt_warp_field_create",
-                 "nnrt_rasterize_ndc_triangles", "nnrt_solve_block_sparse_arrowhead_cholesky"):
+                 "nnrt_rasterize_ndc_triangles", "nnrt_solve_block_sparse_arrowhead_cholesky", "nnrt_fitter_fit_to_image_dlpack",
+                 "nnrt_warp_field_create_dlpack"):
         assert must in names
 
 
@@ -39,7 +42,7 @@ def test_library_exports_every_declared_symbol(native):
     out = subprocess.check_output(["nm", "-D", "--defined-only", native.LIB_PATH], text=True)
     exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
     missing = [n for n in _declared() if n not in exported]
-    assert not missing, f"declared in include/nnrt_mi355x.h but not exported: {missing}"
+    assert not missing, f"declared in include/*.h but not exported: {missing}"
     # every exported nnrt_ symbol is declared (no undocumented ABI)
     extra = sorted(n for n in exported if n.startswith("nnrt_") and n not in _declared())
     assert not extra, f"exported but not declared: {extra}"
@@ -115,3 +118,29 @@ def test_missing_library_fails_loudly(native, monkeypatch, tmp_path):
     monkeypatch.setattr(native, "LIB_PATH", str(tmp_path / "absent.so"))
     with pytest.raises(RuntimeError, match="missing"):
         native.lib()
+
+
+def test_dlpack_entry_points_validate_tensors(native):
+    """include/nnrt_dlpack.h: dtype / shape / layout are checked on the host before any device work, and a valid tensor
+    is forwarded to the pointer entry point (whose own argument check then reports)."""
+    lib = native.lib()
+    out = ctypes.c_void_p()
+
+    def create(arr, anchor_count=4):
+        cap, ptr = native.dlpack(arr)
+        st = lib.nnrt_warp_field_create_dlpack(ptr, 0.05, 0, anchor_count, 0, 1, 1, 4, None, 0, ctypes.byref(out))
+        del cap
+        return st, lib.nnrt_last_error()
+
+    st, msg = create(np.zeros((2, 3), np.float64))
+    assert st == 1 and b"nodes: unsupported dtype" in msg
+    st, msg = create(np.zeros((2, 4), np.float32))
+    assert st == 1 and b"dimension 1 is 4, expected 3" in msg
+    st, msg = create(np.zeros((2, 3, 1), np.float32))
+    assert st == 1 and b"expected 2 dimensions" in msg
+    st, msg = create(np.zeros((6, 2), np.float32)[:, :1].reshape(-1))   # 1-D: rank error first
+    assert st == 1
+    st, msg = create(np.asfortranarray(np.zeros((4, 3), np.float32)))
+    assert st == 1 and b"not a compact row-major tensor" in msg
+    st, msg = create(np.zeros((2, 3), np.float32))   # valid tensor -> pointer entry point: anchor_count > node_count
+    assert st == 1 and b"Anchor count" in msg
