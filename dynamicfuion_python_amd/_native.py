@@ -125,6 +125,8 @@ _SIGNATURES = {
                                                 c_void_p]),
     "nnrt_fitter_fit_to_image_dlpack": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                                   c_float, c_void_p]),
+    "nnrt_rasterize_ndc_triangles_dlpack": (c_int32, [c_void_p, c_void_p, c_float, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                                      c_void_p, c_void_p]),
 }
 
 

@@ -1272,4 +1272,28 @@ nnrt_status nnrt_fitter_fit_to_image_dlpack(nnrt_fitter* ft, nnrt_warp_field* wf
 	                                static_cast<int32_t>(dd[1]), static_cast<const double*>(pk), static_cast<const double*>(pe), depth_scale, stream);
 }
 
+nnrt_status nnrt_rasterize_ndc_triangles_dlpack(const DLManagedTensor* face_ndc, const DLManagedTensor* clip_mask, float blur_radius_pixels,
+                                                int32_t perspective_correct_barycentric_coordinates, int32_t clip_barycentric_coordinates,
+                                                int32_t cull_back_faces, const DLManagedTensor* pixel_faces, const DLManagedTensor* depths,
+                                                const DLManagedTensor* barycentrics, const DLManagedTensor* distances, void* stream) {
+	NNRT_CHECK_ARG(face_ndc != nullptr, "face_ndc: null tensor");
+	const int dev = face_ndc->dl_tensor.device.device_id;
+	const void *pn, *pm = nullptr, *pf, *pd, *pb, *ps;
+	int64_t dn[3], dm[1], df[3], dd[3], db[4], ds[3];
+	nnrt_status st;
+	if ((st = dl_check(face_ndc, "face_ndc", {F32}, 3, {-1, 3, 3}, Mem::device, dev, &pn, dn))) return st;
+	if (clip_mask && (st = dl_check(clip_mask, "clip_mask", {B8, U8}, 1, {dn[0]}, Mem::device, dev, &pm, dm))) return st;
+	if ((st = dl_check(pixel_faces, "pixel_faces", {I64}, 3, {-1, -1, -1}, Mem::device, dev, &pf, df))) return st;
+	if ((st = dl_check(depths, "depths", {F32}, 3, {df[0], df[1], df[2]}, Mem::device, dev, &pd, dd))) return st;
+	if ((st = dl_check(barycentrics, "barycentrics", {F32}, 4, {df[0], df[1], df[2], 3}, Mem::device, dev, &pb, db))) return st;
+	if ((st = dl_check(distances, "distances", {F32}, 3, {df[0], df[1], df[2]}, Mem::device, dev, &ps, ds))) return st;
+	NNRT_CHECK_ARG(df[0] <= INT32_MAX && df[1] <= INT32_MAX && df[2] <= INT32_MAX, "pixel_faces: image too large");
+	DeviceGuard guard(dev);
+	return nnrt_rasterize_ndc_triangles(static_cast<const float*>(pn), static_cast<const uint8_t*>(pm), dn[0], static_cast<int32_t>(df[0]),
+	                                    static_cast<int32_t>(df[1]), blur_radius_pixels, static_cast<int32_t>(df[2]), -1, -1,
+	                                    perspective_correct_barycentric_coordinates, clip_barycentric_coordinates, cull_back_faces,
+	                                    static_cast<int64_t*>(const_cast<void*>(pf)), static_cast<float*>(const_cast<void*>(pd)),
+	                                    static_cast<float*>(const_cast<void*>(pb)), static_cast<float*>(const_cast<void*>(ps)), stream);
+}
+
 } // extern "C"

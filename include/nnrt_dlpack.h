@@ -66,6 +66,15 @@ nnrt_status nnrt_fitter_fit_to_image_dlpack(nnrt_fitter* fitter, nnrt_warp_field
                                             const DLManagedTensor* mask, const DLManagedTensor* K, const DLManagedTensor* E,
                                             float depth_scale, void* stream);
 
+/* nnrt.rendering.rasterize_ndc_triangles (cpp/pybind/rendering/rendering.cpp:36-43) == nnrt_rasterize_ndc_triangles:
+ * face_ndc float32 [F,3,3] and clip_mask bool / uint8 [F] (NULL: all faces) in; the caller-allocated fragment tensors
+ * pixel_faces int64 [H,W,Kf], depths float32 [H,W,Kf], barycentrics float32 [H,W,Kf,3], distances float32 [H,W,Kf]
+ * out (H, W, Kf = faces_per_pixel from pixel_faces' shape). All on one ROCm device (the face_ndc tensor's). */
+nnrt_status nnrt_rasterize_ndc_triangles_dlpack(const DLManagedTensor* face_ndc, const DLManagedTensor* clip_mask, float blur_radius_pixels,
+                                                int32_t perspective_correct_barycentric_coordinates, int32_t clip_barycentric_coordinates,
+                                                int32_t cull_back_faces, const DLManagedTensor* pixel_faces, const DLManagedTensor* depths,
+                                                const DLManagedTensor* barycentrics, const DLManagedTensor* distances, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

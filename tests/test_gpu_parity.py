@@ -624,3 +624,28 @@ def test_dlpack_fit_matches_pointer_fit(nn, S, oracle_mod):
     assert st == 1 and b"faces: unsupported dtype" in lib.nnrt_last_error()
     st = lib.nnrt_fitter_fit_to_image_dlpack(ft._h, h, dl(verts.cpu()), dl(nrms), dl(faces), dl(dep), None, dl(K), dl(E), 1.0, None)
     assert st == 1 and b"vertices: must be a ROCm device tensor" in lib.nnrt_last_error()
+
+
+@pytest.mark.parametrize("kf", [1, 4])
+def test_dlpack_rasterize_matches_binding(nn, oracle_mod, kf):
+    """nnrt_rasterize_ndc_triangles_dlpack writes the same fragments as nnrt.rendering.rasterize_ndc_triangles."""
+    from dynamicfuion_python_amd import _native
+    T = np.array([[-1, 0, 0, 0], [0, 1, 0, 0], [0, 0, -1, 1.2], [0, 0, 0, 1.]])
+    Pt, _, Ft = read_ply(os.path.join(FIXTURES, "plane_skin_25_nodes_target.ply"))
+    Pt = (Pt.astype(np.float64) @ T[:3, :3].T + T[:3, 3]).astype(np.float32)
+    K = np.array([[100.0, 0, 50], [0, 100.0, 50], [0, 0, 1]])
+    fndc, fm = oracle_mod.extract_face_ndc(Pt, Ft, K, 100, 100, 0.0, 10.0)
+    ref = nn.rendering.rasterize_ndc_triangles(fndc, fm, (100, 100), 0.5, kf, -1, -1, True, False, True)
+    nd, md = torch.as_tensor(fndc, device="cuda"), torch.as_tensor(fm.astype(np.bool_), device="cuda")
+    out = [torch.empty((100, 100, kf), dtype=torch.int64, device="cuda"), torch.empty((100, 100, kf), device="cuda"),
+           torch.empty((100, 100, kf, 3), device="cuda"), torch.empty((100, 100, kf), device="cuda")]
+    caps = [_native.dlpack(x) for x in [nd, md] + out]
+    lib = _native.lib()
+    st = lib.nnrt_rasterize_ndc_triangles_dlpack(caps[0][1], caps[1][1], 0.5, 1, 0, 1, *[c[1] for c in caps[2:]], None)
+    assert st == 0, lib.nnrt_last_error()
+    torch.cuda.synchronize()
+    for a, b in zip(out, ref):
+        assert np.array_equal(_np(a), _np(b))
+    bad = _native.dlpack(torch.empty((100, 100, kf, 2), device="cuda"))   # barycentrics with 2 components
+    st = lib.nnrt_rasterize_ndc_triangles_dlpack(caps[0][1], caps[1][1], 0.5, 1, 0, 1, caps[2][1], caps[3][1], bad[1], caps[5][1], None)
+    assert st == 1 and b"barycentrics: dimension 3 is 2, expected 3" in lib.nnrt_last_error()

@@ -144,3 +144,10 @@ def test_dlpack_entry_points_validate_tensors(native):
     assert st == 1 and b"not a compact row-major tensor" in msg
     st, msg = create(np.zeros((2, 3), np.float32))   # valid tensor -> pointer entry point: anchor_count > node_count
     assert st == 1 and b"Anchor count" in msg
+
+
+def test_dlpack_rasterize_rejects_host_tensors(native):
+    lib = native.lib()
+    caps = [native.dlpack(np.zeros((4, 3, 3), np.float32))] + [native.dlpack(np.zeros((8, 8, 1), dt)) for dt in (np.int64, np.float32)]
+    st = lib.nnrt_rasterize_ndc_triangles_dlpack(caps[0][1], None, 0.0, 1, 0, 1, caps[1][1], caps[2][1], caps[2][1], caps[2][1], None)
+    assert st == 1 and b"face_ndc: must be a ROCm device tensor" in lib.nnrt_last_error()
