@@ -5,12 +5,15 @@ Workload (BASELINE.json configs[1]): one 640x480 synthetic de
 (50x30, node coverage 0.03, 4 anchors, block-diagonal solve), a 321x241 grid mesh (77,361 vertices, 153,600
 triangles). The target depth is the mesh rendered under a smooth ground-truth motion; random-free, seed = rank.
 
-A step = restore the identity warp (R = I, t = 0) + one full GN iteration (warp, rasterize, residuals, Jacobians,
-JtJ / Jt r, LM block solve, Rodrigues update); --graph-steps (default 10, C2's GN iterations per frame) steps are
-captured as one hipGraph and replayed as one launch, the way FitToImage replays its iteration loop (the timed step count
-is rounded up to a whole number of launches). The reference's own block-diagonal GN diverges
-on multi-node scenes after 2-3 iterations (SURVEY.md / DESIGN.md section "Divergence"), so every step starts from the
-same state: each timed iteration does the work of the first iteration of a frame, with nothing cached between steps.
+A step = restore a stored mid-motion node state (half the ground-truth motion: non-identity R/t, a deformed mesh) by a
+device copy + one full GN iteration through the general kernels (warp, rasterize, residuals, Jacobians, JtJ / Jt r, LM
+block solve, Rodrigues update); --graph-steps (default 10, C2's GN iterations per frame) steps are captured as one
+hipGraph and replayed as one launch, the way FitToImage replays its iteration loop (the timed step count is rounded up
+to a whole number of launches). Every step does the same work, with nothing cached between steps. The reference's own
+C2 trajectory cannot be timed as a 10-iteration loop: its block-diagonal GN (A17) raises potrf at iteration 2 on C2, on
+the GPU and in the oracle alike (tests/test_gpu_parity.py TRAJECTORIES). --step frame (whole frame fits from the
+identity warp, for configs whose trajectory survives, e.g. C2_ARAP) and --step identity (the first iteration of a frame)
+are the alternatives.
 
 N > 1: one process per GPU (torchrun), each fitting its own independent sequence (seed = rank) -- replicas, no
 collective in the data path; the only collectives are the barrier, the max-over-ranks of the elapsed time and the
@@ -52,6 +55,36 @@ def max_over_ranks(value: float, device=None) -> float:
     t = torch.tensor([float(value)], dtype=torch.float64, device=device if device is not None else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def timed_region(step, launches: int, per_launch: int, world: int, sync) -> tuple:
+    """The timed protocol: barrier + device sync, `launches` x step(per_launch), device sync, barrier. Returns (OR of
+    the step return codes, this rank's elapsed seconds)."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    bad = 0
+    for _ in range(launches):
+        bad |= step(per_launch)
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    return bad, elapsed
+
+
+def exchange_per_rank(steps: int, elapsed: float, update_norm: float, device=None):
+    """End-of-run all-gather of per-rank (iterations/s, seconds, final |update|); None at N = 1."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return None
+    mine = torch.tensor([steps / elapsed, elapsed, update_norm], dtype=torch.float64, device=device if device is not None else "cpu")
+    got = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(got, mine)
+    return [dict(rank=i, iters_per_s=float(g[0]), seconds=float(g[1]), update_norm=float(g[2])) for i, g in enumerate(got)]
 
 
 def aggregate(steps: int, elapsed_s: float, world: int) -> dict:
@@ -132,10 +165,15 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default=DEFAULT_CONFIG, help="synthetic workload (dynamicfuion_python_amd.synthetic.CONFIGS)")
+    ap.add_argument("--step", choices=("frame", "snapshot", "identity"), default="snapshot",
+                    help="snapshot: one GN iteration per step from a mid-motion node state (general kernels); frame: "
+                         "--graph-steps-iteration frame fits from the identity warp (FitToImage's loop; raises potrf on C2, "
+                         "as the reference does); identity: the first iteration of a frame per step")
     ap.add_argument("--timed-steps", type=int, default=100, help="eager per-stage HIP-event timing steps (roofline)")
     ap.add_argument("--graph-steps", type=int, default=10, help="steps per captured graph launch (C2: 10 GN iterations per frame)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU-baseline sample (loop-body seconds)")
-    ap.add_argument("--cpu-threads", type=int, default=16, help="OpenMP threads for the CPU baseline (the box's CPU share)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="OpenMP threads for the CPU baseline (0: this process's CPU share, see cpu_threads_default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch of the roofline kernel (tools/pmc_traffic.py output)")
@@ -186,42 +224,62 @@ def host_cpu():
     return dict(model=model, sockets=len(sockets) or None, logical_cpus=os.cpu_count())
 
 
-def cpu_baseline(sc, depth_host, threads: int, budget_s: float, single_thread_s: float = 4.0):
+def cpu_baseline(sc, depth_host, threads: int, budget_s: float, step: str, iterations: int, R0=None, t0=None, single_thread_s: float = 4.0):
     """The oracle (C++/OpenMP restatement of the reference CPU path; test infrastructure, used here only as the
-    reported baseline) running the same step: 1 GN iteration from the identity warp. Timed = loop body S1-S12
-    (DeformableMeshToImageFitter.cpp:111-275), once-per-frame setup excluded, as in the GPU step. Run with `threads`
-    OpenMP threads (the headline) and again with 1 thread on a smaller sample."""
+    reported baseline) running the same steps as the GPU: `step` = "frame" -> `iterations`-iteration FitToImage loops from
+    the identity warp; "snapshot" -> one GN iteration from the node state (R0, t0); "identity" -> one GN iteration from
+    the identity warp. Timed = loop body S1-S12 (DeformableMeshToImageFitter.cpp:111-275), once-per-frame setup
+    excluded, as in the GPU step. Run with `threads` OpenMP threads (the headline) and again with 1 thread."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     refp, refm = O.unproject(depth_host, sc.K, 1.0, 10.0)
-    res = _cpu_sample(O, sc, refp, refm, threads, budget_s)
-    one = _cpu_sample(O, sc, refp, refm, 1, single_thread_s)
+    res = _cpu_sample(O, sc, refp, refm, threads, budget_s, step, iterations, R0, t0)
+    one = _cpu_sample(O, sc, refp, refm, 1, single_thread_s, step, iterations, R0, t0)
     res["single_thread"] = dict(value=one["value"], unit=one["unit"], cores=1, ms_per_solve=one["ms_per_solve"],
                                 sample=one["sample"])
     res["host"] = host_cpu()
     return res
 
 
-def _cpu_sample(O, sc, refp, refm, threads: int, budget_s: float):
+def _cpu_sample(O, sc, refp, refm, threads: int, budget_s: float, step: str, iterations: int, R0, t0):
     O.set_num_threads(threads)
     N = len(sc.nodes)
-    R0 = np.tile(np.eye(3, dtype=np.float32), (N, 1, 1))
-    t0 = np.zeros((N, 3), np.float32)
+    if step != "snapshot" or R0 is None:
+        R0 = np.tile(np.eye(3, dtype=np.float32), (N, 1, 1))
+        t0 = np.zeros((N, 3), np.float32)
+    per_call = iterations if step == "frame" else 1
+    h = sc.hierarchy
+    hk = {}
+    nodes = sc.nodes
+    if h:   # the fit runs in virtual node order (the synthetic scenes are pre-sorted: identity permutation)
+        nodes = sc.nodes[h["virtual_indices"]]
+        hk = dict(edges=h["edges"], edge_layers=h["edge_layers"], radii=h["radii"], first_layer_count=int(h["layer_counts"][0]))
     body = solve = 0.0
-    iters = 0
+    iters = calls = 0
     wall0 = time.perf_counter()
-    while body < budget_s and time.perf_counter() - wall0 < 3 * budget_s:
-        _, _, dg = O.fit(nodes=sc.nodes, rotations=R0, translations=t0, mesh_points=sc.points, mesh_normals=sc.normals, faces=sc.faces,
-                         ref_points=refp, ref_mask=refm, H=sc.H, W=sc.W, K=sc.K, max_iterations=1, lm_factor=0.001, coverage=sc.coverage)
-        if iters > 0:   # first call warms caches / page-ins
+    while (body < budget_s and time.perf_counter() - wall0 < 3 * budget_s) or calls < 2:
+        _, _, dg = O.fit(nodes=nodes, rotations=R0, translations=t0, mesh_points=sc.points, mesh_normals=sc.normals, faces=sc.faces,
+                         ref_points=refp, ref_mask=refm, H=sc.H, W=sc.W, K=sc.K, max_iterations=per_call, lm_factor=0.001,
+                         coverage=sc.coverage, **hk)
+        if calls > 0:   # first call warms caches / page-ins
             body += dg["stage_seconds"][7]
             solve += dg["stage_seconds"][5]
-        iters += 1
-    n = max(iters - 1, 1)
-    return dict(value=n / body if body > 0 else None, unit="GN iters/s", cores=O.num_threads(), kind="port",
-                ms_per_solve=1000.0 * solve / n,
-                sample=f"{sc.name}: {n} single GN iterations from the identity warp (loop body timed, setup excluded), "
-                       f"oracle/ C++ OpenMP restatement, fast K=1 raster")
+            iters += per_call
+        calls += 1
+    what = {"frame": f"{iters // per_call} {per_call}-iteration frame fits from the identity warp",
+            "snapshot": f"{iters} single GN iterations from the mid-motion node state",
+            "identity": f"{iters} single GN iterations from the identity warp"}[step]
+    return dict(value=iters / body if body > 0 else None, unit="GN iters/s", cores=O.num_threads(), kind="port",
+                ms_per_solve=1000.0 * solve / max(iters, 1),
+                sample=f"{sc.name}: {what} (loop body timed, setup excluded), oracle/ C++ OpenMP restatement, fast K=1 raster")
+
+
+def cpu_threads_default() -> int:
+    """The CPU share of this process: its scheduler affinity, capped by OMP_NUM_THREADS when the environment sets it
+    (the GPU box sets 16 = one GPU's share of the host, while the affinity mask spans the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff
 
 
 def main(argv=None):
@@ -248,14 +306,18 @@ def main(argv=None):
     arap = sc.layer_count > 1
     P, F, V, Nn = sc.H * sc.W, len(sc.faces), len(sc.points), len(sc.nodes)
     solve_kind = f"{sc.layer_count}-layer ARAP arrowhead LM solve" if arap else "block-diagonal LM solve"
-    workload = (f"{sc.name}: {sc.W}x{sc.H} depth, {Nn}-node graph, {V}-vertex/{F}-triangle mesh, {solve_kind}, "
-                f"1 GN iteration per step from the identity warp")
+    step_desc = {"frame": f"FitToImage loop: {min(args.graph_steps, args.steps)}-iteration frame fits from the identity warp, "
+                          f"1 GN iteration per step",
+                 "snapshot": "1 GN iteration per step from a mid-motion node state (half the ground-truth motion)",
+                 "identity": "1 GN iteration per step from the identity warp"}[args.step]
+    workload = f"{sc.name}: {sc.W}x{sc.H} depth, {Nn}-node graph, {V}-vertex/{F}-triangle mesh, {solve_kind}, {step_desc}"
+
     log(f"rank {rank}/{world} on {torch.cuda.get_device_name(dev)}: {workload}")
 
     depth = render_target(sc, G, Rr)
     wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE,
                                       sc.layer_count)
-    ft = A.DeformableMeshToImageFitter(1, [A.IterationMode.ALL], preconditioning_dampening_factor=0.001, use_hip_graph=True)
+    ft = A.DeformableMeshToImageFitter(1, [A.IterationMode.ALL], preconditioning_dampening_factor=0.001, use_hip_graph=A.GRAPH_ALWAYS)
     mesh = G.TriangleMesh(sc.points, sc.normals, sc.faces)
     ft.prepare(wf, mesh, depth, None, sc.K)
 
@@ -264,56 +326,80 @@ def main(argv=None):
     s_ptr = NV.stream_ptr(stream)
     wf_h, ft_h = wf.handle, ft._h
 
-    # One launch = GRAPH_STEPS steps: a hipGraph of GRAPH_STEPS x (reset to the identity warp + one GN iteration), the
-    # way FitToImage replays its iteration loop (C2: 10 GN iterations per frame) as one captured graph.
+    # Step kinds (every one runs the real GN iteration kernels of FitToImage's loop body, :111-275):
+    #   frame    -- one launch = one whole frame fit of --graph-steps iterations (C2: the 10-iteration FitToImage loop)
+    #               from the identity warp: the motion is restored once per frame, iterations 2..10 run the general
+    #               (non-identity R/t) kernels on the deformed mesh; one hipGraph per frame.
+    #   snapshot -- every step restores a mid-motion node state (half the ground-truth motion, sc.partial_motion(0.5))
+    #               and runs one GN iteration through the general kernels (non-identity R/t, deformed mesh; constant
+    #               work per step). The reference's own C2 trajectory cannot serve: its block-diagonal GN (A17) raises
+    #               potrf at iteration 2 on C2 (tests/test_gpu_parity.py TRAJECTORIES), so a 10-iteration C2 frame fit
+    #               does not exist in the reference either.
+    #   identity -- every step is the first GN iteration from the identity warp (identity-specialised warp / update).
     per_launch = max(1, min(args.graph_steps, args.steps))
+    if args.step == "snapshot":
+        R_mid, t_mid = sc.partial_motion(0.5)
+        wf.set_node_rotations(R_mid)
+        wf.set_node_translations(t_mid)
+    ft.snapshot_motion(wf)   # the state every step (snapshot) or every frame (frame) restarts from
+    R1, t1 = wf.get_node_rotations(True), wf.get_node_translations(True)   # (virtual order) for the CPU baseline
 
     def step(n):
+        if args.step == "frame":
+            return lib.nnrt_fitter_fit_from_snapshot(ft_h, wf_h, n, s_ptr)
+        if args.step == "snapshot":
+            return lib.nnrt_fitter_iterate_from_snapshot(ft_h, wf_h, 0, n, s_ptr)
         return lib.nnrt_fitter_iterate_from_identity(ft_h, wf_h, 0, n, s_ptr)
 
-    # warmup (first call captures the iteration graph)
+    # warmup (graphs are captured on first use: use_hip_graph = 2)
     for _ in range(max(1, args.warmup // per_launch)):
         if step(per_launch):
             NV.check(1)
     torch.cuda.synchronize(dev)
     ft.check()
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    bad = 0
     launches = -(-args.steps // per_launch)
     args.steps = launches * per_launch   # whole graphs only: the timed step count is rounded up to a multiple
-    for _ in range(launches):
-        bad |= step(per_launch)
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
+    bad, elapsed = timed_region(step, launches, per_launch, world, lambda: torch.cuda.synchronize(dev))
     if bad:
         NV.check(bad)
     ft.check()   # solver failure flag (potrf) -> raises
     elapsed_max = max_over_ranks(elapsed, dev)
     agg = aggregate(args.steps, elapsed_max, world)
+    final_t = wf.get_node_translations()
+    if not np.isfinite(final_t).all():
+        raise SystemExit("non-finite node motion after the timed steps")
 
-    # per-stage device time (eager launches, HIP events on the fitter's work stream), same step
+    # per-stage device time (eager launches, HIP events on the fitter's work stream) over the same iterations as the
+    # timed steps (a frame's iterations for "frame", the restored iteration otherwise), one iteration at a time so that
+    # each iteration's algorithmic bytes use its own association count E
+    anchors, _ = ft.anchors(V, 4)
     stages = {k: 0.0 for k in A.TIMED_STAGES}
-    for _ in range(args.timed_steps):
-        wf.reset_motion()
-        r = ft.iterate_timed(wf, 0, 1)
-        for k in stages:
-            stages[k] += r[k] / args.timed_steps
+    samples = []   # (E, contributing pixels) per timed iteration
+    while len(samples) < args.timed_steps:
+        if args.step == "identity":
+            wf.reset_motion()
+            its = [0]
+        elif args.step == "snapshot":
+            ft.restore_motion(wf)
+            its = [0]
+        else:
+            ft.restore_motion(wf)
+            its = list(range(per_launch))
+        for it in its:
+            r = ft.iterate_timed(wf, it, 1)
+            for k in stages:
+                stages[k] += r[k]
+            dg = ft.diagnostics()
+            if not (np.isfinite(dg["updates"]).all() and np.abs(dg["updates"]).max() > 0):
+                raise SystemExit(f"non-finite or empty GN update at iteration {it + 1} of the timed configuration")
+            samples.append((count_associations(dg["pixel_faces"], dg["residual_mask"], sc.faces, anchors), int(dg["residual_mask"].sum())))
+    for k in stages:
+        stages[k] /= len(samples)
     ft.check()
 
-    # sanity: the measured iteration produced a finite, non-zero update (parity itself is tests/test_gpu_parity.py)
-    dg = ft.diagnostics()
-    if not (np.isfinite(dg["updates"]).all() and np.abs(dg["updates"]).max() > 0):
-        raise SystemExit("non-finite or empty GN update in the timed configuration")
-
-    anchors, _ = ft.anchors(V, 4)
-    E = count_associations(dg["pixel_faces"], dg["residual_mask"], sc.faces, anchors)
-    P_c = int(dg["residual_mask"].sum())
+    E = int(round(np.mean([e for e, _ in samples])))
+    P_c = int(round(np.mean([p for _, p in samples])))
     sb = stage_bytes(P, F, V, Nn, 4, E)
     kernels = {}
     for stage, kname in STAGE_KERNEL.items():
@@ -352,12 +438,7 @@ def main(argv=None):
     setup_ms = (time.perf_counter() - t_setup) * 1000.0
 
     # end-of-run exchange of per-rank results: iterations/s, seconds, final |update|
-    per_rank = None
-    if world > 1:
-        mine = torch.tensor([args.steps / elapsed, elapsed, float(np.linalg.norm(dg["updates"]))], dtype=torch.float64, device=dev)
-        got = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(got, mine)
-        per_rank = [dict(rank=i, iters_per_s=float(g[0]), seconds=float(g[1]), update_norm=float(g[2])) for i, g in enumerate(got)]
+    per_rank = exchange_per_rank(args.steps, elapsed, float(np.linalg.norm(dg["updates"])), dev)
 
     out = {
         "metric": "GN iters/sec (640x480, 1.5k-node graph)" if args.config == "C2" else f"GN iters/sec ({args.config})",
@@ -374,14 +455,15 @@ def main(argv=None):
         "dtype": "f32",
         "data": "synthetic (smooth grid mesh + GT node motion rendered to depth; seed = rank)",
         "config": {"workload": workload, "config": args.config, "frame": [sc.H, sc.W], "nodes": Nn, "vertices": V, "triangles": F,
-                   "anchors": 4, "iteration_mode": "ALL", "lm_damping": 0.001, "hip_graph": True, "steps_per_graph": per_launch,
+                   "anchors": 4, "iteration_mode": "ALL", "lm_damping": 0.001, "hip_graph": True, "steps_per_graph": per_launch, "step": args.step,
                    "parallelism": f"replicas{world}" if world > 1 else "single"},
         "setup_ms": round(setup_ms, 3),
         "stage_ms": {k: round(v, 5) for k, v in stages.items()},
         "roofline": {"kernel": ROOFLINE_KERNEL, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "algorithmic_bytes": kbytes, "kernel_ms": k_ms,
                      "bytes_formula": "SURVEY.md 8(d): pixel-anchor Jacobians + JtJ/Jtr rows (P*257 + P*72K + 4E + E*28 + P*5 + 168N)",
-                     "associations_E": E, "contributing_pixels": P_c, "traffic_source": traffic_src,
+                     "associations_E": E, "contributing_pixels": P_c,
+                     "associations_note": "E and contributing pixels averaged over the timed iterations", "traffic_source": traffic_src,
                      "compulsory_bytes": node_pass_compulsory_bytes(P, P_c, F, V, Nn, 4),
                      "iteration_algorithmic_bytes": it_bytes,
                      "iteration_frac": it_bytes / (agg["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS},
@@ -393,9 +475,12 @@ def main(argv=None):
     if corner is not None:   # ARAP configs: the dense corner (MFMA-bound) is the dominant stage; the HBM one moves aside
         out["hbm_roofline"] = out["roofline"]
         out["roofline"] = corner
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not arap:
-        log(f"GPU: {agg['value']:.1f} it/s; running the CPU baseline sample (~{args.cpu_seconds:.0f} s)")
-        out["cpu_baseline"] = cpu_baseline(sc, depth.cpu().numpy(), args.cpu_threads, args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or cpu_threads_default()
+        log(f"GPU: {agg['value']:.1f} it/s; running the CPU baseline sample (~{args.cpu_seconds:.0f} s, {threads} threads)")
+        out["cpu_baseline"] = cpu_baseline(sc, depth.cpu().numpy(), threads, args.cpu_seconds, args.step, per_launch, R1, t1)
+        out["cpu_baseline"]["host"]["sched_affinity"] = len(os.sched_getaffinity(0))
+        out["cpu_baseline"]["host"]["omp_num_threads_env"] = os.environ.get("OMP_NUM_THREADS")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

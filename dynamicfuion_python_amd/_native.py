@@ -70,6 +70,11 @@ _SIGNATURES = {
                                                  c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
     "nnrt_fitter_iterate": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "nnrt_fitter_iterate_from_identity": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
+    "nnrt_fitter_graph_count": (c_int32, [c_void_p]),
+    "nnrt_fitter_fit_from_snapshot": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p]),
+    "nnrt_fitter_restore_motion": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "nnrt_fitter_snapshot_motion": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "nnrt_fitter_iterate_from_snapshot": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p]),
     "nnrt_fitter_iterate_timed": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     "nnrt_fitter_check": (c_int32, [c_void_p, c_void_p]),
     "nnrt_fitter_get_diagnostics": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -161,13 +166,15 @@ def lib():
 
 
 class NnrtError(RuntimeError):
-    pass
+    def __init__(self, message: str, status: int = -1):
+        super().__init__(message)
+        self.status = status
 
 
 def check(status: int):
     if status != 0:
         msg = lib().nnrt_last_error()
-        raise NnrtError(f"nnrt status {status}: {msg.decode() if msg else ''}")
+        raise NnrtError(f"nnrt status {status}: {msg.decode() if msg else ''}", status)
 
 
 def require_gpu():

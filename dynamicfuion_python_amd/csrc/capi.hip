@@ -4,6 +4,7 @@
 // prepare() time, nothing in the iteration synchronizes with the host or allocates, so one GN iteration per iteration
 // mode is captured into a hipGraph and replayed (the reference's per-stage host syncs: SURVEY.md section 3 CS-1).
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -17,6 +18,7 @@ namespace nnrt {
 
 namespace {
 thread_local std::string g_error;
+std::atomic<uint64_t> g_next_warp_field_id{1};
 }
 void set_error(const std::string& message) { g_error = message; }
 const std::string& get_error() { return g_error; }
@@ -134,7 +136,7 @@ struct nnrt_warp_field {
 	DeviceBuffer<int32_t> edges;           // [E,2]
 	DeviceBuffer<int8_t> edge_layers;      // [E]
 	DeviceBuffer<float> radii;             // [layers]
-	uint64_t version = 0;                  // bumped when device buffers are re-allocated
+	uint64_t id = 0;                       // unique per created warp field (a fitter's cached graphs capture its buffers)
 	int E() const { return static_cast<int>(h.edge_layers.size()); }
 };
 
@@ -198,6 +200,7 @@ nnrt_status nnrt_warp_field_create(const float* h_nodes, int32_t node_count, flo
 	DeviceGuard guard(device);
 	auto wf = std::make_unique<nnrt_warp_field>();
 	wf->device = device;
+	wf->id = g_next_warp_field_id.fetch_add(1);
 	wf->N = node_count;
 	wf->coverage = node_coverage;
 	wf->threshold = threshold_nodes_by_distance;
@@ -353,7 +356,7 @@ struct nnrt_fitter {
 	int H = 0, W = 0, N = 0, K = 0, E = 0;
 	bool prepared = false;
 	const nnrt_warp_field* wf = nullptr;
-	uint64_t wf_version = 0;
+	uint64_t wf_id = 0;   // id of the warp field whose buffers the cached graphs captured
 	// frame constants
 	NdcSetup ndc{};
 	Camera pix{};
@@ -381,8 +384,12 @@ struct nnrt_fitter {
 	ArrowheadWorkspace aw;
 	int n0 = 0;
 	int last_mode = 0;
-	// graphs: one per iteration sequence (the modes of the `count` iterations of an iterate() call, and whether each
-	// restarts from the identity warp), captured once and replayed as ONE launch; the most recent few are kept
+	DeviceBuffer<float> snapshot;   // [N,16] node state stored by nnrt_fitter_snapshot_motion (restore-before-iteration runs)
+	bool snapshot_valid = false;    // cleared by prepare() (the warp field or the node count may have changed)
+	// graphs: one per iteration sequence (the modes of the `count` iterations of an iterate() call, and what each
+	// iteration restarts from: RESET_NONE / RESET_IDENTITY / RESET_SNAPSHOT), captured once and replayed as ONE launch; the
+	// most recent few are kept. exec == nullptr records a sequence that ran eagerly once (use_hip_graph = 1 captures a
+	// sequence on its second request only, so a sequence launched once per frame never pays capture + instantiate).
 	struct SeqGraph {
 		std::vector<int> modes;
 		int reset = 0;
@@ -627,6 +634,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	NNRT_CHECK_ARG(V > 0 && F > 0 && H > 0 && W > 0, "empty mesh or image");
 	NNRT_CHECK_ARG(V < (int64_t(1) << 31) && F < (int64_t(1) << 31), "mesh too large for int32 indexing");
 	NNRT_CHECK_ARG(ref.depth_scale > 0.f, "depth_scale must be positive");
+	NNRT_CHECK_ARG(wf->device == ft->device, "the warp field and the fitter live on different devices");
 	DeviceGuard guard(ft->device);
 	hipStream_t us = static_cast<hipStream_t>(stream);
 	const int64_t P = static_cast<int64_t>(H) * W;
@@ -719,7 +727,15 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 		ft->aw.edge_list = ft->a_list.ptr;
 	}
 	const auto after = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->a_schur.ptr);
-	if (before != after || ft->wf != wf || ft->V != V || ft->F != F || ft->H != H || ft->W != W || ft->N != N || ft->K != K) ft->drop_graphs();
+	// Captured graphs bake every buffer pointer and the per-frame constants (NDC setup, pixel camera, extrinsics) into
+	// their kernel arguments: any change drops them. The warp field is recognised by its unique id, not its address.
+	const NdcSetup nndc = make_ndc_setup(h_K, H, W, ft->p.ndc_convention == NNRT_NDC_CONSISTENT);
+	const Camera npix = pixel_camera(h_K);
+	const WarpExtrinsics ne = make_extrinsics(h_E);
+	if (before != after || ft->wf != wf || ft->wf_id != wf->id || ft->V != V || ft->F != F || ft->H != H || ft->W != W || ft->N != N ||
+	    ft->K != K || std::memcmp(&nndc, &ft->ndc, sizeof(nndc)) != 0 || std::memcmp(&npix, &ft->pix, sizeof(npix)) != 0 ||
+	    std::memcmp(&ne, &ft->extr, sizeof(ne)) != 0)
+		ft->drop_graphs();
 	ft->V = V;
 	ft->F = F;
 	ft->H = H;
@@ -727,11 +743,11 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	ft->N = N;
 	ft->K = K;
 	ft->wf = wf;
-	ft->ndc = make_ndc_setup(h_K, H, W, ft->p.ndc_convention == NNRT_NDC_CONSISTENT);
-	ft->pix = pixel_camera(h_K);
-	const WarpExtrinsics ne = make_extrinsics(h_E);
-	if (std::memcmp(&ne, &ft->extr, sizeof(ne)) != 0) ft->drop_graphs();
+	ft->wf_id = wf->id;
+	ft->ndc = nndc;
+	ft->pix = npix;
 	ft->extr = ne;
+	ft->snapshot_valid = false;
 	// order the work stream after the caller's stream
 	NNRT_HIP(hipEventRecord(ft->ev_in, us));
 	NNRT_HIP(hipStreamWaitEvent(ft->work, ft->ev_in, 0));
@@ -785,45 +801,81 @@ nnrt_status nnrt_fitter_prepare_point_cloud(nnrt_fitter* ft, nnrt_warp_field* wf
 
 namespace {
 constexpr int MAX_GRAPH_ITERATIONS = 64;   // iterations per captured sequence graph (longer runs replay several)
-constexpr size_t MAX_CACHED_GRAPHS = 4;
+constexpr size_t MAX_CACHED_GRAPHS = 8;
+// what the iterations of a sequence restart from: nothing; the identity warp (every iteration); the stored snapshot (every
+// iteration); the stored snapshot before the first iteration of the call only (a whole frame fit from a stored state)
+enum { RESET_NONE = 0, RESET_IDENTITY = 1, RESET_SNAPSHOT = 2, RESET_SNAPSHOT_FIRST = 3 };
 
 // reset folded into the iteration's warp / update kernels where they support it (no ARAP state reads, <= 4 anchors)
 bool fold_reset(const nnrt_fitter* ft) { return ft->E == 0 && ft->K <= 4; }
 
+nnrt_status check_frame(const nnrt_fitter* ft, const nnrt_warp_field* wf, const char* who) {
+	if (!ft->prepared || ft->wf != wf || ft->wf_id != wf->id) {
+		set_error(std::string("nnrt_fitter_prepare must be called with this warp field before ") + who);
+		return NNRT_ERROR_ARGUMENT;
+	}
+	if (wf->device != ft->device) {
+		set_error("the warp field and the fitter live on different devices");
+		return NNRT_ERROR_ARGUMENT;
+	}
+	return NNRT_OK;
+}
+
+// what one iteration of a sequence restarts from, enqueued on s (inside or outside a capture)
+nnrt_status enqueue_restart(nnrt_fitter* ft, nnrt_warp_field* wf, int reset, bool folded, hipStream_t s) {
+	if (reset == RESET_IDENTITY && !folded) {
+		k_reset_motion<<<static_cast<unsigned>(ceil_div(wf->N, 256)), 256, 0, s>>>(wf->state.ptr, wf->N);
+		if (hipGetLastError() != hipSuccess) {
+			set_error("kernel launch failed (k_reset_motion)");
+			return NNRT_ERROR_HIP;
+		}
+	} else if (reset == RESET_SNAPSHOT || reset == RESET_SNAPSHOT_FIRST) {
+		NNRT_HIP(hipMemcpyAsync(wf->state.ptr, ft->snapshot.ptr, sizeof(float) * NODE_STRIDE * wf->N, hipMemcpyDeviceToDevice, s));
+	}
+	return NNRT_OK;
+}
+
+int restart_of(int reset, bool first_of_call) {
+	return reset == RESET_SNAPSHOT_FIRST ? (first_of_call ? RESET_SNAPSHOT : RESET_NONE) : reset;
+}
+
 nnrt_status iterate_impl(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_iteration, int32_t count, int reset, hipStream_t us) {
 	nnrt_status st;
-	const bool folded = reset && fold_reset(ft);
-	if (!ft->p.use_hip_graph) {
-		for (int it = first_iteration; it < first_iteration + count; it++) {
-			const int mode = ft->p.iteration_modes[it % ft->p.iteration_mode_count];
-			ft->last_mode = mode;
-			if (reset && !folded) {
-				k_reset_motion<<<static_cast<unsigned>(ceil_div(wf->N, 256)), 256, 0, us>>>(wf->state.ptr, wf->N);
-				NNRT_LAUNCH_CHECK();
-			}
-			if ((st = enqueue_iteration(ft, wf, mode, us, nullptr, folded))) return st;
-		}
-		return NNRT_OK;
-	}
-	// Graphs are captured on the fitter's private stream (capture needs a non-legacy stream) and replayed on the
-	// caller's: a whole run of iterations is one launch.
+	const bool folded = reset == RESET_IDENTITY && fold_reset(ft);
 	for (int it0 = first_iteration; it0 < first_iteration + count; it0 += MAX_GRAPH_ITERATIONS) {
 		const int n = std::min(MAX_GRAPH_ITERATIONS, first_iteration + count - it0);
 		std::vector<int> modes(static_cast<size_t>(n));
 		for (int i = 0; i < n; i++) modes[static_cast<size_t>(i)] = ft->p.iteration_modes[(it0 + i) % ft->p.iteration_mode_count];
 		ft->last_mode = modes.back();
-		hipGraphExec_t exec = nullptr;
+		// a sequence graph is keyed by its modes and by what each of its iterations restarts from
+		const int key_reset = reset == RESET_SNAPSHOT_FIRST && it0 != first_iteration ? RESET_NONE : reset;
+		nnrt_fitter::SeqGraph* seen = nullptr;
 		for (auto& g : ft->graphs)
-			if (g.reset == reset && g.modes == modes) exec = g.exec;
-		if (!exec) {
+			if (g.reset == key_reset && g.modes == modes) seen = &g;
+		const bool capture = ft->p.use_hip_graph == NNRT_GRAPH_ALWAYS || (ft->p.use_hip_graph == NNRT_GRAPH_AUTO && seen != nullptr);
+		if (!capture) {
+			// eager launches on the caller's stream
+			for (int i = 0; i < n; i++) {
+				if ((st = enqueue_restart(ft, wf, restart_of(reset, it0 + i == first_iteration), folded, us))) return st;
+				if ((st = enqueue_iteration(ft, wf, modes[static_cast<size_t>(i)], us, nullptr, folded))) return st;
+			}
+			if (ft->p.use_hip_graph == NNRT_GRAPH_AUTO && !seen) {
+				if (ft->graphs.size() >= MAX_CACHED_GRAPHS) {
+					if (ft->graphs.front().exec) hipGraphExecDestroy(ft->graphs.front().exec);
+					ft->graphs.erase(ft->graphs.begin());
+				}
+				ft->graphs.push_back({modes, key_reset, nullptr});
+			}
+			continue;
+		}
+		// Graphs are captured on the fitter's private stream (capture needs a non-legacy stream) and replayed on the
+		// caller's: a whole run of iterations is one launch.
+		if (!seen || !seen->exec) {
 			hipGraph_t g = nullptr;
 			NNRT_HIP(hipStreamBeginCapture(ft->work, hipStreamCaptureModeThreadLocal));
 			st = NNRT_OK;
 			for (int i = 0; i < n && !st; i++) {
-				if (reset && !folded) {
-					k_reset_motion<<<static_cast<unsigned>(ceil_div(wf->N, 256)), 256, 0, ft->work>>>(wf->state.ptr, wf->N);
-					if (hipGetLastError() != hipSuccess) st = NNRT_ERROR_HIP;
-				}
+				st = enqueue_restart(ft, wf, restart_of(reset, it0 + i == first_iteration), folded, ft->work);
 				if (!st) st = enqueue_iteration(ft, wf, modes[static_cast<size_t>(i)], ft->work, nullptr, folded);
 			}
 			hipError_t ce = hipStreamEndCapture(ft->work, &g);
@@ -833,16 +885,22 @@ nnrt_status iterate_impl(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_ite
 				return st;
 			}
 			NNRT_HIP(ce);
+			hipGraphExec_t exec = nullptr;
 			hipError_t ie = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
 			hipGraphDestroy(g);
 			NNRT_HIP(ie);
-			if (ft->graphs.size() >= MAX_CACHED_GRAPHS) {
-				hipGraphExecDestroy(ft->graphs.front().exec);
-				ft->graphs.erase(ft->graphs.begin());
+			if (seen) {
+				seen->exec = exec;
+			} else {
+				if (ft->graphs.size() >= MAX_CACHED_GRAPHS) {
+					if (ft->graphs.front().exec) hipGraphExecDestroy(ft->graphs.front().exec);
+					ft->graphs.erase(ft->graphs.begin());
+				}
+				ft->graphs.push_back({modes, key_reset, exec});
+				seen = &ft->graphs.back();
 			}
-			ft->graphs.push_back({modes, reset, exec});
 		}
-		NNRT_HIP(hipGraphLaunch(exec, us));
+		NNRT_HIP(hipGraphLaunch(seen->exec, us));
 	}
 	return NNRT_OK;
 }
@@ -850,31 +908,78 @@ nnrt_status iterate_impl(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_ite
 
 nnrt_status nnrt_fitter_iterate(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_iteration, int32_t count, void* stream) {
 	NNRT_CHECK_ARG(ft && wf && count >= 0, "invalid arguments");
-	if (!ft->prepared || ft->wf != wf) {
-		set_error("nnrt_fitter_prepare must be called with this warp field before nnrt_fitter_iterate");
-		return NNRT_ERROR_ARGUMENT;
-	}
+	nnrt_status st = check_frame(ft, wf, "nnrt_fitter_iterate");
+	if (st) return st;
 	DeviceGuard guard(ft->device);
-	return iterate_impl(ft, wf, first_iteration, count, 0, static_cast<hipStream_t>(stream));
+	return iterate_impl(ft, wf, first_iteration, count, RESET_NONE, static_cast<hipStream_t>(stream));
 }
 
 nnrt_status nnrt_fitter_iterate_from_identity(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_iteration, int32_t count, void* stream) {
 	NNRT_CHECK_ARG(ft && wf && count >= 0, "invalid arguments");
-	if (!ft->prepared || ft->wf != wf) {
-		set_error("nnrt_fitter_prepare must be called with this warp field before nnrt_fitter_iterate_from_identity");
+	nnrt_status st = check_frame(ft, wf, "nnrt_fitter_iterate_from_identity");
+	if (st) return st;
+	DeviceGuard guard(ft->device);
+	return iterate_impl(ft, wf, first_iteration, count, RESET_IDENTITY, static_cast<hipStream_t>(stream));
+}
+
+int32_t nnrt_fitter_graph_count(const nnrt_fitter* ft) {
+	if (!ft) return -1;
+	int32_t n = 0;
+	for (const auto& g : ft->graphs) n += g.exec != nullptr;
+	return n;
+}
+
+nnrt_status nnrt_fitter_snapshot_motion(nnrt_fitter* ft, nnrt_warp_field* wf, void* stream) {
+	NNRT_CHECK_ARG(ft && wf, "null pointer");
+	nnrt_status st = check_frame(ft, wf, "nnrt_fitter_snapshot_motion");
+	if (st) return st;
+	DeviceGuard guard(ft->device);
+	const auto before = ft->snapshot.ptr;
+	if ((st = ft->snapshot.ensure(static_cast<size_t>(wf->N) * NODE_STRIDE))) return st;
+	if (ft->snapshot.ptr != before) ft->drop_graphs();
+	NNRT_HIP(hipMemcpyAsync(ft->snapshot.ptr, wf->state.ptr, sizeof(float) * NODE_STRIDE * wf->N, hipMemcpyDeviceToDevice,
+	                        static_cast<hipStream_t>(stream)));
+	ft->snapshot_valid = true;
+	return NNRT_OK;
+}
+
+static nnrt_status from_snapshot(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_iteration, int32_t count, int reset, void* stream,
+                                 const char* who) {
+	NNRT_CHECK_ARG(ft && wf && count >= 0, "invalid arguments");
+	nnrt_status st = check_frame(ft, wf, who);
+	if (st) return st;
+	if (!ft->snapshot_valid) {
+		set_error(std::string("nnrt_fitter_snapshot_motion must be called after prepare() before ") + who);
 		return NNRT_ERROR_ARGUMENT;
 	}
 	DeviceGuard guard(ft->device);
-	return iterate_impl(ft, wf, first_iteration, count, 1, static_cast<hipStream_t>(stream));
+	return iterate_impl(ft, wf, first_iteration, count, reset, static_cast<hipStream_t>(stream));
+}
+
+nnrt_status nnrt_fitter_iterate_from_snapshot(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_iteration, int32_t count, void* stream) {
+	return from_snapshot(ft, wf, first_iteration, count, RESET_SNAPSHOT, stream, "nnrt_fitter_iterate_from_snapshot");
+}
+
+nnrt_status nnrt_fitter_fit_from_snapshot(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t count, void* stream) {
+	return from_snapshot(ft, wf, 0, count, RESET_SNAPSHOT_FIRST, stream, "nnrt_fitter_fit_from_snapshot");
+}
+
+nnrt_status nnrt_fitter_restore_motion(nnrt_fitter* ft, nnrt_warp_field* wf, void* stream) {
+	NNRT_CHECK_ARG(ft && wf, "null pointer");
+	nnrt_status st = check_frame(ft, wf, "nnrt_fitter_restore_motion");
+	if (st) return st;
+	if (!ft->snapshot_valid) {
+		set_error("nnrt_fitter_snapshot_motion must be called after prepare() before nnrt_fitter_restore_motion");
+		return NNRT_ERROR_ARGUMENT;
+	}
+	DeviceGuard guard(ft->device);
+	return enqueue_restart(ft, wf, RESET_SNAPSHOT, false, static_cast<hipStream_t>(stream));
 }
 
 nnrt_status nnrt_fitter_iterate_timed(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_iteration, int32_t count, float* h_stage_ms,
                                       void* stream) {
 	NNRT_CHECK_ARG(ft && wf && h_stage_ms && count > 0, "invalid arguments");
-	if (!ft->prepared || ft->wf != wf) {
-		set_error("nnrt_fitter_prepare must be called with this warp field before nnrt_fitter_iterate_timed");
-		return NNRT_ERROR_ARGUMENT;
-	}
+	if (nnrt_status cst = check_frame(ft, wf, "nnrt_fitter_iterate_timed")) return cst;
 	DeviceGuard guard(ft->device);
 	hipStream_t us = static_cast<hipStream_t>(stream);
 	NNRT_HIP(hipEventRecord(ft->ev_in, us));
@@ -1255,7 +1360,8 @@ nnrt_status nnrt_fitter_fit_to_image_dlpack(nnrt_fitter* ft, nnrt_warp_field* wf
                                             const DLManagedTensor* faces, const DLManagedTensor* depth, const DLManagedTensor* mask,
                                             const DLManagedTensor* K, const DLManagedTensor* E, float depth_scale, void* stream) {
 	NNRT_CHECK_ARG(ft && wf, "null handle");
-	const int dev = wf->device;
+	NNRT_CHECK_ARG(wf->device == ft->device, "the warp field and the fitter live on different devices");
+	const int dev = ft->device;
 	const void *pv, *pn, *pf, *pd, *pm = nullptr, *pk, *pe;
 	int64_t dv[2], dn[2], df[2], dd[2], dm[2], dk[2], de[2];
 	nnrt_status st;

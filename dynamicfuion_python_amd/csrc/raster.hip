@@ -44,9 +44,19 @@ __device__ inline void pixel_span_f(float lo, float hi, int dim, int other, int*
 	*last = static_cast<int>(b);
 }
 
+// A face with a non-finite vertex coordinate is never rasterized (the sum of the nine coordinates is non-finite iff one
+// is, for NDC-sized values). Such faces only arise from the reference's A7 NaN rotations; the reference's queue then
+// depends on its face processing order (NaN fails every comparison), so both implementations here reject them.
+__device__ inline bool face_finite(const FaceNdc& fn) {
+	const float s = ((fn.x[0] + fn.x[1]) + (fn.x[2] + fn.y[0])) + ((fn.y[1] + fn.y[2]) + (fn.z[0] + fn.z[1])) + fn.z[2];
+	return __builtin_isfinite(s);
+}
+
 // Exact pixel range of a face: the pixels whose centres pass face_test's bounding-box check (box widened by the blur
-// radius). Returns false for faces face_test rejects for every pixel (culled, zero-area, behind the camera, off-image).
+// radius). Returns false for faces face_test rejects for every pixel (culled, zero-area, behind the camera, off-image,
+// non-finite).
 __device__ inline bool face_pixel_range(const FaceNdc& fn, const RasterOptions& o, int& u0, int& u1, int& v0, int& v1) {
+	if (!face_finite(fn)) return false;
 	const float area = spa_cw(fn.x[0], fn.y[0], fn.x[1], fn.y[1], fn.x[2], fn.y[2]);
 	const bool back = area < 0.f;
 	const bool zero_area = (area <= K_EPSILON && area >= -1.f * K_EPSILON);
@@ -291,6 +301,7 @@ nnrt_status launch_raster_resolve(const float* face_ndc, int64_t F, const Raster
 constexpr int TILE = 16;
 
 __device__ inline bool face_tile_range(const FaceNdc& fn, const RasterOptions& o, int& tx0, int& tx1, int& ty0, int& ty1) {
+	if (!face_finite(fn)) return false;
 	const float area = spa_cw(fn.x[0], fn.y[0], fn.x[1], fn.y[1], fn.x[2], fn.y[2]);
 	const bool zero_area = (area <= K_EPSILON && area >= -1.f * K_EPSILON);
 	const bool zinv = fmax3f(fn.z[0], fn.z[1], fn.z[2]) < K_EPSILON;

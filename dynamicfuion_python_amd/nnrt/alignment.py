@@ -25,13 +25,18 @@ class IterationMode(enum.IntEnum):
 NDC_REFERENCE = 0     # the reference's image -> NDC mapping
 NDC_CONSISTENT = 1    # raster pixel (u, v) == pixel (u, v) of the intrinsics
 
+# use_hip_graph (include/nnrt_mi355x.h NNRT_GRAPH_*): False/0 eager launches; True/1 a sequence of iterations runs eagerly
+# the first time it is requested after prepare() and is graph-captured and replayed from its second request on (the
+# default: a one-off frame fit never pays capture + instantiate); 2 captures on first use
+GRAPH_NEVER, GRAPH_AUTO, GRAPH_ALWAYS = 0, 1, 2
+
 
 class DeformableMeshToImageFitter:
     def __init__(self, max_iteration_count: int = 100, iteration_mode_sequence=(IterationMode.ALL,), minimal_update_threshold: float = 1e-6,
                  use_perspective_correction: bool = True, max_depth: float = 10.0, use_tukey_penalty_for_data_term: bool = False,
                  tukey_penalty_cutoff_cm: float = 0.01, preconditioning_dampening_factor: float = 0.0, arap_term_weight: float = 200.0,
                  use_huber_penalty_for_arap_term: bool = False, huber_penalty_constant: float = 1e-4, device: int | None = None,
-                 use_hip_graph: bool = True, ndc_convention: int = 0):
+                 use_hip_graph: int = 1, ndc_convention: int = 0):
         device = N.current_device() if device is None else int(device)
         p = N.FitterParams()
         N.lib().nnrt_fitter_default_params(ctypes.byref(p))
@@ -113,6 +118,23 @@ class DeformableMeshToImageFitter:
         iteration is the first GN iteration of the prepared frame); graph-captured like iterate()."""
         N.check(N.lib().nnrt_fitter_iterate_from_identity(self._h, warp_field.handle, int(first_iteration), int(count),
                                                            N.stream_ptr(stream)))
+
+    def snapshot_motion(self, warp_field: HierarchicalGraphWarpField, stream=None):
+        """Store the warp field's node motion (R, t) in the fitter (device copy) for iterate_from_snapshot()."""
+        N.check(N.lib().nnrt_fitter_snapshot_motion(self._h, warp_field.handle, N.stream_ptr(stream)))
+
+    def iterate_from_snapshot(self, warp_field: HierarchicalGraphWarpField, first_iteration: int = 0, count: int = 1, stream=None):
+        """iterate() with the node motion restored from the snapshot before every iteration (a device copy captured
+        with the iteration): each iteration is the same GN iteration k of the frame, through the general kernels."""
+        N.check(N.lib().nnrt_fitter_iterate_from_snapshot(self._h, warp_field.handle, int(first_iteration), int(count),
+                                                           N.stream_ptr(stream)))
+
+    def fit_from_snapshot(self, warp_field: HierarchicalGraphWarpField, count: int, stream=None):
+        """A whole frame fit of `count` iterations from the snapshot (restored once, before the first iteration)."""
+        N.check(N.lib().nnrt_fitter_fit_from_snapshot(self._h, warp_field.handle, int(count), N.stream_ptr(stream)))
+
+    def restore_motion(self, warp_field: HierarchicalGraphWarpField, stream=None):
+        N.check(N.lib().nnrt_fitter_restore_motion(self._h, warp_field.handle, N.stream_ptr(stream)))
 
     def iterate_timed(self, warp_field: HierarchicalGraphWarpField, first_iteration: int = 0, count: int = 1, stream=None) -> dict:
         """Eager iterations with HIP events between stages; returns average device ms per iteration per stage."""

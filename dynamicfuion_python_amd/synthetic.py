@@ -119,6 +119,19 @@ class Scene:
     gt_rotations: np.ndarray      # [N,3,3]
     gt_translations: np.ndarray   # [N,3]
     hierarchy: dict = field(default_factory=dict)   # edges, edge_layers, radii, layer_counts, virtual_indices (layers > 1)
+    gt_axis_angles: np.ndarray = None                # [N,3] the ground-truth rotations as axis-angle vectors
+
+    def partial_motion(self, fraction: float, seed: int = 0, noise: float = 0.0):
+        """Node motion `fraction` of the way along the ground truth (R = Rodrigues(fraction * w), t = fraction * t),
+        plus optional N(0, noise^2) on both (original node order). A deterministic non-identity state from which a GN
+        iteration runs the general warp / update kernels on a deformed mesh."""
+        rng = np.random.default_rng(seed)
+        w = self.gt_axis_angles * np.float32(fraction)
+        t = self.gt_translations * np.float32(fraction)
+        if noise > 0:
+            w = w + rng.normal(0, noise, w.shape).astype(np.float32)
+            t = t + rng.normal(0, noise, t.shape).astype(np.float32)
+        return rodrigues_np(w), t.astype(np.float32)
 
 
 def native_hierarchy_builder(nodes, coverage, layer_count):
@@ -153,4 +166,4 @@ def make_scene(name: str = "C2", seed: int = 0, hierarchy_builder=None) -> Scene
         vidx, counts, edges, elayers = hierarchy_builder(nodes, cov, layers)
         radii = np.array([cov * (i + 1) for i in range(layers)], np.float32)
         hier = dict(edges=edges, edge_layers=elayers, radii=radii, layer_counts=counts, virtual_indices=np.asarray(vidx, np.int64))
-    return Scene(name, H, W, K, points, normals, faces, nodes, cov, layers, iters, rodrigues_np(w), t, hier)
+    return Scene(name, H, W, K, points, normals, faces, nodes, cov, layers, iters, rodrigues_np(w), t, hier, w)

@@ -90,7 +90,10 @@ typedef struct nnrt_fitter_params {
 	float arap_term_weight;                 /* 200 */
 	int32_t use_huber_penalty_for_arap_term;/* 0 */
 	float huber_penalty_constant;           /* 1e-4 */
-	int32_t use_hip_graph;                  /* 1: capture one GN iteration per mode into a hipGraph and replay it */
+	int32_t use_hip_graph;                  /* NNRT_GRAPH_AUTO (1, default): an iteration sequence runs eagerly the first
+	                                           time it is requested after (re)preparation and is captured into a hipGraph
+	                                           and replayed from its second request on; NNRT_GRAPH_ALWAYS (2): captured on
+	                                           first use; NNRT_GRAPH_NEVER (0): always eager launches */
 	int32_t ndc_convention;                 /* NNRT_NDC_REFERENCE (0): the reference's image-space -> NDC mapping, whose
 	                                           rendered points are y-mirrored about cy (CoordinateSystemConversions.h:
 	                                           130-136); NNRT_NDC_CONSISTENT (1): raster pixel (u, v) is pixel (u, v) of K, for
@@ -98,6 +101,9 @@ typedef struct nnrt_fitter_params {
 } nnrt_fitter_params;
 #define NNRT_NDC_REFERENCE 0
 #define NNRT_NDC_CONSISTENT 1
+#define NNRT_GRAPH_NEVER 0
+#define NNRT_GRAPH_AUTO 1
+#define NNRT_GRAPH_ALWAYS 2
 
 void nnrt_fitter_default_params(nnrt_fitter_params* params);
 nnrt_status nnrt_fitter_create(const nnrt_fitter_params* params, int32_t device, nnrt_fitter** out);
@@ -136,6 +142,21 @@ nnrt_status nnrt_fitter_iterate(nnrt_fitter* fitter, nnrt_warp_field* warp_field
  * graph behaviour as iterate() (the resets are captured with the iterations). */
 nnrt_status nnrt_fitter_iterate_from_identity(nnrt_fitter* fitter, nnrt_warp_field* warp_field, int32_t first_iteration, int32_t count,
                                               void* stream);
+/* Number of instantiated iteration-sequence graphs the fitter holds (diagnostic for the use_hip_graph policy). */
+int32_t nnrt_fitter_graph_count(const nnrt_fitter* fitter);
+/* Store the warp field's current node motion (R, t) in the fitter (a device copy on `stream`). */
+nnrt_status nnrt_fitter_snapshot_motion(nnrt_fitter* fitter, nnrt_warp_field* warp_field, void* stream);
+/* Benchmark form of iterate() that runs the general (non-identity) kernels: before every iteration the warp field's
+ * node motion is restored from the snapshot by a device copy (captured into the graph with the iteration), so each
+ * iteration is the same GN iteration k of the frame (the state it was taken at). Requires nnrt_fitter_snapshot_motion
+ * after the last prepare(). */
+nnrt_status nnrt_fitter_iterate_from_snapshot(nnrt_fitter* fitter, nnrt_warp_field* warp_field, int32_t first_iteration, int32_t count,
+                                              void* stream);
+/* A whole frame fit (the FitToImage loop, :111-275) from the stored snapshot: the node motion is restored once, then
+ * iterations 0 .. count-1 run (graph-captured as one sequence under the use_hip_graph policy). */
+nnrt_status nnrt_fitter_fit_from_snapshot(nnrt_fitter* fitter, nnrt_warp_field* warp_field, int32_t count, void* stream);
+/* Restore the warp field's node motion from the snapshot (a device copy on `stream`). */
+nnrt_status nnrt_fitter_restore_motion(nnrt_fitter* fitter, nnrt_warp_field* warp_field, void* stream);
 /* iterate() without graphs, with HIP events between the stages of every iteration; h_stage_ms[NNRT_TIMED_STAGES]
  * receives the average per-iteration device time of: 0 warp (+warped Jacobians), 1 raster scatter, 2 pixel pass
  * (residuals + rasterized Jacobians, k_pixel_jacobians), 3 node pass (node Jacobians + JtJ / Jt r,

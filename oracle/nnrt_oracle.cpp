@@ -458,8 +458,17 @@ inline float PointSegmentSq(float px, float py, float ax, float ay, float bx, fl
 	return dx * dx + dy * dy;
 }
 
+// Faces with a non-finite vertex coordinate (A7 NaN rotations warp vertices to NaN) are rejected: the reference's queue
+// would depend on its face order there, since NaN fails every comparison (RayFaceIntersection.h:162-255).
+inline bool FaceFinite(const float* f) {
+	for (int i = 0; i < 9; i++)
+		if (!std::isfinite(f[i])) return false;
+	return true;
+}
+
 // returns true and fills hit if the face is accepted for the pixel (UpdateQueueIfPixelInsideFace minus queue logic)
 inline bool TestFace(const float* f, int32_t face, float px, float py, const RasterOpts& o, Hit& hit) {
+	if (!FaceFinite(f)) return false;
 	const float area = SPA_CW(f[0], f[1], f[3], f[4], f[6], f[7]);
 	const bool back = area < 0.f;
 	const bool zero_area = (area <= K_EPSILON && area >= -1.f * K_EPSILON);
@@ -1306,9 +1315,19 @@ ORC_API int orc_fit(const OrcFitParams* prm, OrcWarpField* wf, const float* mesh
 	std::vector<float> face_nrm(F * 9), vj(V * KA * 4), nj(V * KA * 3), rvj(P * 27), rnj(P * 30), pj(P * M * 6), Hd(N * 36), g(N * 6), x(N * 6);
 	std::vector<int32_t> pcounts(P);
 	double tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+	int s = 6;
+	auto write_outs = [&]() {
+		if (!outs) return;
+		if (outs->residuals) std::memcpy(outs->residuals, res.data(), sizeof(float) * P);
+		if (outs->residual_mask) std::memcpy(outs->residual_mask, resmask.data(), P);
+		if (outs->pixel_faces) std::memcpy(outs->pixel_faces, pface.data(), sizeof(int64_t) * P);
+		if (outs->updates) std::memcpy(outs->updates, x.data(), sizeof(float) * N * s);
+		if (outs->gradient) std::memcpy(outs->gradient, g.data(), sizeof(float) * N * s);
+		if (outs->hessian_diag) std::memcpy(outs->hessian_diag, Hd.data(), sizeof(float) * N * s * s);
+	};
 	for (int it = 0; it < prm->max_iterations; it++) {
 		const int mode = prm->modes[it % prm->mode_count];
-		const int s = mode == 0 ? 6 : 3;
+		s = mode == 0 ? 6 : 3;
 		double t0 = Now();
 		orc_warp_mesh(mesh_points, mesh_normals, V, wf->nodes, wf->rotations, wf->translations, anchors.data(), weights.data(), KA, extrinsics,
 		              wpts.data(), wnrm.data());
@@ -1372,7 +1391,10 @@ ORC_API int orc_fit(const OrcFitParams* prm, OrcWarpField* wf, const float* mesh
 			if (frc) return 20 + frc;
 		} else {
 			frc = orc_solve_block_diagonal(Hd.data(), g.data(), N, s, prm->lm_factor, x.data());
-			if (frc) return 30;
+			if (frc) {   // the reference throws here (NNRT_LAPACK_CHECK); the diagnostics keep this iteration (NaN updates on the failed blocks)
+				write_outs();
+				return 30;
+			}
 		}
 		double t6 = Now();
 		// S12 update (:257-273): R <- R * Rodrigues(w), t <- t + dt
@@ -1395,14 +1417,7 @@ ORC_API int orc_fit(const OrcFitParams* prm, OrcWarpField* wf, const float* mesh
 		double t7 = Now();
 		tacc[0] += t1 - t0; tacc[1] += t2 - t1; tacc[2] += t3 - t2; tacc[3] += t4 - t3; tacc[4] += t5 - t4; tacc[5] += t6 - t5; tacc[6] += t7 - t6;
 		tacc[7] += t7 - t0;
-		if (outs && it == prm->max_iterations - 1) {
-			if (outs->residuals) std::memcpy(outs->residuals, res.data(), sizeof(float) * P);
-			if (outs->residual_mask) std::memcpy(outs->residual_mask, resmask.data(), P);
-			if (outs->pixel_faces) std::memcpy(outs->pixel_faces, pface.data(), sizeof(int64_t) * P);
-			if (outs->updates) std::memcpy(outs->updates, x.data(), sizeof(float) * N * s);
-			if (outs->gradient) std::memcpy(outs->gradient, g.data(), sizeof(float) * N * s);
-			if (outs->hessian_diag) std::memcpy(outs->hessian_diag, Hd.data(), sizeof(float) * N * s * s);
-		}
+		if (it == prm->max_iterations - 1) write_outs();
 	}
 	if (outs && outs->stage_seconds) std::memcpy(outs->stage_seconds, tacc, sizeof(tacc));
 	return 0;

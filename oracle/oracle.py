@@ -403,8 +403,10 @@ def fit(*, nodes, rotations, translations, mesh_points, mesh_normals, faces, ref
         max_iterations=1, modes=("ALL",), use_perspective_correction=True, max_depth=10.0, use_tukey=False, tukey_cutoff=0.01,
         lm_factor=0.0, arap_weight=200.0, use_huber=False, huber_delta=1e-4, anchor_count=4, coverage=0.05, coverage_method=0,
         node_weights=None, min_valid_anchors=0, edges=None, edge_layers=None, radii=None, first_layer_count=None, fast_raster=True,
-        ndc_consistent=False):
-    """Full FitToImage on the CPU restatement (virtual node order). Returns (R, t, diagnostics of the last iteration)."""
+        ndc_consistent=False, raise_on_failure=True):
+    """Full FitToImage on the CPU restatement (virtual node order). Returns (R, t, diagnostics of the last iteration).
+    raise_on_failure=False: a block-diagonal potrf failure (the reference's NNRT_LAPACK_CHECK exception) returns the
+    failing iteration's diagnostics (NaN updates on the failed blocks) with diag["status"] = the oracle error code."""
     nodes = _f32(nodes)
     R = _f32(rotations).copy()
     t = _f32(translations).copy()
@@ -454,7 +456,9 @@ def fit(*, nodes, rotations, translations, mesh_points, mesh_normals, faces, ref
                        ctypes.c_void_p(ptr(_i64(faces))), ctypes.c_int64(len(faces)), ctypes.c_void_p(ptr(_f32(ref_points))),
                        ctypes.c_void_p(ptr(_u8(ref_mask))), ctypes.c_int(H), ctypes.c_int(W),
                        ctypes.c_void_p(ptr(_f64(K))), ctypes.c_void_p(E), ctypes.c_int(int(fast_raster)), ctypes.byref(outs))
-    _check(rc)
+    if raise_on_failure or rc != 30:
+        _check(rc)
+    diag["status"] = rc
     diag["residual_mask"] = diag["residual_mask"].astype(bool)
     return R, t, diag
 

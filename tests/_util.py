@@ -94,11 +94,12 @@ def scene_target(O, sc):
                                 sc.coverage)
 
 
-def oracle_fit_scene(O, sc, depth, iterations=1, lm=0.001, modes=("ALL",), **kw):
+def oracle_fit_scene(O, sc, depth, iterations=1, lm=0.001, modes=("ALL",), R0=None, t0=None, **kw):
+    """FitToImage on the oracle from the node motion (R0, t0) (virtual order; default the identity warp)."""
     refp, refm = O.unproject(depth, sc.K, 1.0, 10.0)
     N = len(sc.nodes)
-    R0 = np.tile(np.eye(3, dtype=np.float32), (N, 1, 1))
-    t0 = np.zeros((N, 3), np.float32)
+    R0 = np.tile(np.eye(3, dtype=np.float32), (N, 1, 1)) if R0 is None else np.ascontiguousarray(R0, np.float32).reshape(N, 3, 3)
+    t0 = np.zeros((N, 3), np.float32) if t0 is None else np.ascontiguousarray(t0, np.float32).reshape(N, 3)
     h = sc.hierarchy
     hk = {}
     nodes = sc.nodes

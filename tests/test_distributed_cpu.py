@@ -56,8 +56,62 @@ def test_two_rank_replica_aggregation():
     assert results[0][-1] != results[1][-1]
 
 
+def _protocol_worker(rank, world, port, q):
+    """bench.main's N > 1 control path with a stubbed fitter step: timed_region (barrier + sync + launches + sync +
+    barrier), max_over_ranks, aggregate and the end-of-run all_gather of per-rank results, over gloo."""
+    import time
+
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        calls = []
+
+        def step(n):                            # stub fitter launch: rank 1 is twice as slow
+            time.sleep(0.01 * (1 + rank))
+            calls.append(n)
+            return 0
+
+        syncs = []
+        bad, elapsed = bench.timed_region(step, 5, 10, world, lambda: syncs.append(1))
+        m = bench.max_over_ranks(elapsed)
+        agg = bench.aggregate(50, m, world)
+        per_rank = bench.exchange_per_rank(50, elapsed, 1.0 + rank)
+        q.put((rank, bad, calls, len(syncs), elapsed, m, agg["value"], per_rank))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_bench_protocol():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_protocol_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    slowest = max(r[4] for r in results)
+    for rank, bad, calls, nsync, elapsed, m, value, per_rank in results:
+        assert bad == 0 and calls == [10] * 5 and nsync == 2
+        assert m == pytest.approx(slowest)                   # every rank sees the slowest rank's time
+        assert value == pytest.approx(world * 50 / slowest)
+        assert [p["rank"] for p in per_rank] == [0, 1]
+        assert [p["update_norm"] for p in per_rank] == [1.0, 2.0]
+        assert per_rank[rank]["seconds"] == pytest.approx(elapsed)
+        assert per_rank[rank]["iters_per_s"] == pytest.approx(50 / elapsed)
+    assert results[1][4] > results[0][4]                     # rank 1's stub is slower
+    assert slowest >= 5 * 0.02
+
+
 def test_single_process_helpers():
     assert bench.max_over_ranks(3.0) == 3.0
+    assert bench.exchange_per_rank(10, 1.0, 0.0) is None
+    bad, el = bench.timed_region(lambda n: 0, 3, 2, 1, lambda: None)
+    assert bad == 0 and el >= 0
     agg = bench.aggregate(10, 0.5, 1)
     assert agg["value"] == pytest.approx(20.0) and agg["ms_per_step"] == pytest.approx(50.0)
 
