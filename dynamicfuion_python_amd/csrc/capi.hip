@@ -327,6 +327,13 @@ __global__ void k_reset_motion(float* state, int N) {
 	s[6] = s[10] = s[14] = 1.f;
 }
 
+// node-state copy (snapshot / restore): one float4 per lane; a 1500-node state is 96 KB (a runtime blit kernel costs
+// several microseconds more inside a graph)
+__global__ void k_copy_state(const float4* __restrict__ src, float4* __restrict__ dst, int count) {
+	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < count) dst[i] = src[i];
+}
+
 nnrt_status nnrt_warp_field_reset_motion(nnrt_warp_field* wf, void* stream) {
 	NNRT_CHECK_ARG(wf, "null pointer");
 	DeviceGuard guard(wf->device);
@@ -448,8 +455,12 @@ __global__ void k_faces_to_int4(const int64_t* __restrict__ faces, int64_t F, in
 
 // from_identity: the warp and the update treat every node's motion as R = I, t = 0 without reading it (only on the
 // block-diagonal path with <= 4 anchors, see fold_reset); the result equals a reset followed by the iteration.
+// state_in (default: the warp field's state): where the warp and the update read the node motion the iteration starts
+// from; the update always writes the warp field's state (a restore-from-snapshot folded into the iteration reads the
+// snapshot directly instead of copying it first).
 nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mode, hipStream_t s, hipEvent_t* marks = nullptr,
-                              bool from_identity = false) {
+                              bool from_identity = false, const float* state_in = nullptr) {
+	if (!state_in) state_in = wf->state.ptr;
 	nnrt_status st;
 	auto mark = [&](int i) -> nnrt_status {
 		if (marks) NNRT_HIP(hipEventRecord(marks[i], s));
@@ -457,7 +468,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 	};
 	if ((st = mark(0))) return st;
 	const bool with_jacobians = true;
-	if ((st = launch_warp_mesh(ft->mesh_p.ptr, ft->mesh_n.ptr, ft->V, wf->state.ptr, ft->anchors.ptr, ft->weights.ptr, ft->K, ft->extr,
+	if ((st = launch_warp_mesh(ft->mesh_p.ptr, ft->mesh_n.ptr, ft->V, state_in, ft->anchors.ptr, ft->weights.ptr, ft->K, ft->extr,
 	                           ft->wpos.ptr, ft->wnrm.ptr, with_jacobians ? ft->jv.ptr : nullptr, ft->jn.ptr, s, from_identity)))
 		return st;
 	if ((st = mark(1))) return st;
@@ -523,6 +534,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 		sa.N = ft->N;
 		sa.lm = ft->p.preconditioning_dampening_factor;
 		sa.acc = ft->acc.ptr;
+		sa.state_in = state_in;
 		sa.node_state = wf->state.ptr;
 		sa.updates_out = ft->updates.ptr;
 		sa.gradient_out = ft->gradient.ptr;
@@ -806,8 +818,11 @@ constexpr size_t MAX_CACHED_GRAPHS = 8;
 // iteration); the stored snapshot before the first iteration of the call only (a whole frame fit from a stored state)
 enum { RESET_NONE = 0, RESET_IDENTITY = 1, RESET_SNAPSHOT = 2, RESET_SNAPSHOT_FIRST = 3 };
 
-// reset folded into the iteration's warp / update kernels where they support it (no ARAP state reads, <= 4 anchors)
+// A restart folded into the iteration's warp / update kernels where they support it (block-diagonal path: no ARAP
+// kernel reads the state): from the identity (<= 4 anchors: the identity-specialised warp / update), or from the
+// snapshot (the general kernels read the snapshot as the starting state). Otherwise a separate kernel restarts.
 bool fold_reset(const nnrt_fitter* ft) { return ft->E == 0 && ft->K <= 4; }
+bool fold_snapshot(const nnrt_fitter* ft) { return ft->E == 0; }
 
 nnrt_status check_frame(const nnrt_fitter* ft, const nnrt_warp_field* wf, const char* who) {
 	if (!ft->prepared || ft->wf != wf || ft->wf_id != wf->id) {
@@ -821,18 +836,50 @@ nnrt_status check_frame(const nnrt_fitter* ft, const nnrt_warp_field* wf, const 
 	return NNRT_OK;
 }
 
-// what one iteration of a sequence restarts from, enqueued on s (inside or outside a capture)
-nnrt_status enqueue_restart(nnrt_fitter* ft, nnrt_warp_field* wf, int reset, bool folded, hipStream_t s) {
-	if (reset == RESET_IDENTITY && !folded) {
+// how iteration i of a sequence starts
+struct Restart {
+	int kernel = RESET_NONE;         // restart launched before the iteration (RESET_NONE: none)
+	bool from_identity = false;      // folded identity start
+	const float* state_in = nullptr; // folded snapshot start
+};
+
+Restart restart_plan(const nnrt_fitter* ft, int r) {
+	Restart p;
+	if (r == RESET_IDENTITY) {
+		if (fold_reset(ft)) p.from_identity = true;
+		else p.kernel = RESET_IDENTITY;
+	} else if (r == RESET_SNAPSHOT) {
+		if (fold_snapshot(ft)) p.state_in = ft->snapshot.ptr;
+		else p.kernel = RESET_SNAPSHOT;
+	}
+	return p;
+}
+
+// a restart launched on s (inside or outside a capture)
+nnrt_status enqueue_restart(nnrt_fitter* ft, nnrt_warp_field* wf, int kernel, hipStream_t s) {
+	if (kernel == RESET_IDENTITY) {
 		k_reset_motion<<<static_cast<unsigned>(ceil_div(wf->N, 256)), 256, 0, s>>>(wf->state.ptr, wf->N);
 		if (hipGetLastError() != hipSuccess) {
 			set_error("kernel launch failed (k_reset_motion)");
 			return NNRT_ERROR_HIP;
 		}
-	} else if (reset == RESET_SNAPSHOT || reset == RESET_SNAPSHOT_FIRST) {
-		NNRT_HIP(hipMemcpyAsync(wf->state.ptr, ft->snapshot.ptr, sizeof(float) * NODE_STRIDE * wf->N, hipMemcpyDeviceToDevice, s));
+	} else if (kernel == RESET_SNAPSHOT) {
+		const int count = wf->N * (NODE_STRIDE / 4);
+		k_copy_state<<<static_cast<unsigned>(ceil_div(count, 256)), 256, 0, s>>>(reinterpret_cast<const float4*>(ft->snapshot.ptr),
+		                                                                        reinterpret_cast<float4*>(wf->state.ptr), count);
+		if (hipGetLastError() != hipSuccess) {
+			set_error("kernel launch failed (k_copy_state)");
+			return NNRT_ERROR_HIP;
+		}
 	}
 	return NNRT_OK;
+}
+
+nnrt_status enqueue_step(nnrt_fitter* ft, nnrt_warp_field* wf, int mode, int restart, hipStream_t s) {
+	const Restart p = restart_plan(ft, restart);
+	nnrt_status st = enqueue_restart(ft, wf, p.kernel, s);
+	if (st) return st;
+	return enqueue_iteration(ft, wf, mode, s, nullptr, p.from_identity, p.state_in);
 }
 
 int restart_of(int reset, bool first_of_call) {
@@ -841,7 +888,6 @@ int restart_of(int reset, bool first_of_call) {
 
 nnrt_status iterate_impl(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_iteration, int32_t count, int reset, hipStream_t us) {
 	nnrt_status st;
-	const bool folded = reset == RESET_IDENTITY && fold_reset(ft);
 	for (int it0 = first_iteration; it0 < first_iteration + count; it0 += MAX_GRAPH_ITERATIONS) {
 		const int n = std::min(MAX_GRAPH_ITERATIONS, first_iteration + count - it0);
 		std::vector<int> modes(static_cast<size_t>(n));
@@ -855,10 +901,8 @@ nnrt_status iterate_impl(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_ite
 		const bool capture = ft->p.use_hip_graph == NNRT_GRAPH_ALWAYS || (ft->p.use_hip_graph == NNRT_GRAPH_AUTO && seen != nullptr);
 		if (!capture) {
 			// eager launches on the caller's stream
-			for (int i = 0; i < n; i++) {
-				if ((st = enqueue_restart(ft, wf, restart_of(reset, it0 + i == first_iteration), folded, us))) return st;
-				if ((st = enqueue_iteration(ft, wf, modes[static_cast<size_t>(i)], us, nullptr, folded))) return st;
-			}
+			for (int i = 0; i < n; i++)
+				if ((st = enqueue_step(ft, wf, modes[static_cast<size_t>(i)], restart_of(reset, it0 + i == first_iteration), us))) return st;
 			if (ft->p.use_hip_graph == NNRT_GRAPH_AUTO && !seen) {
 				if (ft->graphs.size() >= MAX_CACHED_GRAPHS) {
 					if (ft->graphs.front().exec) hipGraphExecDestroy(ft->graphs.front().exec);
@@ -874,10 +918,8 @@ nnrt_status iterate_impl(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_ite
 			hipGraph_t g = nullptr;
 			NNRT_HIP(hipStreamBeginCapture(ft->work, hipStreamCaptureModeThreadLocal));
 			st = NNRT_OK;
-			for (int i = 0; i < n && !st; i++) {
-				st = enqueue_restart(ft, wf, restart_of(reset, it0 + i == first_iteration), folded, ft->work);
-				if (!st) st = enqueue_iteration(ft, wf, modes[static_cast<size_t>(i)], ft->work, nullptr, folded);
-			}
+			for (int i = 0; i < n && !st; i++)
+				st = enqueue_step(ft, wf, modes[static_cast<size_t>(i)], restart_of(reset, it0 + i == first_iteration), ft->work);
 			hipError_t ce = hipStreamEndCapture(ft->work, &g);
 			if (st) {
 				if (g) hipGraphDestroy(g);
@@ -937,8 +979,10 @@ nnrt_status nnrt_fitter_snapshot_motion(nnrt_fitter* ft, nnrt_warp_field* wf, vo
 	const auto before = ft->snapshot.ptr;
 	if ((st = ft->snapshot.ensure(static_cast<size_t>(wf->N) * NODE_STRIDE))) return st;
 	if (ft->snapshot.ptr != before) ft->drop_graphs();
-	NNRT_HIP(hipMemcpyAsync(ft->snapshot.ptr, wf->state.ptr, sizeof(float) * NODE_STRIDE * wf->N, hipMemcpyDeviceToDevice,
-	                        static_cast<hipStream_t>(stream)));
+	const int count = wf->N * (NODE_STRIDE / 4);
+	k_copy_state<<<static_cast<unsigned>(ceil_div(count, 256)), 256, 0, static_cast<hipStream_t>(stream)>>>(
+	    reinterpret_cast<const float4*>(wf->state.ptr), reinterpret_cast<float4*>(ft->snapshot.ptr), count);
+	NNRT_LAUNCH_CHECK();
 	ft->snapshot_valid = true;
 	return NNRT_OK;
 }
@@ -973,7 +1017,7 @@ nnrt_status nnrt_fitter_restore_motion(nnrt_fitter* ft, nnrt_warp_field* wf, voi
 		return NNRT_ERROR_ARGUMENT;
 	}
 	DeviceGuard guard(ft->device);
-	return enqueue_restart(ft, wf, RESET_SNAPSHOT, false, static_cast<hipStream_t>(stream));
+	return enqueue_restart(ft, wf, RESET_SNAPSHOT, static_cast<hipStream_t>(stream));
 }
 
 nnrt_status nnrt_fitter_iterate_timed(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_iteration, int32_t count, float* h_stage_ms,

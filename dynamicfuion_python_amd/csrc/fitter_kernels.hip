@@ -702,13 +702,14 @@ __global__ __launch_bounds__(64) void k_solve_update(SolveArgs a) {
 	const int n = blockIdx.x * blockDim.x + threadIdx.x;
 	if (n >= a.N) return;
 	float* ns = a.node_state + static_cast<int64_t>(n) * NODE_STRIDE;
+	const float* ns_in = a.state_in + static_cast<int64_t>(n) * NODE_STRIDE;
 	float old[12];
 	if constexpr (IDENTITY) {
 #pragma unroll
 		for (int i = 0; i < 12; i++) old[i] = (i == 3 || i == 7 || i == 11) ? 1.f : 0.f;
 	} else {
 #pragma unroll
-		for (int i = 0; i < 12; i++) old[i] = __builtin_nontemporal_load(ns + 3 + i);
+		for (int i = 0; i < 12; i++) old[i] = __builtin_nontemporal_load(ns_in + 3 + i);
 	}
 	double* acc = a.acc + static_cast<int64_t>(n) * ACC_STRIDE;
 	float H[S][S], g[S];

@@ -39,7 +39,8 @@ struct SolveArgs {
 	int N;
 	float lm;
 	double* acc;
-	float* node_state;
+	const float* state_in;  // [N,16] the motion the iteration started from (read)
+	float* node_state;      // [N,16] updated motion (written; may equal state_in)
 	float* updates_out;     // [N*s]
 	float* gradient_out;    // [N*s]
 	float* hessian_out;     // [N*s*s] (nullable)

@@ -569,11 +569,13 @@ def test_graph_policy_and_cache_invalidation(nn, S, oracle_mod):
     assert rel_err(wf.get_node_translations(), t2) < 1e-6
 
 
-def test_iterate_from_snapshot(nn, S, oracle_mod):
+@pytest.mark.parametrize("name", ["S1", "S1_ARAP"])
+def test_iterate_from_snapshot(nn, S, oracle_mod, name):
     """iterate_from_snapshot(count): every iteration restarts from the stored (non-identity) node motion, so after any
-    count the state equals one iteration from the snapshot -- the benchmark step (general kernels)."""
+    count the state equals one iteration from the snapshot -- the benchmark step (general kernels; the block-diagonal
+    path reads the snapshot as its starting state, the ARAP path copies it back first)."""
     A, G = nn.alignment, nn.geometry
-    sc = _scene(S, oracle_mod, "S1")
+    sc = _scene(S, oracle_mod, name)
     depth = scene_target(oracle_mod, sc)
     mesh = G.TriangleMesh(sc.points, sc.normals, sc.faces)
     wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE,
