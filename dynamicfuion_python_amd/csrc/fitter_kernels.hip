@@ -539,15 +539,13 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 		for (int j = 0; j < SEG; j += NG_BATCH) {
 			// every LDS read of the batch is issued before the dependent double adds
 			const float* base = slots + grp * SEG + j;
-			int nodes[NG_BATCH];
 			float prod[NG_BATCH];
-			bool same = true;
 #pragma unroll
-			for (int q = 0; q < NG_BATCH; q++) {
-				nodes[q] = __builtin_bit_cast(int, base[7 * NG_STRIDE + q]);
-				prod[q] = base[c0 * NG_STRIDE + q] * base[c1 * NG_STRIDE + q];
-				same &= nodes[q] == cur;
-			}
+			for (int q = 0; q < NG_BATCH; q++) prod[q] = base[c0 * NG_STRIDE + q] * base[c1 * NG_STRIDE + q];
+			// every node of a chunk forms ONE contiguous run (grouping files all of a node's pending associations at once;
+			// only a chunk's capacity splits it, into the next chunk), so a batch is entirely node `cur` iff its first
+			// and last slots are: two node reads instead of one per slot
+			const bool same = __builtin_bit_cast(int, base[7 * NG_STRIDE]) == cur && __builtin_bit_cast(int, base[7 * NG_STRIDE + NG_BATCH - 1]) == cur;
 			if (__all(same)) {
 				// independent partial sums: the double adds of a batch do not wait on one another
 				double part[4] = {0.0, 0.0, 0.0, 0.0};
@@ -555,6 +553,9 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 				for (int q = 0; q < NG_BATCH; q++) part[q & 3] += static_cast<double>(prod[q]);
 				acc += (part[0] + part[1]) + (part[2] + part[3]);
 			} else {
+				int nodes[NG_BATCH];
+#pragma unroll
+				for (int q = 0; q < NG_BATCH; q++) nodes[q] = __builtin_bit_cast(int, base[7 * NG_STRIDE + q]);
 #pragma unroll
 				for (int q = 0; q < NG_BATCH; q++) {
 					if (nodes[q] != cur) {
