@@ -83,6 +83,13 @@ _SIGNATURES = {
                                                    c_void_p, c_void_p, c_void_p]),
     "nnrt_warp_mesh": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32,
                                  c_void_p, c_void_p, c_void_p, c_void_p]),
+    "nnrt_warp_points": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_float,
+                                   c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "nnrt_compute_point_to_plane_distances": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "nnrt_unproject_depth_image": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_float, c_float, c_void_p, c_void_p,
+                                             c_void_p]),
+    "nnrt_get_meshes_ndc_face_vertices_and_clip_mask": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_int32, c_int32, c_float,
+                                                                  c_float, c_void_p, c_void_p, c_void_p]),
     "nnrt_get_mesh_ndc_face_vertices_and_clip_mask": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int32, c_int32, c_float,
                                                                 c_float, c_void_p, c_void_p, c_void_p]),
     "nnrt_rasterize_ndc_triangles": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_float, c_int32, c_int32, c_int32,
@@ -92,6 +99,8 @@ _SIGNATURES = {
     "nnrt_backproject_depth_ushort": (c_int32, [c_void_p, c_int32, c_int32, c_float, c_float, c_float, c_float, c_float, c_void_p,
                                                 c_void_p]),
     "nnrt_backproject_depth_float": (c_int32, [c_void_p, c_int32, c_int32, c_float, c_float, c_float, c_float, c_void_p, c_void_p]),
+    "nnrt_matmul3d": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p, c_void_p]),
+    "nnrt_median_grid_subsample_3d_points": (c_int32, [c_void_p, c_int64, c_float, c_void_p, c_void_p, c_void_p]),
     "nnrt_axis_angle_to_matrices_rodrigues": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "nnrt_compute_triangle_normals": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
     "nnrt_compute_vertex_normals": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),

@@ -651,6 +651,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	hipStream_t us = static_cast<hipStream_t>(stream);
 	const int64_t P = static_cast<int64_t>(H) * W;
 	const int N = wf->N, K = wf->anchor_count, E = wf->E();
+	NNRT_CHECK_ARG(N >= K, "the warp field has fewer nodes than anchors per vertex");
 	if (E > 0) {
 		for (int i = 0; i < ft->p.iteration_mode_count; i++)
 			if (ft->p.iteration_modes[i] != NNRT_ITERATION_ALL) {
@@ -837,13 +838,13 @@ nnrt_status check_frame(const nnrt_fitter* ft, const nnrt_warp_field* wf, const 
 }
 
 // how iteration i of a sequence starts
-struct Restart {
+struct Restart {   // internal (static helpers below), not part of the C-ABI
 	int kernel = RESET_NONE;         // restart launched before the iteration (RESET_NONE: none)
 	bool from_identity = false;      // folded identity start
 	const float* state_in = nullptr; // folded snapshot start
 };
 
-Restart restart_plan(const nnrt_fitter* ft, int r) {
+static Restart restart_plan(const nnrt_fitter* ft, int r) {
 	Restart p;
 	if (r == RESET_IDENTITY) {
 		if (fold_reset(ft)) p.from_identity = true;
@@ -1156,6 +1157,66 @@ nnrt_status nnrt_warp_mesh(const float* d_vertices, const float* d_normals, int6
 	return st;
 }
 
+nnrt_status nnrt_warp_points(const float* d_points, const float* d_normals, int64_t V, const float* d_nodes, const float* d_rotations,
+                             const float* d_translations, int32_t N, const int32_t* d_anchors, const float* d_weights, int32_t K, float coverage,
+                             int32_t threshold, int32_t minimum_valid, const double* h_E, float* d_out_points, float* d_out_normals,
+                             void* stream) {
+	NNRT_CHECK_ARG((d_points && d_nodes && d_rotations && d_translations && d_out_points) || V == 0, "null pointer");
+	NNRT_CHECK_ARG(!d_normals == !d_out_normals, "normals in and out must both be given or both be NULL");
+	NNRT_CHECK_ARG(K >= 1 && K <= MAX_ANCHORS, "anchor_count needs to satisfy 0 < anchor_count <= 8 (Warping.cpp:70-75)");
+	NNRT_CHECK_ARG(minimum_valid >= 0 && minimum_valid <= K,
+	               "minimum_valid_anchor_count is required to satisfy 0 <= minimum_valid_anchor_count <= anchor_count (Warping.cpp:76-79)");
+	NNRT_CHECK_ARG(!d_anchors == !d_weights, "anchors and anchor_weights must both be given");
+	if (V == 0) return NNRT_OK;
+	hipStream_t s = static_cast<hipStream_t>(stream);
+	float* state = nullptr;
+	int32_t* anchors = nullptr;
+	float* weights = nullptr;
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&state), sizeof(float) * NODE_STRIDE * std::max(N, 1), s));
+	nnrt_status st = launch_pack_nodes(d_nodes, d_rotations, d_translations, N, state, s);
+	const int32_t* a = d_anchors;
+	const float* w = d_weights;
+	if (!st && !d_anchors) {   // online anchors: FindAnchorsAndWeightsForPoint_Euclidean[_Threshold]_FixedNodeCoverageWeight
+		NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&anchors), sizeof(int32_t) * V * K, s));
+		NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&weights), sizeof(float) * V * K, s));
+		st = launch_compute_anchors(d_points, V, d_nodes, N, K, coverage, nullptr, minimum_valid, anchors, weights, s, threshold ? 1 : 0);
+		a = anchors;
+		w = weights;
+	}
+	if (!st) st = launch_warp_points(d_points, d_normals, V, state, a, w, K, threshold ? minimum_valid : -1, make_extrinsics(h_E), d_out_points,
+	                                 d_out_normals, s);
+	hipFreeAsync(state, s);
+	if (anchors) hipFreeAsync(anchors, s);
+	if (weights) hipFreeAsync(weights, s);
+	return st;
+}
+
+nnrt_status nnrt_compute_point_to_plane_distances(const float* d_normals1, const float* d_vertices1, const float* d_vertices2, int64_t count,
+                                                  float* d_out, void* stream) {
+	NNRT_CHECK_ARG((d_normals1 && d_vertices1 && d_vertices2 && d_out) || count == 0, "null pointer");
+	return launch_point_to_plane(d_normals1, d_vertices1, d_vertices2, count, d_out, static_cast<hipStream_t>(stream));
+}
+
+nnrt_status nnrt_get_meshes_ndc_face_vertices_and_clip_mask(const float* const* h_vertex_sets, const int64_t* const* h_face_sets,
+                                                            const int64_t* h_face_counts, int32_t mesh_count, const double* h_K, int32_t H,
+                                                            int32_t W, float near_clip, float far_clip, float* d_face_ndc, uint8_t* d_clip_mask,
+                                                            void* stream) {
+	NNRT_CHECK_ARG(h_K && h_vertex_sets && h_face_sets && h_face_counts && mesh_count >= 0, "null pointer");
+	NNRT_CHECK_ARG(near_clip >= 0.f, "near_clipping_distance cannot be less than 0 (ExtractFaceVertices.cpp:40-44)");
+	NNRT_CHECK_ARG(near_clip <= far_clip, "near_clipping_distance cannot be greater than far_clipping_distance");
+	const NdcSetup ndc = make_ndc_setup(h_K, H, W, false);
+	int64_t offset = 0;
+	for (int m = 0; m < mesh_count; m++) {   // face f of mesh m -> output row offset(m) + f (ExtractClippedFaceVerticesImpl.h:111-116)
+		const int64_t F = h_face_counts[m];
+		NNRT_CHECK_ARG(F >= 0 && (F == 0 || (h_vertex_sets[m] && h_face_sets[m])), "mesh needs both triangle indices and vertex positions");
+		nnrt_status st = launch_extract_face_ndc(h_vertex_sets[m], h_face_sets[m], F, ndc, near_clip, far_clip, d_face_ndc + 9 * offset,
+		                                         d_clip_mask + offset, static_cast<hipStream_t>(stream));
+		if (st) return st;
+		offset += F;
+	}
+	return NNRT_OK;
+}
+
 nnrt_status nnrt_get_mesh_ndc_face_vertices_and_clip_mask(const float* d_vertices, const int64_t* d_faces, int64_t F, const double* h_K, int32_t H,
                                                           int32_t W, float near_clip, float far_clip, float* d_face_ndc, uint8_t* d_clip_mask,
                                                           void* stream) {
@@ -1206,7 +1267,29 @@ nnrt_status nnrt_interpolate_face_attributes(const int64_t* d_pixel_faces, const
 nnrt_status nnrt_unproject_depth(const float* d_depth, int32_t H, int32_t W, const double* h_K, float depth_scale, float depth_max,
                                  float* d_points, uint8_t* d_mask, void* stream) {
 	NNRT_CHECK_ARG(h_K, "null intrinsics");
-	return launch_unproject(d_depth, H, W, pixel_camera(h_K), depth_scale, depth_max, d_points, d_mask, static_cast<hipStream_t>(stream));
+	return launch_unproject(d_depth, NNRT_DTYPE_FLOAT32, H, W, pixel_camera(h_K), make_extrinsics(nullptr), depth_scale, depth_max, d_points,
+	                        d_mask, static_cast<hipStream_t>(stream));
+}
+
+nnrt_status nnrt_unproject_depth_image(const void* d_depth, int32_t depth_dtype, int32_t H, int32_t W, const double* h_K, const double* h_E,
+                                       float depth_scale, float depth_max, float* d_points, uint8_t* d_mask, void* stream) {
+	NNRT_CHECK_ARG(h_K, "null intrinsics");
+	NNRT_CHECK_ARG(depth_dtype == NNRT_DTYPE_UINT16 || depth_dtype == NNRT_DTYPE_FLOAT32, "depth must be uint16 or float32");
+	NNRT_CHECK_ARG(H >= 0 && W >= 0, "negative image size");
+	NNRT_CHECK_ARG((d_depth && d_points && d_mask) || static_cast<int64_t>(H) * W == 0, "null pointer");
+	double pose[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+	if (h_E) {   // Open3D InverseTransformation: [R^T | -R^T t], computed in double, rounded once into TransformIndexer's floats
+		for (int r = 0; r < 3; r++) {
+			double tr = 0.0;
+			for (int c = 0; c < 3; c++) {
+				pose[4 * r + c] = h_E[4 * c + r];
+				tr += h_E[4 * c + r] * h_E[4 * c + 3];
+			}
+			pose[4 * r + 3] = -tr;
+		}
+	}
+	return launch_unproject(d_depth, depth_dtype, H, W, pixel_camera(h_K), make_extrinsics(h_E ? pose : nullptr), depth_scale, depth_max,
+	                        d_points, d_mask, static_cast<hipStream_t>(stream));
 }
 
 nnrt_status nnrt_backproject_depth_ushort(const uint16_t* d_depth, int32_t height, int32_t width, float fx, float fy, float cx, float cy,
@@ -1223,6 +1306,19 @@ nnrt_status nnrt_backproject_depth_float(const float* d_depth, int32_t height, i
 	NNRT_CHECK_ARG((d_depth && d_points) || height * static_cast<int64_t>(width) == 0, "null image");
 	return launch_backproject_depth_f32(d_depth, height, width, BackprojectCamera{fx, fy, cx, cy, 1.0f}, d_points,
 	                                    static_cast<hipStream_t>(stream));
+}
+
+nnrt_status nnrt_matmul3d(const float* d_a, const float* d_b, int64_t batch, int32_t m, int32_t k, int32_t n, float* d_c, void* stream) {
+	NNRT_CHECK_ARG(batch >= 0 && m >= 0 && k >= 0 && n >= 0, "negative dimension");
+	NNRT_CHECK_ARG((d_a && d_b && d_c) || batch * m * n == 0, "null pointer");
+	return launch_matmul3d(d_a, d_b, batch, m, k, n, d_c, static_cast<hipStream_t>(stream));
+}
+
+nnrt_status nnrt_median_grid_subsample_3d_points(const float* d_points, int64_t n, float cell, int64_t* d_out, int64_t* h_count, void* stream) {
+	NNRT_CHECK_ARG(h_count && (n == 0 || (d_points && d_out)), "null pointer");
+	NNRT_CHECK_ARG(n >= 0 && n < (int64_t(1) << 31), "point count out of range");
+	NNRT_CHECK_ARG(cell > 0.f, "grid_cell_size must be positive");
+	return launch_median_grid_subsample(d_points, static_cast<int>(n), cell, d_out, h_count, static_cast<hipStream_t>(stream));
 }
 
 nnrt_status nnrt_axis_angle_to_matrices_rodrigues(const float* d_vectors, int32_t count, float* d_matrices, void* stream) {

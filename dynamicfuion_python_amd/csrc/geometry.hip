@@ -24,7 +24,7 @@ template <int K>
 __global__ __launch_bounds__(ANCHOR_BLOCK) void k_compute_anchors(const float* __restrict__ points, int64_t point_count,
                                                                     const float* __restrict__ nodes, int node_count,
                                                                     float coverage_squared, const float* __restrict__ node_weights,
-                                                                    int minimum_valid, int32_t* __restrict__ anchors,
+                                                                    int threshold, int minimum_valid, int32_t* __restrict__ anchors,
                                                                     float* __restrict__ weights) {
 	typedef float f2 __attribute__((ext_vector_type(2)));
 	const int64_t i = static_cast<int64_t>(blockIdx.x) * ANCHOR_BLOCK + threadIdx.x;
@@ -115,10 +115,12 @@ __global__ __launch_bounds__(ANCHOR_BLOCK) void k_compute_anchors(const float* _
 	float sum = 0.f;
 	int valid = 0;
 	bool normalize = true;
-	if (minimum_valid > 0) {
+	if (threshold) {
 #pragma unroll
 		for (int k = 0; k < K; k++) {
-			const float c2 = node_weights ? node_weights[idx[k]] : coverage_squared;
+			// a slot left empty (node_count < K: index -1, distance inf) fails the 2c test whatever its c^2 (the reference
+			// reads node_weights[-1] there)
+			const float c2 = node_weights ? (idx[k] >= 0 ? node_weights[idx[k]] : 1.f) : coverage_squared;
 			w[k] = d2[k];   // reference repurposes the weight array for squared distances
 			if (d2[k] > 4 * c2) {
 				idx[k] = -1;
@@ -133,7 +135,7 @@ __global__ __launch_bounds__(ANCHOR_BLOCK) void k_compute_anchors(const float* _
 	} else {
 #pragma unroll
 		for (int k = 0; k < K; k++) {
-			const float c2 = node_weights ? node_weights[idx[k]] : coverage_squared;
+			const float c2 = node_weights ? (idx[k] >= 0 ? node_weights[idx[k]] : 1.f) : coverage_squared;   // empty slot: exp(-inf) = 0
 			const float wt = exp_cr(-d2[k] / (2 * c2));
 			sum += wt;
 			w[k] = wt;
@@ -157,15 +159,17 @@ __global__ __launch_bounds__(ANCHOR_BLOCK) void k_compute_anchors(const float* _
 }
 
 nnrt_status launch_compute_anchors(const float* points, int64_t V, const float* nodes, int N, int K, float coverage,
-                                   const float* node_weights, int minimum_valid, int32_t* anchors, float* weights, hipStream_t stream) {
+                                   const float* node_weights, int minimum_valid, int32_t* anchors, float* weights, hipStream_t stream,
+                                   int threshold) {
+	if (threshold < 0) threshold = minimum_valid > 0;   // WarpAnchorComputation.cpp (kernel dispatch): threshold iff minimum > 0
 	NNRT_CHECK_ARG(K >= 1 && K <= MAX_ANCHORS, "anchor_count must be in [1, 8]");
-	NNRT_CHECK_ARG(N >= K, "anchor count exceeds node count");
+	NNRT_CHECK_ARG(N >= 0, "negative node count");   // N < K leaves slots at -1 with weight 0 (the reference's brute-force K-NN)
 	if (V == 0) return NNRT_OK;
 	const dim3 grid(static_cast<unsigned>(ceil_div(V, ANCHOR_BLOCK)));
 	const float c2 = coverage * coverage;
 #define NNRT_ANCHOR_CASE(KK)                                                                                                 \
 	case KK:                                                                                                                 \
-		k_compute_anchors<KK><<<grid, ANCHOR_BLOCK, 0, stream>>>(points, V, nodes, N, c2, node_weights, minimum_valid, anchors, weights); \
+		k_compute_anchors<KK><<<grid, ANCHOR_BLOCK, 0, stream>>>(points, V, nodes, N, c2, node_weights, threshold, minimum_valid, anchors, weights); \
 		break;
 	switch (K) {
 		NNRT_ANCHOR_CASE(1)
@@ -326,6 +330,94 @@ nnrt_status launch_warp_mesh(const float* points, const float* normals, int64_t 
 	return NNRT_OK;
 }
 
+// =====================================================================================================================
+// Point / point+normal warp of the nnrt.geometry.functional API (warp_triangle_mesh, warp_point_cloud): supplied
+// anchors (online anchors are computed first by k_compute_anchors, the reference's Find* then BlendWarp split).
+//   minimum_valid < 0: BlendWarp over the non-(-1) slots (Warp3dPointsAndNormalsImpl.h:173-193, :393-414);
+//   minimum_valid >= 0: BlendWarp_ValidAnchorCountThreshold (WarpUtilities.h:505-580): the point (and normal) stays
+//   zero unless at least minimum_valid slots are valid. For online threshold anchors this is FindAnchors...Threshold
+//   returning false (WarpUtilities.h:242-244): the slots failing the 2c test are exactly the -1 slots.
+// Extrinsics act on the point (rigid) and the normal (rotation) before blending (:369-378). One lane per point, outputs
+// [V,3] as the reference's tensors.
+// =====================================================================================================================
+template <bool NORMALS>
+__global__ __launch_bounds__(256) void k_warp_points(const float* __restrict__ points, const float* __restrict__ normals, int64_t V,
+                                                     const float* __restrict__ node_state, const int32_t* __restrict__ anchors,
+                                                     const float* __restrict__ weights, int K, int minimum_valid, WarpExtrinsics E,
+                                                     float* __restrict__ out_p, float* __restrict__ out_n) {
+	const int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (v >= V) return;
+	int valid = 0;
+	for (int k = 0; k < K; k++) valid += anchors[v * K + k] != -1;
+	f3 wp = make3(0.f, 0.f, 0.f), wn = make3(0.f, 0.f, 0.f);
+	if (minimum_valid < 0 || valid >= minimum_valid) {
+		const f3 p = make3(points[3 * v], points[3 * v + 1], points[3 * v + 2]);
+		const f3 pc = E.identity ? p : apply_extrinsics_point(E, p);
+		f3 nc = make3(0.f, 0.f, 0.f);
+		if constexpr (NORMALS) {
+			const f3 n = make3(normals[3 * v], normals[3 * v + 1], normals[3 * v + 2]);
+			nc = E.identity ? n : apply_extrinsics_normal(E, n);
+		}
+		for (int k = 0; k < K; k++) {
+			const int32_t a = anchors[v * K + k];
+			if (a == -1) continue;
+			const float w = weights[v * K + k];
+			const float* ns = node_state + static_cast<int64_t>(a) * NODE_STRIDE;
+			const f3 g = make3(ns[0], ns[1], ns[2]);
+			const f3 t = make3(ns[3], ns[4], ns[5]);
+			const f3 Rd = matvec3(ns + 6, sub3(pc, g));
+			wp.x += w * ((g.x + Rd.x) + t.x);
+			wp.y += w * ((g.y + Rd.y) + t.y);
+			wp.z += w * ((g.z + Rd.z) + t.z);
+			if constexpr (NORMALS) {
+				const f3 Rn = matvec3(ns + 6, nc);
+				wn.x += w * Rn.x;
+				wn.y += w * Rn.y;
+				wn.z += w * Rn.z;
+			}
+		}
+	}
+	out_p[3 * v] = wp.x;
+	out_p[3 * v + 1] = wp.y;
+	out_p[3 * v + 2] = wp.z;
+	if constexpr (NORMALS) {
+		out_n[3 * v] = wn.x;
+		out_n[3 * v + 1] = wn.y;
+		out_n[3 * v + 2] = wn.z;
+	}
+}
+
+nnrt_status launch_warp_points(const float* points, const float* normals, int64_t V, const float* node_state, const int32_t* anchors,
+                               const float* weights, int K, int minimum_valid, const WarpExtrinsics& E, float* out_p, float* out_n,
+                               hipStream_t stream) {
+	if (V == 0) return NNRT_OK;
+	const unsigned grid = static_cast<unsigned>(ceil_div(V, 256));
+	if (normals)
+		k_warp_points<true><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, minimum_valid, E, out_p, out_n);
+	else
+		k_warp_points<false><<<grid, 256, 0, stream>>>(points, nullptr, V, node_state, anchors, weights, K, minimum_valid, E, out_p, nullptr);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+// ComputePointToPlaneDistances (PointToPlaneDistancesImpl.h:26-50): d = n1 . (v1 - v2), one lane per point. The
+// three-term dot is summed left to right, as every dot product of this library and of the oracle.
+__global__ __launch_bounds__(256) void k_point_to_plane(const float* __restrict__ n1, const float* __restrict__ v1, const float* __restrict__ v2,
+                                                        int64_t count, float* __restrict__ out) {
+	const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (i >= count) return;
+	const f3 n = make3(n1[3 * i], n1[3 * i + 1], n1[3 * i + 2]);
+	const f3 d = sub3(make3(v1[3 * i], v1[3 * i + 1], v1[3 * i + 2]), make3(v2[3 * i], v2[3 * i + 1], v2[3 * i + 2]));
+	out[i] = dot3(n, d);
+}
+
+nnrt_status launch_point_to_plane(const float* n1, const float* v1, const float* v2, int64_t count, float* out, hipStream_t stream) {
+	if (count == 0) return NNRT_OK;
+	k_point_to_plane<<<static_cast<unsigned>(ceil_div(count, 256)), 256, 0, stream>>>(n1, v1, v2, count, out);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
 __global__ void k_pack_nodes(const float* __restrict__ nodes, const float* __restrict__ R, const float* __restrict__ t, int N,
                              float* __restrict__ state) {
 	const int n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -413,19 +505,25 @@ nnrt_status launch_extract_face_ndc(const float* verts, const int64_t* faces, in
 }
 
 // =====================================================================================================================
-// Unprojection (PerspectiveProjectionImpl.h:117-144, identity extrinsics) and attribute interpolation
-// (InterpolateFaceAttributesImpl.h:30-75)
+// Unprojection (UnprojectRasterWithoutDepthFiltering, PerspectiveProjectionImpl.h:60-146) and attribute interpolation
+// (InterpolateFaceAttributesImpl.h:30-75). Depth uint16 or float32, divided by depth_scale in float (the reference's
+// `*depth / depth_scale`); kept iff 0 < d < depth_max: Open3D TransformIndexer::Unproject ((u - cx) d / fx, ...) then
+// RigidTransform by pose = extrinsics^-1 (skipped for the identity, where it is exact). Rejected pixels: zero point,
+// mask 0 (the reference's Zeros-initialised outputs).
 // =====================================================================================================================
-__global__ void k_unproject(const float* __restrict__ depth, int H, int W, Camera K, float scale, float depth_max, float* __restrict__ pts,
-                            uint8_t* __restrict__ mask) {
+template <typename T>
+__global__ void k_unproject(const T* __restrict__ depth, int H, int W, Camera K, WarpExtrinsics pose, float scale, float depth_max,
+                            float* __restrict__ pts, uint8_t* __restrict__ mask) {
 	const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
 	if (i >= static_cast<int64_t>(H) * W) return;
 	const int y = static_cast<int>(i / W), x = static_cast<int>(i % W);
-	const float d = depth[i] / scale;
+	const float d = static_cast<float>(depth[i]) / scale;
 	if (d > 0 && d < depth_max) {
-		pts[3 * i] = (static_cast<float>(x) - K.cx) * d / K.fx;
-		pts[3 * i + 1] = (static_cast<float>(y) - K.cy) * d / K.fy;
-		pts[3 * i + 2] = d;
+		f3 c = make3((static_cast<float>(x) - K.cx) * d / K.fx, (static_cast<float>(y) - K.cy) * d / K.fy, d);
+		if (!pose.identity) c = apply_extrinsics_point(pose, c);
+		pts[3 * i] = c.x;
+		pts[3 * i + 1] = c.y;
+		pts[3 * i + 2] = c.z;
 		mask[i] = 1;
 	} else {
 		pts[3 * i] = pts[3 * i + 1] = pts[3 * i + 2] = 0.f;
@@ -433,11 +531,15 @@ __global__ void k_unproject(const float* __restrict__ depth, int H, int W, Camer
 	}
 }
 
-nnrt_status launch_unproject(const float* depth, int H, int W, const Camera& K, float scale, float depth_max, float* pts, uint8_t* mask,
-                             hipStream_t stream) {
+nnrt_status launch_unproject(const void* depth, int depth_dtype, int H, int W, const Camera& K, const WarpExtrinsics& pose, float scale,
+                             float depth_max, float* pts, uint8_t* mask, hipStream_t stream) {
 	const int64_t P = static_cast<int64_t>(H) * W;
 	if (P == 0) return NNRT_OK;
-	k_unproject<<<static_cast<unsigned>(ceil_div(P, 256)), 256, 0, stream>>>(depth, H, W, K, scale, depth_max, pts, mask);
+	const unsigned grid = static_cast<unsigned>(ceil_div(P, 256));
+	if (depth_dtype == NNRT_DTYPE_UINT16)
+		k_unproject<uint16_t><<<grid, 256, 0, stream>>>(static_cast<const uint16_t*>(depth), H, W, K, pose, scale, depth_max, pts, mask);
+	else
+		k_unproject<float><<<grid, 256, 0, stream>>>(static_cast<const float*>(depth), H, W, K, pose, scale, depth_max, pts, mask);
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;
 }
@@ -534,6 +636,29 @@ nnrt_status launch_interpolate(const int64_t* pixel_faces, const float* bary, in
                                hipStream_t stream) {
 	if (P * C == 0) return NNRT_OK;
 	k_interpolate<<<static_cast<unsigned>(ceil_div(P * C, 256)), 256, 0, stream>>>(pixel_faces, bary, P, Kf, attrs, C, out);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+// Matmul3D (cpp/core/linalg/Matmul3D.cpp:25-83, the batched GEMM behind R <- R dR): C[b] = A[b] B[b], row-major
+// [batch, m, k] x [batch, k, n] (n = 1 for an array of vectors). One lane per output element, products summed in k order.
+__global__ void k_matmul3d(const float* __restrict__ A, const float* __restrict__ B, int64_t batch, int m, int k, int n, float* __restrict__ C) {
+	const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	const int64_t per = static_cast<int64_t>(m) * n;
+	if (i >= batch * per) return;
+	const int64_t b = i / per;
+	const int r = static_cast<int>((i % per) / n), c = static_cast<int>(i % n);
+	const float* a = A + b * m * k + static_cast<int64_t>(r) * k;
+	const float* bb = B + b * k * n + c;
+	float acc = 0.f;
+	for (int j = 0; j < k; j++) acc += a[j] * bb[static_cast<int64_t>(j) * n];
+	C[i] = acc;
+}
+
+nnrt_status launch_matmul3d(const float* A, const float* B, int64_t batch, int m, int k, int n, float* C, hipStream_t stream) {
+	const int64_t total = batch * m * n;
+	if (total == 0) return NNRT_OK;
+	k_matmul3d<<<static_cast<unsigned>(ceil_div(total, 256)), 256, 0, stream>>>(A, B, batch, m, k, n, C);
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;
 }

@@ -13,7 +13,10 @@
 //     two-slot scan in ascending node order.
 // Every kernel scans the candidate set in LDS tiles of HB nodes, each lane owning one query node. All float expressions
 // keep the restatement's order (-ffp-contract=off, correctly rounded sqrt).
+#include <algorithm>
 #include <cfloat>
+
+#include <hipcub/hipcub.hpp>
 
 #include "common.hpp"
 #include "warp_field.hpp"
@@ -273,6 +276,35 @@ public:
 		return NNRT_OK;
 	}
 };
+
+// nnrt.geometry.functional.median_grid_subsample_3d_points (MedianGridSubsample3dPoints, GeometrySampling.cpp:62-68 ->
+// GeometrySamplingMedian.h:264-296): one medoid per occupied grid cell, as indices into `pts`. The reference emits them in
+// its hash map's bin order (not deterministic on the GPU); here in ascending point index (DeviceSelect over the flags).
+nnrt_status launch_median_grid_subsample(const float* pts, int n, float cell, int64_t* out, int64_t* h_count, hipStream_t s) {
+	*h_count = 0;
+	if (n == 0) return NNRT_OK;
+	Scratch<float> d_sums;
+	Scratch<int4> d_keys;
+	Scratch<uint8_t> d_flags;
+	Scratch<int64_t> d_count;
+	nnrt_status st;
+	if ((st = d_sums.alloc(n)) || (st = d_keys.alloc(n)) || (st = d_flags.alloc(n)) || (st = d_count.alloc(1))) return st;
+	k_grid_keys<<<blocks(n), HB, 0, s>>>(pts, n, cell, d_keys.p);
+	NNRT_LAUNCH_CHECK();
+	k_medoid_sums<<<blocks(n), HB, 0, s>>>(pts, d_keys.p, n, d_sums.p);
+	NNRT_LAUNCH_CHECK();
+	k_medoid_flags<<<blocks(n), HB, 0, s>>>(d_sums.p, d_keys.p, n, d_flags.p);
+	NNRT_LAUNCH_CHECK();
+	hipcub::CountingInputIterator<int64_t> idx(0);
+	size_t bytes = 0;
+	NNRT_HIP(hipcub::DeviceSelect::Flagged(nullptr, bytes, idx, d_flags.p, out, d_count.p, n, s));
+	Scratch<uint8_t> tmp;
+	if ((st = tmp.alloc(std::max<size_t>(bytes, 1)))) return st;
+	NNRT_HIP(hipcub::DeviceSelect::Flagged(tmp.p, bytes, idx, d_flags.p, out, d_count.p, n, s));
+	NNRT_HIP(hipMemcpyAsync(h_count, d_count.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+	NNRT_HIP(hipStreamSynchronize(s));
+	return NNRT_OK;
+}
 
 HierarchyOps& device_hierarchy_ops() {
 	static DeviceHierarchyOps ops;

@@ -54,7 +54,8 @@ __device__ inline f3 apply_extrinsics_normal(const WarpExtrinsics& E, f3 n) {
 }
 
 nnrt_status launch_compute_anchors(const float* points, int64_t V, const float* nodes, int N, int K, float coverage,
-                                   const float* node_weights, int minimum_valid, int32_t* anchors, float* weights, hipStream_t stream);
+                                   const float* node_weights, int minimum_valid, int32_t* anchors, float* weights, hipStream_t stream,
+                                   int threshold = -1);   // -1: threshold iff minimum_valid > 0 (the anchor API); 0 / 1: forced
 nnrt_status launch_warp_mesh(const float* points, const float* normals, int64_t V, const float* node_state, const int32_t* anchors,
                              const float* weights, int K, const WarpExtrinsics& E, float4* out_p, float4* out_n, float4* jv, float4* jn,
                              hipStream_t stream, bool from_identity = false);
@@ -67,8 +68,14 @@ struct BackprojectCamera {
 };
 nnrt_status launch_backproject_depth_u16(const uint16_t* depth, int H, int W, const BackprojectCamera& c, float* out, hipStream_t stream);
 nnrt_status launch_backproject_depth_f32(const float* depth, int H, int W, const BackprojectCamera& c, float* out, hipStream_t stream);
-nnrt_status launch_unproject(const float* depth, int H, int W, const Camera& K, float scale, float depth_max, float* pts, uint8_t* mask,
-                             hipStream_t stream);
+nnrt_status launch_unproject(const void* depth, int depth_dtype, int H, int W, const Camera& K, const WarpExtrinsics& pose, float scale,
+                             float depth_max, float* pts, uint8_t* mask, hipStream_t stream);
+nnrt_status launch_warp_points(const float* points, const float* normals, int64_t V, const float* node_state, const int32_t* anchors,
+                               const float* weights, int K, int minimum_valid, const WarpExtrinsics& E, float* out_p, float* out_n,
+                               hipStream_t stream);
+nnrt_status launch_matmul3d(const float* A, const float* B, int64_t batch, int m, int k, int n, float* C, hipStream_t stream);
+nnrt_status launch_median_grid_subsample(const float* pts, int n, float cell, int64_t* out, int64_t* h_count, hipStream_t s);
+nnrt_status launch_point_to_plane(const float* n1, const float* v1, const float* v2, int64_t count, float* out, hipStream_t stream);
 nnrt_status launch_interpolate(const int64_t* pixel_faces, const float* bary, int64_t P, int Kf, const float* attrs, int C, float* out,
                                hipStream_t stream);
 nnrt_status launch_rodrigues(const float* w, int N, float* R, hipStream_t stream);

@@ -45,6 +45,27 @@ def _solve_block_sparse_arrowhead_cholesky(diagonal_blocks, upper_wing_blocks, u
     return x
 
 
+def matmul3d(array_of_matrices_a, array_of_matrices_b) -> torch.Tensor:
+    """nnrt.core.matmul3d (cpp/pybind/core/core.cpp:32 -> cpp/core/linalg/Matmul3D.cpp:25-83): per batch entry A[b] @ B[b];
+    A [batch, m, k], B [batch, k, n] or [batch, k] (array of vectors -> [batch, m, 1])."""
+    N.require_gpu()
+    dev = torch.device("cuda", N.current_device())
+    A = to_device(array_of_matrices_a, torch.float32, dev)
+    B = to_device(array_of_matrices_b, torch.float32, dev)
+    if A.dim() != 3:
+        raise RuntimeError(f"Tensor A must be 3D (array of matrices), but got {A.dim()}D.")
+    if B.dim() not in (2, 3):
+        raise RuntimeError(f"Tensor B must be 2D (array of vectors) or 3D (array of matrices), but got {B.dim()}D.")
+    if A.shape[2] != B.shape[1]:
+        raise RuntimeError(f"Tensor A columns {A.shape[2]} mismatch with Tensor B rows {B.shape[1]}.")
+    if A.shape[0] != B.shape[0]:
+        raise RuntimeError(f"Tensors A and B should have matching first dimension. Got: {A.shape[0]} vs. {B.shape[0]}")
+    n = B.shape[2] if B.dim() == 3 else 1
+    out = torch.empty((A.shape[0], A.shape[1], n), dtype=torch.float32, device=dev)
+    N.check(N.lib().nnrt_matmul3d(N.ptr(A), N.ptr(B), A.shape[0], A.shape[1], A.shape[2], n, N.ptr(out), N.stream_ptr()))
+    return out
+
+
 linalg = types.SimpleNamespace(
     AxisAngleVectorsToMatricesRodrigues=_axis_angle_vectors_to_matrices_rodrigues,
     SolveBlockDiagonalCholesky=_solve_block_diagonal_cholesky,

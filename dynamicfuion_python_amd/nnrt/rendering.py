@@ -1,11 +1,14 @@
 """nnrt.rendering mirror (cpp/pybind/rendering/rendering.cpp:36-43, functional/functional.cpp:36-62)."""
 from __future__ import annotations
 
+import ctypes
 import types
 
+import numpy as np
 import torch
 
 from .. import _native as N
+from ._overloads import Overloaded
 from ._tensors import to_device, to_host_f64
 
 
@@ -33,10 +36,54 @@ def rasterize_ndc_triangles(ndc_face_vertices, clipped_faces_mask, image_size, b
     return fi, dep, bary, dist
 
 
-def get_mesh_ndc_face_vertices_and_clip_mask(mesh, intrinsic_matrix, image_size, near_clipping_distance=0.0,
-                                             far_clipping_distance=float("inf")):
+def _check_clipping(image_size, near_clipping_distance, far_clipping_distance):
+    """CheckClippingRangeAndImageSize (cpp/rendering/functional/ExtractFaceVertices.cpp:41-54)."""
+    if near_clipping_distance < 0.0:
+        raise RuntimeError(f"near_clipping_distance cannot be less than 0.0. Got {near_clipping_distance}.")
+    if near_clipping_distance > far_clipping_distance:
+        raise RuntimeError("near_clipping_distance cannot be greater than far_clipping_distance. Got "
+                           f"{near_clipping_distance} and {far_clipping_distance}, respectively.")
+    if len(image_size) != 2:
+        raise RuntimeError(f"image_size should be a SizeVector of size 2. Got size {len(image_size)}.")
+
+
+def _mesh_arrays(mesh, dev):
+    if mesh.triangle_indices is None or mesh.vertex_positions is None:
+        raise RuntimeError("Argument mesh needs to have both triangle vertex indices and vertex positions.")
+    return to_device(mesh.vertex_positions, torch.float32, dev).reshape(-1, 3), to_device(mesh.triangle_indices, torch.int64, dev).reshape(-1, 3)
+
+
+get_mesh_ndc_face_vertices_and_clip_mask = Overloaded(
+    "get_mesh_ndc_face_vertices_and_clip_mask",
+    "GetMeshNdcFaceVerticesAndClipMask, both overloads (cpp/pybind/rendering/functional/functional.cpp:36-54 -> ExtractFaceVertices.cpp:56-126): "
+    "face vertices in NDC x, y + camera z [F,3,3] and the clip mask [F] (True = keep); a list of meshes is concatenated in mesh order and "
+    "also returns the per-mesh face counts.")
+
+
+@get_mesh_ndc_face_vertices_and_clip_mask.overload(lambda a: isinstance(a["camera_space_meshes"], (list, tuple)))
+def _ndc_meshes(camera_space_meshes, intrinsic_matrix, image_size, near_clipping_distance=0.0, far_clipping_distance=float("inf")):
+    _check_clipping(image_size, near_clipping_distance, far_clipping_distance)
     dev = _dev()
-    p, _, f = mesh.on_device(dev)
+    arrays = [_mesh_arrays(m, dev) for m in camera_space_meshes]
+    counts = np.array([f.shape[0] for _, f in arrays], np.int64)
+    total = int(counts.sum())
+    K = to_host_f64(intrinsic_matrix)
+    H, W = int(image_size[0]), int(image_size[1])
+    out = torch.empty((total, 3, 3), dtype=torch.float32, device=dev)
+    mask = torch.empty(total, dtype=torch.uint8, device=dev)
+    vptr = (ctypes.c_void_p * max(len(arrays), 1))(*[v.data_ptr() for v, _ in arrays])
+    fptr = (ctypes.c_void_p * max(len(arrays), 1))(*[f.data_ptr() for _, f in arrays])
+    N.check(N.lib().nnrt_get_meshes_ndc_face_vertices_and_clip_mask(vptr, fptr, N.ptr(counts), len(arrays), N.ptr(K), H, W,
+                                                                    float(near_clipping_distance), float(far_clipping_distance), N.ptr(out),
+                                                                    N.ptr(mask), N.stream_ptr()))
+    return out, mask.bool(), torch.from_numpy(counts)
+
+
+@get_mesh_ndc_face_vertices_and_clip_mask.overload()
+def _ndc_mesh(camera_space_mesh, intrinsic_matrix, image_size, near_clipping_distance=0.0, far_clipping_distance=float("inf")):
+    _check_clipping(image_size, near_clipping_distance, far_clipping_distance)
+    dev = _dev()
+    p, f = _mesh_arrays(camera_space_mesh, dev)
     K = to_host_f64(intrinsic_matrix)
     H, W = int(image_size[0]), int(image_size[1])
     out = torch.empty((f.shape[0], 3, 3), dtype=torch.float32, device=dev)

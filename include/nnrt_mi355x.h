@@ -189,6 +189,37 @@ nnrt_status nnrt_warp_mesh(const float* d_vertices, const float* d_normals, int6
                            const float* d_rotations, const float* d_translations, int32_t node_count, const int32_t* d_anchors,
                            const float* d_weights, int32_t anchor_count, const double* h_E, float* d_out_vertices,
                            float* d_out_normals, void* stream);
+/* nnrt.geometry.functional.warp_triangle_mesh (both overloads, threshold_nodes_by_distance / minimum_valid_anchor_count /
+ * extrinsics) and warp_point_cloud (both overloads) (cpp/pybind/geometry/functional/functional.cpp:77-111 ->
+ * cpp/geometry/functional/Warping.cpp:61-264 -> Warp3dPointsAndNormalsImpl.h:33-438, WarpUtilities.h:34-580).
+ * d_normals / d_out_normals may be NULL (points only). d_anchors == NULL: anchors computed over d_nodes with the fixed
+ * node_coverage (the online-anchor overloads); otherwise d_anchors int32 / d_weights float32 [count, anchor_count].
+ * threshold_nodes_by_distance = 0: BlendWarp over the valid slots; 1: online anchors farther than 2 * node_coverage are
+ * dropped and a point with fewer than minimum_valid_anchor_count valid anchors stays (0, 0, 0) (warp_point_cloud always
+ * thresholds). h_E: float64[16] or NULL (identity). Outputs [count,3]. */
+nnrt_status nnrt_warp_points(const float* d_points, const float* d_normals, int64_t count, const float* d_nodes, const float* d_rotations,
+                             const float* d_translations, int32_t node_count, const int32_t* d_anchors, const float* d_weights,
+                             int32_t anchor_count, float node_coverage, int32_t threshold_nodes_by_distance,
+                             int32_t minimum_valid_anchor_count, const double* h_E, float* d_out_points, float* d_out_normals, void* stream);
+/* nnrt.geometry.functional.compute_point_to_plane_distances(mesh1, mesh2 | point_cloud) (functional.cpp:118-125 ->
+ * PointToPlaneDistances.cpp:25-90, kernel PointToPlaneDistancesImpl.h:26-50): d_out [count] = n1 . (v1 - v2). */
+nnrt_status nnrt_compute_point_to_plane_distances(const float* d_normals1, const float* d_vertices1, const float* d_vertices2, int64_t count,
+                                                  float* d_out, void* stream);
+/* nnrt.geometry.functional.unproject_raster_depth_without_filtering(depth, intrinsics, extrinsics, depth_scale, depth_max,
+ * preserve_pixel_layout) (functional.cpp:128-140 -> PerspectiveProjection.cpp:26-39, PerspectiveProjectionImpl.h:60-146):
+ * depth uint16 (NNRT_DTYPE_UINT16) or float32 (NNRT_DTYPE_FLOAT32) [H,W]; points [H*W,3] in the frame of
+ * extrinsics^-1 (h_E float64[16] or NULL = identity), zero where rejected; d_mask uint8 [H*W]. The pixel layout of the
+ * outputs is the same either way (preserve_pixel_layout is a shape, [H,W,3] vs [H*W,3]). */
+nnrt_status nnrt_unproject_depth_image(const void* d_depth, int32_t depth_dtype, int32_t height, int32_t width, const double* h_K,
+                                       const double* h_E, float depth_scale, float depth_max, float* d_points, uint8_t* d_mask, void* stream);
+/* nnrt.rendering.functional.get_mesh_ndc_face_vertices_and_clip_mask([meshes], ...) (cpp/pybind/rendering/functional/
+ * functional.cpp:36-44 -> ExtractFaceVertices.cpp:87-126): the meshes' faces concatenated in mesh order; h_vertex_sets /
+ * h_face_sets are HOST arrays of mesh_count DEVICE pointers, h_face_counts the per-mesh face counts (the reference's
+ * face_counts output). d_face_ndc [sum F,3,3], d_clip_mask [sum F]. */
+nnrt_status nnrt_get_meshes_ndc_face_vertices_and_clip_mask(const float* const* h_vertex_sets, const int64_t* const* h_face_sets,
+                                                            const int64_t* h_face_counts, int32_t mesh_count, const double* h_K,
+                                                            int32_t height, int32_t width, float near_clip, float far_clip,
+                                                            float* d_face_ndc, uint8_t* d_clip_mask, void* stream);
 /* nnrt.rendering.functional.get_mesh_ndc_face_vertices_and_clip_mask (cpp/rendering/functional/ExtractFaceVertices.cpp:56-85).
  * d_face_ndc [F,3,3], d_clip_mask [F] uint8 (1 = keep). */
 nnrt_status nnrt_get_mesh_ndc_face_vertices_and_clip_mask(const float* d_vertices, const int64_t* d_faces, int64_t face_count,
@@ -235,6 +266,15 @@ nnrt_status nnrt_compute_vertex_normals(const float* d_vertices, int64_t vertex_
  * kernel NormalsOperationsImpl.h:170-214): organized [H*W,3] points -> [H*W,3] normals facing the camera, 0 on the border */
 nnrt_status nnrt_compute_ordered_point_cloud_normals(const float* d_points, int64_t point_count, int32_t height, int32_t width, float* d_out,
                                                      void* stream);
+/* nnrt.core.matmul3d(array_of_matrices_a, array_of_matrices_b) (cpp/pybind/core/core.cpp:32 -> cpp/core/linalg/Matmul3D.cpp:25-83):
+ * d_c [batch, m, n] = d_a [batch, m, k] x d_b [batch, k, n] per batch entry, float32 row-major (n = 1: array of vectors). */
+nnrt_status nnrt_matmul3d(const float* d_a, const float* d_b, int64_t batch, int32_t m, int32_t k, int32_t n, float* d_c, void* stream);
+/* nnrt.geometry.functional.median_grid_subsample_3d_points(points, grid_cell_size) (functional.cpp:152-153 ->
+ * GeometrySampling.cpp:62-68, GeometrySamplingMedian.h:264-296): indices of one medoid per occupied grid cell, in ascending
+ * index order (the reference's order is its hash map's bin order). d_out_indices needs room for point_count int64;
+ * *h_sample_count receives the number written. Synchronizes `stream`. */
+nnrt_status nnrt_median_grid_subsample_3d_points(const float* d_points, int64_t point_count, float grid_cell_size, int64_t* d_out_indices,
+                                                 int64_t* h_sample_count, void* stream);
 /* nnrt.core.linalg AxisAngleVectorsToMatricesRodrigues (cpp/core/linalg/RodriguesImpl.h:66-88) */
 nnrt_status nnrt_axis_angle_to_matrices_rodrigues(const float* d_vectors, int32_t count, float* d_matrices, void* stream);
 /* SolveBlockDiagonalCholesky (cpp/core/linalg/SolveBlockDiagonalCholesky.cpp): x_i = A_i^-1 b_i, block size 3 or 6 */

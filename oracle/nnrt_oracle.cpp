@@ -171,8 +171,20 @@ void NormalizeAnchorWeights(float* w, float sum, int K, int valid) {
 } // namespace
 
 // node_weights == nullptr -> FIXED_NODE_COVERAGE (c^2 = coverage^2), else MINIMAL_K_NEIGHBOR_NODE_DISTANCE (c^2 = node_weights[n])
+// threshold: FindAnchorsAndWeightsForPoint_Euclidean_Threshold_* (the anchor API thresholds iff minimum_valid_anchor_count > 0,
+// kernel/WarpAnchorComputation.cpp; WarpTriangleMesh with threshold_nodes_by_distance thresholds at any minimum, Warping.cpp:198-213)
+ORC_API void orc_compute_anchors_ex(const float* points, int64_t V, const float* nodes, int N, int K, float coverage,
+                                    const float* node_weights, int threshold, int minimum_valid_anchor_count, int32_t* anchors,
+                                    float* weights);
 ORC_API void orc_compute_anchors(const float* points, int64_t V, const float* nodes, int N, int K, float coverage,
                                  const float* node_weights, int minimum_valid_anchor_count, int32_t* anchors, float* weights) {
+	orc_compute_anchors_ex(points, V, nodes, N, K, coverage, node_weights, minimum_valid_anchor_count > 0, minimum_valid_anchor_count, anchors,
+	                       weights);
+}
+
+ORC_API void orc_compute_anchors_ex(const float* points, int64_t V, const float* nodes, int N, int K, float coverage,
+                                    const float* node_weights, int threshold, int minimum_valid_anchor_count, int32_t* anchors,
+                                    float* weights) {
 	float c2_fixed = coverage * coverage;
 #pragma omp parallel for schedule(static)
 	for (int64_t v = 0; v < V; v++) {
@@ -182,10 +194,10 @@ ORC_API void orc_compute_anchors(const float* points, int64_t V, const float* no
 		KnnBruteForce(points + 3 * v, nodes, N, K, a, w);   // weights array holds squared distances first
 		float sum = 0.f;
 		int valid = 0;
-		if (minimum_valid_anchor_count > 0) {
+		if (threshold) {
 			for (int k = 0; k < K; k++) {
 				float sq = w[k];
-				float c2 = node_weights ? node_weights[a[k]] : c2_fixed;
+				float c2 = node_weights ? (a[k] >= 0 ? node_weights[a[k]] : 1.f) : c2_fixed;   // empty slot (N < K): fails the test
 				if (sq > 4 * c2) { a[k] = -1; continue; }
 				float wt = exp_cr(-sq / (2 * c2));
 				sum += wt;
@@ -197,7 +209,7 @@ ORC_API void orc_compute_anchors(const float* points, int64_t V, const float* no
 		} else {
 			for (int k = 0; k < K; k++) {
 				float sq = w[k];
-				float c2 = node_weights ? node_weights[a[k]] : c2_fixed;
+				float c2 = node_weights ? (a[k] >= 0 ? node_weights[a[k]] : 1.f) : c2_fixed;   // empty slot: exp(-inf) = 0
 				float wt = exp_cr(-sq / (2 * c2));
 				sum += wt;
 				w[k] = wt;
@@ -350,13 +362,31 @@ ORC_API int orc_build_hierarchy(const float* nodes, int N, float coverage, int l
 // Warp: cpp/geometry/functional/kernel/Warp3dPointsAndNormalsImpl.h:334-390 + WarpUtilities.h:448-467 (BlendWarp).
 // extrinsics: double[16] row-major or nullptr (identity); applied as Open3D TransformIndexer::RigidTransform in float.
 // =====================================================================================================================
+// minimum_valid >= 0: BlendWarp_ValidAnchorCountThreshold (WarpUtilities.h:505-580): fewer valid (!= -1) slots than
+// minimum_valid -> the point / normal keep the zero they were initialised with (Warp3dPointsAndNormalsImpl.h:237-238)
+ORC_API void orc_warp_points(const float* points, const float* normals, int64_t V, const float* nodes, const float* rotations,
+                             const float* translations, const int32_t* anchors, const float* weights, int K, int minimum_valid,
+                             const double* extrinsics, float* out_points, float* out_normals);
 ORC_API void orc_warp_mesh(const float* points, const float* normals, int64_t V, const float* nodes, const float* rotations,
                            const float* translations, const int32_t* anchors, const float* weights, int K, const double* extrinsics,
                            float* out_points, float* out_normals) {
+	orc_warp_points(points, normals, V, nodes, rotations, translations, anchors, weights, K, -1, extrinsics, out_points, out_normals);
+}
+
+ORC_API void orc_warp_points(const float* points, const float* normals, int64_t V, const float* nodes, const float* rotations,
+                             const float* translations, const int32_t* anchors, const float* weights, int K, int minimum_valid,
+                             const double* extrinsics, float* out_points, float* out_normals) {
 	float E[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
 	if (extrinsics) for (int i = 0; i < 12; i++) E[i] = static_cast<float>(extrinsics[i]);
 #pragma omp parallel for schedule(static)
 	for (int64_t v = 0; v < V; v++) {
+		int valid = 0;
+		for (int k = 0; k < K; k++) valid += anchors[v * K + k] != -1;
+		if (minimum_valid >= 0 && valid < minimum_valid) {
+			for (int c = 0; c < 3; c++) out_points[3 * v + c] = 0.f;
+			if (normals) for (int c = 0; c < 3; c++) out_normals[3 * v + c] = 0.f;
+			continue;
+		}
 		const float* p = points + 3 * v;
 		float pc[3], nc[3];
 		for (int r = 0; r < 3; r++) pc[r] = ((p[0] * E[4 * r] + p[1] * E[4 * r + 1]) + p[2] * E[4 * r + 2]) + E[4 * r + 3];
@@ -694,6 +724,53 @@ ORC_API void orc_unproject(const float* depth, int H, int W, const double* K, fl
 			o[0] = o[1] = o[2] = 0.f;
 			mask[i] = 0;
 		}
+	}
+}
+
+// UnprojectRasterWithoutDepthFiltering with extrinsics (PerspectiveProjectionImpl.h:60-146): depth uint16 (dtype 1) or float32
+// (any other dtype code) [H,W]; camera point by TransformIndexer::Unproject, then RigidTransform by pose = extrinsics^-1 (Open3D
+// InverseTransformation [R^T | -R^T t], here in double, rounded once to the indexer's floats; extrinsics nullptr = identity).
+ORC_API void orc_unproject_image(const void* depth, int dtype, int H, int W, const double* K, const double* extrinsics, float depth_scale,
+                                 float depth_max, float* points, uint8_t* mask) {
+	const float fx = static_cast<float>(K[0]), fy = static_cast<float>(K[4]), cx = static_cast<float>(K[2]), cy = static_cast<float>(K[5]);
+	float P[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+	bool identity = true;
+	if (extrinsics) {
+		for (int r = 0; r < 3; r++) {
+			double tr = 0.0;
+			for (int c = 0; c < 3; c++) {
+				P[4 * r + c] = static_cast<float>(extrinsics[4 * c + r]);
+				tr += extrinsics[4 * c + r] * extrinsics[4 * c + 3];
+			}
+			P[4 * r + 3] = static_cast<float>(-tr);
+		}
+		const float I[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+		for (int i = 0; i < 12; i++) identity &= P[i] == I[i];
+	}
+#pragma omp parallel for schedule(static)
+	for (int64_t i = 0; i < static_cast<int64_t>(H) * W; i++) {
+		int64_t y = i / W, x = i % W;
+		const float raw = dtype == 1 ? static_cast<float>(static_cast<const uint16_t*>(depth)[i]) : static_cast<const float*>(depth)[i];
+		float d = raw / depth_scale;
+		float* o = points + 3 * i;
+		if (d > 0 && d < depth_max) {
+			const float c[3] = {(static_cast<float>(x) - cx) * d / fx, (static_cast<float>(y) - cy) * d / fy, d};
+			for (int r = 0; r < 3; r++)
+				o[r] = identity ? c[r] : ((c[0] * P[4 * r] + c[1] * P[4 * r + 1]) + c[2] * P[4 * r + 2]) + P[4 * r + 3];
+			mask[i] = 1;
+		} else {
+			o[0] = o[1] = o[2] = 0.f;
+			mask[i] = 0;
+		}
+	}
+}
+
+// ComputePointToPlaneDistances (PointToPlaneDistancesImpl.h:26-50): n1 . (v1 - v2), summed left to right
+ORC_API void orc_point_to_plane(const float* n1, const float* v1, const float* v2, int64_t count, float* out) {
+#pragma omp parallel for schedule(static)
+	for (int64_t i = 0; i < count; i++) {
+		const float d[3] = {v1[3 * i] - v2[3 * i], v1[3 * i + 1] - v2[3 * i + 1], v1[3 * i + 2] - v2[3 * i + 2]};
+		out[i] = dot3(n1 + 3 * i, d);
 	}
 }
 

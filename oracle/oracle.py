@@ -76,14 +76,18 @@ def num_threads() -> int:
     return lib().orc_num_threads()
 
 
-def compute_anchors(points, nodes, anchor_count=4, coverage=0.05, node_weights=None, minimum_valid_anchor_count=0):
+def compute_anchors(points, nodes, anchor_count=4, coverage=0.05, node_weights=None, minimum_valid_anchor_count=0, threshold=None):
+    """threshold None: the anchor API's rule (threshold iff minimum_valid_anchor_count > 0); True / False: forced (WarpTriangleMesh
+    with / without threshold_nodes_by_distance)."""
     points, nodes = _f32(points), _f32(nodes)
     V, N = len(points), len(nodes)
     anchors = np.empty((V, anchor_count), np.int32)
     weights = np.empty((V, anchor_count), np.float32)
     nw = None if node_weights is None else _f32(node_weights)
-    lib().orc_compute_anchors(_p(points), ctypes.c_int64(V), _p(nodes), ctypes.c_int(N), ctypes.c_int(anchor_count),
-                              ctypes.c_float(coverage), _p(nw), ctypes.c_int(minimum_valid_anchor_count), _p(anchors), _p(weights))
+    thr = int(minimum_valid_anchor_count > 0) if threshold is None else int(bool(threshold))
+    lib().orc_compute_anchors_ex(_p(points), ctypes.c_int64(V), _p(nodes), ctypes.c_int(N), ctypes.c_int(anchor_count),
+                                 ctypes.c_float(coverage), _p(nw), ctypes.c_int(thr), ctypes.c_int(minimum_valid_anchor_count), _p(anchors),
+                                 _p(weights))
     return anchors, weights
 
 
@@ -120,6 +124,44 @@ def warp_mesh(points, normals, nodes, rotations, translations, anchors, weights,
     lib().orc_warp_mesh(_p(points), _p(normals), ctypes.c_int64(V), _p(nodes), _p(rotations), _p(translations), _p(anchors),
                         _p(weights), ctypes.c_int(anchors.shape[1]), _p(E), _p(op), _p(on))
     return op, on
+
+
+def warp_points(points, normals, nodes, rotations, translations, anchors, weights, minimum_valid=-1, extrinsics=None):
+    """Warp3dPoints[AndNormals] with supplied anchors; minimum_valid >= 0: BlendWarp_ValidAnchorCountThreshold. normals may be
+    None (points only; the returned normals are then None)."""
+    points, nodes = _f32(points), _f32(nodes)
+    normals = None if normals is None else _f32(normals)
+    rotations, translations, anchors, weights = _f32(rotations), _f32(translations), _i32(anchors), _f32(weights)
+    V = len(points)
+    op = np.empty((V, 3), np.float32)
+    on = None if normals is None else np.empty((V, 3), np.float32)
+    E = None if extrinsics is None else _f64(extrinsics)
+    lib().orc_warp_points(_p(points), _p(normals), ctypes.c_int64(V), _p(nodes), _p(rotations), _p(translations), _p(anchors),
+                          _p(weights), ctypes.c_int(anchors.shape[1]), ctypes.c_int(minimum_valid), _p(E), _p(op), _p(on))
+    return op, on
+
+
+def point_to_plane(normals1, vertices1, vertices2):
+    n, a, b = _f32(normals1), _f32(vertices1), _f32(vertices2)
+    out = np.empty(len(a), np.float32)
+    lib().orc_point_to_plane(_p(n), _p(a), _p(b), ctypes.c_int64(len(a)), _p(out))
+    return out
+
+
+def unproject_image(depth, K, extrinsics=None, depth_scale=1000.0, depth_max=3.0):
+    """uint16 or float32 depth [H,W] -> points [H*W,3] (frame of extrinsics^-1), mask [H*W] bool."""
+    depth = np.ascontiguousarray(depth)
+    dtype = 1 if depth.dtype == np.uint16 else 2
+    if dtype == 2:
+        depth = _f32(depth)
+    K = _f64(K)
+    E = None if extrinsics is None else _f64(extrinsics)
+    H, W = depth.shape[:2]
+    pts = np.empty((H * W, 3), np.float32)
+    mask = np.empty(H * W, np.uint8)
+    lib().orc_unproject_image(_p(depth), ctypes.c_int(dtype), ctypes.c_int(H), ctypes.c_int(W), _p(K), _p(E), ctypes.c_float(depth_scale),
+                              ctypes.c_float(depth_max), _p(pts), _p(mask))
+    return pts, mask.astype(bool)
 
 
 def intrinsics_to_ndc(K, H, W):

@@ -47,6 +47,50 @@ def xy_plane(side, center, subdivisions):
     return V, N, F
 
 
+def sphere_open3d(radius, resolution, center=(0.0, 0.0, 0.0)):
+    """Open3D TriangleMesh::CreateSphere(radius, resolution) vertex / triangle order (Open3D 0.17 TriangleMeshFactory.cpp,
+    third-party, absent here; pinned by the reference fixture extracted_face_mask_multiple_meshes.npy): poles (0, 0, +-r),
+    then rings i = 1 .. res-1 of 2 res vertices (sin a cos t, sin a sin t, cos a) r with a = pi i / res, t = pi j / res;
+    triangles: per j the two pole fans (0, 2+j, 2+j1) and (1, b+j1, b+j), then per ring pair (b2+j, b1+j1, b1+j),
+    (b2+j, b2+j1, b1+j1). Positions computed in double, then float32 + center (the reference's FromLegacy + offset,
+    cpp/tests/test_utils/geometry.cpp:76-94)."""
+    V = [(0.0, 0.0, radius), (0.0, 0.0, -radius)]
+    step = np.pi / resolution
+    for i in range(1, resolution):
+        a = step * i
+        for j in range(2 * resolution):
+            t = step * j
+            V.append((np.sin(a) * np.cos(t) * radius, np.sin(a) * np.sin(t) * radius, np.cos(a) * radius))
+    F = []
+    ring = 2 * resolution
+    for j in range(ring):
+        j1 = (j + 1) % ring
+        F.append((0, 2 + j, 2 + j1))
+        b = 2 + ring * (resolution - 2)
+        F.append((1, b + j1, b + j))
+    for i in range(1, resolution - 1):
+        b1 = 2 + ring * (i - 1)
+        b2 = b1 + ring
+        for j in range(ring):
+            j1 = (j + 1) % ring
+            F.append((b2 + j, b1 + j1, b1 + j))
+            F.append((b2 + j, b2 + j1, b1 + j1))
+    return np.array(V, np.float64).astype(np.float32) + np.asarray(center, np.float32), np.array(F, np.int64)
+
+
+def read_depth_png(path):
+    """16-bit PNG depth (PIL), as Open3D io::ReadImage gives it"""
+    from PIL import Image
+    return np.array(Image.open(path))
+
+
+def neighbours_valid(valid):
+    """pixels whose four 4-neighbours are all valid (the domain the ordered-normals fixture defines)"""
+    nb = np.zeros_like(valid)
+    nb[1:-1, 1:-1] = valid[:-2, 1:-1] & valid[2:, 1:-1] & valid[1:-1, :-2] & valid[1:-1, 2:]
+    return nb
+
+
 def read_ply(path):
     """Binary little-endian PLY (Blender export: x y z nx ny nz s t; faces as uchar count + uint indices). Quads are
     fan-triangulated (0,1,2),(0,2,3)."""

@@ -29,6 +29,10 @@ COPY = [
     "cpp/tests/test_data/arrays/node_translations_25-node_plane.npy",
     "cpp/tests/test_data/meshes/plane_skin_25_nodes_source.ply",
     "cpp/tests/test_data/meshes/plane_skin_25_nodes_target.ply",
+    "cpp/tests/test_data/arrays/extracted_face_vertices_multiple_meshes.npy",
+    "cpp/tests/test_data/arrays/extracted_face_mask_multiple_meshes.npy",
+    "cpp/tests/test_data/arrays/red_shorts_200_normals.npy",
+    "cpp/tests/test_data/images/red_shorts_200_depth.png",
 ]
 
 
@@ -88,5 +92,6 @@ def dense_depth_jacobian_goldens(count=64, seed=7):
 
 if __name__ == "__main__":
     copy_fixtures()
-    dense_depth_jacobian_goldens()
+    if "--copy-only" not in sys.argv:
+        dense_depth_jacobian_goldens()
     print("golden fixtures written to", HERE)

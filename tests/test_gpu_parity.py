@@ -77,7 +77,7 @@ def test_warp_bit_exact(nn, S, oracle_mod, extrinsic):
         E[:3, 3] = [0.01, -0.005, 0.02]
     wp_o, wn_o = oracle_mod.warp_mesh(sc.points, sc.normals, sc.nodes, sc.gt_rotations, sc.gt_translations, a, w, E)
     m = nn.geometry.functional.warp_triangle_mesh(nn.geometry.TriangleMesh(sc.points, sc.normals, sc.faces), sc.nodes, sc.gt_rotations,
-                                                  sc.gt_translations, a, w, E)
+                                                  sc.gt_translations, a, w, extrinsics=np.eye(4) if E is None else E)
     assert np.array_equal(wp_o, _np(m.vertex_positions))
     assert np.array_equal(wn_o, _np(m.vertex_normals))
 
@@ -183,7 +183,7 @@ def test_interpolate_and_unproject(nn, S, oracle_mod):
     assert np.array_equal(r, _np(g))
     depth = np.where(dep[..., 0] > 0, dep[..., 0], 0).astype(np.float32) * 1000.0
     p_o, m_o = oracle_mod.unproject(depth, sc.K, 1000.0, 10.0)
-    p_g, m_g = nn.geometry.functional.unproject_raster_depth_without_filtering(depth, sc.K, 1000.0, 10.0)
+    p_g, m_g = nn.geometry.functional.unproject_raster_depth_without_filtering(depth, sc.K, depth_scale=1000.0, depth_max=10.0)
     assert np.array_equal(p_o, _np(p_g)) and np.array_equal(m_o, _np(m_g))
 
 
@@ -830,7 +830,7 @@ def test_normals_bit_exact(nn, S, oracle_mod, name):
         assert np.array_equal(vn, oracle_mod.vertex_normals(sc.points, sc.faces, normalized))
     assert np.array_equal(_np(mesh.vertex_normals), vn)
     depth = scene_target(oracle_mod, sc)
-    pts, _ = nn.geometry.functional.unproject_raster_depth_without_filtering(depth, sc.K, 1.0, 10.0)
+    pts, _ = nn.geometry.functional.unproject_raster_depth_without_filtering(depth, sc.K, depth_scale=1.0, depth_max=10.0)
     on = _np(G.functional.compute_ordered_point_cloud_normals(pts, (sc.H, sc.W)))
     assert np.array_equal(on, oracle_mod.ordered_point_cloud_normals(_np(pts), sc.H, sc.W))
     with pytest.raises(RuntimeError):

@@ -5,7 +5,8 @@ import os
 import numpy as np
 import pytest
 
-from _util import FIXTURES, GOLDEN, read_ply, rel_err, render_target_oracle, subdivide_midpoint, transform_mesh, xy_plane
+from _util import (FIXTURES, GOLDEN, neighbours_valid, read_depth_png, read_ply, rel_err, render_target_oracle, sphere_open3d,
+                   subdivide_midpoint, transform_mesh, xy_plane)
 from golden import kat_literals as L
 
 
@@ -213,3 +214,84 @@ def test_normals_restatement_properties(oracle_mod):
     assert np.array_equal(O.vertex_normals(v, f)[:, 2], np.ones(4, np.float32))
     z = O.triangle_normals(np.zeros((3, 3), np.float32), np.array([[0, 1, 2]]), normalized=True)
     assert np.array_equal(z, np.zeros((1, 3), np.float32))   # Eigen normalize leaves zero vectors at zero
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# round 2: the remaining in-container reference KATs / fixtures on the nnrt.geometry.functional / rendering surface
+# ---------------------------------------------------------------------------------------------------------------------
+def _sorted_desc(a):
+    return -np.sort(-np.asarray(a), axis=1)
+
+
+def test_anchor_variable_weight_kat(oracle_mod):
+    # cpp/tests/test_anchor_computation.cpp:30-83: 2 nodes for 4 anchors (empty slots -1 / weight 0)
+    a, w = oracle_mod.compute_anchors(L.ANCHOR_VAR_VERTICES, L.ANCHOR_VAR_NODES, 4, node_weights=L.ANCHOR_VAR_NODE_WEIGHTS)
+    assert np.array_equal(_sorted_desc(a), L.ANCHOR_VAR_ANCHORS_SORTED)
+    assert np.allclose(_sorted_desc(w), L.ANCHOR_VAR_WEIGHTS_SORTED, rtol=1e-3, atol=1e-6)
+
+
+def test_unproject_kat(oracle_mod):
+    # cpp/tests/test_unproject_3d_points.cpp:30-78 (uint16 depth, scale 1000, max 3)
+    p, m = oracle_mod.unproject_image(L.UNPROJECT_DEPTH, L.UNPROJECT_K, None, 1000.0, 3.0)
+    assert np.allclose(p, L.UNPROJECT_POINTS, rtol=1e-5, atol=1e-8)
+    assert np.array_equal(m, L.UNPROJECT_MASK)
+
+
+def test_unproject_extrinsics_is_pose_transform(oracle_mod):
+    # extrinsics E -> points in the frame of E^-1 (PerspectiveProjectionImpl.h:88-89): E applied to them gives camera points
+    rng = np.random.default_rng(3)
+    depth = rng.uniform(0.5, 2.5, (6, 7)).astype(np.float32)
+    c, s = np.cos(0.3), np.sin(0.3)
+    E = np.array([[c, -s, 0, 0.1], [s, c, 0, -0.2], [0, 0, 1, 0.3], [0, 0, 0, 1]])
+    p0, m0 = oracle_mod.unproject_image(depth, L.UNPROJECT_K, None, 1.0, 3.0)
+    p1, m1 = oracle_mod.unproject_image(depth, L.UNPROJECT_K, E, 1.0, 3.0)
+    assert np.array_equal(m0, m1)
+    back = p1.astype(np.float64) @ E[:3, :3].T + E[:3, 3]
+    assert np.allclose(back, p0, atol=1e-6)
+
+
+def test_multiple_meshes_ndc_fixture(oracle_mod):
+    # cpp/tests/test_extract_face_vertices.cpp:72-100: faces of [plane, sphere] concatenated in mesh order
+    V0, _, F0 = xy_plane(1.2615, (0, 0, 1), 4)
+    V1, F1 = sphere_open3d(0.4, 32, (0.0, 0.0, 0.5))
+    K = np.array([[580., 0., 320.], [0., 580., 240.], [0., 0., 1.]])
+    a, ma = oracle_mod.extract_face_ndc(V0, F0, K, 480, 640, 0.0, 2.0)
+    b, mb = oracle_mod.extract_face_ndc(V1, F1, K, 480, 640, 0.0, 2.0)
+    mask = np.concatenate([ma, mb]).astype(bool)
+    ndc = np.concatenate([a, b]).reshape(-1, 3, 3)
+    ndc[~mask] = 0
+    gv = np.load(os.path.join(FIXTURES, "extracted_face_vertices_multiple_meshes.npy"))
+    gm = np.load(os.path.join(FIXTURES, "extracted_face_mask_multiple_meshes.npy"))
+    assert mask.sum() == L.MULTI_MESH_KEPT and np.array_equal(mask, gm)
+    n = L.MULTI_MESH_COMPARED_FACES
+    assert np.allclose(ndc[:n], gv[:n], atol=1e-5)
+
+
+def test_red_shorts_ordered_normals_fixture(oracle_mod):
+    # cpp/tests/test_normals_operations.cpp:113-136: the fixture is reproduced bit for bit on every pixel whose four
+    # neighbours have depth (the tensor unprojection at scale 1000, then the ordered normals); elsewhere it holds zeros
+    depth = read_depth_png(os.path.join(FIXTURES, "red_shorts_200_depth.png"))
+    H, W = depth.shape
+    p, _ = oracle_mod.unproject_image(depth, L.RED_SHORTS_K, None, 1000.0, 1000.0)
+    n = oracle_mod.ordered_point_cloud_normals(p, H, W).reshape(H, W, 3)
+    gt = np.load(os.path.join(FIXTURES, "red_shorts_200_normals.npy"))
+    inner = neighbours_valid(depth > 0)
+    assert np.array_equal(n[inner], gt[inner])
+    assert not gt[~inner].any()
+
+
+def test_warp_points_threshold_semantics(oracle_mod):
+    # BlendWarp_ValidAnchorCountThreshold (WarpUtilities.h:505-580): points with fewer valid anchors than the minimum
+    # stay zero; with online threshold anchors the -1 slots are exactly the ones beyond 2c
+    rng = np.random.default_rng(5)
+    nodes = rng.uniform(-1, 1, (12, 3)).astype(np.float32)
+    pts = rng.uniform(-1.2, 1.2, (300, 3)).astype(np.float32)
+    R = np.tile(np.eye(3, dtype=np.float32), (12, 1, 1))
+    t = rng.normal(0, 0.1, (12, 3)).astype(np.float32)
+    a, w = oracle_mod.compute_anchors(pts, nodes, 4, 0.3, minimum_valid_anchor_count=0, threshold=True)
+    valid = (a != -1).sum(1)
+    assert 0 < (valid < 2).sum() < len(pts)
+    wp, _ = oracle_mod.warp_points(pts, None, nodes, R, t, a, w, minimum_valid=2)
+    assert not wp[valid < 2].any()
+    ref, _ = oracle_mod.warp_points(pts, None, nodes, R, t, a, w)
+    assert np.array_equal(wp[valid >= 2], ref[valid >= 2])

@@ -46,7 +46,7 @@ def main():
     wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, True, 4, 1, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE, 1)
     wf.set_node_rotations(sc.gt_rotations)
     wf.set_node_translations(sc.gt_translations)
-    pts, _ = G.functional.unproject_raster_depth_without_filtering(depth, K, 1.0, 10.0)
+    pts, _ = G.functional.unproject_raster_depth_without_filtering(depth, K, depth_scale=1.0, depth_max=10.0)
     normals = G.functional.compute_ordered_point_cloud_normals(pts, (H, W))
     none = np.zeros((0, 3), np.int32)
 
