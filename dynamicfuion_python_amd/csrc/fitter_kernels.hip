@@ -329,7 +329,13 @@ constexpr int NG_STRIDE = 49;
 constexpr int NG_ROWS = 8;     // pixel rows per wave (8 x NG_ROWS pixels)
 static_assert(2 * NG_ROWS == PIX_TILE, "pass 2 walks the pass-1 tiles");
 
+#if NNRT_FIT_VARIANT == 70   // experiment: no accumulator atomics (timing only)
+__device__ inline void ng_flush(double* dst, double v) {
+	if (v == 1.2345e300) *dst = v;
+}
+#else
 __device__ inline void ng_flush(double* dst, double v) { atomicAdd(dst, v); }
+#endif
 
 template <int MODE, int MAXK>
 __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_grouped(FitPixelArgs a) {
@@ -459,6 +465,9 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 	int4 d = make_int4(0, -1, -1, -1);
 	float4 jv[3], jn[3];
 	auto gather = [&](const float* slots, int count) {
+#if NNRT_FIT_VARIANT == 72
+		return;
+#endif
 		d = make_int4(0, -1, -1, -1);
 		if (lane < count)
 			d = make_int4(__builtin_bit_cast(int, slots[lane]), __builtin_bit_cast(int, slots[NG_STRIDE + lane]),
@@ -476,6 +485,10 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 	};
 	// (2b) J and r of association `lane` into its slot
 	auto jacobians = [&](float* slots, int count) {
+#if NNRT_FIT_VARIANT == 72   // experiment: no Jacobians, no gathers (timing only)
+		if (lane < count) slots[lane] = 0.f;
+		return;
+#endif
 		if (lane >= count && lane < NG_CAP) {   // padding: zero products, continuing the chunk's last node
 			const float last = slots[7 * NG_STRIDE + count - 1];
 #pragma unroll
@@ -535,6 +548,10 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 	// (3) exact sums of the chunk's products per node
 	auto sums = [&](const float* slots, int count) {
 		(void)count;
+#if NNRT_FIT_VARIANT == 71 || NNRT_FIT_VARIANT == 72   // experiment: no sums (timing only)
+		acc += slots[lane];
+		return;
+#endif
 #pragma unroll
 		for (int j = 0; j < SEG; j += NG_BATCH) {
 			// every LDS read of the batch is issued before the dependent double adds

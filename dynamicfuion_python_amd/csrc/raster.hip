@@ -6,8 +6,8 @@
 // (float depth bits << 32 | face) with a global atomicMin. The minimum key is exactly the lexicographic (depth, face)
 // winner that the reference's queue logic selects, so no bin capacity (and no silent truncation) exists. A resolve pass
 // recomputes the winner's barycentrics/depth with the same device function, bit-identically.
-// faces_per_pixel > 1 (API only): 16x16-pixel tiles; every face is binned into the tiles its box touches, bin lists are
-// sorted by face index and each pixel walks its tile's list with the reference's bounded queue.
+// faces_per_pixel > 1 (API only): per-pixel lists of the faces that pass the full test at the pixel centre (count, scan,
+// fill), each replayed in ascending face order through the reference's bounded queue.
 #include "kernels.hpp"
 
 #include <hipcub/hipcub.hpp>
@@ -296,67 +296,40 @@ nnrt_status launch_raster_resolve(const float* face_ndc, int64_t F, const Raster
 }
 
 // =====================================================================================================================
-// faces_per_pixel > 1: tile-binned queues (API path)
+// faces_per_pixel > 1 (API path): per-pixel hit lists. Every face walks the exact pixel range of its box (as the K = 1
+// scatter) running the full face test; pass A counts the hits per pixel, a scan places the lists, pass B appends the
+// face indices. One lane per pixel then sorts its list by face index -- the ascending order in which the reference's
+// bounded queue visits a bin's faces -- and replays that queue (RayFaceIntersection.h:162-255: the first K hits, then a
+// hit replaces the current deepest only when strictly nearer), then orders the queue by (depth, face)
+// (RayFaceIntersection.h:42-45). Work is proportional to the hits, not to the faces binned per tile, so dense meshes of
+// tiny faces (millions of sub-pixel triangles) cost what the K = 1 scatter costs.
 // =====================================================================================================================
-constexpr int TILE = 16;
-
-__device__ inline bool face_tile_range(const FaceNdc& fn, const RasterOptions& o, int& tx0, int& tx1, int& ty0, int& ty1) {
-	if (!face_finite(fn)) return false;
-	const float area = spa_cw(fn.x[0], fn.y[0], fn.x[1], fn.y[1], fn.x[2], fn.y[2]);
-	const bool zero_area = (area <= K_EPSILON && area >= -1.f * K_EPSILON);
-	const bool zinv = fmax3f(fn.z[0], fn.z[1], fn.z[2]) < K_EPSILON;
-	if ((o.cull_back_faces && area < 0.f) || zero_area || zinv) return false;
-	const float xmin = fmin3f(fn.x[0], fn.x[1], fn.x[2]) - o.blur, xmax = fmax3f(fn.x[0], fn.x[1], fn.x[2]) + o.blur;
-	const float ymin = fmin3f(fn.y[0], fn.y[1], fn.y[2]) - o.blur, ymax = fmax3f(fn.y[0], fn.y[1], fn.y[2]) + o.blur;
-	if (!(xmax >= xmin) || !(ymax >= ymin)) return false;
+template <bool FILL>
+__global__ __launch_bounds__(256) void k_hit_lists(const float* __restrict__ face_ndc, const uint8_t* __restrict__ mask, int64_t F,
+                                                   RasterOptions o, int* __restrict__ counts, const int* __restrict__ offsets,
+                                                   int32_t* __restrict__ lists) {
+	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (f >= F || (mask && !mask[f])) return;
+	const FaceNdc fn = load_face_ndc(face_ndc, f);
 	int u0, u1, v0, v1;
-	pixel_span(xmin, xmax, o.W, o.H, &u0, &u1);
-	pixel_span(ymin, ymax, o.H, o.W, &v0, &v1);
-	if (u0 > u1 || v0 > v1) return false;
-	tx0 = u0 / TILE;
-	tx1 = u1 / TILE;
-	ty0 = v0 / TILE;
-	ty1 = v1 / TILE;
-	return true;
-}
-
-__global__ void k_tile_count(const float* __restrict__ face_ndc, const uint8_t* __restrict__ mask, int64_t F, RasterOptions o, int tiles_x,
-                             int* __restrict__ counts) {
-	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-	if (f >= F || (mask && !mask[f])) return;
-	int tx0, tx1, ty0, ty1;
-	if (!face_tile_range(load_face_ndc(face_ndc, f), o, tx0, tx1, ty0, ty1)) return;
-	for (int ty = ty0; ty <= ty1; ty++)
-		for (int tx = tx0; tx <= tx1; tx++) atomicAdd(counts + ty * tiles_x + tx, 1);
-}
-
-__global__ void k_tile_fill(const float* __restrict__ face_ndc, const uint8_t* __restrict__ mask, int64_t F, RasterOptions o, int tiles_x,
-                            const int* __restrict__ offsets, int* __restrict__ cursor, int32_t* __restrict__ lists) {
-	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-	if (f >= F || (mask && !mask[f])) return;
-	int tx0, tx1, ty0, ty1;
-	if (!face_tile_range(load_face_ndc(face_ndc, f), o, tx0, tx1, ty0, ty1)) return;
-	for (int ty = ty0; ty <= ty1; ty++)
-		for (int tx = tx0; tx <= tx1; tx++) {
-			const int t = ty * tiles_x + tx;
-			lists[offsets[t] + atomicAdd(cursor + t, 1)] = static_cast<int32_t>(f);
+	if (!face_pixel_range(fn, o, u0, u1, v0, v1)) return;
+	const float w = (fmax3f(fn.x[0], fn.x[1], fn.x[2]) - fmin3f(fn.x[0], fn.x[1], fn.x[2])) + 2.f * o.blur;
+	const float hh = (fmax3f(fn.y[0], fn.y[1], fn.y[2]) - fmin3f(fn.y[0], fn.y[1], fn.y[2])) + 2.f * o.blur;
+	const bool near_all = (w * w + hh * hh) < 0.5f * o.blur;   // A13: every box pixel passes the distance test
+	const float inv_w = rcp_rn(static_cast<float>(o.W)), inv_h = rcp_rn(static_cast<float>(o.H));
+	const float inv_area = face_inv_area(fn);
+	for (int v = v0; v <= v1; v++) {
+		const float py = pixel_to_ndc_r(v, o.H, o.W, inv_h);
+		for (int u = u0; u <= u1; u++) {
+			const float px = pixel_to_ndc_r(u, o.W, o.H, inv_w);
+			RasterHit h;
+			const bool hit = near_all ? face_test<false>(fn, px, py, o.blur, o.perspective, o.clip_barycentric, o.cull_back_faces, h, inv_area)
+			                          : face_test<true>(fn, px, py, o.blur, o.perspective, o.clip_barycentric, o.cull_back_faces, h, inv_area);
+			if (!hit) continue;
+			const int64_t p = static_cast<int64_t>(v) * o.W + u;
+			const int slot = atomicAdd(counts + p, 1);
+			if constexpr (FILL) lists[offsets[p] + slot] = static_cast<int32_t>(f);
 		}
-}
-
-// per-tile insertion sort of the (short) face list so the per-pixel walk visits faces in ascending order
-__global__ void k_tile_sort(const int* __restrict__ offsets, int tiles, int32_t* __restrict__ lists) {
-	const int t = blockIdx.x * blockDim.x + threadIdx.x;
-	if (t >= tiles) return;
-	int32_t* l = lists + offsets[t];
-	const int n = offsets[t + 1] - offsets[t];
-	for (int i = 1; i < n; i++) {
-		int32_t x = l[i];
-		int j = i - 1;
-		while (j >= 0 && l[j] > x) {
-			l[j + 1] = l[j];
-			j--;
-		}
-		l[j + 1] = x;
 	}
 }
 
@@ -365,19 +338,29 @@ struct QEntry {
 	int32_t face;
 };
 
-__global__ __launch_bounds__(256) void k_tile_raster(const float* __restrict__ face_ndc, RasterOptions o, int tiles_x, int K,
-                                                     const int* __restrict__ offsets, const int32_t* __restrict__ lists,
-                                                     int64_t* __restrict__ out_face, float* __restrict__ out_depth, float* __restrict__ out_bary,
-                                                     float* __restrict__ out_dist) {
-	const int tile = blockIdx.x;
-	const int u = (tile % tiles_x) * TILE + (threadIdx.x % TILE), v = (tile / tiles_x) * TILE + (threadIdx.x / TILE);
-	if (u >= o.W || v >= o.H) return;
+__global__ __launch_bounds__(256) void k_hit_resolve(const float* __restrict__ face_ndc, RasterOptions o, int K, const int* __restrict__ offsets,
+                                                     int32_t* __restrict__ lists, int64_t* __restrict__ out_face, float* __restrict__ out_depth,
+                                                     float* __restrict__ out_bary, float* __restrict__ out_dist) {
+	const int64_t p = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (p >= static_cast<int64_t>(o.H) * o.W) return;
+	const int v = static_cast<int>(p / o.W), u = static_cast<int>(p % o.W);
 	const float px = pixel_to_ndc(u, o.W, o.H), py = pixel_to_ndc(v, o.H, o.W);
+	int32_t* l = lists + offsets[p];
+	const int n = offsets[p + 1] - offsets[p];
+	for (int i = 1; i < n; i++) {   // ascending face index (the lists are short: the faces covering this pixel centre)
+		const int32_t x = l[i];
+		int j = i - 1;
+		while (j >= 0 && l[j] > x) {
+			l[j + 1] = l[j];
+			j--;
+		}
+		l[j + 1] = x;
+	}
 	QEntry q[MAX_FACES_PER_PIXEL];
 	int qs = 0, qat = -1;
 	float qmax = -1000.f;
-	for (int i = offsets[tile]; i < offsets[tile + 1]; i++) {
-		const int32_t f = lists[i];
+	for (int i = 0; i < n; i++) {
+		const int32_t f = l[i];
 		RasterHit h;
 		if (!face_test(load_face_ndc(face_ndc, f), px, py, o.blur, o.perspective, o.clip_barycentric, o.cull_back_faces, h)) continue;
 		const QEntry e{h.depth, h.dist, h.b0, h.b1, h.b2, f};
@@ -398,8 +381,7 @@ __global__ __launch_bounds__(256) void k_tile_raster(const float* __restrict__ f
 				}
 		}
 	}
-	// sort by (depth, face): RayFaceIntersection.h:42-45
-	for (int i = 1; i < qs; i++) {
+	for (int i = 1; i < qs; i++) {   // (depth, face): RayFaceIntersection.h:42-45
 		QEntry x = q[i];
 		int j = i - 1;
 		while (j >= 0 && (q[j].depth > x.depth || (q[j].depth == x.depth && q[j].face > x.face))) {
@@ -408,7 +390,6 @@ __global__ __launch_bounds__(256) void k_tile_raster(const float* __restrict__ f
 		}
 		q[j + 1] = x;
 	}
-	const int64_t p = static_cast<int64_t>(v) * o.W + u;
 	for (int i = 0; i < K; i++) {
 		const int64_t o_ = p * K + i;
 		if (i < qs) {
@@ -429,37 +410,33 @@ __global__ __launch_bounds__(256) void k_tile_raster(const float* __restrict__ f
 
 nnrt_status launch_raster_multi(const float* face_ndc, const uint8_t* mask, int64_t F, const RasterOptions& o, int faces_per_pixel,
                                 int64_t* out_face, float* out_depth, float* out_bary, float* out_dist, hipStream_t stream) {
-	const int tiles_x = static_cast<int>(ceil_div(o.W, TILE)), tiles_y = static_cast<int>(ceil_div(o.H, TILE));
-	const int tiles = tiles_x * tiles_y;
-	int *counts = nullptr, *offsets = nullptr, *cursor = nullptr;
+	const int64_t P = static_cast<int64_t>(o.H) * o.W;
+	NNRT_CHECK_ARG(P < (int64_t(1) << 31), "image too large");
+	int *counts = nullptr, *offsets = nullptr;
 	int32_t* lists = nullptr;
 	void* tmp = nullptr;
 	size_t tmp_bytes = 0;
-	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&counts), sizeof(int) * (tiles + 1), stream));
-	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&offsets), sizeof(int) * (tiles + 1), stream));
-	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&cursor), sizeof(int) * tiles, stream));
-	NNRT_HIP(hipMemsetAsync(counts, 0, sizeof(int) * (tiles + 1), stream));
-	NNRT_HIP(hipMemsetAsync(cursor, 0, sizeof(int) * tiles, stream));
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&counts), sizeof(int) * (P + 1), stream));
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&offsets), sizeof(int) * (P + 1), stream));
+	NNRT_HIP(hipMemsetAsync(counts, 0, sizeof(int) * (P + 1), stream));
 	const unsigned fg = static_cast<unsigned>(ceil_div(F > 0 ? F : 1, 256));
-	if (F > 0) k_tile_count<<<fg, 256, 0, stream>>>(face_ndc, mask, F, o, tiles_x, counts);
+	if (F > 0) k_hit_lists<false><<<fg, 256, 0, stream>>>(face_ndc, mask, F, o, counts, nullptr, nullptr);
 	NNRT_LAUNCH_CHECK();
-	NNRT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts, offsets, tiles + 1, stream));
+	NNRT_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, counts, offsets, static_cast<int>(P + 1), stream));
 	NNRT_HIP(hipMallocAsync(&tmp, tmp_bytes, stream));
-	NNRT_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, counts, offsets, tiles + 1, stream));
+	NNRT_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, counts, offsets, static_cast<int>(P + 1), stream));
 	int total = 0;
-	NNRT_HIP(hipMemcpyAsync(&total, offsets + tiles, sizeof(int), hipMemcpyDeviceToHost, stream));
+	NNRT_HIP(hipMemcpyAsync(&total, offsets + P, sizeof(int), hipMemcpyDeviceToHost, stream));
+	NNRT_HIP(hipMemsetAsync(counts, 0, sizeof(int) * (P + 1), stream));
 	NNRT_HIP(hipStreamSynchronize(stream));
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&lists), sizeof(int32_t) * (total > 0 ? total : 1), stream));
-	if (F > 0) k_tile_fill<<<fg, 256, 0, stream>>>(face_ndc, mask, F, o, tiles_x, offsets, cursor, lists);
+	if (F > 0) k_hit_lists<true><<<fg, 256, 0, stream>>>(face_ndc, mask, F, o, counts, offsets, lists);
 	NNRT_LAUNCH_CHECK();
-	k_tile_sort<<<static_cast<unsigned>(ceil_div(tiles, 64)), 64, 0, stream>>>(offsets, tiles, lists);
-	NNRT_LAUNCH_CHECK();
-	k_tile_raster<<<tiles, TILE * TILE, 0, stream>>>(face_ndc, o, tiles_x, faces_per_pixel, offsets, lists, out_face, out_depth, out_bary,
-	                                                   out_dist);
+	k_hit_resolve<<<static_cast<unsigned>(ceil_div(P, 256)), 256, 0, stream>>>(face_ndc, o, faces_per_pixel, offsets, lists, out_face, out_depth,
+	                                                                          out_bary, out_dist);
 	NNRT_LAUNCH_CHECK();
 	NNRT_HIP(hipFreeAsync(counts, stream));
 	NNRT_HIP(hipFreeAsync(offsets, stream));
-	NNRT_HIP(hipFreeAsync(cursor, stream));
 	NNRT_HIP(hipFreeAsync(lists, stream));
 	NNRT_HIP(hipFreeAsync(tmp, stream));
 	return NNRT_OK;

@@ -238,3 +238,24 @@ def test_median_grid_subsample(nn):
     pts = np.random.default_rng(11).uniform(-1, 1, (600, 3)).astype(np.float32)
     got = _np(nn.geometry.functional.median_grid_subsample_3d_points(pts, 0.5))
     assert np.array_equal(got, _medoids_reference(pts, 0.5))
+
+
+@pytest.mark.parametrize("kf", [1, 3, 8])
+def test_rasterize_dense_sphere_array_vs_oracle(nn, oracle_mod, kf):
+    """A dense mesh of sub-pixel triangles (the regime of the reference's 64-bunny benchmark, README.md:21-25): every
+    fragment (face, depth, barycentrics, distance) identical to the oracle at K = 1, 3, 8."""
+    from _util import sphere_open3d
+    V1, F1 = sphere_open3d(0.06, 24)
+    Vs, Fs = [], []
+    for a in range(8):
+        for c in range(8):
+            Fs.append(F1 + len(V1) * len(Vs))
+            Vs.append(V1 + np.array([(a - 3.5) * 0.11, (c - 3.5) * 0.085, 1.0 + 0.05 * ((a + c) % 3)], np.float32))
+    V, F = np.concatenate(Vs), np.concatenate(Fs)
+    K = np.array([[580., 0., 320.], [0., 580., 240.], [0., 0., 1.]])
+    ndc, mask = oracle_mod.extract_face_ndc(V, F, K, 480, 640, 0.0, 10.0)
+    ref = oracle_mod.rasterize(ndc, mask, 480, 640, 0.0, kf, -1, -1, False, False, True)
+    got = nn.rendering.rasterize_ndc_triangles(ndc, mask, (480, 640), 0.0, kf, -1, -1, False, False, True)
+    for r, g in zip(ref, got):
+        assert np.array_equal(np.asarray(r).reshape(-1), _np(g).reshape(-1))
+    assert (_np(got[0])[..., 0] >= 0).sum() > 1000
