@@ -373,6 +373,7 @@ struct nnrt_fitter {
 	DeviceBuffer<int4> faces4;
 	DeviceBuffer<int32_t> anchors;
 	DeviceBuffer<float> weights;
+	DeviceBuffer<uint32_t> face_nodes;   // [F, face_node_slots(K)] distinct anchor nodes per face (once per frame)
 	DeviceBuffer<float4> wpos, wnrm, jv, jn;
 	DeviceBuffer<float4> ref_points;   // [P] reference point (x, y, z, valid)
 	DeviceBuffer<float4> records;      // [P, 4] pixel Jacobian records
@@ -494,6 +495,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 	fa.wpos = ft->wpos.ptr;
 	fa.wnrm = ft->wnrm.ptr;
 	fa.anchors = ft->anchors.ptr;
+	fa.face_nodes = ft->face_nodes.ptr;
 	fa.jv = ft->jv.ptr;
 	fa.jn = ft->jn.ptr;
 	fa.ref_points = ft->ref_points.ptr;
@@ -606,6 +608,7 @@ void nnrt_fitter_destroy(nnrt_fitter* ft) {
 		b->release();
 	ft->faces4.release();
 	ft->anchors.release();
+	ft->face_nodes.release();
 	ft->wpos.release();
 	ft->wnrm.release();
 	ft->jv.release();
@@ -652,6 +655,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	const int64_t P = static_cast<int64_t>(H) * W;
 	const int N = wf->N, K = wf->anchor_count, E = wf->E();
 	NNRT_CHECK_ARG(N >= K, "the warp field has fewer nodes than anchors per vertex");
+	NNRT_CHECK_ARG(N < FACE_NODE_MAX_NODES, "node count exceeds the face-node table's 20-bit node field");
 	if (E > 0) {
 		for (int i = 0; i < ft->p.iteration_mode_count; i++)
 			if (ft->p.iteration_modes[i] != NNRT_ITERATION_ALL) {
@@ -660,10 +664,12 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 			}
 	}
 	// (re)allocate; any reallocation invalidates captured graphs
-	const auto before = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->a_schur.ptr);
+	const auto before = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->a_schur.ptr,
+	                                    ft->face_nodes.ptr);
 	nnrt_status st;
 	if ((st = ft->mesh_p.ensure(3 * V)) || (st = ft->mesh_n.ensure(3 * V)) || (st = ft->faces4.ensure(F)) ||
 	    (st = ft->anchors.ensure(static_cast<size_t>(V) * K)) || (st = ft->weights.ensure(static_cast<size_t>(V) * K)) ||
+	    (st = ft->face_nodes.ensure(static_cast<size_t>(F) * face_node_slots(K))) ||
 	    (st = ft->wpos.ensure(V)) || (st = ft->wnrm.ensure(V)) || (st = ft->jv.ensure(static_cast<size_t>(V) * K)) ||
 	    (st = ft->jn.ensure(static_cast<size_t>(V) * K)) || (st = ft->ref_points.ensure(P)) || (st = ft->records.ensure(4 * P)) || (st = ft->keys.ensure(P)) ||
 	    (st = ft->residuals.ensure(P)) || (st = ft->residual_mask.ensure(P)) || (st = ft->pixel_face.ensure(P)) ||
@@ -739,7 +745,8 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 		ft->aw.edge_offsets = ft->a_offsets.ptr;
 		ft->aw.edge_list = ft->a_list.ptr;
 	}
-	const auto after = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->a_schur.ptr);
+	const auto after = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->a_schur.ptr,
+	                                   ft->face_nodes.ptr);
 	// Captured graphs bake every buffer pointer and the per-frame constants (NDC setup, pixel camera, extrinsics) into
 	// their kernel arguments: any change drops them. The warp field is recognised by its unique id, not its address.
 	const NdcSetup nndc = make_ndc_setup(h_K, H, W, ft->p.ndc_convention == NNRT_NDC_CONSISTENT);
@@ -775,6 +782,8 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	                                 wf->coverage_method == NNRT_MINIMAL_K_NEIGHBOR_NODE_DISTANCE ? wf->node_weights.ptr : nullptr,
 	                                 wf->threshold ? wf->minimum_valid : 0, ft->anchors.ptr, ft->weights.ptr, s)))
 		return st;
+	// the faces' distinct anchor nodes (AssociateFacesWithAnchors, :105), consumed by the node pass of every iteration
+	if ((st = launch_face_node_table(ft->faces4.ptr, F, ft->anchors.ptr, K, ft->face_nodes.ptr, s))) return st;
 	// reference point cloud (:289-306): depth / scale with 0 < d < max_depth, AND the user mask; stored as depth (0 = masked)
 	if (ref.depth)
 		k_prepare_reference_depth<<<static_cast<unsigned>(ceil_div(P, 256)), 256, 0, s>>>(ref.depth, ref.mask, H, W, ref.depth_scale,

@@ -307,13 +307,76 @@ __global__ __launch_bounds__(PIX_BLOCK, NNRT_FIT_VARIANT == 60 || NNRT_FIT_VARIA
 	FSTAMP(0, 2);
 }
 
+// ---- once per frame: the face -> distinct anchor node table (AssociateFacesWithAnchorsImpl.h:34-107) --------------------
+template <int MAXK>
+__global__ __launch_bounds__(256) void k_face_node_table(const int4* __restrict__ faces4, int64_t F, const int32_t* __restrict__ anchors, int K,
+                                                         uint32_t* __restrict__ out) {
+	constexpr int NS = 3 * MAXK;
+	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (f >= F) return;
+	const int4 fi = faces4[f];
+	const int vid[3] = {fi.x, fi.y, fi.z};
+	int node[NS];
+	uint32_t code[NS];
+	int n = 0;
+#pragma unroll
+	for (int fv = 0; fv < 3; fv++)
+		for (int k = 0; k < K; k++) {
+			const int a = anchors[static_cast<int64_t>(vid[fv]) * K + k];
+			if (a < 0) continue;
+			int at = -1;
+			for (int i = 0; i < n; i++)
+				if (node[i] == a) at = i;
+			if (at < 0) {
+				at = n++;
+				node[at] = a;
+				code[at] = 0xFFFu;
+			}
+			// per face vertex the LAST slot holding the node (ascending k overwrites)
+			code[at] = (code[at] & ~(0xFu << (4 * fv))) | (static_cast<uint32_t>(k) << (4 * fv));
+		}
+	for (int i = 1; i < n; i++) {   // ascending node
+		const int x = node[i];
+		const uint32_t c = code[i];
+		int j = i - 1;
+		while (j >= 0 && node[j] > x) {
+			node[j + 1] = node[j];
+			code[j + 1] = code[j];
+			j--;
+		}
+		node[j + 1] = x;
+		code[j + 1] = c;
+	}
+	uint32_t* o = out + f * NS;
+	for (int i = 0; i < NS; i++) o[i] = i < n ? (static_cast<uint32_t>(node[i]) << FACE_NODE_SHIFT) | code[i] : FACE_NODE_NONE;
+}
+
+nnrt_status launch_face_node_table(const int4* faces4, int64_t F, const int32_t* anchors, int K, uint32_t* out, hipStream_t stream) {
+	if (F == 0) return NNRT_OK;
+	const unsigned grid = static_cast<unsigned>(ceil_div(F, 256));
+	if (K <= 4) k_face_node_table<4><<<grid, 256, 0, stream>>>(faces4, F, anchors, K, out);
+	else k_face_node_table<MAX_ANCHORS><<<grid, 256, 0, stream>>>(faces4, F, anchors, K, out);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
+// minimum over the 64 lanes (DPP row shifts, then row broadcasts into lane 63), wave-uniform result
+__device__ inline int wave_min_i32(int v) {
+	v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x111, 0xf, 0xf, false));   // row_shr:1
+	v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x112, 0xf, 0xf, false));   // row_shr:2
+	v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x114, 0xf, 0xf, false));   // row_shr:4
+	v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x118, 0xf, 0xf, false));   // row_shr:8
+	v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+	v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
+	return __builtin_amdgcn_readlane(v, 63);
+}
+
 // ---- pass 2, node-grouped per wave --------------------------------------------------------------------------------
 // 8x8 pixels per wave (the K1 mapping); the wave's (pixel, node) associations are processed in chunks of NG_CAP.
-// (1) Group: a wave-uniform loop over anchor slots picks the next pending node (readlane of the first lane holding
-//     it in that slot); every lane matches it against its remaining slots with scalar wave masks (per face vertex the
-//     LAST matching slot: AssociateFacesWithAnchors) and the matching lanes file one association (pixel, vertex-anchor
-//     row per face vertex) at consecutive LDS positions (mbcnt) -- no LDS atomics, no hash. A node that does not fit
-//     the chunk is split: its first lanes are filed, the rest stay pending.
+// (1) Group: every contributing pixel lane holds its face's distinct anchor nodes in ascending order (the per-frame face
+//     table), so the wave's next node is the minimum of the lanes' list heads (one DPP reduction); the lanes whose head it
+//     is file one association each (pixel lane, the jv/jn row of every face vertex anchored to the node) at consecutive
+//     LDS positions (mbcnt) and advance their list. A node that does not fit the chunk continues in the next one.
 // (2) Jacobians: one association per lane (no idle lanes); J (S floats) and r overwrite the association's slot.
 // (3) Sums: the wave splits into 64 / GROUP lane groups; lane e of a group owns accumulator entry e (JJᵀ upper
 //     triangle, then J r) and walks its group's share of the chunk adding the float product J[c0] * J[c1] in double;
@@ -347,6 +410,7 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 	constexpr int SEG = NG_CAP / G;
 	constexpr int NG_BATCH = SEG % 8 == 0 ? 8 : 6;   // associations per group read ahead in (3)
 	static_assert(T::NACC <= GROUP && NG_CAP % G == 0 && SEG % NG_BATCH == 0 && NG_STRIDE >= NG_CAP && (NG_STRIDE & 1), "slot layout");
+	static_assert(NSLOT % 4 == 0, "face table rows are loaded as int4");
 	__shared__ float s_slots[PIX_BLOCK / 64][2][8 * NG_STRIDE];
 	__shared__ float s_rec[PIX_BLOCK / 64][16 * 64];                 // component-major pixel records
 
@@ -362,10 +426,10 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 	float* recs = s_rec[wave];
 	const int KA = a.anchor_count;
 
-	int anc[NSLOT];
+	uint32_t ent[NSLOT];   // this pixel's face: distinct anchor nodes still to be filed, ascending (head = ent[0])
 	int vid[3] = {0, 0, 0};
 #pragma unroll
-	for (int t = 0; t < NSLOT; t++) anc[t] = -1;
+	for (int t = 0; t < NSLOT; t++) ent[t] = FACE_NODE_NONE;
 	[[maybe_unused]] const unsigned long long t_start = FCLOCK();
 	unsigned long long t_jac = 0, t_sum = 0;
 	if (in_image) {
@@ -377,19 +441,24 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 			const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2], q3 = rec[3];
 			const int face = static_cast<int>(key & 0xffffffffu);
 			const int4 fi = a.faces4[face];
+			const uint4* fn4 = reinterpret_cast<const uint4*>(a.face_nodes + static_cast<int64_t>(face) * NSLOT);
+#pragma unroll
+			for (int t = 0; t < NSLOT / 4; t++) {
+				const uint4 e4 = fn4[t];
+				ent[4 * t] = e4.x;
+				ent[4 * t + 1] = e4.y;
+				ent[4 * t + 2] = e4.z;
+				ent[4 * t + 3] = e4.w;
+			}
 			vid[0] = fi.x;
 			vid[1] = fi.y;
 			vid[2] = fi.z;
-#pragma unroll
-			for (int fv = 0; fv < 3; fv++)
-#pragma unroll
-				for (int k = 0; k < MAXK; k++) anc[fv * MAXK + k] = (k < KA) ? a.anchors[static_cast<int64_t>(vid[fv]) * KA + k] : -1;
 			const float q[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
 #pragma unroll
 			for (int w = 0; w < 16; w++) recs[w * 64 + lane] = q[w];
 		}
 	}
-	if (FIT_STAMPS && __ballot(anc[NSLOT - 1] == 123456789) == 777ull) a.acc[0] = 0;   // stamp after the prologue loads
+	if (FIT_STAMPS && __ballot(ent[NSLOT - 1] == 123456789u) == 777ull) a.acc[0] = 0;   // stamp after the prologue loads
 	const unsigned long long t_loaded = FCLOCK();
 
 	// accumulator entry of this lane within its group
@@ -420,43 +489,31 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 
 	// (1) file up to NG_CAP associations into `slots`; returns the count (0: nothing pending)
 	const uint64_t lanes_below = (1ull << lane) - 1ull;
-	uint64_t pend[NSLOT];   // lanes whose slot t is still to be filed (wave masks: scalar registers)
-#pragma unroll
-	for (int t = 0; t < NSLOT; t++) pend[t] = __ballot(anc[t] >= 0);
 	auto group = [&](float* slots) -> int {
 		int filed = 0;
+		while (filed < NG_CAP) {
+			const int head = static_cast<int>(ent[0] >> FACE_NODE_SHIFT);   // FACE_NODE_MAX_NODES: list exhausted
+			const int X = wave_min_i32(head);
+			if (X == FACE_NODE_MAX_NODES) break;
+			const uint64_t M = __ballot(head == X);
+			if (M == 0) break;   // unreachable (X is some lane's head); guarantees progress
+			const int rank = __popcll(M & lanes_below);
+			const int room = NG_CAP - filed;
+			if (head == X && rank < room) {
+				const int pos = filed + rank;
+				const uint32_t code = ent[0];
+				slots[pos] = __builtin_bit_cast(float, lane);
 #pragma unroll
-		for (int s = 0; s < NSLOT; s++) {
-			while (filed < NG_CAP && pend[s] != 0) {
-				const int leader = __ffsll(static_cast<unsigned long long>(pend[s])) - 1;
-				const int X = __builtin_amdgcn_readlane(anc[s], leader);
-				uint64_t hs[NSLOT];
-				uint64_t M = 0;
-#pragma unroll
-				for (int t = s; t < NSLOT; t++) {   // slots before s are exhausted wave-wide
-					hs[t] = __ballot(anc[t] == X) & pend[t];
-					M |= hs[t];
+				for (int fv = 0; fv < 3; fv++) {
+					const int k = static_cast<int>((code >> (4 * fv)) & 0xFu);
+					slots[(1 + fv) * NG_STRIDE + pos] = __builtin_bit_cast(float, k != 0xF ? vid[fv] * KA + k : -1);
 				}
-				// lanes beyond the chunk's room stay pending (split node)
-				const int rank = __popcll(M & lanes_below);
-				const uint64_t keep = __ballot(__builtin_amdgcn_inverse_ballot_w64(M) && rank < NG_CAP - filed);
-				int kf[3] = {-1, -1, -1};
+				slots[7 * NG_STRIDE + pos] = __builtin_bit_cast(float, X);
 #pragma unroll
-				for (int t = s; t < NSLOT; t++) {
-					const uint64_t h = hs[t] & keep;
-					pend[t] &= ~h;
-					if (__builtin_amdgcn_inverse_ballot_w64(h)) kf[t / MAXK] = t % MAXK;   // per face vertex the LAST match
-				}
-				if (__builtin_amdgcn_inverse_ballot_w64(keep)) {
-					const int pos = filed + rank;
-					slots[pos] = __builtin_bit_cast(float, lane);
-#pragma unroll
-					for (int fv = 0; fv < 3; fv++)
-						slots[(1 + fv) * NG_STRIDE + pos] = __builtin_bit_cast(float, kf[fv] >= 0 ? vid[fv] * KA + kf[fv] : -1);
-					slots[7 * NG_STRIDE + pos] = __builtin_bit_cast(float, X);
-				}
-				filed += __popcll(keep);
+				for (int t = 0; t < NSLOT - 1; t++) ent[t] = ent[t + 1];
+				ent[NSLOT - 1] = FACE_NODE_NONE;
 			}
+			filed += min(__popcll(M), room);
 		}
 		return filed;
 	};

@@ -25,6 +25,7 @@ struct FitPixelArgs {
 	const float4* wpos;     // [V] warped positions
 	const float4* wnrm;     // [V] warped normals
 	const int32_t* anchors; // [V,K]
+	const uint32_t* face_nodes; // [F, face_node_slots(K)] per face: its unique anchor nodes, ascending (face_node_entry)
 	const float4* jv;       // [V,K] (-w R (v-g), w)
 	const float4* jn;       // [V,K] (-w R n, 0)
 	const float4* ref_points; // [P] reference point (x, y, z, valid)
@@ -46,6 +47,15 @@ struct SolveArgs {
 	float* hessian_out;     // [N*s*s] (nullable)
 	int* error_flag;
 };
+
+// Per face (once per frame, after the anchors): the face's distinct anchor nodes in ascending order, each with, per face
+// vertex, the LAST anchor slot holding it (AssociateFacesWithAnchorsImpl.h:34-107): entry = node << 12 | k2 << 8 | k1 << 4 | k0
+// (k = 0xF: the vertex does not anchor to the node), padded with FACE_NODE_NONE. Nodes must be < 2^20 - 1.
+constexpr uint32_t FACE_NODE_NONE = 0xFFFFFFFFu;
+constexpr int FACE_NODE_SHIFT = 12;
+constexpr int FACE_NODE_MAX_NODES = (1 << 20) - 1;
+inline int face_node_slots(int K) { return K <= 4 ? 12 : 3 * MAX_ANCHORS; }
+nnrt_status launch_face_node_table(const int4* faces4, int64_t F, const int32_t* anchors, int K, uint32_t* out, hipStream_t stream);
 
 // pass 1 (k_pixel_jacobians) then pass 2 (k_node_reduce_grouped); `between` (optional) is recorded between them
 nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t stream, hipEvent_t between = nullptr);
