@@ -530,14 +530,14 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 			d = make_int4(__builtin_bit_cast(int, slots[lane]), __builtin_bit_cast(int, slots[NG_STRIDE + lane]),
 			              __builtin_bit_cast(int, slots[2 * NG_STRIDE + lane]), __builtin_bit_cast(int, slots[3 * NG_STRIDE + lane]));
 		const int rows[3] = {d.y, d.z, d.w};
+		// unconditional loads (row -1 reads row 0, ignored in (2b)): a branch per load would make the compiler wait for
+		// each gather before issuing the next, serialising the chunk's six row fetches
 #pragma unroll
 		for (int fv = 0; fv < 3; fv++) {
-			jv[fv] = make_float4(0.f, 0.f, 0.f, 0.f);
-			jn[fv] = make_float4(0.f, 0.f, 0.f, 0.f);
-			if (rows[fv] >= 0) {
-				jv[fv] = a.jv[rows[fv]];
-				if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) jn[fv] = a.jn[rows[fv]];
-			}
+			const int r = rows[fv] >= 0 ? rows[fv] : 0;
+			jv[fv] = a.jv[r];
+			if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) jn[fv] = a.jn[r];
+			else jn[fv] = make_float4(0.f, 0.f, 0.f, 0.f);
 		}
 	};
 	// (2b) J and r of association `lane` into its slot
@@ -648,24 +648,28 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 	};
 
-	int cb = 0, count = 0;   // buffer and size of the chunk in flight (gathered, not yet reduced)
-	while (true) {
-		float* nxt = s_slots[wave][cb ^ 1];
+	// chunk c: its row gathers are issued first and land while chunk c + 1 is grouped (LDS / scalar work); the loads
+	// are consumed in the same iteration, so no loaded register is carried across the loop (a loop-carried load
+	// destination gets copied into the phi register right after the load, i.e. waited for)
+	int cb = 0;
+	int count = group(s_slots[wave][0]);
+	while (count > 0) {
 		float* cur_slots = s_slots[wave][cb];
+		float* nxt = s_slots[wave][cb ^ 1];
+		wave_sync();
+		gather(cur_slots, count);
 		const int next = group(nxt);
 		wave_sync();
 		const unsigned long long tc0 = FCLOCK();
-		if (count > 0) jacobians(cur_slots, count);
-		if (next > 0) gather(nxt, next);
+		jacobians(cur_slots, count);
 		wave_sync();
 		const unsigned long long tc1 = FCLOCK();
-		if (count > 0) sums(cur_slots, count);
+		sums(cur_slots, count);
 		wave_sync();
 		if (FIT_STAMPS && __ballot(acc == 1.2345) == 777ull) a.acc[0] = 0;
 		const unsigned long long tc2 = FCLOCK();
 		t_jac += tc1 - tc0;
 		t_sum += tc2 - tc1;
-		if (next == 0) break;
 		cb ^= 1;
 		count = next;
 	}
