@@ -562,22 +562,24 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 			const float rn[3] = {q[9], q[10], q[11]};
 			const float rho[3] = {q[12], q[13], q[14]};
 			float jr[3] = {0.f, 0.f, 0.f}, jt[3] = {0.f, 0.f, 0.f};
+			// branch-free over the face vertices: a vertex not anchored to the node adds an exact +0 (selected, so the
+			// row it loaded in its place -- row 0 -- never reaches the sums, NaN or not)
 #pragma unroll
 			for (int fv = 0; fv < 3; fv++) {
-				if (rows[fv] < 0) continue;
+				const bool on = rows[fv] >= 0;
 				const f3 dv = make3(dr_dV[3 * fv], dr_dV[3 * fv + 1], dr_dV[3 * fv + 2]);
 				if (MODE != NNRT_ITERATION_ROTATION_ONLY) {
-					jt[0] += dv.x * jv[fv].w;
-					jt[1] += dv.y * jv[fv].w;
-					jt[2] += dv.z * jv[fv].w;
+					jt[0] += on ? dv.x * jv[fv].w : 0.f;
+					jt[1] += on ? dv.y * jv[fv].w : 0.f;
+					jt[2] += on ? dv.z * jv[fv].w : 0.f;
 				}
 				if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) {
 					const f3 dn = make3(rn[0] * rho[fv], rn[1] * rho[fv], rn[2] * rho[fv]);
 					const f3 t1 = row_times_skew(dv, make3(jv[fv].x, jv[fv].y, jv[fv].z));
 					const f3 t2 = row_times_skew(dn, make3(jn[fv].x, jn[fv].y, jn[fv].z));
-					jr[0] += t1.x + t2.x;
-					jr[1] += t1.y + t2.y;
-					jr[2] += t1.z + t2.z;
+					jr[0] += on ? t1.x + t2.x : 0.f;
+					jr[1] += on ? t1.y + t2.y : 0.f;
+					jr[2] += on ? t1.z + t2.z : 0.f;
 				}
 			}
 			float J[8];
