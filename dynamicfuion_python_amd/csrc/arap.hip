@@ -10,9 +10,6 @@
 //                    (the reference drops them: A3) as in sparse_block_cholesky_scripts.py:106-160.
 #include <algorithm>
 
-#ifndef NNRT_FIT_VARIANT
-#define NNRT_FIT_VARIANT 0   // development timing builds only (Makefile `variants`): 0 = product
-#endif
 
 #include "fitter_kernels.hpp"
 
@@ -493,21 +490,6 @@ __device__ inline float rhs_row_update(const float* L, int64_t ld, const float* 
 	return s;
 }
 
-#if NNRT_FIT_VARIANT == 30   // development: s_memrealtime phase stamps of the diagonal workgroup (tools/chol_stamps.py)
-__device__ unsigned long long g_chol_stamps[64][8];
-#define CSTAMP(i) \
-	do { \
-		if (blockIdx.x == 0 && threadIdx.x == 0 && k < 64) { \
-			g_chol_stamps[k][i] = __builtin_amdgcn_s_memrealtime(); \
-			g_chol_stamps[k][4 + i] = __builtin_amdgcn_s_memtime(); \
-		} \
-	} while (0)
-extern "C" int nnrt_dev_chol_stamps(unsigned long long* host) {
-	return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_chol_stamps), sizeof(g_chol_stamps)) == hipSuccess ? 0 : 1;
-}
-#else
-#define CSTAMP(i) do {} while (0)
-#endif
 
 __global__ __launch_bounds__(CT) void k_chol_step(float* __restrict__ A, int ld, int k, int T, float* __restrict__ b, int* error_flag) {
 	__shared__ float s_d[CORNER_NB * CS4];   // A_kk after the previous block's update
@@ -540,7 +522,6 @@ __global__ __launch_bounds__(CT) void k_chol_step(float* __restrict__ A, int ld,
 		return;
 	}
 	// ---- panel row I = k + blockIdx.x ----
-	CSTAMP(0);
 	const bool diag = blockIdx.x == 0;
 	const int64_t rI = ok0 + static_cast<int64_t>(blockIdx.x) * CORNER_NB;
 	if (k > 0) {
@@ -560,7 +541,6 @@ __global__ __launch_bounds__(CT) void k_chol_step(float* __restrict__ A, int ld,
 		if (diag && t < CORNER_NB) s_b[t] = b[ok0 + t];
 	}
 	__syncthreads();
-	CSTAMP(1);
 	if (wave != 0) return;
 	// ap[c] = (A_kk[lane][c], A_Ik[lane][c]): both rows see the same column operations, so one packed FMA
 	// (v_pk_fma_f32) updates the pair
@@ -582,7 +562,6 @@ __global__ __launch_bounds__(CT) void k_chol_step(float* __restrict__ A, int ld,
 	// later column c with four packed FMAs whose multipliers L_c,jb..jb+3 are read from lane c by readlane (scalar
 	// operands: nothing on the elimination path waits on LDS). Every element sees its updates in ascending column order.
 	__shared__ float4 s_l4[2][CORNER_NB];   // s_l4[.][c] = (L_c,jb .. L_c,jb+3)
-	CSTAMP(2);
 	int bad = 0;
 #pragma clang loop unroll(full)
 	for (int jb = 0; jb < CORNER_NB; jb += 4) {
@@ -654,7 +633,6 @@ __global__ __launch_bounds__(CT) void k_chol_step(float* __restrict__ A, int ld,
 		}
 	}
 	const bool ok = !bad;
-	CSTAMP(3);
 	if (diag) {
 		float4* wa = reinterpret_cast<float4*>(A + (ok0 + lane) * LD + ok0);
 #pragma unroll

@@ -13,32 +13,7 @@
 // exactly-summed reference data term (see DESIGN.md "Numerics"); no node-list cap.
 #include "fitter_kernels.hpp"
 
-#ifndef NNRT_FIT_VARIANT
-#define NNRT_FIT_VARIANT 0   // development timing builds only (tools/fit_variants.py): 0 = product
-#endif
 
-#if NNRT_FIT_VARIANT == 30
-#define FIT_STAMPS 1
-__device__ unsigned long long g_fit_stamps[2][1 << 17];
-#define FSTAMP(k, i)                                                                                                          \
-	do {                                                                                                                    \
-		if ((threadIdx.x & 63) == 0) g_fit_stamps[k][(blockIdx.x * 4 + threadIdx.x / 64) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
-	} while (0)
-extern "C" int nnrt_dev_fit_stamps(int k, unsigned long long* host, int n) {
-	return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fit_stamps), sizeof(unsigned long long) * n, sizeof(unsigned long long) * (1 << 17) * k) ==
-	               hipSuccess ? 0 : 1;
-}
-#define FSTAMP_AT(k, i, t)                                                                                                    \
-	do {                                                                                                                    \
-		if ((threadIdx.x & 63) == 0) g_fit_stamps[k][(blockIdx.x * 4 + threadIdx.x / 64) * 8 + (i)] = (t);                \
-	} while (0)
-#define FCLOCK() __builtin_amdgcn_s_memrealtime()
-#else
-#define FIT_STAMPS 0
-#define FSTAMP(k, i) do {} while (0)
-#define FSTAMP_AT(k, i, t) do {} while (0)
-#define FCLOCK() 0ull
-#endif
 
 namespace nnrt {
 
@@ -65,7 +40,7 @@ struct ModeTraits<NNRT_ITERATION_ROTATION_ONLY> {
 // term, the compact per-pixel Jacobian record [dr/dV (9), dr/dn_l (3), rho (3), r] (4 x float4). The raster key is
 // replaced by the contributing face (or EMPTY) for pass 2, which resets it.
 template <int MODE>
-__global__ __launch_bounds__(PIX_BLOCK, NNRT_FIT_VARIANT == 60 || NNRT_FIT_VARIANT == 61 ? 5 : 1) void k_pixel_jacobians(FitPixelArgs a) {
+__global__ __launch_bounds__(PIX_BLOCK) void k_pixel_jacobians(FitPixelArgs a) {
 
 	// XCD-aware tile order: consecutive workgroups are dealt round-robin over the 8 XCDs, so give each XCD a contiguous
 	// band of tiles (neighbouring tiles share vertices, anchors and nodes -> L2 reuse within the XCD).
@@ -85,7 +60,6 @@ __global__ __launch_bounds__(PIX_BLOCK, NNRT_FIT_VARIANT == 60 || NNRT_FIT_VARIA
 	float dr_dV[9];
 	float rn[3] = {0.f, 0.f, 0.f}, rho[3] = {0.f, 0.f, 0.f};
 
-	FSTAMP(0, 0);
 	if (in_image) {
 		const uint64_t key = a.keys[p];
 		int32_t face = -1;
@@ -111,7 +85,6 @@ __global__ __launch_bounds__(PIX_BLOCK, NNRT_FIT_VARIANT == 60 || NNRT_FIT_VARIA
 			// the scatter accepted this face for this pixel after the full test; re-resolving needs no distance test
 			if (!face_test<false>(fn, px, py, a.blur, a.perspective, false, true, h)) face = -1;
 		}
-		FSTAMP(0, 1);
 		// ---- ComputeDepthResiduals (:331-390) ----
 		const float depth = face >= 0 ? h.depth : -1.f;
 		const bool rendered_valid = depth > 0 && depth < a.max_depth;
@@ -238,18 +211,6 @@ __global__ __launch_bounds__(PIX_BLOCK, NNRT_FIT_VARIANT == 60 || NNRT_FIT_VARIA
 			rn[0] = dr_dnl.x;
 			rn[1] = dr_dnl.y;
 			rn[2] = dr_dnl.z;
-#if NNRT_FIT_VARIANT == 60 || NNRT_FIT_VARIANT == 62
-			// the face vertices are re-read (L1/L2) for the per-vertex chain instead of being held through the
-			// Jacobian set-up above: 18 fewer live registers there (occupancy), same values
-			asm volatile("" ::: "memory");
-#pragma unroll
-			for (int i = 0; i < 3; i++) {
-				const float4 wp = a.wpos[vid[i]];
-				const float4 wn = a.wnrm[vid[i]];
-				V3[i] = make3(wp.x, wp.y, wp.z);
-				N3[i] = make3(wn.x, wn.y, wn.z);
-			}
-#endif
 #pragma unroll
 			for (int i = 0; i < 3; i++) {
 				const float z = V3[i].z;
@@ -304,7 +265,6 @@ __global__ __launch_bounds__(PIX_BLOCK, NNRT_FIT_VARIANT == 60 || NNRT_FIT_VARIA
 		}
 		a.keys[p] = contributes ? static_cast<uint64_t>(static_cast<uint32_t>(face)) : EMPTY_KEY;
 	}
-	FSTAMP(0, 2);
 }
 
 // ---- once per frame: the face -> distinct anchor node table (AssociateFacesWithAnchorsImpl.h:34-107) --------------------
@@ -377,7 +337,8 @@ __device__ inline int wave_min_i32(int v) {
 //     table), so the wave's next node is the minimum of the lanes' list heads (one DPP reduction); the lanes whose head it
 //     is file one association each (pixel lane, the jv/jn row of every face vertex anchored to the node) at consecutive
 //     LDS positions (mbcnt) and advance their list. A node that does not fit the chunk continues in the next one.
-// (2) Jacobians: one association per lane (no idle lanes); J (S floats) and r overwrite the association's slot.
+// (2) Jacobians: one association per lane (no idle lanes); J (S floats, formed as the reference forms them) and r
+//     overwrite the association's slot.
 // (3) Sums: the wave splits into 64 / GROUP lane groups; lane e of a group owns accumulator entry e (JJᵀ upper
 //     triangle, then J r) and walks its group's share of the chunk adding the float product J[c0] * J[c1] in double;
 //     at a node change the group adds its totals to the node's fp64 row (one 27-lane atomic). No cross-lane reduction.
@@ -392,13 +353,7 @@ constexpr int NG_STRIDE = 49;
 constexpr int NG_ROWS = 8;     // pixel rows per wave (8 x NG_ROWS pixels)
 static_assert(2 * NG_ROWS == PIX_TILE, "pass 2 walks the pass-1 tiles");
 
-#if NNRT_FIT_VARIANT == 70   // experiment: no accumulator atomics (timing only)
-__device__ inline void ng_flush(double* dst, double v) {
-	if (v == 1.2345e300) *dst = v;
-}
-#else
 __device__ inline void ng_flush(double* dst, double v) { atomicAdd(dst, v); }
-#endif
 
 template <int MODE, int MAXK>
 __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_grouped(FitPixelArgs a) {
@@ -412,7 +367,6 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 	static_assert(T::NACC <= GROUP && NG_CAP % G == 0 && SEG % NG_BATCH == 0 && NG_STRIDE >= NG_CAP && (NG_STRIDE & 1), "slot layout");
 	static_assert(NSLOT % 4 == 0, "face table rows are loaded as int4");
 	__shared__ float s_slots[PIX_BLOCK / 64][2][8 * NG_STRIDE];
-	__shared__ float s_rec[PIX_BLOCK / 64][16 * 64];                 // component-major pixel records
 
 	// tiles of 16 x 16 pixels (the pass-1 tiles), one 8 x 8 block per wave
 	const int tiles = a.tiles_x * a.tiles_y;
@@ -423,15 +377,13 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 	const int lane = static_cast<int>(threadIdx.x & 63), wave = static_cast<int>(threadIdx.x >> 6);
 	const int u = tu * PIX_TILE + (wave & 1) * 8 + (lane & 7), v = tv * 2 * NG_ROWS + (wave >> 1) * NG_ROWS + (lane >> 3);
 	const bool in_image = tile < tiles && (lane >> 3) < NG_ROWS && u < a.W && v < a.H;
-	float* recs = s_rec[wave];
+	const int pu0 = tu * PIX_TILE + (wave & 1) * 8, pv0 = tv * 2 * NG_ROWS + (wave >> 1) * NG_ROWS;
 	const int KA = a.anchor_count;
 
 	uint32_t ent[NSLOT];   // this pixel's face: distinct anchor nodes still to be filed, ascending (head = ent[0])
 	int vid[3] = {0, 0, 0};
 #pragma unroll
 	for (int t = 0; t < NSLOT; t++) ent[t] = FACE_NODE_NONE;
-	[[maybe_unused]] const unsigned long long t_start = FCLOCK();
-	unsigned long long t_jac = 0, t_sum = 0;
 	if (in_image) {
 		const int64_t p = static_cast<int64_t>(v) * a.W + u;
 		const uint64_t key = a.keys[p];
@@ -453,13 +405,9 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 			vid[0] = fi.x;
 			vid[1] = fi.y;
 			vid[2] = fi.z;
-			const float q[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
-#pragma unroll
-			for (int w = 0; w < 16; w++) recs[w * 64 + lane] = q[w];
+			(void)q0; (void)q1; (void)q2; (void)q3;
 		}
 	}
-	if (FIT_STAMPS && __ballot(ent[NSLOT - 1] == 123456789u) == 777ull) a.acc[0] = 0;   // stamp after the prologue loads
-	const unsigned long long t_loaded = FCLOCK();
 
 	// accumulator entry of this lane within its group
 	const int grp = lane / GROUP, e = lane % GROUP;
@@ -521,10 +469,8 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 	// (2a) gather: association `lane` of a filed chunk -> its jv / jn rows (in flight until (2b))
 	int4 d = make_int4(0, -1, -1, -1);
 	float4 jv[3], jn[3];
+	float4 rq[4];
 	auto gather = [&](const float* slots, int count) {
-#if NNRT_FIT_VARIANT == 72
-		return;
-#endif
 		d = make_int4(0, -1, -1, -1);
 		if (lane < count)
 			d = make_int4(__builtin_bit_cast(int, slots[lane]), __builtin_bit_cast(int, slots[NG_STRIDE + lane]),
@@ -539,13 +485,14 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 			if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) jn[fv] = a.jn[r];
 			else jn[fv] = make_float4(0.f, 0.f, 0.f, 0.f);
 		}
+		{
+			const int64_t pp = static_cast<int64_t>(min(pv0 + (d.x >> 3), a.H - 1)) * a.W + min(pu0 + (d.x & 7), a.W - 1);
+#pragma unroll
+			for (int w = 0; w < 4; w++) rq[w] = a.records[4 * pp + w];
+		}
 	};
 	// (2b) J and r of association `lane` into its slot
 	auto jacobians = [&](float* slots, int count) {
-#if NNRT_FIT_VARIANT == 72   // experiment: no Jacobians, no gathers (timing only)
-		if (lane < count) slots[lane] = 0.f;
-		return;
-#endif
 		if (lane >= count && lane < NG_CAP) {   // padding: zero products, continuing the chunk's last node
 			const float last = slots[7 * NG_STRIDE + count - 1];
 #pragma unroll
@@ -555,9 +502,9 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 		if (lane < count) {
 			const int l = d.x;
 			const int rows[3] = {d.y, d.z, d.w};
-			float q[16];
-#pragma unroll
-			for (int w = 0; w < 16; w++) q[w] = recs[w * 64 + l];
+			(void)l;
+			const float q[16] = {rq[0].x, rq[0].y, rq[0].z, rq[0].w, rq[1].x, rq[1].y, rq[1].z, rq[1].w,
+			                     rq[2].x, rq[2].y, rq[2].z, rq[2].w, rq[3].x, rq[3].y, rq[3].z, rq[3].w};
 			const float dr_dV[9] = {q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7], q[8]};
 			const float rn[3] = {q[9], q[10], q[11]};
 			const float rho[3] = {q[12], q[13], q[14]};
@@ -607,10 +554,6 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 	// (3) exact sums of the chunk's products per node
 	auto sums = [&](const float* slots, int count) {
 		(void)count;
-#if NNRT_FIT_VARIANT == 71 || NNRT_FIT_VARIANT == 72   // experiment: no sums (timing only)
-		acc += slots[lane];
-		return;
-#endif
 #pragma unroll
 		for (int j = 0; j < SEG; j += NG_BATCH) {
 			// every LDS read of the batch is issued before the dependent double adds
@@ -662,29 +605,14 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 		gather(cur_slots, count);
 		const int next = group(nxt);
 		wave_sync();
-		const unsigned long long tc0 = FCLOCK();
 		jacobians(cur_slots, count);
 		wave_sync();
-		const unsigned long long tc1 = FCLOCK();
 		sums(cur_slots, count);
 		wave_sync();
-		if (FIT_STAMPS && __ballot(acc == 1.2345) == 777ull) a.acc[0] = 0;
-		const unsigned long long tc2 = FCLOCK();
-		t_jac += tc1 - tc0;
-		t_sum += tc2 - tc1;
 		cb ^= 1;
 		count = next;
 	}
 	if (cur >= 0 && e_valid) ng_flush(a.acc + static_cast<int64_t>(cur) * ACC_STRIDE + e, acc);
-	if (FIT_STAMPS) {
-		const unsigned long long t_end = FCLOCK();
-		[[maybe_unused]] const unsigned long long t_group = t_end - t_loaded - t_jac - t_sum;
-		FSTAMP_AT(1, 0, t_start);
-		FSTAMP_AT(1, 1, t_loaded);
-		FSTAMP_AT(1, 2, t_loaded + t_group);
-		FSTAMP_AT(1, 3, t_loaded + t_group + t_jac);
-		FSTAMP_AT(1, 4, t_end);
-	}
 }
 
 static nnrt_status launch_pixel_pass(int mode, const FitPixelArgs& args, hipStream_t stream) {

@@ -86,39 +86,16 @@ __device__ inline bool face_pixel_range(const FaceNdc& fn, const RasterOptions& 
 // per scattered lane: MI355X_MICROARCH.md "Global float atomics"). Workgroups whose rectangle exceeds the LDS tile fall
 // back to per-pixel global atomics. Result = min over all faces of the key, i.e. identical to a direct scatter.
 constexpr int SCATTER_BLOCK = 256;
-#ifndef NNRT_FIT_VARIANT
-#define NNRT_FIT_VARIANT 0
-#endif
-#if NNRT_FIT_VARIANT == 21
 constexpr int SCATTER_LANES_PER_FACE = 1;
-#elif NNRT_FIT_VARIANT == 22
-constexpr int SCATTER_LANES_PER_FACE = 2;
-#else
-constexpr int SCATTER_LANES_PER_FACE = 1;
-#endif
 constexpr int SCATTER_FACES_PER_BLOCK = SCATTER_BLOCK / SCATTER_LANES_PER_FACE;
 constexpr int SCATTER_LDS_KEYS = 4096;   // 32 KiB
 
-#if NNRT_FIT_VARIANT == 30
-__device__ unsigned long long g_raster_stamps[1 << 18];
-#define RSTAMP(i)                                                                                                             \
-	do {                                                                                                                    \
-		if ((threadIdx.x & 63) == 0) g_raster_stamps[(blockIdx.x * (SCATTER_BLOCK / 64) + threadIdx.x / 64) * 8 + (i)] =        \
-		                                 __builtin_amdgcn_s_memrealtime();                                                    \
-	} while (0)
-extern "C" int nnrt_dev_raster_stamps(unsigned long long* host, int n) {
-	return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_raster_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
-}
-#else
-#define RSTAMP(i) do {} while (0)
-#endif
 
 __device__ inline void scatter_block(const FaceNdc& fn, bool ok, int32_t face, const RasterOptions& o, uint64_t* keys) {
 	__shared__ uint64_t s_keys[SCATTER_LDS_KEYS];
 	__shared__ int s_box[4];
 	int u0 = 0, u1 = -1, v0 = 0, v1 = -1;
 	if (ok) ok = face_pixel_range(fn, o, u0, u1, v0, v1);
-	RSTAMP(1);
 	if (threadIdx.x == 0) {
 		s_box[0] = 0x7fffffff;
 		s_box[1] = -1;
@@ -144,7 +121,6 @@ __device__ inline void scatter_block(const FaceNdc& fn, bool ok, int32_t face, c
 		}
 	}
 	__syncthreads();
-	RSTAMP(2);
 	const int bu0 = s_box[0], bv0 = s_box[2];
 	const int bw = s_box[1] - bu0 + 1, bh = s_box[3] - bv0 + 1;
 	if (bw <= 0 || bh <= 0) return;   // uniform: no face of this workgroup covers a pixel
@@ -153,7 +129,6 @@ __device__ inline void scatter_block(const FaceNdc& fn, bool ok, int32_t face, c
 		for (int i = threadIdx.x; i < bw * bh; i += SCATTER_BLOCK) s_keys[i] = EMPTY_KEY;
 		__syncthreads();
 	}
-	RSTAMP(3);
 	// A13: the blur radius is compared against SQUARED NDC distances, so for a face whose blur-widened box has a squared
 	// diagonal well below the radius every pixel in the box passes the distance test: skip computing it.
 	bool near_all = false;
@@ -186,17 +161,14 @@ __device__ inline void scatter_block(const FaceNdc& fn, bool ok, int32_t face, c
 			}
 		}
 	}
-	RSTAMP(4);
 	if (!staged) return;
 	__syncthreads();
-	RSTAMP(5);
 	for (int i = threadIdx.x; i < bw * bh; i += SCATTER_BLOCK) {
 		const uint64_t k = s_keys[i];
 		if (k == EMPTY_KEY) continue;
 		const int64_t p = static_cast<int64_t>(bv0 + i / bw) * o.W + bu0 + i % bw;
 		atomicMin(reinterpret_cast<unsigned long long*>(keys + p), static_cast<unsigned long long>(k));
 	}
-	RSTAMP(6);
 }
 
 __global__ __launch_bounds__(SCATTER_BLOCK) void k_raster_scatter_ndc(const float* __restrict__ face_ndc, const uint8_t* __restrict__ mask,
@@ -242,7 +214,6 @@ __device__ inline bool project_mesh_face(const float4* __restrict__ wpos, int4 f
 __global__ __launch_bounds__(SCATTER_BLOCK) void k_raster_scatter_mesh(const float4* __restrict__ wpos, const int4* __restrict__ faces4,
                                                                        int64_t F, NdcSetup s, float near_clip, float far_clip, RasterOptions o,
                                                                        uint64_t* __restrict__ keys) {
-	RSTAMP(0);
 	const int64_t f = static_cast<int64_t>(blockIdx.x) * SCATTER_FACES_PER_BLOCK + threadIdx.x / SCATTER_LANES_PER_FACE;
 	FaceNdc fn{};
 	const bool ok = f < F && project_mesh_face(wpos, faces4[f], s, near_clip, far_clip, fn);
