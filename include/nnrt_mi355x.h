@@ -229,7 +229,8 @@ nnrt_status nnrt_get_mesh_ndc_face_vertices_and_clip_mask(const float* d_vertice
  * Outputs fragments: face [H,W,Kf] int64 (-1), depth [H,W,Kf], barycentrics [H,W,Kf,3], signed distance [H,W,Kf]
  * (-1 fill). d_clip_mask may be NULL. bin_size / max_faces_per_bin are accepted for signature parity; the MI355X
  * rasterizer does not need coarse bins (faces_per_pixel == 1: per-face scatter with a (depth, face) 64-bit atomic
- * minimum; faces_per_pixel > 1: tile-binned per-pixel queues). */
+ * minimum; faces_per_pixel > 1: per-pixel lists of the faces covering the pixel centre, replayed in ascending face
+ * order through the reference's bounded queue). */
 nnrt_status nnrt_rasterize_ndc_triangles(const float* d_face_ndc, const uint8_t* d_clip_mask, int64_t face_count, int32_t height,
                                          int32_t width, float blur_radius_pixels, int32_t faces_per_pixel, int32_t bin_size,
                                          int32_t max_faces_per_bin, int32_t perspective_correct_barycentric_coordinates,
