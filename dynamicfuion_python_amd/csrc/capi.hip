@@ -473,7 +473,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 	                           ft->wpos.ptr, ft->wnrm.ptr, with_jacobians ? ft->jv.ptr : nullptr, ft->jn.ptr, s, from_identity)))
 		return st;
 	if ((st = mark(1))) return st;
-	RasterOptions ro{ft->H, ft->W, 0.5f / (static_cast<float>(fminf(ft->H, ft->W)) / 2.0f), ft->p.use_perspective_correction, 0, 1};
+	const RasterOptions ro = make_raster_options(ft->H, ft->W, 0.5f / (static_cast<float>(fminf(ft->H, ft->W)) / 2.0f), ft->p.use_perspective_correction, 0, 1);
 	if ((st = launch_raster_scatter_mesh(ft->wpos.ptr, ft->faces4.ptr, ft->F, ft->ndc, 0.0f, 10.0f, ro, ft->keys.ptr, s))) return st;
 	if ((st = mark(2))) return st;
 	FitPixelArgs fa{};
@@ -665,7 +665,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	}
 	// (re)allocate; any reallocation invalidates captured graphs
 	const auto before = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->a_schur.ptr,
-	                                    ft->face_nodes.ptr);
+	                                    ft->face_nodes.ptr, ft->wpos.ptr);
 	nnrt_status st;
 	if ((st = ft->mesh_p.ensure(3 * V)) || (st = ft->mesh_n.ensure(3 * V)) || (st = ft->faces4.ensure(F)) ||
 	    (st = ft->anchors.ensure(static_cast<size_t>(V) * K)) || (st = ft->weights.ensure(static_cast<size_t>(V) * K)) ||
@@ -746,7 +746,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 		ft->aw.edge_list = ft->a_list.ptr;
 	}
 	const auto after = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->a_schur.ptr,
-	                                   ft->face_nodes.ptr);
+	                                   ft->face_nodes.ptr, ft->wpos.ptr);
 	// Captured graphs bake every buffer pointer and the per-frame constants (NDC setup, pixel camera, extrinsics) into
 	// their kernel arguments: any change drops them. The warp field is recognised by its unique id, not its address.
 	const NdcSetup nndc = make_ndc_setup(h_K, H, W, ft->p.ndc_convention == NNRT_NDC_CONSISTENT);
@@ -1254,7 +1254,7 @@ nnrt_status nnrt_rasterize_ndc_triangles(const float* d_face_ndc, const uint8_t*
 		return NNRT_ERROR_ARGUMENT;
 	}
 	hipStream_t s = static_cast<hipStream_t>(stream);
-	RasterOptions o{H, W, blur_radius_pixels / (static_cast<float>(fminf(H, W)) / 2.0f), perspective, clip_barycentric, cull_back_faces};
+	const RasterOptions o = make_raster_options(H, W, blur_radius_pixels / (static_cast<float>(fminf(H, W)) / 2.0f), perspective, clip_barycentric, cull_back_faces);
 	if (faces_per_pixel == 1) {
 		const int64_t P = static_cast<int64_t>(H) * W;
 		uint64_t* keys = nullptr;

@@ -100,6 +100,30 @@ __device__ inline float pixel_to_ndc_r(int i, int d1, int d2, float inv_d1) {
 	return -offset + div_rn(range * static_cast<float>(i) + offset, static_cast<float>(d1), inv_d1);
 }
 
+// pixel_to_ndc(i, d1, d2) along one image axis with its constants precomputed on the host: range = ndc_range(d1, d2),
+// offset = range / 2 (exact), inv = RN(1/d1). The numerator range * i + offset lies in [offset, range * d1] for pixel
+// indices 0 <= i < d1 (normal floats), so the Markstein quotient needs no range guard: bit-identical to pixel_to_ndc.
+struct PixelAxis {
+	int dim;
+	float dimf, range, offset, inv, scale;   // scale = d1 / range (estimates only)
+};
+inline PixelAxis make_pixel_axis(int d1, int d2) {
+	PixelAxis a;
+	a.dim = d1;
+	a.dimf = static_cast<float>(d1);
+	a.range = ndc_range(d1, d2);
+	a.offset = a.range / 2.0f;
+	a.inv = static_cast<float>(1.0 / static_cast<double>(d1));
+	a.scale = a.dimf / a.range;
+	return a;
+}
+__device__ inline float pixel_ndc(int i, const PixelAxis& a) {
+	const float n = a.range * static_cast<float>(i) + a.offset;
+	const float q = n * a.inv;
+	const float r = fmaf(-a.dimf, q, n);
+	return -a.offset + fmaf(r, a.inv, q);
+}
+
 // Open3D TransformIndexer::Project with float intrinsics
 struct Camera {
 	float fx, fy, cx, cy;
@@ -152,22 +176,16 @@ __device__ inline float face_area_cw(const FaceNdc& f) { return spa_cw(f.x[0], f
 // reciprocal of the barycentric denominator (area + K_EPSILON) of a face, for face_test's shared-reciprocal division
 __device__ inline float face_inv_area(const FaceNdc& f) { return rcp_rn(face_area_cw(f) + K_EPSILON); }
 
-template <bool DIST = true>
-__device__ inline bool face_test(const FaceNdc& f, float px, float py, float blur, bool persp, bool clip, bool cull, RasterHit& h,
-                                 float inv_area) {
-	const float area = spa_cw(f.x[0], f.y[0], f.x[1], f.y[1], f.x[2], f.y[2]);
-	const bool back = area < 0.f;
-	const bool zero_area = (area <= K_EPSILON && area >= -1.f * K_EPSILON);
-	const float xmin = fmin3f(f.x[0], f.x[1], f.x[2]) - blur;
-	const float xmax = fmax3f(f.x[0], f.x[1], f.x[2]) + blur;
-	const float ymin = fmin3f(f.y[0], f.y[1], f.y[2]) - blur;
-	const float ymax = fmax3f(f.y[0], f.y[1], f.y[2]) + blur;
-	const bool zinv = fmax3f(f.z[0], f.z[1], f.z[2]) < K_EPSILON;
-	if ((px > xmax || px < xmin || py > ymax || py < ymin || zinv) || (cull && back) || zero_area) return false;
-	const float A = area + K_EPSILON;
-	float b0 = div_rn(spa_cw(px, py, f.x[1], f.y[1], f.x[2], f.y[2]), A, inv_area);
-	float b1 = div_rn(spa_cw(px, py, f.x[2], f.y[2], f.x[0], f.y[0]), A, inv_area);
-	float b2 = div_rn(spa_cw(px, py, f.x[0], f.y[0], f.x[1], f.y[1]), A, inv_area);
+// The per-pixel part of the test once the box, culling and degeneracy checks have passed: barycentrics from the three
+// signed parallelogram areas s_i of the pixel centre against the edges opposite vertex i (A = area + K_EPSILON,
+// inv_area = rcp_rn(A)), perspective correction, clipping, depth and the blur-distance test. Shared by face_test and
+// the rasterizer's row walk (which forms the s_i from row-shared terms with the same operations), so both are bit-identical.
+template <bool DIST>
+__device__ inline bool face_hit_from_spa(const FaceNdc& f, float s0, float s1, float s2, float A, float inv_area, float px, float py, float blur,
+                                         bool persp, bool clip, RasterHit& h) {
+	float b0 = div_rn(s0, A, inv_area);
+	float b1 = div_rn(s1, A, inv_area);
+	float b2 = div_rn(s2, A, inv_area);
 	if (persp) {
 		const float n0 = b0 * f.z[1] * f.z[2], n1 = f.z[0] * b1 * f.z[2], n2 = f.z[0] * f.z[1] * b2;
 		const float den = fmaxf(n0 + n1 + n2, K_EPSILON);
@@ -202,6 +220,22 @@ __device__ inline bool face_test(const FaceNdc& f, float px, float py, float blu
 	h.b1 = c1;
 	h.b2 = c2;
 	return true;
+}
+
+template <bool DIST = true>
+__device__ inline bool face_test(const FaceNdc& f, float px, float py, float blur, bool persp, bool clip, bool cull, RasterHit& h,
+                                 float inv_area) {
+	const float area = spa_cw(f.x[0], f.y[0], f.x[1], f.y[1], f.x[2], f.y[2]);
+	const bool back = area < 0.f;
+	const bool zero_area = (area <= K_EPSILON && area >= -1.f * K_EPSILON);
+	const float xmin = fmin3f(f.x[0], f.x[1], f.x[2]) - blur;
+	const float xmax = fmax3f(f.x[0], f.x[1], f.x[2]) + blur;
+	const float ymin = fmin3f(f.y[0], f.y[1], f.y[2]) - blur;
+	const float ymax = fmax3f(f.y[0], f.y[1], f.y[2]) + blur;
+	const bool zinv = fmax3f(f.z[0], f.z[1], f.z[2]) < K_EPSILON;
+	if ((px > xmax || px < xmin || py > ymax || py < ymin || zinv) || (cull && back) || zero_area) return false;
+	return face_hit_from_spa<DIST>(f, spa_cw(px, py, f.x[1], f.y[1], f.x[2], f.y[2]), spa_cw(px, py, f.x[2], f.y[2], f.x[0], f.y[0]),
+	                               spa_cw(px, py, f.x[0], f.y[0], f.x[1], f.y[1]), area + K_EPSILON, inv_area, px, py, blur, persp, clip, h);
 }
 template <bool DIST = true>
 __device__ inline bool face_test(const FaceNdc& f, float px, float py, float blur, bool persp, bool clip, bool cull, RasterHit& h) {

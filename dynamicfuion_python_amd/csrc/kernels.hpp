@@ -87,7 +87,9 @@ struct RasterOptions {
 	int perspective;
 	int clip_barycentric;
 	int cull_back_faces;
+	PixelAxis ax, ay;    // pixel-centre NDC constants of the x (W over H) and y (H over W) axes: set by make_raster_options
 };
+RasterOptions make_raster_options(int H, int W, float blur, int perspective, int clip_barycentric, int cull_back_faces);
 nnrt_status launch_raster_scatter_ndc(const float* face_ndc, const uint8_t* mask, int64_t F, const RasterOptions& o, uint64_t* keys,
                                       hipStream_t stream);
 nnrt_status launch_raster_resolve(const float* face_ndc, int64_t F, const RasterOptions& o, uint64_t* keys, int64_t* out_face,

@@ -26,22 +26,31 @@ __device__ inline FaceNdc load_face_ndc(const float* face_ndc, int64_t f) {
 	return r;
 }
 
-// Conservative pixel index range of [lo, hi] along one image axis, in float (two pixels of margin absorb the rounding
-// of the estimate; face_pixel_range trims it exactly). Empty for NaN / off-image bounds.
-__device__ inline void pixel_span_f(float lo, float hi, int dim, int other, int* first, int* last) {
-	const float r = ndc_range(dim, other);
-	const float s = static_cast<float>(dim) / r;
-	float a = floorf((lo + 0.5f * r) * s - 0.5f) - 2.f;
-	float b = ceilf((hi + 0.5f * r) * s - 0.5f) + 2.f;
-	if (!(a <= static_cast<float>(dim - 1)) || !(b >= 0.f)) {
-		*first = 1;
-		*last = 0;
-		return;
-	}
-	a = fmaxf(a, 0.f);
-	b = fminf(b, static_cast<float>(dim - 1));
-	*first = static_cast<int>(a);
-	*last = static_cast<int>(b);
+RasterOptions make_raster_options(int H, int W, float blur, int perspective, int clip_barycentric, int cull_back_faces) {
+	RasterOptions o{H, W, blur, perspective, clip_barycentric, cull_back_faces, make_pixel_axis(W, H), make_pixel_axis(H, W)};
+	return o;
+}
+
+// First pixel index i in [0, dim] whose centre pixel_ndc(i) >= lo (dim: none) and last index in [-1, dim) whose centre is
+// <= hi (-1: none). pixel_ndc is non-decreasing in i; a float estimate lands at most a step away and the walks make it
+// exact (typically one evaluation each). lo, hi finite.
+__device__ inline int pixel_first(float lo, const PixelAxis& a) {
+	const float e = fminf(fmaxf(ceilf((lo + a.offset) * a.scale - 0.5f), 0.f), a.dimf);
+	int i = static_cast<int>(e);
+#pragma clang loop unroll(disable) vectorize(disable)
+	while (i > 0 && pixel_ndc(i - 1, a) >= lo) i--;
+#pragma clang loop unroll(disable) vectorize(disable)
+	while (i < a.dim && pixel_ndc(i, a) < lo) i++;
+	return i;
+}
+__device__ inline int pixel_last(float hi, const PixelAxis& a) {
+	const float e = fminf(fmaxf(floorf((hi + a.offset) * a.scale - 0.5f), -1.f), a.dimf - 1.f);
+	int i = static_cast<int>(e);
+#pragma clang loop unroll(disable) vectorize(disable)
+	while (i < a.dim - 1 && pixel_ndc(i + 1, a) <= hi) i++;
+#pragma clang loop unroll(disable) vectorize(disable)
+	while (i >= 0 && pixel_ndc(i, a) > hi) i--;
+	return i;
 }
 
 // A face with a non-finite vertex coordinate is never rasterized (the sum of the nine coordinates is non-finite iff one
@@ -67,122 +76,217 @@ __device__ inline bool face_pixel_range(const FaceNdc& fn, const RasterOptions& 
 	const float ymin = fmin3f(fn.y[0], fn.y[1], fn.y[2]) - o.blur;
 	const float ymax = fmax3f(fn.y[0], fn.y[1], fn.y[2]) + o.blur;
 	if (!(xmax >= xmin) || !(ymax >= ymin)) return false;
-	pixel_span_f(xmin, xmax, o.W, o.H, &u0, &u1);
-	pixel_span_f(ymin, ymax, o.H, o.W, &v0, &v1);
-	// pixel_to_ndc is monotone: trim the widening so only pixels inside the box remain
-	const float inv_w = rcp_rn(static_cast<float>(o.W)), inv_h = rcp_rn(static_cast<float>(o.H));
-	while (u0 <= u1 && pixel_to_ndc_r(u0, o.W, o.H, inv_w) < xmin) u0++;
-	while (u1 >= u0 && pixel_to_ndc_r(u1, o.W, o.H, inv_w) > xmax) u1--;
-	while (v0 <= v1 && pixel_to_ndc_r(v0, o.H, o.W, inv_h) < ymin) v0++;
-	while (v1 >= v0 && pixel_to_ndc_r(v1, o.H, o.W, inv_h) > ymax) v1--;
+	u0 = pixel_first(xmin, o.ax);
+	u1 = pixel_last(xmax, o.ax);
+	v0 = pixel_first(ymin, o.ay);
+	v1 = pixel_last(ymax, o.ay);
 	return u0 <= u1 && v0 <= v1;
 }
 
-// One workgroup = 64 consecutive faces, 4 lanes per face (the lanes of a quad split the face's pixel tests, so a launch
-// has 4x the waves of a lane-per-face launch and each lane a quarter of the serial test loop). Consecutive faces of a
-// mesh are spatially coherent, so their pixel boxes share a small bounding rectangle: the workgroup resolves its
-// faces' (depth, face) minima in LDS with 64-bit LDS atomics and then merges the rectangle into the image with one
-// global atomicMin per touched pixel, row-contiguous across lanes (memory-side global atomics cost one 64-B request
-// per scattered lane: MI355X_MICROARCH.md "Global float atomics"). Workgroups whose rectangle exceeds the LDS tile fall
-// back to per-pixel global atomics. Result = min over all faces of the key, i.e. identical to a direct scatter.
+// K = 1 scatter. Each wave owns SCATTER_FPW consecutive faces. Consecutive faces of a mesh are spatially coherent, so
+// the wave's pixel boxes share a small bounding rectangle, held as a wave-private tile of (depth, face) keys in LDS; the
+// tile is merged into the image with one global atomicMin per touched pixel, row-contiguous across lanes (memory-side
+// global atomics cost one request per scattered lane: MI355X_MICROARCH.md "Global float atomics"). A wave whose rectangle
+// exceeds the tile (e.g. a face run that wraps to the next mesh row) scatters straight to the image instead. Either way
+// the result is the minimum key over all faces, i.e. identical to a direct scatter.
+// Load balance: a face's work is its box rows. The wave lists its faces' rows (a wave-wide prefix sum of row counts)
+// and deals them out one row per lane, so lanes walk rows of ~equal length instead of whole boxes of unequal size. A
+// row shares its pixel-row NDC coordinate and the y-terms of the three edge functions across its pixels.
 constexpr int SCATTER_BLOCK = 256;
-constexpr int SCATTER_LANES_PER_FACE = 1;
-constexpr int SCATTER_FACES_PER_BLOCK = SCATTER_BLOCK / SCATTER_LANES_PER_FACE;
-constexpr int SCATTER_LDS_KEYS = 4096;   // 32 KiB
+constexpr int SCATTER_WAVES = SCATTER_BLOCK / 64;
+constexpr int SCATTER_FPW = 32;                                          // faces per wave
+constexpr int SCATTER_FACES_PER_BLOCK = SCATTER_WAVES * SCATTER_FPW;
+constexpr int SCATTER_TILE_KEYS = 512;                                   // 4 KiB per wave
 
+struct ScatterWaveLds {
+	uint64_t keys[SCATTER_TILE_KEYS];
+	float4 rec[SCATTER_FPW][3];   // x0 x1 x2 y0 | y1 y2 z0 z1 | z2 inv_area (u0 | span_u << 16) (v0 | near_all << 31)
+	uint32_t row[64];             // one round of row tasks: face slot | row << 8
+};
 
-__device__ inline void scatter_block(const FaceNdc& fn, bool ok, int32_t face, const RasterOptions& o, uint64_t* keys) {
-	__shared__ uint64_t s_keys[SCATTER_LDS_KEYS];
-	__shared__ int s_box[4];
+__device__ inline void scatter_wave_sync() {
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// one face row: pixels u0 .. u0 + span - 1 of image row v
+// Markstein quotient a / b through y = RN(1/b), without div_rn's operand-range guard (see depth_near_all_fast)
+__device__ inline float div_mk(float a, float b, float y) {
+	const float q = a * y;
+	const float r = fmaf(-b, q, a);
+	return fmaf(r, y, q);
+}
+
+// Depth at a pixel of a face whose every box pixel passes the distance test (A13 near_all), fast path. The reference
+// forms the barycentrics and the perspective weights as correctly rounded quotients; here they are Markstein quotients
+// through the correctly rounded reciprocals of A and of the perspective denominator, without div_rn's guard. The guard
+// exists for numerators outside [1e-30, 1e30]. Above: excluded (the caller admits faces with |A| in [1e-30, 1e30],
+// |z| < 1e10 and a box within the blur radius, blur < 1e20, so |s_i| stays far below 1e30; the perspective numerators are
+// checked here). Below: such a quotient can differ from the correctly rounded one only in the sign of a zero or in
+// subnormal digits, i.e. by < 1e-35 after the |z| < 1e10 weighting, which cannot change the bits of a depth of
+// magnitude >= 1e-20; smaller depths are recomputed on the guarded path. Returns false where face_hit_from_spa rejects.
+__device__ inline bool depth_near_all_fast(const FaceNdc& f, float s0, float s1, float s2, float A, float inv_area, float px, float py,
+                                           const RasterOptions& o, float& depth) {
+	float b0 = div_mk(s0, A, inv_area), b1 = div_mk(s1, A, inv_area), b2 = div_mk(s2, A, inv_area);
+	if (o.perspective) {
+		const float n0 = b0 * f.z[1] * f.z[2], n1 = f.z[0] * b1 * f.z[2], n2 = f.z[0] * f.z[1] * b2;
+		const float den = fmaxf(n0 + n1 + n2, K_EPSILON);
+		if (fmaxf(fmaxf(fabsf(n0), fabsf(n1)), fabsf(n2)) < 1e29f && den < 1e30f) {
+			const float y = rcp_rn(den);
+			b0 = div_mk(n0, den, y);
+			b1 = div_mk(n1, den, y);
+			b2 = div_mk(n2, den, y);
+		} else {
+			b0 = n0 / den;
+			b1 = n1 / den;
+			b2 = n2 / den;
+		}
+	}
+	depth = b0 * f.z[0] + b1 * f.z[1] + b2 * f.z[2];
+	if (!(fabsf(depth) >= 1e-20f)) {
+		RasterHit h;
+		if (!face_hit_from_spa<false>(f, s0, s1, s2, A, inv_area, px, py, o.blur, o.perspective, 0, h)) return false;
+		depth = h.depth;
+		return true;
+	}
+	return !(depth < 0.f);
+}
+
+// one face row: pixels u0 .. u0 + span - 1 of image row v. MODE 0: full test (distance included); 1: near_all face
+// (guarded quotients); 2: near_all face on the fast path (depth_near_all_fast's conditions hold).
+template <int MODE>
+__device__ inline void scatter_row(const FaceNdc& fn, float inv_area, int u0, int span, int v, int32_t face, const RasterOptions& o, bool staged,
+                                   uint64_t* tile, int tu0, int tv0, int tw, uint64_t* keys) {
+	const float py = pixel_ndc(v, o.ay);
+	const float A = spa_cw(fn.x[0], fn.y[0], fn.x[1], fn.y[1], fn.x[2], fn.y[2]) + K_EPSILON;
+	// spa_cw(p, a, b) = (px - ax) * (ay - by) - (py - ay) * (ax - bx), edges (v1, v2), (v2, v0), (v0, v1)
+	const float c0 = fn.y[1] - fn.y[2], c1 = fn.y[2] - fn.y[0], c2 = fn.y[0] - fn.y[1];
+	const float r0 = (py - fn.y[1]) * (fn.x[1] - fn.x[2]), r1 = (py - fn.y[2]) * (fn.x[2] - fn.x[0]), r2 = (py - fn.y[0]) * (fn.x[0] - fn.x[1]);
+	uint64_t* trow = tile + (v - tv0) * tw - tu0;
+#pragma clang loop unroll(disable) vectorize(disable)
+	for (int u = u0; u < u0 + span; u++) {
+		const float px = pixel_ndc(u, o.ax);
+		const float s0 = (px - fn.x[1]) * c0 - r0, s1 = (px - fn.x[2]) * c1 - r1, s2 = (px - fn.x[0]) * c2 - r2;
+		float depth;
+		if constexpr (MODE == 2) {
+			if (!depth_near_all_fast(fn, s0, s1, s2, A, inv_area, px, py, o, depth)) continue;
+		} else {
+			RasterHit h;
+			if (!face_hit_from_spa<MODE == 0>(fn, s0, s1, s2, A, inv_area, px, py, o.blur, o.perspective, o.clip_barycentric, h)) continue;
+			depth = h.depth;
+		}
+		const unsigned long long key = raster_key(depth, face);
+		if (staged)
+			__hip_atomic_fetch_min(reinterpret_cast<unsigned long long*>(trow + u), key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+		else
+			atomicMin(reinterpret_cast<unsigned long long*>(keys + static_cast<int64_t>(v) * o.W + u), key);
+	}
+}
+
+// lane < SCATTER_FPW holds face face0 + lane (ok = it exists and is not masked out); all 64 lanes of the wave call this
+__device__ inline void scatter_wave(const FaceNdc& fn, bool ok, int32_t face0, const RasterOptions& o, uint64_t* keys, ScatterWaveLds& w) {
+	const int lane = static_cast<int>(threadIdx.x & 63);
 	int u0 = 0, u1 = -1, v0 = 0, v1 = -1;
 	if (ok) ok = face_pixel_range(fn, o, u0, u1, v0, v1);
-	if (threadIdx.x == 0) {
-		s_box[0] = 0x7fffffff;
-		s_box[1] = -1;
-		s_box[2] = 0x7fffffff;
-		s_box[3] = -1;
-	}
-	__syncthreads();
-	{
-		// wave-level min/max first: one LDS atomic per wave instead of 64 same-address atomics per wave
-		int bu0 = ok ? u0 : 0x7fffffff, bu1 = ok ? u1 : -1, bv0 = ok ? v0 : 0x7fffffff, bv1 = ok ? v1 : -1;
+	int bu0 = ok ? u0 : 0x7fffffff, bu1 = ok ? u1 : -1, bv0 = ok ? v0 : 0x7fffffff, bv1 = ok ? v1 : -1;
 #pragma unroll
-		for (int d = 32; d >= 1; d >>= 1) {
-			bu0 = min(bu0, __shfl_xor(bu0, d));
-			bu1 = max(bu1, __shfl_xor(bu1, d));
-			bv0 = min(bv0, __shfl_xor(bv0, d));
-			bv1 = max(bv1, __shfl_xor(bv1, d));
-		}
-		if ((threadIdx.x & 63) == 0 && bu1 >= 0) {
-			atomicMin(&s_box[0], bu0);
-			atomicMax(&s_box[1], bu1);
-			atomicMin(&s_box[2], bv0);
-			atomicMax(&s_box[3], bv1);
-		}
+	for (int d = 32; d >= 1; d >>= 1) {
+		bu0 = min(bu0, __shfl_xor(bu0, d));
+		bu1 = max(bu1, __shfl_xor(bu1, d));
+		bv0 = min(bv0, __shfl_xor(bv0, d));
+		bv1 = max(bv1, __shfl_xor(bv1, d));
 	}
-	__syncthreads();
-	const int bu0 = s_box[0], bv0 = s_box[2];
-	const int bw = s_box[1] - bu0 + 1, bh = s_box[3] - bv0 + 1;
-	if (bw <= 0 || bh <= 0) return;   // uniform: no face of this workgroup covers a pixel
-	const bool staged = bw * bh <= SCATTER_LDS_KEYS;
-	if (staged) {
-		for (int i = threadIdx.x; i < bw * bh; i += SCATTER_BLOCK) s_keys[i] = EMPTY_KEY;
-		__syncthreads();
-	}
-	// A13: the blur radius is compared against SQUARED NDC distances, so for a face whose blur-widened box has a squared
-	// diagonal well below the radius every pixel in the box passes the distance test: skip computing it.
-	bool near_all = false;
+	if (bu1 < 0) return;   // wave-uniform: none of the wave's faces covers a pixel
+	const int tw = bu1 - bu0 + 1, th = bv1 - bv0 + 1;
+	const bool staged = tw * th <= SCATTER_TILE_KEYS;
+	if (staged)
+		for (int i = lane; i < tw * th; i += 64) w.keys[i] = EMPTY_KEY;
+	const int rows = ok ? v1 - v0 + 1 : 0;
 	if (ok) {
-		const float w = (fmax3f(fn.x[0], fn.x[1], fn.x[2]) - fmin3f(fn.x[0], fn.x[1], fn.x[2])) + 2.f * o.blur;
-		const float hh = (fmax3f(fn.y[0], fn.y[1], fn.y[2]) - fmin3f(fn.y[0], fn.y[1], fn.y[2])) + 2.f * o.blur;
-		near_all = (w * w + hh * hh) < 0.5f * o.blur;
+		// A13: the blur radius is compared against SQUARED NDC distances, so for a face whose blur-widened box has a
+		// squared diagonal well below the radius every pixel in the box passes the distance test: skip computing it.
+		const float bw = (fmax3f(fn.x[0], fn.x[1], fn.x[2]) - fmin3f(fn.x[0], fn.x[1], fn.x[2])) + 2.f * o.blur;
+		const float bh = (fmax3f(fn.y[0], fn.y[1], fn.y[2]) - fmin3f(fn.y[0], fn.y[1], fn.y[2])) + 2.f * o.blur;
+		const bool near_all = (bw * bw + bh * bh) < 0.5f * o.blur;
+		w.rec[lane][0] = make_float4(fn.x[0], fn.x[1], fn.x[2], fn.y[0]);
+		w.rec[lane][1] = make_float4(fn.y[1], fn.y[2], fn.z[0], fn.z[1]);
+		w.rec[lane][2] = make_float4(fn.z[2], face_inv_area(fn), __uint_as_float(static_cast<uint32_t>(u0) | static_cast<uint32_t>(u1 - u0 + 1) << 16),
+		                             __uint_as_float(static_cast<uint32_t>(v0) | (near_all ? 0x80000000u : 0u)));
 	}
-	if (ok) {
-		const float inv_w = rcp_rn(static_cast<float>(o.W)), inv_h = rcp_rn(static_cast<float>(o.H));
-		const float inv_area = face_inv_area(fn);
-		const int sub = static_cast<int>(threadIdx.x % SCATTER_LANES_PER_FACE);
-		const int span_u = u1 - u0 + 1;
-		const int count = span_u * (v1 - v0 + 1);
-		for (int i = sub; i < count; i += SCATTER_LANES_PER_FACE) {
-			const int v = v0 + i / span_u, u = u0 + i % span_u;
-			{
-				const float py = pixel_to_ndc_r(v, o.H, o.W, inv_h);
-				const float px = pixel_to_ndc_r(u, o.W, o.H, inv_w);
-				RasterHit h;
-				const bool hit = near_all ? face_test<false>(fn, px, py, o.blur, o.perspective, o.clip_barycentric, o.cull_back_faces, h, inv_area)
-				                          : face_test<true>(fn, px, py, o.blur, o.perspective, o.clip_barycentric, o.cull_back_faces, h, inv_area);
-				if (!hit) continue;
-				const unsigned long long key = raster_key(h.depth, face);
-				if (staged)
-					__hip_atomic_fetch_min(reinterpret_cast<unsigned long long*>(s_keys + (v - bv0) * bw + (u - bu0)), key, __ATOMIC_RELAXED,
-					                       __HIP_MEMORY_SCOPE_WORKGROUP);
+	int incl = rows;
+#pragma unroll
+	for (int d = 1; d < 64; d <<= 1) {
+		const int t = __shfl_up(incl, d);
+		if (lane >= d) incl += t;
+	}
+	const int total = __shfl(incl, 63);
+	const int start = incl - rows;
+	for (int base = 0; base < total; base += 64) {
+#pragma clang loop unroll(disable) vectorize(disable)
+		for (int t = max(start, base); t < min(start + rows, base + 64); t++) w.row[t - base] = static_cast<uint32_t>(lane) | static_cast<uint32_t>(t - start) << 8;
+		scatter_wave_sync();
+		if (base + lane < total) {
+			const uint32_t e = w.row[lane];
+			const int slot = static_cast<int>(e & 255u), r = static_cast<int>(e >> 8);
+			const float4 q0 = w.rec[slot][0], q1 = w.rec[slot][1], q2 = w.rec[slot][2];
+			FaceNdc g;
+			g.x[0] = q0.x;
+			g.x[1] = q0.y;
+			g.x[2] = q0.z;
+			g.y[0] = q0.w;
+			g.y[1] = q1.x;
+			g.y[2] = q1.y;
+			g.z[0] = q1.z;
+			g.z[1] = q1.w;
+			g.z[2] = q2.x;
+			const uint32_t ui = __float_as_uint(q2.z), vi = __float_as_uint(q2.w);
+			const int fu0 = static_cast<int>(ui & 0xffffu), span = static_cast<int>(ui >> 16);
+			const int v = static_cast<int>(vi & 0x7fffffffu) + r;
+			if (!(vi >> 31)) {
+				scatter_row<0>(g, q2.y, fu0, span, v, face0 + slot, o, staged, w.keys, bu0, bv0, tw, keys);
+			} else {
+				const float A = spa_cw(g.x[0], g.y[0], g.x[1], g.y[1], g.x[2], g.y[2]) + K_EPSILON;
+				const bool fast = !o.clip_barycentric && o.blur < 1e20f && fabsf(A) > 1e-30f && fabsf(A) < 1e30f &&
+				                  fmaxf(fmaxf(fabsf(g.z[0]), fabsf(g.z[1])), fabsf(g.z[2])) < 1e10f;
+				if (fast)
+					scatter_row<2>(g, q2.y, fu0, span, v, face0 + slot, o, staged, w.keys, bu0, bv0, tw, keys);
 				else
-					atomicMin(reinterpret_cast<unsigned long long*>(keys + static_cast<int64_t>(v) * o.W + u), key);
+					scatter_row<1>(g, q2.y, fu0, span, v, face0 + slot, o, staged, w.keys, bu0, bv0, tw, keys);
 			}
 		}
+		scatter_wave_sync();
 	}
 	if (!staged) return;
-	__syncthreads();
-	for (int i = threadIdx.x; i < bw * bh; i += SCATTER_BLOCK) {
-		const uint64_t k = s_keys[i];
+	// merge the tile row by row: i = y * tw + x, y from a float quotient corrected to the exact one
+	const float inv_tw = 1.0f / static_cast<float>(tw);
+	for (int i = lane; i < tw * th; i += 64) {
+		const uint64_t k = w.keys[i];
 		if (k == EMPTY_KEY) continue;
-		const int64_t p = static_cast<int64_t>(bv0 + i / bw) * o.W + bu0 + i % bw;
+		int y = static_cast<int>(static_cast<float>(i) * inv_tw);
+		if (y * tw > i) y--;
+		if ((y + 1) * tw <= i) y++;
+		const int64_t p = static_cast<int64_t>(bv0 + y) * o.W + bu0 + (i - y * tw);
 		atomicMin(reinterpret_cast<unsigned long long*>(keys + p), static_cast<unsigned long long>(k));
 	}
 }
 
 __global__ __launch_bounds__(SCATTER_BLOCK) void k_raster_scatter_ndc(const float* __restrict__ face_ndc, const uint8_t* __restrict__ mask,
                                                                       int64_t F, RasterOptions o, uint64_t* __restrict__ keys) {
-	const int64_t f = static_cast<int64_t>(blockIdx.x) * SCATTER_FACES_PER_BLOCK + threadIdx.x / SCATTER_LANES_PER_FACE;
+	__shared__ ScatterWaveLds s_wave[SCATTER_WAVES];
+	const int64_t face0 = (static_cast<int64_t>(blockIdx.x) * SCATTER_WAVES + (threadIdx.x >> 6)) * SCATTER_FPW;
+	const int lane = static_cast<int>(threadIdx.x & 63);
+	const int64_t f = face0 + lane;
 	FaceNdc fn{};
-	bool ok = f < F && !(mask && !mask[f]);
+	bool ok = lane < SCATTER_FPW && f < F && !(mask && !mask[f]);
 	if (ok) fn = load_face_ndc(face_ndc, f);
-	scatter_block(fn, ok, static_cast<int32_t>(f), o, keys);
+	scatter_wave(fn, ok, static_cast<int32_t>(face0), o, keys, s_wave[threadIdx.x >> 6]);
 }
 
 nnrt_status launch_raster_scatter_ndc(const float* face_ndc, const uint8_t* mask, int64_t F, const RasterOptions& o, uint64_t* keys,
                                       hipStream_t stream) {
 	if (F == 0) return NNRT_OK;
+	NNRT_CHECK_ARG(o.W < 65536 && F < (int64_t(1) << 31), "image wider than 65535 pixels or more than 2^31 faces");
 	k_raster_scatter_ndc<<<static_cast<unsigned>(ceil_div(F, SCATTER_FACES_PER_BLOCK)), SCATTER_BLOCK, 0, stream>>>(face_ndc, mask, F, o, keys);
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;
@@ -214,16 +318,21 @@ __device__ inline bool project_mesh_face(const float4* __restrict__ wpos, int4 f
 __global__ __launch_bounds__(SCATTER_BLOCK) void k_raster_scatter_mesh(const float4* __restrict__ wpos, const int4* __restrict__ faces4,
                                                                        int64_t F, NdcSetup s, float near_clip, float far_clip, RasterOptions o,
                                                                        uint64_t* __restrict__ keys) {
-	const int64_t f = static_cast<int64_t>(blockIdx.x) * SCATTER_FACES_PER_BLOCK + threadIdx.x / SCATTER_LANES_PER_FACE;
+	__shared__ ScatterWaveLds s_wave[SCATTER_WAVES];
+	const int64_t face0 = (static_cast<int64_t>(blockIdx.x) * SCATTER_WAVES + (threadIdx.x >> 6)) * SCATTER_FPW;
+	const int lane = static_cast<int>(threadIdx.x & 63);
+	const int64_t f = face0 + lane;
 	FaceNdc fn{};
-	const bool ok = f < F && project_mesh_face(wpos, faces4[f], s, near_clip, far_clip, fn);
-	scatter_block(fn, ok, static_cast<int32_t>(f), o, keys);
+	const bool ok = lane < SCATTER_FPW && f < F && project_mesh_face(wpos, faces4[f], s, near_clip, far_clip, fn);
+	scatter_wave(fn, ok, static_cast<int32_t>(face0), o, keys, s_wave[threadIdx.x >> 6]);
 }
 
 nnrt_status launch_raster_scatter_mesh(const float4* wpos, const int4* faces4, int64_t F, const NdcSetup& s, float near_clip, float far_clip,
                                        const RasterOptions& o, uint64_t* keys, hipStream_t stream) {
 	if (F == 0) return NNRT_OK;
-	k_raster_scatter_mesh<<<static_cast<unsigned>(ceil_div(F, SCATTER_FACES_PER_BLOCK)), SCATTER_BLOCK, 0, stream>>>(wpos, faces4, F, s, near_clip, far_clip, o, keys);
+	NNRT_CHECK_ARG(o.W < 65536 && F < (int64_t(1) << 31), "image wider than 65535 pixels or more than 2^31 faces");
+	k_raster_scatter_mesh<<<static_cast<unsigned>(ceil_div(F, SCATTER_FACES_PER_BLOCK)), SCATTER_BLOCK, 0, stream>>>(wpos, faces4, F, s, near_clip,
+	                                                                                                                 far_clip, o, keys);
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;
 }
@@ -287,12 +396,11 @@ __global__ __launch_bounds__(256) void k_hit_lists(const float* __restrict__ fac
 	const float w = (fmax3f(fn.x[0], fn.x[1], fn.x[2]) - fmin3f(fn.x[0], fn.x[1], fn.x[2])) + 2.f * o.blur;
 	const float hh = (fmax3f(fn.y[0], fn.y[1], fn.y[2]) - fmin3f(fn.y[0], fn.y[1], fn.y[2])) + 2.f * o.blur;
 	const bool near_all = (w * w + hh * hh) < 0.5f * o.blur;   // A13: every box pixel passes the distance test
-	const float inv_w = rcp_rn(static_cast<float>(o.W)), inv_h = rcp_rn(static_cast<float>(o.H));
 	const float inv_area = face_inv_area(fn);
 	for (int v = v0; v <= v1; v++) {
-		const float py = pixel_to_ndc_r(v, o.H, o.W, inv_h);
+		const float py = pixel_ndc(v, o.ay);
 		for (int u = u0; u <= u1; u++) {
-			const float px = pixel_to_ndc_r(u, o.W, o.H, inv_w);
+			const float px = pixel_ndc(u, o.ax);
 			RasterHit h;
 			const bool hit = near_all ? face_test<false>(fn, px, py, o.blur, o.perspective, o.clip_barycentric, o.cull_back_faces, h, inv_area)
 			                          : face_test<true>(fn, px, py, o.blur, o.perspective, o.clip_barycentric, o.cull_back_faces, h, inv_area);
