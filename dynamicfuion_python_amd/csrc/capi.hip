@@ -485,6 +485,8 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 	fa.pix = ft->pix;
 	fa.ndc = ft->ndc;
 	fa.blur = ro.blur;
+	fa.ax = ro.ax;
+	fa.ay = ro.ay;
 	fa.perspective = ft->p.use_perspective_correction;
 	fa.max_depth = ft->p.max_depth;
 	fa.use_tukey = ft->p.use_tukey_penalty_for_data_term;

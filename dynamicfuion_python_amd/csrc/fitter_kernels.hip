@@ -40,7 +40,8 @@ struct ModeTraits<NNRT_ITERATION_ROTATION_ONLY> {
 // term, the compact per-pixel Jacobian record [dr/dV (9), dr/dn_l (3), rho (3), r] (4 x float4). The raster key is
 // replaced by the contributing face (or EMPTY) for pass 2, which resets it.
 template <int MODE>
-__global__ __launch_bounds__(PIX_BLOCK) void k_pixel_jacobians(FitPixelArgs a) {
+__global__ __launch_bounds__(PIX_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) void k_pixel_jacobians(FitPixelArgs a) {
+	__shared__ float s_dn[27][PIX_BLOCK];
 
 	// XCD-aware tile order: consecutive workgroups are dealt round-robin over the 8 XCDs, so give each XCD a contiguous
 	// band of tiles (neighbouring tiles share vertices, anchors and nodes -> L2 reuse within the XCD).
@@ -57,7 +58,6 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_pixel_jacobians(FitPixelArgs a) {
 	const int64_t p = static_cast<int64_t>(v) * a.W + u;
 
 	int vid[3] = {0, 0, 0};
-	float dr_dV[9];
 	float rn[3] = {0.f, 0.f, 0.f}, rho[3] = {0.f, 0.f, 0.f};
 
 	if (in_image) {
@@ -66,7 +66,7 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_pixel_jacobians(FitPixelArgs a) {
 		RasterHit h{0.f, 0.f, 0.f, 0.f, 0.f};
 		f3 V3[3], N3[3];
 		FaceNdc fn;
-		const float px = pixel_to_ndc(u, a.W, a.H), py = pixel_to_ndc(v, a.H, a.W);
+		const float px = pixel_ndc(u, a.ax), py = pixel_ndc(v, a.ay);
 		if (key != EMPTY_KEY) {
 			face = static_cast<int32_t>(key & 0xffffffffu);
 			const int4 fi = a.faces4[face];
@@ -141,6 +141,7 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_pixel_jacobians(FitPixelArgs a) {
 			dr_dnl = make3(psi * d.x, psi * d.y, psi * d.z);
 			dr_dwl = make3(psi * nl.x, psi * nl.y, psi * nl.z);
 		}
+		a.keys[p] = contributes ? static_cast<uint64_t>(static_cast<uint32_t>(face)) : EMPTY_KEY;
 		if (contributes) {
 			// ---- rasterized surface Jacobians (RasterizedSurfaceJacobiansImpl.h:114-200) ----
 			rho[0] = h.b0;
@@ -167,22 +168,26 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_pixel_jacobians(FitPixelArgs a) {
 			const float s1a[2] = {fn.y[0] - py, px - fn.x[0]}, s1b[2] = {py - fn.y[2], fn.x[2] - px};   // (p, v2, v0)
 			const float s2a[2] = {fn.y[1] - py, px - fn.x[1]}, s2b[2] = {py - fn.y[0], fn.x[0] - px};   // (p, v0, v1)
 			const float inv_den = rcp_rn(den);
-			float Dn[3][3][2];
+			// d rho_r / d ndc of face vertex i, component c, and (below) the perspective z-terms of vertex i: parked in LDS
+			// (lane-private slots) until vertex i's columns are formed, which keeps the kernel at <= 96 VGPRs (5 waves/SIMD:
+			// one residency round at 640x480)
+#define DN(i, r, c) s_dn[((i) * 3 + (r)) * 2 + (c)][threadIdx.x]
+#define PZ(r, i) s_dn[18 + (r) * 3 + (i)][threadIdx.x]
 #pragma unroll
 			for (int c = 0; c < 2; c++) {
-				Dn[0][0][c] = div_rn(-sa[0] * dA[0][c], den, inv_den);
-				Dn[1][0][c] = div_rn(A * s0a[c] - sa[0] * dA[1][c], den, inv_den);
-				Dn[2][0][c] = div_rn(A * s0b[c] - sa[0] * dA[2][c], den, inv_den);
-				Dn[0][1][c] = div_rn(A * s1b[c] - sa[1] * dA[0][c], den, inv_den);
-				Dn[1][1][c] = div_rn(-sa[1] * dA[1][c], den, inv_den);
-				Dn[2][1][c] = div_rn(A * s1a[c] - sa[1] * dA[2][c], den, inv_den);
-				Dn[0][2][c] = div_rn(A * s2a[c] - sa[2] * dA[0][c], den, inv_den);
-				Dn[1][2][c] = div_rn(A * s2b[c] - sa[2] * dA[1][c], den, inv_den);
-				Dn[2][2][c] = div_rn(-sa[2] * dA[2][c], den, inv_den);
+				DN(0, 0, c) = div_rn(-sa[0] * dA[0][c], den, inv_den);
+				DN(1, 0, c) = div_rn(A * s0a[c] - sa[0] * dA[1][c], den, inv_den);
+				DN(2, 0, c) = div_rn(A * s0b[c] - sa[0] * dA[2][c], den, inv_den);
+				DN(0, 1, c) = div_rn(A * s1b[c] - sa[1] * dA[0][c], den, inv_den);
+				DN(1, 1, c) = div_rn(-sa[1] * dA[1][c], den, inv_den);
+				DN(2, 1, c) = div_rn(A * s1a[c] - sa[1] * dA[2][c], den, inv_den);
+				DN(0, 2, c) = div_rn(A * s2a[c] - sa[2] * dA[0][c], den, inv_den);
+				DN(1, 2, c) = div_rn(A * s2b[c] - sa[2] * dA[1][c], den, inv_den);
+				DN(2, 2, c) = div_rn(-sa[2] * dA[2][c], den, inv_den);
 			}
 			// perspective-correction factors first (RasterizedSurfaceJacobiansImpl.h:217-284), so the 3x9 Jacobian can be
 			// streamed one face vertex (3 columns) at a time: same expressions, far fewer live registers
-			float Pd[3][3], Pz[3][3];
+			float Pd[3][3];
 			if (a.perspective) {
 				const float z0 = V3[0].z, z1 = V3[1].z, z2 = V3[2].z;
 				const float v12 = z1 * z2, v02 = z0 * z2, v01 = z0 * z1;
@@ -203,9 +208,15 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_pixel_jacobians(FitPixelArgs a) {
 #pragma unroll
 					for (int c = 0; c < 3; c++) {
 						Pd[r][c] = div_rn(pd[r][c], dd2, inv_dd2);
-						Pz[r][c] = div_rn(pz[r][c], dd2, inv_dd2);
+						PZ(r, c) = div_rn(pz[r][c], dd2, inv_dd2);
 					}
 			}
+			// record [dr/dV (9), dr/dn_l (3), rho (3), r]; everything but dr/dV first, so it is not held across the columns
+			float* rec_f = reinterpret_cast<float*>(a.records + 4 * p);
+			rec_f[9] = dr_dnl.x;
+			rec_f[10] = dr_dnl.y;
+			rec_f[11] = dr_dnl.z;
+			reinterpret_cast<float4*>(rec_f)[3] = make_float4(rho[0], rho[1], rho[2], residual);
 			// dr/dV = dr/dwl * dwl/dV + dr/dnl * dnl/dV ; dr/dN = dr/dnl (rho (x) I)
 			const float rw[3] = {dr_dwl.x, dr_dwl.y, dr_dwl.z};
 			rn[0] = dr_dnl.x;
@@ -213,6 +224,7 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_pixel_jacobians(FitPixelArgs a) {
 			rn[2] = dr_dnl.z;
 #pragma unroll
 			for (int i = 0; i < 3; i++) {
+				__builtin_amdgcn_sched_barrier(0);   // one face vertex's columns at a time: bounds the live registers
 				const float z = V3[i].z;
 				const float z2 = z * z;
 				const float P0[3] = {a.ndc.ndc.fx / z, 0.f, -a.ndc.ndc.fx * V3[i].x / z2};
@@ -221,7 +233,7 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_pixel_jacobians(FitPixelArgs a) {
 #pragma unroll
 				for (int r = 0; r < 3; r++)
 #pragma unroll
-					for (int c = 0; c < 3; c++) Jc[r][c] = Dn[i][r][0] * P0[c] + Dn[i][r][1] * P1[c];
+					for (int c = 0; c < 3; c++) Jc[r][c] = DN(i, r, 0) * P0[c] + DN(i, r, 1) * P1[c];
 				if (a.perspective) {
 					float J2[3][3];
 #pragma unroll
@@ -229,7 +241,7 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_pixel_jacobians(FitPixelArgs a) {
 #pragma unroll
 						for (int c = 0; c < 3; c++) J2[r][c] = (Pd[r][0] * Jc[0][c] + Pd[r][1] * Jc[1][c]) + Pd[r][2] * Jc[2][c];
 #pragma unroll
-					for (int r = 0; r < 3; r++) J2[r][2] += Pz[r][i];
+					for (int r = 0; r < 3; r++) J2[r][2] += PZ(r, i);
 #pragma unroll
 					for (int r = 0; r < 3; r++)
 #pragma unroll
@@ -254,16 +266,13 @@ __global__ __launch_bounds__(PIX_BLOCK) void k_pixel_jacobians(FitPixelArgs a) {
 					}
 					const float x = (rw[0] * w_rc[0] + rw[1] * w_rc[1]) + rw[2] * w_rc[2];
 					const float y = (rn[0] * n_rc[0] + rn[1] * n_rc[1]) + rn[2] * n_rc[2];
-					dr_dV[3 * i + c] = x + y;
+					rec_f[3 * i + c] = x + y;   // stored as formed: no 9-float tail of live outputs
 				}
 			}
-			float4* rec = a.records + 4 * p;
-			rec[0] = make_float4(dr_dV[0], dr_dV[1], dr_dV[2], dr_dV[3]);
-			rec[1] = make_float4(dr_dV[4], dr_dV[5], dr_dV[6], dr_dV[7]);
-			rec[2] = make_float4(dr_dV[8], rn[0], rn[1], rn[2]);
-			rec[3] = make_float4(rho[0], rho[1], rho[2], residual);
+#undef DN
+#undef PZ
+
 		}
-		a.keys[p] = contributes ? static_cast<uint64_t>(static_cast<uint32_t>(face)) : EMPTY_KEY;
 	}
 }
 

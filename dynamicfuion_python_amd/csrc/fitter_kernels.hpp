@@ -15,6 +15,7 @@ struct FitPixelArgs {
 	Camera pix;             // pixel-space intrinsics (float)
 	NdcSetup ndc;
 	float blur;             // NDC units
+	PixelAxis ax, ay;       // pixel-centre NDC constants (make_pixel_axis)
 	int perspective;
 	float max_depth;
 	int use_tukey;
