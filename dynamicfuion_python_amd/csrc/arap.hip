@@ -491,6 +491,84 @@ __device__ inline float rhs_row_update(const float* L, int64_t ld, const float* 
 }
 
 
+// Column eliminations J0 <= j < J1 of the row pairs ap (lane = row), applied to the columns c < J1 only, in blocks of
+// four: the four columns are factored among themselves, then applied to every later column c with four packed FMAs
+// whose multipliers L_c,jb..jb+3 are read from lane c by readlane (scalar operands: nothing on the elimination path
+// waits on LDS). Every element sees its updates in ascending column order.
+template <int J0, int J1>
+__device__ inline void eliminate_columns(f32x2 (&ap)[CORNER_NB], int lane, int& bad) {
+	__shared__ float4 s_l4[2][CORNER_NB];   // s_l4[.][c] = (L_c,jb .. L_c,jb+3)
+#pragma clang loop unroll(full)
+	for (int jb = J0; jb < J1; jb += 4) {
+		// The 4 x 4 diagonal sub-block is read once (10 independent readlanes) and factored wave-uniformly; every lane
+		// then runs the same operations on its own row with the uniform multipliers. The uniform values are exactly
+		// the ones lanes jb..jb+3 compute (same operations, same order), so the pivot chain has no readlane round trip
+		// per column.
+		float M[4][4], Lu[4][4], rsv[4];
+#pragma unroll
+		for (int q = 0; q < 4; q++)
+#pragma unroll
+			for (int i = q; i < 4; i++) M[i][q] = lane_bcast(ap[jb + q].x, jb + i);
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			float piv = M[q][q];   // A_jj after the first j eliminations
+			bad |= !(piv > 0.f);
+			piv = piv > 0.f ? piv : 1.f;
+			rsv[q] = __builtin_amdgcn_rsqf(piv);
+#pragma unroll
+			for (int i = q; i < 4; i++) Lu[i][q] = M[i][q] * rsv[q];
+#pragma unroll
+			for (int q2 = q + 1; q2 < 4; q2++)
+#pragma unroll
+				for (int i = q2; i < 4; i++) M[i][q2] = __builtin_fmaf(-Lu[i][q], Lu[q2][q], M[i][q2]);
+		}
+		float lx[4];
+		f32x2 nl[4];
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			const f32x2 l = ap[jb + q] * rsv[q];   // (L_rj for rows r >= j of the diagonal block, panel / rhs entry)
+			ap[jb + q] = l;
+			lx[q] = l.x;
+			nl[q] = -l;
+#pragma unroll
+			for (int q2 = q + 1; q2 < 4; q2++) {
+				const float lc = Lu[q2][q];
+				ap[jb + q2] = __builtin_elementwise_fma(nl[q], f32x2{lc, lc}, ap[jb + q2]);
+			}
+		}
+		// next block's columns first (readlane: on the pivot chain), the rest from a wave-uniform 16-B LDS broadcast
+		// whose latency hides behind them
+		float4* row = &s_l4[(jb >> 2) & 1][0];
+		if (jb + 8 < J1) row[lane] = make_float4(lx[0], lx[1], lx[2], lx[3]);
+#pragma unroll
+		for (int q = 0; q < 4; q++)   // q outer: consecutive FMAs are independent
+#pragma unroll
+			for (int c = jb + 4; c < J1 && c < jb + 8; c++) {
+				const float lc = lane_bcast(lx[q], c);   // L_c,jb+q, c > jb + 3
+				ap[c] = __builtin_elementwise_fma(nl[q], f32x2{lc, lc}, ap[c]);
+			}
+#pragma unroll
+		for (int c0 = jb + 8; c0 < J1; c0 += 8) {   // chunks of 8 columns: 8 broadcasts in flight
+			float4 L4[8];
+#pragma unroll
+			for (int u = 0; u < 8; u++)
+				if (c0 + u < J1) L4[u] = row[c0 + u];
+#pragma unroll
+			for (int u = 0; u < 8; u++)
+				if (c0 + u < J1) ap[c0 + u] = __builtin_elementwise_fma(nl[0], f32x2{L4[u].x, L4[u].x}, ap[c0 + u]);
+#pragma unroll
+			for (int u = 0; u < 8; u++)
+				if (c0 + u < J1) ap[c0 + u] = __builtin_elementwise_fma(nl[1], f32x2{L4[u].y, L4[u].y}, ap[c0 + u]);
+#pragma unroll
+			for (int u = 0; u < 8; u++)
+				if (c0 + u < J1) ap[c0 + u] = __builtin_elementwise_fma(nl[2], f32x2{L4[u].z, L4[u].z}, ap[c0 + u]);
+#pragma unroll
+			for (int u = 0; u < 8; u++)
+				if (c0 + u < J1) ap[c0 + u] = __builtin_elementwise_fma(nl[3], f32x2{L4[u].w, L4[u].w}, ap[c0 + u]);
+		}
+	}
+}
+
 __global__ __launch_bounds__(CT) void k_chol_step(float* __restrict__ A, int ld, int k, int T, float* __restrict__ b, int* error_flag) {
 	__shared__ float s_d[CORNER_NB * CS4];   // A_kk after the previous block's update
 	__shared__ float s_p[CORNER_NB * CS4];   // A_Ik after the previous block's update (panel workgroups below the diagonal)
@@ -541,97 +619,68 @@ __global__ __launch_bounds__(CT) void k_chol_step(float* __restrict__ A, int ld,
 		if (diag && t < CORNER_NB) s_b[t] = b[ok0 + t];
 	}
 	__syncthreads();
-	if (wave != 0) return;
 	// ap[c] = (A_kk[lane][c], A_Ik[lane][c]): both rows see the same column operations, so one packed FMA
-	// (v_pk_fma_f32) updates the pair
+	// (v_pk_fma_f32) updates the pair. Wave 0 holds them; the other waves join for the rank-32 update between the halves.
 	f32x2 ap[CORNER_NB];
-#pragma unroll
-	for (int q = 0; q < CORNER_NB / 4; q++) {
-		const float4 va = *reinterpret_cast<const float4*>(s_d + lane * CS4 + 4 * q);
-		float4 vp;
-		if (diag)   // the augmented row: b_k on lane 0, zero elsewhere
-			vp = lane == 0 ? *reinterpret_cast<const float4*>(s_b + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
-		else
-			vp = *reinterpret_cast<const float4*>(s_p + lane * CS4 + 4 * q);
-		ap[4 * q] = f32x2{va.x, vp.x};
-		ap[4 * q + 1] = f32x2{va.y, vp.y};
-		ap[4 * q + 2] = f32x2{va.z, vp.z};
-		ap[4 * q + 3] = f32x2{va.w, vp.w};
-	}
-	// Column eliminations in blocks of four: the four columns are factored among themselves, then applied to every
-	// later column c with four packed FMAs whose multipliers L_c,jb..jb+3 are read from lane c by readlane (scalar
-	// operands: nothing on the elimination path waits on LDS). Every element sees its updates in ascending column order.
-	__shared__ float4 s_l4[2][CORNER_NB];   // s_l4[.][c] = (L_c,jb .. L_c,jb+3)
 	int bad = 0;
-#pragma clang loop unroll(full)
-	for (int jb = 0; jb < CORNER_NB; jb += 4) {
-		// The 4 x 4 diagonal sub-block is read once (10 independent readlanes) and factored wave-uniformly; every lane
-		// then runs the same operations on its own row with the uniform multipliers. The uniform values are exactly
-		// the ones lanes jb..jb+3 compute (same operations, same order), so the pivot chain has no readlane round trip
-		// per column.
-		float M[4][4], Lu[4][4], rsv[4];
+	if (wave == 0) {
 #pragma unroll
-		for (int q = 0; q < 4; q++)
-#pragma unroll
-			for (int i = q; i < 4; i++) M[i][q] = lane_bcast(ap[jb + q].x, jb + i);
-#pragma unroll
-		for (int q = 0; q < 4; q++) {
-			float piv = M[q][q];   // A_jj after the first j eliminations
-			bad |= !(piv > 0.f);
-			piv = piv > 0.f ? piv : 1.f;
-			rsv[q] = __builtin_amdgcn_rsqf(piv);
-#pragma unroll
-			for (int i = q; i < 4; i++) Lu[i][q] = M[i][q] * rsv[q];
-#pragma unroll
-			for (int q2 = q + 1; q2 < 4; q2++)
-#pragma unroll
-				for (int i = q2; i < 4; i++) M[i][q2] = __builtin_fmaf(-Lu[i][q], Lu[q2][q], M[i][q2]);
+		for (int q = 0; q < CORNER_NB / 4; q++) {
+			const float4 va = *reinterpret_cast<const float4*>(s_d + lane * CS4 + 4 * q);
+			float4 vp;
+			if (diag)   // the augmented row: b_k on lane 0, zero elsewhere
+				vp = lane == 0 ? *reinterpret_cast<const float4*>(s_b + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+			else
+				vp = *reinterpret_cast<const float4*>(s_p + lane * CS4 + 4 * q);
+			ap[4 * q] = f32x2{va.x, vp.x};
+			ap[4 * q + 1] = f32x2{va.y, vp.y};
+			ap[4 * q + 2] = f32x2{va.z, vp.z};
+			ap[4 * q + 3] = f32x2{va.w, vp.w};
 		}
-		float lx[4];
-		f32x2 nl[4];
+		eliminate_columns<0, CORNER_NB / 2>(ap, lane, bad);
+		// L[:, 0:32] of the A_kk rows and of the panel rows -> LDS (s_d / s_p are free once loaded)
 #pragma unroll
-		for (int q = 0; q < 4; q++) {
-			const f32x2 l = ap[jb + q] * rsv[q];   // (L_rj for rows r >= j of the diagonal block, panel / rhs entry)
-			ap[jb + q] = l;
-			lx[q] = l.x;
-			nl[q] = -l;
-#pragma unroll
-			for (int q2 = q + 1; q2 < 4; q2++) {
-				const float lc = Lu[q2][q];
-				ap[jb + q2] = __builtin_elementwise_fma(nl[q], f32x2{lc, lc}, ap[jb + q2]);
-			}
-		}
-		// next block's columns first (readlane: on the pivot chain), the rest from a wave-uniform 16-B LDS broadcast
-		// whose latency hides behind them
-		float4* row = &s_l4[(jb >> 2) & 1][0];
-		if (jb + 8 < CORNER_NB) row[lane] = make_float4(lx[0], lx[1], lx[2], lx[3]);
-#pragma unroll
-		for (int q = 0; q < 4; q++)   // q outer: consecutive FMAs are independent
-#pragma unroll
-			for (int c = jb + 4; c < CORNER_NB && c < jb + 8; c++) {
-				const float lc = lane_bcast(lx[q], c);   // L_c,jb+q, c > jb + 3
-				ap[c] = __builtin_elementwise_fma(nl[q], f32x2{lc, lc}, ap[c]);
-			}
-#pragma unroll
-		for (int c0 = jb + 8; c0 < CORNER_NB; c0 += 8) {   // chunks of 8 columns: 8 broadcasts in flight
-			float4 L4[8];
-#pragma unroll
-			for (int u = 0; u < 8; u++)
-				if (c0 + u < CORNER_NB) L4[u] = row[c0 + u];
-#pragma unroll
-			for (int u = 0; u < 8; u++)
-				if (c0 + u < CORNER_NB) ap[c0 + u] = __builtin_elementwise_fma(nl[0], f32x2{L4[u].x, L4[u].x}, ap[c0 + u]);
-#pragma unroll
-			for (int u = 0; u < 8; u++)
-				if (c0 + u < CORNER_NB) ap[c0 + u] = __builtin_elementwise_fma(nl[1], f32x2{L4[u].y, L4[u].y}, ap[c0 + u]);
-#pragma unroll
-			for (int u = 0; u < 8; u++)
-				if (c0 + u < CORNER_NB) ap[c0 + u] = __builtin_elementwise_fma(nl[2], f32x2{L4[u].z, L4[u].z}, ap[c0 + u]);
-#pragma unroll
-			for (int u = 0; u < 8; u++)
-				if (c0 + u < CORNER_NB) ap[c0 + u] = __builtin_elementwise_fma(nl[3], f32x2{L4[u].w, L4[u].w}, ap[c0 + u]);
+		for (int q = 0; q < CORNER_NB / 8; q++) {
+			*reinterpret_cast<float4*>(s_d + lane * CS4 + 4 * q) = make_float4(ap[4 * q].x, ap[4 * q + 1].x, ap[4 * q + 2].x, ap[4 * q + 3].x);
+			*reinterpret_cast<float4*>(s_p + lane * CS4 + 4 * q) = make_float4(ap[4 * q].y, ap[4 * q + 1].y, ap[4 * q + 2].y, ap[4 * q + 3].y);
 		}
 	}
+	__syncthreads();
+	// rank-32 update of columns 32..63: C = L[rows, 0:32] L_kk[32:64, 0:32]^T on the MFMA, one 32-row block per wave
+	// (wave 1: A_kk rows 32..63; waves 2, 3: panel rows 0..31, 32..63; A_kk rows 0..31 lie above the diagonal there)
+	f32x16 cacc = {};
+	if (wave > 0) {
+		const float* X = wave == 1 ? s_d + 32 * CS4 : s_p + 32 * (wave - 2) * CS4;
+		const int half = lane >> 5, l32 = lane & 31;
+		const float4* x4 = reinterpret_cast<const float4*>(X + l32 * CS4 + 16 * half);
+		const float4* y4 = reinterpret_cast<const float4*>(s_d + (32 + l32) * CS4 + 16 * half);
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			const float4 vx = x4[q], vy = y4[q];
+			cacc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx.x, vy.x, cacc, 0, 0, 0);
+			cacc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx.y, vy.y, cacc, 0, 0, 0);
+			cacc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx.z, vy.z, cacc, 0, 0, 0);
+			cacc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx.w, vy.w, cacc, 0, 0, 0);
+		}
+	}
+	__syncthreads();   // every wave is done reading L before the products overwrite it
+	if (wave > 0) {
+		float* Cb = wave == 1 ? s_d + 32 * CS4 : s_p + 32 * (wave - 2) * CS4;
+#pragma unroll
+		for (int v = 0; v < 16; v++) Cb[quad_row(v, lane) * CS4 + 32 + (lane & 31)] = cacc[v];
+	}
+	__syncthreads();
+	if (wave != 0) return;
+#pragma unroll
+	for (int q = CORNER_NB / 8; q < CORNER_NB / 4; q++) {
+		const float4 ca = lane >= 32 ? *reinterpret_cast<const float4*>(s_d + lane * CS4 + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+		const float4 cp = *reinterpret_cast<const float4*>(s_p + lane * CS4 + 4 * q);
+		ap[4 * q] -= f32x2{ca.x, cp.x};
+		ap[4 * q + 1] -= f32x2{ca.y, cp.y};
+		ap[4 * q + 2] -= f32x2{ca.z, cp.z};
+		ap[4 * q + 3] -= f32x2{ca.w, cp.w};
+	}
+	eliminate_columns<CORNER_NB / 2, CORNER_NB>(ap, lane, bad);
 	const bool ok = !bad;
 	if (diag) {
 		float4* wa = reinterpret_cast<float4*>(A + (ok0 + lane) * LD + ok0);
