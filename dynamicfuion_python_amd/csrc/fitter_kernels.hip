@@ -330,13 +330,15 @@ nnrt_status launch_face_node_table(const int4* faces4, int64_t F, const int32_t*
 }
 
 // minimum over the 64 lanes (DPP row shifts, then row broadcasts into lane 63), wave-uniform result
+// (lanes without a DPP source read the identity INT_MAX, which lets the compiler fold each step into one v_min_i32_dpp)
 __device__ inline int wave_min_i32(int v) {
-	v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x111, 0xf, 0xf, false));   // row_shr:1
-	v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x112, 0xf, 0xf, false));   // row_shr:2
-	v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x114, 0xf, 0xf, false));   // row_shr:4
-	v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x118, 0xf, 0xf, false));   // row_shr:8
-	v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
-	v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
+	constexpr int ID = 0x7fffffff;
+	v = min(v, __builtin_amdgcn_update_dpp(ID, v, 0x111, 0xf, 0xf, false));   // row_shr:1
+	v = min(v, __builtin_amdgcn_update_dpp(ID, v, 0x112, 0xf, 0xf, false));   // row_shr:2
+	v = min(v, __builtin_amdgcn_update_dpp(ID, v, 0x114, 0xf, 0xf, false));   // row_shr:4
+	v = min(v, __builtin_amdgcn_update_dpp(ID, v, 0x118, 0xf, 0xf, false));   // row_shr:8
+	v = min(v, __builtin_amdgcn_update_dpp(ID, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+	v = min(v, __builtin_amdgcn_update_dpp(ID, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
 	return __builtin_amdgcn_readlane(v, 63);
 }
 
@@ -470,7 +472,8 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 				for (int t = 0; t < NSLOT - 1; t++) ent[t] = ent[t + 1];
 				ent[NSLOT - 1] = FACE_NODE_NONE;
 			}
-			filed += min(__popcll(M), room);
+			const int n_head = __popcll(M);
+			filed += n_head < room ? n_head : room;   // (integer select: the generic min() overload went through double)
 		}
 		return filed;
 	};
