@@ -106,6 +106,7 @@ _SIGNATURES = {
     "nnrt_compute_vertex_normals": (c_int32, [c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
     "nnrt_compute_ordered_point_cloud_normals": (c_int32, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p]),
     "nnrt_solve_block_diagonal_cholesky": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
+    "nnrt_invert_positive_semidefinite_blocks": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     "nnrt_solve_block_sparse_arrowhead_cholesky": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p,
                                                              c_void_p, c_void_p]),
     # TSDF voxel block grid

@@ -210,14 +210,7 @@ __global__ __launch_bounds__(64) void k_arrow_stem(int n0, const float* __restri
 		return;
 	}
 	float Di[6][6];
-#pragma unroll
-	for (int c = 0; c < 6; c++) {
-		float col[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-		col[c] = 1.f;
-		cholesky_solve_small<6>(L, col);
-#pragma unroll
-		for (int r = 0; r < 6; r++) Di[r][c] = col[r];
-	}
+	invert_from_cholesky_small<6>(L, Di);
 #pragma unroll
 	for (int k = 0; k < 36; k++) dinv[static_cast<int64_t>(i) * 36 + k] = Di[k / 6][k % 6];
 	for (int ei = edge_offsets[i]; ei < edge_offsets[i + 1]; ei++) {

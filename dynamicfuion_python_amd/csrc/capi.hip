@@ -1357,6 +1357,27 @@ nnrt_status nnrt_solve_block_diagonal_cholesky(const float* d_blocks, const floa
 	return NNRT_OK;
 }
 
+nnrt_status nnrt_invert_positive_semidefinite_blocks(const float* d_blocks, int32_t count, int32_t block_size, float* d_out, void* stream) {
+	hipStream_t s = static_cast<hipStream_t>(stream);
+	NNRT_CHECK_ARG(count >= 0, "negative block count");
+	int* flag = nullptr;
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&flag), sizeof(int), s));
+	NNRT_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
+	nnrt_status st = launch_invert_psd_blocks(d_blocks, count, block_size, d_out, flag, s);
+	int host_flag = 0;
+	if (!st) {
+		NNRT_HIP(hipMemcpyAsync(&host_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
+		NNRT_HIP(hipStreamSynchronize(s));
+	}
+	hipFreeAsync(flag, s);
+	if (st) return st;
+	if (host_flag) {
+		set_error("potrf failed in InvertPositiveSemidefiniteBlocks (block not positive-definite)");
+		return NNRT_ERROR_NOT_POSITIVE_DEFINITE;
+	}
+	return NNRT_OK;
+}
+
 nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, const float* d_wing, const int32_t* d_coords, int32_t E, int32_t N,
                                                        int32_t n0, const float* d_b, float* d_x, void* stream) {
 	NNRT_CHECK_ARG(n0 >= 0 && n0 <= N, "arrow_base_block_index out of range");

@@ -831,4 +831,42 @@ nnrt_status launch_solve_block_diagonal(const float* blocks, const float* b, int
 	return NNRT_OK;
 }
 
+// block-wise SPD inverse (API stage entry point; the same device functions as the arrowhead stem's D^-1)
+template <int S>
+__global__ void k_invert_psd_blocks(const float* __restrict__ blocks, int count, float* __restrict__ out, int* error_flag) {
+	const int n = blockIdx.x * blockDim.x + threadIdx.x;
+	if (n >= count) return;
+	float L[S][S], Ai[S][S];
+#pragma unroll
+	for (int r = 0; r < S; r++)
+#pragma unroll
+		for (int c = 0; c < S; c++) L[r][c] = blocks[static_cast<int64_t>(n) * S * S + r * S + c];
+	if (!cholesky_small<S>(L)) {
+		atomicOr(error_flag, 1);
+#pragma unroll
+		for (int r = 0; r < S; r++)
+#pragma unroll
+			for (int c = 0; c < S; c++) Ai[r][c] = NAN;
+	} else {
+		invert_from_cholesky_small<S>(L, Ai);
+	}
+#pragma unroll
+	for (int r = 0; r < S; r++)
+#pragma unroll
+		for (int c = 0; c < S; c++) out[static_cast<int64_t>(n) * S * S + r * S + c] = Ai[r][c];
+}
+
+nnrt_status launch_invert_psd_blocks(const float* blocks, int count, int s, float* out, int* error_flag, hipStream_t stream) {
+	if (count == 0) return NNRT_OK;
+	const unsigned grid = static_cast<unsigned>(ceil_div(count, 256));
+	if (s == 6) k_invert_psd_blocks<6><<<grid, 256, 0, stream>>>(blocks, count, out, error_flag);
+	else if (s == 3) k_invert_psd_blocks<3><<<grid, 256, 0, stream>>>(blocks, count, out, error_flag);
+	else {
+		set_error("block size must be 3 or 6");
+		return NNRT_ERROR_ARGUMENT;
+	}
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
 } // namespace nnrt

@@ -170,7 +170,23 @@ __host__ __device__ inline void cholesky_solve_small(const float (&L)[n][n], flo
 	}
 }
 
+// A^-1 from the lower Cholesky factor L of an SPD block: one potrs per identity column (InvertBlocks.cpp:82-126,
+// potrf + potrs against the identity); the arrowhead stem's D^-1 and nnrt_invert_positive_semidefinite_blocks
+template <int n>
+__host__ __device__ inline void invert_from_cholesky_small(const float (&L)[n][n], float (&Ai)[n][n]) {
+#pragma unroll
+	for (int c = 0; c < n; c++) {
+		float col[n];
+#pragma unroll
+		for (int r = 0; r < n; r++) col[r] = r == c ? 1.f : 0.f;
+		cholesky_solve_small<n>(L, col);
+#pragma unroll
+		for (int r = 0; r < n; r++) Ai[r][c] = col[r];
+	}
+}
+
 nnrt_status launch_solve_block_diagonal(const float* blocks, const float* b, int count, int s, float* x, int* error_flag, hipStream_t stream);
+nnrt_status launch_invert_psd_blocks(const float* blocks, int count, int s, float* out, int* error_flag, hipStream_t stream);
 nnrt_status solve_arrowhead(const float* diag, const float* wing, const int32_t* coords, int E, int N, int n0, const float* b, float* x,
                             int* error_flag, hipStream_t stream);
 

@@ -281,6 +281,11 @@ nnrt_status nnrt_axis_angle_to_matrices_rodrigues(const float* d_vectors, int32_
 /* SolveBlockDiagonalCholesky (cpp/core/linalg/SolveBlockDiagonalCholesky.cpp): x_i = A_i^-1 b_i, block size 3 or 6 */
 nnrt_status nnrt_solve_block_diagonal_cholesky(const float* d_blocks, const float* d_b, int32_t block_count, int32_t block_size,
                                                float* d_x, void* stream);
+/* InvertPositiveSemidefiniteBlocks (cpp/core/linalg/InvertBlocks.cpp:82-126: potrf + potrs against the identity per
+ * block), block size 3 or 6, row-major [count, s, s] -> [count, s, s]; the arrowhead stem's D^-1 runs the same device
+ * functions. NNRT_ERROR_NOT_POSITIVE_DEFINITE if a block's potrf fails (its output is NaN). */
+nnrt_status nnrt_invert_positive_semidefinite_blocks(const float* d_blocks, int32_t block_count, int32_t block_size, float* d_out,
+                                                     void* stream);
 /* SolveBlockSparseArrowheadCholesky (cpp/core/linalg/SolveBlockSparseArrowheadCholesky.cpp:30-95), 6x6 blocks:
  * d_diagonal_blocks [N,6,6], d_wing_blocks [E,6,6] at block coordinates d_wing_coordinates [E,2] (row < arrow_base
  * <= column for stem-to-corner blocks; row >= arrow_base for corner off-diagonal blocks), b [6N]. */

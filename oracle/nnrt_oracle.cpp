@@ -1193,6 +1193,27 @@ void CholeskySolveInPlace(const float* L, int n, float* b) {
 }
 } // namespace
 
+// InvertBlocks.cpp:82-126 (InvertPositiveSemidefiniteBlocks): potrf, then potrs against the identity, per block.
+// Returns 0, or 1 + the first block whose potrf fails.
+ORC_API int orc_invert_psd_blocks(const float* blocks, int N, int s, float* out) {
+	int fail = 0;
+	for (int n = 0; n < N; n++) {
+		float L[36];
+		for (int i = 0; i < s * s; i++) L[i] = blocks[static_cast<int64_t>(n) * s * s + i];
+		if (!CholeskyInPlace(L, s)) {
+			if (!fail) fail = n + 1;
+			continue;
+		}
+		for (int c = 0; c < s; c++) {
+			float col[6] = {0, 0, 0, 0, 0, 0};
+			col[c] = 1.f;
+			CholeskySolveInPlace(L, s, col);
+			for (int r = 0; r < s; r++) out[static_cast<int64_t>(n) * s * s + r * s + c] = col[r];
+		}
+	}
+	return fail;
+}
+
 // lm: added to block diagonals first (PreconditionDiagonalBlocksImpl.h), if > 0. Returns 0, or 1 + failing block.
 ORC_API int orc_solve_block_diagonal(const float* H, const float* g, int N, int s, float lm, float* x) {
 	int fail = 0;

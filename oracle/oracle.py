@@ -343,6 +343,15 @@ def arap_gradient(edges, edge_jacobians, residuals, g):
     return g
 
 
+def invert_psd_blocks(blocks):
+    """InvertPositiveSemidefiniteBlocks (InvertBlocks.cpp:82-126) -> (inverses, rc: 0 or 1 + failing block)."""
+    blocks = _f32(blocks)
+    N, s = blocks.shape[0], blocks.shape[1]
+    out = np.full((N, s, s), np.nan, np.float32)
+    rc = lib().orc_invert_psd_blocks(_p(blocks), ctypes.c_int(N), ctypes.c_int(s), _p(out))
+    return out, rc
+
+
 def solve_block_diagonal(H, g, lm=0.0):
     H, g = _f32(H), _f32(g)
     N, s = H.shape[0], H.shape[1]

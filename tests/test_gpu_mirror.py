@@ -204,6 +204,32 @@ def test_anchor_variable_weight_kat(nn):
     assert np.allclose(-np.sort(-_np(w), axis=1), L.ANCHOR_VAR_WEIGHTS_SORTED, rtol=1e-3, atol=1e-6)
 
 
+def test_invert_psd_blocks_kat(nn, oracle_mod):
+    """cpp/tests/test_linalg_block_routines.cpp:158-190 through the C-ABI (the arrowhead stem's D^-1 device functions),
+    bit-exact against the oracle's potrf + potrs restatement, and for 6x6 blocks; a non-PD block raises like potrf."""
+    import torch
+    from dynamicfuion_python_amd import _native as NV
+    dev = torch.device("cuda", 0)
+
+    def inv(blocks):
+        d = torch.from_numpy(np.ascontiguousarray(blocks, np.float32)).to(dev)
+        out = torch.empty_like(d)
+        NV.check(NV.lib().nnrt_invert_positive_semidefinite_blocks(NV.ptr(d), d.shape[0], d.shape[1], NV.ptr(out), NV.stream_ptr()))
+        return out.cpu().numpy()
+
+    g = inv(L.INVERT_PSD_BLOCKS)
+    assert np.allclose(g, L.INVERT_PSD_BLOCKS_GT, rtol=1e-4, atol=1e-8)
+    assert np.array_equal(g, oracle_mod.invert_psd_blocks(L.INVERT_PSD_BLOCKS)[0])
+    rng = np.random.default_rng(3)
+    a = rng.normal(size=(300, 6, 6)).astype(np.float32)
+    spd = (a @ a.transpose(0, 2, 1) + 6 * np.eye(6, dtype=np.float32)).astype(np.float32)
+    assert np.array_equal(inv(spd), oracle_mod.invert_psd_blocks(spd)[0])
+    bad = spd.copy()
+    bad[7] = -bad[7]
+    with pytest.raises(RuntimeError, match="potrf"):
+        inv(bad)
+
+
 def test_matmul3d_kat(nn):
     c = nn.core.matmul3d(L.MATMUL3D_A, L.MATMUL3D_B)
     assert np.allclose(_np(c), L.MATMUL3D_C, atol=1e-6)

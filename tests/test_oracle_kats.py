@@ -295,3 +295,20 @@ def test_warp_points_threshold_semantics(oracle_mod):
     assert not wp[valid < 2].any()
     ref, _ = oracle_mod.warp_points(pts, None, nodes, R, t, a, w)
     assert np.array_equal(wp[valid >= 2], ref[valid >= 2])
+
+
+def test_invert_psd_blocks_kat(oracle_mod):
+    # cpp/tests/test_linalg_block_routines.cpp:158-190 (potrf + potrs against the identity, InvertBlocks.cpp:82-126)
+    inv, rc = oracle_mod.invert_psd_blocks(L.INVERT_PSD_BLOCKS)
+    assert rc == 0
+    assert np.allclose(inv, L.INVERT_PSD_BLOCKS_GT, rtol=1e-4, atol=1e-8)
+    # 6x6 blocks (the arrowhead stem's D^-1): inverse times block is the identity
+    rng = np.random.default_rng(3)
+    a = rng.normal(size=(5, 6, 6)).astype(np.float32)
+    spd = (a @ a.transpose(0, 2, 1) + 6 * np.eye(6, dtype=np.float32)).astype(np.float32)
+    inv6, rc6 = oracle_mod.invert_psd_blocks(spd)
+    assert rc6 == 0
+    assert np.allclose(inv6.astype(np.float64) @ spd.astype(np.float64), np.eye(6), atol=1e-4)
+    bad = spd.copy()
+    bad[2] = -bad[2]
+    assert oracle_mod.invert_psd_blocks(bad)[1] == 3
