@@ -367,7 +367,7 @@ static_assert(2 * NG_ROWS == PIX_TILE, "pass 2 walks the pass-1 tiles");
 __device__ inline void ng_flush(double* dst, double v) { atomicAdd(dst, v); }
 
 template <int MODE, int MAXK>
-__global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_grouped(FitPixelArgs a) {
+__global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 6 : 4) void k_node_reduce_grouped(FitPixelArgs a) {
 	using T = ModeTraits<MODE>;
 	constexpr int S = T::S;
 	constexpr int NSLOT = 3 * MAXK;
@@ -378,6 +378,7 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 	static_assert(T::NACC <= GROUP && NG_CAP % G == 0 && SEG % NG_BATCH == 0 && NG_STRIDE >= NG_CAP && (NG_STRIDE & 1), "slot layout");
 	static_assert(NSLOT % 4 == 0, "face table rows are loaded as int4");
 	__shared__ float s_slots[PIX_BLOCK / 64][2][8 * NG_STRIDE];
+	__shared__ uint32_t s_ent[PIX_BLOCK / 64][NSLOT][64];   // each pixel lane's face-table row (lane-private column)
 
 	// tiles of 16 x 16 pixels (the pass-1 tiles), one 8 x 8 block per wave
 	const int tiles = a.tiles_x * a.tiles_y;
@@ -391,32 +392,31 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 	const int pu0 = tu * PIX_TILE + (wave & 1) * 8, pv0 = tv * 2 * NG_ROWS + (wave >> 1) * NG_ROWS;
 	const int KA = a.anchor_count;
 
-	uint32_t ent[NSLOT];   // this pixel's face: distinct anchor nodes still to be filed, ascending (head = ent[0])
+	// this pixel's face: distinct anchor nodes still to be filed, ascending; the row waits in LDS (s_ent[wave][.][lane]),
+	// the current head in a register (head_at: its index)
+	uint32_t head_e = FACE_NODE_NONE;
+	int head_at = 0;
 	int vid[3] = {0, 0, 0};
-#pragma unroll
-	for (int t = 0; t < NSLOT; t++) ent[t] = FACE_NODE_NONE;
 	if (in_image) {
 		const int64_t p = static_cast<int64_t>(v) * a.W + u;
 		const uint64_t key = a.keys[p];
 		a.keys[p] = EMPTY_KEY;   // ready for the next iteration's scatter
 		if (key != EMPTY_KEY) {
-			const float4* rec = a.records + 4 * p;
-			const float4 q0 = rec[0], q1 = rec[1], q2 = rec[2], q3 = rec[3];
 			const int face = static_cast<int>(key & 0xffffffffu);
 			const int4 fi = a.faces4[face];
 			const uint4* fn4 = reinterpret_cast<const uint4*>(a.face_nodes + static_cast<int64_t>(face) * NSLOT);
 #pragma unroll
 			for (int t = 0; t < NSLOT / 4; t++) {
 				const uint4 e4 = fn4[t];
-				ent[4 * t] = e4.x;
-				ent[4 * t + 1] = e4.y;
-				ent[4 * t + 2] = e4.z;
-				ent[4 * t + 3] = e4.w;
+				s_ent[wave][4 * t][lane] = e4.x;
+				s_ent[wave][4 * t + 1][lane] = e4.y;
+				s_ent[wave][4 * t + 2][lane] = e4.z;
+				s_ent[wave][4 * t + 3][lane] = e4.w;
+				if (t == 0) head_e = e4.x;
 			}
 			vid[0] = fi.x;
 			vid[1] = fi.y;
 			vid[2] = fi.z;
-			(void)q0; (void)q1; (void)q2; (void)q3;
 		}
 	}
 
@@ -451,7 +451,7 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 	auto group = [&](float* slots) -> int {
 		int filed = 0;
 		while (filed < NG_CAP) {
-			const int head = static_cast<int>(ent[0] >> FACE_NODE_SHIFT);   // FACE_NODE_MAX_NODES: list exhausted
+			const int head = static_cast<int>(head_e >> FACE_NODE_SHIFT);   // FACE_NODE_MAX_NODES: list exhausted
 			const int X = wave_min_i32(head);
 			if (X == FACE_NODE_MAX_NODES) break;
 			const uint64_t M = __ballot(head == X);
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 			const int room = NG_CAP - filed;
 			if (head == X && rank < room) {
 				const int pos = filed + rank;
-				const uint32_t code = ent[0];
+				const uint32_t code = head_e;
 				slots[pos] = __builtin_bit_cast(float, lane);
 #pragma unroll
 				for (int fv = 0; fv < 3; fv++) {
@@ -468,9 +468,8 @@ __global__ __launch_bounds__(PIX_BLOCK, MAXK <= 4 ? 5 : 4) void k_node_reduce_gr
 					slots[(1 + fv) * NG_STRIDE + pos] = __builtin_bit_cast(float, k != 0xF ? vid[fv] * KA + k : -1);
 				}
 				slots[7 * NG_STRIDE + pos] = __builtin_bit_cast(float, X);
-#pragma unroll
-				for (int t = 0; t < NSLOT - 1; t++) ent[t] = ent[t + 1];
-				ent[NSLOT - 1] = FACE_NODE_NONE;
+				head_at++;
+				head_e = head_at < NSLOT ? s_ent[wave][head_at][lane] : FACE_NODE_NONE;
 			}
 			const int n_head = __popcll(M);
 			filed += n_head < room ? n_head : room;   // (integer select: the generic min() overload went through double)
