@@ -355,12 +355,12 @@ __device__ inline int wave_min_i32(int v) {
 //     at a node change the group adds its totals to the node's fp64 row (one 27-lane atomic). No cross-lane reduction.
 // Chunks are software-pipelined over two LDS buffers: the jv / jn row gathers of chunk c + 1 are in flight while
 // chunk c is summed, and chunk c + 1 is grouped while chunk c's gathers land. Pixel records are staged in LDS.
-constexpr int NG_CAP = 48;     // associations per chunk (one lane each in (2)); lane group g of (3) owns slots
+constexpr int NG_CAP = 64;     // associations per chunk (one lane each in (2)); lane group g of (3) owns slots
                                // [g * NG_CAP / G, (g + 1) * NG_CAP / G), zero-padded past the chunk's count
 // Slot buffers are component-major (word c of slot i at c * NG_STRIDE + i; odd stride: the words one lane group reads
 // in (3) fall in distinct LDS banks). Words: (1) pixel lane, jv/jn row per face vertex (-1: none), node at word 7;
 // (2) J[0..S-1], r at word S (zeros past the count, whose node word repeats the chunk's last node).
-constexpr int NG_STRIDE = 49;
+constexpr int NG_STRIDE = 65;
 constexpr int NG_ROWS = 8;     // pixel rows per wave (8 x NG_ROWS pixels)
 static_assert(2 * NG_ROWS == PIX_TILE, "pass 2 walks the pass-1 tiles");
 
