@@ -432,7 +432,7 @@ __device__ inline float lane_bcast(float v, int src) {
 // A[i = l & 31][k'] = X[32 qr + i][32 (l >> 5) + s] and B[k'][j] = Y[32 qc + j][32 (l >> 5) + s] to MFMA step s, so the 32
 // steps x 2 lane halves cover the 64-wide k range; each lane reads 32 contiguous floats). C/D map: column l & 31, row
 // (v & 3) + 8 (v >> 2) + 4 (l >> 5).
-__device__ inline f32x16 quadrant_xyt(const float* X, const float* Y, int64_t ld, int qr, int qc, int lane) {
+__device__ inline f32x16 quadrant_xyt(const float* X, const float* Y, int64_t ld, int qr, int qc, int lane, f32x16 acc = {}) {
 	const int half = lane >> 5, l32 = lane & 31;
 	const float4* x4 = reinterpret_cast<const float4*>(X + (32 * qr + l32) * ld + 32 * half);
 	const float4* y4 = reinterpret_cast<const float4*>(Y + (32 * qc + l32) * ld + 32 * half);
@@ -442,7 +442,6 @@ __device__ inline f32x16 quadrant_xyt(const float* X, const float* Y, int64_t ld
 		vx[q] = x4[q];
 		vy[q] = y4[q];
 	}
-	f32x16 acc = {};
 #pragma unroll
 	for (int q = 0; q < 8; q++) {
 		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].x, vy[q].x, acc, 0, 0, 0);
@@ -571,24 +570,40 @@ __global__ __launch_bounds__(CT) void k_chol_step(float* __restrict__ A, int ld,
 	const int npanel = T - k;
 	const int64_t ok0 = static_cast<int64_t>(k) * CORNER_NB, op = ok0 - CORNER_NB;   // column offsets of blocks k and k - 1
 	if (static_cast<int>(blockIdx.x) >= npanel) {
-		// ---- trailing tile (I, J), k < J <= I: the previous block's update ----
-		int r = static_cast<int>(blockIdx.x) - npanel, ii = 0;
-		while (r > ii) {   // row ii holds ii + 1 tiles
-			r -= ii + 1;
-			ii++;
+		// ---- trailing tile (I, J), k < J <= I: lazy updates on alternate columns. Launch k updates the columns
+		// J = k + 1, k + 3, .. (every tile I >= J of them) with their pending blocks max(0, k - 2) .. k - 1: each column
+		// takes a rank-128 update every other launch (half the tile passes of one update per block) and is complete up
+		// to block J - 2 when its panel launch stages block J - 1.
+		int r = static_cast<int>(blockIdx.x) - npanel, m = 0, cnt = T - (k + 1);
+		while (r >= cnt) {   // column k + 1 + 2m holds T - (k + 1 + 2m) tiles
+			r -= cnt;
+			m++;
+			cnt -= 2;
 		}
-		const int64_t rI = static_cast<int64_t>(k + 1 + ii) * CORNER_NB, rJ = static_cast<int64_t>(k + 1 + r) * CORNER_NB;
+		const int jj = 2 * m, ii = jj + r;   // J = k + 1 + jj, I = k + 1 + ii
+		const int b0 = k >= 2 ? k - 2 : 0;
+		const int64_t rI = static_cast<int64_t>(k + 1 + ii) * CORNER_NB, rJ = static_cast<int64_t>(k + 1 + jj) * CORNER_NB;
 		const int qr = wave >> 1, qc = wave & 1;
 		float* C = A + rI * LD + rJ + 32 * qc + (lane & 31);
 		float cv[16];
 #pragma unroll
 		for (int v = 0; v < 16; v++) cv[v] = C[(32 * qr + quad_row(v, lane)) * LD];
-		const f32x16 acc = quadrant_xyt(A + rI * LD + op, A + rJ * LD + op, LD, qr, qc, lane);
+		// one product per pending block, subtracted in block order: the same float operations as one update per launch
+		for (int pb = b0; pb < k; pb++) {
+			const int64_t ob = static_cast<int64_t>(pb) * CORNER_NB;
+			const f32x16 acc = quadrant_xyt(A + rI * LD + ob, A + rJ * LD + ob, LD, qr, qc, lane);
 #pragma unroll
-		for (int v = 0; v < 16; v++) C[(32 * qr + quad_row(v, lane)) * LD] = cv[v] - acc[v];
+			for (int v = 0; v < 16; v++) cv[v] -= acc[v];
+		}
+#pragma unroll
+		for (int v = 0; v < 16; v++) C[(32 * qr + quad_row(v, lane)) * LD] = cv[v];
 		if (rI == rJ) {
-			const float s = rhs_row_update(A + rJ * LD + op, LD, b + op, t);
-			if ((t & 3) == 0) b[rJ + (t >> 2)] -= s;
+			float bj = (t & 3) == 0 ? b[rJ + (t >> 2)] : 0.f;
+			for (int pb = b0; pb < k; pb++) {
+				const int64_t ob = static_cast<int64_t>(pb) * CORNER_NB;
+				bj -= rhs_row_update(A + rJ * LD + ob, LD, b + ob, t);
+			}
+			if ((t & 3) == 0) b[rJ + (t >> 2)] = bj;
 		}
 		return;
 	}
@@ -788,8 +803,10 @@ __global__ void k_corner_out(int m, const float* __restrict__ cb, float* __restr
 nnrt_status corner_cholesky_solve(float* A, int ld, float* cb, int* error_flag, hipStream_t stream) {
 	const int T = ld / CORNER_NB;
 	for (int k = 0; k < T; k++) {   // factor [S | b]: the forward substitution rides along as an augmented row
-		const int panel = T - k, below = T - 1 - k;
-		const int trailing = k > 0 ? below * (below + 1) / 2 : 0;
+		const int panel = T - k;
+		int trailing = 0;   // lazy trailing updates on alternate columns (k_chol_step)
+		if (k > 0)
+			for (int J = k + 1; J < T; J += 2) trailing += T - J;
 		k_chol_step<<<panel + trailing, CT, 0, stream>>>(A, ld, k, T, cb, error_flag);
 		NNRT_LAUNCH_CHECK();
 	}
