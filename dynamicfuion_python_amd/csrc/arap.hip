@@ -419,6 +419,8 @@ StemSchurLists build_stem_schur_lists(const int32_t* edges, int E, int n0, int N
 // Every operand of launch k was finished by launch k - 1, so consecutive launches are the only synchronisation.
 // The block back substitution L^T x = y then runs BACK_G block rows per launch (k_chol_back_group).
 constexpr int CT = 256;   // threads per workgroup of the corner kernels
+constexpr int CORNER_LAZY = 4;   // trailing columns are updated every CORNER_LAZY-th launch (k_chol_step; C5: 2 / 3 / 4 / 5 / 6
+                                 // / 8 -> 769 / 743 / 737 / 749 / 814 / 950 us solve stage)
 constexpr int CS4 = CORNER_NB + 4;   // LDS row stride of the staged tiles (16-B aligned rows for ds_read_b128)
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -570,18 +572,18 @@ __global__ __launch_bounds__(CT) void k_chol_step(float* __restrict__ A, int ld,
 	const int npanel = T - k;
 	const int64_t ok0 = static_cast<int64_t>(k) * CORNER_NB, op = ok0 - CORNER_NB;   // column offsets of blocks k and k - 1
 	if (static_cast<int>(blockIdx.x) >= npanel) {
-		// ---- trailing tile (I, J), k < J <= I: lazy updates on alternate columns. Launch k updates the columns
-		// J = k + 1, k + 3, .. (every tile I >= J of them) with their pending blocks max(0, k - 2) .. k - 1: each column
-		// takes a rank-128 update every other launch (half the tile passes of one update per block) and is complete up
-		// to block J - 2 when its panel launch stages block J - 1.
+		// ---- trailing tile (I, J), k < J <= I: lazy updates. Launch k updates the columns J = k + 1, k + 1 + LAZY, ..
+		// (every tile I >= J of them) with their pending blocks max(0, k - LAZY) .. k - 1: each column takes LAZY blocks
+		// every LAZY-th launch (1 / LAZY of the tile passes of one update per block) and is complete up to block J - 2
+		// when its panel launch stages block J - 1.
 		int r = static_cast<int>(blockIdx.x) - npanel, m = 0, cnt = T - (k + 1);
-		while (r >= cnt) {   // column k + 1 + 2m holds T - (k + 1 + 2m) tiles
+		while (r >= cnt) {   // column k + 1 + LAZY m holds T - (k + 1 + LAZY m) tiles
 			r -= cnt;
 			m++;
-			cnt -= 2;
+			cnt -= CORNER_LAZY;
 		}
-		const int jj = 2 * m, ii = jj + r;   // J = k + 1 + jj, I = k + 1 + ii
-		const int b0 = k >= 2 ? k - 2 : 0;
+		const int jj = CORNER_LAZY * m, ii = jj + r;   // J = k + 1 + jj, I = k + 1 + ii
+		const int b0 = k >= CORNER_LAZY ? k - CORNER_LAZY : 0;
 		const int64_t rI = static_cast<int64_t>(k + 1 + ii) * CORNER_NB, rJ = static_cast<int64_t>(k + 1 + jj) * CORNER_NB;
 		const int qr = wave >> 1, qc = wave & 1;
 		float* C = A + rI * LD + rJ + 32 * qc + (lane & 31);
@@ -804,9 +806,9 @@ nnrt_status corner_cholesky_solve(float* A, int ld, float* cb, int* error_flag, 
 	const int T = ld / CORNER_NB;
 	for (int k = 0; k < T; k++) {   // factor [S | b]: the forward substitution rides along as an augmented row
 		const int panel = T - k;
-		int trailing = 0;   // lazy trailing updates on alternate columns (k_chol_step)
+		int trailing = 0;   // lazy trailing updates on every CORNER_LAZY-th column (k_chol_step)
 		if (k > 0)
-			for (int J = k + 1; J < T; J += 2) trailing += T - J;
+			for (int J = k + 1; J < T; J += CORNER_LAZY) trailing += T - J;
 		k_chol_step<<<panel + trailing, CT, 0, stream>>>(A, ld, k, T, cb, error_flag);
 		NNRT_LAUNCH_CHECK();
 	}
