@@ -716,10 +716,11 @@ __global__ __launch_bounds__(CT) void k_chol_step(float* __restrict__ A, int ld,
 // x_{k0-g2} is known every later wave subtracts L_{k0-g2,k0-g}^T x_{k0-g2} from its z (coupling tiles staged in LDS by
 // the whole workgroup), and wave g, once its z is complete, solves L^T x = z by column-oriented substitution (x_i broadcast by readlane; lane = column, so column i of L^T is the lanes'
 // register i). Every workgroup forms the group's x redundantly; workgroup i < kl then applies y_i -= sum L_ki^T x_k
-// (its tiles prefetched meanwhile) and the group's own workgroups store x.
+// (its tiles prefetched meanwhile) and the group's own workgroups store x (into xout, not over y).
 constexpr int BACK_G = 4;
 
-__global__ __launch_bounds__(CT) void k_chol_back_group(const float* __restrict__ A, int ld, int k0, int kl, float* __restrict__ b) {
+__global__ __launch_bounds__(CT) void k_chol_back_group(const float* __restrict__ A, int ld, int k0, int kl, float* __restrict__ b, int m,
+                                                       float* __restrict__ xout) {
 	__shared__ float s_cpl[BACK_G * (BACK_G - 1) / 2][CORNER_NB][CORNER_NB + 1];   // [g(g-1)/2 + g2][r][c] = L_{k0-g2,k0-g}[r][c]
 	__shared__ __attribute__((aligned(16))) float s_x[BACK_G][CORNER_NB];
 	__shared__ float s_part[4][CORNER_NB];
@@ -781,8 +782,8 @@ __global__ __launch_bounds__(CT) void k_chol_back_group(const float* __restrict_
 		}
 	}
 	__syncthreads();
-	if (i >= kl) {
-		if (t < CORNER_NB) b[ci + t] = s_x[k0 - i][t];
+	if (i >= kl) {   // x goes to its own array: the group's y, which b holds, may still be read by a workgroup starting late
+		if (t < CORNER_NB && ci + t < m) xout[ci + t] = s_x[k0 - i][t];
 		return;
 	}
 	float acc = 0.f;
@@ -797,12 +798,8 @@ __global__ __launch_bounds__(CT) void k_chol_back_group(const float* __restrict_
 	if (t < CORNER_NB) b[ci + t] -= (s_part[0][t] + s_part[1][t]) + (s_part[2][t] + s_part[3][t]);
 }
 
-__global__ void k_corner_out(int m, const float* __restrict__ cb, float* __restrict__ x) {
-	const int i = blockIdx.x * blockDim.x + threadIdx.x;
-	if (i < m) x[i] = cb[i];
-}
-
-nnrt_status corner_cholesky_solve(float* A, int ld, float* cb, int* error_flag, hipStream_t stream) {
+// x (the first m corner unknowns) -> xout
+nnrt_status corner_cholesky_solve(float* A, int ld, float* cb, int m, float* xout, int* error_flag, hipStream_t stream) {
 	const int T = ld / CORNER_NB;
 	for (int k = 0; k < T; k++) {   // factor [S | b]: the forward substitution rides along as an augmented row
 		const int panel = T - k;
@@ -814,7 +811,7 @@ nnrt_status corner_cholesky_solve(float* A, int ld, float* cb, int* error_flag, 
 	}
 	for (int k0 = T - 1; k0 >= 0; k0 -= BACK_G) {
 		const int kl = k0 - BACK_G + 1 > 0 ? k0 - BACK_G + 1 : 0;
-		k_chol_back_group<<<k0 + 1, CT, 0, stream>>>(A, ld, k0, kl, cb);
+		k_chol_back_group<<<k0 + 1, CT, 0, stream>>>(A, ld, k0, kl, cb, m, xout);
 		NNRT_LAUNCH_CHECK();
 	}
 	return NNRT_OK;
@@ -895,10 +892,8 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 		}
 	}
 	if (m > 0) {
-		nnrt_status st = corner_cholesky_solve(ws.schur, ld, ws.cb, error_flag, stream);
+		nnrt_status st = corner_cholesky_solve(ws.schur, ld, ws.cb, m, ws.x + 6 * static_cast<int64_t>(ws.n0), error_flag, stream);
 		if (st) return st;
-		k_corner_out<<<static_cast<unsigned>(ceil_div(m, 256)), 256, 0, stream>>>(m, ws.cb, ws.x + 6 * static_cast<int64_t>(ws.n0));
-		NNRT_LAUNCH_CHECK();
 	}
 	if (ws.n0 > 0) {
 		k_arrow_back<<<static_cast<unsigned>(ceil_div(ws.n0, 64)), 64, 0, stream>>>(ws.n0, ws.dinv, ws.edge_offsets, ws.edge_list, edges, wing,
