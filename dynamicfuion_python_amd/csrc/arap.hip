@@ -801,6 +801,10 @@ __global__ __launch_bounds__(CT) void k_chol_back_group(const float* __restrict_
 // x (the first m corner unknowns) -> xout
 nnrt_status corner_cholesky_solve(float* A, int ld, float* cb, int m, float* xout, int* error_flag, hipStream_t stream) {
 	const int T = ld / CORNER_NB;
+	// k_chol_step's panel workgroups read A_kk while the diagonal one overwrites it with L_kk: they must all be resident
+	// before any finishes, which the dispatch order (panels first) guarantees while T fits the chip's 512 workgroup
+	// slots at two per CU (a 32768-unknown corner, 5461 coarse nodes)
+	NNRT_CHECK_ARG(T <= 512, "arrowhead corner larger than 32768 unknowns");
 	for (int k = 0; k < T; k++) {   // factor [S | b]: the forward substitution rides along as an augmented row
 		const int panel = T - k;
 		int trailing = 0;   // lazy trailing updates on every CORNER_LAZY-th column (k_chol_step)
