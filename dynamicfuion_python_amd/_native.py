@@ -107,6 +107,17 @@ _SIGNATURES = {
     "nnrt_compute_ordered_point_cloud_normals": (c_int32, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p]),
     "nnrt_solve_block_diagonal_cholesky": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     "nnrt_invert_positive_semidefinite_blocks": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
+    "nnrt_matmul_block_sparse_row_wise": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
+    "nnrt_matmul_block_sparse": (c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32, c_void_p, c_int32, c_int32,
+                                           c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
+    "nnrt_block_sparse_and_vector_product": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_int64,
+                                                       c_int64, c_void_p, c_void_p]),
+    "nnrt_diagonal_block_sparse_and_vector_product": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
+    "nnrt_sparse_blocks_op": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_int32, c_int32, c_int64, c_int64, c_int32, c_int32,
+                                        c_void_p]),
+    "nnrt_get_sparse_blocks": (c_int32, [c_void_p, c_int64, c_int64, c_int32, c_void_p, c_int32, c_void_p, c_void_p]),
+    "nnrt_transpose_blocks_in_place": (c_int32, [c_void_p, c_int32, c_int32, c_void_p]),
+    "nnrt_invert_triangular_blocks": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p]),
     "nnrt_solve_block_sparse_arrowhead_cholesky": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p,
                                                              c_void_p, c_void_p]),
     # TSDF voxel block grid

@@ -1378,6 +1378,109 @@ nnrt_status nnrt_invert_positive_semidefinite_blocks(const float* d_blocks, int3
 	return NNRT_OK;
 }
 
+extern "C++" {
+// runs launch(flag) on the stream with a zeroed device flag; a raised flag becomes `code` with `message`
+template <typename F>
+nnrt_status with_device_flag(hipStream_t s, nnrt_status code, const char* message, F&& launch) {
+	int* flag = nullptr;
+	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&flag), sizeof(int), s));
+	NNRT_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
+	nnrt_status st = launch(flag);
+	int host_flag = 0;
+	if (!st) {
+		NNRT_HIP(hipMemcpyAsync(&host_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
+		NNRT_HIP(hipStreamSynchronize(s));
+	}
+	hipFreeAsync(flag, s);
+	if (st) return st;
+	if (host_flag) {
+		set_error(message);
+		return code;
+	}
+	return NNRT_OK;
+}
+} // extern "C++"
+
+nnrt_status nnrt_matmul_block_sparse_row_wise(const float* d_a_blocks, int32_t a_block_count, const float* d_b_blocks,
+                                              const int32_t* d_b_coordinates, int32_t b_block_count, int32_t block_size, float* d_c_blocks,
+                                              uint8_t* d_c_mask, void* stream) {
+	NNRT_CHECK_ARG(a_block_count >= 0 && b_block_count >= 0 && block_size > 0, "bad block count or block size");
+	NNRT_CHECK_ARG(b_block_count == 0 || (d_b_blocks && d_b_coordinates && d_c_blocks && d_c_mask), "null pointer");
+	hipStream_t s = static_cast<hipStream_t>(stream);
+	return with_device_flag(s, NNRT_ERROR_ARGUMENT, "negative block row coordinate in MatmulBlockSparseRowWise", [&](int* flag) {
+		return launch_matmul_block_sparse_row_wise(d_a_blocks, a_block_count, d_b_blocks, d_b_coordinates, b_block_count, block_size, d_c_blocks,
+		                                           d_c_mask, flag, s);
+	});
+}
+
+nnrt_status nnrt_matmul_block_sparse(const float* d_a_blocks, int32_t a_block_count, const int16_t* d_a_breadboard, int32_t a_block_rows,
+                                     int32_t a_block_columns, int32_t transpose_a, const float* d_b_blocks, int32_t b_block_count,
+                                     const int16_t* d_b_breadboard, int32_t b_block_rows, int32_t b_block_columns, int32_t transpose_b,
+                                     int32_t block_size, float* d_c_blocks, uint8_t* d_c_mask, void* stream) {
+	NNRT_CHECK_ARG(a_block_count >= 0 && b_block_count >= 0 && block_size > 0, "bad block count or block size");
+	NNRT_CHECK_ARG(a_block_rows >= 0 && a_block_columns >= 0 && b_block_rows >= 0 && b_block_columns >= 0, "negative breadboard size");
+	const int32_t a_inner = transpose_a ? a_block_rows : a_block_columns, b_inner = transpose_b ? b_block_columns : b_block_rows;
+	NNRT_CHECK_ARG(a_inner == b_inner, "Matrix inner dimensions must but do not match.");
+	hipStream_t s = static_cast<hipStream_t>(stream);
+	return with_device_flag(s, NNRT_ERROR_ARGUMENT, "breadboard block index out of range in MatmulBlockSparse", [&](int* flag) {
+		return launch_matmul_block_sparse(d_a_blocks, a_block_count, d_a_breadboard, a_block_rows, a_block_columns, transpose_a != 0, d_b_blocks,
+		                                  b_block_count, d_b_breadboard, b_block_rows, b_block_columns, transpose_b != 0, block_size, d_c_blocks,
+		                                  d_c_mask, flag, s);
+	});
+}
+
+nnrt_status nnrt_block_sparse_and_vector_product(const float* d_blocks, const int32_t* d_coordinates, int32_t block_count, int32_t block_size,
+                                                 int32_t block_row_offset, int32_t block_column_offset, int32_t transpose,
+                                                 const float* d_vector, int64_t vector_length, int64_t m, float* d_out, void* stream) {
+	NNRT_CHECK_ARG(block_count >= 0 && block_size > 0 && vector_length >= 0 && m >= 0, "bad size");
+	NNRT_CHECK_ARG(m % block_size == 0, "output length m must be a multiple of the block size");
+	hipStream_t s = static_cast<hipStream_t>(stream);
+	return with_device_flag(s, NNRT_ERROR_ARGUMENT, "block coordinate outside the matrix in BlockSparseAndVectorProduct", [&](int* flag) {
+		return launch_block_sparse_vector(d_blocks, d_coordinates, block_count, block_size, block_row_offset, block_column_offset, transpose != 0,
+		                                  d_vector, vector_length, d_out, m, flag, s);
+	});
+}
+
+nnrt_status nnrt_diagonal_block_sparse_and_vector_product(const float* d_blocks, int32_t block_count, int32_t block_size, const float* d_vector,
+                                                          float* d_out, void* stream) {
+	NNRT_CHECK_ARG(block_count >= 0 && block_size > 0, "bad block count or block size");
+	return launch_diagonal_block_vector(d_blocks, block_count, block_size, d_vector, d_out, static_cast<hipStream_t>(stream));
+}
+
+nnrt_status nnrt_sparse_blocks_op(float* d_matrix, int64_t rows, int64_t columns, const float* d_blocks, const int32_t* d_coordinates,
+                                  int32_t block_count, int32_t block_size, int64_t block_row_offset, int64_t block_column_offset,
+                                  int32_t transpose, int32_t op, void* stream) {
+	NNRT_CHECK_ARG(rows >= 0 && columns >= 0 && block_count >= 0 && block_size > 0, "bad size");
+	NNRT_CHECK_ARG(op >= 0 && op <= 2, "op must be 0 (fill), 1 (add) or 2 (subtract)");
+	hipStream_t s = static_cast<hipStream_t>(stream);
+	return with_device_flag(s, NNRT_ERROR_ARGUMENT, "block placed outside the matrix", [&](int* flag) {
+		return launch_sparse_blocks_op(d_matrix, rows, columns, d_blocks, d_coordinates, block_count, block_size, block_row_offset,
+		                               block_column_offset, transpose != 0, op, flag, s);
+	});
+}
+
+nnrt_status nnrt_get_sparse_blocks(const float* d_matrix, int64_t rows, int64_t columns, int32_t block_size, const int32_t* d_coordinates,
+                                   int32_t block_count, float* d_blocks, void* stream) {
+	NNRT_CHECK_ARG(rows >= 0 && columns >= 0 && block_count >= 0 && block_size > 0, "bad size");
+	hipStream_t s = static_cast<hipStream_t>(stream);
+	return with_device_flag(s, NNRT_ERROR_ARGUMENT, "block coordinate outside the matrix", [&](int* flag) {
+		return launch_get_sparse_blocks(d_matrix, rows, columns, block_size, d_coordinates, block_count, d_blocks, flag, s);
+	});
+}
+
+nnrt_status nnrt_transpose_blocks_in_place(float* d_blocks, int32_t block_count, int32_t block_size, void* stream) {
+	NNRT_CHECK_ARG(block_count >= 0 && block_size > 0, "bad block count or block size");
+	return launch_transpose_blocks(d_blocks, block_count, block_size, static_cast<hipStream_t>(stream));
+}
+
+nnrt_status nnrt_invert_triangular_blocks(const float* d_blocks, int32_t block_count, int32_t block_size, int32_t upper, float* d_out,
+                                          void* stream) {
+	NNRT_CHECK_ARG(block_count >= 0 && block_size > 0, "bad block count or block size");
+	hipStream_t s = static_cast<hipStream_t>(stream);
+	return with_device_flag(s, NNRT_ERROR_NOT_POSITIVE_DEFINITE, "trtri failed in InvertTriangularBlocks (zero on a block diagonal)",
+	                        [&](int* flag) { return launch_invert_triangular_blocks(d_blocks, block_count, block_size, upper != 0, d_out, flag, s); });
+}
+
 nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, const float* d_wing, const int32_t* d_coords, int32_t E, int32_t N,
                                                        int32_t n0, const float* d_b, float* d_x, void* stream) {
 	NNRT_CHECK_ARG(n0 >= 0 && n0 <= N, "arrow_base_block_index out of range");

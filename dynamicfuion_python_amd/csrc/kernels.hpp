@@ -187,6 +187,22 @@ __host__ __device__ inline void invert_from_cholesky_small(const float (&L)[n][n
 
 nnrt_status launch_solve_block_diagonal(const float* blocks, const float* b, int count, int s, float* x, int* error_flag, hipStream_t stream);
 nnrt_status launch_invert_psd_blocks(const float* blocks, int count, int s, float* out, int* error_flag, hipStream_t stream);
+// block_sparse.hip: the arrowhead's block-sparse stages as API entry points (nnrt.core.linalg)
+nnrt_status launch_matmul_block_sparse_row_wise(const float* a, int a_count, const float* b, const int32_t* b_coords, int64_t count, int s,
+                                                float* c, uint8_t* mask, int* error_flag, hipStream_t stream);
+nnrt_status launch_matmul_block_sparse(const float* a, int a_count, const int16_t* a_board, int a_rows, int a_cols, bool ta, const float* b,
+                                       int b_count, const int16_t* b_board, int b_rows, int b_cols, bool tb, int s, float* c, uint8_t* mask,
+                                       int* error_flag, hipStream_t stream);
+nnrt_status launch_block_sparse_vector(const float* blocks, const int32_t* coords, int64_t count, int s, int row_off, int col_off, bool ta,
+                                       const float* v, int64_t n_v, float* out, int64_t m, int* error_flag, hipStream_t stream);
+nnrt_status launch_diagonal_block_vector(const float* blocks, int64_t count, int s, const float* v, float* out, hipStream_t stream);
+nnrt_status launch_sparse_blocks_op(float* matrix, int64_t rows, int64_t cols, const float* blocks, const int32_t* coords, int64_t count, int s,
+                                    int64_t row_off, int64_t col_off, bool transpose, int op, int* error_flag, hipStream_t stream);
+nnrt_status launch_get_sparse_blocks(const float* matrix, int64_t rows, int64_t cols, int s, const int32_t* coords, int64_t count, float* blocks,
+                                     int* error_flag, hipStream_t stream);
+nnrt_status launch_transpose_blocks(float* blocks, int64_t count, int s, hipStream_t stream);
+nnrt_status launch_invert_triangular_blocks(const float* blocks, int64_t count, int s, bool upper, float* out, int* error_flag,
+                                            hipStream_t stream);
 nnrt_status solve_arrowhead(const float* diag, const float* wing, const int32_t* coords, int E, int N, int n0, const float* b, float* x,
                             int* error_flag, hipStream_t stream);
 

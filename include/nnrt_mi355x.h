@@ -286,6 +286,45 @@ nnrt_status nnrt_solve_block_diagonal_cholesky(const float* d_blocks, const floa
  * functions. NNRT_ERROR_NOT_POSITIVE_DEFINITE if a block's potrf fails (its output is NaN). */
 nnrt_status nnrt_invert_positive_semidefinite_blocks(const float* d_blocks, int32_t block_count, int32_t block_size, float* d_out,
                                                      void* stream);
+/* ---- block-sparse stages of the arrowhead solve (SolveBlockSparseArrowheadCholesky.cpp:30-95, SchurComplement.cpp:43-78),
+ * standalone; row-major [count, s, s] float blocks, int32 [count, 2] block coordinates (row, column). Coordinates outside
+ * the matrix / vector give NNRT_ERROR_ARGUMENT (the reference does not check them). ---- */
+/* MatmulBlockSparseRowWisePadded (cpp/core/linalg/MatmulBlockSparse.h; MatmulBlockSparseImpl.h:39-157): c_i = a[row_i] b_i;
+ * blocks whose row has no A block (row >= a_block_count) are zero with mask 0. MatmulBlockSparseRowWise = the mask-1 blocks
+ * and their coordinates. */
+nnrt_status nnrt_matmul_block_sparse_row_wise(const float* d_a_blocks, int32_t a_block_count, const float* d_b_blocks,
+                                              const int32_t* d_b_coordinates, int32_t b_block_count, int32_t block_size, float* d_c_blocks,
+                                              uint8_t* d_c_mask, void* stream);
+/* MatmulBlockSparse (MatmulBlockSparseImpl.h:160-439): op(A) op(B) with int16 breadboards [block rows, block columns]
+ * holding block indices (-1 = empty); op = transpose when transpose_x != 0. Output: d_c_blocks [out_rows * out_cols, s, s]
+ * in row-major block order and d_c_mask (1 = some block pair contributes); the reference returns the mask-1 blocks and
+ * their (row, column) coordinates. */
+nnrt_status nnrt_matmul_block_sparse(const float* d_a_blocks, int32_t a_block_count, const int16_t* d_a_breadboard, int32_t a_block_rows,
+                                     int32_t a_block_columns, int32_t transpose_a, const float* d_b_blocks, int32_t b_block_count,
+                                     const int16_t* d_b_breadboard, int32_t b_block_rows, int32_t b_block_columns, int32_t transpose_b,
+                                     int32_t block_size, float* d_c_blocks, uint8_t* d_c_mask, void* stream);
+/* BlockSparseAndVectorProduct (MatmulBlockSparseImpl.h:441-602): out [m] = op(A) v, A given by blocks at coordinates + the
+ * (row, column) block offset; transpose places block (i, j) at (j, i) transposed. */
+nnrt_status nnrt_block_sparse_and_vector_product(const float* d_blocks, const int32_t* d_coordinates, int32_t block_count, int32_t block_size,
+                                                 int32_t block_row_offset, int32_t block_column_offset, int32_t transpose,
+                                                 const float* d_vector, int64_t vector_length, int64_t m, float* d_out, void* stream);
+/* DiagonalBlockSparseAndVectorProduct (MatmulBlockSparseImpl.h:604-690): out_i = D_i v_i, [count * s] */
+nnrt_status nnrt_diagonal_block_sparse_and_vector_product(const float* d_blocks, int32_t block_count, int32_t block_size, const float* d_vector,
+                                                          float* d_out, void* stream);
+/* FillInSparseBlocks / AddSparseBlocks / SubtractSparseBlocks (SparseBlocksImpl.h:30-190), op 0 / 1 / 2, into a row-major
+ * [rows, columns] matrix; d_coordinates == NULL: block i at (i, i) (FillInDiagonalBlocks, DiagonalBlocksImpl.h). */
+nnrt_status nnrt_sparse_blocks_op(float* d_matrix, int64_t rows, int64_t columns, const float* d_blocks, const int32_t* d_coordinates,
+                                  int32_t block_count, int32_t block_size, int64_t block_row_offset, int64_t block_column_offset,
+                                  int32_t transpose, int32_t op, void* stream);
+/* GetSparseBlocks (SparseBlocksImpl.h:192-230); d_coordinates == NULL: GetDiagonalBlocks */
+nnrt_status nnrt_get_sparse_blocks(const float* d_matrix, int64_t rows, int64_t columns, int32_t block_size, const int32_t* d_coordinates,
+                                   int32_t block_count, float* d_blocks, void* stream);
+/* TransposeBlocksInPlace (TransposeBlocks.h) */
+nnrt_status nnrt_transpose_blocks_in_place(float* d_blocks, int32_t block_count, int32_t block_size, void* stream);
+/* InvertTriangularBlocks (InvertBlocks.cpp, trtri per block), upper != 0: UpLoTriangular::UPPER; a zero diagonal entry
+ * gives NNRT_ERROR_NOT_POSITIVE_DEFINITE (trtri info > 0). */
+nnrt_status nnrt_invert_triangular_blocks(const float* d_blocks, int32_t block_count, int32_t block_size, int32_t upper, float* d_out,
+                                          void* stream);
 /* SolveBlockSparseArrowheadCholesky (cpp/core/linalg/SolveBlockSparseArrowheadCholesky.cpp:30-95), 6x6 blocks:
  * d_diagonal_blocks [N,6,6], d_wing_blocks [E,6,6] at block coordinates d_wing_coordinates [E,2] (row < arrow_base
  * <= column for stem-to-corner blocks; row >= arrow_base for corner off-diagonal blocks), b [6N]. */

@@ -1520,3 +1520,173 @@ ORC_API int orc_fit(const OrcFitParams* prm, OrcWarpField* wf, const float* mesh
 	if (outs && outs->stage_seconds) std::memcpy(outs->stage_seconds, tacc, sizeof(tacc));
 	return 0;
 }
+
+// ---- block-sparse stages of the arrowhead solve (SolveBlockSparseArrowheadCholesky.cpp:30-95, SchurComplement.cpp:43-78).
+// Every block product entry is a float sum over the inner index in ascending order starting from 0; products of several
+// block pairs are added in ascending inner-block order (the first one taken as is). Returns 0, or 1 on a coordinate /
+// block index outside the operands (the reference reads out of bounds there).
+
+// MatmulBlockSparseImpl.h:39-157 (padded form): c_i = a[row_i] b_i, zero block + mask 0 where row_i >= a_count
+ORC_API int orc_matmul_block_sparse_row_wise(const float* a, int a_count, const float* b, const int32_t* coords, int count, int s, float* c,
+                                             uint8_t* mask) {
+	const int64_t ss = static_cast<int64_t>(s) * s;
+	int bad = 0;
+	for (int i = 0; i < count; i++) {
+		const int row = coords[2 * i];
+		bad |= row < 0;
+		const bool ok = row >= 0 && row < a_count;
+		mask[i] = ok;
+		for (int r = 0; r < s; r++)
+			for (int q = 0; q < s; q++) {
+				float acc = 0.f;
+				if (ok)
+					for (int l = 0; l < s; l++) acc += a[row * ss + r * s + l] * b[i * ss + l * s + q];
+				c[i * ss + r * s + q] = acc;
+			}
+	}
+	return bad;
+}
+
+// MatmulBlockSparseImpl.h:160-391: dense [out_rows * out_cols] output blocks + mask (the reference's meshgrid order)
+ORC_API int orc_matmul_block_sparse(const float* a, int a_count, const int16_t* a_board, int a_rows, int a_cols, int ta, const float* b,
+                                    int b_count, const int16_t* b_board, int b_rows, int b_cols, int tb, int s, float* c, uint8_t* mask) {
+	const int out_rows = ta ? a_cols : a_rows, out_cols = tb ? b_rows : b_cols, inner = ta ? a_rows : a_cols;
+	const int64_t ss = static_cast<int64_t>(s) * s;
+	int bad = 0;
+	for (int oi = 0; oi < out_rows; oi++)
+		for (int oj = 0; oj < out_cols; oj++) {
+			const int64_t ob = static_cast<int64_t>(oi) * out_cols + oj;
+			std::vector<float> acc(ss, 0.f);
+			bool any = false;
+			for (int k = 0; k < inner; k++) {
+				const int ia = ta ? a_board[k * a_cols + oi] : a_board[oi * a_cols + k];
+				if (ia == -1) continue;
+				const int ib = tb ? b_board[oj * b_cols + k] : b_board[k * b_cols + oj];
+				if (ib == -1) continue;
+				if (ia < 0 || ia >= a_count || ib < 0 || ib >= b_count) {
+					bad = 1;
+					continue;
+				}
+				for (int r = 0; r < s; r++)
+					for (int q = 0; q < s; q++) {
+						float p = 0.f;
+						for (int l = 0; l < s; l++) {
+							const float av = ta ? a[ia * ss + l * s + r] : a[ia * ss + r * s + l];
+							const float bv = tb ? b[ib * ss + q * s + l] : b[ib * ss + l * s + q];
+							p += av * bv;
+						}
+						acc[r * s + q] = any ? acc[r * s + q] + p : p;
+					}
+				any = true;
+			}
+			for (int e = 0; e < ss; e++) c[ob * ss + e] = acc[e];
+			mask[ob] = any;
+		}
+	return bad;
+}
+
+// MatmulBlockSparseImpl.h:441-582: out[m] = op(A) v; per-block products added to their rows in block order
+ORC_API int orc_block_sparse_vector(const float* blocks, const int32_t* coords, int count, int s, int row_off, int col_off, int ta,
+                                    const float* v, int64_t n_v, float* out, int64_t m) {
+	const int64_t ss = static_cast<int64_t>(s) * s;
+	for (int64_t i = 0; i < m; i++) out[i] = 0.f;
+	int bad = 0;
+	for (int i = 0; i < count; i++) {
+		const int64_t br = ta ? coords[2 * i + 1] + col_off : coords[2 * i] + row_off;
+		const int64_t bc = ta ? coords[2 * i] + row_off : coords[2 * i + 1] + col_off;
+		if (br < 0 || (br + 1) * s > m || bc < 0 || (bc + 1) * s > n_v) {
+			bad = 1;
+			continue;
+		}
+		for (int r = 0; r < s; r++) {
+			float p = 0.f;
+			for (int l = 0; l < s; l++) p += (ta ? blocks[i * ss + l * s + r] : blocks[i * ss + r * s + l]) * v[bc * s + l];
+			out[br * s + r] += p;
+		}
+	}
+	return bad;
+}
+
+// MatmulBlockSparseImpl.h:604-690
+ORC_API void orc_diagonal_block_vector(const float* blocks, int count, int s, const float* v, float* out) {
+	const int64_t ss = static_cast<int64_t>(s) * s;
+	for (int i = 0; i < count; i++)
+		for (int r = 0; r < s; r++) {
+			float p = 0.f;
+			for (int l = 0; l < s; l++) p += blocks[i * ss + r * s + l] * v[static_cast<int64_t>(i) * s + l];
+			out[static_cast<int64_t>(i) * s + r] = p;
+		}
+}
+
+// SparseBlocksImpl.h:30-190 (op 0 fill, 1 add, 2 subtract); coords == NULL: block i at (i, i) (FillInDiagonalBlocks)
+ORC_API int orc_sparse_blocks_op(float* matrix, int64_t rows, int64_t cols, const float* blocks, const int32_t* coords, int count, int s,
+                                 int64_t row_off, int64_t col_off, int transpose, int op) {
+	const int64_t ss = static_cast<int64_t>(s) * s;
+	int bad = 0;
+	for (int64_t blk = 0; blk < count; blk++) {
+		const int64_t ci = coords ? coords[2 * blk] : blk, cj = coords ? coords[2 * blk + 1] : blk;
+		const int64_t br = (transpose ? cj : ci) + row_off, bc = (transpose ? ci : cj) + col_off;
+		for (int e = 0; e < ss; e++) {
+			const int64_t i = br * s + (transpose ? e % s : e / s), j = bc * s + (transpose ? e / s : e % s);
+			if (br < 0 || bc < 0 || i >= rows || j >= cols) {
+				bad = 1;
+				continue;
+			}
+			float& d = matrix[i * cols + j];
+			const float x = blocks[blk * ss + e];
+			d = op == 0 ? x : op == 1 ? d + x : d - x;
+		}
+	}
+	return bad;
+}
+
+// SparseBlocksImpl.h:192-230; coords == NULL: GetDiagonalBlocks
+ORC_API int orc_get_sparse_blocks(const float* matrix, int64_t rows, int64_t cols, int s, const int32_t* coords, int count, float* blocks) {
+	const int64_t ss = static_cast<int64_t>(s) * s;
+	int bad = 0;
+	for (int64_t blk = 0; blk < count; blk++) {
+		const int64_t br = coords ? coords[2 * blk] : blk, bc = coords ? coords[2 * blk + 1] : blk;
+		for (int e = 0; e < ss; e++) {
+			const int64_t i = br * s + e / s, j = bc * s + e % s;
+			if (br < 0 || bc < 0 || i >= rows || j >= cols) {
+				bad = 1;
+				blocks[blk * ss + e] = NAN;
+				continue;
+			}
+			blocks[blk * ss + e] = matrix[i * cols + j];
+		}
+	}
+	return bad;
+}
+
+// InvertBlocksCPU.cpp (trtri per block): column j of the inverse by substitution; returns 1 on a zero diagonal entry
+ORC_API int orc_invert_triangular_blocks(const float* blocks, int count, int s, int upper, float* out) {
+	const int64_t ss = static_cast<int64_t>(s) * s;
+	int bad = 0;
+	for (int64_t blk = 0; blk < count; blk++) {
+		const float* A = blocks + blk * ss;
+		float* X = out + blk * ss;
+		for (int j = 0; j < s; j++) {
+			if (!upper) {
+				for (int i = 0; i < j; i++) X[i * s + j] = 0.f;
+				for (int i = j; i < s; i++) {
+					float acc = 0.f;
+					for (int k = j; k < i; k++) acc += A[i * s + k] * X[k * s + j];
+					const float d = A[i * s + i];
+					bad |= d == 0.f;
+					X[i * s + j] = i == j ? 1.f / d : -acc / d;
+				}
+			} else {
+				for (int i = j + 1; i < s; i++) X[i * s + j] = 0.f;
+				for (int i = j; i >= 0; i--) {
+					float acc = 0.f;
+					for (int k = i + 1; k <= j; k++) acc += A[i * s + k] * X[k * s + j];
+					const float d = A[i * s + i];
+					bad |= d == 0.f;
+					X[i * s + j] = i == j ? 1.f / d : -acc / d;
+				}
+			}
+		}
+	}
+	return bad;
+}

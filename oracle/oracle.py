@@ -352,6 +352,81 @@ def invert_psd_blocks(blocks):
     return out, rc
 
 
+def _i16(a):
+    return np.ascontiguousarray(a, dtype=np.int16)
+
+
+def matmul_block_sparse_row_wise(a_blocks, b_blocks, b_coordinates):
+    """MatmulBlockSparseRowWisePadded (MatmulBlockSparseImpl.h:39-157) -> (blocks [count, s, s], mask [count] bool, rc)."""
+    a, b, c = _f32(a_blocks), _f32(b_blocks), _i32(b_coordinates)
+    out = np.zeros_like(b)
+    mask = np.zeros(b.shape[0], np.uint8)
+    rc = lib().orc_matmul_block_sparse_row_wise(_p(a), ctypes.c_int(a.shape[0]), _p(b), _p(c), ctypes.c_int(b.shape[0]),
+                                                ctypes.c_int(b.shape[1]), _p(out), _p(mask))
+    return out, mask.astype(bool), rc
+
+
+def matmul_block_sparse(a_blocks, a_breadboard, transpose_a, b_blocks, b_breadboard, transpose_b):
+    """MatmulBlockSparse (MatmulBlockSparseImpl.h:160-391) -> (dense output blocks [out_rows*out_cols, s, s], mask, rc)."""
+    a, b, ab, bb = _f32(a_blocks), _f32(b_blocks), _i16(a_breadboard), _i16(b_breadboard)
+    s = a.shape[1]
+    out_rows = ab.shape[1] if transpose_a else ab.shape[0]
+    out_cols = bb.shape[0] if transpose_b else bb.shape[1]
+    out = np.zeros((out_rows * out_cols, s, s), np.float32)
+    mask = np.zeros(out_rows * out_cols, np.uint8)
+    rc = lib().orc_matmul_block_sparse(_p(a), ctypes.c_int(a.shape[0]), _p(ab), ctypes.c_int(ab.shape[0]), ctypes.c_int(ab.shape[1]),
+                                       ctypes.c_int(int(transpose_a)), _p(b), ctypes.c_int(b.shape[0]), _p(bb), ctypes.c_int(bb.shape[0]),
+                                       ctypes.c_int(bb.shape[1]), ctypes.c_int(int(transpose_b)), ctypes.c_int(s), _p(out), _p(mask))
+    return out, mask.astype(bool), rc
+
+
+def block_sparse_and_vector_product(blocks, m, coordinates, offset, transpose, vector):
+    """BlockSparseAndVectorProduct (MatmulBlockSparseImpl.h:441-602) -> (out [m], rc)."""
+    bl, c, v = _f32(blocks), _i32(coordinates), _f32(vector).reshape(-1)
+    out = np.zeros(m, np.float32)
+    rc = lib().orc_block_sparse_vector(_p(bl), _p(c), ctypes.c_int(bl.shape[0]), ctypes.c_int(bl.shape[1]), ctypes.c_int(offset[0]),
+                                       ctypes.c_int(offset[1]), ctypes.c_int(int(transpose)), _p(v), ctypes.c_int64(v.shape[0]), _p(out),
+                                       ctypes.c_int64(m))
+    return out, rc
+
+
+def diagonal_block_sparse_and_vector_product(blocks, vector):
+    """DiagonalBlockSparseAndVectorProduct (MatmulBlockSparseImpl.h:604-690)."""
+    bl, v = _f32(blocks), _f32(vector).reshape(-1)
+    out = np.zeros(bl.shape[0] * bl.shape[1], np.float32)
+    lib().orc_diagonal_block_vector(_p(bl), ctypes.c_int(bl.shape[0]), ctypes.c_int(bl.shape[1]), _p(v), _p(out))
+    return out
+
+
+def sparse_blocks_op(matrix, blocks, coordinates, offset=(0, 0), transpose=False, op=0):
+    """Fill (0) / Add (1) / SubtractSparseBlocks (2) (SparseBlocksImpl.h:30-190), in place; coordinates None = diagonal."""
+    bl = _f32(blocks)
+    c = None if coordinates is None else _i32(coordinates)
+    assert matrix.dtype == np.float32 and matrix.flags.c_contiguous
+    return lib().orc_sparse_blocks_op(_p(matrix), ctypes.c_int64(matrix.shape[0]), ctypes.c_int64(matrix.shape[1]), _p(bl), _p(c),
+                                      ctypes.c_int(bl.shape[0]), ctypes.c_int(bl.shape[1]), ctypes.c_int64(offset[0]),
+                                      ctypes.c_int64(offset[1]), ctypes.c_int(int(transpose)), ctypes.c_int(op))
+
+
+def get_sparse_blocks(matrix, block_size, coordinates=None, count=None):
+    """GetSparseBlocks / GetDiagonalBlocks (SparseBlocksImpl.h:192-230) -> (blocks, rc)."""
+    mat = _f32(matrix)
+    c = None if coordinates is None else _i32(coordinates)
+    n = c.shape[0] if c is not None else (count if count is not None else mat.shape[0] // block_size)
+    out = np.zeros((n, block_size, block_size), np.float32)
+    rc = lib().orc_get_sparse_blocks(_p(mat), ctypes.c_int64(mat.shape[0]), ctypes.c_int64(mat.shape[1]), ctypes.c_int(block_size), _p(c),
+                                     ctypes.c_int(n), _p(out))
+    return out, rc
+
+
+def invert_triangular_blocks(blocks, upper):
+    """InvertTriangularBlocks (InvertBlocksCPU.cpp, trtri per block) -> (inverses, rc: 1 on a zero diagonal)."""
+    bl = _f32(blocks)
+    out = np.zeros_like(bl)
+    rc = lib().orc_invert_triangular_blocks(_p(bl), ctypes.c_int(bl.shape[0]), ctypes.c_int(bl.shape[1]), ctypes.c_int(int(upper)), _p(out))
+    return out, rc
+
+
 def solve_block_diagonal(H, g, lm=0.0):
     H, g = _f32(H), _f32(g)
     N, s = H.shape[0], H.shape[1]

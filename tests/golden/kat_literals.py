@@ -137,3 +137,74 @@ INVERT_PSD_BLOCKS_GT = np.array([0.59375, -0.875, 0.375, -0.875, 2.5, -1.5, 0.37
                                  0.02040816,
                                  0.00966704, -0.00550583, 0.00007925, -0.00550583, 0.0118947, -0.00633981, 0.00007925, -0.00633981,
                                  0.00591716], np.float32).reshape(3, 3, 3)
+
+# ---- cpp/tests/test_linalg_matmul_block_sparse.cpp:30-220: MatmulBlockSparseRowWise / RowWisePadded (AllClose defaults) ----
+ROWWISE_A = np.arange(27, 0, -1, dtype=np.float32).reshape(3, 3, 3)
+ROWWISE_B = np.concatenate([np.arange(0, 18), np.arange(27, 108)]).astype(np.float32).reshape(11, 3, 3)
+ROWWISE_B_COORDS = np.array([[0, 0], [1, 0], [3, 0], [0, 1], [1, 1], [2, 1], [3, 1], [0, 2], [1, 2], [2, 2], [3, 2]], np.int32)
+ROWWISE_C = np.array([228, 306, 384, 201, 270, 339, 174, 234, 294,
+                      606, 657, 708, 498, 540, 582, 390, 423, 456,
+                      3036, 3114, 3192, 2685, 2754, 2823, 2334, 2394, 2454,
+                      2442, 2493, 2544, 2010, 2052, 2094, 1578, 1611, 1644,
+                      1362, 1386, 1410, 849, 864, 879, 336, 342, 348,
+                      5844, 5922, 6000, 5169, 5238, 5307, 4494, 4554, 4614,
+                      4278, 4329, 4380, 3522, 3564, 3606, 2766, 2799, 2832,
+                      2226, 2250, 2274, 1389, 1404, 1419, 552, 558, 564], np.float32).reshape(8, 3, 3)
+ROWWISE_C_COORDS = np.array([[0, 0], [1, 0], [0, 1], [1, 1], [2, 1], [0, 2], [1, 2], [2, 2]], np.int32)
+ROWWISE_PADDED_ZERO_BLOCKS = (2, 6, 10)   # the padded result is ROWWISE_C with zero blocks inserted at these indices
+
+# ---- test_linalg_matmul_block_sparse.cpp:233-386: MatmulBlockSparse with int16 breadboards (-1 = empty) ----
+MBS_A = np.array([3, 4, 5, 6, 1, 2, 3, 4, 5, 6, 7, 8], np.float32).reshape(3, 2, 2)
+MBS_A_BOARD = np.array([[0, 1, -1], [-1, -1, 2]], np.int16)
+MBS_B = np.array([1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 0], np.float32).reshape(3, 2, 2)
+MBS_B_BOARD = np.array([[0, -1], [-1, 1], [2, -1]], np.int16)
+# (lhs, transpose lhs, rhs, transpose rhs) -> (blocks, coordinates)
+MBS_CASES = {
+    "AB": (("A", 0, "B", 0), np.array([15, 22, 23, 34, 19, 22, 43, 50, 111, 50, 151, 70], np.float32).reshape(3, 2, 2),
+           np.array([[0, 0], [0, 1], [1, 0]], np.int32)),
+    "BtAt": (("B", 1, "A", 1), np.array([15, 23, 22, 34, 111, 151, 50, 70, 19, 43, 22, 50], np.float32).reshape(3, 2, 2),
+             np.array([[0, 0], [0, 1], [1, 0]], np.int32)),
+    "BtB": (("B", 1, "B", 0), np.array([212, 104, 104, 120, 74, 86, 86, 100], np.float32).reshape(2, 2, 2),
+            np.array([[0, 0], [1, 1]], np.int32)),
+    "AAt": (("A", 0, "A", 1), np.array([30, 50, 50, 86, 61, 83, 83, 113], np.float32).reshape(2, 2, 2),
+            np.array([[0, 0], [1, 1]], np.int32)),
+}
+
+# ---- test_linalg_matmul_block_sparse.cpp:398-486: BlockSparseAndVectorProduct (m = 4), NONE with A, TRANSPOSE with B ----
+BSV_A_COORDS = np.array([[0, 0], [0, 1], [1, 2]], np.int32)
+BSV_B_COORDS = np.array([[0, 0], [1, 1], [2, 0]], np.int32)
+BSV_V = np.array([-2, -1, 0, 1, 2, 3], np.float32)
+BSV_C = np.array([-8, -12, 28, 38], np.float32)
+BSV_D = np.array([46, 12, 7, 8], np.float32)
+
+# ---- test_linalg_matmul_block_sparse.cpp:499-531: DiagonalBlockSparseAndVectorProduct ----
+DBSV_D = np.array([2, -3, 2, 2, 1, 1, 4, 2, 4, 3, 6, 3], np.float32).reshape(3, 2, 2)
+DBSV_C = np.array([-1, -6, 1, 2, 17, 21], np.float32)
+
+# ---- cpp/tests/test_linalg_block_routines.cpp:32-154: InvertTriangularBlocks (AllClose rtol 1e-4), TransposeBlocksInPlace ----
+TRI_LOWER = np.array([1, 0, 0, 2, 3, 0, 4, 5, 6, 7, 0, 0, 8, 9, 0, 10, 11, 12, 13, 0, 0, 14, 15, 0, 16, 17, 18], np.float32).reshape(3, 3, 3)
+TRI_LOWER_INV = np.array([1., -0., 0., -0.6666667, 0.33333334, -0., -0.11111111, -0.2777778, 0.16666667,
+                          0.14285715, 0., -0., -0.12698413, 0.11111111, 0., -0.0026455, -0.10185185, 0.08333334,
+                          0.07692308, 0., 0., -0.07179487, 0.06666667, 0., -0.0005698, -0.06296296, 0.05555556], np.float32).reshape(3, 3, 3)
+TRI_UPPER = np.array([4, 5, 6, 0, 2, 3, 0, 0, 1, 10, 11, 12, 0, 8, 9, 0, 0, 7, 16, 17, 18, 0, 14, 15, 0, 0, 13], np.float32).reshape(3, 3, 3)
+TRI_UPPER_INV = np.array([0.25, -0.625, 0.375, 0., 0.5, -1.5, 0., 0., 1.,
+                          0.1, -0.1375, 0.00535714, 0., 0.125, -0.16071428, 0., 0., 0.14285715,
+                          0.0625, -0.07589286, 0.00103022, 0., 0.07142857, -0.08241758, 0., 0., 0.07692308], np.float32).reshape(3, 3, 3)
+TRANSPOSED_TRI_LOWER = np.array([1, 2, 4, 0, 3, 5, 0, 0, 6, 7, 8, 10, 0, 9, 11, 0, 0, 12, 13, 14, 16, 0, 15, 17, 0, 0, 18],
+                                np.float32).reshape(3, 3, 3)
+
+# ---- test_linalg_block_routines.cpp:207-400: Fill / Get diagonal and sparse blocks, 12 x 12 matrix, 2 x 2 blocks ----
+ARANGE_BLOCKS = np.arange(24, dtype=np.float32).reshape(6, 2, 2)
+SPARSE_COORDS = np.array([[0, 0], [0, 1], [2, 0], [3, 3], [2, 4], [5, 5]], np.int32)
+SPARSE_FILLED = np.zeros((12, 12), np.float32)
+SPARSE_FILLED[0:2, 0:4] = [[0, 1, 4, 5], [2, 3, 6, 7]]
+SPARSE_FILLED[4:6, 0:2] = [[8, 9], [10, 11]]
+SPARSE_FILLED[4:6, 8:10] = [[16, 17], [18, 19]]
+SPARSE_FILLED[6:8, 6:8] = [[12, 13], [14, 15]]
+SPARSE_FILLED[10:12, 10:12] = [[20, 21], [22, 23]]
+TRANSPOSE_FILL_BLOCKS = np.array([4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19], np.float32).reshape(3, 2, 2)
+TRANSPOSE_FILL_COORDS = np.array([[0, 1], [2, 0], [2, 4]], np.int32)
+SPARSE_FILLED_2 = SPARSE_FILLED.copy()
+SPARSE_FILLED_2[0:2, 4:6] = [[8, 10], [9, 11]]
+SPARSE_FILLED_2[2:4, 0:2] = [[4, 6], [5, 7]]
+SPARSE_FILLED_2[8:10, 4:6] = [[16, 18], [17, 19]]

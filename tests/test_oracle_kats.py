@@ -312,3 +312,114 @@ def test_invert_psd_blocks_kat(oracle_mod):
     bad = spd.copy()
     bad[2] = -bad[2]
     assert oracle_mod.invert_psd_blocks(bad)[1] == 3
+
+
+# ---- block-sparse stages of the arrowhead solve: cpp/tests/test_linalg_matmul_block_sparse.cpp,
+# cpp/tests/test_linalg_block_routines.cpp (AllClose defaults rtol 1e-5 / atol 1e-8 unless the test states otherwise) ----
+
+def _padded_rowwise_gt():
+    blocks = list(L.ROWWISE_C)
+    for i in L.ROWWISE_PADDED_ZERO_BLOCKS:
+        blocks.insert(i, np.zeros((3, 3), np.float32))
+    return np.stack(blocks)
+
+
+def test_matmul_block_sparse_row_wise_kat(oracle_mod):
+    # test_linalg_matmul_block_sparse.cpp:30-220
+    c, mask, rc = oracle_mod.matmul_block_sparse_row_wise(L.ROWWISE_A, L.ROWWISE_B, L.ROWWISE_B_COORDS)
+    assert rc == 0
+    assert np.allclose(c, _padded_rowwise_gt(), rtol=1e-5, atol=1e-8)
+    assert np.allclose(c[mask], L.ROWWISE_C, rtol=1e-5, atol=1e-8)
+    assert np.array_equal(L.ROWWISE_B_COORDS[mask], L.ROWWISE_C_COORDS)
+
+
+@pytest.mark.parametrize("case", sorted(L.MBS_CASES))
+def test_matmul_block_sparse_kat(oracle_mod, case):
+    # test_linalg_matmul_block_sparse.cpp:233-386
+    (lhs, tl, rhs, tr), gt_blocks, gt_coords = L.MBS_CASES[case]
+    ops = {"A": (L.MBS_A, L.MBS_A_BOARD), "B": (L.MBS_B, L.MBS_B_BOARD)}
+    c, mask, rc = oracle_mod.matmul_block_sparse(*ops[lhs], tl, *ops[rhs], tr)
+    assert rc == 0
+    out_cols = (ops[rhs][1].shape[0] if tr else ops[rhs][1].shape[1])
+    coords = np.stack(np.nonzero(mask.reshape(-1, out_cols)), axis=1)
+    assert np.allclose(c[mask], gt_blocks, rtol=1e-5, atol=1e-8)
+    assert np.array_equal(coords, gt_coords)
+
+
+def test_block_sparse_and_vector_product_kat(oracle_mod):
+    # test_linalg_matmul_block_sparse.cpp:398-486
+    c, rc = oracle_mod.block_sparse_and_vector_product(L.MBS_A, 4, L.BSV_A_COORDS, (0, 0), False, L.BSV_V)
+    assert rc == 0 and np.allclose(c, L.BSV_C, rtol=1e-5, atol=1e-8)
+    d, rc = oracle_mod.block_sparse_and_vector_product(L.MBS_B, 4, L.BSV_B_COORDS, (0, 0), True, L.BSV_V)
+    assert rc == 0 and np.allclose(d, L.BSV_D, rtol=1e-5, atol=1e-8)
+    # a block beyond m is reported, not written
+    assert oracle_mod.block_sparse_and_vector_product(L.MBS_A, 2, L.BSV_A_COORDS, (0, 0), False, L.BSV_V)[1] == 1
+
+
+def test_diagonal_block_sparse_and_vector_product_kat(oracle_mod):
+    # test_linalg_matmul_block_sparse.cpp:499-531
+    assert np.allclose(oracle_mod.diagonal_block_sparse_and_vector_product(L.DBSV_D, L.BSV_V), L.DBSV_C, rtol=1e-5, atol=1e-8)
+
+
+@pytest.mark.parametrize("upper", [False, True])
+def test_invert_triangular_blocks_kat(oracle_mod, upper):
+    # test_linalg_block_routines.cpp:32-110 (AllClose rtol 1e-4)
+    inv, rc = oracle_mod.invert_triangular_blocks(L.TRI_UPPER if upper else L.TRI_LOWER, upper)
+    assert rc == 0
+    assert np.allclose(inv, L.TRI_UPPER_INV if upper else L.TRI_LOWER_INV, rtol=1e-4, atol=1e-8)
+    singular = L.TRI_LOWER.copy()
+    singular[1, 2, 2] = 0
+    assert oracle_mod.invert_triangular_blocks(singular, False)[1] == 1
+
+
+def test_fill_and_get_blocks_kat(oracle_mod):
+    # test_linalg_block_routines.cpp:207-400
+    diag_gt = np.zeros((12, 12), np.float32)
+    for i in range(6):
+        diag_gt[2 * i:2 * i + 2, 2 * i:2 * i + 2] = L.ARANGE_BLOCKS[i]
+    m = np.zeros((12, 12), np.float32)
+    assert oracle_mod.sparse_blocks_op(m, L.ARANGE_BLOCKS, None) == 0
+    assert np.array_equal(m, diag_gt)
+    assert np.array_equal(oracle_mod.get_sparse_blocks(diag_gt, 2)[0], L.ARANGE_BLOCKS)
+    m = np.zeros((12, 12), np.float32)
+    assert oracle_mod.sparse_blocks_op(m, L.ARANGE_BLOCKS, L.SPARSE_COORDS) == 0
+    assert np.array_equal(m, L.SPARSE_FILLED)
+    assert oracle_mod.sparse_blocks_op(m, L.TRANSPOSE_FILL_BLOCKS, L.TRANSPOSE_FILL_COORDS, transpose=True) == 0
+    assert np.array_equal(m, L.SPARSE_FILLED_2)
+    assert np.array_equal(oracle_mod.get_sparse_blocks(L.SPARSE_FILLED, 2, L.SPARSE_COORDS)[0], L.ARANGE_BLOCKS)
+    # subtract undoes add; a block past the matrix edge is reported
+    m2 = L.SPARSE_FILLED.copy()
+    oracle_mod.sparse_blocks_op(m2, L.ARANGE_BLOCKS, L.SPARSE_COORDS, op=1)
+    oracle_mod.sparse_blocks_op(m2, L.ARANGE_BLOCKS, L.SPARSE_COORDS, op=2)
+    assert np.array_equal(m2, L.SPARSE_FILLED)
+    assert oracle_mod.sparse_blocks_op(np.zeros((12, 12), np.float32), L.ARANGE_BLOCKS, L.SPARSE_COORDS, offset=(1, 0)) == 1
+
+
+def test_block_sparse_pieces_compose_the_stem_schur_complement(oracle_mod):
+    """SchurComplement.cpp:43-78 composed from the restated pieces equals the dense S = C - W^T D^-1 W (float64 check)."""
+    rng = np.random.default_rng(11)
+    n0, n1, s = 5, 3, 6
+    a = rng.normal(size=(n0, s, s))
+    D = (a @ a.transpose(0, 2, 1) + 6 * np.eye(s)).astype(np.float32)
+    wing_coords = np.array([[0, 0], [1, 0], [1, 2], [3, 1], [4, 2], [2, 1]], np.int32)
+    W = rng.normal(size=(len(wing_coords), s, s)).astype(np.float32)
+    C = np.eye(n1 * s, dtype=np.float32) * 50
+    Dinv, rc = oracle_mod.invert_psd_blocks(D)
+    assert rc == 0
+    DinvW, mask, rc = oracle_mod.matmul_block_sparse_row_wise(Dinv, W, wing_coords)     # SolveBlockSparseArrowheadCholesky.cpp:54
+    assert rc == 0 and mask.all()
+    board = np.full((n0, n1), -1, np.int16)
+    board[wing_coords[:, 0], wing_coords[:, 1]] = np.arange(len(wing_coords))
+    prod, pmask, rc = oracle_mod.matmul_block_sparse(W, board, 1, DinvW, board, 0)        # SchurComplement.cpp:71-73
+    assert rc == 0
+    S = C.copy()
+    coords = np.stack(np.nonzero(pmask.reshape(n1, n1)), axis=1).astype(np.int32)
+    oracle_mod.sparse_blocks_op(S, prod[pmask], coords, op=2)                              # SchurComplement.cpp:75
+    Wd = np.zeros((n0 * s, n1 * s))
+    for (i, j), blk in zip(wing_coords, W):
+        Wd[i * s:(i + 1) * s, j * s:(j + 1) * s] = blk
+    Dd = np.zeros((n0 * s, n0 * s))
+    for i in range(n0):
+        Dd[i * s:(i + 1) * s, i * s:(i + 1) * s] = D[i]
+    S_ref = C.astype(np.float64) - Wd.T @ np.linalg.solve(Dd, Wd)
+    assert np.abs(S - S_ref).max() < 1e-3 * np.abs(S_ref).max()
