@@ -154,3 +154,22 @@ def test_stem_schur_pieces_bit_exact_vs_oracle(la, oracle_mod):
     assert np.abs(wx - wx_o).max() <= 1e-5 * np.abs(wx_o).max()
     xs = _np(la.DiagonalBlockSparseAndVectorProduct(Dinv, b_stem - wx))
     assert np.array_equal(xs, oracle_mod.diagonal_block_sparse_and_vector_product(Dinv_o, b_stem - wx))
+
+
+def test_empty_operands(la):
+    """Zero blocks everywhere: empty results of the right shape, no launch, no error (the reference's ParallelFor over 0)."""
+    e3 = np.zeros((0, 3, 3), np.float32)
+    c0 = np.zeros((0, 2), np.int32)
+    assert la.MatmulBlockSparseRowWisePadded(L.ROWWISE_A, e3, c0).shape == (0, 3, 3)
+    blocks, coords = la.MatmulBlockSparseRowWise(L.ROWWISE_A, e3, c0)
+    assert blocks.shape == (0, 3, 3) and coords.shape == (0, 2)
+    blocks, coords = la.MatmulBlockSparse(L.MBS_A, np.full((2, 3), -1, np.int16), 0, L.MBS_B, np.full((3, 2), -1, np.int16), 0)
+    assert blocks.shape == (0, 2, 2) and coords.shape == (0, 2)
+    out = la.BlockSparseAndVectorProduct(np.zeros((0, 2, 2), np.float32), 4, c0, (0, 0), 0, L.BSV_V)
+    assert np.array_equal(_np(out), np.zeros(4, np.float32))
+    assert la.DiagonalBlockSparseAndVectorProduct(np.zeros((0, 2, 2), np.float32), np.zeros(0, np.float32)).shape == (0,)
+    assert la.InvertTriangularBlocks(e3, la.UpLoTriangular.LOWER).shape == (0, 3, 3)
+    m = torch.zeros((4, 4), dtype=torch.float32, device=DEV)
+    la.FillInSparseBlocks(m, np.zeros((0, 2, 2), np.float32), c0)
+    assert not m.any()
+    assert la.GetSparseBlocks(_np(m), 2, c0).shape == (0, 2, 2)
