@@ -1406,6 +1406,7 @@ nnrt_status nnrt_matmul_block_sparse_row_wise(const float* d_a_blocks, int32_t a
                                               uint8_t* d_c_mask, void* stream) {
 	NNRT_CHECK_ARG(a_block_count >= 0 && b_block_count >= 0 && block_size > 0, "bad block count or block size");
 	NNRT_CHECK_ARG(b_block_count == 0 || (d_b_blocks && d_b_coordinates && d_c_blocks && d_c_mask), "null pointer");
+	NNRT_CHECK_ARG(a_block_count == 0 || d_a_blocks, "null pointer");
 	hipStream_t s = static_cast<hipStream_t>(stream);
 	return with_device_flag(s, NNRT_ERROR_ARGUMENT, "negative block row coordinate in MatmulBlockSparseRowWise", [&](int* flag) {
 		return launch_matmul_block_sparse_row_wise(d_a_blocks, a_block_count, d_b_blocks, d_b_coordinates, b_block_count, block_size, d_c_blocks,
@@ -1421,6 +1422,9 @@ nnrt_status nnrt_matmul_block_sparse(const float* d_a_blocks, int32_t a_block_co
 	NNRT_CHECK_ARG(a_block_rows >= 0 && a_block_columns >= 0 && b_block_rows >= 0 && b_block_columns >= 0, "negative breadboard size");
 	const int32_t a_inner = transpose_a ? a_block_rows : a_block_columns, b_inner = transpose_b ? b_block_columns : b_block_rows;
 	NNRT_CHECK_ARG(a_inner == b_inner, "Matrix inner dimensions must but do not match.");
+	const int64_t out_blocks = static_cast<int64_t>(transpose_a ? a_block_columns : a_block_rows) * (transpose_b ? b_block_rows : b_block_columns);
+	NNRT_CHECK_ARG(out_blocks == 0 || (d_c_blocks && d_c_mask && d_a_breadboard && d_b_breadboard), "null pointer");
+	NNRT_CHECK_ARG((a_block_count == 0 || d_a_blocks) && (b_block_count == 0 || d_b_blocks), "null pointer");
 	hipStream_t s = static_cast<hipStream_t>(stream);
 	return with_device_flag(s, NNRT_ERROR_ARGUMENT, "breadboard block index out of range in MatmulBlockSparse", [&](int* flag) {
 		return launch_matmul_block_sparse(d_a_blocks, a_block_count, d_a_breadboard, a_block_rows, a_block_columns, transpose_a != 0, d_b_blocks,
@@ -1434,6 +1438,7 @@ nnrt_status nnrt_block_sparse_and_vector_product(const float* d_blocks, const in
                                                  const float* d_vector, int64_t vector_length, int64_t m, float* d_out, void* stream) {
 	NNRT_CHECK_ARG(block_count >= 0 && block_size > 0 && vector_length >= 0 && m >= 0, "bad size");
 	NNRT_CHECK_ARG(m % block_size == 0, "output length m must be a multiple of the block size");
+	NNRT_CHECK_ARG((m == 0 || d_out) && (block_count == 0 || (d_blocks && d_coordinates && d_vector)), "null pointer");
 	hipStream_t s = static_cast<hipStream_t>(stream);
 	return with_device_flag(s, NNRT_ERROR_ARGUMENT, "block coordinate outside the matrix in BlockSparseAndVectorProduct", [&](int* flag) {
 		return launch_block_sparse_vector(d_blocks, d_coordinates, block_count, block_size, block_row_offset, block_column_offset, transpose != 0,
@@ -1444,6 +1449,7 @@ nnrt_status nnrt_block_sparse_and_vector_product(const float* d_blocks, const in
 nnrt_status nnrt_diagonal_block_sparse_and_vector_product(const float* d_blocks, int32_t block_count, int32_t block_size, const float* d_vector,
                                                           float* d_out, void* stream) {
 	NNRT_CHECK_ARG(block_count >= 0 && block_size > 0, "bad block count or block size");
+	NNRT_CHECK_ARG(block_count == 0 || (d_blocks && d_vector && d_out), "null pointer");
 	return launch_diagonal_block_vector(d_blocks, block_count, block_size, d_vector, d_out, static_cast<hipStream_t>(stream));
 }
 
@@ -1452,6 +1458,7 @@ nnrt_status nnrt_sparse_blocks_op(float* d_matrix, int64_t rows, int64_t columns
                                   int32_t transpose, int32_t op, void* stream) {
 	NNRT_CHECK_ARG(rows >= 0 && columns >= 0 && block_count >= 0 && block_size > 0, "bad size");
 	NNRT_CHECK_ARG(op >= 0 && op <= 2, "op must be 0 (fill), 1 (add) or 2 (subtract)");
+	NNRT_CHECK_ARG(block_count == 0 || (d_matrix && d_blocks), "null pointer");
 	hipStream_t s = static_cast<hipStream_t>(stream);
 	return with_device_flag(s, NNRT_ERROR_ARGUMENT, "block placed outside the matrix", [&](int* flag) {
 		return launch_sparse_blocks_op(d_matrix, rows, columns, d_blocks, d_coordinates, block_count, block_size, block_row_offset,
@@ -1462,6 +1469,7 @@ nnrt_status nnrt_sparse_blocks_op(float* d_matrix, int64_t rows, int64_t columns
 nnrt_status nnrt_get_sparse_blocks(const float* d_matrix, int64_t rows, int64_t columns, int32_t block_size, const int32_t* d_coordinates,
                                    int32_t block_count, float* d_blocks, void* stream) {
 	NNRT_CHECK_ARG(rows >= 0 && columns >= 0 && block_count >= 0 && block_size > 0, "bad size");
+	NNRT_CHECK_ARG(block_count == 0 || (d_matrix && d_blocks), "null pointer");
 	hipStream_t s = static_cast<hipStream_t>(stream);
 	return with_device_flag(s, NNRT_ERROR_ARGUMENT, "block coordinate outside the matrix", [&](int* flag) {
 		return launch_get_sparse_blocks(d_matrix, rows, columns, block_size, d_coordinates, block_count, d_blocks, flag, s);
@@ -1470,12 +1478,14 @@ nnrt_status nnrt_get_sparse_blocks(const float* d_matrix, int64_t rows, int64_t 
 
 nnrt_status nnrt_transpose_blocks_in_place(float* d_blocks, int32_t block_count, int32_t block_size, void* stream) {
 	NNRT_CHECK_ARG(block_count >= 0 && block_size > 0, "bad block count or block size");
+	NNRT_CHECK_ARG(block_count == 0 || d_blocks, "null pointer");
 	return launch_transpose_blocks(d_blocks, block_count, block_size, static_cast<hipStream_t>(stream));
 }
 
 nnrt_status nnrt_invert_triangular_blocks(const float* d_blocks, int32_t block_count, int32_t block_size, int32_t upper, float* d_out,
                                           void* stream) {
 	NNRT_CHECK_ARG(block_count >= 0 && block_size > 0, "bad block count or block size");
+	NNRT_CHECK_ARG(block_count == 0 || (d_blocks && d_out), "null pointer");
 	hipStream_t s = static_cast<hipStream_t>(stream);
 	return with_device_flag(s, NNRT_ERROR_NOT_POSITIVE_DEFINITE, "trtri failed in InvertTriangularBlocks (zero on a block diagonal)",
 	                        [&](int* flag) { return launch_invert_triangular_blocks(d_blocks, block_count, block_size, upper != 0, d_out, flag, s); });

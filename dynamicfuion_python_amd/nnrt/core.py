@@ -199,8 +199,12 @@ def _fill_in_diagonal_blocks(matrix, blocks):
 def _get_sparse_blocks(matrix, block_size, coordinates=None):
     dev = _dev()
     mat = to_device(matrix, torch.float32, dev).contiguous()
-    c = None if coordinates is None else to_device(coordinates, torch.int32, dev).contiguous()
-    n = c.shape[0] if c is not None else mat.shape[0] // int(block_size)
+    if coordinates is None:
+        c, n = None, mat.shape[0] // int(block_size)
+    else:
+        c = to_device(coordinates, torch.int32, dev).contiguous()
+        n = c.shape[0]
+        c = _coords(c, dev, n)
     out = torch.empty((n, int(block_size), int(block_size)), dtype=torch.float32, device=dev)
     N.check(N.lib().nnrt_get_sparse_blocks(N.ptr(mat), mat.shape[0], mat.shape[1], int(block_size), None if c is None else N.ptr(c), n,
                                             N.ptr(out), N.stream_ptr()))
