@@ -19,7 +19,7 @@ N > 1: one process per GPU (torchrun), each fitting its own independent sequence
 collective in the data path; the only collectives are the barrier, the max-over-ranks of the elapsed time and the
 end-of-run all-gather of per-rank results.
 
-Also reported: the dominant kernel's roofline (k_node_reduce_grouped, HIP-event timed on the fitter's work stream; every
+Also reported: the dominant kernel's roofline (k_fit_pixels_fused: both pixel passes in one launch, HIP-event timed on the fitter's work stream; every
 other kernel of the iteration under "kernels"), the once-per-frame setup time, and the CPU baseline (the oracle/ C++
 restatement, OpenMP, on a bounded sample of the same workload, rank 0, N = 1; also at 1 thread).
 """
@@ -37,7 +37,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM": 8 TB/s spec)
 MFMA_F32_PEAK_TFS = 157.3   # dense f32-input MFMA peak (MI355X_MICROARCH.md MFMA table, "F32 (f32 in)")
 DEFAULT_CONFIG = "C2"
-ROOFLINE_KERNEL = "k_node_reduce_grouped"
+ROOFLINE_KERNEL = "k_fit_pixels_fused"
 
 
 # ---------------------------------------------------------------------------------------------------------------------
@@ -115,13 +115,12 @@ def stage_bytes(P: int, F: int, V: int, N: int, K: int, E: int) -> dict:
 KERNEL_STAGES = {
     "k_warp_mesh_quad": ("warp", "warped_jacobians"),
     "k_raster_scatter_mesh": ("ndc", "raster"),
-    "k_pixel_jacobians": ("residual", "rasterized_jacobians"),
-    "k_node_reduce_grouped": ("pixel_anchor_jacobians", "jtj_jtr"),
+    "k_fit_pixels_fused": ("residual", "rasterized_jacobians", "pixel_anchor_jacobians", "jtj_jtr"),
     "k_solve_update": ("solve",),
 }
 # nnrt_fitter_iterate_timed stage -> the kernel it times
-STAGE_KERNEL = {"warp": "k_warp_mesh_quad", "raster": "k_raster_scatter_mesh", "pixel_jacobians": "k_pixel_jacobians",
-                "node_reduce": "k_node_reduce_grouped", "solve": "k_solve_update"}
+# (the pixel-pass stage reads 0: both pixel passes run in the one launch the node-pass stage times)
+STAGE_KERNEL = {"warp": "k_warp_mesh_quad", "raster": "k_raster_scatter_mesh", "node_reduce": "k_fit_pixels_fused", "solve": "k_solve_update"}
 
 
 def arap_stage_bytes(N: int, n0: int, Ee: int) -> dict:
@@ -141,10 +140,12 @@ def kernel_bytes(kernel: str, sb: dict) -> int:
 
 
 def node_pass_compulsory_bytes(P: int, P_c: int, F: int, V: int, N: int, K: int) -> int:
-    """What k_node_reduce_grouped itself must move: per pixel the pass-1 key (8 B read + 8 B reset); per
-    contributing pixel its 64-B Jacobian record; each face record once (int4); per vertex its anchors (4 B x K) and
-    warped-Jacobian rows (2 x float4 x K); per node the fp64 accumulator row (27 x 8 B read-modify-write)."""
-    return P * 16 + P_c * 64 + F * 16 + V * K * (4 + 32) + N * 27 * 8 * 2
+    """What k_fit_pixels_fused itself must move: per pixel the raster key (8 B read + 8 B reset), the reference
+    point (16 B) and the residual / mask / face outputs (9 B); per contributing pixel its 64-B Jacobian record (written
+    and re-read by the same wave); each face record once (int4) and its vertices' warped position and normal (2 x
+    float4); per vertex its anchors (4 B x K) and warped-Jacobian rows (2 x float4 x K); per node the fp64 accumulator
+    row (27 x 8 B read-modify-write)."""
+    return P * (16 + 16 + 9) + P_c * 64 * 2 + F * 16 + V * 32 + V * K * (4 + 32) + N * 27 * 8 * 2
 
 
 def count_associations(pixel_faces, residual_mask, faces, anchors) -> int:
@@ -461,7 +462,7 @@ def main(argv=None):
         "stage_ms": {k: round(v, 5) for k, v in stages.items()},
         "roofline": {"kernel": ROOFLINE_KERNEL, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "algorithmic_bytes": kbytes, "kernel_ms": k_ms,
-                     "bytes_formula": "SURVEY.md 8(d): pixel-anchor Jacobians + JtJ/Jtr rows (P*257 + P*72K + 4E + E*28 + P*5 + 168N)",
+                     "bytes_formula": "SURVEY.md 8(d): residuals + rasterized Jacobians + pixel-anchor Jacobians + JtJ/Jtr rows (P*58 + F*36 + P*244 + F*72 + P*257 + P*72K + 4E + E*28 + P*5 + 168N)",
                      "associations_E": E, "contributing_pixels": P_c,
                      "associations_note": "E and contributing pixels averaged over the timed iterations", "traffic_source": traffic_src,
                      "compulsory_bytes": node_pass_compulsory_bytes(P, P_c, F, V, Nn, 4),

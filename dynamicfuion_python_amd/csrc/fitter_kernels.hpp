@@ -58,7 +58,7 @@ constexpr int FACE_NODE_MAX_NODES = (1 << 20) - 1;
 inline int face_node_slots(int K) { return K <= 4 ? 12 : 3 * MAX_ANCHORS; }
 nnrt_status launch_face_node_table(const int4* faces4, int64_t F, const int32_t* anchors, int K, uint32_t* out, hipStream_t stream);
 
-// pass 1 (k_pixel_jacobians) then pass 2 (k_node_reduce_grouped); `between` (optional) is recorded between them
+// pass 1 then pass 2 in one launch (k_fit_pixels_fused); `between` (optional, stage timing) is recorded before it
 nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t stream, hipEvent_t between = nullptr);
 nnrt_status launch_solve_update(int mode, const SolveArgs& args, hipStream_t stream, bool from_identity = false);
 

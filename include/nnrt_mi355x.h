@@ -159,8 +159,8 @@ nnrt_status nnrt_fitter_fit_from_snapshot(nnrt_fitter* fitter, nnrt_warp_field* 
 nnrt_status nnrt_fitter_restore_motion(nnrt_fitter* fitter, nnrt_warp_field* warp_field, void* stream);
 /* iterate() without graphs, with HIP events between the stages of every iteration; h_stage_ms[NNRT_TIMED_STAGES]
  * receives the average per-iteration device time of: 0 warp (+warped Jacobians), 1 raster scatter, 2 pixel pass
- * (residuals + rasterized Jacobians, k_pixel_jacobians), 3 node pass (node Jacobians + JtJ / Jt r,
- * k_node_reduce_grouped), 4 ARAP edges, 5 linear solve + update ("ms/solve"). Synchronizes `stream`. */
+ * (0: fused into 3), 3 pixel + node pass (residuals, rasterized Jacobians, node Jacobians, JtJ / Jt r: one launch,
+ * k_fit_pixels_fused), 4 ARAP edges, 5 linear solve + update ("ms/solve"). Synchronizes `stream`. */
 #define NNRT_TIMED_STAGES 6
 nnrt_status nnrt_fitter_iterate_timed(nnrt_fitter* fitter, nnrt_warp_field* warp_field, int32_t first_iteration, int32_t count,
                                       float* h_stage_ms, void* stream);

@@ -13,7 +13,7 @@ import csv, glob, sys
 f = glob.glob(f"gpurun_out/vp/{sys.argv[1]}/**/run_kernel_stats.csv", recursive=True)[0]
 out = []
 for r in csv.DictReader(open(f)):
-    if any(k in r["Name"] for k in ("raster_scatter_mesh", "pixel_jac", "node_reduce", "warp_mesh", "solve_update", "chol", "arap")) and int(r["Calls"]) > 50:
+    if any(k in r["Name"] for k in ("raster_scatter_mesh", "pixel_jac", "node_reduce", "fit_pixels_fused", "warp_mesh", "solve_update", "chol", "arap")) and int(r["Calls"]) > 50:
         out.append(f'{r["Name"].split("(")[0].replace("void nnrt::","").replace("nnrt::","")[:34]} {float(r["AverageNs"])/1000:.2f}')
 print(f"{sys.argv[1]:16s}", " | ".join(out))
 PY

@@ -7,7 +7,7 @@ import sys
 d = collections.defaultdict(lambda: collections.defaultdict(list))
 for r in csv.DictReader(open(sys.argv[1])):
     d[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
-keys = sys.argv[2:] or ["k_node_reduce", "k_pixel_jacobians", "k_raster_scatter_mesh"]
+keys = sys.argv[2:] or ["k_fit_pixels_fused", "k_raster_scatter_mesh"]
 for k, v in d.items():
     if any(x in k for x in keys):
         m = {c: sum(x) / len(x) for c, x in v.items()}
