@@ -460,6 +460,8 @@ def main(argv=None):
                    "parallelism": f"replicas{world}" if world > 1 else "single"},
         "setup_ms": round(setup_ms, 3),
         "stage_ms": {k: round(v, 5) for k, v in stages.items()},
+        "stage_note": "eager launches between HIP events; pixel_jacobians is back-to-back event overhead only: both pixel "
+                      "passes run in the one launch node_reduce times (k_fit_pixels_fused)",
         "roofline": {"kernel": ROOFLINE_KERNEL, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "algorithmic_bytes": kbytes, "kernel_ms": k_ms,
                      "bytes_formula": "SURVEY.md 8(d): residuals + rasterized Jacobians + pixel-anchor Jacobians + JtJ/Jtr rows (P*58 + F*36 + P*244 + F*72 + P*257 + P*72K + 4E + E*28 + P*5 + 168N)",
