@@ -165,19 +165,29 @@ __global__ __launch_bounds__(256) void k_arrow_prepare(int N, float lm, double* 
 }
 
 // ---- corner init: S = C (diagonal corner blocks + corner off-diagonal blocks), identity on the padding; cb = b_C ----
+// One thread per 4 consecutive entries of a row (one 16-B store; 32-bit index arithmetic: ld <= 32768). Strictly-upper
+// 64 x 64 tiles are left unwritten: the factorization and both substitutions touch tiles I >= J only (k_chol_step,
+// k_chol_back_group), so half the corner's bytes need no initialisation.
 __global__ void k_arrow_corner_init(int n0, int m, int ld, const float* __restrict__ diag, float* __restrict__ S, const float* __restrict__ rhs,
                                     float* __restrict__ cb) {
-	const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-	if (idx >= static_cast<int64_t>(ld) * ld) return;
-	const int r = static_cast<int>(idx / ld), c = static_cast<int>(idx % ld);
-	float v = 0.f;
-	if (r < m && c < m) {
-		if (r / 6 == c / 6) v = diag[static_cast<int64_t>(n0 + r / 6) * 36 + 6 * (r % 6) + (c % 6)];
-	} else if (r == c) {
-		v = 1.f;
+	const int q = ld >> 2;
+	const int idx = static_cast<int>(blockIdx.x) * static_cast<int>(blockDim.x) + static_cast<int>(threadIdx.x);
+	if (idx >= ld * q) return;
+	const int r = idx / q, c0 = (idx - r * q) * 4;
+	if (c0 == 0) cb[r] = r < m ? rhs[6 * static_cast<int64_t>(n0) + r] : 0.f;
+	if ((c0 / CORNER_NB) > (r / CORNER_NB)) return;
+	float v[4];
+#pragma unroll
+	for (int j = 0; j < 4; j++) {
+		const int c = c0 + j;
+		v[j] = 0.f;
+		if (r < m && c < m) {
+			if (r / 6 == c / 6) v[j] = diag[static_cast<int64_t>(n0 + r / 6) * 36 + 6 * (r % 6) + (c % 6)];
+		} else if (r == c) {
+			v[j] = 1.f;
+		}
 	}
-	S[idx] = v;
-	if (c == 0) cb[r] = r < m ? rhs[6 * static_cast<int64_t>(n0) + r] : 0.f;
+	*reinterpret_cast<float4*>(S + static_cast<int64_t>(r) * ld + c0) = make_float4(v[0], v[1], v[2], v[3]);
 }
 
 __global__ void k_arrow_corner_offdiag(int E, int n0, int ld, const int32_t* __restrict__ edges, const float* __restrict__ wing,
@@ -870,8 +880,9 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
                                  bool arap_wings) {
 	const int m = ws.m, ld = ws.ld;
 	if (m > 0) {
-		k_arrow_corner_init<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ld) * ld, 256)), 256, 0, stream>>>(ws.n0, m, ld, ws.diag,
-		                                                                                                               ws.schur, ws.rhs, ws.cb);
+		NNRT_CHECK_ARG(ld <= 32768, "arrowhead corner larger than 32768 unknowns");
+		k_arrow_corner_init<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ld) * (ld / 4), 256)), 256, 0, stream>>>(ws.n0, m, ld, ws.diag,
+		                                                                                                                    ws.schur, ws.rhs, ws.cb);
 		NNRT_LAUNCH_CHECK();
 		if (ws.E > 0) {
 			k_arrow_corner_offdiag<<<ws.E, 64, 0, stream>>>(ws.E, ws.n0, ld, edges, wing, ws.schur);
