@@ -39,10 +39,11 @@ struct ModeTraits<NNRT_ITERATION_ROTATION_ONLY> {
 // ---- pass 1: per pixel (S3b-S9) -----------------------------------------------------------------------------------
 // Resolves the raster winner, writes the residual / mask / face outputs and, for pixels that contribute to the data
 // term, the compact per-pixel Jacobian record [dr/dV (9), dr/dn_l (3), rho (3), r] (4 x float4). The raster key is
-// replaced by the contributing face (or EMPTY) for pass 2, which resets it.
+// reset to EMPTY for the next iteration's scatter; the contributing face goes to pass 2 in registers.
 // dn: this lane's 27 parked floats at dn[i * dn_stride] (lane-private LDS column)
+// out_face / out_vid: the pixel's contributing face (-1: none) and its vertices, handed to pass 2 in registers
 template <int MODE>
-__device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int dn_stride) {
+__device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int dn_stride, int& out_face, int (&out_vid)[3]) {
 	// XCD-aware tile order: consecutive workgroups are dealt round-robin over the 8 XCDs, so give each XCD a contiguous
 	// band of tiles (neighbouring tiles share vertices, anchors and nodes -> L2 reuse within the XCD).
 	const int tiles = a.tiles_x * a.tiles_y;
@@ -141,7 +142,11 @@ __device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int
 			dr_dnl = make3(psi * d.x, psi * d.y, psi * d.z);
 			dr_dwl = make3(psi * nl.x, psi * nl.y, psi * nl.z);
 		}
-		a.keys[p] = contributes ? static_cast<uint64_t>(static_cast<uint32_t>(face)) : EMPTY_KEY;
+		a.keys[p] = EMPTY_KEY;   // ready for the next iteration's scatter (pass 2 takes the face from registers)
+		out_face = contributes ? face : -1;
+		out_vid[0] = vid[0];
+		out_vid[1] = vid[1];
+		out_vid[2] = vid[2];
 		if (contributes) {
 			// ---- rasterized surface Jacobians (RasterizedSurfaceJacobiansImpl.h:114-200) ----
 			rho[0] = h.b0;
@@ -367,8 +372,10 @@ static_assert(2 * NG_ROWS == PIX_TILE, "pass 2 walks the pass-1 tiles");
 __device__ inline void ng_flush(double* dst, double v) { atomicAdd(dst, v); }
 
 // slots0 / slots1: this wave's two chunk buffers (8 * NG_STRIDE words each); ent: its face-table rows ([NSLOT][64])
+// face_in / vid_in: this lane's pixel's contributing face (-1: none) and its vertices, from pass 1
 template <int MODE, int MAXK>
-__device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, float* slots1, uint32_t* ent) {
+__device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, float* slots1, uint32_t* ent, int face_in,
+                                          const int (&vid_in)[3]) {
 	using T = ModeTraits<MODE>;
 	constexpr int S = T::S;
 	constexpr int NSLOT = 3 * MAXK;
@@ -396,12 +403,8 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 	int head_at = 0;
 	int vid[3] = {0, 0, 0};
 	if (in_image) {
-		const int64_t p = static_cast<int64_t>(v) * a.W + u;
-		const uint64_t key = a.keys[p];
-		a.keys[p] = EMPTY_KEY;   // ready for the next iteration's scatter
-		if (key != EMPTY_KEY) {
-			const int face = static_cast<int>(key & 0xffffffffu);
-			const int4 fi = a.faces4[face];
+		if (face_in >= 0) {
+			const int face = face_in;
 			const uint4* fn4 = reinterpret_cast<const uint4*>(a.face_nodes + static_cast<int64_t>(face) * NSLOT);
 #pragma unroll
 			for (int t = 0; t < NSLOT / 4; t++) {
@@ -412,9 +415,9 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 				ent[(4 * t + 3) * 64 + lane] = e4.w;
 				if (t == 0) head_e = e4.x;
 			}
-			vid[0] = fi.x;
-			vid[1] = fi.y;
-			vid[2] = fi.z;
+			vid[0] = vid_in[0];
+			vid[1] = vid_in[1];
+			vid[2] = vid_in[2];
 		}
 	}
 
@@ -637,14 +640,15 @@ __global__ __launch_bounds__(PIX_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) 
 	__shared__ float s_u[PIX_BLOCK / 64][WORDS];
 	const int wave = static_cast<int>(threadIdx.x >> 6), lane = static_cast<int>(threadIdx.x & 63);
 	float* w = s_u[wave];
-	pixel_body<MODE>(a, w + lane, 64);
+	int face = -1, vid[3] = {0, 0, 0};
+	pixel_body<MODE>(a, w + lane, 64, face, vid);
 	// the node pass reads the records / keys this wave just stored (other lanes' pixels; same CU, same L1): workgroup-scope
 	// release + acquire (an agent-scope release writes back L2 on gfx950: 10x slower); the LDS region is reused in program
 	// order by the same wave
 	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 	__builtin_amdgcn_wave_barrier();
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-	node_body<MODE, MAXK>(a, w, w + 8 * NG_STRIDE, reinterpret_cast<uint32_t*>(w + 2 * 8 * NG_STRIDE));
+	node_body<MODE, MAXK>(a, w, w + 8 * NG_STRIDE, reinterpret_cast<uint32_t*>(w + 2 * 8 * NG_STRIDE), face, vid);
 }
 
 #define NNRT_EV(call)                                                                                                   \
