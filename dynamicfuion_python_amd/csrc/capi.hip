@@ -1439,6 +1439,7 @@ nnrt_status nnrt_block_sparse_and_vector_product(const float* d_blocks, const in
 	NNRT_CHECK_ARG(block_count >= 0 && block_size > 0 && vector_length >= 0 && m >= 0, "bad size");
 	NNRT_CHECK_ARG(m % block_size == 0, "output length m must be a multiple of the block size");
 	NNRT_CHECK_ARG((m == 0 || d_out) && (block_count == 0 || (d_blocks && d_coordinates && d_vector)), "null pointer");
+	NNRT_CHECK_ARG(m == 0 || static_cast<const void*>(d_out) != static_cast<const void*>(d_vector), "d_out must not alias d_vector (it is zeroed first)");
 	hipStream_t s = static_cast<hipStream_t>(stream);
 	return with_device_flag(s, NNRT_ERROR_ARGUMENT, "block coordinate outside the matrix in BlockSparseAndVectorProduct", [&](int* flag) {
 		return launch_block_sparse_vector(d_blocks, d_coordinates, block_count, block_size, block_row_offset, block_column_offset, transpose != 0,

@@ -304,7 +304,7 @@ nnrt_status nnrt_matmul_block_sparse(const float* d_a_blocks, int32_t a_block_co
                                      const int16_t* d_b_breadboard, int32_t b_block_rows, int32_t b_block_columns, int32_t transpose_b,
                                      int32_t block_size, float* d_c_blocks, uint8_t* d_c_mask, void* stream);
 /* BlockSparseAndVectorProduct (MatmulBlockSparseImpl.h:441-602): out [m] = op(A) v, A given by blocks at coordinates + the
- * (row, column) block offset; transpose places block (i, j) at (j, i) transposed. */
+ * (row, column) block offset; transpose places block (i, j) at (j, i) transposed. d_out must not alias d_vector. */
 nnrt_status nnrt_block_sparse_and_vector_product(const float* d_blocks, const int32_t* d_coordinates, int32_t block_count, int32_t block_size,
                                                  int32_t block_row_offset, int32_t block_column_offset, int32_t transpose,
                                                  const float* d_vector, int64_t vector_length, int64_t m, float* d_out, void* stream);
@@ -312,7 +312,9 @@ nnrt_status nnrt_block_sparse_and_vector_product(const float* d_blocks, const in
 nnrt_status nnrt_diagonal_block_sparse_and_vector_product(const float* d_blocks, int32_t block_count, int32_t block_size, const float* d_vector,
                                                           float* d_out, void* stream);
 /* FillInSparseBlocks / AddSparseBlocks / SubtractSparseBlocks (SparseBlocksImpl.h:30-190), op 0 / 1 / 2, into a row-major
- * [rows, columns] matrix; d_coordinates == NULL: block i at (i, i) (FillInDiagonalBlocks, DiagonalBlocksImpl.h). */
+ * [rows, columns] matrix; d_coordinates == NULL: block i at (i, i) (FillInDiagonalBlocks, DiagonalBlocksImpl.h). Add and
+ * subtract are atomic; a fill with repeated coordinates keeps one of the blocks, unspecified which (the reference's
+ * ParallelFor races the same way). */
 nnrt_status nnrt_sparse_blocks_op(float* d_matrix, int64_t rows, int64_t columns, const float* d_blocks, const int32_t* d_coordinates,
                                   int32_t block_count, int32_t block_size, int64_t block_row_offset, int64_t block_column_offset,
                                   int32_t transpose, int32_t op, void* stream);
