@@ -210,23 +210,46 @@ __global__ __launch_bounds__(64) void k_arrow_stem(int n0, const float* __restri
                              const float* __restrict__ wing, float* __restrict__ dinv, float* __restrict__ dinv_b, int* error_flag) {
 	const int i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n0) return;
+	// 6 x 6 blocks are 144 B = nine 16-B words: loaded and stored as float4
 	float L[6][6];
+	{
+		const float4* d4 = reinterpret_cast<const float4*>(diag + static_cast<int64_t>(i) * 36);
+		float f[36];
 #pragma unroll
-	for (int r = 0; r < 6; r++)
+		for (int q = 0; q < 9; q++) {
+			const float4 v = d4[q];
+			f[4 * q] = v.x;
+			f[4 * q + 1] = v.y;
+			f[4 * q + 2] = v.z;
+			f[4 * q + 3] = v.w;
+		}
 #pragma unroll
-		for (int c = 0; c < 6; c++) L[r][c] = diag[static_cast<int64_t>(i) * 36 + 6 * r + c];
+		for (int k = 0; k < 36; k++) L[k / 6][k % 6] = f[k];
+	}
 	if (!cholesky_small<6>(L)) {
 		atomicOr(error_flag, 1);
 		return;
 	}
 	float Di[6][6];
 	invert_from_cholesky_small<6>(L, Di);
+	float4* o4 = reinterpret_cast<float4*>(dinv + static_cast<int64_t>(i) * 36);
 #pragma unroll
-	for (int k = 0; k < 36; k++) dinv[static_cast<int64_t>(i) * 36 + k] = Di[k / 6][k % 6];
+	for (int q = 0; q < 9; q++)
+		o4[q] = make_float4(Di[(4 * q) / 6][(4 * q) % 6], Di[(4 * q + 1) / 6][(4 * q + 1) % 6], Di[(4 * q + 2) / 6][(4 * q + 2) % 6],
+		                    Di[(4 * q + 3) / 6][(4 * q + 3) % 6]);
 	for (int ei = edge_offsets[i]; ei < edge_offsets[i + 1]; ei++) {
 		const int e = edge_list[ei];
-		const float* B = wing + static_cast<int64_t>(e) * 36;
-		float* Y = dinv_b + static_cast<int64_t>(e) * 36;
+		const float4* B4 = reinterpret_cast<const float4*>(wing + static_cast<int64_t>(e) * 36);
+		float B[36];
+#pragma unroll
+		for (int q = 0; q < 9; q++) {
+			const float4 v = B4[q];
+			B[4 * q] = v.x;
+			B[4 * q + 1] = v.y;
+			B[4 * q + 2] = v.z;
+			B[4 * q + 3] = v.w;
+		}
+		float Y[36];
 #pragma unroll
 		for (int r = 0; r < 6; r++)
 #pragma unroll
@@ -236,6 +259,9 @@ __global__ __launch_bounds__(64) void k_arrow_stem(int n0, const float* __restri
 				for (int k = 0; k < 6; k++) acc += Di[r][k] * B[6 * k + c];
 				Y[6 * r + c] = acc;
 			}
+		float4* Y4 = reinterpret_cast<float4*>(dinv_b + static_cast<int64_t>(e) * 36);
+#pragma unroll
+		for (int q = 0; q < 9; q++) Y4[q] = make_float4(Y[4 * q], Y[4 * q + 1], Y[4 * q + 2], Y[4 * q + 3]);
 	}
 }
 

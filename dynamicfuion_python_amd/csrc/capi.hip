@@ -1495,6 +1495,8 @@ nnrt_status nnrt_invert_triangular_blocks(const float* d_blocks, int32_t block_c
 nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, const float* d_wing, const int32_t* d_coords, int32_t E, int32_t N,
                                                        int32_t n0, const float* d_b, float* d_x, void* stream) {
 	NNRT_CHECK_ARG(n0 >= 0 && n0 <= N, "arrow_base_block_index out of range");
+	NNRT_CHECK_ARG((reinterpret_cast<uintptr_t>(d_diag) & 15) == 0 && (reinterpret_cast<uintptr_t>(d_wing) & 15) == 0,
+	               "diagonal and wing blocks must be 16-byte aligned (the stem reads 6x6 blocks as float4)");
 	hipStream_t s = static_cast<hipStream_t>(stream);
 	std::vector<int32_t> coords(2 * static_cast<size_t>(E));
 	if (E > 0) {
