@@ -865,22 +865,51 @@ __global__ void k_arrow_back(int n0, const float* __restrict__ dinv, const int* 
 	if (i >= n0) return;
 	float r6[6];
 	for (int c = 0; c < 6; c++) r6[c] = rhs[6 * static_cast<int64_t>(i) + c];
+	// 6 x 6 blocks as nine float4, 6-vectors as three float2 (the same products and sums as element-wise loads)
+	auto load36 = [](const float* src, float (&dst)[36]) {
+		const float4* s4 = reinterpret_cast<const float4*>(src);
+#pragma unroll
+		for (int q = 0; q < 9; q++) {
+			const float4 v = s4[q];
+			dst[4 * q] = v.x;
+			dst[4 * q + 1] = v.y;
+			dst[4 * q + 2] = v.z;
+			dst[4 * q + 3] = v.w;
+		}
+	};
 	for (int ei = edge_offsets[i]; ei < edge_offsets[i + 1]; ei++) {
 		const int e = edge_list[ei];
 		const int j = edges[2 * e + 1];
-		const float* B = wing + static_cast<int64_t>(e) * 36;
+		float B[36], xj[6];
+		load36(wing + static_cast<int64_t>(e) * 36, B);
+		const float2* x2 = reinterpret_cast<const float2*>(x + 6 * static_cast<int64_t>(j));
+#pragma unroll
+		for (int q = 0; q < 3; q++) {
+			const float2 v = x2[q];
+			xj[2 * q] = v.x;
+			xj[2 * q + 1] = v.y;
+		}
+#pragma unroll
 		for (int r = 0; r < 6; r++) {
 			float acc = 0.f;
-			for (int k = 0; k < 6; k++) acc += B[6 * r + k] * x[6 * static_cast<int64_t>(j) + k];
+#pragma unroll
+			for (int k = 0; k < 6; k++) acc += B[6 * r + k] * xj[k];
 			r6[r] -= acc;
 		}
 	}
-	const float* D = dinv + static_cast<int64_t>(i) * 36;
+	float D[36];
+	load36(dinv + static_cast<int64_t>(i) * 36, D);
+	float o[6];
+#pragma unroll
 	for (int r = 0; r < 6; r++) {
 		float acc = 0.f;
+#pragma unroll
 		for (int k = 0; k < 6; k++) acc += D[6 * r + k] * r6[k];
-		x[6 * static_cast<int64_t>(i) + r] = acc;
+		o[r] = acc;
 	}
+	float2* xo = reinterpret_cast<float2*>(x + 6 * static_cast<int64_t>(i));
+#pragma unroll
+	for (int q = 0; q < 3; q++) xo[q] = make_float2(o[2 * q], o[2 * q + 1]);
 }
 
 __global__ void k_arrow_update(int N, const float* __restrict__ x, float* __restrict__ node_state, float* __restrict__ updates_out) {

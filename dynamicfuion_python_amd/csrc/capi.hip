@@ -1497,6 +1497,7 @@ nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, cons
 	NNRT_CHECK_ARG(n0 >= 0 && n0 <= N, "arrow_base_block_index out of range");
 	NNRT_CHECK_ARG((reinterpret_cast<uintptr_t>(d_diag) & 15) == 0 && (reinterpret_cast<uintptr_t>(d_wing) & 15) == 0,
 	               "diagonal and wing blocks must be 16-byte aligned (the stem reads 6x6 blocks as float4)");
+	NNRT_CHECK_ARG((reinterpret_cast<uintptr_t>(d_x) & 7) == 0, "x must be 8-byte aligned");
 	hipStream_t s = static_cast<hipStream_t>(stream);
 	std::vector<int32_t> coords(2 * static_cast<size_t>(E));
 	if (E > 0) {
