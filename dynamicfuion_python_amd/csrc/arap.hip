@@ -164,47 +164,6 @@ __global__ __launch_bounds__(256) void k_arrow_prepare(int N, float lm, double* 
 	}
 }
 
-// ---- corner init: S = C (diagonal corner blocks + corner off-diagonal blocks), identity on the padding; cb = b_C ----
-// One thread per 4 consecutive entries of a row (one 16-B store; 32-bit index arithmetic: ld <= 32768). Strictly-upper
-// 64 x 64 tiles are left unwritten: the factorization and both substitutions touch tiles I >= J only (k_chol_step,
-// k_chol_back_group), so half the corner's bytes need no initialisation.
-__global__ void k_arrow_corner_init(int n0, int m, int ld, const float* __restrict__ diag, float* __restrict__ S, const float* __restrict__ rhs,
-                                    float* __restrict__ cb) {
-	const int q = ld >> 2;
-	const int idx = static_cast<int>(blockIdx.x) * static_cast<int>(blockDim.x) + static_cast<int>(threadIdx.x);
-	if (idx >= ld * q) return;
-	const int r = idx / q, c0 = (idx - r * q) * 4;
-	if (c0 == 0) cb[r] = r < m ? rhs[6 * static_cast<int64_t>(n0) + r] : 0.f;
-	if ((c0 / CORNER_NB) > (r / CORNER_NB)) return;
-	float v[4];
-#pragma unroll
-	for (int j = 0; j < 4; j++) {
-		const int c = c0 + j;
-		v[j] = 0.f;
-		if (r < m && c < m) {
-			if (r / 6 == c / 6) v[j] = diag[static_cast<int64_t>(n0 + r / 6) * 36 + 6 * (r % 6) + (c % 6)];
-		} else if (r == c) {
-			v[j] = 1.f;
-		}
-	}
-	*reinterpret_cast<float4*>(S + static_cast<int64_t>(r) * ld + c0) = make_float4(v[0], v[1], v[2], v[3]);
-}
-
-__global__ void k_arrow_corner_offdiag(int E, int n0, int ld, const int32_t* __restrict__ edges, const float* __restrict__ wing,
-                                       float* __restrict__ S) {
-	const int e = blockIdx.x;
-	const int i = edges[2 * e], j = edges[2 * e + 1];
-	if (i < n0) return;
-	const int t = threadIdx.x;
-	if (t >= 36) return;
-	const int r = t / 6, c = t % 6;
-	const float v = wing[static_cast<int64_t>(e) * 36 + t];
-	const int ai = i - n0, bj = j - n0;
-	atomicAdd(S + static_cast<int64_t>(6 * ai + r) * ld + 6 * bj + c, v);
-	atomicAdd(S + static_cast<int64_t>(6 * bj + c) * ld + 6 * ai + r, v);
-	(void) E;
-}
-
 // ---- stem: D^-1 and D^-1 B per stem node (one thread per stem node) ----
 __global__ __launch_bounds__(64) void k_arrow_stem(int n0, const float* __restrict__ diag, const int* __restrict__ edge_offsets, const int* __restrict__ edge_list,
                              const float* __restrict__ wing, float* __restrict__ dinv, float* __restrict__ dinv_b, int* error_flag) {
@@ -269,9 +228,8 @@ __global__ __launch_bounds__(64) void k_arrow_stem(int n0, const float* __restri
 // Lane (r, c) < 36 owns entry (r, c) of the 6x6 target block. The target's pair list is loaded once, one pair per lane,
 // and broadcast by shuffle, so the wing / D^-1 B loads of eight pairs are in flight together (no dependent index load
 // per pair). Pairs are summed in list order.
-__global__ __launch_bounds__(256) void k_stem_schur(int targets, int ld, const int* __restrict__ tgt_off, const int2* __restrict__ tgt_ab,
-                                                    const int2* __restrict__ pairs, const float* __restrict__ wing, const float* __restrict__ dinv_b,
-                                                    float* __restrict__ S) {
+__global__ __launch_bounds__(256) void k_stem_schur(int targets, CornerMap S, const int* __restrict__ tgt_off, const int2* __restrict__ tgt_ab,
+                                                    const int2* __restrict__ pairs, const float* __restrict__ wing, const float* __restrict__ dinv_b) {
 	const int w = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
 	const int lane = static_cast<int>(threadIdx.x & 63);
 	if (w >= targets) return;
@@ -308,16 +266,17 @@ __global__ __launch_bounds__(256) void k_stem_schur(int targets, int ld, const i
 	}
 	if (lane < 36) {
 		const int2 ab = tgt_ab[w];
-		S[static_cast<int64_t>(6 * ab.x + r) * ld + 6 * ab.y + c] -= acc;
+		float* dst = corner_block_entry(S, ab.x, ab.y, r, c);
+		if (dst) *dst -= acc;
 	}
 }
 
 // ---- fitter form of the Schur update: the ARAP wing blocks dEi^T dEj (dEj = [0 | b I]) are zero outside their last
 // three columns, so B_ia^T D_i^-1 B_ib is zero outside its lower-right 3x3 block and only those 9 entries change
 // (the others would subtract exact zeros). 7 pair slots x 9 entries per wave; slots reduced in order at the end.
-__global__ __launch_bounds__(256) void k_stem_schur_t3(int targets, int ld, const int* __restrict__ tgt_off, const int2* __restrict__ tgt_ab,
+__global__ __launch_bounds__(256) void k_stem_schur_t3(int targets, CornerMap S, const int* __restrict__ tgt_off, const int2* __restrict__ tgt_ab,
                                                        const int2* __restrict__ pairs, const float* __restrict__ wing,
-                                                       const float* __restrict__ dinv_b, float* __restrict__ S) {
+                                                       const float* __restrict__ dinv_b) {
 	__shared__ float s_part[4][7][9];
 	const int w = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
 	const int lane = static_cast<int>(threadIdx.x & 63), wl = static_cast<int>(threadIdx.x >> 6);
@@ -358,14 +317,15 @@ __global__ __launch_bounds__(256) void k_stem_schur_t3(int targets, int ld, cons
 #pragma unroll
 		for (int sl = 0; sl < 7; sl++) t += s_part[wl][sl][lane];
 		const int2 ab = tgt_ab[w];
-		S[static_cast<int64_t>(6 * ab.x + 3 + lane / 3) * ld + 6 * ab.y + 3 + lane % 3] -= t;
+		float* dst = corner_block_entry(S, ab.x, ab.y, 3 + lane / 3, 3 + lane % 3);
+		if (dst) *dst -= t;
 	}
 }
 
 // ---- b_C -= sum over stem edges i->a of (D_i^-1 B_ia)^T b_i (one wave per corner node; lanes over its edges) ----
 __global__ __launch_bounds__(256) void k_stem_rhs(int nc, const int* __restrict__ rhs_off, const int* __restrict__ rhs_edges,
                                                   const int32_t* __restrict__ edges, const float* __restrict__ dinv_b, const float* __restrict__ rhs,
-                                                  float* __restrict__ cb) {
+                                                  const int* __restrict__ node_row, float* __restrict__ cb) {
 	const int a = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
 	const int lane = static_cast<int>(threadIdx.x & 63);
 	if (a >= nc) return;
@@ -395,7 +355,7 @@ __global__ __launch_bounds__(256) void k_stem_rhs(int nc, const int* __restrict_
 		float v = s[0];
 #pragma unroll
 		for (int c = 1; c < 6; c++) v = lane == c ? s[c] : v;
-		cb[6 * static_cast<int64_t>(a) + lane] -= v;
+		cb[node_row[a] + lane] -= v;   // the corner's permuted order
 	}
 }
 
@@ -440,421 +400,6 @@ StemSchurLists build_stem_schur_lists(const int32_t* edges, int E, int n0, int N
 	}
 	if (!q.empty()) L.tgt_off.push_back(static_cast<int>(q.size()));
 	return L;
-}
-
-// ---- dense corner: blocked right-looking Cholesky of S (ld x ld, row-major, lower triangle) and S x = b -------------
-// SolveBlockSparseArrowheadCholesky.cpp:30-95 factors the Schur complement with a dense potrf. Here ONE launch per
-// 64-column block k (k_chol_step), whose workgroups play two roles:
-//   panel   (block rows I >= k, dealt first): apply the previous block's update to the two tiles this row needs,
-//           A_kk -= L_k,k-1 L_k,k-1^T and A_Ik -= L_I,k-1 L_k,k-1^T (f32 MFMA, v_mfma_f32_32x32x2_f32, one 32 x 32
-//           quadrant per wave, into LDS); then one wave holds both tiles (lane = row) in registers and runs the 64
-//           column eliminations of A_kk, applying each to its panel row as it goes (one packed FMA per column pair):
-//           L_kk and L_Ik = A_Ik L_kk^-T come out of one pass with no inverse. The right-hand side rides along as the
-//           panel row of the diagonal workgroup (lane 0): y_k = L_kk^-1 b_k.
-//   trailing (tiles k < J <= I): A_IJ -= L_I,k-1 L_J,k-1^T on the MFMA, and b_J -= L_J,k-1 y_k-1 by the diagonal tiles.
-// Every operand of launch k was finished by launch k - 1, so consecutive launches are the only synchronisation.
-// The block back substitution L^T x = y then runs BACK_G block rows per launch (k_chol_back_group).
-constexpr int CT = 256;   // threads per workgroup of the corner kernels
-constexpr int CORNER_LAZY = 4;   // trailing columns are updated every CORNER_LAZY-th launch (k_chol_step; C5: 2 / 3 / 4 / 5 / 6
-                                 // / 8 -> 769 / 743 / 737 / 749 / 814 / 950 us solve stage)
-constexpr int CS4 = CORNER_NB + 4;   // LDS row stride of the staged tiles (16-B aligned rows for ds_read_b128)
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-__device__ inline float lane_bcast(float v, int src) {
-	return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
-}
-
-// 32 x 32 quadrant (qr, qc) of X Y^T for X, Y 64 x 64 row-major tiles at row stride ld (lane l feeds
-// A[i = l & 31][k'] = X[32 qr + i][32 (l >> 5) + s] and B[k'][j] = Y[32 qc + j][32 (l >> 5) + s] to MFMA step s, so the 32
-// steps x 2 lane halves cover the 64-wide k range; each lane reads 32 contiguous floats). C/D map: column l & 31, row
-// (v & 3) + 8 (v >> 2) + 4 (l >> 5).
-__device__ inline f32x16 quadrant_xyt(const float* X, const float* Y, int64_t ld, int qr, int qc, int lane, f32x16 acc = {}) {
-	const int half = lane >> 5, l32 = lane & 31;
-	const float4* x4 = reinterpret_cast<const float4*>(X + (32 * qr + l32) * ld + 32 * half);
-	const float4* y4 = reinterpret_cast<const float4*>(Y + (32 * qc + l32) * ld + 32 * half);
-	float4 vx[8], vy[8];
-#pragma unroll
-	for (int q = 0; q < 8; q++) {
-		vx[q] = x4[q];
-		vy[q] = y4[q];
-	}
-#pragma unroll
-	for (int q = 0; q < 8; q++) {
-		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].x, vy[q].x, acc, 0, 0, 0);
-		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].y, vy[q].y, acc, 0, 0, 0);
-		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].z, vy[q].z, acc, 0, 0, 0);
-		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].w, vy[q].w, acc, 0, 0, 0);
-	}
-	return acc;
-}
-
-__device__ inline int quad_row(int v, int lane) { return (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5); }
-
-// s_t[r][c] = T[r][c] - (X Y^T)[r][c] for the workgroup's quadrant of a 64 x 64 tile T (global, row stride ld)
-__device__ inline void stage_updated_tile(const float* T, const float* X, const float* Y, int64_t ld, int wave, int lane, float* s_t) {
-	const int qr = wave >> 1, qc = wave & 1;
-	float tv[16];
-#pragma unroll
-	for (int v = 0; v < 16; v++) tv[v] = T[(32 * qr + quad_row(v, lane)) * ld + 32 * qc + (lane & 31)];
-	const f32x16 acc = quadrant_xyt(X, Y, ld, qr, qc, lane);
-#pragma unroll
-	for (int v = 0; v < 16; v++) s_t[(32 * qr + quad_row(v, lane)) * CS4 + 32 * qc + (lane & 31)] = tv[v] - acc[v];
-}
-
-// b_J -= L_J y for a 64 x 64 tile L (row stride ld) and the 64-vector y: 4 threads per row, 16 columns each
-__device__ inline float rhs_row_update(const float* L, int64_t ld, const float* y, int t) {
-	const int r = t >> 2, q4 = t & 3;
-	const float* Lr = L + r * ld + 16 * q4;
-	const float* yq = y + 16 * q4;
-	float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-	for (int c = 0; c < 16; c += 2) {
-		s0 += Lr[c] * yq[c];
-		s1 += Lr[c + 1] * yq[c + 1];
-	}
-	float s = s0 + s1;
-	s += __shfl_xor(s, 1);
-	s += __shfl_xor(s, 2);
-	return s;
-}
-
-
-// Column eliminations J0 <= j < J1 of the row pairs ap (lane = row), applied to the columns c < J1 only, in blocks of
-// four: the four columns are factored among themselves, then applied to every later column c with four packed FMAs
-// whose multipliers L_c,jb..jb+3 are read from lane c by readlane (scalar operands: nothing on the elimination path
-// waits on LDS). Every element sees its updates in ascending column order.
-template <int J0, int J1>
-__device__ inline void eliminate_columns(f32x2 (&ap)[CORNER_NB], int lane, int& bad) {
-	__shared__ float4 s_l4[2][CORNER_NB];   // s_l4[.][c] = (L_c,jb .. L_c,jb+3)
-#pragma clang loop unroll(full)
-	for (int jb = J0; jb < J1; jb += 4) {
-		// The 4 x 4 diagonal sub-block is read once (10 independent readlanes) and factored wave-uniformly; every lane
-		// then runs the same operations on its own row with the uniform multipliers. The uniform values are exactly
-		// the ones lanes jb..jb+3 compute (same operations, same order), so the pivot chain has no readlane round trip
-		// per column.
-		float M[4][4], Lu[4][4], rsv[4];
-#pragma unroll
-		for (int q = 0; q < 4; q++)
-#pragma unroll
-			for (int i = q; i < 4; i++) M[i][q] = lane_bcast(ap[jb + q].x, jb + i);
-#pragma unroll
-		for (int q = 0; q < 4; q++) {
-			float piv = M[q][q];   // A_jj after the first j eliminations
-			bad |= !(piv > 0.f);
-			piv = piv > 0.f ? piv : 1.f;
-			rsv[q] = __builtin_amdgcn_rsqf(piv);
-#pragma unroll
-			for (int i = q; i < 4; i++) Lu[i][q] = M[i][q] * rsv[q];
-#pragma unroll
-			for (int q2 = q + 1; q2 < 4; q2++)
-#pragma unroll
-				for (int i = q2; i < 4; i++) M[i][q2] = __builtin_fmaf(-Lu[i][q], Lu[q2][q], M[i][q2]);
-		}
-		float lx[4];
-		f32x2 nl[4];
-#pragma unroll
-		for (int q = 0; q < 4; q++) {
-			const f32x2 l = ap[jb + q] * rsv[q];   // (L_rj for rows r >= j of the diagonal block, panel / rhs entry)
-			ap[jb + q] = l;
-			lx[q] = l.x;
-			nl[q] = -l;
-#pragma unroll
-			for (int q2 = q + 1; q2 < 4; q2++) {
-				const float lc = Lu[q2][q];
-				ap[jb + q2] = __builtin_elementwise_fma(nl[q], f32x2{lc, lc}, ap[jb + q2]);
-			}
-		}
-		// next block's columns first (readlane: on the pivot chain), the rest from a wave-uniform 16-B LDS broadcast
-		// whose latency hides behind them
-		float4* row = &s_l4[(jb >> 2) & 1][0];
-		if (jb + 8 < J1) row[lane] = make_float4(lx[0], lx[1], lx[2], lx[3]);
-#pragma unroll
-		for (int q = 0; q < 4; q++)   // q outer: consecutive FMAs are independent
-#pragma unroll
-			for (int c = jb + 4; c < J1 && c < jb + 8; c++) {
-				const float lc = lane_bcast(lx[q], c);   // L_c,jb+q, c > jb + 3
-				ap[c] = __builtin_elementwise_fma(nl[q], f32x2{lc, lc}, ap[c]);
-			}
-#pragma unroll
-		for (int c0 = jb + 8; c0 < J1; c0 += 8) {   // chunks of 8 columns: 8 broadcasts in flight
-			float4 L4[8];
-#pragma unroll
-			for (int u = 0; u < 8; u++)
-				if (c0 + u < J1) L4[u] = row[c0 + u];
-#pragma unroll
-			for (int u = 0; u < 8; u++)
-				if (c0 + u < J1) ap[c0 + u] = __builtin_elementwise_fma(nl[0], f32x2{L4[u].x, L4[u].x}, ap[c0 + u]);
-#pragma unroll
-			for (int u = 0; u < 8; u++)
-				if (c0 + u < J1) ap[c0 + u] = __builtin_elementwise_fma(nl[1], f32x2{L4[u].y, L4[u].y}, ap[c0 + u]);
-#pragma unroll
-			for (int u = 0; u < 8; u++)
-				if (c0 + u < J1) ap[c0 + u] = __builtin_elementwise_fma(nl[2], f32x2{L4[u].z, L4[u].z}, ap[c0 + u]);
-#pragma unroll
-			for (int u = 0; u < 8; u++)
-				if (c0 + u < J1) ap[c0 + u] = __builtin_elementwise_fma(nl[3], f32x2{L4[u].w, L4[u].w}, ap[c0 + u]);
-		}
-	}
-}
-
-__global__ __launch_bounds__(CT) void k_chol_step(float* __restrict__ A, int ld, int k, int T, float* __restrict__ b, int* error_flag) {
-	__shared__ float s_d[CORNER_NB * CS4];   // A_kk after the previous block's update
-	__shared__ float s_p[CORNER_NB * CS4];   // A_Ik after the previous block's update (panel workgroups below the diagonal)
-	__shared__ float s_b[CORNER_NB];         // b_k after the previous block's update (diagonal workgroup)
-	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-	const int64_t LD = ld;
-	const int npanel = T - k;
-	const int64_t ok0 = static_cast<int64_t>(k) * CORNER_NB, op = ok0 - CORNER_NB;   // column offsets of blocks k and k - 1
-	if (static_cast<int>(blockIdx.x) >= npanel) {
-		// ---- trailing tile (I, J), k < J <= I: lazy updates. Launch k updates the columns J = k + 1, k + 1 + LAZY, ..
-		// (every tile I >= J of them) with their pending blocks max(0, k - LAZY) .. k - 1: each column takes LAZY blocks
-		// every LAZY-th launch (1 / LAZY of the tile passes of one update per block) and is complete up to block J - 2
-		// when its panel launch stages block J - 1.
-		int r = static_cast<int>(blockIdx.x) - npanel, m = 0, cnt = T - (k + 1);
-		while (r >= cnt) {   // column k + 1 + LAZY m holds T - (k + 1 + LAZY m) tiles
-			r -= cnt;
-			m++;
-			cnt -= CORNER_LAZY;
-		}
-		const int jj = CORNER_LAZY * m, ii = jj + r;   // J = k + 1 + jj, I = k + 1 + ii
-		const int b0 = k >= CORNER_LAZY ? k - CORNER_LAZY : 0;
-		const int64_t rI = static_cast<int64_t>(k + 1 + ii) * CORNER_NB, rJ = static_cast<int64_t>(k + 1 + jj) * CORNER_NB;
-		const int qr = wave >> 1, qc = wave & 1;
-		float* C = A + rI * LD + rJ + 32 * qc + (lane & 31);
-		float cv[16];
-#pragma unroll
-		for (int v = 0; v < 16; v++) cv[v] = C[(32 * qr + quad_row(v, lane)) * LD];
-		// one product per pending block, subtracted in block order: the same float operations as one update per launch
-		for (int pb = b0; pb < k; pb++) {
-			const int64_t ob = static_cast<int64_t>(pb) * CORNER_NB;
-			const f32x16 acc = quadrant_xyt(A + rI * LD + ob, A + rJ * LD + ob, LD, qr, qc, lane);
-#pragma unroll
-			for (int v = 0; v < 16; v++) cv[v] -= acc[v];
-		}
-#pragma unroll
-		for (int v = 0; v < 16; v++) C[(32 * qr + quad_row(v, lane)) * LD] = cv[v];
-		if (rI == rJ) {
-			float bj = (t & 3) == 0 ? b[rJ + (t >> 2)] : 0.f;
-			for (int pb = b0; pb < k; pb++) {
-				const int64_t ob = static_cast<int64_t>(pb) * CORNER_NB;
-				bj -= rhs_row_update(A + rJ * LD + ob, LD, b + ob, t);
-			}
-			if ((t & 3) == 0) b[rJ + (t >> 2)] = bj;
-		}
-		return;
-	}
-	// ---- panel row I = k + blockIdx.x ----
-	const bool diag = blockIdx.x == 0;
-	const int64_t rI = ok0 + static_cast<int64_t>(blockIdx.x) * CORNER_NB;
-	if (k > 0) {
-		stage_updated_tile(A + ok0 * LD + ok0, A + ok0 * LD + op, A + ok0 * LD + op, LD, wave, lane, s_d);
-		if (!diag) {
-			stage_updated_tile(A + rI * LD + ok0, A + rI * LD + op, A + ok0 * LD + op, LD, wave, lane, s_p);
-		} else {
-			const float s = rhs_row_update(A + ok0 * LD + op, LD, b + op, t);
-			if ((t & 3) == 0) s_b[t >> 2] = b[ok0 + (t >> 2)] - s;
-		}
-	} else {
-		for (int e = t; e < CORNER_NB * CORNER_NB; e += CT) {
-			const int rr = e / CORNER_NB, cc = e % CORNER_NB;
-			s_d[rr * CS4 + cc] = A[(ok0 + rr) * LD + ok0 + cc];
-			if (!diag) s_p[rr * CS4 + cc] = A[(rI + rr) * LD + ok0 + cc];
-		}
-		if (diag && t < CORNER_NB) s_b[t] = b[ok0 + t];
-	}
-	__syncthreads();
-	// ap[c] = (A_kk[lane][c], A_Ik[lane][c]): both rows see the same column operations, so one packed FMA
-	// (v_pk_fma_f32) updates the pair. Wave 0 holds them; the other waves join for the rank-32 update between the halves.
-	f32x2 ap[CORNER_NB];
-	int bad = 0;
-	if (wave == 0) {
-#pragma unroll
-		for (int q = 0; q < CORNER_NB / 4; q++) {
-			const float4 va = *reinterpret_cast<const float4*>(s_d + lane * CS4 + 4 * q);
-			float4 vp;
-			if (diag)   // the augmented row: b_k on lane 0, zero elsewhere
-				vp = lane == 0 ? *reinterpret_cast<const float4*>(s_b + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
-			else
-				vp = *reinterpret_cast<const float4*>(s_p + lane * CS4 + 4 * q);
-			ap[4 * q] = f32x2{va.x, vp.x};
-			ap[4 * q + 1] = f32x2{va.y, vp.y};
-			ap[4 * q + 2] = f32x2{va.z, vp.z};
-			ap[4 * q + 3] = f32x2{va.w, vp.w};
-		}
-		eliminate_columns<0, CORNER_NB / 2>(ap, lane, bad);
-		// L[:, 0:32] of the A_kk rows and of the panel rows -> LDS (s_d / s_p are free once loaded)
-#pragma unroll
-		for (int q = 0; q < CORNER_NB / 8; q++) {
-			*reinterpret_cast<float4*>(s_d + lane * CS4 + 4 * q) = make_float4(ap[4 * q].x, ap[4 * q + 1].x, ap[4 * q + 2].x, ap[4 * q + 3].x);
-			*reinterpret_cast<float4*>(s_p + lane * CS4 + 4 * q) = make_float4(ap[4 * q].y, ap[4 * q + 1].y, ap[4 * q + 2].y, ap[4 * q + 3].y);
-		}
-	}
-	__syncthreads();
-	// rank-32 update of columns 32..63: C = L[rows, 0:32] L_kk[32:64, 0:32]^T on the MFMA, one 32-row block per wave
-	// (wave 1: A_kk rows 32..63; waves 2, 3: panel rows 0..31, 32..63; A_kk rows 0..31 lie above the diagonal there)
-	f32x16 cacc = {};
-	if (wave > 0) {
-		const float* X = wave == 1 ? s_d + 32 * CS4 : s_p + 32 * (wave - 2) * CS4;
-		const int half = lane >> 5, l32 = lane & 31;
-		const float4* x4 = reinterpret_cast<const float4*>(X + l32 * CS4 + 16 * half);
-		const float4* y4 = reinterpret_cast<const float4*>(s_d + (32 + l32) * CS4 + 16 * half);
-#pragma unroll
-		for (int q = 0; q < 4; q++) {
-			const float4 vx = x4[q], vy = y4[q];
-			cacc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx.x, vy.x, cacc, 0, 0, 0);
-			cacc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx.y, vy.y, cacc, 0, 0, 0);
-			cacc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx.z, vy.z, cacc, 0, 0, 0);
-			cacc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx.w, vy.w, cacc, 0, 0, 0);
-		}
-	}
-	__syncthreads();   // every wave is done reading L before the products overwrite it
-	if (wave > 0) {
-		float* Cb = wave == 1 ? s_d + 32 * CS4 : s_p + 32 * (wave - 2) * CS4;
-#pragma unroll
-		for (int v = 0; v < 16; v++) Cb[quad_row(v, lane) * CS4 + 32 + (lane & 31)] = cacc[v];
-	}
-	__syncthreads();
-	if (wave != 0) return;
-#pragma unroll
-	for (int q = CORNER_NB / 8; q < CORNER_NB / 4; q++) {
-		const float4 ca = lane >= 32 ? *reinterpret_cast<const float4*>(s_d + lane * CS4 + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
-		const float4 cp = *reinterpret_cast<const float4*>(s_p + lane * CS4 + 4 * q);
-		ap[4 * q] -= f32x2{ca.x, cp.x};
-		ap[4 * q + 1] -= f32x2{ca.y, cp.y};
-		ap[4 * q + 2] -= f32x2{ca.z, cp.z};
-		ap[4 * q + 3] -= f32x2{ca.w, cp.w};
-	}
-	eliminate_columns<CORNER_NB / 2, CORNER_NB>(ap, lane, bad);
-	const bool ok = !bad;
-	if (diag) {
-		float4* wa = reinterpret_cast<float4*>(A + (ok0 + lane) * LD + ok0);
-#pragma unroll
-		for (int q = 0; q < CORNER_NB / 4; q++)
-			wa[q] = make_float4(4 * q <= lane ? ap[4 * q].x : 0.f, 4 * q + 1 <= lane ? ap[4 * q + 1].x : 0.f,
-			                    4 * q + 2 <= lane ? ap[4 * q + 2].x : 0.f, 4 * q + 3 <= lane ? ap[4 * q + 3].x : 0.f);
-		if (lane == 0) {
-			float4* wb = reinterpret_cast<float4*>(b + ok0);
-#pragma unroll
-			for (int q = 0; q < CORNER_NB / 4; q++) wb[q] = make_float4(ap[4 * q].y, ap[4 * q + 1].y, ap[4 * q + 2].y, ap[4 * q + 3].y);
-			if (!ok) atomicOr(error_flag, 1);
-		}
-	} else {
-		float4* wp = reinterpret_cast<float4*>(A + (rI + lane) * LD + ok0);
-#pragma unroll
-		for (int q = 0; q < CORNER_NB / 4; q++) wp[q] = make_float4(ap[4 * q].y, ap[4 * q + 1].y, ap[4 * q + 2].y, ap[4 * q + 3].y);
-	}
-}
-
-// ---- block back substitution L^T x = y, BACK_G block rows per launch (from the last block up) ----------------------
-// Launch for blocks k0, k0 - 1, .., kl (g = k0 - block): wave g holds L_{k0-g,k0-g} by columns in registers; as soon as
-// x_{k0-g2} is known every later wave subtracts L_{k0-g2,k0-g}^T x_{k0-g2} from its z (coupling tiles staged in LDS by
-// the whole workgroup), and wave g, once its z is complete, solves L^T x = z by column-oriented substitution (x_i broadcast by readlane; lane = column, so column i of L^T is the lanes'
-// register i). Every workgroup forms the group's x redundantly; workgroup i < kl then applies y_i -= sum L_ki^T x_k
-// (its tiles prefetched meanwhile) and the group's own workgroups store x (into xout, not over y).
-constexpr int BACK_G = 4;
-
-__global__ __launch_bounds__(CT) void k_chol_back_group(const float* __restrict__ A, int ld, int k0, int kl, float* __restrict__ b, int m,
-                                                       float* __restrict__ xout) {
-	__shared__ float s_cpl[BACK_G * (BACK_G - 1) / 2][CORNER_NB][CORNER_NB + 1];   // [g(g-1)/2 + g2][r][c] = L_{k0-g2,k0-g}[r][c]
-	__shared__ __attribute__((aligned(16))) float s_x[BACK_G][CORNER_NB];
-	__shared__ float s_part[4][CORNER_NB];
-	const int t = threadIdx.x, c = t % CORNER_NB, seg = t / CORNER_NB, wave = t >> 6, lane = t & 63;
-	const int i = static_cast<int>(blockIdx.x);   // target block (i >= kl: a block of the group, store its x)
-	const int64_t LD = ld, ci = static_cast<int64_t>(i) * CORNER_NB;
-	const int G = k0 - kl + 1;
-	float lk[BACK_G][16];
-	if (i < kl) {   // L_ki (rows of block k, columns of block i) for the target update
-#pragma unroll
-		for (int g = 0; g < BACK_G; g++)
-			if (g < G) {
-				const int64_t ck = static_cast<int64_t>(k0 - g) * CORNER_NB;
-#pragma unroll
-				for (int q = 0; q < 16; q++) lk[g][q] = A[(ck + seg * 16 + q) * LD + ci + c];
-			}
-	}
-	for (int g = 1; g < G; g++)
-		for (int g2 = 0; g2 < g; g2++) {
-			const int64_t rr = static_cast<int64_t>(k0 - g2) * CORNER_NB, cc = static_cast<int64_t>(k0 - g) * CORNER_NB;
-			float(*dst)[CORNER_NB + 1] = s_cpl[g * (g - 1) / 2 + g2];
-#pragma unroll
-			for (int q = 0; q < 16; q++) dst[seg * 16 + q][c] = A[(rr + seg * 16 + q) * LD + cc + c];
-		}
-	float col[CORNER_NB];   // wave g: col[r] = L_kk[r][lane], k = k0 - g
-	float inv_d = 1.f, z = 0.f;
-	if (wave < G) {
-		const int64_t ok = static_cast<int64_t>(k0 - wave) * CORNER_NB;
-#pragma unroll
-		for (int r = 0; r < CORNER_NB; r++) col[r] = A[(ok + r) * LD + ok + lane];
-		inv_d = 1.f / A[(ok + lane) * LD + ok + lane];
-		z = b[ok + lane];
-	}
-	for (int g = 0; g < G; g++) {
-		__syncthreads();   // x_{g-1} and the staged coupling tiles are visible
-		if (g > 0 && wave >= g && wave < G) {   // every later block applies the newest x at once (off the chain)
-			const float(*cp)[CORNER_NB + 1] = s_cpl[wave * (wave - 1) / 2 + g - 1];
-			const float4* xv = reinterpret_cast<const float4*>(s_x[g - 1]);
-			float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-			for (int r4 = 0; r4 < CORNER_NB / 4; r4++) {
-				const float4 x4 = xv[r4];
-				s0 += cp[4 * r4][lane] * x4.x;
-				s1 += cp[4 * r4 + 1][lane] * x4.y;
-				s0 += cp[4 * r4 + 2][lane] * x4.z;
-				s1 += cp[4 * r4 + 3][lane] * x4.w;
-			}
-			z -= s0 + s1;
-		}
-		if (wave == g) {
-			float x = 0.f;
-#pragma unroll
-			for (int r = CORNER_NB - 1; r >= 0; r--) {
-				const float xr = lane_bcast(z, r) * lane_bcast(inv_d, r);   // x_r = z_r / L_rr
-				x = lane == r ? xr : x;
-				z -= col[r] * xr;   // z_c -= L_rc x_r (only c < r matter)
-			}
-			s_x[g][lane] = x;
-		}
-	}
-	__syncthreads();
-	if (i >= kl) {   // x goes to its own array: the group's y, which b holds, may still be read by a workgroup starting late
-		if (t < CORNER_NB && ci + t < m) xout[ci + t] = s_x[k0 - i][t];
-		return;
-	}
-	float acc = 0.f;
-#pragma unroll
-	for (int g = 0; g < BACK_G; g++)
-		if (g < G) {
-#pragma unroll
-			for (int q = 0; q < 16; q++) acc += lk[g][q] * s_x[g][seg * 16 + q];
-		}
-	s_part[seg][c] = acc;
-	__syncthreads();
-	if (t < CORNER_NB) b[ci + t] -= (s_part[0][t] + s_part[1][t]) + (s_part[2][t] + s_part[3][t]);
-}
-
-// x (the first m corner unknowns) -> xout
-nnrt_status corner_cholesky_solve(float* A, int ld, float* cb, int m, float* xout, int* error_flag, hipStream_t stream) {
-	const int T = ld / CORNER_NB;
-	// k_chol_step's panel workgroups read A_kk while the diagonal one overwrites it with L_kk: they must all be resident
-	// before any finishes, which the dispatch order (panels first) guarantees while T fits the chip's 512 workgroup
-	// slots at two per CU (a 32768-unknown corner, 5461 coarse nodes)
-	NNRT_CHECK_ARG(T <= 512, "arrowhead corner larger than 32768 unknowns");
-	for (int k = 0; k < T; k++) {   // factor [S | b]: the forward substitution rides along as an augmented row
-		const int panel = T - k;
-		int trailing = 0;   // lazy trailing updates on every CORNER_LAZY-th column (k_chol_step)
-		if (k > 0)
-			for (int J = k + 1; J < T; J += CORNER_LAZY) trailing += T - J;
-		k_chol_step<<<panel + trailing, CT, 0, stream>>>(A, ld, k, T, cb, error_flag);
-		NNRT_LAUNCH_CHECK();
-	}
-	for (int k0 = T - 1; k0 >= 0; k0 -= BACK_G) {
-		const int kl = k0 - BACK_G + 1 > 0 ? k0 - BACK_G + 1 : 0;
-		k_chol_back_group<<<k0 + 1, CT, 0, stream>>>(A, ld, k0, kl, cb, m, xout);
-		NNRT_LAUNCH_CHECK();
-	}
-	return NNRT_OK;
 }
 
 // ---- stem back-substitution: x_D = D^-1 (b_D - B x_C) ----
@@ -933,36 +478,32 @@ __global__ void k_arrow_update(int N, const float* __restrict__ x, float* __rest
 
 nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* edges, const float* wing, int* error_flag, hipStream_t stream,
                                  bool arap_wings) {
-	const int m = ws.m, ld = ws.ld;
+	const int m = ws.m;
+	NNRT_CHECK_ARG(m == 0 || ws.corner, "arrowhead workspace without a corner plan");
 	if (m > 0) {
-		NNRT_CHECK_ARG(ld <= 32768, "arrowhead corner larger than 32768 unknowns");
-		k_arrow_corner_init<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ld) * (ld / 4), 256)), 256, 0, stream>>>(ws.n0, m, ld, ws.diag,
-		                                                                                                                    ws.schur, ws.rhs, ws.cb);
-		NNRT_LAUNCH_CHECK();
-		if (ws.E > 0) {
-			k_arrow_corner_offdiag<<<ws.E, 64, 0, stream>>>(ws.E, ws.n0, ld, edges, wing, ws.schur);
-			NNRT_LAUNCH_CHECK();
-		}
+		nnrt_status st = ws.corner->launch_init(ws.n0, ws.diag, ws.rhs, edges, wing, stream);
+		if (st) return st;
 	}
 	if (ws.n0 > 0) {
 		k_arrow_stem<<<static_cast<unsigned>(ceil_div(ws.n0, 64)), 64, 0, stream>>>(ws.n0, ws.diag, ws.edge_offsets, ws.edge_list, wing, ws.dinv,
 		                                                                           ws.dinv_b, error_flag);
 		NNRT_LAUNCH_CHECK();
 		if (m > 0 && ws.targets > 0) {
+			const CornerMap cm = ws.corner->map();
 			if (arap_wings)
 				k_stem_schur_t3<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ws.targets) * 64, 256)), 256, 0, stream>>>(
-				    ws.targets, ld, ws.tgt_off, ws.tgt_ab, ws.pairs, wing, ws.dinv_b, ws.schur);
+				    ws.targets, cm, ws.tgt_off, ws.tgt_ab, ws.pairs, wing, ws.dinv_b);
 			else
 				k_stem_schur<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ws.targets) * 64, 256)), 256, 0, stream>>>(
-				    ws.targets, ld, ws.tgt_off, ws.tgt_ab, ws.pairs, wing, ws.dinv_b, ws.schur);
+				    ws.targets, cm, ws.tgt_off, ws.tgt_ab, ws.pairs, wing, ws.dinv_b);
 			NNRT_LAUNCH_CHECK();
-			k_stem_rhs<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(m / 6) * 64, 256)), 256, 0, stream>>>(m / 6, ws.rhs_off, ws.rhs_edges,
-			                                                                                                         edges, ws.dinv_b, ws.rhs, ws.cb);
+			k_stem_rhs<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(m / 6) * 64, 256)), 256, 0, stream>>>(
+			    m / 6, ws.rhs_off, ws.rhs_edges, edges, ws.dinv_b, ws.rhs, cm.node_row, ws.corner->rhs_perm());
 			NNRT_LAUNCH_CHECK();
 		}
 	}
 	if (m > 0) {
-		nnrt_status st = corner_cholesky_solve(ws.schur, ld, ws.cb, m, ws.x + 6 * static_cast<int64_t>(ws.n0), error_flag, stream);
+		nnrt_status st = ws.corner->launch_solve(ws.x + 6 * static_cast<int64_t>(ws.n0), error_flag, stream);
 		if (st) return st;
 	}
 	if (ws.n0 > 0) {

@@ -386,7 +386,8 @@ struct nnrt_fitter {
 	DeviceBuffer<float> updates, gradient, hessian;
 	DeviceBuffer<int> error_flag;
 	// ARAP / arrowhead
-	DeviceBuffer<float> wing, edge_residuals, a_diag, a_dinv, a_dinvb, a_schur, a_cb, a_rhs, a_x;
+	DeviceBuffer<float> wing, edge_residuals, a_diag, a_dinv, a_dinvb, a_rhs, a_x;
+	CornerSolver corner;   // Schur corner of the arrowhead solve (tile-sparse Cholesky plan + storage)
 	DeviceBuffer<int> a_offsets, a_list, a_tgt_off, a_rhs_off, a_rhs_edges, a_inc_off, a_inc_list;
 	DeviceBuffer<int2> a_tgt_ab, a_pairs;
 	ArrowheadWorkspace aw;
@@ -606,7 +607,7 @@ void nnrt_fitter_destroy(nnrt_fitter* ft) {
 	ft->ref_points.release();
 	ft->records.release();
 	for (auto* b : {&ft->mesh_p, &ft->mesh_n, &ft->weights, &ft->residuals, &ft->edge_jr, &ft->updates, &ft->gradient,
-	                &ft->hessian, &ft->wing, &ft->edge_residuals, &ft->a_diag, &ft->a_dinv, &ft->a_dinvb, &ft->a_schur, &ft->a_cb, &ft->a_rhs, &ft->a_x})
+	                &ft->hessian, &ft->wing, &ft->edge_residuals, &ft->a_diag, &ft->a_dinv, &ft->a_dinvb, &ft->a_rhs, &ft->a_x})
 		b->release();
 	ft->faces4.release();
 	ft->anchors.release();
@@ -666,7 +667,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 			}
 	}
 	// (re)allocate; any reallocation invalidates captured graphs
-	const auto before = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->a_schur.ptr,
+	const auto before = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->corner.generation,
 	                                    ft->face_nodes.ptr, ft->wpos.ptr);
 	nnrt_status st;
 	if ((st = ft->mesh_p.ensure(3 * V)) || (st = ft->mesh_n.ensure(3 * V)) || (st = ft->faces4.ensure(F)) ||
@@ -683,11 +684,12 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	ft->E = E;
 	ft->n0 = wf->h.layer_counts.empty() ? N : wf->h.layer_counts[0];
 	if (E > 0) {
-		const int n0 = ft->n0, m = 6 * (N - n0), ld = corner_ld(m);
+		const int n0 = ft->n0, m = 6 * (N - n0);
+		if ((st = ft->corner.prepare(wf->h.edges.data(), E, n0, N))) return st;
 		if ((st = ft->wing.ensure(static_cast<size_t>(E) * 36)) || (st = ft->edge_residuals.ensure(3 * static_cast<size_t>(E))) ||
 		    (st = ft->a_diag.ensure(static_cast<size_t>(N) * 36)) || (st = ft->a_dinv.ensure(static_cast<size_t>(n0) * 36)) ||
-		    (st = ft->a_dinvb.ensure(static_cast<size_t>(E) * 36)) || (st = ft->a_schur.ensure(static_cast<size_t>(ld) * ld)) ||
-		    (st = ft->edge_jr.ensure(static_cast<size_t>(E) * EDGE_TERMS)) || (st = ft->a_cb.ensure(static_cast<size_t>(ld))) ||
+		    (st = ft->a_dinvb.ensure(static_cast<size_t>(E) * 36)) ||
+		    (st = ft->edge_jr.ensure(static_cast<size_t>(E) * EDGE_TERMS)) ||
 		    (st = ft->a_rhs.ensure(6 * static_cast<size_t>(N))) || (st = ft->a_x.ensure(6 * static_cast<size_t>(N))) ||
 		    (st = ft->a_offsets.ensure(n0 + 1)) || (st = ft->a_list.ensure(E)))
 			return st;
@@ -736,18 +738,16 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 		ft->aw.n0 = n0;
 		ft->aw.E = E;
 		ft->aw.m = m;
-		ft->aw.ld = ld;
-		ft->aw.cb = ft->a_cb.ptr;
+		ft->aw.corner = &ft->corner;
 		ft->aw.diag = ft->a_diag.ptr;
 		ft->aw.dinv = ft->a_dinv.ptr;
 		ft->aw.dinv_b = ft->a_dinvb.ptr;
-		ft->aw.schur = ft->a_schur.ptr;
 		ft->aw.rhs = ft->a_rhs.ptr;
 		ft->aw.x = ft->a_x.ptr;
 		ft->aw.edge_offsets = ft->a_offsets.ptr;
 		ft->aw.edge_list = ft->a_list.ptr;
 	}
-	const auto after = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->a_schur.ptr,
+	const auto after = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->corner.generation,
 	                                   ft->face_nodes.ptr, ft->wpos.ptr);
 	// Captured graphs bake every buffer pointer and the per-frame constants (NDC setup, pixel camera, extrinsics) into
 	// their kernel arguments: any change drops them. The warp field is recognised by its unique id, not its address.
@@ -1504,6 +1504,12 @@ nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, cons
 		NNRT_HIP(hipMemcpyAsync(coords.data(), d_coords, sizeof(int32_t) * 2 * E, hipMemcpyDeviceToHost, s));
 		NNRT_HIP(hipStreamSynchronize(s));
 	}
+	for (int e = 0; e < E; e++) {   // before any allocation: the host lists below index by these
+		const int i = coords[2 * e], j = coords[2 * e + 1];
+		NNRT_CHECK_ARG(i >= 0 && i < N && j >= 0 && j < N, "wing block coordinate outside [0, diagonal_block_count)");
+		NNRT_CHECK_ARG(i != j, "wing block on the block diagonal");
+		NNRT_CHECK_ARG(j >= n0, "wing block column inside the arrow stem (the stem is block-diagonal)");
+	}
 	std::vector<int> counts(n0 + 1, 0), list(std::max(E, 1)), fill;
 	for (int e = 0; e < E; e++)
 		if (coords[2 * e] < n0) counts[coords[2 * e] + 1]++;
@@ -1511,17 +1517,18 @@ nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, cons
 	fill.assign(counts.begin(), counts.end() - 1);
 	for (int e = 0; e < E; e++)
 		if (coords[2 * e] < n0) list[fill[coords[2 * e]]++] = e;
+	CornerSolver corner;
+	nnrt_status st = corner.prepare(coords.data(), E, n0, N);
+	if (st) return st;
 	ArrowheadWorkspace ws;
 	ws.N = N;
 	ws.n0 = n0;
 	ws.E = E;
 	ws.m = 6 * (N - n0);
-	ws.ld = corner_ld(ws.m);
+	ws.corner = &corner;
 	int* flag = nullptr;
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.dinv), sizeof(float) * 36 * std::max(n0, 1), s));
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.dinv_b), sizeof(float) * 36 * std::max(E, 1), s));
-	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.schur), sizeof(float) * std::max<int64_t>(static_cast<int64_t>(ws.ld) * ws.ld, 1), s));
-	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.cb), sizeof(float) * std::max(ws.ld, 1), s));
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.edge_offsets), sizeof(int) * (n0 + 1), s));
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.edge_list), sizeof(int) * std::max(E, 1), s));
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&flag), sizeof(int), s));
@@ -1544,14 +1551,13 @@ nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, cons
 	ws.diag = const_cast<float*>(d_diag);
 	ws.rhs = const_cast<float*>(d_b);
 	ws.x = d_x;
-	nnrt_status st = arrowhead_solve_core(ws, d_coords, d_wing, flag, s);
+	st = arrowhead_solve_core(ws, d_coords, d_wing, flag, s);
 	int host_flag = 0;
 	if (!st) {
 		NNRT_HIP(hipMemcpyAsync(&host_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
 		NNRT_HIP(hipStreamSynchronize(s));
 	}
-	for (void* p : {static_cast<void*>(ws.dinv), static_cast<void*>(ws.dinv_b), static_cast<void*>(ws.schur),
-	                static_cast<void*>(ws.cb), static_cast<void*>(ws.tgt_off), static_cast<void*>(ws.tgt_ab), static_cast<void*>(ws.pairs),
+	for (void* p : {static_cast<void*>(ws.dinv), static_cast<void*>(ws.dinv_b), static_cast<void*>(ws.tgt_off), static_cast<void*>(ws.tgt_ab), static_cast<void*>(ws.pairs),
 	                static_cast<void*>(ws.rhs_off), static_cast<void*>(ws.rhs_edges), static_cast<void*>(ws.edge_offsets),
 	                static_cast<void*>(ws.edge_list), static_cast<void*>(flag)})
 		hipFreeAsync(p, s);

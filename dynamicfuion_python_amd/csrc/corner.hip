@@ -1,0 +1,810 @@
+// Schur corner of the arrowhead solve: tile-sparse supernodal Cholesky (SolveBlockSparseArrowheadCholesky.cpp:30-95
+// factors S = C - B^T D^-1 B with a dense potrf; SolveCholesky{CPU,CUDA}.cpp). The corner of a deformation-graph hierarchy
+// is the Schur complement of a 2-D node grid: every corner node couples only to the corner nodes it shares a stem node
+// with (and to its own corner edges, >= 3 layers), so S and its factor are sparse. Here:
+//
+//   host (once per hierarchy, CornerSolver::prepare): nested-dissection order of the corner nodes (BFS level-set
+//   separators, leaves of ND_LEAF nodes), every ND group starting on a 64-unknown tile boundary (identity padding), the
+//   tile structure of L (symbolic factorisation over the tile elimination tree) and its levels (tile columns whose
+//   subtrees are independent share a level);
+//   device: one launch per level (k_corner_factor). Its panel workgroups factor the level's tile columns -- each stages
+//   its diagonal tile and its panel tile with the updates of the previous level's columns applied (f32 MFMA), then one
+//   wave eliminates the 64 columns in registers (L_JJ and L_IJ = A_IJ L_JJ^-T in one pass, the right-hand side riding
+//   along as the diagonal workgroup's augmented row); its trailing workgroups apply the previous level's updates to
+//   every later structurally non-zero tile. Back substitution runs one launch per level from the root down
+//   (k_corner_back). Only structurally non-zero tiles are stored (slot-major 64 x 64 tiles).
+//
+// Race freedom: a launch reads only tiles finished by earlier launches and writes tiles no other workgroup of the same
+// launch reads: the diagonal factor L_JJ goes to its own array (ldiag), never over A_JJ, which the column's other panel
+// workgroups stage concurrently. Nothing depends on workgroup co-residency or dispatch order; the corner size is bounded
+// by memory only.
+//
+// Numerics: the same float operations per tile as a right-looking blocked Cholesky (MFMA tile products, column
+// eliminations in ascending order); the elimination order (nested dissection) differs from the reference's natural
+// order, which changes float rounding only (the tests hold the solve against the oracle and an fp64 solution).
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <tuple>
+
+#include "fitter_kernels.hpp"
+
+namespace nnrt {
+
+constexpr int CT = 256;                       // threads per workgroup of the corner kernels
+constexpr int TILE = CORNER_NB;               // 64
+constexpr int TILE_ELEMS = TILE * TILE;
+constexpr int CS4 = TILE + 4;                 // LDS row stride of staged tiles (16-B aligned rows for ds_read_b128)
+constexpr int ND_LEAF = 42;                   // nodes per nested-dissection leaf: 252 unknowns = four tiles
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ===================================================================================================================
+// host: ordering, symbolic factorisation, launch plan
+// ===================================================================================================================
+namespace {
+
+struct Dissection {
+	const std::vector<std::vector<int>>* adj = nullptr;
+	std::vector<int> sub, vis, level;   // epoch marks: subset membership, BFS visit
+	int epoch = 0;
+	std::vector<std::vector<int>> groups;   // elimination order: leaves and separators, post-order
+
+	// BFS inside the subset marked `sep` from src; returns the visit order, level[] of every visited node
+	void bfs(int sep, int src, std::vector<int>& order) {
+		const int vep = ++epoch;
+		order.clear();
+		order.push_back(src);
+		vis[src] = vep;
+		level[src] = 0;
+		for (size_t h = 0; h < order.size(); h++) {
+			const int u = order[h];
+			for (int v : (*adj)[u])
+				if (sub[v] == sep && vis[v] != vep) {
+					vis[v] = vep;
+					level[v] = level[u] + 1;
+					order.push_back(v);
+				}
+		}
+	}
+
+	void leaf(std::vector<int> nodes) {
+		std::sort(nodes.begin(), nodes.end());
+		if (!nodes.empty()) groups.push_back(std::move(nodes));
+	}
+
+	void dissect(std::vector<int> nodes) {
+		if (static_cast<int>(nodes.size()) <= ND_LEAF) return leaf(std::move(nodes));
+		std::sort(nodes.begin(), nodes.end());
+		const int sep = ++epoch;
+		for (int u : nodes) sub[u] = sep;
+		// connected components (in ascending order of their smallest node)
+		std::vector<std::vector<int>> comps;
+		{
+			const int cep = ++epoch;
+			std::vector<int> order;
+			for (int u : nodes) {
+				if (vis[u] == cep) continue;
+				bfs(sep, u, order);
+				for (int v : order) vis[v] = cep;
+				comps.push_back(order);
+			}
+		}
+		if (comps.size() > 1) {   // independent subtrees; small components share leaves (no false coupling: same chain)
+			std::vector<int> small;
+			for (auto& c : comps) {
+				if (static_cast<int>(c.size()) > ND_LEAF) {
+					dissect(std::move(c));
+					continue;
+				}
+				if (small.size() + c.size() > static_cast<size_t>(ND_LEAF)) {
+					leaf(std::move(small));
+					small.clear();
+				}
+				small.insert(small.end(), c.begin(), c.end());
+			}
+			leaf(std::move(small));
+			return;
+		}
+		// pseudo-peripheral start: repeated BFS from the farthest node while the eccentricity grows
+		std::vector<int> order;
+		int start = nodes.front();
+		bfs(sep, start, order);
+		int ecc = level[order.back()];
+		for (int it = 0; it < 4; it++) {
+			const int far = order.back();
+			std::vector<int> o2;
+			bfs(sep, far, o2);
+			if (level[o2.back()] <= ecc) break;
+			ecc = level[o2.back()];
+			start = far;
+			order.swap(o2);
+		}
+		bfs(sep, start, order);
+		const int L = level[order.back()];
+		if (L < 2) return leaf(std::move(nodes));
+		// separator: the BFS level at which the cumulative count first reaches half the nodes (level sets separate)
+		std::vector<int> cnt(static_cast<size_t>(L) + 1, 0);
+		for (int u : nodes) cnt[static_cast<size_t>(level[u])]++;
+		int s = 0, cum = 0;
+		for (; s <= L; s++) {
+			cum += cnt[static_cast<size_t>(s)];
+			if (2 * cum >= static_cast<int>(nodes.size())) break;
+		}
+		s = std::min(std::max(s, 1), L - 1);
+		std::vector<int> left, right, mid;
+		for (int u : nodes) (level[u] < s ? left : level[u] > s ? right : mid).push_back(u);
+		dissect(std::move(left));
+		dissect(std::move(right));
+		leaf(std::move(mid));
+	}
+};
+
+} // namespace
+
+struct CornerPlan {
+	int nc = 0, ld = 0, T = 0, H = 0;
+	std::vector<int> node_row;        // [nc] first (permuted) unknown of each corner node
+	std::vector<int> row_node;        // [ld] 8 * node + component, -1 on identity padding
+	std::vector<int> tile_slot;       // [T * T] slot of tile (I, J), I >= J; -1: structurally zero
+	std::vector<int2> slot_ij;        // [slots] (I, J)
+	std::vector<int> level_off, level_panel;   // [H + 1] task offsets per factor launch, [H] panel tasks first
+	std::vector<CornerTask> tasks;
+	std::vector<int4> srcs;           // (slot X, slot Y, column k, 0): X Y^T update terms; rhs term L_k y_k uses X and k
+	std::vector<int> back_off;        // [H + 1] back-substitution columns per level
+	std::vector<int4> back_cols;      // (J, entry offset, entry count, 0)
+	std::vector<int2> back_ent;       // (slot of L_IJ, I)
+	std::vector<int> corner_edges;    // edges between two corner nodes (>= 3 layers)
+};
+
+static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N) {
+	CornerPlan p;
+	const int nc = N - n0;
+	p.nc = nc;
+	if (nc <= 0) return p;
+	// corner adjacency: corner edges + pairs of corner nodes sharing a stem node (the Schur fill B^T D^-1 B)
+	std::vector<std::vector<int>> adj(static_cast<size_t>(nc)), stem_targets(static_cast<size_t>(std::max(n0, 0)));
+	for (int e = 0; e < E; e++) {
+		const int i = edges[2 * e], j = edges[2 * e + 1];
+		if (i >= n0) {
+			adj[static_cast<size_t>(i - n0)].push_back(j - n0);
+			adj[static_cast<size_t>(j - n0)].push_back(i - n0);
+			p.corner_edges.push_back(e);
+		} else {
+			stem_targets[static_cast<size_t>(i)].push_back(j - n0);
+		}
+	}
+	for (auto& ts : stem_targets)
+		for (int a : ts)
+			for (int b : ts)
+				if (a != b) adj[static_cast<size_t>(a)].push_back(b);
+	for (auto& a : adj) {
+		std::sort(a.begin(), a.end());
+		a.erase(std::unique(a.begin(), a.end()), a.end());
+	}
+	// nested dissection
+	Dissection nd;
+	nd.adj = &adj;
+	nd.sub.assign(static_cast<size_t>(nc), 0);
+	nd.vis.assign(static_cast<size_t>(nc), 0);
+	nd.level.assign(static_cast<size_t>(nc), 0);
+	{
+		std::vector<int> all(static_cast<size_t>(nc));
+		for (int a = 0; a < nc; a++) all[static_cast<size_t>(a)] = a;
+		nd.dissect(std::move(all));
+	}
+	// layout: every group starts on a tile boundary
+	p.node_row.assign(static_cast<size_t>(nc), -1);
+	int off = 0;
+	for (const auto& g : nd.groups) {
+		off = (off + TILE - 1) / TILE * TILE;
+		for (int a : g) {
+			p.node_row[static_cast<size_t>(a)] = off;
+			off += 6;
+		}
+	}
+	p.ld = (off + TILE - 1) / TILE * TILE;
+	const int T = p.T = p.ld / TILE;
+	p.row_node.assign(static_cast<size_t>(p.ld), -1);
+	for (int a = 0; a < nc; a++)
+		for (int c = 0; c < 6; c++) p.row_node[static_cast<size_t>(p.node_row[static_cast<size_t>(a)] + c)] = 8 * a + c;
+	// initial tile structure (strictly lower tiles per column), then the symbolic factorisation over the elimination tree
+	std::vector<std::vector<int>> cs(static_cast<size_t>(T));   // cs[J]: rows I > J of column J's non-zero tiles
+	for (int a = 0; a < nc; a++) {
+		const int ra = p.node_row[static_cast<size_t>(a)];
+		for (int b : adj[static_cast<size_t>(a)]) {
+			const int rb = p.node_row[static_cast<size_t>(b)];
+			for (int ti = ra / TILE; ti <= (ra + 5) / TILE; ti++)
+				for (int tj = rb / TILE; tj <= (rb + 5) / TILE; tj++)
+					if (ti > tj) cs[static_cast<size_t>(tj)].push_back(ti);
+		}
+		if (ra / TILE != (ra + 5) / TILE) cs[static_cast<size_t>(ra / TILE)].push_back((ra + 5) / TILE);   // a node straddling two tiles
+	}
+	std::vector<int> parent(static_cast<size_t>(T), -1), lvl(static_cast<size_t>(T), 0);
+	for (int J = 0; J < T; J++) {
+		auto& c = cs[static_cast<size_t>(J)];
+		std::sort(c.begin(), c.end());
+		c.erase(std::unique(c.begin(), c.end()), c.end());
+		if (c.empty()) continue;
+		const int par = c.front();
+		parent[static_cast<size_t>(J)] = par;
+		auto& pc = cs[static_cast<size_t>(par)];
+		pc.insert(pc.end(), c.begin() + 1, c.end());
+	}
+	for (int J = 0; J < T; J++)
+		if (parent[static_cast<size_t>(J)] >= 0)
+			lvl[static_cast<size_t>(parent[static_cast<size_t>(J)])] =
+			    std::max(lvl[static_cast<size_t>(parent[static_cast<size_t>(J)])], lvl[static_cast<size_t>(J)] + 1);
+	p.H = 0;
+	for (int J = 0; J < T; J++) p.H = std::max(p.H, lvl[static_cast<size_t>(J)] + 1);
+	// slots: per column its diagonal tile, then its panel tiles
+	p.tile_slot.assign(static_cast<size_t>(T) * T, -1);
+	for (int J = 0; J < T; J++) {
+		p.tile_slot[static_cast<size_t>(J) * T + J] = static_cast<int>(p.slot_ij.size());
+		p.slot_ij.push_back(make_int2(J, J));
+		for (int I : cs[static_cast<size_t>(J)]) {
+			p.tile_slot[static_cast<size_t>(I) * T + J] = static_cast<int>(p.slot_ij.size());
+			p.slot_ij.push_back(make_int2(I, J));
+		}
+	}
+	auto slot = [&](int I, int J) { return p.tile_slot[static_cast<size_t>(I) * T + J]; };
+	// update terms: column k contributes L_Ik L_Jk^T to every tile (I, J), I >= J in its structure, applied at launch
+	// lvl[k] + 1 -- by the panel of column J if J sits at that level, else by a trailing workgroup
+	std::map<std::tuple<int, int, int>, std::vector<int>> contrib;   // (launch, J, I) -> columns k, ascending
+	for (int k = 0; k < T; k++) {
+		const auto& c = cs[static_cast<size_t>(k)];
+		for (size_t x = 0; x < c.size(); x++)
+			for (size_t y = 0; y <= x; y++) contrib[std::make_tuple(lvl[static_cast<size_t>(k)] + 1, c[y], c[x])].push_back(k);
+	}
+	auto terms = [&](int launch, int J, int I) -> const std::vector<int>* {
+		auto it = contrib.find(std::make_tuple(launch, J, I));
+		return it == contrib.end() ? nullptr : &it->second;
+	};
+	p.level_off.push_back(0);
+	for (int l = 0; l < p.H; l++) {
+		int panels = 0;
+		for (int J = 0; J < T; J++) {
+			if (lvl[static_cast<size_t>(J)] != l) continue;
+			const std::vector<int>* dterms = terms(l, J, J);
+			std::vector<int> rows(1, J);
+			rows.insert(rows.end(), cs[static_cast<size_t>(J)].begin(), cs[static_cast<size_t>(J)].end());
+			for (int I : rows) {
+				CornerTask t{};
+				t.I = I;
+				t.J = J;
+				t.slot_t = slot(I, J);
+				t.slot_d = slot(J, J);
+				t.src = static_cast<int>(p.srcs.size());
+				if (dterms)
+					for (int k : *dterms) p.srcs.push_back(make_int4(slot(J, k), slot(J, k), k, 0));
+				t.nd = dterms ? static_cast<int>(dterms->size()) : 0;
+				if (I != J) {
+					const std::vector<int>* pterms = terms(l, J, I);
+					if (pterms)
+						for (int k : *pterms) p.srcs.push_back(make_int4(slot(I, k), slot(J, k), k, 0));
+					t.np = pterms ? static_cast<int>(pterms->size()) : 0;
+				}
+				p.tasks.push_back(t);
+				panels++;
+			}
+		}
+		p.level_panel.push_back(panels);
+		for (auto it = contrib.lower_bound(std::make_tuple(l, -1, -1)); it != contrib.end() && std::get<0>(it->first) == l; ++it) {
+			const int J = std::get<1>(it->first), I = std::get<2>(it->first);
+			if (lvl[static_cast<size_t>(J)] == l) continue;   // the panel's own staging
+			CornerTask t{};
+			t.I = I;
+			t.J = J;
+			t.slot_t = slot(I, J);
+			t.slot_d = -1;
+			t.src = static_cast<int>(p.srcs.size());
+			for (int k : it->second) p.srcs.push_back(make_int4(slot(I, k), slot(J, k), k, 0));
+			t.nd = static_cast<int>(it->second.size());
+			p.tasks.push_back(t);
+		}
+		p.level_off.push_back(static_cast<int>(p.tasks.size()));
+	}
+	// back substitution: per level, each column with its panel tiles (I, J), I > J
+	p.back_off.push_back(0);
+	for (int l = 0; l < p.H; l++) {
+		for (int J = 0; J < T; J++) {
+			if (lvl[static_cast<size_t>(J)] != l) continue;
+			const auto& c = cs[static_cast<size_t>(J)];
+			p.back_cols.push_back(make_int4(J, static_cast<int>(p.back_ent.size()), static_cast<int>(c.size()), 0));
+			for (int I : c) p.back_ent.push_back(make_int2(slot(I, J), I));
+		}
+		p.back_off.push_back(static_cast<int>(p.back_cols.size()));
+	}
+	return p;
+}
+
+// ===================================================================================================================
+// device
+// ===================================================================================================================
+__device__ inline float lane_bcast(float v, int src) {
+	return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
+}
+
+// corner init: every stored tile gets its entries of C (the corner nodes' diagonal blocks) and the identity on the
+// padding; cb = b_C in the permuted order. One thread per 4 consecutive entries of a tile row (one 16-B store).
+__global__ void k_corner_init(int n0, int ld, int slots, const int2* __restrict__ slot_ij, const int* __restrict__ row_node,
+                              const float* __restrict__ diag, const float* __restrict__ rhs, float* __restrict__ tiles, float* __restrict__ cb) {
+	const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (idx < ld) {
+		const int rn = row_node[idx];
+		cb[idx] = rn >= 0 ? rhs[6 * static_cast<int64_t>(n0 + (rn >> 3)) + (rn & 7)] : 0.f;
+	}
+	if (idx >= static_cast<int64_t>(slots) * (TILE_ELEMS / 4)) return;
+	const int s = static_cast<int>(idx / (TILE_ELEMS / 4)), w = static_cast<int>(idx % (TILE_ELEMS / 4));
+	const int r = w / (TILE / 4), c0 = (w % (TILE / 4)) * 4;
+	const int2 ij = slot_ij[s];
+	const int R = ij.x * TILE + r;
+	const int rn = row_node[R];
+	float v[4];
+#pragma unroll
+	for (int j = 0; j < 4; j++) {
+		const int C = ij.y * TILE + c0 + j;
+		const int cn = row_node[C];
+		v[j] = 0.f;
+		if (rn >= 0 && cn >= 0) {
+			if ((rn >> 3) == (cn >> 3)) v[j] = diag[static_cast<int64_t>(n0 + (rn >> 3)) * 36 + 6 * (rn & 7) + (cn & 7)];
+		} else if (R == C) {
+			v[j] = 1.f;
+		}
+	}
+	*reinterpret_cast<float4*>(tiles + static_cast<int64_t>(s) * TILE_ELEMS + r * TILE + c0) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// corner off-diagonal blocks (edges between two corner nodes, >= 3 layers; the reference drops them, A3): each entry of
+// the wing block is added once, at its lower-triangle position (S is symmetric)
+__global__ void k_corner_offdiag(const int* __restrict__ corner_edges, int n0, const int32_t* __restrict__ edges, const float* __restrict__ wing,
+                                 CornerMap m) {
+	const int e = corner_edges[blockIdx.x];
+	const int t = threadIdx.x;
+	if (t >= 36) return;
+	const int a = edges[2 * e] - n0, b = edges[2 * e + 1] - n0;
+	int R = m.node_row[a] + t / 6, C = m.node_row[b] + t % 6;
+	if (R < C) {
+		const int x = R;
+		R = C;
+		C = x;
+	}
+	atomicAdd(corner_entry(m, R, C), wing[static_cast<int64_t>(e) * 36 + t]);
+}
+
+// 32 x 32 quadrant (qr, qc) of X Y^T for 64 x 64 row-major tiles X, Y at row stride ld (lane l feeds
+// A[i = l & 31][k'] = X[32 qr + i][32 (l >> 5) + s] and B[k'][j] = Y[32 qc + j][32 (l >> 5) + s] to MFMA step s, so the 32
+// steps x 2 lane halves cover the 64-wide k range; each lane reads 32 contiguous floats). C/D map: column l & 31, row
+// (v & 3) + 8 (v >> 2) + 4 (l >> 5).
+__device__ inline f32x16 quadrant_xyt(const float* X, const float* Y, int64_t ld, int qr, int qc, int lane, f32x16 acc) {
+	const int half = lane >> 5, l32 = lane & 31;
+	const float4* x4 = reinterpret_cast<const float4*>(X + (32 * qr + l32) * ld + 32 * half);
+	const float4* y4 = reinterpret_cast<const float4*>(Y + (32 * qc + l32) * ld + 32 * half);
+	float4 vx[8], vy[8];
+#pragma unroll
+	for (int q = 0; q < 8; q++) {
+		vx[q] = x4[q];
+		vy[q] = y4[q];
+	}
+#pragma unroll
+	for (int q = 0; q < 8; q++) {
+		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].x, vy[q].x, acc, 0, 0, 0);
+		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].y, vy[q].y, acc, 0, 0, 0);
+		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].z, vy[q].z, acc, 0, 0, 0);
+		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].w, vy[q].w, acc, 0, 0, 0);
+	}
+	return acc;
+}
+
+__device__ inline int quad_row(int v, int lane) { return (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5); }
+
+// sum over the update terms of X Y^T for this wave's quadrant
+__device__ inline f32x16 sum_updates(const float* tiles, const int4* src, int n, int qr, int qc, int lane) {
+	f32x16 acc = {};
+	for (int e = 0; e < n; e++) {
+		const int4 s = src[e];
+		acc = quadrant_xyt(tiles + static_cast<int64_t>(s.x) * TILE_ELEMS, tiles + static_cast<int64_t>(s.y) * TILE_ELEMS, TILE, qr, qc, lane, acc);
+	}
+	return acc;
+}
+
+// s_t = A - sum X Y^T for the workgroup's quadrant of the 64 x 64 tile A (LDS, row stride CS4)
+__device__ inline void stage_tile(const float* tiles, const float* A, const int4* src, int n, int wave, int lane, float* s_t) {
+	const int qr = wave >> 1, qc = wave & 1;
+	float tv[16];
+#pragma unroll
+	for (int v = 0; v < 16; v++) tv[v] = A[(32 * qr + quad_row(v, lane)) * TILE + 32 * qc + (lane & 31)];
+	const f32x16 acc = sum_updates(tiles, src, n, qr, qc, lane);
+#pragma unroll
+	for (int v = 0; v < 16; v++) s_t[(32 * qr + quad_row(v, lane)) * CS4 + 32 * qc + (lane & 31)] = tv[v] - acc[v];
+}
+
+// (L y) row t >> 2 for a 64 x 64 tile L and the 64-vector y: 4 threads per row, 16 columns each (all 4 get the sum)
+__device__ inline float rhs_row_update(const float* L, const float* y, int t) {
+	const int r = t >> 2, q4 = t & 3;
+	const float* Lr = L + r * TILE + 16 * q4;
+	const float* yq = y + 16 * q4;
+	float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+	for (int c = 0; c < 16; c += 2) {
+		s0 += Lr[c] * yq[c];
+		s1 += Lr[c + 1] * yq[c + 1];
+	}
+	float s = s0 + s1;
+	s += __shfl_xor(s, 1);
+	s += __shfl_xor(s, 2);
+	return s;
+}
+
+__device__ inline float rhs_updates(const float* tiles, const int4* src, int n, const float* cb, int t) {
+	float s = 0.f;
+	for (int e = 0; e < n; e++) {
+		const int4 q = src[e];
+		s += rhs_row_update(tiles + static_cast<int64_t>(q.x) * TILE_ELEMS, cb + static_cast<int64_t>(q.z) * TILE, t);
+	}
+	return s;
+}
+
+// Column eliminations J0 <= j < J1 of the row pairs ap (lane = row), applied to the columns c < J1 only, in blocks of
+// four: the four columns are factored among themselves, then applied to every later column c with four packed FMAs
+// whose multipliers L_c,jb..jb+3 are read from lane c by readlane (scalar operands: nothing on the elimination path
+// waits on LDS). Every element sees its updates in ascending column order.
+template <int J0, int J1>
+__device__ inline void eliminate_columns(f32x2 (&ap)[TILE], int lane, int& bad) {
+	__shared__ float4 s_l4[2][TILE];   // s_l4[.][c] = (L_c,jb .. L_c,jb+3)
+#pragma clang loop unroll(full)
+	for (int jb = J0; jb < J1; jb += 4) {
+		// The 4 x 4 diagonal sub-block is read once (10 independent readlanes) and factored wave-uniformly; every lane
+		// then runs the same operations on its own row with the uniform multipliers (the values lanes jb..jb+3 compute).
+		float M[4][4], Lu[4][4], rsv[4];
+#pragma unroll
+		for (int q = 0; q < 4; q++)
+#pragma unroll
+			for (int i = q; i < 4; i++) M[i][q] = lane_bcast(ap[jb + q].x, jb + i);
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			float piv = M[q][q];   // A_jj after the first j eliminations
+			bad |= !(piv > 0.f);
+			piv = piv > 0.f ? piv : 1.f;
+			rsv[q] = __builtin_amdgcn_rsqf(piv);
+#pragma unroll
+			for (int i = q; i < 4; i++) Lu[i][q] = M[i][q] * rsv[q];
+#pragma unroll
+			for (int q2 = q + 1; q2 < 4; q2++)
+#pragma unroll
+				for (int i = q2; i < 4; i++) M[i][q2] = __builtin_fmaf(-Lu[i][q], Lu[q2][q], M[i][q2]);
+		}
+		float lx[4];
+		f32x2 nl[4];
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			const f32x2 l = ap[jb + q] * rsv[q];   // (L_rj for rows r >= j of the diagonal block, panel / rhs entry)
+			ap[jb + q] = l;
+			lx[q] = l.x;
+			nl[q] = -l;
+#pragma unroll
+			for (int q2 = q + 1; q2 < 4; q2++) {
+				const float lc = Lu[q2][q];
+				ap[jb + q2] = __builtin_elementwise_fma(nl[q], f32x2{lc, lc}, ap[jb + q2]);
+			}
+		}
+		// next block's columns first (readlane: on the pivot chain), the rest from a wave-uniform 16-B LDS broadcast
+		// whose latency hides behind them
+		float4* row = &s_l4[(jb >> 2) & 1][0];
+		if (jb + 8 < J1) row[lane] = make_float4(lx[0], lx[1], lx[2], lx[3]);
+#pragma unroll
+		for (int q = 0; q < 4; q++)   // q outer: consecutive FMAs are independent
+#pragma unroll
+			for (int c = jb + 4; c < J1 && c < jb + 8; c++) {
+				const float lc = lane_bcast(lx[q], c);   // L_c,jb+q, c > jb + 3
+				ap[c] = __builtin_elementwise_fma(nl[q], f32x2{lc, lc}, ap[c]);
+			}
+#pragma unroll
+		for (int c0 = jb + 8; c0 < J1; c0 += 8) {   // chunks of 8 columns: 8 broadcasts in flight
+			float4 L4[8];
+#pragma unroll
+			for (int u = 0; u < 8; u++)
+				if (c0 + u < J1) L4[u] = row[c0 + u];
+#pragma unroll
+			for (int u = 0; u < 8; u++)
+				if (c0 + u < J1) ap[c0 + u] = __builtin_elementwise_fma(nl[0], f32x2{L4[u].x, L4[u].x}, ap[c0 + u]);
+#pragma unroll
+			for (int u = 0; u < 8; u++)
+				if (c0 + u < J1) ap[c0 + u] = __builtin_elementwise_fma(nl[1], f32x2{L4[u].y, L4[u].y}, ap[c0 + u]);
+#pragma unroll
+			for (int u = 0; u < 8; u++)
+				if (c0 + u < J1) ap[c0 + u] = __builtin_elementwise_fma(nl[2], f32x2{L4[u].z, L4[u].z}, ap[c0 + u]);
+#pragma unroll
+			for (int u = 0; u < 8; u++)
+				if (c0 + u < J1) ap[c0 + u] = __builtin_elementwise_fma(nl[3], f32x2{L4[u].w, L4[u].w}, ap[c0 + u]);
+		}
+	}
+}
+
+struct CornerFactorArgs {
+	float* tiles;            // [slots, 64, 64]
+	float* ldiag;            // [T, 64, 64] L_JJ (lower; zero above the diagonal)
+	float* cb;               // [ld] b_C -> y (forward substitution)
+	const CornerTask* tasks; // this launch's tasks, panels first
+	const int4* srcs;
+	int n_panel;
+	int* error_flag;
+};
+
+// One launch per level of the tile elimination tree.
+//   panel (I, J) (blockIdx < n_panel): s_d = A_JJ - sum_k L_Jk L_Jk^T and s_p = A_IJ - sum_k L_Ik L_Jk^T over the columns k of
+//   the previous level (MFMA, one 32 x 32 quadrant per wave, into LDS); the diagonal workgroup stages b_J - sum_k L_Jk y_k
+//   as its augmented row. Wave 0 then holds both (lane = row) in registers and runs the 64 column eliminations of A_JJ,
+//   applying each to the panel row as it goes (one packed FMA per column pair), in two 32-column halves joined by a
+//   rank-32 MFMA update on the other three waves.
+//   trailing (blockIdx >= n_panel): A_IJ -= sum_k L_Ik L_Jk^T (and b_J -= sum_k L_Jk y_k on diagonal tiles).
+__global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
+	__shared__ float s_d[TILE * CS4];   // A_JJ after the previous level's updates
+	__shared__ float s_p[TILE * CS4];   // A_IJ after the previous level's updates (panel workgroups below the diagonal)
+	__shared__ float s_b[TILE];         // b_J after the previous level's updates (diagonal workgroup)
+	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+	const CornerTask tk = a.tasks[blockIdx.x];
+	const int4* src = a.srcs + tk.src;
+	if (static_cast<int>(blockIdx.x) >= a.n_panel) {
+		const int qr = wave >> 1, qc = wave & 1;
+		float* C = a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS + 32 * qc + (lane & 31);
+		float cv[16];
+#pragma unroll
+		for (int v = 0; v < 16; v++) cv[v] = C[(32 * qr + quad_row(v, lane)) * TILE];
+		const f32x16 acc = sum_updates(a.tiles, src, tk.nd, qr, qc, lane);
+#pragma unroll
+		for (int v = 0; v < 16; v++) C[(32 * qr + quad_row(v, lane)) * TILE] = cv[v] - acc[v];
+		if (tk.I == tk.J) {
+			float* bj = a.cb + static_cast<int64_t>(tk.J) * TILE;
+			const float bv = (t & 3) == 0 ? bj[t >> 2] : 0.f;
+			const float s = rhs_updates(a.tiles, src, tk.nd, a.cb, t);
+			if ((t & 3) == 0) bj[t >> 2] = bv - s;
+		}
+		return;
+	}
+	const bool diag = tk.I == tk.J;
+	stage_tile(a.tiles, a.tiles + static_cast<int64_t>(tk.slot_d) * TILE_ELEMS, src, tk.nd, wave, lane, s_d);
+	if (!diag) {
+		stage_tile(a.tiles, a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS, src + tk.nd, tk.np, wave, lane, s_p);
+	} else {
+		const float s = rhs_updates(a.tiles, src, tk.nd, a.cb, t);
+		if ((t & 3) == 0) s_b[t >> 2] = a.cb[static_cast<int64_t>(tk.J) * TILE + (t >> 2)] - s;
+	}
+	__syncthreads();
+	// ap[c] = (A_JJ[lane][c], A_IJ[lane][c]): both rows see the same column operations, so one packed FMA
+	// (v_pk_fma_f32) updates the pair. Wave 0 holds them; the other waves join for the rank-32 update between the halves.
+	f32x2 ap[TILE];
+	int bad = 0;
+	if (wave == 0) {
+#pragma unroll
+		for (int q = 0; q < TILE / 4; q++) {
+			const float4 va = *reinterpret_cast<const float4*>(s_d + lane * CS4 + 4 * q);
+			float4 vp;
+			if (diag)   // the augmented row: b_J on lane 0, zero elsewhere
+				vp = lane == 0 ? *reinterpret_cast<const float4*>(s_b + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+			else
+				vp = *reinterpret_cast<const float4*>(s_p + lane * CS4 + 4 * q);
+			ap[4 * q] = f32x2{va.x, vp.x};
+			ap[4 * q + 1] = f32x2{va.y, vp.y};
+			ap[4 * q + 2] = f32x2{va.z, vp.z};
+			ap[4 * q + 3] = f32x2{va.w, vp.w};
+		}
+		eliminate_columns<0, TILE / 2>(ap, lane, bad);
+		// L[:, 0:32] of the A_JJ rows and of the panel rows -> LDS (s_d / s_p are free once loaded)
+#pragma unroll
+		for (int q = 0; q < TILE / 8; q++) {
+			*reinterpret_cast<float4*>(s_d + lane * CS4 + 4 * q) = make_float4(ap[4 * q].x, ap[4 * q + 1].x, ap[4 * q + 2].x, ap[4 * q + 3].x);
+			*reinterpret_cast<float4*>(s_p + lane * CS4 + 4 * q) = make_float4(ap[4 * q].y, ap[4 * q + 1].y, ap[4 * q + 2].y, ap[4 * q + 3].y);
+		}
+	}
+	__syncthreads();
+	// rank-32 update of columns 32..63: C = L[rows, 0:32] L_JJ[32:64, 0:32]^T on the MFMA, one 32-row block per wave
+	// (wave 1: A_JJ rows 32..63; waves 2, 3: panel rows 0..31, 32..63; A_JJ rows 0..31 lie above the diagonal there)
+	f32x16 cacc = {};
+	if (wave > 0) {
+		const float* X = wave == 1 ? s_d + 32 * CS4 : s_p + 32 * (wave - 2) * CS4;
+		const int half = lane >> 5, l32 = lane & 31;
+		const float4* x4 = reinterpret_cast<const float4*>(X + l32 * CS4 + 16 * half);
+		const float4* y4 = reinterpret_cast<const float4*>(s_d + (32 + l32) * CS4 + 16 * half);
+#pragma unroll
+		for (int q = 0; q < 4; q++) {
+			const float4 vx = x4[q], vy = y4[q];
+			cacc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx.x, vy.x, cacc, 0, 0, 0);
+			cacc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx.y, vy.y, cacc, 0, 0, 0);
+			cacc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx.z, vy.z, cacc, 0, 0, 0);
+			cacc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx.w, vy.w, cacc, 0, 0, 0);
+		}
+	}
+	__syncthreads();   // every wave is done reading L before the products overwrite it
+	if (wave > 0) {
+		float* Cb = wave == 1 ? s_d + 32 * CS4 : s_p + 32 * (wave - 2) * CS4;
+#pragma unroll
+		for (int v = 0; v < 16; v++) Cb[quad_row(v, lane) * CS4 + 32 + (lane & 31)] = cacc[v];
+	}
+	__syncthreads();
+	if (wave != 0) return;
+#pragma unroll
+	for (int q = TILE / 8; q < TILE / 4; q++) {
+		const float4 ca = lane >= 32 ? *reinterpret_cast<const float4*>(s_d + lane * CS4 + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+		const float4 cp = *reinterpret_cast<const float4*>(s_p + lane * CS4 + 4 * q);
+		ap[4 * q] -= f32x2{ca.x, cp.x};
+		ap[4 * q + 1] -= f32x2{ca.y, cp.y};
+		ap[4 * q + 2] -= f32x2{ca.z, cp.z};
+		ap[4 * q + 3] -= f32x2{ca.w, cp.w};
+	}
+	eliminate_columns<TILE / 2, TILE>(ap, lane, bad);
+	if (diag) {
+		float4* wa = reinterpret_cast<float4*>(a.ldiag + static_cast<int64_t>(tk.J) * TILE_ELEMS + lane * TILE);
+#pragma unroll
+		for (int q = 0; q < TILE / 4; q++)
+			wa[q] = make_float4(4 * q <= lane ? ap[4 * q].x : 0.f, 4 * q + 1 <= lane ? ap[4 * q + 1].x : 0.f,
+			                    4 * q + 2 <= lane ? ap[4 * q + 2].x : 0.f, 4 * q + 3 <= lane ? ap[4 * q + 3].x : 0.f);
+		if (lane == 0) {
+			float4* wb = reinterpret_cast<float4*>(a.cb + static_cast<int64_t>(tk.J) * TILE);
+#pragma unroll
+			for (int q = 0; q < TILE / 4; q++) wb[q] = make_float4(ap[4 * q].y, ap[4 * q + 1].y, ap[4 * q + 2].y, ap[4 * q + 3].y);
+			if (bad) atomicOr(a.error_flag, 1);
+		}
+	} else {
+		float4* wp = reinterpret_cast<float4*>(a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS + lane * TILE);
+#pragma unroll
+		for (int q = 0; q < TILE / 4; q++) wp[q] = make_float4(ap[4 * q].y, ap[4 * q + 1].y, ap[4 * q + 2].y, ap[4 * q + 3].y);
+	}
+}
+
+struct CornerBackArgs {
+	const float* tiles;
+	const float* ldiag;
+	const float* cb;         // y
+	float* xp;               // [ld] x in the permuted order
+	const int* row_node;
+	float* xout;             // [6 nc] x in node order
+	const int4* cols;        // this launch's columns (J, entry offset, count, 0)
+	const int2* ent;         // (slot of L_IJ, I)
+};
+
+// Back substitution L^T x = y for the tile columns of one level (one workgroup each; from the root level down):
+// z = y_J - sum_I L_IJ^T x_I (each wave a quarter of every tile's rows), then x_J = L_JJ^-T z by column-oriented
+// substitution on wave 0 (lane = column; x_r broadcast by readlane).
+__global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
+	__shared__ float s_part[4][TILE];
+	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+	const int4 col = a.cols[blockIdx.x];
+	const int J = col.x;
+	float acc0 = 0.f, acc1 = 0.f;
+	for (int e = 0; e < col.z; e++) {
+		const int2 en = a.ent[col.y + e];
+		const float* L = a.tiles + static_cast<int64_t>(en.x) * TILE_ELEMS + 16 * wave * TILE + lane;
+		const float* xi = a.xp + static_cast<int64_t>(en.y) * TILE + 16 * wave;
+#pragma unroll
+		for (int r = 0; r < 16; r += 2) {
+			acc0 += L[r * TILE] * xi[r];
+			acc1 += L[(r + 1) * TILE] * xi[r + 1];
+		}
+	}
+	s_part[wave][lane] = acc0 + acc1;
+	__syncthreads();
+	if (wave != 0) return;
+	const float* Ld = a.ldiag + static_cast<int64_t>(J) * TILE_ELEMS;
+	float colv[TILE];   // colv[r] = L_JJ[r][lane]
+#pragma unroll
+	for (int r = 0; r < TILE; r++) colv[r] = Ld[r * TILE + lane];
+	const float inv_d = 1.f / Ld[lane * TILE + lane];
+	float z = a.cb[static_cast<int64_t>(J) * TILE + lane] - ((s_part[0][lane] + s_part[1][lane]) + (s_part[2][lane] + s_part[3][lane]));
+	float x = 0.f;
+#pragma unroll
+	for (int r = TILE - 1; r >= 0; r--) {
+		const float xr = lane_bcast(z, r) * lane_bcast(inv_d, r);   // x_r = z_r / L_rr
+		x = lane == r ? xr : x;
+		z -= colv[r] * xr;   // z_c -= L_rc x_r (only c < r matter)
+	}
+	const int64_t row = static_cast<int64_t>(J) * TILE + lane;
+	a.xp[row] = x;
+	const int rn = a.row_node[row];
+	if (rn >= 0) a.xout[6 * static_cast<int64_t>(rn >> 3) + (rn & 7)] = x;
+}
+
+// ===================================================================================================================
+// CornerSolver
+// ===================================================================================================================
+template <typename T>
+static nnrt_status dev_upload(T*& ptr, const std::vector<T>& host) {
+	if (ptr) hipFree(ptr);
+	ptr = nullptr;
+	NNRT_HIP(hipMalloc(reinterpret_cast<void**>(&ptr), sizeof(T) * std::max<size_t>(host.size(), 1)));
+	if (!host.empty()) NNRT_HIP(hipMemcpy(ptr, host.data(), sizeof(T) * host.size(), hipMemcpyHostToDevice));
+	return NNRT_OK;
+}
+
+static void dev_free(void*& p) {
+	if (p) hipFree(p);
+	p = nullptr;
+}
+
+CornerSolver::~CornerSolver() { release(); }
+
+void CornerSolver::release() {
+	for (void** p : {reinterpret_cast<void**>(&tiles), reinterpret_cast<void**>(&ldiag), reinterpret_cast<void**>(&cb),
+	                 reinterpret_cast<void**>(&xp), reinterpret_cast<void**>(&d_tile_slot), reinterpret_cast<void**>(&d_slot_ij),
+	                 reinterpret_cast<void**>(&d_row_node), reinterpret_cast<void**>(&d_node_row), reinterpret_cast<void**>(&d_tasks),
+	                 reinterpret_cast<void**>(&d_srcs), reinterpret_cast<void**>(&d_back_cols), reinterpret_cast<void**>(&d_back_ent),
+	                 reinterpret_cast<void**>(&d_corner_edges)})
+		dev_free(*p);
+	nc = ld = T = H = slots = n_corner_edges = 0;
+	level_off.clear();
+	level_panel.clear();
+	back_off.clear();
+	key.clear();
+}
+
+nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N) {
+	std::vector<int32_t> k(edges, edges + 2 * static_cast<size_t>(E));
+	k.push_back(n0);
+	k.push_back(N);
+	if (k == key && (nc == 0 || tiles)) return NNRT_OK;   // same hierarchy: keep the plan and its buffers
+	release();
+	const CornerPlan p = plan_corner(edges, E, n0, N);
+	nc = p.nc;
+	if (nc > 0) {
+		ld = p.ld;
+		T = p.T;
+		H = p.H;
+		slots = static_cast<int>(p.slot_ij.size());
+		n_corner_edges = static_cast<int>(p.corner_edges.size());
+		NNRT_HIP(hipMalloc(reinterpret_cast<void**>(&tiles), sizeof(float) * static_cast<size_t>(slots) * TILE_ELEMS));
+		NNRT_HIP(hipMalloc(reinterpret_cast<void**>(&ldiag), sizeof(float) * static_cast<size_t>(T) * TILE_ELEMS));
+		NNRT_HIP(hipMalloc(reinterpret_cast<void**>(&cb), sizeof(float) * static_cast<size_t>(ld)));
+		NNRT_HIP(hipMalloc(reinterpret_cast<void**>(&xp), sizeof(float) * static_cast<size_t>(ld)));
+		nnrt_status st;
+		if ((st = dev_upload(d_tile_slot, p.tile_slot)) || (st = dev_upload(d_slot_ij, p.slot_ij)) || (st = dev_upload(d_row_node, p.row_node)) ||
+		    (st = dev_upload(d_node_row, p.node_row)) || (st = dev_upload(d_tasks, p.tasks)) || (st = dev_upload(d_srcs, p.srcs)) ||
+		    (st = dev_upload(d_back_cols, p.back_cols)) || (st = dev_upload(d_back_ent, p.back_ent)) ||
+		    (st = dev_upload(d_corner_edges, p.corner_edges)))
+			return st;
+		level_off = p.level_off;
+		level_panel = p.level_panel;
+		back_off = p.back_off;
+		fill_tiles = static_cast<int64_t>(slots);
+		dense_tiles = static_cast<int64_t>(corner_ld(6 * nc) / TILE) * (corner_ld(6 * nc) / TILE + 1) / 2;
+	}
+	key.swap(k);
+	generation++;
+	return NNRT_OK;
+}
+
+CornerMap CornerSolver::map() const { return CornerMap{T, d_tile_slot, d_node_row, tiles}; }
+
+nnrt_status CornerSolver::launch_init(int n0, const float* diag, const float* rhs, const int32_t* edges, const float* wing, hipStream_t s) const {
+	if (nc == 0) return NNRT_OK;
+	const int64_t threads = std::max<int64_t>(static_cast<int64_t>(slots) * (TILE_ELEMS / 4), ld);
+	k_corner_init<<<static_cast<unsigned>(ceil_div(threads, 256)), 256, 0, s>>>(n0, ld, slots, d_slot_ij, d_row_node, diag, rhs, tiles, cb);
+	NNRT_LAUNCH_CHECK();
+	if (n_corner_edges > 0) {
+		k_corner_offdiag<<<n_corner_edges, 64, 0, s>>>(d_corner_edges, n0, edges, wing, map());
+		NNRT_LAUNCH_CHECK();
+	}
+	return NNRT_OK;
+}
+
+nnrt_status CornerSolver::launch_solve(float* xout, int* error_flag, hipStream_t s) const {
+	if (nc == 0) return NNRT_OK;
+	CornerFactorArgs fa{tiles, ldiag, cb, nullptr, d_srcs, 0, error_flag};
+	for (int l = 0; l < H; l++) {
+		const int n = level_off[static_cast<size_t>(l) + 1] - level_off[static_cast<size_t>(l)];
+		fa.tasks = d_tasks + level_off[static_cast<size_t>(l)];
+		fa.n_panel = level_panel[static_cast<size_t>(l)];
+		k_corner_factor<<<n, CT, 0, s>>>(fa);
+		NNRT_LAUNCH_CHECK();
+	}
+	CornerBackArgs ba{tiles, ldiag, cb, xp, d_row_node, xout, nullptr, d_back_ent};
+	for (int l = H - 1; l >= 0; l--) {
+		const int n = back_off[static_cast<size_t>(l) + 1] - back_off[static_cast<size_t>(l)];
+		ba.cols = d_back_cols + back_off[static_cast<size_t>(l)];
+		k_corner_back<<<n, CT, 0, s>>>(ba);
+		NNRT_LAUNCH_CHECK();
+	}
+	return NNRT_OK;
+}
+
+} // namespace nnrt

@@ -82,17 +82,71 @@ struct ArapArgs {
 nnrt_status launch_arap_edges(const ArapArgs& args, hipStream_t stream);
 
 constexpr int EDGE_TERMS = 32;  // per ARAP edge: 21 + 6 source terms, 1 + 3 target terms, 1 pad
-constexpr int CORNER_NB = 64;   // dense-corner Cholesky block size (the corner is padded to a multiple with identity)
+constexpr int CORNER_NB = 64;   // Schur-corner tile size (tile columns are padded to a multiple with identity)
 inline int corner_ld(int m) { return (m + CORNER_NB - 1) / CORNER_NB * CORNER_NB; }
+
+// ---- Schur corner: tile-sparse supernodal Cholesky (corner.hip) ----
+struct CornerTask {   // one workgroup of a factor launch
+	int I, J;           // tile (I, J), I >= J
+	int slot_t, slot_d; // slots of tile (I, J) and of the diagonal tile (J, J) (-1 for trailing tasks)
+	int src, nd, np;    // update terms in `srcs`: nd for the diagonal tile (trailing: the tile's), then np for the panel tile
+	int pad;
+};
+struct CornerMap {      // device view: permuted (row, column) -> stored entry
+	int T;
+	const int* tile_slot;   // [T, T]
+	const int* node_row;    // [nc] first permuted unknown of each corner node
+	float* tiles;           // [slots, 64, 64]
+};
+// stored position of corner entry (R, C), R >= C (permuted unknowns)
+__device__ inline float* corner_entry(const CornerMap& m, int R, int C) {
+	const int slot = m.tile_slot[static_cast<int64_t>(R / CORNER_NB) * m.T + C / CORNER_NB];
+	return m.tiles + static_cast<int64_t>(slot) * (CORNER_NB * CORNER_NB) + (R % CORNER_NB) * CORNER_NB + (C % CORNER_NB);
+}
+// entry (r, c) of the 6 x 6 corner block of nodes (a, b), a >= b, at its lower-triangle position (S is symmetric: an
+// entry above the diagonal is its transpose partner's); nullptr for the upper half of a diagonal block (a == b), which the
+// block's lower half already carries
+__device__ inline float* corner_block_entry(const CornerMap& m, int a, int b, int r, int c) {
+	const int R = m.node_row[a] + r, C = m.node_row[b] + c;
+	if (R >= C) return corner_entry(m, R, C);
+	return a == b ? nullptr : corner_entry(m, C, R);
+}
+class CornerSolver {
+public:
+	~CornerSolver();
+	// host, once per hierarchy (edges [E,2] host, virtual order; corner = nodes >= n0): ordering, symbolic factorisation,
+	// launch plan, device buffers. A repeated call with the same structure keeps everything (stable pointers for graphs).
+	nnrt_status prepare(const int32_t* edges, int E, int n0, int N);
+	// S = C (+ corner off-diagonal blocks) in the stored tiles, cb = b_C (permuted); diag [N,36], rhs [6N], edges / wing device
+	nnrt_status launch_init(int n0, const float* diag, const float* rhs, const int32_t* edges, const float* wing, hipStream_t s) const;
+	// factor S (after the stem's Schur update), solve S x = cb; x -> xout[6 nc] in corner-node order
+	nnrt_status launch_solve(float* xout, int* error_flag, hipStream_t s) const;
+	CornerMap map() const;
+	float* rhs_perm() const { return cb; }
+	int levels() const { return H; }
+	int64_t stored_tiles() const { return fill_tiles; }
+	int64_t dense_lower_tiles() const { return dense_tiles; }
+	uint64_t generation = 0;    // bumped whenever the plan (and its buffers) change
+
+private:
+	void release();
+	std::vector<int32_t> key;
+	int nc = 0, ld = 0, T = 0, H = 0, slots = 0, n_corner_edges = 0;
+	int64_t fill_tiles = 0, dense_tiles = 0;
+	float *tiles = nullptr, *ldiag = nullptr, *cb = nullptr, *xp = nullptr;
+	int *d_tile_slot = nullptr, *d_row_node = nullptr, *d_node_row = nullptr, *d_corner_edges = nullptr;
+	int2 *d_slot_ij = nullptr, *d_back_ent = nullptr;
+	CornerTask* d_tasks = nullptr;
+	int4 *d_srcs = nullptr, *d_back_cols = nullptr;
+	std::vector<int> level_off, level_panel, back_off;
+};
 
 struct ArrowheadWorkspace {
 	int N = 0, n0 = 0, E = 0, m = 0;
-	int ld = 0;                 // corner_ld(m): padded corner size and row stride of `schur`
+	const CornerSolver* corner = nullptr;   // Schur corner (m = 6 (N - n0) > 0)
 	float* diag = nullptr;      // [N,36] full diagonal blocks (with LM)
 	float* dinv = nullptr;      // [n0,36]
 	float* dinv_b = nullptr;    // [E,36]
-	float* schur = nullptr;     // [ld,ld] Schur complement of the stem (lower triangle factored in place)
-	float* cb = nullptr;        // [ld] corner right-hand side / solution (zero padded)
 	float* rhs = nullptr;       // [6N] negative gradient
 	float* x = nullptr;         // [6N]
 	int* edge_offsets = nullptr;// [n0+1] CSR of stem edges by source node (edges grouped by source)
@@ -103,7 +157,7 @@ struct ArrowheadWorkspace {
 	// node: each target is written by one owner, no atomics (build_stem_schur_lists)
 	int targets = 0;
 	int* tgt_off = nullptr;     // [targets+1] CSR into `pairs`
-	int2* tgt_ab = nullptr;     // [targets] (a, b) corner block coordinates, a >= b
+	int2* tgt_ab = nullptr;     // [targets] (a, b) corner node coordinates, a >= b
 	int2* pairs = nullptr;      // (e1, e2): stem edges i->a, i->b of one stem node i
 	int* rhs_off = nullptr;     // [N - n0 + 1] CSR into `rhs_edges` by corner node
 	int* rhs_edges = nullptr;   // stem edges into each corner node

@@ -203,7 +203,5 @@ nnrt_status launch_get_sparse_blocks(const float* matrix, int64_t rows, int64_t 
 nnrt_status launch_transpose_blocks(float* blocks, int64_t count, int s, hipStream_t stream);
 nnrt_status launch_invert_triangular_blocks(const float* blocks, int64_t count, int s, bool upper, float* out, int* error_flag,
                                             hipStream_t stream);
-nnrt_status solve_arrowhead(const float* diag, const float* wing, const int32_t* coords, int E, int N, int n0, const float* b, float* x,
-                            int* error_flag, hipStream_t stream);
 
 } // namespace nnrt

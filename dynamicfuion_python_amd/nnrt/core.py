@@ -31,14 +31,20 @@ def _solve_block_diagonal_cholesky(blocks, b) -> torch.Tensor:
     return x
 
 
+def _aligned16(t: torch.Tensor) -> torch.Tensor:
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
 def _solve_block_sparse_arrowhead_cholesky(diagonal_blocks, upper_wing_blocks, upper_wing_block_coordinates, arrow_base_block_index, b):
     """SolveBlockSparseArrowheadCholesky (cpp/core/linalg/SolveBlockSparseArrowheadCholesky.cpp:30-95), uncapped."""
     N.require_gpu()
     dev = torch.device("cuda", N.current_device())
-    D = to_device(diagonal_blocks, torch.float32, dev)
-    Wb = to_device(upper_wing_blocks, torch.float32, dev)
-    C = to_device(upper_wing_block_coordinates, torch.int32, dev)
-    bb = to_device(b, torch.float32, dev).reshape(-1)
+    # the C-ABI reads 6x6 blocks as float4: a view at an offset that is not a multiple of 4 floats is copied into a fresh
+    # (aligned) buffer first, as the reference accepts any contiguous tensor (ADVICE r2)
+    D = _aligned16(to_device(diagonal_blocks, torch.float32, dev).contiguous())
+    Wb = _aligned16(to_device(upper_wing_blocks, torch.float32, dev).contiguous())
+    C = to_device(upper_wing_block_coordinates, torch.int32, dev).contiguous()
+    bb = to_device(b, torch.float32, dev).reshape(-1).contiguous()
     x = torch.empty_like(bb)
     N.check(N.lib().nnrt_solve_block_sparse_arrowhead_cholesky(N.ptr(D), N.ptr(Wb), N.ptr(C), Wb.shape[0], D.shape[0],
                                                               int(arrow_base_block_index), N.ptr(bb), N.ptr(x), N.stream_ptr()))

@@ -97,9 +97,14 @@ CONFIGS = {
     "C2_ARAP": (480, 640, 580.0, 321, 241, 50, 30, 0.03, 2, 10),
     "C3": (960, 1280, 1160.0, 1501, 1501, 75, 40, 0.022, 1, 10),
     "C5": (480, 640, 580.0, 321, 241, 100, 50, 0.018, 2, 10),
+    # >= 3 layers (the binding's default is 4, HierarchicalGraphWarpField.h:44): corner off-diagonal blocks
+    "C2_ARAP3": (480, 640, 580.0, 321, 241, 50, 30, 0.03, 3, 10),
+    "C2_ARAP4": (480, 640, 580.0, 321, 241, 50, 30, 0.03, 4, 10),
+    "C5_L4": (480, 640, 580.0, 321, 241, 100, 50, 0.018, 4, 10),
     # small configs for fast CPU-oracle parity tests
     "S1": (96, 128, 116.0, 49, 37, 6, 4, 0.25, 1, 2),
     "S1_ARAP": (96, 128, 116.0, 49, 37, 8, 6, 0.16, 2, 2),
+    "S1_ARAP4": (96, 128, 116.0, 49, 37, 12, 9, 0.1, 4, 2),
 }
 
 

@@ -329,7 +329,10 @@ nnrt_status nnrt_invert_triangular_blocks(const float* d_blocks, int32_t block_c
                                           void* stream);
 /* SolveBlockSparseArrowheadCholesky (cpp/core/linalg/SolveBlockSparseArrowheadCholesky.cpp:30-95), 6x6 blocks:
  * d_diagonal_blocks [N,6,6], d_wing_blocks [E,6,6] at block coordinates d_wing_coordinates [E,2] (row < arrow_base
- * <= column for stem-to-corner blocks; row >= arrow_base for corner off-diagonal blocks), b [6N]. */
+ * <= column for stem-to-corner blocks; row >= arrow_base for corner off-diagonal blocks), b [6N]. Coordinates outside
+ * [0, N), a diagonal coordinate (row == column) or a column inside the stem (column < arrow_base) give
+ * NNRT_ERROR_ARGUMENT, checked before any allocation. The Schur corner is factored tile-sparse (nested-dissection order
+ * of the corner blocks); its size is bounded by device memory only. */
 nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diagonal_blocks, const float* d_wing_blocks,
                                                        const int32_t* d_wing_coordinates, int32_t wing_block_count,
                                                        int32_t diagonal_block_count, int32_t arrow_base_block_index,
