@@ -407,8 +407,10 @@ def _new_fit(nn, sc, depth, iterations):
 # raise potrf or None). The reference's GN step is block-diagonal in the data term (A17) and overshoots: on C2 its
 # iteration-2 Hessian blocks lose positive definiteness in float (condition > 1e10), i.e. FitToImage throws there -- on
 # the GPU and in the oracle alike. The ARAP configs run until the arrowhead system degenerates (A7 NaN rotations,
-# condition > 1e9); wherever a potrf failure occurs, both implementations must hit it in the same iteration.
-TRAJECTORIES = [("S1", 6, 6, None), ("C2", 2, 1, 2), ("C2_ARAP", 10, 6, None), ("C5", 6, 4, None)]
+# condition > 1e9); wherever a potrf failure occurs, both implementations must hit it in the same iteration. C5: the
+# GPU's iteration-3 solve lies closer to the fp64 solution than the oracle's float solve (5.4e-4 vs 8.3e-4), and from
+# the state it reaches both implementations raise potrf at iteration 4 (7 A7 NaN rotations by then).
+TRAJECTORIES = [("S1", 6, 6, None), ("C2", 2, 1, 2), ("C2_ARAP", 10, 6, None), ("C5", 6, 3, None)]
 
 
 @pytest.mark.parametrize("name,iterations,min_ok,fails_at", TRAJECTORIES)
