@@ -152,7 +152,8 @@ struct CornerPlan {
 	std::vector<int> level_off, level_panel;   // [H + 1] task offsets per factor launch, [H] panel tasks first
 	std::vector<CornerTask> tasks;
 	std::vector<int4> srcs;           // (slot X, slot Y, column k, 0): X Y^T update terms; rhs term L_k y_k uses X and k
-	std::vector<int> back_off;        // [H + 1] back-substitution columns per level
+	std::vector<int> back_off;        // [launches + 1] back-substitution chains per launch
+	std::vector<int2> back_chains;    // (first column entry, column count): a chain of the elimination tree, root end first
 	std::vector<int4> back_cols;      // (J, entry offset, entry count, 0)
 	std::vector<int2> back_ent;       // (slot of L_IJ, I)
 	std::vector<int> corner_edges;    // edges between two corner nodes (>= 3 layers)
@@ -305,16 +306,42 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N) {
 		}
 		p.level_off.push_back(static_cast<int>(p.tasks.size()));
 	}
-	// back substitution: per level, each column with its panel tiles (I, J), I > J
+	// back substitution over chains of the elimination tree: a chain starts at a root or at a child of a node with two or
+	// more children and follows single children down; one workgroup walks a chain from its root end, so a launch holds
+	// every chain at the same number of branchings below the root (x of every column above a chain's top is known
+	// before its launch: struct(J) holds ancestors only)
+	std::vector<std::vector<int>> kids(static_cast<size_t>(T));
+	for (int J = 0; J < T; J++)
+		if (parent[static_cast<size_t>(J)] >= 0) kids[static_cast<size_t>(parent[static_cast<size_t>(J)])].push_back(J);
+	std::vector<std::vector<int>> chains_at;   // chain tops per depth
+	std::vector<std::pair<int, int>> stack;    // (chain top, depth)
+	for (int J = T - 1; J >= 0; J--)
+		if (parent[static_cast<size_t>(J)] < 0) stack.push_back({J, 0});
+	std::vector<std::vector<int>> chain_cols;
+	std::vector<int> chain_depth;
+	while (!stack.empty()) {
+		const auto [top, d] = stack.back();
+		stack.pop_back();
+		std::vector<int> cols(1, top);
+		while (kids[static_cast<size_t>(cols.back())].size() == 1) cols.push_back(kids[static_cast<size_t>(cols.back())][0]);
+		for (int c : kids[static_cast<size_t>(cols.back())]) stack.push_back({c, d + 1});
+		chain_cols.push_back(std::move(cols));
+		chain_depth.push_back(d);
+	}
+	int depth_max = 0;
+	for (int d : chain_depth) depth_max = std::max(depth_max, d);
 	p.back_off.push_back(0);
-	for (int l = 0; l < p.H; l++) {
-		for (int J = 0; J < T; J++) {
-			if (lvl[static_cast<size_t>(J)] != l) continue;
-			const auto& c = cs[static_cast<size_t>(J)];
-			p.back_cols.push_back(make_int4(J, static_cast<int>(p.back_ent.size()), static_cast<int>(c.size()), 0));
-			for (int I : c) p.back_ent.push_back(make_int2(slot(I, J), I));
+	for (int d = 0; d <= depth_max; d++) {
+		for (size_t c = 0; c < chain_cols.size(); c++) {
+			if (chain_depth[c] != d) continue;
+			p.back_chains.push_back(make_int2(static_cast<int>(p.back_cols.size()), static_cast<int>(chain_cols[c].size())));
+			for (int J : chain_cols[c]) {
+				const auto& cc = cs[static_cast<size_t>(J)];
+				p.back_cols.push_back(make_int4(J, static_cast<int>(p.back_ent.size()), static_cast<int>(cc.size()), 0));
+				for (int I : cc) p.back_ent.push_back(make_int2(slot(I, J), I));
+			}
 		}
-		p.back_off.push_back(static_cast<int>(p.back_cols.size()));
+		p.back_off.push_back(static_cast<int>(p.back_chains.size()));
 	}
 	return p;
 }
@@ -522,6 +549,20 @@ __device__ inline void eliminate_columns(f32x2 (&ap)[TILE], int lane, int& bad) 
 	}
 }
 
+// development timing build only (-DNNRT_CORNER_STAMPS, tools/dev/corner_stamps.sh): shader-clock stamps of the first
+// workgroup of each factor launch at its phase boundaries, read back by nnrt_dev_corner_stamps
+#ifdef NNRT_CORNER_STAMPS
+__device__ unsigned long long g_corner_stamps[256][8];
+#define CORNER_STAMP(i)                                                                                                  \
+	do {                                                                                                                 \
+		if (blockIdx.x == 0 && threadIdx.x == 0 && a.level < 256) g_corner_stamps[a.level][i] = __builtin_amdgcn_s_memtime(); \
+	} while (0)
+#else
+#define CORNER_STAMP(i) \
+	do {                \
+	} while (0)
+#endif
+
 struct CornerFactorArgs {
 	float* tiles;            // [slots, 64, 64]
 	float* ldiag;            // [T, 64, 64] L_JJ (lower; zero above the diagonal)
@@ -530,6 +571,7 @@ struct CornerFactorArgs {
 	const int4* srcs;
 	int n_panel;
 	int* error_flag;
+	int level;
 };
 
 // One launch per level of the tile elimination tree.
@@ -544,6 +586,7 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 	__shared__ float s_p[TILE * CS4];   // A_IJ after the previous level's updates (panel workgroups below the diagonal)
 	__shared__ float s_b[TILE];         // b_J after the previous level's updates (diagonal workgroup)
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+	CORNER_STAMP(0);
 	const CornerTask tk = a.tasks[blockIdx.x];
 	const int4* src = a.srcs + tk.src;
 	if (static_cast<int>(blockIdx.x) >= a.n_panel) {
@@ -572,6 +615,7 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 		if ((t & 3) == 0) s_b[t >> 2] = a.cb[static_cast<int64_t>(tk.J) * TILE + (t >> 2)] - s;
 	}
 	__syncthreads();
+	CORNER_STAMP(1);
 	// ap[c] = (A_JJ[lane][c], A_IJ[lane][c]): both rows see the same column operations, so one packed FMA
 	// (v_pk_fma_f32) updates the pair. Wave 0 holds them; the other waves join for the rank-32 update between the halves.
 	f32x2 ap[TILE];
@@ -591,6 +635,7 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 			ap[4 * q + 3] = f32x2{va.w, vp.w};
 		}
 		eliminate_columns<0, TILE / 2>(ap, lane, bad);
+		CORNER_STAMP(2);
 		// L[:, 0:32] of the A_JJ rows and of the panel rows -> LDS (s_d / s_p are free once loaded)
 #pragma unroll
 		for (int q = 0; q < TILE / 8; q++) {
@@ -633,7 +678,9 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 		ap[4 * q + 2] -= f32x2{ca.z, cp.z};
 		ap[4 * q + 3] -= f32x2{ca.w, cp.w};
 	}
+	CORNER_STAMP(3);
 	eliminate_columns<TILE / 2, TILE>(ap, lane, bad);
+	CORNER_STAMP(4);
 	if (diag) {
 		float4* wa = reinterpret_cast<float4*>(a.ldiag + static_cast<int64_t>(tk.J) * TILE_ELEMS + lane * TILE);
 #pragma unroll
@@ -646,6 +693,7 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 			for (int q = 0; q < TILE / 4; q++) wb[q] = make_float4(ap[4 * q].y, ap[4 * q + 1].y, ap[4 * q + 2].y, ap[4 * q + 3].y);
 			if (bad) atomicOr(a.error_flag, 1);
 		}
+		CORNER_STAMP(5);
 	} else {
 		float4* wp = reinterpret_cast<float4*>(a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS + lane * TILE);
 #pragma unroll
@@ -660,49 +708,75 @@ struct CornerBackArgs {
 	float* xp;               // [ld] x in the permuted order
 	const int* row_node;
 	float* xout;             // [6 nc] x in node order
-	const int4* cols;        // this launch's columns (J, entry offset, count, 0)
+	const int2* chains;      // this launch's chains (first column, column count)
+	const int4* cols;        // (J, entry offset, entry count, 0), each chain root end first
 	const int2* ent;         // (slot of L_IJ, I)
 };
 
-// Back substitution L^T x = y for the tile columns of one level (one workgroup each; from the root level down):
-// z = y_J - sum_I L_IJ^T x_I (each wave a quarter of every tile's rows), then x_J = L_JJ^-T z by column-oriented
-// substitution on wave 0 (lane = column; x_r broadcast by readlane).
+// Back substitution L^T x = y along chains of the elimination tree (one workgroup per chain, its columns in order; the
+// launches run from the root's chain down). Per column J: z = y_J - sum_I L_IJ^T x_I (each wave a quarter of every tile's
+// rows; the entries are read one per lane and broadcast, two tiles' loads in flight), then x_J = L_JJ^-T z by
+// column-oriented substitution on wave 0 (lane = column; x_r broadcast by readlane). x_J goes to global memory before
+// the workgroup barrier, so the chain's next column reads it like the x of earlier launches.
 __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 	__shared__ float s_part[4][TILE];
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-	const int4 col = a.cols[blockIdx.x];
-	const int J = col.x;
-	float acc0 = 0.f, acc1 = 0.f;
-	for (int e = 0; e < col.z; e++) {
-		const int2 en = a.ent[col.y + e];
-		const float* L = a.tiles + static_cast<int64_t>(en.x) * TILE_ELEMS + 16 * wave * TILE + lane;
-		const float* xi = a.xp + static_cast<int64_t>(en.y) * TILE + 16 * wave;
+	const int2 ch = a.chains[blockIdx.x];
+	for (int q = 0; q < ch.y; q++) {
+		const int4 col = a.cols[ch.x + q];
+		const int J = col.x;
+		const float* Ld = a.ldiag + static_cast<int64_t>(J) * TILE_ELEMS;
+		float colv[TILE];   // colv[r] = L_JJ[r][lane] (wave 0; issued before the sums so the loads overlap them)
+		if (wave == 0) {
 #pragma unroll
-		for (int r = 0; r < 16; r += 2) {
-			acc0 += L[r * TILE] * xi[r];
-			acc1 += L[(r + 1) * TILE] * xi[r + 1];
+			for (int r = 0; r < TILE; r++) colv[r] = Ld[r * TILE + lane];
 		}
-	}
-	s_part[wave][lane] = acc0 + acc1;
-	__syncthreads();
-	if (wave != 0) return;
-	const float* Ld = a.ldiag + static_cast<int64_t>(J) * TILE_ELEMS;
-	float colv[TILE];   // colv[r] = L_JJ[r][lane]
+		float acc0 = 0.f, acc1 = 0.f;
+		for (int e0 = 0; e0 < col.z; e0 += 64) {
+			const int ne = col.z - e0 < 64 ? col.z - e0 : 64;
+			const int2 mine = lane < ne ? a.ent[col.y + e0 + lane] : make_int2(0, 0);
+			for (int e = 0; e < ne; e += 2) {
+				const bool two = e + 1 < ne;
+				const int s0 = __shfl(mine.x, e), i0 = __shfl(mine.y, e);
+				const int s1 = __shfl(mine.x, two ? e + 1 : e), i1 = __shfl(mine.y, two ? e + 1 : e);
+				const float* L0 = a.tiles + static_cast<int64_t>(s0) * TILE_ELEMS + 16 * wave * TILE + lane;
+				const float* L1 = a.tiles + static_cast<int64_t>(s1) * TILE_ELEMS + 16 * wave * TILE + lane;
+				const float* x0 = a.xp + static_cast<int64_t>(i0) * TILE + 16 * wave;
+				const float* x1 = a.xp + static_cast<int64_t>(i1) * TILE + 16 * wave;
+				float l0[16], l1[16], v0[16], v1[16];
 #pragma unroll
-	for (int r = 0; r < TILE; r++) colv[r] = Ld[r * TILE + lane];
-	const float inv_d = 1.f / Ld[lane * TILE + lane];
-	float z = a.cb[static_cast<int64_t>(J) * TILE + lane] - ((s_part[0][lane] + s_part[1][lane]) + (s_part[2][lane] + s_part[3][lane]));
-	float x = 0.f;
+				for (int r = 0; r < 16; r++) {
+					l0[r] = L0[r * TILE];
+					v0[r] = x0[r];
+					l1[r] = L1[r * TILE];
+					v1[r] = two ? x1[r] : 0.f;
+				}
 #pragma unroll
-	for (int r = TILE - 1; r >= 0; r--) {
-		const float xr = lane_bcast(z, r) * lane_bcast(inv_d, r);   // x_r = z_r / L_rr
-		x = lane == r ? xr : x;
-		z -= colv[r] * xr;   // z_c -= L_rc x_r (only c < r matter)
+				for (int r = 0; r < 16; r++) {
+					acc0 += l0[r] * v0[r];
+					acc1 += l1[r] * v1[r];
+				}
+			}
+		}
+		s_part[wave][lane] = acc0 + acc1;
+		__syncthreads();
+		if (wave == 0) {
+			const float inv_d = 1.f / Ld[lane * TILE + lane];
+			float z = a.cb[static_cast<int64_t>(J) * TILE + lane] - ((s_part[0][lane] + s_part[1][lane]) + (s_part[2][lane] + s_part[3][lane]));
+			float x = 0.f;
+#pragma unroll
+			for (int r = TILE - 1; r >= 0; r--) {
+				const float xr = lane_bcast(z, r) * lane_bcast(inv_d, r);   // x_r = z_r / L_rr
+				x = lane == r ? xr : x;
+				z -= colv[r] * xr;   // z_c -= L_rc x_r (only c < r matter)
+			}
+			const int64_t row = static_cast<int64_t>(J) * TILE + lane;
+			a.xp[row] = x;
+			const int rn = a.row_node[row];
+			if (rn >= 0) a.xout[6 * static_cast<int64_t>(rn >> 3) + (rn & 7)] = x;
+		}
+		__syncthreads();   // x_J visible to the chain's next column; s_part free
 	}
-	const int64_t row = static_cast<int64_t>(J) * TILE + lane;
-	a.xp[row] = x;
-	const int rn = a.row_node[row];
-	if (rn >= 0) a.xout[6 * static_cast<int64_t>(rn >> 3) + (rn & 7)] = x;
 }
 
 // ===================================================================================================================
@@ -728,7 +802,7 @@ void CornerSolver::release() {
 	for (void** p : {reinterpret_cast<void**>(&tiles), reinterpret_cast<void**>(&ldiag), reinterpret_cast<void**>(&cb),
 	                 reinterpret_cast<void**>(&xp), reinterpret_cast<void**>(&d_tile_slot), reinterpret_cast<void**>(&d_slot_ij),
 	                 reinterpret_cast<void**>(&d_row_node), reinterpret_cast<void**>(&d_node_row), reinterpret_cast<void**>(&d_tasks),
-	                 reinterpret_cast<void**>(&d_srcs), reinterpret_cast<void**>(&d_back_cols), reinterpret_cast<void**>(&d_back_ent),
+	                 reinterpret_cast<void**>(&d_srcs), reinterpret_cast<void**>(&d_back_cols), reinterpret_cast<void**>(&d_back_ent), reinterpret_cast<void**>(&d_back_chains),
 	                 reinterpret_cast<void**>(&d_corner_edges)})
 		dev_free(*p);
 	nc = ld = T = H = slots = n_corner_edges = 0;
@@ -759,7 +833,7 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N) {
 		nnrt_status st;
 		if ((st = dev_upload(d_tile_slot, p.tile_slot)) || (st = dev_upload(d_slot_ij, p.slot_ij)) || (st = dev_upload(d_row_node, p.row_node)) ||
 		    (st = dev_upload(d_node_row, p.node_row)) || (st = dev_upload(d_tasks, p.tasks)) || (st = dev_upload(d_srcs, p.srcs)) ||
-		    (st = dev_upload(d_back_cols, p.back_cols)) || (st = dev_upload(d_back_ent, p.back_ent)) ||
+		    (st = dev_upload(d_back_cols, p.back_cols)) || (st = dev_upload(d_back_ent, p.back_ent)) || (st = dev_upload(d_back_chains, p.back_chains)) ||
 		    (st = dev_upload(d_corner_edges, p.corner_edges)))
 			return st;
 		level_off = p.level_off;
@@ -789,22 +863,29 @@ nnrt_status CornerSolver::launch_init(int n0, const float* diag, const float* rh
 
 nnrt_status CornerSolver::launch_solve(float* xout, int* error_flag, hipStream_t s) const {
 	if (nc == 0) return NNRT_OK;
-	CornerFactorArgs fa{tiles, ldiag, cb, nullptr, d_srcs, 0, error_flag};
+	CornerFactorArgs fa{tiles, ldiag, cb, nullptr, d_srcs, 0, error_flag, 0};
 	for (int l = 0; l < H; l++) {
+		fa.level = l;
 		const int n = level_off[static_cast<size_t>(l) + 1] - level_off[static_cast<size_t>(l)];
 		fa.tasks = d_tasks + level_off[static_cast<size_t>(l)];
 		fa.n_panel = level_panel[static_cast<size_t>(l)];
 		k_corner_factor<<<n, CT, 0, s>>>(fa);
 		NNRT_LAUNCH_CHECK();
 	}
-	CornerBackArgs ba{tiles, ldiag, cb, xp, d_row_node, xout, nullptr, d_back_ent};
-	for (int l = H - 1; l >= 0; l--) {
-		const int n = back_off[static_cast<size_t>(l) + 1] - back_off[static_cast<size_t>(l)];
-		ba.cols = d_back_cols + back_off[static_cast<size_t>(l)];
+	CornerBackArgs ba{tiles, ldiag, cb, xp, d_row_node, xout, nullptr, d_back_cols, d_back_ent};
+	for (size_t l = 0; l + 1 < back_off.size(); l++) {
+		const int n = back_off[l + 1] - back_off[l];
+		ba.chains = d_back_chains + back_off[l];
 		k_corner_back<<<n, CT, 0, s>>>(ba);
 		NNRT_LAUNCH_CHECK();
 	}
 	return NNRT_OK;
 }
+
+#ifdef NNRT_CORNER_STAMPS
+extern "C" int nnrt_dev_corner_stamps(unsigned long long* out) {   // [256][8] shader-clock stamps of the last solve
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_corner_stamps), sizeof(unsigned long long) * 256 * 8) == hipSuccess ? 0 : 1;
+}
+#endif
 
 } // namespace nnrt

@@ -124,6 +124,7 @@ public:
 	CornerMap map() const;
 	float* rhs_perm() const { return cb; }
 	int levels() const { return H; }
+	int back_launches() const { return back_off.empty() ? 0 : static_cast<int>(back_off.size()) - 1; }
 	int64_t stored_tiles() const { return fill_tiles; }
 	int64_t dense_lower_tiles() const { return dense_tiles; }
 	uint64_t generation = 0;    // bumped whenever the plan (and its buffers) change
@@ -135,7 +136,7 @@ private:
 	int64_t fill_tiles = 0, dense_tiles = 0;
 	float *tiles = nullptr, *ldiag = nullptr, *cb = nullptr, *xp = nullptr;
 	int *d_tile_slot = nullptr, *d_row_node = nullptr, *d_node_row = nullptr, *d_corner_edges = nullptr;
-	int2 *d_slot_ij = nullptr, *d_back_ent = nullptr;
+	int2 *d_slot_ij = nullptr, *d_back_ent = nullptr, *d_back_chains = nullptr;
 	CornerTask* d_tasks = nullptr;
 	int4 *d_srcs = nullptr, *d_back_cols = nullptr;
 	std::vector<int> level_off, level_panel, back_off;
