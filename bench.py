@@ -17,11 +17,14 @@ are the alternatives.
 
 N > 1: one process per GPU (torchrun), each fitting its own independent sequence (seed = rank) -- replicas, no
 collective in the data path; the only collectives are the barrier, the max-over-ranks of the elapsed time and the
-end-of-run all-gather of per-rank results.
+end-of-run all-gather of per-rank results. --replicas R: R independent sequences per process, each with
+its own fitter, warp field and stream on the one device (seeds rank * R + r); a step launches every replica's iteration
+on its stream; value = all sequences' iterations / the slowest rank's time.
 
 Also reported: the dominant kernel's roofline (k_fit_pixels_fused: both pixel passes in one launch, HIP-event timed on the fitter's work stream; every
 other kernel of the iteration under "kernels"), the once-per-frame setup time, and the CPU baseline (the oracle/ C++
-restatement, OpenMP, on a bounded sample of the same workload, rank 0, N = 1; also at 1 thread).
+restatement with the reference's binned rasterizer, OpenMP, on a bounded sample of the same workload, rank 0, N = 1: one
+socket's physical cores with OMP_PROC_BIND=close as the value, plus this process's CPU share and 1 thread).
 """
 from __future__ import annotations
 
@@ -170,6 +173,7 @@ def parse_args(argv=None):
                     help="snapshot: one GN iteration per step from a mid-motion node state (general kernels); frame: "
                          "--graph-steps-iteration frame fits from the identity warp (FitToImage's loop; raises potrf on C2, "
                          "as the reference does); identity: the first iteration of a frame per step")
+    ap.add_argument("--replicas", type=int, default=1, help="independent sequences per GPU, one stream each (C4's per-rank work)")
     ap.add_argument("--timed-steps", type=int, default=100, help="eager per-stage HIP-event timing steps (roofline)")
     ap.add_argument("--graph-steps", type=int, default=10, help="steps per captured graph launch (C2: 10 GN iterations per frame)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU-baseline sample (loop-body seconds)")
@@ -209,8 +213,9 @@ def load_traffic(path: str, workload: str):
 
 
 def host_cpu():
-    """CPU model, sockets and logical CPUs of this host (/proc/cpuinfo; os.cpu_count() is the whole machine)."""
-    model, sockets = None, set()
+    """CPU model, sockets, physical cores per socket and logical CPUs of this host (/proc/cpuinfo; os.cpu_count() is the
+    whole machine)."""
+    model, sockets, cores = None, set(), None
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
@@ -220,29 +225,44 @@ def host_cpu():
                     model = v
                 elif k == "physical id":
                     sockets.add(v)
+                elif k == "cpu cores" and cores is None and v.isdigit():
+                    cores = int(v)
     except OSError:
         pass
-    return dict(model=model, sockets=len(sockets) or None, logical_cpus=os.cpu_count())
+    return dict(model=model, sockets=len(sockets) or None, cores_per_socket=cores, logical_cpus=os.cpu_count())
 
 
-def cpu_baseline(sc, depth_host, threads: int, budget_s: float, step: str, iterations: int, R0=None, t0=None, single_thread_s: float = 4.0):
+def cpu_baseline(sc, depth_host, share_threads: int, budget_s: float, step: str, iterations: int, R0=None, t0=None,
+                 single_thread_s: float = 4.0):
     """The oracle (C++/OpenMP restatement of the reference CPU path; test infrastructure, used here only as the
     reported baseline) running the same steps as the GPU: `step` = "frame" -> `iterations`-iteration FitToImage loops from
     the identity warp; "snapshot" -> one GN iteration from the node state (R0, t0); "identity" -> one GN iteration from
     the identity warp. Timed = loop body S1-S12 (DeformableMeshToImageFitter.cpp:111-275), once-per-frame setup
-    excluded, as in the GPU step. Run with `threads` OpenMP threads (the headline) and again with 1 thread."""
+    excluded, as in the GPU step; the rasterizer is the reference's binned one (GridBinNdcTriangles + per-pixel bin loop,
+    RasterizeNdcTrianglesImpl.h:187-391), not the oracle's fast K = 1 path. Threads: the physical
+    cores of one socket with OMP_PROC_BIND=close (the headline value), this process's CPU share (16 on the GPU box) and 1."""
+    os.environ.setdefault("OMP_PROC_BIND", "close")   # read when the oracle's OpenMP runtime initialises (first load)
+    os.environ.setdefault("OMP_PLACES", "cores")
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
+    host = host_cpu()
+    socket = min(host["cores_per_socket"] or share_threads, len(os.sched_getaffinity(0)))
     refp, refm = O.unproject(depth_host, sc.K, 1.0, 10.0)
-    res = _cpu_sample(O, sc, refp, refm, threads, budget_s, step, iterations, R0, t0)
-    one = _cpu_sample(O, sc, refp, refm, 1, single_thread_s, step, iterations, R0, t0)
-    res["single_thread"] = dict(value=one["value"], unit=one["unit"], cores=1, ms_per_solve=one["ms_per_solve"],
-                                sample=one["sample"])
-    res["host"] = host_cpu()
+    res = _cpu_sample(O, sc, refp, refm, socket, budget_s, step, iterations, R0, t0)
+    if share_threads != socket:
+        sh = _cpu_sample(O, sc, refp, refm, share_threads, budget_s, step, iterations, R0, t0)
+        res["cpu_share"] = dict(value=sh["value"], unit=sh["unit"], cores=sh["cores"], ms_per_solve=sh["ms_per_solve"], sample=sh["sample"])
+    one = _cpu_sample(O, sc, refp, refm, 1, single_thread_s, step, iterations, R0, t0, min_timed=1)
+    res["single_thread"] = dict(value=one["value"], unit=one["unit"], cores=1, ms_per_solve=one["ms_per_solve"], sample=one["sample"])
+    res["host"] = host
+    res["omp_proc_bind"] = os.environ.get("OMP_PROC_BIND")
     return res
 
 
-def _cpu_sample(O, sc, refp, refm, threads: int, budget_s: float, step: str, iterations: int, R0, t0):
+def _cpu_sample(O, sc, refp, refm, threads: int, budget_s: float, step: str, iterations: int, R0, t0, min_timed: int = 1):
+    """Timed oracle fits until `budget_s` of loop body has accumulated (at least `min_timed` timed calls); a first
+    untimed call warms caches / page-ins unless the process has already run one (the single-thread sample follows the
+    multi-thread ones on the same data)."""
     O.set_num_threads(threads)
     N = len(sc.nodes)
     if step != "snapshot" or R0 is None:
@@ -256,23 +276,27 @@ def _cpu_sample(O, sc, refp, refm, threads: int, budget_s: float, step: str, ite
         nodes = sc.nodes[h["virtual_indices"]]
         hk = dict(edges=h["edges"], edge_layers=h["edge_layers"], radii=h["radii"], first_layer_count=int(h["layer_counts"][0]))
     body = solve = 0.0
-    iters = calls = 0
+    iters = calls = timed = 0
+    warm = threads == 1 and getattr(_cpu_sample, "warmed", False)
     wall0 = time.perf_counter()
-    while (body < budget_s and time.perf_counter() - wall0 < 3 * budget_s) or calls < 2:
+    while (body < budget_s and time.perf_counter() - wall0 < 3 * budget_s) or timed < min_timed:
         _, _, dg = O.fit(nodes=nodes, rotations=R0, translations=t0, mesh_points=sc.points, mesh_normals=sc.normals, faces=sc.faces,
                          ref_points=refp, ref_mask=refm, H=sc.H, W=sc.W, K=sc.K, max_iterations=per_call, lm_factor=0.001,
-                         coverage=sc.coverage, **hk)
-        if calls > 0:   # first call warms caches / page-ins
+                         coverage=sc.coverage, fast_raster=False, **hk)
+        if calls > 0 or warm:
             body += dg["stage_seconds"][7]
             solve += dg["stage_seconds"][5]
             iters += per_call
+            timed += 1
         calls += 1
+    _cpu_sample.warmed = True
     what = {"frame": f"{iters // per_call} {per_call}-iteration frame fits from the identity warp",
             "snapshot": f"{iters} single GN iterations from the mid-motion node state",
             "identity": f"{iters} single GN iterations from the identity warp"}[step]
     return dict(value=iters / body if body > 0 else None, unit="GN iters/s", cores=O.num_threads(), kind="port",
                 ms_per_solve=1000.0 * solve / max(iters, 1),
-                sample=f"{sc.name}: {what} (loop body timed, setup excluded), oracle/ C++ OpenMP restatement, fast K=1 raster")
+                sample=f"{sc.name}: {what} (loop body timed, setup excluded), oracle/ C++ OpenMP restatement, binned raster "
+                       f"(the reference's GridBin + per-pixel bin loop)")
 
 
 def cpu_threads_default() -> int:
@@ -303,7 +327,8 @@ def main(argv=None):
     from dynamicfuion_python_amd.nnrt import geometry as G
     from dynamicfuion_python_amd.nnrt import rendering as Rr
 
-    sc = S.make_scene(args.config, seed=rank, hierarchy_builder=S.native_hierarchy_builder)
+    R = max(1, args.replicas)
+    sc = S.make_scene(args.config, seed=rank * R, hierarchy_builder=S.native_hierarchy_builder)
     arap = sc.layer_count > 1
     P, F, V, Nn = sc.H * sc.W, len(sc.faces), len(sc.points), len(sc.nodes)
     solve_kind = f"{sc.layer_count}-layer ARAP arrowhead LM solve" if arap else "block-diagonal LM solve"
@@ -312,20 +337,12 @@ def main(argv=None):
                  "snapshot": "1 GN iteration per step from a mid-motion node state (half the ground-truth motion)",
                  "identity": "1 GN iteration per step from the identity warp"}[args.step]
     workload = f"{sc.name}: {sc.W}x{sc.H} depth, {Nn}-node graph, {V}-vertex/{F}-triangle mesh, {solve_kind}, {step_desc}"
+    if R > 1:
+        workload += f"; {R} independent sequences per GPU on {R} streams"
 
     log(f"rank {rank}/{world} on {torch.cuda.get_device_name(dev)}: {workload}")
-
-    depth = render_target(sc, G, Rr)
-    wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE,
-                                      sc.layer_count)
-    ft = A.DeformableMeshToImageFitter(1, [A.IterationMode.ALL], preconditioning_dampening_factor=0.001, use_hip_graph=A.GRAPH_ALWAYS)
-    mesh = G.TriangleMesh(sc.points, sc.normals, sc.faces)
-    ft.prepare(wf, mesh, depth, None, sc.K)
-
     lib = NV.lib()
-    stream = torch.cuda.current_stream(dev)
-    s_ptr = NV.stream_ptr(stream)
-    wf_h, ft_h = wf.handle, ft._h
+    per_launch = max(1, min(args.graph_steps, args.steps))
 
     # Step kinds (every one runs the real GN iteration kernels of FitToImage's loop body, :111-275):
     #   frame    -- one launch = one whole frame fit of --graph-steps iterations (C2: the 10-iteration FitToImage loop)
@@ -337,39 +354,65 @@ def main(argv=None):
     #               potrf at iteration 2 on C2 (tests/test_gpu_parity.py TRAJECTORIES), so a 10-iteration C2 frame fit
     #               does not exist in the reference either.
     #   identity -- every step is the first GN iteration from the identity warp (identity-specialised warp / update).
-    per_launch = max(1, min(args.graph_steps, args.steps))
-    if args.step == "snapshot":
-        R_mid, t_mid = sc.partial_motion(0.5)
-        wf.set_node_rotations(R_mid)
-        wf.set_node_translations(t_mid)
-    ft.snapshot_motion(wf)   # the state every step (snapshot) or every frame (frame) restarts from
+    def make_replica(scene, stream):
+        depth_r = render_target(scene, G, Rr)
+        wf_r = G.HierarchicalGraphWarpField(scene.nodes, scene.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE,
+                                            scene.layer_count)
+        ft_r = A.DeformableMeshToImageFitter(1, [A.IterationMode.ALL], preconditioning_dampening_factor=0.001, use_hip_graph=A.GRAPH_ALWAYS)
+        mesh_r = G.TriangleMesh(scene.points, scene.normals, scene.faces)
+        if args.step == "snapshot":
+            R_mid, t_mid = scene.partial_motion(0.5)
+            wf_r.set_node_rotations(R_mid)
+            wf_r.set_node_translations(t_mid)
+        ft_r.prepare(wf_r, mesh_r, depth_r, None, scene.K, stream=stream)
+        ft_r.snapshot_motion(wf_r, stream=stream)   # the state every step (snapshot) or every frame (frame) restarts from
+        return dict(sc=scene, depth=depth_r, wf=wf_r, ft=ft_r, mesh=mesh_r, stream=stream, s_ptr=NV.stream_ptr(stream))
+
+    reps = [make_replica(sc, torch.cuda.current_stream(dev))]
+    for r in range(1, R):
+        reps.append(make_replica(S.make_scene(args.config, seed=rank * R + r, hierarchy_builder=S.native_hierarchy_builder),
+                                 torch.cuda.Stream(dev)))
+    torch.cuda.synchronize(dev)
+    depth, wf, ft, mesh = reps[0]["depth"], reps[0]["wf"], reps[0]["ft"], reps[0]["mesh"]
     R1, t1 = wf.get_node_rotations(True), wf.get_node_translations(True)   # (virtual order) for the CPU baseline
 
-    def step(n):
+    def step_one(rp, n):
         if args.step == "frame":
-            return lib.nnrt_fitter_fit_from_snapshot(ft_h, wf_h, n, s_ptr)
+            return lib.nnrt_fitter_fit_from_snapshot(rp["ft"]._h, rp["wf"].handle, n, rp["s_ptr"])
         if args.step == "snapshot":
-            return lib.nnrt_fitter_iterate_from_snapshot(ft_h, wf_h, 0, n, s_ptr)
-        return lib.nnrt_fitter_iterate_from_identity(ft_h, wf_h, 0, n, s_ptr)
+            return lib.nnrt_fitter_iterate_from_snapshot(rp["ft"]._h, rp["wf"].handle, 0, n, rp["s_ptr"])
+        return lib.nnrt_fitter_iterate_from_identity(rp["ft"]._h, rp["wf"].handle, 0, n, rp["s_ptr"])
+
+    def step(n):   # every replica's iterations, each on its own stream
+        bad = 0
+        for rp in reps:
+            bad |= step_one(rp, n)
+        return bad
 
     # warmup (graphs are captured on first use: use_hip_graph = 2)
     for _ in range(max(1, args.warmup // per_launch)):
         if step(per_launch):
             NV.check(1)
     torch.cuda.synchronize(dev)
-    ft.check()
+    for rp in reps:
+        rp["ft"].check(stream=rp["stream"])
 
     launches = -(-args.steps // per_launch)
     args.steps = launches * per_launch   # whole graphs only: the timed step count is rounded up to a multiple
     bad, elapsed = timed_region(step, launches, per_launch, world, lambda: torch.cuda.synchronize(dev))
     if bad:
         NV.check(bad)
-    ft.check()   # solver failure flag (potrf) -> raises
+    per_replica = []
+    for r, rp in enumerate(reps):
+        rp["ft"].check(stream=rp["stream"])   # solver failure flag (potrf) -> raises
+        final_t = rp["wf"].get_node_translations()
+        if not np.isfinite(final_t).all():
+            raise SystemExit(f"non-finite node motion after the timed steps (replica {r})")
+        per_replica.append(dict(replica=r, seed=rank * R + r,
+                                update_norm=float(np.linalg.norm(rp["ft"].diagnostics(stream=rp["stream"])["updates"]))))
     elapsed_max = max_over_ranks(elapsed, dev)
-    agg = aggregate(args.steps, elapsed_max, world)
-    final_t = wf.get_node_translations()
-    if not np.isfinite(final_t).all():
-        raise SystemExit("non-finite node motion after the timed steps")
+    agg = aggregate(args.steps * R, elapsed_max, world)
+    agg["ms_per_step"] = 1000.0 * elapsed_max / args.steps   # one step = every replica's iteration
 
     # per-stage device time (eager launches, HIP events on the fitter's work stream) over the same iterations as the
     # timed steps (a frame's iterations for "frame", the restored iteration otherwise), one iteration at a time so that
@@ -419,11 +462,13 @@ def main(argv=None):
         kernels["k_arap_edges"] = dict(ms=round(stages["arap"], 5), algorithmic_bytes=ab["arap"],
                                        frac=ab["arap"] / (stages["arap"] * 1e-3) / 1e9 / HBM_PEAK_GBS)
         fl = corner_flops(Nn - n0)
-        corner = dict(kernel="arrowhead solve stage (stem Schur update + dense corner Cholesky + substitutions + update)",
+        corner = dict(kernel="arrowhead solve stage (stem Schur update + tile-sparse corner Cholesky + substitutions + update)",
                       bound="mfma", achieved=fl / (stages["solve"] * 1e-3) / 1e12, peak=MFMA_F32_PEAK_TFS, unit="TFLOP/s",
                       frac=fl / (stages["solve"] * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS, traffic=None, flops=fl, kernel_ms=stages["solve"],
                       n0=n0, n1=Nn - n0, corner_size=6 * (Nn - n0), edges=Ee,
-                      flops_formula="SURVEY.md 8(d): (6 n1)^3 / 3 + 2 (6 n1)^2 (1 + n_rhs), n_rhs = 1")
+                      flops_formula="SURVEY.md 8(d): (6 n1)^3 / 3 + 2 (6 n1)^2 (1 + n_rhs), n_rhs = 1 (the reference's dense corner; "
+                                    "the tile-sparse factorization performs fewer: plan below)",
+                      plan=ft.corner_info())
     kbytes = kernels[ROOFLINE_KERNEL]["algorithmic_bytes"]
     k_ms = stages["node_reduce"]
     achieved = kbytes / (k_ms * 1e-3) / 1e9
@@ -439,7 +484,7 @@ def main(argv=None):
     setup_ms = (time.perf_counter() - t_setup) * 1000.0
 
     # end-of-run exchange of per-rank results: iterations/s, seconds, final |update|
-    per_rank = exchange_per_rank(args.steps, elapsed, float(np.linalg.norm(dg["updates"])), dev)
+    per_rank = exchange_per_rank(args.steps * R, elapsed, float(np.linalg.norm(dg["updates"])), dev)
 
     out = {
         "metric": "GN iters/sec (640x480, 1.5k-node graph)" if args.config == "C2" else f"GN iters/sec ({args.config})",
@@ -457,7 +502,7 @@ def main(argv=None):
         "data": "synthetic (smooth grid mesh + GT node motion rendered to depth; seed = rank)",
         "config": {"workload": workload, "config": args.config, "frame": [sc.H, sc.W], "nodes": Nn, "vertices": V, "triangles": F,
                    "anchors": 4, "iteration_mode": "ALL", "lm_damping": 0.001, "hip_graph": True, "steps_per_graph": per_launch, "step": args.step,
-                   "parallelism": f"replicas{world}" if world > 1 else "single"},
+                   "parallelism": f"replicas{world * R}" if world * R > 1 else "single", "replicas_per_gpu": R},
         "setup_ms": round(setup_ms, 3),
         "stage_ms": {k: round(v, 5) for k, v in stages.items()},
         "stage_note": "eager launches between HIP events; pixel_jacobians is back-to-back event overhead only: both pixel "
@@ -473,6 +518,7 @@ def main(argv=None):
         "kernels": kernels,
         "hbm_roofline": None,
         "per_rank": per_rank,
+        "per_replica": per_replica if R > 1 else None,
         "cpu_baseline": None,
     }
     if corner is not None:   # ARAP configs: the dense corner (MFMA-bound) is the dominant stage; the HBM one moves aside
@@ -480,7 +526,8 @@ def main(argv=None):
         out["roofline"] = corner
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or cpu_threads_default()
-        log(f"GPU: {agg['value']:.1f} it/s; running the CPU baseline sample (~{args.cpu_seconds:.0f} s, {threads} threads)")
+        log(f"GPU: {agg['value']:.1f} it/s; running the CPU baseline samples (~{args.cpu_seconds:.0f} s each: one socket's physical "
+            f"cores, {threads} threads, 1 thread)")
         out["cpu_baseline"] = cpu_baseline(sc, depth.cpu().numpy(), threads, args.cpu_seconds, args.step, per_launch, R1, t1)
         out["cpu_baseline"]["host"]["sched_affinity"] = len(os.sched_getaffinity(0))
         out["cpu_baseline"]["host"]["omp_num_threads_env"] = os.environ.get("OMP_NUM_THREADS")

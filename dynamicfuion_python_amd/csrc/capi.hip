@@ -976,6 +976,19 @@ nnrt_status nnrt_fitter_iterate_from_identity(nnrt_fitter* ft, nnrt_warp_field* 
 	return iterate_impl(ft, wf, first_iteration, count, RESET_IDENTITY, static_cast<hipStream_t>(stream));
 }
 
+nnrt_status nnrt_fitter_corner_info(const nnrt_fitter* ft, int64_t* h_out) {
+	NNRT_CHECK_ARG(ft && h_out, "null pointer");
+	const CornerSolver& c = ft->corner;
+	const bool on = ft->E > 0;
+	h_out[0] = on ? ft->N - ft->n0 : 0;
+	h_out[1] = on ? c.tile_columns() : 0;
+	h_out[2] = on ? c.levels() : 0;
+	h_out[3] = on ? c.back_launches() : 0;
+	h_out[4] = on ? c.stored_tiles() : 0;
+	h_out[5] = on ? c.dense_lower_tiles() : 0;
+	return NNRT_OK;
+}
+
 int32_t nnrt_fitter_graph_count(const nnrt_fitter* ft) {
 	if (!ft) return -1;
 	int32_t n = 0;

@@ -124,6 +124,7 @@ public:
 	CornerMap map() const;
 	float* rhs_perm() const { return cb; }
 	int levels() const { return H; }
+	int tile_columns() const { return T; }
 	int back_launches() const { return back_off.empty() ? 0 : static_cast<int>(back_off.size()) - 1; }
 	int64_t stored_tiles() const { return fill_tiles; }
 	int64_t dense_lower_tiles() const { return dense_tiles; }

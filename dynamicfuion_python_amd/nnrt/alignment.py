@@ -185,6 +185,14 @@ class DeformableMeshToImageFitter:
         out["residual_mask"] = out["residual_mask"].astype(bool)
         return out
 
+    def corner_info(self) -> dict:
+        """Schur-corner plan of the prepared frame's arrowhead solve (csrc/corner.hip): corner nodes, tile columns,
+        factorization / back-substitution launches, stored vs dense lower 64 x 64 tiles."""
+        out = np.zeros(6, np.int64)
+        N.check(N.lib().nnrt_fitter_corner_info(self._h, N.ptr(out)))
+        keys = ("corner_nodes", "tile_columns", "factor_launches", "back_launches", "stored_tiles", "dense_lower_tiles")
+        return {k: int(v) for k, v in zip(keys, out)}
+
     def anchors(self, vertex_count: int, anchor_count: int, stream=None):
         a = np.empty((vertex_count, anchor_count), np.int32)
         w = np.empty((vertex_count, anchor_count), np.float32)

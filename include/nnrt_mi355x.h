@@ -144,6 +144,10 @@ nnrt_status nnrt_fitter_iterate_from_identity(nnrt_fitter* fitter, nnrt_warp_fie
                                               void* stream);
 /* Number of instantiated iteration-sequence graphs the fitter holds (diagnostic for the use_hip_graph policy). */
 int32_t nnrt_fitter_graph_count(const nnrt_fitter* fitter);
+/* Schur-corner plan of the prepared frame's arrowhead solve (diagnostic; zeros without ARAP): h_out[6] = corner nodes,
+ * 64-unknown tile columns, factorization launches (elimination-tree levels), back-substitution launches, stored
+ * (structurally non-zero) tiles, lower tiles of the dense corner. */
+nnrt_status nnrt_fitter_corner_info(const nnrt_fitter* fitter, int64_t* h_out);
 /* Store the warp field's current node motion (R, t) in the fitter (a device copy on `stream`). */
 nnrt_status nnrt_fitter_snapshot_motion(nnrt_fitter* fitter, nnrt_warp_field* warp_field, void* stream);
 /* Benchmark form of iterate() that runs the general (non-identity) kernels: before every iteration the warp field's

@@ -841,6 +841,20 @@ def test_c3_raster_parity_and_iteration_properties(nn, S, oracle_mod):
     assert (np.linalg.eigvalsh(Hb.astype(np.float64)) > -1e-3 * np.abs(Hb).max()).all()
     assert np.array_equal(dg["residual_mask"], (dg["pixel_faces"] >= 0) & (depth.reshape(-1) > 0))
     assert np.isfinite(dg["updates"]).all()
+    # the full GN iteration against the oracle at 1280x960 / 4.5 M triangles / 3000 nodes (DeformableMeshToImageFitter.cpp:
+    # 111-275): pixel faces exact, residuals, H and g <= 1e-6, updates <= 1e-4
+    _, t_o, dg_o = oracle_fit_scene(oracle_mod, sc, depth, 1)
+    _compare_iteration(dg_o, dg, 6, N)
+    assert rel_err(wf.get_node_translations(True), t_o) < 1e-4
+    # SURVEY 8(d) C3's parity condition (A4, PixelVertexAnchorJacobiansImpl.h:33, :348-358): no node's pixel list reaches
+    # the reference's 4000-entry cap, so its capped lists hold the same associations as the uncapped math here
+    a, _ = ft.anchors(len(sc.points), 4)
+    sel = dg["residual_mask"] & (dg["pixel_faces"] >= 0)
+    fn = np.sort(a[sc.faces[dg["pixel_faces"][sel].astype(np.int64)]].reshape(int(sel.sum()), -1), axis=1)
+    uniq = (fn >= 0) & np.concatenate([np.ones((len(fn), 1), bool), fn[:, 1:] != fn[:, :-1]], axis=1)
+    per_node = np.bincount(fn[uniq], minlength=N)
+    print(f"C3: {int(sel.sum())} residual pixels, {int(uniq.sum())} associations, max pixels per node {per_node.max()}")
+    assert per_node.max() <= 3999
 
 
 def test_errors_fail_loudly(nn, S, oracle_mod):
