@@ -24,7 +24,7 @@ on its stream; value = all sequences' iterations / the slowest rank's time.
 Also reported: the dominant kernel's roofline (k_fit_pixels_fused: both pixel passes in one launch, HIP-event timed on the fitter's work stream; every
 other kernel of the iteration under "kernels"), the once-per-frame setup time, and the CPU baseline (the oracle/ C++
 restatement with the reference's binned rasterizer, OpenMP, on a bounded sample of the same workload, rank 0, N = 1: one
-socket's physical cores with OMP_PROC_BIND=close as the value, plus this process's CPU share and 1 thread).
+socket's physical cores with OMP_PROC_BIND=close and this process's CPU share, the faster as the value; also 1 thread).
 """
 from __future__ import annotations
 
@@ -240,7 +240,8 @@ def cpu_baseline(sc, depth_host, share_threads: int, budget_s: float, step: str,
     the identity warp. Timed = loop body S1-S12 (DeformableMeshToImageFitter.cpp:111-275), once-per-frame setup
     excluded, as in the GPU step; the rasterizer is the reference's binned one (GridBinNdcTriangles + per-pixel bin loop,
     RasterizeNdcTrianglesImpl.h:187-391), not the oracle's fast K = 1 path. Threads: the physical
-    cores of one socket with OMP_PROC_BIND=close (the headline value), this process's CPU share (16 on the GPU box) and 1."""
+    cores of one socket with OMP_PROC_BIND=close and this process's CPU share (16 on the GPU box) -- the faster of the two is
+    the value, both are listed under "samples" -- and 1."""
     os.environ.setdefault("OMP_PROC_BIND", "close")   # read when the oracle's OpenMP runtime initialises (first load)
     os.environ.setdefault("OMP_PLACES", "cores")
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -248,11 +249,14 @@ def cpu_baseline(sc, depth_host, share_threads: int, budget_s: float, step: str,
     host = host_cpu()
     socket = min(host["cores_per_socket"] or share_threads, len(os.sched_getaffinity(0)))
     refp, refm = O.unproject(depth_host, sc.K, 1.0, 10.0)
-    res = _cpu_sample(O, sc, refp, refm, socket, budget_s, step, iterations, R0, t0)
+    runs = [_cpu_sample(O, sc, refp, refm, socket, budget_s, step, iterations, R0, t0)]
     if share_threads != socket:
-        sh = _cpu_sample(O, sc, refp, refm, share_threads, budget_s, step, iterations, R0, t0)
-        res["cpu_share"] = dict(value=sh["value"], unit=sh["unit"], cores=sh["cores"], ms_per_solve=sh["ms_per_solve"], sample=sh["sample"])
+        runs.append(_cpu_sample(O, sc, refp, refm, share_threads, budget_s, step, iterations, R0, t0))
     one = _cpu_sample(O, sc, refp, refm, 1, single_thread_s, step, iterations, R0, t0, min_timed=1)
+    # value: the faster multi-thread sample (the binned raster does not scale to a whole socket on a shared host)
+    best = max(runs, key=lambda r: r["value"] or 0.0)
+    res = dict(best)
+    res["samples"] = [dict(value=r["value"], cores=r["cores"], ms_per_solve=r["ms_per_solve"], sample=r["sample"]) for r in runs]
     res["single_thread"] = dict(value=one["value"], unit=one["unit"], cores=1, ms_per_solve=one["ms_per_solve"], sample=one["sample"])
     res["host"] = host
     res["omp_proc_bind"] = os.environ.get("OMP_PROC_BIND")

@@ -549,7 +549,7 @@ __device__ inline void eliminate_columns(f32x2 (&ap)[TILE], int lane, int& bad) 
 	}
 }
 
-// development timing build only (-DNNRT_CORNER_STAMPS, tools/dev/corner_stamps.sh): shader-clock stamps of the first
+// development timing build only (-DNNRT_CORNER_STAMPS, tools/dev/stamps_build.sh): shader-clock stamps of the first
 // workgroup of each factor launch at its phase boundaries, read back by nnrt_dev_corner_stamps
 #ifdef NNRT_CORNER_STAMPS
 __device__ unsigned long long g_corner_stamps[256][8];

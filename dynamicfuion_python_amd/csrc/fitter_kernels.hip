@@ -633,15 +633,34 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 // rows; the records and keys go through global memory and are re-read by the same wave (L1 / L2 hits). Fusing removes a
 // launch boundary and lets one wave's pass-2 memory phases overlap other waves' pass-1 arithmetic: C2 17.5 + 25.2 us
 // as two launches -> one launch ~6 us shorter.
+// development timing build only (-DNNRT_FIT_STAMPS, tools/dev/stamps_build.sh): per wave of the fused launch, the
+// constant-rate clock (100 MHz) at its start, after pass 1 and at its end, and its hardware id (CU / SIMD placement)
+#ifdef NNRT_FIT_STAMPS
+__device__ unsigned long long g_fit_stamps[16384][4];
+#define FIT_STAMP(i, v)                                                                                                  \
+	do {                                                                                                                 \
+		const int wid_ = static_cast<int>(blockIdx.x) * (PIX_BLOCK / 64) + static_cast<int>(threadIdx.x >> 6);         \
+		if ((threadIdx.x & 63) == 0 && wid_ < 16384) g_fit_stamps[wid_][i] = (v);                                      \
+	} while (0)
+#else
+#define FIT_STAMP(i, v) \
+	do {                \
+	} while (0)
+#endif
+
 template <int MODE, int MAXK>
 __global__ __launch_bounds__(PIX_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) void k_fit_pixels_fused(FitPixelArgs a) {
 	constexpr int NODE_WORDS = 2 * 8 * NG_STRIDE + 3 * MAXK * 64;
 	constexpr int WORDS = NODE_WORDS > 27 * 64 ? NODE_WORDS : 27 * 64;
 	__shared__ float s_u[PIX_BLOCK / 64][WORDS];
 	const int wave = static_cast<int>(threadIdx.x >> 6), lane = static_cast<int>(threadIdx.x & 63);
+	FIT_STAMP(0, __builtin_amdgcn_s_memrealtime());
+	FIT_STAMP(3, static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11))) |
+	                 (static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11))) << 32));
 	float* w = s_u[wave];
 	int face = -1, vid[3] = {0, 0, 0};
 	pixel_body<MODE>(a, w + lane, 64, face, vid);
+	FIT_STAMP(1, __builtin_amdgcn_s_memrealtime());
 	// the node pass reads the records / keys this wave just stored (other lanes' pixels; same CU, same L1): workgroup-scope
 	// release + acquire (an agent-scope release writes back L2 on gfx950: 10x slower); the LDS region is reused in program
 	// order by the same wave
@@ -649,6 +668,7 @@ __global__ __launch_bounds__(PIX_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) 
 	__builtin_amdgcn_wave_barrier();
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 	node_body<MODE, MAXK>(a, w, w + 8 * NG_STRIDE, reinterpret_cast<uint32_t*>(w + 2 * 8 * NG_STRIDE), face, vid);
+	FIT_STAMP(2, __builtin_amdgcn_s_memrealtime());
 }
 
 #define NNRT_EV(call)                                                                                                   \
@@ -658,6 +678,12 @@ __global__ __launch_bounds__(PIX_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) 
 			return NNRT_ERROR_HIP;                                                                                      \
 		}                                                                                                               \
 	} while (0)
+
+#ifdef NNRT_FIT_STAMPS
+extern "C" int nnrt_dev_fit_stamps(unsigned long long* out) {   // [16384][4] of the last fused launch
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fit_stamps), sizeof(unsigned long long) * 16384 * 4) == hipSuccess ? 0 : 1;
+}
+#endif
 
 nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t stream, hipEvent_t between) {
 	// `between` (stage timing) is recorded before the fused launch: the pixel-pass stage reads 0, the node-pass stage

@@ -1,4 +1,4 @@
-"""Phase timing of the Schur-corner factor launches (development; needs tools/dev/libnnrt_stamps.so from corner_stamps.sh).
+"""Phase timing of the Schur-corner factor launches (development; needs tools/dev/libnnrt_stamps.so: tools/dev/stamps_build.sh NNRT_CORNER_STAMPS tools/dev/libnnrt_stamps.so).
 Runs one C5 GN iteration and prints, per factor launch, the shader-clock cycles of workgroup 0's phases: staging,
 first elimination half, rank-32 update, second half, stores."""
 import ctypes
