@@ -41,6 +41,24 @@ struct Status {
 
 #define NNRT_LAUNCH_CHECK() NNRT_HIP(hipGetLastError())
 
+// Development timing builds only (-DNNRT_KERNEL_STAMPS, tools/dev/stamps_build.sh): per wave of a stamped launch, the
+// constant-rate clock (100 MHz) at its start and end and its hardware id (XCC << 32 | HW_ID), into a per-file __device__
+// array read back by that file's nnrt_dev_<name>_stamps export. The product build compiles the macros to nothing.
+#ifdef NNRT_KERNEL_STAMPS
+#define NNRT_WAVE_STAMP(arr, slot, value)                                                                                  \
+	do {                                                                                                                   \
+		const int wid_ = static_cast<int>(blockIdx.x) * static_cast<int>(blockDim.x >> 6) + static_cast<int>(threadIdx.x >> 6); \
+		if ((threadIdx.x & 63) == 0 && wid_ < 16384) arr[wid_][slot] = (value);                                                \
+	} while (0)
+#define NNRT_STAMP_HWID()                                                                                                  \
+	(static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11))) |                            \
+	 (static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11))) << 32))
+#else
+#define NNRT_WAVE_STAMP(arr, slot, value) \
+	do {                                  \
+	} while (0)
+#endif
+
 constexpr float K_EPSILON = 1e-8f;        // cpp/rendering/kernel/RasterizationConstants.h:24
 constexpr int MAX_ANCHORS = 8;            // cpp/geometry/functional/kernel/Defines.h MAX_ANCHOR_COUNT
 constexpr int MAX_FACES_PER_PIXEL = 8;    // RasterizationConstants.h:20

@@ -252,11 +252,20 @@ __device__ inline float quad_bcast(float x) {
 
 // IDENTITY: every node at R = I, t = 0 without reading them (iterate-from-identity, the benchmark protocol); the
 // arithmetic is the same as with the identity loaded from memory.
+#ifdef NNRT_KERNEL_STAMPS
+__device__ unsigned long long g_warp_stamps[16384][4];
+extern "C" int nnrt_dev_warp_stamps(unsigned long long* out) {
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_warp_stamps), sizeof(g_warp_stamps)) == hipSuccess ? 0 : 1;
+}
+#endif
+
 template <bool IDENTITY>
 __global__ __launch_bounds__(256) void k_warp_mesh_quad(const float* __restrict__ points, const float* __restrict__ normals, int64_t V,
                                                         const float* __restrict__ node_state, const int32_t* __restrict__ anchors,
                                                         const float* __restrict__ weights, int K, WarpExtrinsics E, float4* __restrict__ out_p,
                                                         float4* __restrict__ out_n, float4* __restrict__ jv, float4* __restrict__ jn) {
+	NNRT_WAVE_STAMP(g_warp_stamps, 0, __builtin_amdgcn_s_memrealtime());
+	NNRT_WAVE_STAMP(g_warp_stamps, 3, NNRT_STAMP_HWID());
 	const int64_t tid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
 	const int64_t v = tid >> 2;
 	const int k = static_cast<int>(tid & 3);
@@ -305,6 +314,7 @@ __global__ __launch_bounds__(256) void k_warp_mesh_quad(const float* __restrict_
 		out_p[v] = make_float4(acc[0], acc[1], acc[2], 0.f);
 		out_n[v] = make_float4(acc[3], acc[4], acc[5], 0.f);
 	}
+	NNRT_WAVE_STAMP(g_warp_stamps, 2, __builtin_amdgcn_s_memrealtime());
 }
 
 nnrt_status launch_warp_mesh(const float* points, const float* normals, int64_t V, const float* node_state, const int32_t* anchors,

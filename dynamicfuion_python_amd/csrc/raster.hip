@@ -315,6 +315,13 @@ __device__ inline bool project_mesh_face(const float4* __restrict__ wpos, int4 f
 	return inlier;
 }
 
+#ifdef NNRT_KERNEL_STAMPS
+__device__ unsigned long long g_raster_stamps[16384][4];
+extern "C" int nnrt_dev_raster_stamps(unsigned long long* out) {
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_raster_stamps), sizeof(g_raster_stamps)) == hipSuccess ? 0 : 1;
+}
+#endif
+
 __global__ __launch_bounds__(SCATTER_BLOCK) void k_raster_scatter_mesh(const float4* __restrict__ wpos, const int4* __restrict__ faces4,
                                                                        int64_t F, NdcSetup s, float near_clip, float far_clip, RasterOptions o,
                                                                        uint64_t* __restrict__ keys) {
@@ -323,8 +330,12 @@ __global__ __launch_bounds__(SCATTER_BLOCK) void k_raster_scatter_mesh(const flo
 	const int lane = static_cast<int>(threadIdx.x & 63);
 	const int64_t f = face0 + lane;
 	FaceNdc fn{};
+	NNRT_WAVE_STAMP(g_raster_stamps, 0, __builtin_amdgcn_s_memrealtime());
+	NNRT_WAVE_STAMP(g_raster_stamps, 3, NNRT_STAMP_HWID());
 	const bool ok = lane < SCATTER_FPW && f < F && project_mesh_face(wpos, faces4[f], s, near_clip, far_clip, fn);
+	NNRT_WAVE_STAMP(g_raster_stamps, 1, __builtin_amdgcn_s_memrealtime());
 	scatter_wave(fn, ok, static_cast<int32_t>(face0), o, keys, s_wave[threadIdx.x >> 6]);
+	NNRT_WAVE_STAMP(g_raster_stamps, 2, __builtin_amdgcn_s_memrealtime());
 }
 
 nnrt_status launch_raster_scatter_mesh(const float4* wpos, const int4* faces4, int64_t F, const NdcSetup& s, float near_clip, float far_clip,

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "kernels.hpp"
+#include "mc_table.hpp"
 
 namespace nnrt {
 namespace {
@@ -824,9 +825,8 @@ __global__ void k_and_mask(int* __restrict__ keep, const uint8_t* __restrict__ m
 // only if all 8 corners exist with weight > threshold. Every cube edge is owned by its lower voxel and axis (the
 // reference's edge_shifts): a vertex lives on each owned edge of some valid surface cube, at the zero crossing of the
 // linear interpolation, with the normal interpolated from central-difference tsdf gradients and the color likewise.
-// The triangle table is generated at start-up by tracing the iso-polygon of each of the 256 cube states around the
-// cube faces (ambiguous faces: the inside corners are cut off separately), fan-triangulated, oriented with normals
-// towards positive tsdf -- watertight by construction, since two cubes sharing a face resolve it identically.
+// The triangle table is the published one Open3D indexes (csrc/mc_table.hpp: Lorensen-Cline / Bourke), each triangle
+// emitted in Open3D's vertex order (normals towards positive tsdf).
 // Vertex and triangle order: blocks in buffer order, voxels in block order, owned edges x, y, z -- deterministic.
 // ---------------------------------------------------------------------------------------------------------------------
 constexpr int MC_MAX_TRI = 10;
@@ -840,63 +840,18 @@ __constant__ int8_t c_edge_owner[12][4] = {{0, 0, 0, 0}, {1, 0, 0, 1}, {0, 1, 0,
                                            {0, 1, 1, 0}, {0, 0, 1, 1}, {0, 0, 0, 2}, {1, 0, 0, 2}, {1, 1, 0, 2}, {0, 1, 0, 2}};
 
 McTables build_mc_tables() {
-	static const int corner[8][3] = {{0, 0, 0}, {1, 0, 0}, {1, 1, 0}, {0, 1, 0}, {0, 0, 1}, {1, 0, 1}, {1, 1, 1}, {0, 1, 1}};
 	static const int edge_v[12][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 0}, {4, 5}, {5, 6}, {6, 7}, {7, 4}, {0, 4}, {1, 5}, {2, 6}, {3, 7}};
-	// faces, corners counter-clockwise seen from outside the cube
-	static const int face[6][4] = {{0, 3, 2, 1}, {4, 5, 6, 7}, {0, 1, 5, 4}, {3, 7, 6, 2}, {0, 4, 7, 3}, {1, 2, 6, 5}};
-	(void) corner;
-	auto edge_of = [&](int a, int b) {
-		for (int e = 0; e < 12; e++)
-			if ((edge_v[e][0] == a && edge_v[e][1] == b) || (edge_v[e][0] == b && edge_v[e][1] == a)) return e;
-		return -1;
-	};
 	McTables t{};
 	for (int cfg = 0; cfg < 256; cfg++) {
-		auto inside = [&](int c) { return (cfg >> c) & 1; };
 		uint16_t mask = 0;
 		for (int e = 0; e < 12; e++)
-			if (inside(edge_v[e][0]) != inside(edge_v[e][1])) mask |= static_cast<uint16_t>(1u << e);
+			if (((cfg >> edge_v[e][0]) & 1) != ((cfg >> edge_v[e][1]) & 1)) mask |= static_cast<uint16_t>(1u << e);
 		t.edge_mask[cfg] = mask;
-		int next[12];
-		for (int e = 0; e < 12; e++) next[e] = -1;
-		for (int f = 0; f < 6; f++) {
-			// crossing edges in CCW order: entry (outside -> inside) and exit (inside -> outside)
-			int ed[4], kind[4], n = 0;
-			for (int i = 0; i < 4; i++) {
-				const int a = face[f][i], b = face[f][(i + 1) & 3];
-				if (inside(a) != inside(b)) {
-					ed[n] = edge_of(a, b);
-					kind[n] = inside(b) ? 0 : 1;   // 0 entry, 1 exit
-					n++;
-				}
-			}
-			for (int i = 0; i < n; i++) {
-				if (kind[i] != 0) continue;
-				for (int j = 1; j < n; j++) {   // the next exit in CCW order
-					const int k = (i + j) % n;
-					if (kind[k] == 1) {
-						next[ed[i]] = ed[k];
-						break;
-					}
-				}
-			}
-		}
 		int nt = 0;
-		bool used[12] = {false};
-		for (int e0 = 0; e0 < 12; e0++) {
-			if (!(mask & (1u << e0)) || used[e0]) continue;
-			int loop[12], ln = 0, e = e0;
-			while (!used[e]) {
-				used[e] = true;
-				loop[ln++] = e;
-				e = next[e];
-			}
-			for (int i = 1; i + 1 < ln; i++) {
-				t.tri[cfg][3 * nt] = static_cast<int8_t>(loop[0]);
-				t.tri[cfg][3 * nt + 1] = static_cast<int8_t>(loop[i]);
-				t.tri[cfg][3 * nt + 2] = static_cast<int8_t>(loop[i + 1]);
-				nt++;
-			}
+		for (int i = 0; i < 16 && MC_TRI_TABLE[cfg][i] >= 0; i += 3, nt++) {   // (a, b, c) -> (a, c, b), as Open3D emits
+			t.tri[cfg][3 * nt] = MC_TRI_TABLE[cfg][i];
+			t.tri[cfg][3 * nt + 1] = MC_TRI_TABLE[cfg][i + 2];
+			t.tri[cfg][3 * nt + 2] = MC_TRI_TABLE[cfg][i + 1];
 		}
 		t.tri[cfg][3 * nt] = -1;
 		t.ntri[cfg] = static_cast<int8_t>(nt);
@@ -1669,7 +1624,7 @@ nnrt_status nnrt_voxel_grid_copy_mesh(const nnrt_voxel_grid* vg, float* d_vertic
 	return NNRT_OK;
 }
 
-// the generated marching-cubes triangle table (host copy, for tests): tri [256][31] int8 (edge triples, -1 terminated)
+// the marching-cubes triangle table in emission order (host copy, for tests): tri [256][31] int8 (edge triples, -1 terminated)
 nnrt_status nnrt_marching_cubes_table(int8_t* h_tri, uint16_t* h_edge_mask) {
 	NNRT_CHECK_ARG(h_tri || h_edge_mask, "null output");
 	const McTables t = build_mc_tables();

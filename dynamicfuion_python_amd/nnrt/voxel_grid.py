@@ -295,7 +295,8 @@ def get_axis_aligned_boxes_intersecting_surface_mask(boxes, depth, intrinsics, d
 
 
 def marching_cubes_table():
-    """The generated triangle table: tri [256, 31] int8 edge triples (-1 terminated), edge mask [256] uint16."""
+    """The marching-cubes triangle table in emission order (the published Lorensen-Cline / Bourke table Open3D indexes,
+    each triangle (a, b, c) as (a, c, b)): tri [256, 31] int8 edge triples (-1 terminated), edge mask [256] uint16."""
     tri = np.zeros((256, 31), np.int8)
     mask = np.zeros(256, np.uint16)
     N.check(N.lib().nnrt_marching_cubes_table(N.ptr(tri), N.ptr(mask)))

@@ -420,7 +420,8 @@ nnrt_status nnrt_voxel_grid_extract_triangle_mesh(nnrt_voxel_grid* grid, float w
                                                   int64_t* h_triangle_count, void* stream);
 nnrt_status nnrt_voxel_grid_copy_mesh(const nnrt_voxel_grid* grid, float* d_vertices, float* d_normals, float* d_colors,
                                       int64_t* d_triangles, void* stream);
-/* the generated marching-cubes tables (host): tri [256][31] int8 edge triples (-1 terminated), edge mask [256] */
+/* the marching-cubes tables (host): tri [256][31] int8 edge triples in emission order (-1 terminated; the published
+ * Lorensen-Cline / Bourke table Open3D indexes, each triangle (a, b, c) emitted as (a, c, b)), edge mask [256] */
 nnrt_status nnrt_marching_cubes_table(int8_t* h_tri, uint16_t* h_edge_mask);
 
 #ifdef __cplusplus

@@ -722,6 +722,13 @@ def boxes_mask(boxes, depth, K, scale, dmax, stride, trunc):
     return out
 
 
+def marching_cubes_table():
+    """The oracle's marching-cubes table in emission order: tri [256, 16] int8 edge triples, -1 terminated."""
+    tri = np.full((256, 16), -1, np.int8)
+    _check(lib().orc_marching_cubes_table(_p(tri)))
+    return tri
+
+
 def backproject_depth(depth, fx, fy, cx, cy, normalizer=1.0):
     """image_proc.cpp:275-302 (uint16, depth = d / normalizer) and :312-339 (float32, normalizer 1) in float32 numpy: each
     operation is one correctly rounded IEEE op, in the reference's order ((depth * (x - cx)) / fx), so the GPU kernel is

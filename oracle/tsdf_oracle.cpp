@@ -9,12 +9,13 @@
 //   * the Open3D 0.17 kernels NNRT's VoxelBlockGrid calls (HashMap::Activate, voxel_grid::DepthTouch / Integrate /
 //     ExtractTriangleMesh) -- third-party, absent from the reference tree: restated from Open3D's published algorithm
 //     (the DepthTouch sampling and the Integrate update are also exercised by the IntegrateNonRigid KAT, whose volume is
-//     built with them); the marching-cubes triangulation is this project's generated table (parity with Open3D's table
-//     unpinned).
+//     built with them); the marching-cubes triangulation is the published Lorensen-Cline / Bourke table Open3D indexes
+//     (mc_table_oracle.hpp; no Open3D output fixture exists here, so mesh parity with Open3D stays unpinned).
 // Deterministic policies (shared with the HIP path by specification, not by code): blocks are numbered in first-
 // activation order (first occurrence within an activation call); anchors of a voxel are the K nearest nodes among those
 // within 2 * (largest) coverage, ascending node order, replace-the-maximum insertion.
 // =====================================================================================================================
+#include "mc_table_oracle.hpp"
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
@@ -216,8 +217,8 @@ void blend(const Field& f, const int* idx, const float* w, const float* p, float
 	}
 }
 
-// ---- marching-cubes table: iso-polygons traced around the cube faces (independent restatement of the product's rule:
-// ambiguous faces cut their inside corners off separately; polygons fan-triangulated; normals toward positive tsdf) ----
+// ---- marching-cubes table: the published Lorensen-Cline / Bourke table Open3D indexes (oracle copy: mc_table_oracle.hpp);
+// each triangle (a, b, c) is emitted as (a, c, b), as Open3D emits it (faces away from negative tsdf) ----
 struct McTable {
 	uint16_t mask[256];
 	std::vector<int> tri[256];
@@ -227,44 +228,13 @@ const McTable& mc_table() {
 	static bool built = false;
 	if (built) return T;
 	const int ev[12][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 0}, {4, 5}, {5, 6}, {6, 7}, {7, 4}, {0, 4}, {1, 5}, {2, 6}, {3, 7}};
-	const int faces[6][4] = {{0, 3, 2, 1}, {4, 5, 6, 7}, {0, 1, 5, 4}, {3, 7, 6, 2}, {0, 4, 7, 3}, {1, 2, 6, 5}};
 	for (int cfg = 0; cfg < 256; cfg++) {
-		std::map<int, int> succ;   // entry edge -> paired exit edge
 		uint16_t mask = 0;
 		for (int e = 0; e < 12; e++)
 			if (((cfg >> ev[e][0]) & 1) != ((cfg >> ev[e][1]) & 1)) mask |= static_cast<uint16_t>(1 << e);
-		for (const auto& fc : faces) {
-			std::vector<std::pair<int, bool>> cross;   // (edge, is_entry) in CCW order
-			for (int i = 0; i < 4; i++) {
-				const int a = fc[i], b = fc[(i + 1) % 4];
-				const bool ia = (cfg >> a) & 1, ib = (cfg >> b) & 1;
-				if (ia == ib) continue;
-				int e = 0;
-				while (!((ev[e][0] == a && ev[e][1] == b) || (ev[e][0] == b && ev[e][1] == a))) e++;
-				cross.push_back({e, ib});
-			}
-			for (size_t i = 0; i < cross.size(); i++) {
-				if (!cross[i].second) continue;
-				for (size_t j = 1; j < cross.size(); j++) {
-					const auto& c = cross[(i + j) % cross.size()];
-					if (!c.second) {
-						succ[cross[i].first] = c.first;
-						break;
-					}
-				}
-			}
-		}
 		T.mask[cfg] = mask;
-		std::vector<bool> seen(12, false);
-		for (int e0 = 0; e0 < 12; e0++) {
-			if (!(mask >> e0 & 1) || seen[e0]) continue;
-			std::vector<int> loop;
-			for (int e = e0; !seen[e]; e = succ[e]) {
-				seen[e] = true;
-				loop.push_back(e);
-			}
-			for (size_t i = 1; i + 1 < loop.size(); i++) T.tri[cfg].insert(T.tri[cfg].end(), {loop[0], loop[i], loop[i + 1]});
-		}
+		for (int i = 0; i < 16 && ORC_MC_TRI_TABLE[cfg][i] >= 0; i += 3)
+			T.tri[cfg].insert(T.tri[cfg].end(), {ORC_MC_TRI_TABLE[cfg][i], ORC_MC_TRI_TABLE[cfg][i + 2], ORC_MC_TRI_TABLE[cfg][i + 1]});
 	}
 	built = true;
 	return T;
@@ -671,4 +641,12 @@ ORC_API void orc_grid_set_values(void* h, const float* tsdf, const float* weight
 	Grid* g = static_cast<Grid*>(h);
 	std::copy(tsdf, tsdf + g->tsdf.size(), g->tsdf.begin());
 	std::copy(weight, weight + g->weight.size(), g->weight.begin());
+}
+
+// the table in emission order (tests): tri [256][16] int8 edge triples, -1 terminated
+ORC_API int orc_marching_cubes_table(int8_t* tri) {
+	const McTable& T = mc_table();
+	for (int cfg = 0; cfg < 256; cfg++)
+		for (int i = 0; i < 16; i++) tri[16 * cfg + i] = i < static_cast<int>(T.tri[cfg].size()) ? static_cast<int8_t>(T.tri[cfg][i]) : -1;
+	return 0;
 }

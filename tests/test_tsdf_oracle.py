@@ -83,3 +83,78 @@ def _sphere_fill(O, g, tsdf):
     lib.orc_grid_set_values.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     w = np.ones_like(tsdf)
     lib.orc_grid_set_values(g.h, tsdf.ctypes.data, w.ctypes.data)
+
+
+CUBE_CORNERS = [(0, 0, 0), (1, 0, 0), (1, 1, 0), (0, 1, 0), (0, 0, 1), (1, 0, 1), (1, 1, 1), (0, 1, 1)]
+CUBE_EDGES = [(0, 1), (1, 2), (2, 3), (3, 0), (4, 5), (5, 6), (6, 7), (7, 4), (0, 4), (1, 5), (2, 6), (3, 7)]
+
+
+def _mc_python(vol, tri):
+    """Marching cubes in plain Python with a [256, >=16] emission-order table (bit c: corner c has value < 0)."""
+    verts, tris, states = {}, [], set()
+    nx, ny, nz = vol.shape
+
+    def vid(x, y, z, e):
+        a, b = CUBE_EDGES[e]
+        p = (x + CUBE_CORNERS[a][0], y + CUBE_CORNERS[a][1], z + CUBE_CORNERS[a][2])
+        q = (x + CUBE_CORNERS[b][0], y + CUBE_CORNERS[b][1], z + CUBE_CORNERS[b][2])
+        key = (min(p, q), max(p, q))
+        if key not in verts:
+            r = (0.0 - vol[p]) / (vol[q] - vol[p])
+            verts[key] = (len(verts), np.array(p, float) + r * (np.array(q, float) - np.array(p, float)))
+        return verts[key][0]
+
+    for x in range(nx - 1):
+        for y in range(ny - 1):
+            for z in range(nz - 1):
+                idx = sum(1 << c for c in range(8) if vol[x + CUBE_CORNERS[c][0], y + CUBE_CORNERS[c][1], z + CUBE_CORNERS[c][2]] < 0)
+                states.add(idx)
+                row = tri[idx]
+                for t in range(0, len(row), 3):
+                    if row[t] < 0:
+                        break
+                    tris.append(tuple(vid(x, y, z, int(e)) for e in row[t:t + 3]))
+    V = np.zeros((len(verts), 3))
+    for i, p in verts.values():
+        V[i] = p
+    return V, np.array(tris, np.int64), states
+
+
+def test_marching_cubes_table_is_the_published_one(oracle_mod):
+    """The product's and the oracle's marching-cubes tables (csrc/mc_table.hpp, oracle/mc_table_oracle.hpp: the published
+    Lorensen-Cline / Bourke table that Open3D's ExtractTriangleMesh indexes, VoxelBlockGrid.cpp:461-497) are equal in
+    emission order; every cube state uses exactly its crossing edges; random volumes -- every one of the 256 states --
+    give closed, consistently oriented surfaces whose triangles face away from negative values. Topology parity with
+    Open3D's own meshes stays unpinned (no Open3D output exists here)."""
+    from dynamicfuion_python_amd.nnrt.voxel_grid import marching_cubes_table
+    tri_p, mask_p = marching_cubes_table()
+    tri_o = oracle_mod.marching_cubes_table()
+    for cfg in range(256):   # the product's rows end at their first -1
+        end = int(np.argmax(tri_p[cfg] < 0))
+        assert np.array_equal(tri_p[cfg, :end], tri_o[cfg, :end]) and (tri_o[cfg, end:] == -1).all(), cfg
+    ntri = [(tri_o[c] >= 0).sum() // 3 for c in range(256)]
+    assert max(ntri) == 5 and ntri[0] == ntri[255] == 0
+    for cfg in range(256):
+        inside = [(cfg >> c) & 1 for c in range(8)]
+        cross = {e for e, (a, b) in enumerate(CUBE_EDGES) if inside[a] != inside[b]}
+        assert set(int(e) for e in tri_o[cfg] if e >= 0) == cross, cfg
+        assert mask_p[cfg] == sum(1 << e for e in cross)
+    rng = np.random.default_rng(3)
+    seen = set()
+    for _ in range(4):
+        vol = rng.uniform(-1, 1, (12, 12, 12))
+        vol[[0, -1], :, :] = vol[:, [0, -1], :] = vol[:, :, [0, -1]] = 1.0   # outside on the border: closed surfaces
+        V, T, states = _mc_python(vol, tri_o)
+        seen |= states
+        directed = {}
+        for t in T:
+            for a, b in ((t[0], t[1]), (t[1], t[2]), (t[2], t[0])):
+                directed[(a, b)] = directed.get((a, b), 0) + 1
+        assert all(c == 1 for c in directed.values()), "inconsistent orientation"
+        assert all((b, a) in directed for (a, b) in directed), "open boundary"
+    n = 20
+    g = np.mgrid[0:n, 0:n, 0:n].transpose(1, 2, 3, 0).astype(float)
+    V, T, _ = _mc_python(np.linalg.norm(g - 9.5, axis=-1) - 6.3, tri_o)
+    fn = np.cross(V[T[:, 1]] - V[T[:, 0]], V[T[:, 2]] - V[T[:, 0]])
+    assert (np.einsum("ij,ij->i", fn, V[T].mean(1) - 9.5) > 0).all()
+    assert len(seen) >= 250
