@@ -552,6 +552,12 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 
 } // namespace
 
+// [a, a + na) and [b, b + nb) share a byte
+inline bool ranges_overlap(const void* a, size_t na, const void* b, size_t nb) {
+	const uintptr_t x = reinterpret_cast<uintptr_t>(a), y = reinterpret_cast<uintptr_t>(b);
+	return na > 0 && nb > 0 && x < y + nb && y < x + na;
+}
+
 extern "C" {
 
 void nnrt_fitter_default_params(nnrt_fitter_params* p) {
@@ -1452,7 +1458,8 @@ nnrt_status nnrt_block_sparse_and_vector_product(const float* d_blocks, const in
 	NNRT_CHECK_ARG(block_count >= 0 && block_size > 0 && vector_length >= 0 && m >= 0, "bad size");
 	NNRT_CHECK_ARG(m % block_size == 0, "output length m must be a multiple of the block size");
 	NNRT_CHECK_ARG((m == 0 || d_out) && (block_count == 0 || (d_blocks && d_coordinates && d_vector)), "null pointer");
-	NNRT_CHECK_ARG(m == 0 || static_cast<const void*>(d_out) != static_cast<const void*>(d_vector), "d_out must not alias d_vector (it is zeroed first)");
+	NNRT_CHECK_ARG(m == 0 || block_count == 0 || !ranges_overlap(d_out, sizeof(float) * m, d_vector, sizeof(float) * vector_length),
+	               "d_out must not overlap d_vector (it is zeroed first)");
 	hipStream_t s = static_cast<hipStream_t>(stream);
 	return with_device_flag(s, NNRT_ERROR_ARGUMENT, "block coordinate outside the matrix in BlockSparseAndVectorProduct", [&](int* flag) {
 		return launch_block_sparse_vector(d_blocks, d_coordinates, block_count, block_size, block_row_offset, block_column_offset, transpose != 0,
@@ -1500,6 +1507,9 @@ nnrt_status nnrt_invert_triangular_blocks(const float* d_blocks, int32_t block_c
                                           void* stream) {
 	NNRT_CHECK_ARG(block_count >= 0 && block_size > 0, "bad block count or block size");
 	NNRT_CHECK_ARG(block_count == 0 || (d_blocks && d_out), "null pointer");
+	const size_t bytes = sizeof(float) * static_cast<size_t>(block_count) * block_size * block_size;
+	NNRT_CHECK_ARG(block_count == 0 || !ranges_overlap(d_out, bytes, d_blocks, bytes),
+	               "d_out must not overlap d_blocks (each block's inverse is built column by column while its entries are read)");
 	hipStream_t s = static_cast<hipStream_t>(stream);
 	return with_device_flag(s, NNRT_ERROR_NOT_POSITIVE_DEFINITE, "trtri failed in InvertTriangularBlocks (zero on a block diagonal)",
 	                        [&](int* flag) { return launch_invert_triangular_blocks(d_blocks, block_count, block_size, upper != 0, d_out, flag, s); });

@@ -308,7 +308,8 @@ nnrt_status nnrt_matmul_block_sparse(const float* d_a_blocks, int32_t a_block_co
                                      const int16_t* d_b_breadboard, int32_t b_block_rows, int32_t b_block_columns, int32_t transpose_b,
                                      int32_t block_size, float* d_c_blocks, uint8_t* d_c_mask, void* stream);
 /* BlockSparseAndVectorProduct (MatmulBlockSparseImpl.h:441-602): out [m] = op(A) v, A given by blocks at coordinates + the
- * (row, column) block offset; transpose places block (i, j) at (j, i) transposed. d_out must not alias d_vector. */
+ * (row, column) block offset; transpose places block (i, j) at (j, i) transposed. d_out must not overlap d_vector
+ * (NNRT_ERROR_ARGUMENT). */
 nnrt_status nnrt_block_sparse_and_vector_product(const float* d_blocks, const int32_t* d_coordinates, int32_t block_count, int32_t block_size,
                                                  int32_t block_row_offset, int32_t block_column_offset, int32_t transpose,
                                                  const float* d_vector, int64_t vector_length, int64_t m, float* d_out, void* stream);
@@ -328,7 +329,7 @@ nnrt_status nnrt_get_sparse_blocks(const float* d_matrix, int64_t rows, int64_t 
 /* TransposeBlocksInPlace (TransposeBlocks.h) */
 nnrt_status nnrt_transpose_blocks_in_place(float* d_blocks, int32_t block_count, int32_t block_size, void* stream);
 /* InvertTriangularBlocks (InvertBlocks.cpp, trtri per block), upper != 0: UpLoTriangular::UPPER; a zero diagonal entry
- * gives NNRT_ERROR_NOT_POSITIVE_DEFINITE (trtri info > 0). */
+ * gives NNRT_ERROR_NOT_POSITIVE_DEFINITE (trtri info > 0). d_out must not overlap d_blocks (NNRT_ERROR_ARGUMENT). */
 nnrt_status nnrt_invert_triangular_blocks(const float* d_blocks, int32_t block_count, int32_t block_size, int32_t upper, float* d_out,
                                           void* stream);
 /* SolveBlockSparseArrowheadCholesky (cpp/core/linalg/SolveBlockSparseArrowheadCholesky.cpp:30-95), 6x6 blocks:

@@ -106,6 +106,23 @@ def test_argument_errors_are_reported(native):
     assert b"ndc_convention" in lib.nnrt_last_error()
 
 
+def test_overlapping_outputs_are_rejected(native):
+    """outputs that overlap an input the kernel still reads are refused before any device work (pointer
+    arithmetic only, so this runs without a GPU): InvertTriangularBlocks into its own blocks, BlockSparseAndVectorProduct
+    into a range overlapping the vector."""
+    lib = native.lib()
+    base = 0x7f0000000000
+    blocks = ctypes.c_void_p(base)
+    # 3 blocks of 6x6 floats = 432 B; an output starting 4 floats in overlaps
+    assert lib.nnrt_invert_triangular_blocks(blocks, 3, 6, 0, ctypes.c_void_p(base + 16), None) == 1
+    assert b"overlap" in lib.nnrt_last_error()
+    coords = ctypes.c_void_p(base + 0x100000)
+    vec = ctypes.c_void_p(base + 0x200000)
+    # vector of 12 floats at vec, output of m = 12 floats starting 8 floats into it
+    assert lib.nnrt_block_sparse_and_vector_product(blocks, coords, 3, 6, 0, 0, 0, vec, 12, 12, ctypes.c_void_p(base + 0x200000 + 32), None) == 1
+    assert b"overlap" in lib.nnrt_last_error()
+
+
 def test_no_cpu_fallback(native, monkeypatch):
     import torch
     monkeypatch.setattr(torch.cuda, "is_available", lambda: False)
