@@ -691,7 +691,14 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	ft->n0 = wf->h.layer_counts.empty() ? N : wf->h.layer_counts[0];
 	if (E > 0) {
 		const int n0 = ft->n0, m = 6 * (N - n0);
-		if ((st = ft->corner.prepare(wf->h.edges.data(), E, n0, N))) return st;
+		{   // corner node positions (virtual order) for the nested-dissection bisection
+			std::vector<float> cpos(3 * static_cast<size_t>(N - n0));
+			for (int a = 0; a < N - n0; a++) {
+				const int64_t o = wf->h.virtual_indices.empty() ? n0 + a : wf->h.virtual_indices[static_cast<size_t>(n0 + a)];
+				for (int c = 0; c < 3; c++) cpos[3 * static_cast<size_t>(a) + c] = wf->nodes_original[3 * static_cast<size_t>(o) + c];
+			}
+			if ((st = ft->corner.prepare(wf->h.edges.data(), E, n0, N, cpos.data()))) return st;
+		}
 		if ((st = ft->wing.ensure(static_cast<size_t>(E) * 36)) || (st = ft->edge_residuals.ensure(3 * static_cast<size_t>(E))) ||
 		    (st = ft->a_diag.ensure(static_cast<size_t>(N) * 36)) || (st = ft->a_dinv.ensure(static_cast<size_t>(n0) * 36)) ||
 		    (st = ft->a_dinvb.ensure(static_cast<size_t>(E) * 36)) ||

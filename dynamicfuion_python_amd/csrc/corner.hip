@@ -3,8 +3,8 @@
 // is the Schur complement of a 2-D node grid: every corner node couples only to the corner nodes it shares a stem node
 // with (and to its own corner edges, >= 3 layers), so S and its factor are sparse. Here:
 //
-//   host (once per hierarchy, CornerSolver::prepare): nested-dissection order of the corner nodes (BFS level-set
-//   separators, leaves of ND_LEAF nodes), every ND group starting on a 64-unknown tile boundary (identity padding), the
+//   host (once per hierarchy, CornerSolver::prepare): nested-dissection order of the corner nodes (coordinate bisection
+//   when node positions are given, else BFS level-set separators; separators thinned; leaves of ND_LEAF nodes), every ND group starting on a 64-unknown tile boundary (identity padding), the
 //   tile structure of L (symbolic factorisation over the tile elimination tree) and its levels (tile columns whose
 //   subtrees are independent share a level);
 //   device: one launch per level (k_corner_factor). Its panel workgroups factor the level's tile columns -- each stages
@@ -23,6 +23,7 @@
 // eliminations in ascending order); the elimination order (nested dissection) differs from the reference's natural
 // order, which changes float rounding only (the tests hold the solve against the oracle and an fp64 solution).
 #include <algorithm>
+#include <cfloat>
 #include <cstring>
 #include <map>
 #include <tuple>
@@ -47,7 +48,8 @@ namespace {
 
 struct Dissection {
 	const std::vector<std::vector<int>>* adj = nullptr;
-	std::vector<int> sub, vis, level;   // epoch marks: subset membership, BFS visit
+	const float* pos = nullptr;         // [nc, 3] corner node positions (nullable: graph-only separators)
+	std::vector<int> sub, vis, level, mark;   // epoch marks: subset membership, BFS visit / side; BFS levels; separator
 	int epoch = 0;
 	std::vector<std::vector<int>> groups;   // elimination order: leaves and separators, post-order
 
@@ -107,7 +109,54 @@ struct Dissection {
 			leaf(std::move(small));
 			return;
 		}
-		// pseudo-peripheral start: repeated BFS from the farthest node while the eccentricity grows
+		std::vector<int> left, right, mid;
+		if (pos ? split_geometric(nodes, left, mid, right) : split_bfs(sep, nodes, left, mid, right)) {
+			refine(left, mid, right);
+			dissect(std::move(left));
+			dissect(std::move(right));
+			leaf(std::move(mid));
+		} else {
+			leaf(std::move(nodes));
+		}
+	}
+
+	// separator from coordinate bisection: the half-sets at the median of the longest axis (ties by node index), the
+	// separator the smaller of the two boundary sets (nodes with a neighbour across)
+	bool split_geometric(const std::vector<int>& nodes, std::vector<int>& left, std::vector<int>& mid, std::vector<int>& right) {
+		float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+		for (int u : nodes)
+			for (int c = 0; c < 3; c++) {
+				lo[c] = std::min(lo[c], pos[3 * u + c]);
+				hi[c] = std::max(hi[c], pos[3 * u + c]);
+			}
+		int ax = 0;
+		for (int c = 1; c < 3; c++)
+			if (hi[c] - lo[c] > hi[ax] - lo[ax]) ax = c;
+		std::vector<int> order(nodes);
+		std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return pos[3 * x + ax] < pos[3 * y + ax]; });
+		const size_t half = order.size() / 2;
+		const int side_l = ++epoch, side_r = ++epoch;
+		for (size_t i = 0; i < order.size(); i++) vis[order[i]] = i < half ? side_l : side_r;
+		std::vector<int> bl, br;
+		for (int u : nodes) {
+			const int other = vis[u] == side_l ? side_r : side_l;
+			bool across = false;
+			for (int v : (*adj)[u]) across |= vis[v] == other;
+			if (across) (vis[u] == side_l ? bl : br).push_back(u);
+		}
+		const bool use_l = bl.size() <= br.size();
+		const int sep_ep = ++epoch;
+		for (int u : use_l ? bl : br) mark[u] = sep_ep;
+		for (int u : nodes) {
+			if (mark[u] == sep_ep) mid.push_back(u);
+			else (vis[u] == side_l ? left : right).push_back(u);
+		}
+		return !left.empty() && !right.empty();
+	}
+
+	// separator from BFS level sets: the level at which the cumulative count first reaches half the nodes, BFS from a
+	// pseudo-peripheral node (repeated BFS from the farthest node while the eccentricity grows)
+	bool split_bfs(int sep, const std::vector<int>& nodes, std::vector<int>& left, std::vector<int>& mid, std::vector<int>& right) {
 		std::vector<int> order;
 		int start = nodes.front();
 		bfs(sep, start, order);
@@ -123,8 +172,7 @@ struct Dissection {
 		}
 		bfs(sep, start, order);
 		const int L = level[order.back()];
-		if (L < 2) return leaf(std::move(nodes));
-		// separator: the BFS level at which the cumulative count first reaches half the nodes (level sets separate)
+		if (L < 2) return false;
 		std::vector<int> cnt(static_cast<size_t>(L) + 1, 0);
 		for (int u : nodes) cnt[static_cast<size_t>(level[u])]++;
 		int s = 0, cum = 0;
@@ -133,11 +181,40 @@ struct Dissection {
 			if (2 * cum >= static_cast<int>(nodes.size())) break;
 		}
 		s = std::min(std::max(s, 1), L - 1);
-		std::vector<int> left, right, mid;
 		for (int u : nodes) (level[u] < s ? left : level[u] > s ? right : mid).push_back(u);
-		dissect(std::move(left));
-		dissect(std::move(right));
-		leaf(std::move(mid));
+		return true;
+	}
+
+	// a separator node with no neighbour on one side joins the other side (repeat until none moves): thinner separators,
+	// shorter chains at the top of the elimination tree
+	void refine(std::vector<int>& left, std::vector<int>& mid, std::vector<int>& right) {
+		const int el = ++epoch, er = ++epoch, em = ++epoch;
+		for (int u : left) vis[u] = el;
+		for (int u : right) vis[u] = er;
+		for (int u : mid) vis[u] = em;
+		for (bool moved = true; moved;) {
+			moved = false;
+			std::vector<int> keep;
+			for (int u : mid) {
+				bool nl = false, nr = false;
+				for (int v : (*adj)[u]) {
+					nl |= vis[v] == el;
+					nr |= vis[v] == er;
+				}
+				if (!nr) {
+					vis[u] = el;
+					left.push_back(u);
+					moved = true;
+				} else if (!nl) {
+					vis[u] = er;
+					right.push_back(u);
+					moved = true;
+				} else {
+					keep.push_back(u);
+				}
+			}
+			mid.swap(keep);
+		}
 	}
 };
 
@@ -159,7 +236,7 @@ struct CornerPlan {
 	std::vector<int> corner_edges;    // edges between two corner nodes (>= 3 layers)
 };
 
-static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N) {
+static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const float* corner_pos) {
 	CornerPlan p;
 	const int nc = N - n0;
 	p.nc = nc;
@@ -187,6 +264,8 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N) {
 	// nested dissection
 	Dissection nd;
 	nd.adj = &adj;
+	nd.pos = corner_pos;
+	nd.mark.assign(static_cast<size_t>(nc), 0);
 	nd.sub.assign(static_cast<size_t>(nc), 0);
 	nd.vis.assign(static_cast<size_t>(nc), 0);
 	nd.level.assign(static_cast<size_t>(nc), 0);
@@ -812,13 +891,19 @@ void CornerSolver::release() {
 	key.clear();
 }
 
-nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N) {
+nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, const float* corner_pos) {
 	std::vector<int32_t> k(edges, edges + 2 * static_cast<size_t>(E));
 	k.push_back(n0);
 	k.push_back(N);
+	if (corner_pos) {   // the plan depends on the positions too
+		const size_t nf = 3 * static_cast<size_t>(std::max(N - n0, 0));
+		const size_t at = k.size();
+		k.resize(at + nf);
+		std::memcpy(k.data() + at, corner_pos, sizeof(float) * nf);
+	}
 	if (k == key && (nc == 0 || tiles)) return NNRT_OK;   // same hierarchy: keep the plan and its buffers
 	release();
-	const CornerPlan p = plan_corner(edges, E, n0, N);
+	const CornerPlan p = plan_corner(edges, E, n0, N, corner_pos);
 	nc = p.nc;
 	if (nc > 0) {
 		ld = p.ld;

@@ -114,9 +114,10 @@ __device__ inline float* corner_block_entry(const CornerMap& m, int a, int b, in
 class CornerSolver {
 public:
 	~CornerSolver();
-	// host, once per hierarchy (edges [E,2] host, virtual order; corner = nodes >= n0): ordering, symbolic factorisation,
-	// launch plan, device buffers. A repeated call with the same structure keeps everything (stable pointers for graphs).
-	nnrt_status prepare(const int32_t* edges, int E, int n0, int N);
+	// host, once per hierarchy (edges [E,2] host, virtual order; corner = nodes >= n0; corner_pos [N - n0, 3] host or
+	// nullptr): ordering (coordinate bisection with positions, graph separators without), symbolic factorisation, launch
+	// plan, device buffers. A repeated call with the same inputs keeps everything (stable pointers for graphs).
+	nnrt_status prepare(const int32_t* edges, int E, int n0, int N, const float* corner_pos = nullptr);
 	// S = C (+ corner off-diagonal blocks) in the stored tiles, cb = b_C (permuted); diag [N,36], rhs [6N], edges / wing device
 	nnrt_status launch_init(int n0, const float* diag, const float* rhs, const int32_t* edges, const float* wing, hipStream_t s) const;
 	// factor S (after the stem's Schur update), solve S x = cb; x -> xout[6 nc] in corner-node order
