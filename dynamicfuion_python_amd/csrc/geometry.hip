@@ -1,7 +1,5 @@
 // Geometry stages of the hot path on gfx950: anchors (once per frame), mesh warp (+ warped-surface Jacobians),
 // NDC face extraction, depth unprojection, attribute interpolation, Rodrigues.
-#include <cstdlib>
-
 #include "kernels.hpp"
 
 namespace nnrt {
@@ -319,103 +317,10 @@ __global__ __launch_bounds__(256) void k_warp_mesh_quad(const float* __restrict_
 	NNRT_WAVE_STAMP(g_warp_stamps, 2, __builtin_amdgcn_s_memrealtime());
 }
 
-// K <= 4, one lane per vertex: the vertex's anchors and weights as one 16-B load each, then the node records of all its
-// anchors (4 x 64 B) gathered together before any arithmetic (16 loads in flight per lane, one dependent round trip), the
-// slots summed in slot order in the lane (((0 + c0) + c1) + c2) + c3, skipping invalid anchors: the reference's serial
-// order, the same arithmetic as k_warp_mesh_quad), Jv / Jn stored as 64 contiguous bytes per vertex.
-template <bool IDENTITY>
-__global__ __launch_bounds__(256) void k_warp_mesh_v4(const float* __restrict__ points, const float* __restrict__ normals, int64_t V,
-                                                      const float* __restrict__ node_state, const int32_t* __restrict__ anchors,
-                                                      const float* __restrict__ weights, int K, WarpExtrinsics E, float4* __restrict__ out_p,
-                                                      float4* __restrict__ out_n, float4* __restrict__ jv, float4* __restrict__ jn) {
-	const int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-	if (v >= V) return;
-	int a[4];
-	float w[4];
-	if (K == 4) {
-		const int4 a4 = reinterpret_cast<const int4*>(anchors)[v];
-		const float4 w4 = reinterpret_cast<const float4*>(weights)[v];
-		a[0] = a4.x, a[1] = a4.y, a[2] = a4.z, a[3] = a4.w;
-		w[0] = w4.x, w[1] = w4.y, w[2] = w4.z, w[3] = w4.w;
-	} else {
-#pragma unroll
-		for (int k = 0; k < 4; k++) {
-			a[k] = k < K ? anchors[v * K + k] : -1;
-			w[k] = k < K ? weights[v * K + k] : 0.f;
-		}
-	}
-	float4 st[4][4];   // node records (g t R pad), loaded unconditionally (row 0 for an invalid anchor, never used)
-#pragma unroll
-	for (int k = 0; k < 4; k++) {
-		const float4* ns = reinterpret_cast<const float4*>(node_state + static_cast<int64_t>(a[k] >= 0 ? a[k] : 0) * NODE_STRIDE);
-#pragma unroll
-		for (int q = 0; q < (IDENTITY ? 1 : 4); q++) st[k][q] = ns[q];
-	}
-	const f3 p = make3(points[3 * v], points[3 * v + 1], points[3 * v + 2]);
-	const f3 n = make3(normals[3 * v], normals[3 * v + 1], normals[3 * v + 2]);
-	f3 pc = p, nc = n;
-	if (!E.identity) {
-		pc = apply_extrinsics_point(E, p);
-		nc = apply_extrinsics_normal(E, n);
-	}
-	float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-	for (int k = 0; k < 4; k++) {
-		float4 ojv = make_float4(0.f, 0.f, 0.f, 0.f), ojn = make_float4(0.f, 0.f, 0.f, 0.f);
-		if (k < K && a[k] != -1) {
-			f3 g, t;
-			float R[9];
-			g = make3(st[k][0].x, st[k][0].y, st[k][0].z);
-			if constexpr (IDENTITY) {
-				t = make3(0.f, 0.f, 0.f);
-#pragma unroll
-				for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.f : 0.f;
-			} else {
-				t = make3(st[k][0].w, st[k][1].x, st[k][1].y);
-				const float Rl[9] = {st[k][1].z, st[k][1].w, st[k][2].x, st[k][2].y, st[k][2].z, st[k][2].w, st[k][3].x, st[k][3].y, st[k][3].z};
-#pragma unroll
-				for (int i = 0; i < 9; i++) R[i] = Rl[i];
-			}
-			const f3 Rd = matvec3(R, sub3(pc, g));
-			acc[0] += w[k] * ((g.x + Rd.x) + t.x);
-			acc[1] += w[k] * ((g.y + Rd.y) + t.y);
-			acc[2] += w[k] * ((g.z + Rd.z) + t.z);
-			const f3 Rn = matvec3(R, nc);
-			acc[3] += w[k] * Rn.x;
-			acc[4] += w[k] * Rn.y;
-			acc[5] += w[k] * Rn.z;
-			const f3 Rj = E.identity ? Rd : matvec3(R, sub3(p, g));
-			const f3 Rnj = E.identity ? Rn : matvec3(R, n);
-			ojv = make_float4(-w[k] * Rj.x, -w[k] * Rj.y, -w[k] * Rj.z, w[k]);
-			ojn = make_float4(-w[k] * Rnj.x, -w[k] * Rnj.y, -w[k] * Rnj.z, 0.f);
-		}
-		if (jv && k < K) {
-			jv[v * K + k] = ojv;
-			jn[v * K + k] = ojn;
-		}
-	}
-	out_p[v] = make_float4(acc[0], acc[1], acc[2], 0.f);
-	out_n[v] = make_float4(acc[3], acc[4], acc[5], 0.f);
-}
-
 nnrt_status launch_warp_mesh(const float* points, const float* normals, int64_t V, const float* node_state, const int32_t* anchors,
                              const float* weights, int K, const WarpExtrinsics& E, float4* out_p, float4* out_n, float4* jv, float4* jn,
                              hipStream_t stream, bool from_identity) {
 	if (V == 0) return NNRT_OK;
-	static int variant = -1;   // development A/B switch (NNRT_WARP_VARIANT=1: lane per vertex)
-	if (variant < 0) {
-		const char* e = getenv("NNRT_WARP_VARIANT");
-		variant = e ? atoi(e) : 0;
-	}
-	if (K <= 4 && variant == 1) {
-		const unsigned grid = static_cast<unsigned>(ceil_div(V, 256));
-		if (from_identity)
-			k_warp_mesh_v4<true><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n, jv, jn);
-		else
-			k_warp_mesh_v4<false><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n, jv, jn);
-		NNRT_LAUNCH_CHECK();
-		return NNRT_OK;
-	}
 	if (K <= 4) {
 		const unsigned grid = static_cast<unsigned>(ceil_div(4 * V, 256));
 		if (from_identity)

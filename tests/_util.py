@@ -155,3 +155,53 @@ def oracle_fit_scene(O, sc, depth, iterations=1, lm=0.001, modes=("ALL",), R0=No
     return O.fit(nodes=nodes, rotations=R0, translations=t0, mesh_points=sc.points, mesh_normals=sc.normals, faces=sc.faces,
                  ref_points=refp, ref_mask=refm, H=sc.H, W=sc.W, K=sc.K, max_iterations=iterations, lm_factor=lm, modes=modes,
                  coverage=sc.coverage, **hk)
+
+
+def arrowhead_fp64_solution(oracle_mod, sc, R0, t0, dg_o, lm=0.001, arap_weight=200.0, hessian_diag=None, gradient=None):
+    """fp64 solution of the iteration's arrowhead system (DeformableMeshToImageFitter.cpp:222-254), solved by sparse LU
+    in double (arrowhead_fp64_system)."""
+    import scipy.sparse.linalg as spl
+    A, b = arrowhead_fp64_system(oracle_mod, sc, R0, t0, dg_o, lm, arap_weight, hessian_diag, gradient)
+    return spl.spsolve(A, b)
+
+
+def fp64_pivot_ratio(A):
+    """min / max of the fp64 Cholesky pivots (LDLᵀ diagonal) of the symmetric sparse matrix A under a symmetric
+    fill-reducing order; <= 0: not positive definite."""
+    import scipy.sparse.linalg as spl
+    lu = spl.splu(A.tocsc(), permc_spec="MMD_AT_PLUS_A", diag_pivot_thresh=0.0, options=dict(SymmetricMode=True))
+    assert np.array_equal(lu.perm_r, lu.perm_c), "SuperLU pivoted off the diagonal"
+    d = lu.U.diagonal()
+    return float(d.min() / np.abs(d).max())
+
+
+def arrowhead_fp64_system(oracle_mod, sc, R0, t0, dg_o=None, lm=0.001, arap_weight=200.0, hessian_diag=None, gradient=None):
+    """fp64 matrix and right-hand side of the iteration's arrowhead system: data blocks (the oracle's, equal to the
+    GPU's to 1e-6; or `hessian_diag`) + ARAP diagonal and wing blocks (ArapHessianImpl.h; every edge, so with >= 3 layers
+    the corner off-diagonal blocks of sparse_block_cholesky_scripts.py:106-160) + LM, right-hand side = data + ARAP
+    gradient (or `gradient`); assembled from the oracle's stage functions. `sc`: anything with `nodes` (original order)
+    and `hierarchy` (virtual_indices, edges, edge_layers, radii, optional node_weights)."""
+    import scipy.sparse as sp
+    h = sc.hierarchy
+    N = len(sc.nodes)
+    nodes = sc.nodes[h["virtual_indices"]]
+    edges = np.asarray(h["edges"], np.int32)
+    # variable coverage (coverage_method 1): edge weights from the node coverage weights (virtual order)
+    ej = oracle_mod.arap_edge_jacobians(edges, h["edge_layers"], h["radii"], h.get("node_weights"), nodes, R0, arap_weight)
+    adiag, wing = oracle_mod.arap_hessian(edges, ej, N)
+    hd = dg_o["hessian_diag"] if hessian_diag is None else hessian_diag
+    D = adiag.astype(np.float64) + np.asarray(hd).reshape(N, 6, 6).astype(np.float64) + lm * np.eye(6)
+    rows, cols, vals = [], [], []
+    bi, bj = np.meshgrid(np.arange(6), np.arange(6), indexing="ij")
+    for n in range(N):
+        rows.append(6 * n + bi.ravel())
+        cols.append(6 * n + bj.ravel())
+        vals.append(D[n].ravel())
+    for e, (i, j) in enumerate(edges):
+        w = wing[e].astype(np.float64)
+        rows += [6 * i + bi.ravel(), 6 * j + bi.ravel()]
+        cols += [6 * j + bj.ravel(), 6 * i + bj.ravel()]
+        vals += [w.ravel(), w.T.ravel()]
+    A = sp.csc_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))), shape=(6 * N, 6 * N))
+    b = np.asarray(dg_o["gradient"] if gradient is None else gradient).astype(np.float64)
+    return A, b

@@ -4,6 +4,7 @@ DeepDeformGraph nodes (tests/golden/deepdeform), stage by stage against the orac
 Bit-exact: depth back-projection, rigid integration, marching cubes, truncation-region search, non-rigid integration.
 Within the fitter's tolerances: one Gauss-Newton iteration of the canonical mesh against frame 600."""
 import os
+from types import SimpleNamespace
 
 import numpy as np
 import pytest
@@ -12,7 +13,7 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-from _util import rel_err  # noqa: E402
+from _util import arrowhead_fp64_solution, rel_err  # noqa: E402
 
 DD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "deepdeform")
 
@@ -107,8 +108,21 @@ def test_real_frame_pair_stages_vs_oracle(nn, oracle_mod, pair, intr):
     assert np.array_equal(dg_o["residual_mask"], dg["residual_mask"]) and dg["residual_mask"].sum() > 50000
     assert np.allclose(dg_o["residuals"], dg["residuals"], rtol=0, atol=1e-6)
     assert rel_err(dg["gradient"][:N * 6], dg_o["gradient"]) < 1e-6
-    assert rel_err(wf.get_node_translations(True), t_o) < 1e-4
-    assert rel_err(wf.get_node_rotations(True) - np.eye(3), R_o - np.eye(3)) < 1e-4
+    u_err = rel_err(dg["updates"][:N * 6], dg_o["updates"])
+    if u_err >= 1e-4:
+        # the two float32 arrowhead solves (GPU: nested-dissection tile order; oracle: natural order) differ by more than
+        # 1e-4 only on an ill-conditioned system; then the GPU's must be as close to the fp64 solution as the oracle's
+        # (the trajectory tests' rule, tests/test_gpu_parity.py::_synchronised_iteration)
+        sc = SimpleNamespace(nodes=nodes, hierarchy=dict(virtual_indices=vidx_o, edges=edges, edge_layers=elayers,
+                                                        radii=np.array([0.05, 0.1], np.float32)))
+        I3 = np.tile(np.eye(3, dtype=np.float32), (N, 1, 1))
+        x64 = arrowhead_fp64_solution(O, sc, I3, np.zeros((N, 3), np.float32), dg_o)
+        e_g, e_o = rel_err(dg["updates"][:N * 6], x64), rel_err(dg_o["updates"], x64)
+        print(f"fp64 rule: GPU vs fp64 {e_g:.3g}, oracle vs fp64 {e_o:.3g}")
+        assert e_g <= max(2.0 * e_o, 1e-4), f"GPU update {u_err:.3g} from the oracle's; vs fp64 GPU {e_g:.3g}, oracle {e_o:.3g}"
+    else:
+        assert rel_err(wf.get_node_translations(True), t_o) < 1e-4
+        assert rel_err(wf.get_node_rotations(True) - np.eye(3), R_o - np.eye(3)) < 1e-4
     assert np.abs(t_o).max() > 1e-4   # the frames differ: the fit moves the graph
 
     # fuse frame 600 under the GPU-fitted motion (both sides read the same R, t)
@@ -186,14 +200,24 @@ def test_fusion_pipeline_on_real_frames(nn, oracle_mod):
     fx, fy, cx, cy = pipe.fx, pipe.fy, pipe.cx, pipe.cy
     pts = O.backproject_depth(f600.load_depth_image_numpy(), fx, fy, cx, cy, 1000.0).reshape(-1, 3)
     N = len(nodes_v)
-    R_o, t_o, _ = O.fit(nodes=nodes_v, rotations=np.tile(np.eye(3, dtype=np.float32), (N, 1, 1)), translations=np.zeros((N, 3), np.float32),
+    R_o, t_o, dg_o = O.fit(nodes=nodes_v, rotations=np.tile(np.eye(3, dtype=np.float32), (N, 1, 1)), translations=np.zeros((N, 3), np.float32),
                         mesh_points=V, mesh_normals=Nn, faces=T, ref_points=pts, ref_mask=(pts[:, 2] > 0).astype(np.uint8), H=480, W=640,
                         K=pipe.K, max_iterations=1, lm_factor=params.alignment.preconditioning_dampening_factor, coverage=0.05,
                         coverage_method=1, node_weights=weights_v, edges=edges, edge_layers=elayers,
                         radii=np.array([0.05, 0.1], np.float32), first_layer_count=int(counts[0]), ndc_consistent=True)
     t = wf.get_node_translations(True)
     assert np.isfinite(t).all() and np.abs(t).max() > 1e-3
-    assert rel_err(t, t_o) < 1e-4
+    if rel_err(t, t_o) >= 1e-4:
+        # ill-conditioned arrowhead system: both float32 solves are held against its fp64 solution (the trajectory
+        # tests' rule); the translation rows of the update are the node translations (the fit starts at t = 0)
+        sc = SimpleNamespace(nodes=nodes_v, hierarchy=dict(virtual_indices=np.arange(N), edges=edges, edge_layers=elayers,
+                                                          radii=np.array([0.05, 0.1], np.float32), node_weights=weights_v))
+        I3 = np.tile(np.eye(3, dtype=np.float32), (N, 1, 1))
+        x64 = arrowhead_fp64_solution(O, sc, I3, np.zeros((N, 3), np.float32), dg_o,
+                                      lm=params.alignment.preconditioning_dampening_factor).reshape(N, 6)[:, 3:]
+        e_g, e_o = rel_err(t, x64), rel_err(t_o, x64)
+        print(f"fp64 rule: GPU vs fp64 {e_g:.3g}, oracle vs fp64 {e_o:.3g}")
+        assert e_g <= max(2.0 * e_o, 1e-4), f"translations {rel_err(t, t_o):.3g} from the oracle's; vs fp64 GPU {e_g:.3g}, oracle {e_o:.3g}"
     # the ramp asks for weight > 1 after two frames: only voxels observed in both frames under the fitted motion qualify
     assert pipe.mesh_extraction_threshold() == 1
     assert (pipe.warped_mesh is None) == (pipe.canonical_mesh.triangle_indices.shape[0] == 0)

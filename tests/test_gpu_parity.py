@@ -15,7 +15,8 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-from _util import FIXTURES, oracle_fit_scene, read_ply, rel_err, scene_target, transform_mesh, xy_plane  # noqa: E402
+from _util import (FIXTURES, arrowhead_fp64_solution, arrowhead_fp64_system, fp64_pivot_ratio, oracle_fit_scene, read_ply,  # noqa: E402
+                   rel_err, scene_target, transform_mesh, xy_plane)
 from golden import kat_literals as L  # noqa: E402
 
 
@@ -316,9 +317,25 @@ def _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k):
     try:
         R_o, t_o, dg_o = oracle_fit_scene(oracle_mod, sc, depth, 1, R0=R0, t0=t0, raise_on_failure=False)
         oracle_failed = dg_o["status"] != 0
-    except RuntimeError:   # the arrowhead solve aborts without diagnostics
-        oracle_failed, dg_o = True, None
-    assert gpu_failed == oracle_failed, f"iteration {k + 1}: GPU potrf failure {gpu_failed}, oracle {oracle_failed}"
+    except RuntimeError as e:   # the arrowhead solve aborts without diagnostics
+        oracle_failed, dg_o, oracle_msg = True, None, str(e)
+    else:
+        oracle_msg = ""
+    if gpu_failed != oracle_failed:
+        # Only one float32 factorization broke down. Allowed only on an arrowhead system that is positive definite but so
+        # ill-conditioned in fp64 that a float32 Cholesky's success depends on its elimination order (the GPU's
+        # nested-dissection corner vs the oracle's natural order); the trajectory ends there (the reference raises on
+        # one side only, so later states have no counterpart).
+        msg = (f"iteration {k + 1}: GPU potrf failure {gpu_failed}, oracle {oracle_failed} ({oracle_msg}); GPU H / g / updates "
+               f"non-finite: {int((~np.isfinite(dg_g['hessian'])).sum())} / {int((~np.isfinite(dg_g['gradient'])).sum())} / "
+               f"{int((~np.isfinite(dg_g['updates'])).sum())}")
+        assert sc.layer_count > 1, msg
+        A, _ = arrowhead_fp64_system(oracle_mod, sc, R0, t0, hessian_diag=dg_g["hessian"][: N * 36], gradient=dg_g["gradient"][: 6 * N])
+        ratio = fp64_pivot_ratio(A)
+        assert 0.0 < ratio < 1e-6, f"{msg}; fp64 min / max Cholesky pivot {ratio:.3g}"
+        if not gpu_failed:
+            assert np.isfinite(dg_g["updates"][: 6 * N]).all(), msg
+        return f"potrf ({'oracle' if oracle_failed else 'GPU'} only: fp64 pivot ratio {ratio:.2g})", None
     if gpu_failed:
         if dg_o is not None:   # block-diagonal: the same blocks fail (NaN updates), every other node's update agrees
             u_g, u_o = dg_g["updates"][: 6 * N], dg_o["updates"]
@@ -332,7 +349,7 @@ def _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k):
         # Ill-conditioned arrowhead system: two float32 solves with different blockings cannot agree to 1e-4 (the GPU
         # factors the dense Schur corner with MFMA tiles, the oracle serially). Both are held against the fp64 solution
         # of the same system instead: the GPU's solve must be as accurate as the reference-order float solve.
-        x64 = _arrowhead_fp64_solution(oracle_mod, sc, R0, t0, dg_o)
+        x64 = arrowhead_fp64_solution(oracle_mod, sc, R0, t0, dg_o)
         e_g = nan_rel_err(dg_g["updates"][: 6 * N], x64)
         e_o = nan_rel_err(dg_o["updates"], x64)
         assert e_g <= max(2.0 * e_o, 1e-4), f"iteration {k + 1}: GPU solve error {e_g:.3g} vs fp64, oracle float solve {e_o:.3g}"
@@ -362,38 +379,6 @@ def _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k):
     return ("ok" if nan_nodes == 0 else f"ok, {nan_nodes} NaN rotations (A7)") + solve_note, u_err
 
 
-def _arrowhead_fp64_solution(oracle_mod, sc, R0, t0, dg_o, lm=0.001, arap_weight=200.0, hessian_diag=None, gradient=None):
-    """fp64 solution of the iteration's arrowhead system (DeformableMeshToImageFitter.cpp:222-254): data blocks (the
-    oracle's, equal to the GPU's to 1e-6; or `hessian_diag`) + ARAP diagonal and wing blocks (ArapHessianImpl.h; every
-    edge, so with >= 3 layers the corner off-diagonal blocks of sparse_block_cholesky_scripts.py:106-160) + LM, right-hand
-    side = data + ARAP gradient (or `gradient`); assembled from the oracle's stage functions, solved by sparse LU in
-    double."""
-    import scipy.sparse as sp
-    import scipy.sparse.linalg as spl
-    h = sc.hierarchy
-    N = len(sc.nodes)
-    nodes = sc.nodes[h["virtual_indices"]]
-    edges = np.asarray(h["edges"], np.int32)
-    ej = oracle_mod.arap_edge_jacobians(edges, h["edge_layers"], h["radii"], None, nodes, R0, arap_weight)
-    adiag, wing = oracle_mod.arap_hessian(edges, ej, N)
-    hd = dg_o["hessian_diag"] if hessian_diag is None else hessian_diag
-    D = adiag.astype(np.float64) + np.asarray(hd).reshape(N, 6, 6).astype(np.float64) + lm * np.eye(6)
-    rows, cols, vals = [], [], []
-    bi, bj = np.meshgrid(np.arange(6), np.arange(6), indexing="ij")
-    for n in range(N):
-        rows.append(6 * n + bi.ravel())
-        cols.append(6 * n + bj.ravel())
-        vals.append(D[n].ravel())
-    for e, (i, j) in enumerate(edges):
-        w = wing[e].astype(np.float64)
-        rows += [6 * i + bi.ravel(), 6 * j + bi.ravel()]
-        cols += [6 * j + bj.ravel(), 6 * i + bj.ravel()]
-        vals += [w.ravel(), w.T.ravel()]
-    A = sp.csc_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))), shape=(6 * N, 6 * N))
-    b = np.asarray(dg_o["gradient"] if gradient is None else gradient).astype(np.float64)
-    return spl.spsolve(A, b)
-
-
 def _new_fit(nn, sc, depth, iterations):
     G, A = nn.geometry, nn.alignment
     wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE,
@@ -409,8 +394,11 @@ def _new_fit(nn, sc, depth, iterations):
 # the GPU and in the oracle alike. The ARAP configs run until the arrowhead system degenerates (A7 NaN rotations,
 # condition > 1e9); wherever a potrf failure occurs, both implementations must hit it in the same iteration. C5: the
 # GPU's iteration-3 solve lies closer to the fp64 solution than the oracle's float solve (5.4e-4 vs 8.3e-4), and from
-# the state it reaches both implementations raise potrf at iteration 4 (7 A7 NaN rotations by then).
-TRAJECTORIES = [("S1", 6, 6, None), ("C2", 2, 1, 2), ("C2_ARAP", 10, 6, None), ("C5", 6, 3, None)]
+# the state it reaches both implementations raise potrf at iteration 4 (7 A7 NaN rotations by then). C2_ARAP: after
+# iteration 4 (condition ~1e9, both float solves 0.14 from fp64, one A7 NaN rotation) the iteration-5 system is positive
+# definite in fp64 with a pivot ratio below 1e-6: the oracle's natural-order float Cholesky breaks down, the GPU's
+# nested-dissection order does not (round 2's order broke down too) -- accepted as a one-sided breakdown, trajectory ends.
+TRAJECTORIES = [("S1", 6, 6, None), ("C2", 2, 1, 2), ("C2_ARAP", 10, 4, None), ("C5", 6, 3, None)]
 
 
 @pytest.mark.parametrize("name,iterations,min_ok,fails_at", TRAJECTORIES)
@@ -428,7 +416,7 @@ def test_fit_state_synchronised_trajectory(nn, S, oracle_mod, name, iterations, 
         status, err = _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k)
         print(f"{name} iteration {k + 1}: {status}, update rel err {err}, NaN rotations before {nan_before}", flush=True)
         report.append((k + 1, status, err))
-        if status == "potrf":
+        if status.startswith("potrf"):
             break
     print(f"{name}: {report}")
     assert sum(r[1].startswith("ok") for r in report) >= min_ok
@@ -486,7 +474,7 @@ def test_fit_multilayer_arap_parity(nn, S, oracle_mod, name):
     wf, _, dg_g = _gpu_fit(nn, sc, depth, 1)
     assert np.array_equal(wf.get_edges(), h["edges"])
     I3 = np.tile(np.eye(3, dtype=np.float32), (N, 1, 1))
-    x64 = _arrowhead_fp64_solution(oracle_mod, sc, I3, np.zeros((N, 3), np.float32), dg_o)
+    x64 = arrowhead_fp64_solution(oracle_mod, sc, I3, np.zeros((N, 3), np.float32), dg_o)
     e_g = nan_rel_err(dg_g["updates"][: 6 * N], x64)
     e_o = nan_rel_err(dg_o["updates"], x64)
     print(f"{name}: layers {list(h['layer_counts'])}, GPU update err vs fp64 {e_g:.3g}, oracle float {e_o:.3g}")
@@ -507,7 +495,7 @@ def test_c5_four_layer_solve_vs_fp64(nn, S, oracle_mod):
     depth = scene_target(oracle_mod, sc)
     wf, ft, dg_g = _gpu_fit(nn, sc, depth, 1)
     I3 = np.tile(np.eye(3, dtype=np.float32), (N, 1, 1))
-    x64 = _arrowhead_fp64_solution(oracle_mod, sc, I3, np.zeros((N, 3), np.float32), None, hessian_diag=dg_g["hessian"][: 36 * N],
+    x64 = arrowhead_fp64_solution(oracle_mod, sc, I3, np.zeros((N, 3), np.float32), None, hessian_diag=dg_g["hessian"][: 36 * N],
                                    gradient=dg_g["gradient"][: 6 * N])
     e_g = nan_rel_err(dg_g["updates"][: 6 * N], x64)
     print(f"C5_L4: layers {list(sc.hierarchy['layer_counts'])}, GPU update err vs fp64 {e_g:.3g}")
