@@ -19,7 +19,23 @@
 namespace nnrt {
 
 constexpr int PIX_TILE = 16;
-constexpr int PIX_BLOCK = PIX_TILE * PIX_TILE;
+// waves per workgroup of the fused launch; each wave owns one 8x8 quadrant of a 16x16 tile
+#ifndef NNRT_PIX_WAVES
+#define NNRT_PIX_WAVES 4
+#endif
+constexpr int PIX_WAVES = NNRT_PIX_WAVES;
+constexpr int PIX_BLOCK = 64 * PIX_WAVES;
+static_assert(PIX_WAVES == 1 || PIX_WAVES == 2 || PIX_WAVES == 4, "waves per workgroup");
+
+// this wave's tile and quadrant (0..3: (q & 1, q >> 1) in 8-pixel steps). XCD-aware: consecutive workgroups are dealt
+// round-robin over the 8 XCDs, so each XCD gets a contiguous band of quadrants (neighbouring pixels share vertices,
+// anchors and nodes -> L2 reuse within the XCD).
+__device__ inline int pix_quadrant(const FitPixelArgs& a) {
+	const int blocks = (4 * a.tiles_x * a.tiles_y + PIX_WAVES - 1) / PIX_WAVES;
+	const int per_xcd = (blocks + 7) / 8;
+	const int b = static_cast<int>(blockIdx.x);
+	return ((b % 8) * per_xcd + b / 8) * PIX_WAVES + static_cast<int>(threadIdx.x >> 6);
+}
 
 template <int MODE>
 struct ModeTraits;
@@ -44,17 +60,13 @@ struct ModeTraits<NNRT_ITERATION_ROTATION_ONLY> {
 // out_face / out_vid: the pixel's contributing face (-1: none) and its vertices, handed to pass 2 in registers
 template <int MODE>
 __device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int dn_stride, int& out_face, int (&out_vid)[3]) {
-	// XCD-aware tile order: consecutive workgroups are dealt round-robin over the 8 XCDs, so give each XCD a contiguous
-	// band of tiles (neighbouring tiles share vertices, anchors and nodes -> L2 reuse within the XCD).
+	// one 8x8 quadrant per wave: compact pixel sets touch the fewest nodes
 	const int tiles = a.tiles_x * a.tiles_y;
-	const int per_xcd = (tiles + 7) / 8;
-	const int b = blockIdx.x;
-	const int tile = (b % 8) * per_xcd + b / 8;
+	const int qd = pix_quadrant(a), tile = qd >> 2, quad = qd & 3;
 	const int tu = tile % a.tiles_x, tv = a.tile_row0 + tile / a.tiles_x;
-	// wave w of the workgroup owns the 8x8 quadrant (w & 1, w >> 1): compact pixel sets touch the fewest nodes
-	const int lane = static_cast<int>(threadIdx.x & 63), wave = static_cast<int>(threadIdx.x >> 6);
-	const int u = tu * PIX_TILE + (wave & 1) * 8 + (lane & 7);
-	const int v = tv * PIX_TILE + (wave >> 1) * 8 + (lane >> 3);
+	const int lane = static_cast<int>(threadIdx.x & 63);
+	const int u = tu * PIX_TILE + (quad & 1) * 8 + (lane & 7);
+	const int v = tv * PIX_TILE + (quad >> 1) * 8 + (lane >> 3);
 	const bool in_image = tile < tiles && u < a.W && v < a.H;
 	const int64_t p = static_cast<int64_t>(v) * a.W + u;
 
@@ -387,14 +399,12 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 	static_assert(NSLOT % 4 == 0, "face table rows are loaded as int4");
 	// tiles of 16 x 16 pixels (the pass-1 tiles), one 8 x 8 block per wave
 	const int tiles = a.tiles_x * a.tiles_y;
-	const int per_xcd = (tiles + 7) / 8;
-	const int b = blockIdx.x;
-	const int tile = (b % 8) * per_xcd + b / 8;
+	const int qd = pix_quadrant(a), tile = qd >> 2, quad = qd & 3;
 	const int tu = tile % a.tiles_x, tv = a.tile_row0 + tile / a.tiles_x;
-	const int lane = static_cast<int>(threadIdx.x & 63), wave = static_cast<int>(threadIdx.x >> 6);
-	const int u = tu * PIX_TILE + (wave & 1) * 8 + (lane & 7), v = tv * 2 * NG_ROWS + (wave >> 1) * NG_ROWS + (lane >> 3);
+	const int lane = static_cast<int>(threadIdx.x & 63);
+	const int u = tu * PIX_TILE + (quad & 1) * 8 + (lane & 7), v = tv * 2 * NG_ROWS + (quad >> 1) * NG_ROWS + (lane >> 3);
 	const bool in_image = tile < tiles && (lane >> 3) < NG_ROWS && u < a.W && v < a.H;
-	const int pu0 = tu * PIX_TILE + (wave & 1) * 8, pv0 = tv * 2 * NG_ROWS + (wave >> 1) * NG_ROWS;
+	const int pu0 = tu * PIX_TILE + (quad & 1) * 8, pv0 = tv * 2 * NG_ROWS + (quad >> 1) * NG_ROWS;
 	const int KA = a.anchor_count;
 
 	// this pixel's face: distinct anchor nodes still to be filed, ascending; the row waits in LDS (s_ent[wave][.][lane]),
@@ -689,7 +699,7 @@ nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t st
 	// `between` (stage timing) is recorded before the fused launch: the pixel-pass stage reads 0, the node-pass stage
 	// times both passes
 	if (between) NNRT_EV(hipEventRecord(between, stream));
-	const unsigned grid = static_cast<unsigned>(((args.tiles_x * args.tiles_y + 7) / 8) * 8);
+	const unsigned grid = static_cast<unsigned>(((4 * args.tiles_x * args.tiles_y + PIX_WAVES - 1) / PIX_WAVES + 7) / 8 * 8);
 	// anchor slots per vertex: the common 4-anchor configuration gets its own instantiation (half the slot logic)
 	const bool k4 = args.anchor_count <= 4;
 	switch (mode) {
