@@ -180,7 +180,7 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="OpenMP threads for the CPU baseline (0: this process's CPU share, see cpu_threads_default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r02_pmc_traffic.json"),
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r03_pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch of the roofline kernel (tools/pmc_traffic.py output)")
     return ap.parse_args(argv)
 

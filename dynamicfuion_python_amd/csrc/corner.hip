@@ -36,7 +36,10 @@ constexpr int CT = 256;                       // threads per workgroup of the co
 constexpr int TILE = CORNER_NB;               // 64
 constexpr int TILE_ELEMS = TILE * TILE;
 constexpr int CS4 = TILE + 4;                 // LDS row stride of staged tiles (16-B aligned rows for ds_read_b128)
-constexpr int ND_LEAF = 42;                   // nodes per nested-dissection leaf: 252 unknowns = four tiles
+#ifndef NNRT_ND_LEAF
+#define NNRT_ND_LEAF 42
+#endif
+constexpr int ND_LEAF = NNRT_ND_LEAF;         // nodes per nested-dissection leaf: 252 unknowns = four tiles
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
