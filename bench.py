@@ -323,10 +323,18 @@ def main(argv=None):
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a HIP device (the MI355X path has no CPU fallback)")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # NNRT_BENCH_BACKEND=gloo (rehearsal only): several ranks sharing the GPUs of a smaller box (device = local rank
+    # modulo the visible devices), their collectives on gloo over host tensors; the default is RCCL, one GPU per rank
+    backend = os.environ.get("NNRT_BENCH_BACKEND", "nccl")
+    local_dev = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group(backend="nccl", device_id=dev)
+        if backend == "gloo":
+            dist.init_process_group(backend="gloo")
+        else:
+            dist.init_process_group(backend="nccl", device_id=dev)
+    coll_dev = "cpu" if backend == "gloo" else dev
 
     from dynamicfuion_python_amd import _native as NV
     from dynamicfuion_python_amd import synthetic as S
@@ -425,7 +433,7 @@ def main(argv=None):
             raise SystemExit(f"non-finite node motion after the timed steps (replica {r})")
         per_replica.append(dict(replica=r, seed=rank * R + r,
                                 update_norm=float(np.linalg.norm(rp["ft"].diagnostics(stream=rp["stream"])["updates"]))))
-    elapsed_max = max_over_ranks(elapsed, dev)
+    elapsed_max = max_over_ranks(elapsed, coll_dev)
     agg = aggregate(args.steps * R, elapsed_max, world)
     agg["ms_per_step"] = 1000.0 * elapsed_max / args.steps   # one step = every replica's iteration
 
@@ -499,7 +507,7 @@ def main(argv=None):
     setup_ms = (time.perf_counter() - t_setup) * 1000.0
 
     # end-of-run exchange of per-rank results: iterations/s, seconds, final |update|
-    per_rank = exchange_per_rank(args.steps * R, elapsed, float(np.linalg.norm(dg["updates"])), dev)
+    per_rank = exchange_per_rank(args.steps * R, elapsed, float(np.linalg.norm(dg["updates"])), coll_dev)
 
     out = {
         "metric": "GN iters/sec (640x480, 1.5k-node graph)" if args.config == "C2" else f"GN iters/sec ({args.config})",
@@ -517,7 +525,10 @@ def main(argv=None):
         "data": "synthetic (smooth grid mesh + GT node motion rendered to depth; seed = rank)",
         "config": {"workload": workload, "config": args.config, "frame": [sc.H, sc.W], "nodes": Nn, "vertices": V, "triangles": F,
                    "anchors": 4, "iteration_mode": "ALL", "lm_damping": 0.001, "hip_graph": True, "steps_per_graph": per_launch, "step": args.step,
-                   "parallelism": f"replicas{world * R}" if world * R > 1 else "single", "replicas_per_gpu": R},
+                   "parallelism": f"replicas{world * R}" if world * R > 1 else "single", "replicas_per_gpu": R,
+                   **({"collectives": "rccl" if backend == "nccl" else f"{backend} (rehearsal: {world} ranks on "
+                                                                       f"{torch.cuda.device_count()} visible GPU(s))"}
+                      if world > 1 else {})},
         "setup_ms": round(setup_ms, 3),
         "stage_ms": {k: round(v, 5) for k, v in stages.items()},
         "stage_note": "eager launches between HIP events; pixel_jacobians is back-to-back event overhead only: both pixel "
