@@ -170,7 +170,7 @@ __device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int
 				sa[0] = spa_cw(px, py, fn.x[1], fn.y[1], fn.x[2], fn.y[2]);
 				sa[1] = spa_cw(px, py, fn.x[2], fn.y[2], fn.x[0], fn.y[0]);
 				sa[2] = spa_cw(px, py, fn.x[0], fn.y[0], fn.x[1], fn.y[1]);
-				const float inv_A = rcp_rn(A);
+				const float inv_A = rcp_rn_normal(A);   // consumed by div_rn only, which ignores it outside (1e-30, 1e30)
 #pragma unroll
 				for (int i = 0; i < 3; i++) drho[i] = div_rn(sa[i], A, inv_A);
 			} else {
@@ -184,7 +184,7 @@ __device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int
 			const float s0a[2] = {fn.y[2] - py, px - fn.x[2]}, s0b[2] = {py - fn.y[1], fn.x[1] - px};   // (p, v1, v2)
 			const float s1a[2] = {fn.y[0] - py, px - fn.x[0]}, s1b[2] = {py - fn.y[2], fn.x[2] - px};   // (p, v2, v0)
 			const float s2a[2] = {fn.y[1] - py, px - fn.x[1]}, s2b[2] = {py - fn.y[0], fn.x[0] - px};   // (p, v0, v1)
-			const float inv_den = rcp_rn(den);
+			const float inv_den = rcp_rn_normal(den);   // (div_rn only)
 			// d rho_r / d ndc of face vertex i, component c, and (below) the perspective z-terms of vertex i: parked in LDS
 			// (lane-private slots) until vertex i's columns are formed, which keeps the kernel at <= 96 VGPRs (5 waves/SIMD:
 			// one residency round at 640x480)
@@ -219,7 +219,7 @@ __device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int
 				const float pz[3][3] = {{-n0 * pz0, dd * drho[0] * z2 - n0 * pz1, dd * drho[0] * z1 - n0 * pz2},
 				                        {dd * drho[1] * z2 - n1 * pz0, -n1 * pz1, dd * drho[1] * z0 - n1 * pz2},
 				                        {dd * drho[2] * z1 - n2 * pz0, dd * drho[2] * z0 - n2 * pz1, -n2 * pz2}};
-				const float inv_dd2 = rcp_rn(dd2);
+				const float inv_dd2 = rcp_rn_normal(dd2);   // (div_rn only)
 #pragma unroll
 				for (int r = 0; r < 3; r++)
 #pragma unroll

@@ -133,7 +133,7 @@ __device__ inline bool depth_near_all_fast(const FaceNdc& f, float s0, float s1,
 		const float n0 = b0 * f.z[1] * f.z[2], n1 = f.z[0] * b1 * f.z[2], n2 = f.z[0] * f.z[1] * b2;
 		const float den = fmaxf(n0 + n1 + n2, K_EPSILON);
 		if (fmaxf(fmaxf(fabsf(n0), fabsf(n1)), fabsf(n2)) < 1e29f && den < 1e30f) {
-			const float y = rcp_rn(den);
+			const float y = rcp_rn_normal(den);   // den in [K_EPSILON, 1e30): rcp_rn_normal's exact range
 			b0 = div_mk(n0, den, y);
 			b1 = div_mk(n1, den, y);
 			b2 = div_mk(n2, den, y);
