@@ -383,6 +383,13 @@ static_assert(2 * NG_ROWS == PIX_TILE, "pass 2 walks the pass-1 tiles");
 
 __device__ inline void ng_flush(double* dst, double v) { atomicAdd(dst, v); }
 
+// development timing build only (-DNNRT_FIT_STAMPS): per wave, shader cycles spent in pass 2's phases (group, gather +
+// Jacobians, sums, and the chunk count), read back by nnrt_dev_fit_phases
+#ifdef NNRT_FIT_STAMPS
+__device__ unsigned long long g_fit_phases[16384][4];
+#define PHASE_CLOCK() __builtin_amdgcn_s_memtime()
+#endif
+
 // slots0 / slots1: this wave's two chunk buffers (8 * NG_STRIDE words each); ent: its face-table rows ([NSLOT][64])
 // face_in / vid_in: this lane's pixel's contributing face (-1: none) and its vertices, from pass 1
 template <int MODE, int MAXK>
@@ -619,7 +626,14 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 	// are consumed in the same iteration, so no loaded register is carried across the loop (a loop-carried load
 	// destination gets copied into the phi register right after the load, i.e. waited for)
 	int cb = 0;
+#ifdef NNRT_FIT_STAMPS
+	unsigned long long ph[4] = {0, 0, 0, 0}, t0 = PHASE_CLOCK(), t1;
+#define PHASE_ADD(i) (t1 = PHASE_CLOCK(), ph[i] += t1 - t0, t0 = t1)
+#else
+#define PHASE_ADD(i) ((void)0)
+#endif
 	int count = group(slots0);
+	PHASE_ADD(0);
 	while (count > 0) {
 		float* cur_slots = cb ? slots1 : slots0;
 		float* nxt = cb ? slots0 : slots1;
@@ -627,14 +641,28 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 		gather(cur_slots, count);
 		const int next = group(nxt);
 		wave_sync();
+		PHASE_ADD(0);
 		jacobians(cur_slots, count);
 		wave_sync();
+		PHASE_ADD(1);
 		sums(cur_slots, count);
 		wave_sync();
+		PHASE_ADD(2);
+#ifdef NNRT_FIT_STAMPS
+		ph[3]++;
+#endif
 		cb ^= 1;
 		count = next;
 	}
 	if (cur >= 0 && e_valid) ng_flush(a.acc + static_cast<int64_t>(cur) * ACC_STRIDE + e, acc);
+#ifdef NNRT_FIT_STAMPS
+	{
+		const int wid_ = static_cast<int>(blockIdx.x) * (PIX_BLOCK / 64) + static_cast<int>(threadIdx.x >> 6);
+		if (lane == 0 && wid_ < 16384)
+			for (int i = 0; i < 4; i++) g_fit_phases[wid_][i] = ph[i];
+	}
+#endif
+#undef PHASE_ADD
 }
 
 // ---- both passes in one launch ------------------------------------------------------------------------------------
@@ -690,6 +718,9 @@ __global__ __launch_bounds__(PIX_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) 
 	} while (0)
 
 #ifdef NNRT_FIT_STAMPS
+extern "C" int nnrt_dev_fit_phases(unsigned long long* out) {   // [16384][4] of the last fused launch
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fit_phases), sizeof(unsigned long long) * 16384 * 4) == hipSuccess ? 0 : 1;
+}
 extern "C" int nnrt_dev_fit_stamps(unsigned long long* out) {   // [16384][4] of the last fused launch
 	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fit_stamps), sizeof(unsigned long long) * 16384 * 4) == hipSuccess ? 0 : 1;
 }

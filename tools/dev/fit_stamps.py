@@ -62,3 +62,19 @@ hist, edges = np.histogram(life / 1e3, bins=12)
 print("lifetime histogram (us):", [(round(float(e), 1), int(h)) for e, h in zip(edges, hist)])
 if out_json:
     json.dump(dict(start=start.tolist(), mid=mid.tolist(), end=end.tolist(), hw=hw.tolist(), xcc=xcc.tolist()), open(out_json, "w"))
+
+# pass-2 phase split (shader cycles per wave: group, gather + Jacobians, sums; chunk count)
+fnp = getattr(lib, "nnrt_dev_fit_phases", None)
+if fnp is not None:
+    fnp.argtypes = [ctypes.c_void_p]
+    ph = np.zeros((16384, 4), np.uint64)
+    assert fnp(ph.ctypes.data) == 0
+    ph = ph[:nw].astype(np.float64)
+    busy = ph[:, 3] > 0
+    tot = ph[busy, :3].sum(1)
+    p2_ns = p2[busy].astype(np.float64)
+    clk = (tot / np.maximum(p2_ns, 1)).mean()   # cycles per ns of wave time in pass 2 (the phases cover it)
+    print(f"pass-2 phases over {busy.sum()} waves with work: chunks mean {ph[busy, 3].mean():.2f}; cycles mean group "
+          f"{ph[busy, 0].mean():.0f}, gather+Jacobians {ph[busy, 1].mean():.0f}, sums {ph[busy, 2].mean():.0f} "
+          f"(shares {ph[busy, 0].sum() / tot.sum():.2f} / {ph[busy, 1].sum() / tot.sum():.2f} / {ph[busy, 2].sum() / tot.sum():.2f}); "
+          f"{clk:.2f} cycles per ns of pass-2 time")
