@@ -252,10 +252,23 @@ def cpu_baseline(sc, depth_host, share_threads: int, budget_s: float, step: str,
     host = host_cpu()
     socket = min(host["cores_per_socket"] or share_threads, len(os.sched_getaffinity(0)))
     refp, refm = O.unproject(depth_host, sc.K, 1.0, 10.0)
-    runs = [_cpu_sample(O, sc, refp, refm, socket, budget_s, step, iterations, R0, t0)]
-    if share_threads != socket:
-        runs.append(_cpu_sample(O, sc, refp, refm, share_threads, budget_s, step, iterations, R0, t0))
-    one = _cpu_sample(O, sc, refp, refm, 1, single_thread_s, step, iterations, R0, t0, min_timed=1)
+    # a progress line every 60 s while the samples run (a single-thread C3 iteration takes minutes)
+    import threading
+    done = threading.Event()
+
+    def heartbeat():
+        t_start = time.perf_counter()
+        while not done.wait(60.0):
+            log(f"CPU baseline still running ({time.perf_counter() - t_start:.0f} s)")
+
+    threading.Thread(target=heartbeat, daemon=True).start()
+    try:
+        runs = [_cpu_sample(O, sc, refp, refm, socket, budget_s, step, iterations, R0, t0)]
+        if share_threads != socket:
+            runs.append(_cpu_sample(O, sc, refp, refm, share_threads, budget_s, step, iterations, R0, t0))
+        one = _cpu_sample(O, sc, refp, refm, 1, single_thread_s, step, iterations, R0, t0, min_timed=1)
+    finally:
+        done.set()
     # value: the faster multi-thread sample (the binned raster does not scale to a whole socket on a shared host)
     best = max(runs, key=lambda r: r["value"] or 0.0)
     res = dict(best)

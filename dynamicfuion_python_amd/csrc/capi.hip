@@ -8,6 +8,8 @@
 #include <cmath>
 #include <cstring>
 #include <memory>
+#include <mutex>
+#include <list>
 #include <vector>
 
 #include "fitter_kernels.hpp"
@@ -1522,6 +1524,67 @@ nnrt_status nnrt_invert_triangular_blocks(const float* d_blocks, int32_t block_c
 	                        [&](int* flag) { return launch_invert_triangular_blocks(d_blocks, block_count, block_size, upper != 0, d_out, flag, s); });
 }
 
+} // extern "C"
+
+namespace {
+// Everything the arrowhead solve derives from the wing structure alone -- the stem CSR, the target-grouped Schur lists,
+// the tile-sparse corner plan and its buffers, the per-call scratch -- kept per (device, N, n0, coordinates) so a
+// repeated structure (a fixed hierarchy, solved every iteration) skips the host planning and the allocations. An entry
+// is owned by one call at a time (taken out of the pool, returned after the call has synchronised its stream), so
+// concurrent calls never share device scratch; the pool holds the ARROW_POOL_MAX most recently used structures.
+struct ArrowheadPlan {
+	int device = -1, N = 0, n0 = 0, E = 0, targets = 0;
+	std::vector<int32_t> coords;
+	CornerSolver corner;
+	DeviceBuffer<float> dinv, dinv_b;
+	DeviceBuffer<int> edge_offsets, edge_list, flag, tgt_off, rhs_off, rhs_edges;
+	DeviceBuffer<int2> tgt_ab, pairs;
+	~ArrowheadPlan() {
+		for (auto* b : {&dinv, &dinv_b}) b->release();
+		for (auto* b : {&edge_offsets, &edge_list, &flag, &tgt_off, &rhs_off, &rhs_edges}) b->release();
+		for (auto* b : {&tgt_ab, &pairs}) b->release();
+	}
+	bool matches(int dev, int32_t n, int32_t base, const std::vector<int32_t>& c) const {
+		return device == dev && N == n && n0 == base && coords == c;
+	}
+	nnrt_status build(int dev, int32_t n, int32_t base, std::vector<int32_t> c) {
+		device = dev;
+		N = n;
+		n0 = base;
+		coords = std::move(c);
+		E = static_cast<int>(coords.size() / 2);
+		std::vector<int> counts(n0 + 1, 0), list(std::max(E, 1)), fill;
+		for (int e = 0; e < E; e++)
+			if (coords[2 * e] < n0) counts[coords[2 * e] + 1]++;
+		for (int i = 0; i < n0; i++) counts[i + 1] += counts[i];
+		fill.assign(counts.begin(), counts.end() - 1);
+		for (int e = 0; e < E; e++)
+			if (coords[2 * e] < n0) list[fill[coords[2 * e]]++] = e;
+		nnrt_status st = corner.prepare(coords.data(), E, n0, N);
+		if (st) return st;
+		const StemSchurLists sl = build_stem_schur_lists(coords.data(), E, n0, N);
+		targets = static_cast<int>(sl.tgt_ab.size());
+		if ((st = dinv.ensure(36 * static_cast<size_t>(std::max(n0, 1)))) || (st = dinv_b.ensure(36 * static_cast<size_t>(std::max(E, 1)))) ||
+		    (st = flag.ensure(1)) || (st = upload(edge_offsets, counts)) || (st = upload(edge_list, list)) || (st = upload(tgt_off, sl.tgt_off)) ||
+		    (st = upload(tgt_ab, sl.tgt_ab)) || (st = upload(pairs, sl.pairs)) || (st = upload(rhs_off, sl.rhs_off)) ||
+		    (st = upload(rhs_edges, sl.rhs_edges)))
+			return st;
+		return NNRT_OK;
+	}
+};
+constexpr size_t ARROW_POOL_MAX = 4;
+std::mutex g_arrow_mu;
+// heap-allocated and never destroyed: device memory must not be released by static destructors after the HIP runtime
+// has shut down at process exit
+std::list<std::unique_ptr<ArrowheadPlan>>& arrow_pool() {
+	static auto* pool = new std::list<std::unique_ptr<ArrowheadPlan>>();
+	return *pool;
+}
+
+} // namespace
+
+extern "C" {
+
 nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, const float* d_wing, const int32_t* d_coords, int32_t E, int32_t N,
                                                        int32_t n0, const float* d_b, float* d_x, void* stream) {
 	NNRT_CHECK_ARG(n0 >= 0 && n0 <= N, "arrow_base_block_index out of range");
@@ -1534,63 +1597,67 @@ nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, cons
 		NNRT_HIP(hipMemcpyAsync(coords.data(), d_coords, sizeof(int32_t) * 2 * E, hipMemcpyDeviceToHost, s));
 		NNRT_HIP(hipStreamSynchronize(s));
 	}
-	for (int e = 0; e < E; e++) {   // before any allocation: the host lists below index by these
+	for (int e = 0; e < E; e++) {   // before any allocation: the host lists index by these
 		const int i = coords[2 * e], j = coords[2 * e + 1];
 		NNRT_CHECK_ARG(i >= 0 && i < N && j >= 0 && j < N, "wing block coordinate outside [0, diagonal_block_count)");
 		NNRT_CHECK_ARG(i != j, "wing block on the block diagonal");
 		NNRT_CHECK_ARG(j >= n0, "wing block column inside the arrow stem (the stem is block-diagonal)");
 	}
-	std::vector<int> counts(n0 + 1, 0), list(std::max(E, 1)), fill;
-	for (int e = 0; e < E; e++)
-		if (coords[2 * e] < n0) counts[coords[2 * e] + 1]++;
-	for (int i = 0; i < n0; i++) counts[i + 1] += counts[i];
-	fill.assign(counts.begin(), counts.end() - 1);
-	for (int e = 0; e < E; e++)
-		if (coords[2 * e] < n0) list[fill[coords[2 * e]]++] = e;
-	CornerSolver corner;
-	nnrt_status st = corner.prepare(coords.data(), E, n0, N);
-	if (st) return st;
+	int device = 0;
+	NNRT_HIP(hipGetDevice(&device));
+	std::unique_ptr<ArrowheadPlan> plan;
+	{
+		std::lock_guard<std::mutex> lock(g_arrow_mu);
+		auto& pool = arrow_pool();
+		for (auto it = pool.begin(); it != pool.end(); ++it)
+			if ((*it)->matches(device, N, n0, coords)) {
+				plan = std::move(*it);
+				pool.erase(it);
+				break;
+			}
+	}
+	nnrt_status st = NNRT_OK;
+	if (!plan) {
+		plan = std::make_unique<ArrowheadPlan>();
+		if ((st = plan->build(device, N, n0, std::move(coords)))) return st;
+	}
 	ArrowheadWorkspace ws;
 	ws.N = N;
 	ws.n0 = n0;
 	ws.E = E;
 	ws.m = 6 * (N - n0);
-	ws.corner = &corner;
-	int* flag = nullptr;
-	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.dinv), sizeof(float) * 36 * std::max(n0, 1), s));
-	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.dinv_b), sizeof(float) * 36 * std::max(E, 1), s));
-	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.edge_offsets), sizeof(int) * (n0 + 1), s));
-	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&ws.edge_list), sizeof(int) * std::max(E, 1), s));
-	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&flag), sizeof(int), s));
-	NNRT_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
-	NNRT_HIP(hipMemcpyAsync(ws.edge_offsets, counts.data(), sizeof(int) * (n0 + 1), hipMemcpyHostToDevice, s));
-	NNRT_HIP(hipMemcpyAsync(ws.edge_list, list.data(), sizeof(int) * std::max(E, 1), hipMemcpyHostToDevice, s));
-	const StemSchurLists sl = build_stem_schur_lists(coords.data(), E, n0, N);
-	ws.targets = static_cast<int>(sl.tgt_ab.size());
-	auto dev_copy = [&](const auto& v, auto** out) -> hipError_t {
-		using T = typename std::decay_t<decltype(v)>::value_type;
-		hipError_t e = hipMallocAsync(reinterpret_cast<void**>(out), sizeof(T) * std::max<size_t>(v.size(), 1), s);
-		if (e == hipSuccess && !v.empty()) e = hipMemcpyAsync(*out, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, s);
-		return e;
-	};
-	NNRT_HIP(dev_copy(sl.tgt_off, &ws.tgt_off));
-	NNRT_HIP(dev_copy(sl.tgt_ab, &ws.tgt_ab));
-	NNRT_HIP(dev_copy(sl.pairs, &ws.pairs));
-	NNRT_HIP(dev_copy(sl.rhs_off, &ws.rhs_off));
-	NNRT_HIP(dev_copy(sl.rhs_edges, &ws.rhs_edges));
+	ws.corner = &plan->corner;
+	ws.dinv = plan->dinv.ptr;
+	ws.dinv_b = plan->dinv_b.ptr;
+	ws.edge_offsets = plan->edge_offsets.ptr;
+	ws.edge_list = plan->edge_list.ptr;
+	ws.targets = plan->targets;
+	ws.tgt_off = plan->tgt_off.ptr;
+	ws.tgt_ab = plan->tgt_ab.ptr;
+	ws.pairs = plan->pairs.ptr;
+	ws.rhs_off = plan->rhs_off.ptr;
+	ws.rhs_edges = plan->rhs_edges.ptr;
 	ws.diag = const_cast<float*>(d_diag);
 	ws.rhs = const_cast<float*>(d_b);
 	ws.x = d_x;
-	st = arrowhead_solve_core(ws, d_coords, d_wing, flag, s);
 	int host_flag = 0;
-	if (!st) {
-		NNRT_HIP(hipMemcpyAsync(&host_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
-		NNRT_HIP(hipStreamSynchronize(s));
+	if (hipMemsetAsync(plan->flag.ptr, 0, sizeof(int), s) != hipSuccess) {
+		set_error("hipMemsetAsync failed");
+		return NNRT_ERROR_HIP;
 	}
-	for (void* p : {static_cast<void*>(ws.dinv), static_cast<void*>(ws.dinv_b), static_cast<void*>(ws.tgt_off), static_cast<void*>(ws.tgt_ab), static_cast<void*>(ws.pairs),
-	                static_cast<void*>(ws.rhs_off), static_cast<void*>(ws.rhs_edges), static_cast<void*>(ws.edge_offsets),
-	                static_cast<void*>(ws.edge_list), static_cast<void*>(flag)})
-		hipFreeAsync(p, s);
+	st = arrowhead_solve_core(ws, d_coords, d_wing, plan->flag.ptr, s);
+	if (!st) {
+		if (hipMemcpyAsync(&host_flag, plan->flag.ptr, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+		    hipStreamSynchronize(s) != hipSuccess) {
+			set_error("arrowhead solve: stream synchronisation failed");
+			return NNRT_ERROR_HIP;   // the plan is dropped (its device work state is unknown)
+		}
+		// the stream is drained: the plan's scratch is free for the next call with this structure
+		std::lock_guard<std::mutex> lock(g_arrow_mu);
+		auto& pool = arrow_pool();
+		pool.push_front(std::move(plan));
+		while (pool.size() > ARROW_POOL_MAX) pool.pop_back();
+	}
 	if (st) return st;
 	if (host_flag) {
 		set_error("arrowhead solve: a stem block or the Schur complement is not positive-definite");
