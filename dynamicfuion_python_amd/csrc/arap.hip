@@ -228,11 +228,8 @@ __global__ __launch_bounds__(64) void k_arrow_stem(int n0, const float* __restri
 // Lane (r, c) < 36 owns entry (r, c) of the 6x6 target block. The target's pair list is loaded once, one pair per lane,
 // and broadcast by shuffle, so the wing / D^-1 B loads of eight pairs are in flight together (no dependent index load
 // per pair). Pairs are summed in list order.
-__global__ __launch_bounds__(256) void k_stem_schur(int targets, CornerMap S, const int* __restrict__ tgt_off, const int2* __restrict__ tgt_ab,
-                                                    const int2* __restrict__ pairs, const float* __restrict__ wing, const float* __restrict__ dinv_b) {
-	const int w = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
-	const int lane = static_cast<int>(threadIdx.x & 63);
-	if (w >= targets) return;
+__device__ __forceinline__ void stem_schur_wave(int w, int lane, const CornerMap& S, const int* __restrict__ tgt_off, const int2* __restrict__ tgt_ab,
+                                                const int2* __restrict__ pairs, const float* __restrict__ wing, const float* __restrict__ dinv_b) {
 	const int r = lane < 36 ? lane / 6 : 0, c = lane < 36 ? lane % 6 : 0;
 	const int beg = tgt_off[w], end = tgt_off[w + 1];
 	float acc = 0.f;
@@ -274,13 +271,10 @@ __global__ __launch_bounds__(256) void k_stem_schur(int targets, CornerMap S, co
 // ---- fitter form of the Schur update: the ARAP wing blocks dEi^T dEj (dEj = [0 | b I]) are zero outside their last
 // three columns, so B_ia^T D_i^-1 B_ib is zero outside its lower-right 3x3 block and only those 9 entries change
 // (the others would subtract exact zeros). 7 pair slots x 9 entries per wave; slots reduced in order at the end.
-__global__ __launch_bounds__(256) void k_stem_schur_t3(int targets, CornerMap S, const int* __restrict__ tgt_off, const int2* __restrict__ tgt_ab,
-                                                       const int2* __restrict__ pairs, const float* __restrict__ wing,
-                                                       const float* __restrict__ dinv_b) {
-	__shared__ float s_part[4][7][9];
-	const int w = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
-	const int lane = static_cast<int>(threadIdx.x & 63), wl = static_cast<int>(threadIdx.x >> 6);
-	if (w >= targets) return;
+// s_part: this wave's [7][9] LDS partials
+__device__ __forceinline__ void stem_schur_t3_wave(int w, int lane, float (*s_part)[9], const CornerMap& S, const int* __restrict__ tgt_off,
+                                                   const int2* __restrict__ tgt_ab, const int2* __restrict__ pairs, const float* __restrict__ wing,
+                                                   const float* __restrict__ dinv_b) {
 	const int slot = lane < 63 ? lane / 9 : 6, ent = lane < 63 ? lane % 9 : 0;
 	const int r = 3 + ent / 3, c = 3 + ent % 3;
 	const int beg = tgt_off[w], end = tgt_off[w + 1];
@@ -310,12 +304,12 @@ __global__ __launch_bounds__(256) void k_stem_schur_t3(int targets, CornerMap S,
 				acc += sum;
 			}
 	}
-	if (lane < 63) s_part[wl][slot][ent] = acc;
+	if (lane < 63) s_part[slot][ent] = acc;
 	__builtin_amdgcn_wave_barrier();   // LDS is in order within the wave; keep the compiler from moving the reads up
 	if (lane < 9) {
 		float t = 0.f;
 #pragma unroll
-		for (int sl = 0; sl < 7; sl++) t += s_part[wl][sl][lane];
+		for (int sl = 0; sl < 7; sl++) t += s_part[sl][lane];
 		const int2 ab = tgt_ab[w];
 		float* dst = corner_block_entry(S, ab.x, ab.y, 3 + lane / 3, 3 + lane % 3);
 		if (dst) *dst -= t;
@@ -323,12 +317,9 @@ __global__ __launch_bounds__(256) void k_stem_schur_t3(int targets, CornerMap S,
 }
 
 // ---- b_C -= sum over stem edges i->a of (D_i^-1 B_ia)^T b_i (one wave per corner node; lanes over its edges) ----
-__global__ __launch_bounds__(256) void k_stem_rhs(int nc, const int* __restrict__ rhs_off, const int* __restrict__ rhs_edges,
-                                                  const int32_t* __restrict__ edges, const float* __restrict__ dinv_b, const float* __restrict__ rhs,
-                                                  const int* __restrict__ node_row, float* __restrict__ cb) {
-	const int a = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
-	const int lane = static_cast<int>(threadIdx.x & 63);
-	if (a >= nc) return;
+__device__ __forceinline__ void stem_rhs_wave(int a, int lane, const int* __restrict__ rhs_off, const int* __restrict__ rhs_edges,
+                                              const int32_t* __restrict__ edges, const float* __restrict__ dinv_b, const float* __restrict__ rhs,
+                                              const int* __restrict__ node_row, float* __restrict__ cb) {
 	float s[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 	for (int q = rhs_off[a] + lane; q < rhs_off[a + 1]; q += 64) {
 		const int e = rhs_edges[q];
@@ -356,6 +347,24 @@ __global__ __launch_bounds__(256) void k_stem_rhs(int nc, const int* __restrict_
 #pragma unroll
 		for (int c = 1; c < 6; c++) v = lane == c ? s[c] : v;
 		cb[node_row[a] + lane] -= v;   // the corner's permuted order
+	}
+}
+
+// Both stem-side corner updates in one launch (they read the same D^-1 B and write disjoint outputs): waves
+// [0, targets) update the Schur targets, waves [targets, targets + nc) the corner right-hand side.
+template <bool T3>
+__global__ __launch_bounds__(256) void k_stem_schur_rhs(int targets, int nc, CornerMap S, const int* __restrict__ tgt_off,
+                                                        const int2* __restrict__ tgt_ab, const int2* __restrict__ pairs, const float* __restrict__ wing,
+                                                        const float* __restrict__ dinv_b, const int* __restrict__ rhs_off, const int* __restrict__ rhs_edges,
+                                                        const int32_t* __restrict__ edges, const float* __restrict__ rhs, float* __restrict__ cb) {
+	__shared__ float s_part[4][7][9];
+	const int w = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
+	const int lane = static_cast<int>(threadIdx.x & 63), wl = static_cast<int>(threadIdx.x >> 6);
+	if (w < targets) {
+		if constexpr (T3) stem_schur_t3_wave(w, lane, s_part[wl], S, tgt_off, tgt_ab, pairs, wing, dinv_b);
+		else stem_schur_wave(w, lane, S, tgt_off, tgt_ab, pairs, wing, dinv_b);
+	} else if (w - targets < nc) {
+		stem_rhs_wave(w - targets, lane, rhs_off, rhs_edges, edges, dinv_b, rhs, S.node_row, cb);
 	}
 }
 
@@ -403,11 +412,34 @@ StemSchurLists build_stem_schur_lists(const int32_t* edges, int E, int n0, int N
 }
 
 // ---- stem back-substitution: x_D = D^-1 (b_D - B x_C) ----
-__global__ void k_arrow_back(int n0, const float* __restrict__ dinv, const int* __restrict__ edge_offsets, const int* __restrict__ edge_list,
+// node update (R <- R Rodrigues(omega), t += dt) from the node's solved increment x6; updates_out gets x6
+__device__ __forceinline__ void arrow_update_node(int n, const float (&xl)[6], float* __restrict__ node_state, float* __restrict__ updates_out) {
+	for (int c = 0; c < 6; c++) updates_out[6 * static_cast<int64_t>(n) + c] = xl[c];
+	float* ns = node_state + static_cast<int64_t>(n) * NODE_STRIDE;
+	ns[3] += xl[3];
+	ns[4] += xl[4];
+	ns[5] += xl[5];
+	float dR[9], R[9];
+	rodrigues_device(xl[0], xl[1], xl[2], dR);
+	for (int i = 0; i < 9; i++) R[i] = ns[6 + i];
+	for (int r = 0; r < 3; r++)
+		for (int c = 0; c < 3; c++) ns[6 + 3 * r + c] = (R[3 * r] * dR[c] + R[3 * r + 1] * dR[3 + c]) + R[3 * r + 2] * dR[6 + c];
+}
+
+// threads [0, n0): stem back substitution (and, with node_state, that node's update from the x it just formed);
+// threads [n0, n_update): the corner nodes' updates from the corner solve's x (node_state non-null only)
+__global__ void k_arrow_back(int n0, int n_update, const float* __restrict__ dinv, const int* __restrict__ edge_offsets, const int* __restrict__ edge_list,
                              const int32_t* __restrict__ edges, const float* __restrict__ wing, const float* __restrict__ rhs,
-                             float* __restrict__ x) {
+                             float* __restrict__ x, float* __restrict__ node_state, float* __restrict__ updates_out) {
 	const int i = blockIdx.x * blockDim.x + threadIdx.x;
-	if (i >= n0) return;
+	if (i >= n0) {
+		if (node_state && i < n_update) {
+			float xl[6];
+			for (int c = 0; c < 6; c++) xl[c] = x[6 * static_cast<int64_t>(i) + c];
+			arrow_update_node(i, xl, node_state, updates_out);
+		}
+		return;
+	}
 	float r6[6];
 	for (int c = 0; c < 6; c++) r6[c] = rhs[6 * static_cast<int64_t>(i) + c];
 	// 6 x 6 blocks as nine float4, 6-vectors as three float2 (the same products and sums as element-wise loads)
@@ -455,29 +487,11 @@ __global__ void k_arrow_back(int n0, const float* __restrict__ dinv, const int* 
 	float2* xo = reinterpret_cast<float2*>(x + 6 * static_cast<int64_t>(i));
 #pragma unroll
 	for (int q = 0; q < 3; q++) xo[q] = make_float2(o[2 * q], o[2 * q + 1]);
-}
-
-__global__ void k_arrow_update(int N, const float* __restrict__ x, float* __restrict__ node_state, float* __restrict__ updates_out) {
-	const int n = blockIdx.x * blockDim.x + threadIdx.x;
-	if (n >= N) return;
-	float xl[6];
-	for (int c = 0; c < 6; c++) {
-		xl[c] = x[6 * static_cast<int64_t>(n) + c];
-		updates_out[6 * static_cast<int64_t>(n) + c] = xl[c];
-	}
-	float* ns = node_state + static_cast<int64_t>(n) * NODE_STRIDE;
-	ns[3] += xl[3];
-	ns[4] += xl[4];
-	ns[5] += xl[5];
-	float dR[9], R[9];
-	rodrigues_device(xl[0], xl[1], xl[2], dR);
-	for (int i = 0; i < 9; i++) R[i] = ns[6 + i];
-	for (int r = 0; r < 3; r++)
-		for (int c = 0; c < 3; c++) ns[6 + 3 * r + c] = (R[3 * r] * dR[c] + R[3 * r + 1] * dR[3 + c]) + R[3 * r + 2] * dR[6 + c];
+	if (node_state) arrow_update_node(i, o, node_state, updates_out);
 }
 
 nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* edges, const float* wing, int* error_flag, hipStream_t stream,
-                                 bool arap_wings) {
+                                 bool arap_wings, float* node_state, float* updates_out) {
 	const int m = ws.m;
 	NNRT_CHECK_ARG(m == 0 || ws.corner, "arrowhead workspace without a corner plan");
 	if (m > 0) {
@@ -490,15 +504,13 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 		NNRT_LAUNCH_CHECK();
 		if (m > 0 && ws.targets > 0) {
 			const CornerMap cm = ws.corner->map();
+			const unsigned grid = static_cast<unsigned>(ceil_div((static_cast<int64_t>(ws.targets) + m / 6) * 64, 256));
 			if (arap_wings)
-				k_stem_schur_t3<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ws.targets) * 64, 256)), 256, 0, stream>>>(
-				    ws.targets, cm, ws.tgt_off, ws.tgt_ab, ws.pairs, wing, ws.dinv_b);
+				k_stem_schur_rhs<true><<<grid, 256, 0, stream>>>(ws.targets, m / 6, cm, ws.tgt_off, ws.tgt_ab, ws.pairs, wing, ws.dinv_b, ws.rhs_off,
+				                                                 ws.rhs_edges, edges, ws.rhs, ws.corner->rhs_perm());
 			else
-				k_stem_schur<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ws.targets) * 64, 256)), 256, 0, stream>>>(
-				    ws.targets, cm, ws.tgt_off, ws.tgt_ab, ws.pairs, wing, ws.dinv_b);
-			NNRT_LAUNCH_CHECK();
-			k_stem_rhs<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(m / 6) * 64, 256)), 256, 0, stream>>>(
-			    m / 6, ws.rhs_off, ws.rhs_edges, edges, ws.dinv_b, ws.rhs, cm.node_row, ws.corner->rhs_perm());
+				k_stem_schur_rhs<false><<<grid, 256, 0, stream>>>(ws.targets, m / 6, cm, ws.tgt_off, ws.tgt_ab, ws.pairs, wing, ws.dinv_b, ws.rhs_off,
+				                                                  ws.rhs_edges, edges, ws.rhs, ws.corner->rhs_perm());
 			NNRT_LAUNCH_CHECK();
 		}
 	}
@@ -506,9 +518,10 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 		nnrt_status st = ws.corner->launch_solve(ws.x + 6 * static_cast<int64_t>(ws.n0), error_flag, stream);
 		if (st) return st;
 	}
-	if (ws.n0 > 0) {
-		k_arrow_back<<<static_cast<unsigned>(ceil_div(ws.n0, 64)), 64, 0, stream>>>(ws.n0, ws.dinv, ws.edge_offsets, ws.edge_list, edges, wing,
-		                                                                           ws.rhs, ws.x);
+	const int threads = node_state ? ws.N : ws.n0;   // with node_state, the node updates ride along (all N nodes)
+	if (threads > 0) {
+		k_arrow_back<<<static_cast<unsigned>(ceil_div(threads, 64)), 64, 0, stream>>>(ws.n0, threads, ws.dinv, ws.edge_offsets, ws.edge_list, edges,
+		                                                                             wing, ws.rhs, ws.x, node_state, updates_out);
 		NNRT_LAUNCH_CHECK();
 	}
 	return NNRT_OK;
@@ -520,11 +533,7 @@ nnrt_status launch_arrowhead_iteration(const ArrowheadWorkspace& ws, const doubl
 	k_arrow_prepare<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ws.N) * 32, 256)), 256, 0, stream>>>(
 	    ws.N, lm, const_cast<double*>(acc), ws.inc_off, ws.inc_list, edge_jr, ws.diag, ws.rhs, gradient_out, hessian_out);
 	NNRT_LAUNCH_CHECK();
-	nnrt_status st = arrowhead_solve_core(ws, edges, wing, error_flag, stream, true);
-	if (st) return st;
-	k_arrow_update<<<static_cast<unsigned>(ceil_div(ws.N, 256)), 256, 0, stream>>>(ws.N, ws.x, node_state, updates_out);
-	NNRT_LAUNCH_CHECK();
-	return NNRT_OK;
+	return arrowhead_solve_core(ws, edges, wing, error_flag, stream, true, node_state, updates_out);
 }
 
 } // namespace nnrt
