@@ -164,10 +164,20 @@ __global__ __launch_bounds__(256) void k_arrow_prepare(int N, float lm, double* 
 	}
 }
 
-// ---- stem: D^-1 and D^-1 B per stem node (one thread per stem node) ----
-__global__ __launch_bounds__(64) void k_arrow_stem(int n0, const float* __restrict__ diag, const int* __restrict__ edge_offsets, const int* __restrict__ edge_list,
-                             const float* __restrict__ wing, float* __restrict__ dinv, float* __restrict__ dinv_b, int* error_flag) {
-	const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// ---- stem: D^-1 and D^-1 B per stem node, four lanes per node (each forms D^-1 with the same arithmetic and the products
+// of every fourth of the node's edges), in one launch with the corner init (blocks [0, init_blocks): corner.hip's
+// corner_init_thread; both read the prepared diagonal blocks and write disjoint outputs) ----
+constexpr int STEM_LANES = 4;
+__global__ __launch_bounds__(256) void k_init_stem(CornerInitArgs ia, int init_blocks, const float* __restrict__ rhs, int n0,
+                                                   const float* __restrict__ diag, const int* __restrict__ edge_offsets,
+                                                   const int* __restrict__ edge_list, const float* __restrict__ wing, float* __restrict__ dinv,
+                                                   float* __restrict__ dinv_b, int* error_flag) {
+	if (static_cast<int>(blockIdx.x) < init_blocks) {
+		corner_init_thread(static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x, ia, diag, rhs);
+		return;
+	}
+	const int64_t t = static_cast<int64_t>(blockIdx.x - init_blocks) * blockDim.x + threadIdx.x;
+	const int i = static_cast<int>(t / STEM_LANES), sub = static_cast<int>(t % STEM_LANES);
 	if (i >= n0) return;
 	// 6 x 6 blocks are 144 B = nine 16-B words: loaded and stored as float4
 	float L[6][6];
@@ -186,17 +196,19 @@ __global__ __launch_bounds__(64) void k_arrow_stem(int n0, const float* __restri
 		for (int k = 0; k < 36; k++) L[k / 6][k % 6] = f[k];
 	}
 	if (!cholesky_small<6>(L)) {
-		atomicOr(error_flag, 1);
+		if (sub == 0) atomicOr(error_flag, 1);
 		return;
 	}
 	float Di[6][6];
 	invert_from_cholesky_small<6>(L, Di);
-	float4* o4 = reinterpret_cast<float4*>(dinv + static_cast<int64_t>(i) * 36);
+	if (sub == 0) {
+		float4* o4 = reinterpret_cast<float4*>(dinv + static_cast<int64_t>(i) * 36);
 #pragma unroll
-	for (int q = 0; q < 9; q++)
-		o4[q] = make_float4(Di[(4 * q) / 6][(4 * q) % 6], Di[(4 * q + 1) / 6][(4 * q + 1) % 6], Di[(4 * q + 2) / 6][(4 * q + 2) % 6],
-		                    Di[(4 * q + 3) / 6][(4 * q + 3) % 6]);
-	for (int ei = edge_offsets[i]; ei < edge_offsets[i + 1]; ei++) {
+		for (int q = 0; q < 9; q++)
+			o4[q] = make_float4(Di[(4 * q) / 6][(4 * q) % 6], Di[(4 * q + 1) / 6][(4 * q + 1) % 6], Di[(4 * q + 2) / 6][(4 * q + 2) % 6],
+			                    Di[(4 * q + 3) / 6][(4 * q + 3) % 6]);
+	}
+	for (int ei = edge_offsets[i] + sub; ei < edge_offsets[i + 1]; ei += STEM_LANES) {
 		const int e = edge_list[ei];
 		const float4* B4 = reinterpret_cast<const float4*>(wing + static_cast<int64_t>(e) * 36);
 		float B[36];
@@ -494,14 +506,19 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
                                  bool arap_wings, float* node_state, float* updates_out) {
 	const int m = ws.m;
 	NNRT_CHECK_ARG(m == 0 || ws.corner, "arrowhead workspace without a corner plan");
-	if (m > 0) {
-		nnrt_status st = ws.corner->launch_init(ws.n0, ws.diag, ws.rhs, edges, wing, stream);
-		if (st) return st;
+	if (ws.n0 > 0 || m > 0) {   // corner init and stem in one launch
+		const CornerInitArgs ia = m > 0 ? ws.corner->init_args(ws.n0) : CornerInitArgs{0, 0, 0, nullptr, nullptr, nullptr, nullptr};
+		const int init_blocks = m > 0 ? static_cast<int>(ceil_div(ia.threads(), 256)) : 0;
+		const int stem_blocks = static_cast<int>(ceil_div(static_cast<int64_t>(ws.n0) * STEM_LANES, 256));
+		k_init_stem<<<static_cast<unsigned>(init_blocks + stem_blocks), 256, 0, stream>>>(ia, init_blocks, ws.rhs, ws.n0, ws.diag, ws.edge_offsets,
+		                                                                                  ws.edge_list, wing, ws.dinv, ws.dinv_b, error_flag);
+		NNRT_LAUNCH_CHECK();
+		if (m > 0) {
+			nnrt_status st = ws.corner->launch_offdiag(ws.n0, edges, wing, stream);   // >= 3 layers: after the init
+			if (st) return st;
+		}
 	}
 	if (ws.n0 > 0) {
-		k_arrow_stem<<<static_cast<unsigned>(ceil_div(ws.n0, 64)), 64, 0, stream>>>(ws.n0, ws.diag, ws.edge_offsets, ws.edge_list, wing, ws.dinv,
-		                                                                           ws.dinv_b, error_flag);
-		NNRT_LAUNCH_CHECK();
 		if (m > 0 && ws.targets > 0) {
 			const CornerMap cm = ws.corner->map();
 			const unsigned grid = static_cast<unsigned>(ceil_div((static_cast<int64_t>(ws.targets) + m / 6) * 64, 256));

@@ -435,34 +435,8 @@ __device__ inline float lane_bcast(float v, int src) {
 	return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
 }
 
-// corner init: every stored tile gets its entries of C (the corner nodes' diagonal blocks) and the identity on the
-// padding; cb = b_C in the permuted order. One thread per 4 consecutive entries of a tile row (one 16-B store).
-__global__ void k_corner_init(int n0, int ld, int slots, const int2* __restrict__ slot_ij, const int* __restrict__ row_node,
-                              const float* __restrict__ diag, const float* __restrict__ rhs, float* __restrict__ tiles, float* __restrict__ cb) {
-	const int64_t idx = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-	if (idx < ld) {
-		const int rn = row_node[idx];
-		cb[idx] = rn >= 0 ? rhs[6 * static_cast<int64_t>(n0 + (rn >> 3)) + (rn & 7)] : 0.f;
-	}
-	if (idx >= static_cast<int64_t>(slots) * (TILE_ELEMS / 4)) return;
-	const int s = static_cast<int>(idx / (TILE_ELEMS / 4)), w = static_cast<int>(idx % (TILE_ELEMS / 4));
-	const int r = w / (TILE / 4), c0 = (w % (TILE / 4)) * 4;
-	const int2 ij = slot_ij[s];
-	const int R = ij.x * TILE + r;
-	const int rn = row_node[R];
-	float v[4];
-#pragma unroll
-	for (int j = 0; j < 4; j++) {
-		const int C = ij.y * TILE + c0 + j;
-		const int cn = row_node[C];
-		v[j] = 0.f;
-		if (rn >= 0 && cn >= 0) {
-			if ((rn >> 3) == (cn >> 3)) v[j] = diag[static_cast<int64_t>(n0 + (rn >> 3)) * 36 + 6 * (rn & 7) + (cn & 7)];
-		} else if (R == C) {
-			v[j] = 1.f;
-		}
-	}
-	*reinterpret_cast<float4*>(tiles + static_cast<int64_t>(s) * TILE_ELEMS + r * TILE + c0) = make_float4(v[0], v[1], v[2], v[3]);
+__global__ void k_corner_init(CornerInitArgs a, const float* __restrict__ diag, const float* __restrict__ rhs) {
+	corner_init_thread(static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x, a, diag, rhs);
 }
 
 // corner off-diagonal blocks (edges between two corner nodes, >= 3 layers; the reference drops them, A3): each entry of
@@ -939,9 +913,14 @@ CornerMap CornerSolver::map() const { return CornerMap{T, d_tile_slot, d_node_ro
 
 nnrt_status CornerSolver::launch_init(int n0, const float* diag, const float* rhs, const int32_t* edges, const float* wing, hipStream_t s) const {
 	if (nc == 0) return NNRT_OK;
-	const int64_t threads = std::max<int64_t>(static_cast<int64_t>(slots) * (TILE_ELEMS / 4), ld);
-	k_corner_init<<<static_cast<unsigned>(ceil_div(threads, 256)), 256, 0, s>>>(n0, ld, slots, d_slot_ij, d_row_node, diag, rhs, tiles, cb);
+	const CornerInitArgs ia = init_args(n0);
+	k_corner_init<<<static_cast<unsigned>(ceil_div(ia.threads(), 256)), 256, 0, s>>>(ia, diag, rhs);
 	NNRT_LAUNCH_CHECK();
+	return launch_offdiag(n0, edges, wing, s);
+}
+
+nnrt_status CornerSolver::launch_offdiag(int n0, const int32_t* edges, const float* wing, hipStream_t s) const {
+	if (nc == 0) return NNRT_OK;
 	if (n_corner_edges > 0) {
 		k_corner_offdiag<<<n_corner_edges, 64, 0, s>>>(d_corner_edges, n0, edges, wing, map());
 		NNRT_LAUNCH_CHECK();

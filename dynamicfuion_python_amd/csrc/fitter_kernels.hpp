@@ -1,6 +1,7 @@
 // Argument blocks of the GN-iteration kernels (passed by value; stable pointers so iterations can be hipGraph-captured).
 #pragma once
 
+#include <algorithm>
 #include <vector>
 
 #include "kernels.hpp"
@@ -111,6 +112,44 @@ __device__ inline float* corner_block_entry(const CornerMap& m, int a, int b, in
 	if (R >= C) return corner_entry(m, R, C);
 	return a == b ? nullptr : corner_entry(m, C, R);
 }
+// corner init (corner.hip): every stored tile gets its entries of C (the corner nodes' diagonal blocks) and the identity
+// on the padding; cb = b_C in the permuted order. Thread idx < threads(): 4 consecutive entries of a tile row (one 16-B
+// store) and, for idx < ld, one entry of cb. Exposed so the arrowhead launch can run it beside the stem (arap.hip).
+struct CornerInitArgs {
+	int n0, ld, slots;
+	const int2* slot_ij;
+	const int* row_node;
+	float* tiles;
+	float* cb;
+	int64_t threads() const { return std::max<int64_t>(static_cast<int64_t>(slots) * (CORNER_NB * CORNER_NB / 4), ld); }
+};
+__device__ inline void corner_init_thread(int64_t idx, const CornerInitArgs& a, const float* __restrict__ diag, const float* __restrict__ rhs) {
+	constexpr int TL = CORNER_NB, TE = CORNER_NB * CORNER_NB;
+	if (idx < a.ld) {
+		const int rn = a.row_node[idx];
+		a.cb[idx] = rn >= 0 ? rhs[6 * static_cast<int64_t>(a.n0 + (rn >> 3)) + (rn & 7)] : 0.f;
+	}
+	if (idx >= static_cast<int64_t>(a.slots) * (TE / 4)) return;
+	const int s = static_cast<int>(idx / (TE / 4)), w = static_cast<int>(idx % (TE / 4));
+	const int r = w / (TL / 4), c0 = (w % (TL / 4)) * 4;
+	const int2 ij = a.slot_ij[s];
+	const int R = ij.x * TL + r;
+	const int rn = a.row_node[R];
+	float v[4];
+#pragma unroll
+	for (int j = 0; j < 4; j++) {
+		const int C = ij.y * TL + c0 + j;
+		const int cn = a.row_node[C];
+		v[j] = 0.f;
+		if (rn >= 0 && cn >= 0) {
+			if ((rn >> 3) == (cn >> 3)) v[j] = diag[static_cast<int64_t>(a.n0 + (rn >> 3)) * 36 + 6 * (rn & 7) + (cn & 7)];
+		} else if (R == C) {
+			v[j] = 1.f;
+		}
+	}
+	*reinterpret_cast<float4*>(a.tiles + static_cast<int64_t>(s) * TE + r * TL + c0) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
 class CornerSolver {
 public:
 	~CornerSolver();
@@ -120,6 +159,9 @@ public:
 	nnrt_status prepare(const int32_t* edges, int E, int n0, int N, const float* corner_pos = nullptr);
 	// S = C (+ corner off-diagonal blocks) in the stored tiles, cb = b_C (permuted); diag [N,36], rhs [6N], edges / wing device
 	nnrt_status launch_init(int n0, const float* diag, const float* rhs, const int32_t* edges, const float* wing, hipStream_t s) const;
+	// the two halves of launch_init, for callers that run the init threads inside a launch of their own
+	CornerInitArgs init_args(int n0) const { return CornerInitArgs{n0, ld, slots, d_slot_ij, d_row_node, tiles, cb}; }
+	nnrt_status launch_offdiag(int n0, const int32_t* edges, const float* wing, hipStream_t s) const;   // >= 3 layers
 	// factor S (after the stem's Schur update), solve S x = cb; x -> xout[6 nc] in corner-node order
 	nnrt_status launch_solve(float* xout, int* error_flag, hipStream_t s) const;
 	CornerMap map() const;
