@@ -1666,6 +1666,11 @@ nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, cons
 	return NNRT_OK;
 }
 
+void nnrt_release_arrowhead_plans(void) {
+	std::lock_guard<std::mutex> lock(g_arrow_mu);
+	arrow_pool().clear();
+}
+
 // ---- DLPack entry points (include/nnrt_dlpack.h): validate, then forward to the pointer entry points ----------------
 namespace {
 enum class Mem { device, host };

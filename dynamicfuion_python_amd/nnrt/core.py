@@ -51,6 +51,12 @@ def _solve_block_sparse_arrowhead_cholesky(diagonal_blocks, upper_wing_blocks, u
     return x
 
 
+def release_arrowhead_plans() -> None:
+    """Frees the per-structure plans the arrowhead solve keeps for reuse (device memory; MI355X extension, no reference
+    counterpart)."""
+    N.lib().nnrt_release_arrowhead_plans()
+
+
 def matmul3d(array_of_matrices_a, array_of_matrices_b) -> torch.Tensor:
     """nnrt.core.matmul3d (cpp/pybind/core/core.cpp:32 -> cpp/core/linalg/Matmul3D.cpp:25-83): per batch entry A[b] @ B[b];
     A [batch, m, k], B [batch, k, n] or [batch, k] (array of vectors -> [batch, m, 1])."""

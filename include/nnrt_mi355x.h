@@ -337,11 +337,17 @@ nnrt_status nnrt_invert_triangular_blocks(const float* d_blocks, int32_t block_c
  * <= column for stem-to-corner blocks; row >= arrow_base for corner off-diagonal blocks), b [6N]. Coordinates outside
  * [0, N), a diagonal coordinate (row == column) or a column inside the stem (column < arrow_base) give
  * NNRT_ERROR_ARGUMENT, checked before any allocation. The Schur corner is factored tile-sparse (nested-dissection order
- * of the corner blocks); its size is bounded by device memory only. */
+ * of the corner blocks); its size is bounded by device memory only. The structure-derived plan (stem lists, corner plan,
+ * scratch) of the 4 most recently solved wing structures is kept per process and reused by a later call with the same
+ * device, block count, arrow base and coordinates (one call owns a plan at a time; calls synchronise their stream
+ * before returning it); nnrt_release_arrowhead_plans frees them. */
 nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diagonal_blocks, const float* d_wing_blocks,
                                                        const int32_t* d_wing_coordinates, int32_t wing_block_count,
                                                        int32_t diagonal_block_count, int32_t arrow_base_block_index,
                                                        const float* d_b, float* d_x, void* stream);
+/* Frees the arrowhead plans kept by nnrt_solve_block_sparse_arrowhead_cholesky (device memory; none is in use by a
+ * concurrent call: plans being solved with are not in the pool). */
+void nnrt_release_arrowhead_plans(void);
 
 /* ---- TSDF voxel block grid (NonRigidSurfaceVoxelBlockGrid, cpp/geometry/NonRigidSurfaceVoxelBlockGrid.h:30-65 over
  * VoxelBlockGrid, cpp/geometry/VoxelBlockGrid.h; Python: nnrt.geometry.NonRigidSurfaceVoxelBlockGrid, pybind

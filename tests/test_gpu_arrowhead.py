@@ -160,3 +160,27 @@ def test_arrowhead_accepts_offset_views(la):
     assert D.data_ptr() % 16 != 0 and Wb.data_ptr() % 16 != 0
     x = la.SolveBlockSparseArrowheadCholesky(D, Wb, edges, n0, b).cpu().numpy()
     assert np.array_equal(x, x_ref)
+
+
+def test_plan_reuse_and_release(la):
+    """The C-ABI keeps each wing structure's plan: solving two structures alternately (reusing both plans), new values
+    on a known structure, and a solve after releasing every plan all give the fresh-plan results."""
+    from dynamicfuion_python_amd.nnrt import core
+    s1 = grid_arrowhead(6, 5, 3, True, seed=11)
+    s2 = grid_arrowhead(7, 4, 2, False, seed=12)
+    core.release_arrowhead_plans()
+    ref1 = la.SolveBlockSparseArrowheadCholesky(*s1).cpu().numpy()
+    ref2 = la.SolveBlockSparseArrowheadCholesky(*s2).cpu().numpy()
+    for _ in range(2):
+        assert np.array_equal(la.SolveBlockSparseArrowheadCholesky(*s1).cpu().numpy(), ref1)
+        assert np.array_equal(la.SolveBlockSparseArrowheadCholesky(*s2).cpu().numpy(), ref2)
+    diag, wing, edges, n0, b = s1
+    rng = np.random.default_rng(13)
+    b2 = rng.normal(size=b.shape).astype(np.float32)
+    wing2 = (wing * 0.5).astype(np.float32)
+    x_new = la.SolveBlockSparseArrowheadCholesky(diag, wing2, edges, n0, b2).cpu().numpy()   # same structure, new values
+    core.release_arrowhead_plans()
+    x_fresh = la.SolveBlockSparseArrowheadCholesky(diag, wing2, edges, n0, b2).cpu().numpy()
+    assert np.array_equal(x_new, x_fresh)
+    x64, _ = fp64_solution(diag, wing2, edges, b2)
+    assert rel_err(x_new, x64) < 1e-5
