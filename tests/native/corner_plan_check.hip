@@ -1,0 +1,111 @@
+// Host-only check of the Schur-corner plan (csrc/corner.hip plan_corner), test infrastructure: builds the plan for an
+// arrowhead structure read from argv[1] (int32 E, n0, N, edges [E,2], optional float32 corner positions [N-n0,3]),
+// then emulates every factor launch in double precision task by task, checking that every structurally non-zero entry
+// has a stored tile, that no task of a launch writes anything another task of the same launch reads or writes, that
+// the back substitution only reads x of earlier launches or of its own chain, and that the solution of a random SPD
+// system with that structure has a residual below 1e-9. Exit code 0 = all checks pass.
+#include "corner.hip"   // the product plan code, compiled here for the host (no kernel is launched)
+#include <cmath>
+#include <cstdio>
+#include <random>
+#include <set>
+namespace nnrt { void set_error(const std::string& m) { fprintf(stderr, "%s\n", m.c_str()); } }
+using namespace nnrt;
+int main(int argc, char** argv) {
+	FILE* f = fopen(argv[1], "rb");
+	int E, n0, N;
+	fread(&E, 4, 1, f); fread(&n0, 4, 1, f); fread(&N, 4, 1, f);
+	std::vector<int32_t> edges(2 * E);
+	fread(edges.data(), 4, 2 * E, f);
+	std::vector<float> pos(3 * (N - n0));
+	const bool has_pos = fread(pos.data(), 4, pos.size(), f) == pos.size() && !pos.empty();
+	fclose(f);
+	CornerPlan p = plan_corner(edges.data(), E, n0, N, has_pos ? pos.data() : nullptr);
+	printf("positions %d\n", (int)has_pos);
+	const int nc = p.nc, m = 6 * nc, T = p.T;
+	printf("nc %d ld %d T %d H %d slots %zu tasks %zu srcs %zu back_cols %zu\n", nc, p.ld, T, p.H, p.slot_ij.size(), p.tasks.size(), p.srcs.size(), p.back_cols.size());
+	// random SPD corner with the plan's adjacency pattern (natural order)
+	std::mt19937 rng(5);
+	std::normal_distribution<double> nd(0, 0.3);
+	std::vector<double> M((size_t)m * m, 0.0);
+	std::vector<std::vector<int>> adj(nc);
+	for (int e = 0; e < E; e++) { int i = edges[2*e], j = edges[2*e+1]; if (i >= n0) { adj[i-n0].push_back(j-n0); } }
+	std::vector<std::vector<int>> st(n0);
+	for (int e = 0; e < E; e++) { int i = edges[2*e], j = edges[2*e+1]; if (i < n0) st[i].push_back(j-n0); }
+	for (auto& s : st) for (int a : s) for (int b : s) if (a < b) adj[a].push_back(b);
+	for (int a = 0; a < nc; a++) { std::sort(adj[a].begin(), adj[a].end()); adj[a].erase(std::unique(adj[a].begin(), adj[a].end()), adj[a].end()); }
+	for (int a = 0; a < nc; a++) for (int b : adj[a]) for (int r = 0; r < 6; r++) for (int c = 0; c < 6; c++) { double v = nd(rng); M[(size_t)(6*a+r)*m + 6*b+c] += v; M[(size_t)(6*b+c)*m + 6*a+r] += v; }
+	for (int i = 0; i < m; i++) { double s = 0; for (int j = 0; j < m; j++) if (j != i) s += fabs(M[(size_t)i*m+j]); M[(size_t)i*m+i] = s + 1.0; }
+	std::vector<double> bnat(m); for (auto& v : bnat) v = nd(rng);
+	// storage
+	const int TE = TILE_ELEMS;
+	std::vector<double> tiles(p.slot_ij.size() * TE, 0.0), ldiag((size_t)T * TE, 0.0), cb(p.ld, 0.0), xp(p.ld, 0.0), xout(m, 0.0);
+	auto ent = [&](int R, int C) -> double { int rn = p.row_node[R], cn = p.row_node[C]; if (rn >= 0 && cn >= 0) return M[(size_t)(6*(rn>>3)+(rn&7))*m + 6*(cn>>3)+(cn&7)]; return R == C ? 1.0 : 0.0; };
+	// every non-zero entry of M must land in a stored tile
+	for (int a = 0; a < nc; a++) for (int b = 0; b < nc; b++) { bool nz = false; for (int r=0;r<6;r++) for(int c=0;c<6;c++) nz |= M[(size_t)(6*a+r)*m+6*b+c] != 0; if (!nz) continue;
+		for (int r=0;r<6;r++) for(int c=0;c<6;c++){ int R = p.node_row[a]+r, C = p.node_row[b]+c; if (R < C) continue; if (p.tile_slot[(size_t)(R/TILE)*T + C/TILE] < 0) { printf("MISSING tile for entry %d %d\n", R, C); return 1; } } }
+	for (size_t s = 0; s < p.slot_ij.size(); s++) { int I = p.slot_ij[s].x, J = p.slot_ij[s].y; for (int r = 0; r < TILE; r++) for (int c = 0; c < TILE; c++) tiles[s*TE + r*TILE + c] = ent(I*TILE+r, J*TILE+c); }
+	for (int R = 0; R < p.ld; R++) { int rn = p.row_node[R]; cb[R] = rn >= 0 ? bnat[6*(rn>>3)+(rn&7)] : 0.0; }
+	auto tile = [&](int s) { return &tiles[(size_t)s * TE]; };
+	for (int l = 0; l < p.H; l++) {
+		std::set<std::pair<int,int>> reads, writes;   // (kind, id): 0 tile slot, 1 ldiag J, 2 cb J
+		std::vector<std::set<std::pair<int,int>>> tr, tw;
+		for (int q = p.level_off[l]; q < p.level_off[l+1]; q++) {
+			const CornerTask& tk = p.tasks[q];
+			const bool panel = q - p.level_off[l] < p.level_panel[l];
+			std::set<std::pair<int,int>> r, w;
+			const int4* src = &p.srcs[tk.src];
+			auto upd = [&](double* out, const double* A, const int4* s, int n) { for (int i=0;i<TILE;i++) for(int j=0;j<TILE;j++){ double v = A[i*TILE+j]; for (int e=0;e<n;e++){ const double* X = tile(s[e].x); const double* Y = tile(s[e].y); for(int k=0;k<TILE;k++) v -= X[i*TILE+k]*Y[j*TILE+k]; r.insert({0,s[e].x}); r.insert({0,s[e].y}); } out[i*TILE+j]=v; } };
+			auto rhsu = [&](int J, const int4* s, int n) { std::vector<double> o(TILE); for (int i=0;i<TILE;i++){ double v = cb[J*TILE+i]; for(int e=0;e<n;e++){ const double* X = tile(s[e].x); for (int k=0;k<TILE;k++) v -= X[i*TILE+k]*cb[s[e].z*TILE+k]; r.insert({2,s[e].z}); r.insert({0,s[e].x}); } o[i]=v; } return o; };
+			if (!panel) {
+				std::vector<double> o(TE); upd(o.data(), tile(tk.slot_t), src, tk.nd); r.insert({0,tk.slot_t}); w.insert({0,tk.slot_t});
+				std::copy(o.begin(), o.end(), tile(tk.slot_t));
+				if (tk.I == tk.J) { auto y = rhsu(tk.J, src, tk.nd); for (int i=0;i<TILE;i++) cb[tk.J*TILE+i] = y[i]; r.insert({2,tk.J}); w.insert({2,tk.J}); }
+			} else {
+				std::vector<double> d(TE), pp(TE); upd(d.data(), tile(tk.slot_d), src, tk.nd); r.insert({0,tk.slot_d});
+				// cholesky of d
+				for (int j=0;j<TILE;j++){ double s = d[j*TILE+j]; for(int k=0;k<j;k++) s -= d[j*TILE+k]*d[j*TILE+k]; if (!(s>0)) { printf("not PD\n"); return 1;} s = sqrt(s); d[j*TILE+j]=s; for(int i=j+1;i<TILE;i++){ double t = d[i*TILE+j]; for(int k=0;k<j;k++) t -= d[i*TILE+k]*d[j*TILE+k]; d[i*TILE+j] = t/s; } for (int c=j+1;c<TILE;c++) d[j*TILE+c]=0; }
+				if (tk.I == tk.J) {
+					auto y = rhsu(tk.J, src, tk.nd); r.insert({2,tk.J});
+					for (int i=0;i<TILE;i++){ double v=y[i]; for(int k=0;k<i;k++) v -= d[i*TILE+k]*y[k]; y[i] = v/d[i*TILE+i]; }
+					for (int i=0;i<TILE;i++) cb[tk.J*TILE+i] = y[i]; w.insert({2,tk.J});
+					std::copy(d.begin(), d.end(), &ldiag[(size_t)tk.J*TE]); w.insert({1,tk.J});
+				} else {
+					upd(pp.data(), tile(tk.slot_t), src + tk.nd, tk.np); r.insert({0,tk.slot_t});
+					// L_IJ = pp L_JJ^-T : solve X L^T = pp row by row
+					for (int i=0;i<TILE;i++) for (int j=0;j<TILE;j++){ double v = pp[i*TILE+j]; for (int k=0;k<j;k++) v -= pp[i*TILE+k]*d[j*TILE+k]; pp[i*TILE+j] = v / d[j*TILE+j]; }
+					std::copy(pp.begin(), pp.end(), tile(tk.slot_t)); w.insert({0,tk.slot_t});
+				}
+			}
+			tr.push_back(r); tw.push_back(w);
+		}
+		for (size_t a = 0; a < tw.size(); a++) for (size_t b = 0; b < tw.size(); b++) if (a != b) for (auto& x : tw[a]) if (tr[b].count(x) || tw[b].count(x)) { printf("RACE level %d task %zu writes (%d,%d) touched by task %zu\n", l, a, x.first, x.second, b); return 1; }
+	}
+	std::vector<int> done_launch(T, -1);   // launch index in which x_J was produced
+	printf("back launches %zu chains %zu\n", p.back_off.size() - 1, p.back_chains.size());
+	for (size_t l = 0; l + 1 < p.back_off.size(); l++) {
+		for (int q = p.back_off[l]; q < p.back_off[l+1]; q++) {
+			int2 chn = p.back_chains[q];
+			std::set<int> mine;
+			for (int k = 0; k < chn.y; k++) {
+				int4 c = p.back_cols[chn.x + k]; int J = c.x;
+				std::vector<double> z(TILE); for (int i=0;i<TILE;i++) z[i] = cb[J*TILE+i];
+				for (int e=0;e<c.z;e++){ int2 en = p.back_ent[c.y+e];
+					bool ok = (done_launch[en.y] >= 0 && done_launch[en.y] < (int)l) || mine.count(en.y);
+					if (!ok) { printf("BACK ORDER violation: column %d needs x_%d\n", J, en.y); return 1; }
+					const double* L = tile(en.x); for (int r=0;r<TILE;r++) for (int cc=0;cc<TILE;cc++) z[cc] -= L[r*TILE+cc]*xp[en.y*TILE+r]; }
+				const double* Ld = &ldiag[(size_t)J*TE];
+				for (int i=TILE-1;i>=0;i--){ double v = z[i]; for (int k2=i+1;k2<TILE;k2++) v -= Ld[k2*TILE+i]*xp[J*TILE+k2]; xp[J*TILE+i] = v/Ld[i*TILE+i]; }
+				for (int i=0;i<TILE;i++){ int rn = p.row_node[J*TILE+i]; if (rn>=0) xout[6*(rn>>3)+(rn&7)] = xp[J*TILE+i]; }
+				mine.insert(J);
+			}
+			for (int J : mine) done_launch[J] = (int)l;
+		}
+	}
+	for (int J = 0; J < T; J++) if (done_launch[J] < 0) { printf("column %d never solved\n", J); return 1; }
+	// residual vs natural-order M
+	double res = 0, bmax = 0;
+	for (int i=0;i<m;i++){ double s = -bnat[i]; for (int j=0;j<m;j++) s += M[(size_t)i*m+j]*xout[j]; res = std::max(res, fabs(s)); bmax = std::max(bmax, fabs(bnat[i])); }
+	printf("residual %.3g (|b| %.3g)\n", res, bmax);
+	return res < 1e-9 * bmax ? 0 : 1;
+}
