@@ -184,6 +184,9 @@ __device__ inline void scatter_row(const FaceNdc& fn, float inv_area, int u0, in
 	}
 }
 
+__device__ inline void scatter_rows(int rows, int slot, int32_t face0, const RasterOptions& o, uint64_t* keys, ScatterWaveLds& w, bool staged,
+                                    int bu0, int bv0, int tw, int th);
+
 // lane < SCATTER_FPW holds face face0 + lane (ok = it exists and is not masked out); all 64 lanes of the wave call this
 __device__ inline void scatter_wave(const FaceNdc& fn, bool ok, int32_t face0, const RasterOptions& o, uint64_t* keys, ScatterWaveLds& w) {
 	const int lane = static_cast<int>(threadIdx.x & 63);
@@ -214,6 +217,14 @@ __device__ inline void scatter_wave(const FaceNdc& fn, bool ok, int32_t face0, c
 		w.rec[lane][2] = make_float4(fn.z[2], face_inv_area(fn), __uint_as_float(static_cast<uint32_t>(u0) | static_cast<uint32_t>(u1 - u0 + 1) << 16),
 		                             __uint_as_float(static_cast<uint32_t>(v0) | (near_all ? 0x80000000u : 0u)));
 	}
+	scatter_rows(rows, lane, face0, o, keys, w, staged, bu0, bv0, tw, th);
+}
+
+// Deals the wave's face rows one per lane (rows: this lane's face's box rows, slot: its face's record) and scatters
+// them, then merges the staged tile into the image. All 64 lanes call this.
+__device__ inline void scatter_rows(int rows, int slot, int32_t face0, const RasterOptions& o, uint64_t* keys, ScatterWaveLds& w, bool staged,
+                                    int bu0, int bv0, int tw, int th) {
+	const int lane = static_cast<int>(threadIdx.x & 63);
 	int incl = rows;
 #pragma unroll
 	for (int d = 1; d < 64; d <<= 1) {
@@ -224,7 +235,7 @@ __device__ inline void scatter_wave(const FaceNdc& fn, bool ok, int32_t face0, c
 	const int start = incl - rows;
 	for (int base = 0; base < total; base += 64) {
 #pragma clang loop unroll(disable) vectorize(disable)
-		for (int t = max(start, base); t < min(start + rows, base + 64); t++) w.row[t - base] = static_cast<uint32_t>(lane) | static_cast<uint32_t>(t - start) << 8;
+		for (int t = max(start, base); t < min(start + rows, base + 64); t++) w.row[t - base] = static_cast<uint32_t>(slot) | static_cast<uint32_t>(t - start) << 8;
 		scatter_wave_sync();
 		if (base + lane < total) {
 			const uint32_t e = w.row[lane];
@@ -269,6 +280,77 @@ __device__ inline void scatter_wave(const FaceNdc& fn, bool ok, int32_t face0, c
 		const int64_t p = static_cast<int64_t>(bv0 + y) * o.W + bu0 + (i - y * tw);
 		atomicMin(reinterpret_cast<unsigned long long*>(keys + p), static_cast<unsigned long long>(k));
 	}
+}
+
+// value of the partner lane of a lane pair (lane ^ 1): DPP quad permutation [1, 0, 3, 2]
+__device__ inline int pair_swap(int v) { return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false); }
+__device__ inline float pair_swap(float v) { return __builtin_bit_cast(float, pair_swap(__builtin_bit_cast(int, v))); }
+
+// Mesh path: lane pair (2f, 2f + 1) holds face face0 + f, f < SCATTER_FPW (both lanes hold the whole projected face, ok
+// alike). The per-face setup is split between the pair -- the even lane works the x axis (the face's pixel columns),
+// the odd lane the y axis (its rows) -- so one instruction stream covers both axes (face_pixel_range's operations,
+// per axis, unchanged); the row dealing and scatter are scatter_wave's (scatter_rows).
+__device__ inline void scatter_wave_pairs(const FaceNdc& fn, bool ok, int32_t face0, const RasterOptions& o, uint64_t* keys, ScatterWaveLds& w) {
+	const int lane = static_cast<int>(threadIdx.x & 63);
+	const bool odd = lane & 1;
+	// face_pixel_range's face checks (both lanes)
+	if (ok) {
+		if (!face_finite(fn)) ok = false;
+		const float area = spa_cw(fn.x[0], fn.y[0], fn.x[1], fn.y[1], fn.x[2], fn.y[2]);
+		const bool back = area < 0.f;
+		const bool zero_area = (area <= K_EPSILON && area >= -1.f * K_EPSILON);
+		const bool zinv = fmax3f(fn.z[0], fn.z[1], fn.z[2]) < K_EPSILON;
+		if ((o.cull_back_faces && back) || zero_area || zinv) ok = false;
+	}
+	// this lane's axis: box (widened by the blur radius) and its exact pixel range
+	const float c0 = odd ? fn.y[0] : fn.x[0], c1 = odd ? fn.y[1] : fn.x[1], c2 = odd ? fn.y[2] : fn.x[2];
+	const PixelAxis ax = odd ? o.ay : o.ax;
+	const float cmin = fmin3f(c0, c1, c2), cmax = fmax3f(c0, c1, c2);
+	const float lo = cmin - o.blur, hi = cmax + o.blur;
+	int a0 = 0, a1 = -1;
+	const bool axis_ok = ok && hi >= lo;
+	if (axis_ok) {
+		a0 = pixel_first(lo, ax);
+		a1 = pixel_last(hi, ax);
+	}
+	// the pair's verdict: both boxes non-empty (face_pixel_range: the two extent checks, then u0 <= u1 && v0 <= v1)
+	const bool both_extents = axis_ok && pair_swap(static_cast<int>(axis_ok)) != 0;
+	const bool mine_nonempty = a0 <= a1;
+	ok = both_extents && mine_nonempty && pair_swap(static_cast<int>(mine_nonempty)) != 0;
+	// wave box: min / max of the valid faces' ranges per axis (butterfly over the lanes of the same parity)
+	int blo = ok ? a0 : 0x7fffffff, bhi = ok ? a1 : -1;
+#pragma unroll
+	for (int d = 32; d >= 2; d >>= 1) {
+		blo = min(blo, __shfl_xor(blo, d));
+		bhi = max(bhi, __shfl_xor(bhi, d));
+	}
+	const int bu0 = __builtin_amdgcn_readlane(blo, 0), bu1 = __builtin_amdgcn_readlane(bhi, 0);
+	const int bv0 = __builtin_amdgcn_readlane(blo, 1), bv1 = __builtin_amdgcn_readlane(bhi, 1);
+	if (bu1 < 0) return;   // wave-uniform: none of the wave's faces covers a pixel
+	const int tw = bu1 - bu0 + 1, th = bv1 - bv0 + 1;
+	const bool staged = tw * th <= SCATTER_TILE_KEYS;
+	if (staged)
+		for (int i = lane; i < tw * th; i += 64) w.keys[i] = EMPTY_KEY;
+	// the partner's range: the even lane gets (v0, v1), the odd lane (u0, u1)
+	const int p0 = pair_swap(a0), p1 = pair_swap(a1);
+	const int u0 = odd ? p0 : a0, u1 = odd ? p1 : a1, v0 = odd ? a0 : p0, v1 = odd ? a1 : p1;
+	const int slot = lane >> 1;
+	const int rows = ok && !odd ? v1 - v0 + 1 : 0;   // a face's rows are dealt from its even lane
+	// A13 near_all (as in scatter_wave): squared blur-widened box diagonal, each lane its own axis' side
+	const float side = (cmax - cmin) + 2.f * o.blur;
+	const float other = pair_swap(side);
+	const float bw = odd ? other : side, bh = odd ? side : other;
+	const bool near_all = (bw * bw + bh * bh) < 0.5f * o.blur;
+	if (ok) {
+		if (!odd) {
+			w.rec[slot][0] = make_float4(fn.x[0], fn.x[1], fn.x[2], fn.y[0]);
+			w.rec[slot][2] = make_float4(fn.z[2], face_inv_area(fn), __uint_as_float(static_cast<uint32_t>(u0) | static_cast<uint32_t>(u1 - u0 + 1) << 16),
+			                             __uint_as_float(static_cast<uint32_t>(v0) | (near_all ? 0x80000000u : 0u)));
+		} else {
+			w.rec[slot][1] = make_float4(fn.y[1], fn.y[2], fn.z[0], fn.z[1]);
+		}
+	}
+	scatter_rows(rows, slot, face0, o, keys, w, staged, bu0, bv0, tw, th);
 }
 
 __global__ __launch_bounds__(SCATTER_BLOCK) void k_raster_scatter_ndc(const float* __restrict__ face_ndc, const uint8_t* __restrict__ mask,
@@ -328,13 +410,13 @@ __global__ __launch_bounds__(SCATTER_BLOCK) void k_raster_scatter_mesh(const flo
 	__shared__ ScatterWaveLds s_wave[SCATTER_WAVES];
 	const int64_t face0 = (static_cast<int64_t>(blockIdx.x) * SCATTER_WAVES + (threadIdx.x >> 6)) * SCATTER_FPW;
 	const int lane = static_cast<int>(threadIdx.x & 63);
-	const int64_t f = face0 + lane;
+	const int64_t f = face0 + (lane >> 1);   // lane pairs (scatter_wave_pairs)
 	FaceNdc fn{};
 	NNRT_WAVE_STAMP(g_raster_stamps, 0, __builtin_amdgcn_s_memrealtime());
 	NNRT_WAVE_STAMP(g_raster_stamps, 3, NNRT_STAMP_HWID());
-	const bool ok = lane < SCATTER_FPW && f < F && project_mesh_face(wpos, faces4[f], s, near_clip, far_clip, fn);
+	const bool ok = f < F && project_mesh_face(wpos, faces4[f], s, near_clip, far_clip, fn);
 	NNRT_WAVE_STAMP(g_raster_stamps, 1, __builtin_amdgcn_s_memrealtime());
-	scatter_wave(fn, ok, static_cast<int32_t>(face0), o, keys, s_wave[threadIdx.x >> 6]);
+	scatter_wave_pairs(fn, ok, static_cast<int32_t>(face0), o, keys, s_wave[threadIdx.x >> 6]);
 	NNRT_WAVE_STAMP(g_raster_stamps, 2, __builtin_amdgcn_s_memrealtime());
 }
 
