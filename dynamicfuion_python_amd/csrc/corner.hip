@@ -771,11 +771,12 @@ struct CornerBackArgs {
 
 // Back substitution L^T x = y along chains of the elimination tree (one workgroup per chain, its columns in order; the
 // launches run from the root's chain down). Per column J: z = y_J - sum_I L_IJ^T x_I (each wave a quarter of every tile's
-// rows; the entries are read one per lane and broadcast, two tiles' loads in flight), then x_J = L_JJ^-T z by
+// rows, read as 16-B row pieces, BACK_BATCH tiles' loads in flight), then x_J = L_JJ^-T z by
 // column-oriented substitution on wave 0 (lane = column; x_r broadcast by readlane). x_J goes to global memory before
 // the workgroup barrier, so the chain's next column reads it like the x of earlier launches.
+constexpr int BACK_BATCH = 6;   // entry tiles per batch of loads (6 x (4 + 4) = 48 outstanding loads per lane)
 __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
-	__shared__ float s_part[4][TILE];
+	__shared__ __attribute__((aligned(16))) float s_part[4][TILE];
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
 	const int2 ch = a.chains[blockIdx.x];
 	for (int q = 0; q < ch.y; q++) {
@@ -787,34 +788,47 @@ __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 #pragma unroll
 			for (int r = 0; r < TILE; r++) colv[r] = Ld[r * TILE + lane];
 		}
-		float acc0 = 0.f, acc1 = 0.f;
+		// z partials: lane (row quarter rq, column group cg) covers rows 16 wave + rq + 4k (k < 4) and columns 4 cg .. 4 cg + 3
+		// of every entry tile (four 16-B loads per tile), BACK_BATCH tiles' loads in flight; the four row quarters are
+		// then summed across lanes
+		const int cg = lane & 15, rq = lane >> 4;
+		float acc[4] = {0.f, 0.f, 0.f, 0.f};
 		for (int e0 = 0; e0 < col.z; e0 += 64) {
 			const int ne = col.z - e0 < 64 ? col.z - e0 : 64;
 			const int2 mine = lane < ne ? a.ent[col.y + e0 + lane] : make_int2(0, 0);
-			for (int e = 0; e < ne; e += 2) {
-				const bool two = e + 1 < ne;
-				const int s0 = __shfl(mine.x, e), i0 = __shfl(mine.y, e);
-				const int s1 = __shfl(mine.x, two ? e + 1 : e), i1 = __shfl(mine.y, two ? e + 1 : e);
-				const float* L0 = a.tiles + static_cast<int64_t>(s0) * TILE_ELEMS + 16 * wave * TILE + lane;
-				const float* L1 = a.tiles + static_cast<int64_t>(s1) * TILE_ELEMS + 16 * wave * TILE + lane;
-				const float* x0 = a.xp + static_cast<int64_t>(i0) * TILE + 16 * wave;
-				const float* x1 = a.xp + static_cast<int64_t>(i1) * TILE + 16 * wave;
-				float l0[16], l1[16], v0[16], v1[16];
+			for (int e = 0; e < ne; e += BACK_BATCH) {
+				float4 l[BACK_BATCH][4];
+				float xv[BACK_BATCH][4];
 #pragma unroll
-				for (int r = 0; r < 16; r++) {
-					l0[r] = L0[r * TILE];
-					v0[r] = x0[r];
-					l1[r] = L1[r * TILE];
-					v1[r] = two ? x1[r] : 0.f;
+				for (int j = 0; j < BACK_BATCH; j++) {
+					const bool ok = e + j < ne;   // a missing entry repeats entry e's tile against x = 0 (exact zeros)
+					const int sj = __shfl(mine.x, ok ? e + j : e);
+					const int ij = __shfl(mine.y, ok ? e + j : e);
+					const float* Lj = a.tiles + static_cast<int64_t>(sj) * TILE_ELEMS + (16 * wave + rq) * TILE + 4 * cg;
+					const float* xj = a.xp + static_cast<int64_t>(ij) * TILE + 16 * wave + rq;
+#pragma unroll
+					for (int k = 0; k < 4; k++) {
+						l[j][k] = *reinterpret_cast<const float4*>(Lj + 4 * k * TILE);
+						xv[j][k] = ok ? xj[4 * k] : 0.f;
+					}
 				}
 #pragma unroll
-				for (int r = 0; r < 16; r++) {
-					acc0 += l0[r] * v0[r];
-					acc1 += l1[r] * v1[r];
-				}
+				for (int j = 0; j < BACK_BATCH; j++)
+#pragma unroll
+					for (int k = 0; k < 4; k++) {
+						acc[0] += l[j][k].x * xv[j][k];
+						acc[1] += l[j][k].y * xv[j][k];
+						acc[2] += l[j][k].z * xv[j][k];
+						acc[3] += l[j][k].w * xv[j][k];
+					}
 			}
 		}
-		s_part[wave][lane] = acc0 + acc1;
+#pragma unroll
+		for (int i = 0; i < 4; i++) {
+			acc[i] += __shfl_xor(acc[i], 16);
+			acc[i] += __shfl_xor(acc[i], 32);
+		}
+		if (lane < 16) *reinterpret_cast<float4*>(&s_part[wave][4 * lane]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
 		__syncthreads();
 		if (wave == 0) {
 			const float inv_d = 1.f / Ld[lane * TILE + lane];
