@@ -690,7 +690,11 @@ template <int MODE, int MAXK>
 __global__ __launch_bounds__(PIX_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) void k_fit_pixels_fused(FitPixelArgs a) {
 	constexpr int NODE_WORDS = 2 * 8 * NG_STRIDE + 3 * MAXK * 64;
 	constexpr int WORDS = NODE_WORDS > 27 * 64 ? NODE_WORDS : 27 * 64;
+#ifdef NNRT_DEV_PIX_LDS_WORDS   // timing build only: per-wave LDS region padded to this many words (occupancy probe)
+	__shared__ float s_u[PIX_BLOCK / 64][NNRT_DEV_PIX_LDS_WORDS > WORDS ? NNRT_DEV_PIX_LDS_WORDS : WORDS];
+#else
 	__shared__ float s_u[PIX_BLOCK / 64][WORDS];
+#endif
 	const int wave = static_cast<int>(threadIdx.x >> 6), lane = static_cast<int>(threadIdx.x & 63);
 	FIT_STAMP(0, __builtin_amdgcn_s_memrealtime());
 	FIT_STAMP(3, static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11))) |
