@@ -149,9 +149,9 @@ def node_pass_compulsory_bytes(P: int, P_c: int, F: int, V: int, N: int, K: int)
     """What k_fit_pixels_fused itself must move: per pixel the raster key (8 B read + 8 B reset), the reference
     point (16 B) and the residual / mask / face outputs (9 B); per contributing pixel its 64-B Jacobian record (written
     and re-read by the same wave); each face record once (int4) and its vertices' warped position and normal (2 x
-    float4); per vertex its anchors (4 B x K) and warped-Jacobian rows (2 x float4 x K); per node the fp64 accumulator
+    float4); per vertex its anchors and weights (2 x 4 B x K) and warped-Jacobian rows (24 B x K); per node the fp64 accumulator
     row (27 x 8 B read-modify-write)."""
-    return P * (16 + 16 + 9) + P_c * 64 * 2 + F * 16 + V * 32 + V * K * (4 + 32) + N * 27 * 8 * 2
+    return P * (16 + 16 + 9) + P_c * 64 * 2 + F * 16 + V * 32 + V * K * (4 + 4 + 24) + N * 27 * 8 * 2
 
 
 def count_associations(pixel_faces, residual_mask, faces, anchors) -> int:

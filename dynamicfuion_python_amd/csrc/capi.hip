@@ -376,7 +376,8 @@ struct nnrt_fitter {
 	DeviceBuffer<int32_t> anchors;
 	DeviceBuffer<float> weights;
 	DeviceBuffer<uint32_t> face_nodes;   // [F, face_node_slots(K)] distinct anchor nodes per face (once per frame)
-	DeviceBuffer<float4> wpos, wnrm, jv, jn;
+	DeviceBuffer<float4> wpos, wnrm;
+	DeviceBuffer<float2> jrows;        // [V,K,3] warped-Jacobian rows (store_jacobian_row)
 	DeviceBuffer<float4> ref_points;   // [P] reference point (x, y, z, valid)
 	DeviceBuffer<float4> records;      // [P, 4] pixel Jacobian records
 	DeviceBuffer<uint64_t> keys;
@@ -473,7 +474,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 	if ((st = mark(0))) return st;
 	const bool with_jacobians = true;
 	if ((st = launch_warp_mesh(ft->mesh_p.ptr, ft->mesh_n.ptr, ft->V, state_in, ft->anchors.ptr, ft->weights.ptr, ft->K, ft->extr,
-	                           ft->wpos.ptr, ft->wnrm.ptr, with_jacobians ? ft->jv.ptr : nullptr, ft->jn.ptr, s, from_identity)))
+	                           ft->wpos.ptr, ft->wnrm.ptr, with_jacobians ? ft->jrows.ptr : nullptr, s, from_identity)))
 		return st;
 	if ((st = mark(1))) return st;
 	const RasterOptions ro = make_raster_options(ft->H, ft->W, 0.5f / (static_cast<float>(fminf(ft->H, ft->W)) / 2.0f), ft->p.use_perspective_correction, 0, 1);
@@ -501,8 +502,8 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 	fa.wnrm = ft->wnrm.ptr;
 	fa.anchors = ft->anchors.ptr;
 	fa.face_nodes = ft->face_nodes.ptr;
-	fa.jv = ft->jv.ptr;
-	fa.jn = ft->jn.ptr;
+	fa.jrows = ft->jrows.ptr;
+	fa.weights = ft->weights.ptr;
 	fa.ref_points = ft->ref_points.ptr;
 	fa.records = ft->records.ptr;
 	fa.residuals = ft->residuals.ptr;
@@ -622,8 +623,7 @@ void nnrt_fitter_destroy(nnrt_fitter* ft) {
 	ft->face_nodes.release();
 	ft->wpos.release();
 	ft->wnrm.release();
-	ft->jv.release();
-	ft->jn.release();
+	ft->jrows.release();
 	ft->keys.release();
 	ft->residual_mask.release();
 	ft->pixel_face.release();
@@ -681,8 +681,8 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	if ((st = ft->mesh_p.ensure(3 * V)) || (st = ft->mesh_n.ensure(3 * V)) || (st = ft->faces4.ensure(F)) ||
 	    (st = ft->anchors.ensure(static_cast<size_t>(V) * K)) || (st = ft->weights.ensure(static_cast<size_t>(V) * K)) ||
 	    (st = ft->face_nodes.ensure(static_cast<size_t>(F) * face_node_slots(K))) ||
-	    (st = ft->wpos.ensure(V)) || (st = ft->wnrm.ensure(V)) || (st = ft->jv.ensure(static_cast<size_t>(V) * K)) ||
-	    (st = ft->jn.ensure(static_cast<size_t>(V) * K)) || (st = ft->ref_points.ensure(P)) || (st = ft->records.ensure(4 * P)) || (st = ft->keys.ensure(P)) ||
+	    (st = ft->wpos.ensure(V)) || (st = ft->wnrm.ensure(V)) || (st = ft->jrows.ensure(3 * static_cast<size_t>(V) * K)) ||
+	    (st = ft->ref_points.ensure(P)) || (st = ft->records.ensure(4 * P)) || (st = ft->keys.ensure(P)) ||
 	    (st = ft->residuals.ensure(P)) || (st = ft->residual_mask.ensure(P)) || (st = ft->pixel_face.ensure(P)) ||
 	    (st = ft->acc.ensure(static_cast<size_t>(N) * ACC_STRIDE)) ||
 	    (st = ft->updates.ensure(static_cast<size_t>(N) * 6)) || (st = ft->gradient.ensure(static_cast<size_t>(N) * 6)) ||
@@ -1187,7 +1187,7 @@ nnrt_status nnrt_warp_mesh(const float* d_vertices, const float* d_normals, int6
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&wp), sizeof(float4) * std::max<int64_t>(V, 1), s));
 	NNRT_HIP(hipMallocAsync(reinterpret_cast<void**>(&wn), sizeof(float4) * std::max<int64_t>(V, 1), s));
 	nnrt_status st = launch_pack_nodes(d_nodes, d_rotations, d_translations, N, state, s);
-	if (!st) st = launch_warp_mesh(d_vertices, d_normals, V, state, d_anchors, d_weights, K, make_extrinsics(h_E), wp, wn, nullptr, nullptr, s);
+	if (!st) st = launch_warp_mesh(d_vertices, d_normals, V, state, d_anchors, d_weights, K, make_extrinsics(h_E), wp, wn, nullptr, s);
 	if (!st) st = launch_unpack_float4x3(wp, V, d_out_vertices, s);
 	if (!st) st = launch_unpack_float4x3(wn, V, d_out_normals, s);
 	hipFreeAsync(state, s);

@@ -510,9 +510,16 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 #pragma unroll
 		for (int fv = 0; fv < 3; fv++) {
 			const int r = rows[fv] >= 0 ? rows[fv] : 0;
-			jv[fv] = a.jv[r];
-			if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) jn[fv] = a.jn[r];
-			else jn[fv] = make_float4(0.f, 0.f, 0.f, 0.f);
+			const float w = MODE != NNRT_ITERATION_ROTATION_ONLY ? a.weights[r] : 0.f;
+			if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) {
+				const float2* row = a.jrows + 3 * static_cast<int64_t>(r);
+				const float2 j0 = row[0], j1 = row[1], j2 = row[2];
+				jv[fv] = make_float4(j0.x, j0.y, j1.x, w);
+				jn[fv] = make_float4(j1.y, j2.x, j2.y, 0.f);
+			} else {
+				jv[fv] = make_float4(0.f, 0.f, 0.f, w);
+				jn[fv] = make_float4(0.f, 0.f, 0.f, 0.f);
+			}
 		}
 		{
 			const int64_t pp = static_cast<int64_t>(min(pv0 + (d.x >> 3), a.H - 1)) * a.W + min(pu0 + (d.x & 7), a.W - 1);

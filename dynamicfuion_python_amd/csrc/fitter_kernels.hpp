@@ -28,8 +28,8 @@ struct FitPixelArgs {
 	const float4* wnrm;     // [V] warped normals
 	const int32_t* anchors; // [V,K]
 	const uint32_t* face_nodes; // [F, face_node_slots(K)] per face: its unique anchor nodes, ascending (face_node_entry)
-	const float4* jv;       // [V,K] (-w R (v-g), w)
-	const float4* jn;       // [V,K] (-w R n, 0)
+	const float2* jrows;    // [V,K,3] (-w R (v-g), -w R n) as 24 B (store_jacobian_row)
+	const float* weights;   // [V,K] anchor weights w
 	const float4* ref_points; // [P] reference point (x, y, z, valid)
 	float* residuals;       // [P]
 	uint8_t* residual_mask; // [P]

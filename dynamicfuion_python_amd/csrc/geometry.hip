@@ -191,12 +191,12 @@ nnrt_status launch_compute_anchors(const float* points, int64_t V, const float* 
 //   warped point  v' = sum_k w_k (g_k + R_k (E v - g_k) + t_k)        Warp3dPointsAndNormalsImpl.h:334-390, WarpUtilities.h:448-467
 //   warped normal n' = sum_k w_k R_k (E_R n)    (not normalized: A12)
 //   Jv[v,k] = (-w R_k (v - g_k), w) ; Jn[v,k] = -w R_k n   (canonical v, n)   WarpedSurfaceJacobiansImpl.h:117-156
-// Outputs: float4 warped positions / normals [V] (w unused), Jv/Jn float4 [V,K] (internal layout).
+// Outputs: float4 warped positions / normals [V] (w unused), Jacobian rows [V,K] of 24 B (store_jacobian_row).
 // =====================================================================================================================
 __global__ __launch_bounds__(256) void k_warp_mesh(const float* __restrict__ points, const float* __restrict__ normals, int64_t V,
                                                    const float* __restrict__ node_state, const int32_t* __restrict__ anchors,
                                                    const float* __restrict__ weights, int K, WarpExtrinsics E, float4* __restrict__ out_p,
-                                                   float4* __restrict__ out_n, float4* __restrict__ jv, float4* __restrict__ jn) {
+                                                   float4* __restrict__ out_n, float2* __restrict__ jrows) {
 	const int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
 	if (v >= V) return;
 	const f3 p = make3(points[3 * v], points[3 * v + 1], points[3 * v + 2]);
@@ -226,17 +226,14 @@ __global__ __launch_bounds__(256) void k_warp_mesh(const float* __restrict__ poi
 			wn.x += w * Rn.x;
 			wn.y += w * Rn.y;
 			wn.z += w * Rn.z;
-			if (jv) {
+			{
 				const f3 Rj = E.identity ? Rd : matvec3(R, sub3(p, g));
 				const f3 Rnj = E.identity ? Rn : matvec3(R, n);
 				ojv = make_float4(-w * Rj.x, -w * Rj.y, -w * Rj.z, w);
 				ojn = make_float4(-w * Rnj.x, -w * Rnj.y, -w * Rnj.z, 0.f);
 			}
 		}
-		if (jv) {
-			jv[v * K + k] = ojv;
-			jn[v * K + k] = ojn;
-		}
+		if (jrows) store_jacobian_row(jrows, v * K + k, ojv, ojn);
 	}
 	out_p[v] = make_float4(wp.x, wp.y, wp.z, 0.f);
 	out_n[v] = make_float4(wn.x, wn.y, wn.z, 0.f);
@@ -263,7 +260,7 @@ template <bool IDENTITY>
 __global__ __launch_bounds__(256) void k_warp_mesh_quad(const float* __restrict__ points, const float* __restrict__ normals, int64_t V,
                                                         const float* __restrict__ node_state, const int32_t* __restrict__ anchors,
                                                         const float* __restrict__ weights, int K, WarpExtrinsics E, float4* __restrict__ out_p,
-                                                        float4* __restrict__ out_n, float4* __restrict__ jv, float4* __restrict__ jn) {
+                                                        float4* __restrict__ out_n, float2* __restrict__ jrows) {
 	NNRT_WAVE_STAMP(g_warp_stamps, 0, __builtin_amdgcn_s_memrealtime());
 	NNRT_WAVE_STAMP(g_warp_stamps, 3, NNRT_STAMP_HWID());
 	const int64_t tid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -287,10 +284,7 @@ __global__ __launch_bounds__(256) void k_warp_mesh_quad(const float* __restrict_
 			valid = true;
 			warp_slot<IDENTITY>(node_state, a, weights[v * K + k], p, n, pc, nc, E.identity, cp, cn, ojv, ojn);
 		}
-		if (jv) {
-			jv[v * K + k] = ojv;
-			jn[v * K + k] = ojn;
-		}
+		if (jrows) store_jacobian_row(jrows, v * K + k, ojv, ojn);
 	}
 	// serial slot-order sum on the quad's first lane: ((0 + c0) + c1) + c2) + c3, skipping invalid anchors
 	const float vf = valid ? 1.f : 0.f;
@@ -318,15 +312,15 @@ __global__ __launch_bounds__(256) void k_warp_mesh_quad(const float* __restrict_
 }
 
 nnrt_status launch_warp_mesh(const float* points, const float* normals, int64_t V, const float* node_state, const int32_t* anchors,
-                             const float* weights, int K, const WarpExtrinsics& E, float4* out_p, float4* out_n, float4* jv, float4* jn,
+                             const float* weights, int K, const WarpExtrinsics& E, float4* out_p, float4* out_n, float2* jrows,
                              hipStream_t stream, bool from_identity) {
 	if (V == 0) return NNRT_OK;
 	if (K <= 4) {
 		const unsigned grid = static_cast<unsigned>(ceil_div(4 * V, 256));
 		if (from_identity)
-			k_warp_mesh_quad<true><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n, jv, jn);
+			k_warp_mesh_quad<true><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n, jrows);
 		else
-			k_warp_mesh_quad<false><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n, jv, jn);
+			k_warp_mesh_quad<false><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n, jrows);
 		NNRT_LAUNCH_CHECK();
 		return NNRT_OK;
 	}
@@ -335,7 +329,7 @@ nnrt_status launch_warp_mesh(const float* points, const float* normals, int64_t 
 		return NNRT_ERROR_ARGUMENT;
 	}
 	k_warp_mesh<<<static_cast<unsigned>(ceil_div(V, 256)), 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p,
-	                                                                          out_n, jv, jn);
+	                                                                          out_n, jrows);
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;
 }

@@ -45,6 +45,15 @@ __device__ inline void warp_slot(const float* __restrict__ node_state, int32_t a
 	ojn = make_float4(-w * Rnj.x, -w * Rnj.y, -w * Rnj.z, 0.f);
 }
 
+// one (vertex, anchor) slot's warped-Jacobian row as 24 B: (jv.x, jv.y) (jv.z, jn.x) (jn.y, jn.z); the weight w is not
+// repeated here (the fitter reads it from the anchor weights)
+__device__ inline void store_jacobian_row(float2* __restrict__ jrows, int64_t slot, float4 ojv, float4 ojn) {
+	float2* o = jrows + 3 * slot;
+	o[0] = make_float2(ojv.x, ojv.y);
+	o[1] = make_float2(ojv.z, ojn.x);
+	o[2] = make_float2(ojn.y, ojn.z);
+}
+
 __device__ inline f3 apply_extrinsics_point(const WarpExtrinsics& E, f3 p) {
 	return make3(((p.x * E.m[0] + p.y * E.m[1]) + p.z * E.m[2]) + E.m[3], ((p.x * E.m[4] + p.y * E.m[5]) + p.z * E.m[6]) + E.m[7],
 	             ((p.x * E.m[8] + p.y * E.m[9]) + p.z * E.m[10]) + E.m[11]);
@@ -57,7 +66,7 @@ nnrt_status launch_compute_anchors(const float* points, int64_t V, const float* 
                                    const float* node_weights, int minimum_valid, int32_t* anchors, float* weights, hipStream_t stream,
                                    int threshold = -1);   // -1: threshold iff minimum_valid > 0 (the anchor API); 0 / 1: forced
 nnrt_status launch_warp_mesh(const float* points, const float* normals, int64_t V, const float* node_state, const int32_t* anchors,
-                             const float* weights, int K, const WarpExtrinsics& E, float4* out_p, float4* out_n, float4* jv, float4* jn,
+                             const float* weights, int K, const WarpExtrinsics& E, float4* out_p, float4* out_n, float2* jrows,
                              hipStream_t stream, bool from_identity = false);
 nnrt_status launch_pack_nodes(const float* nodes, const float* R, const float* t, int N, float* state, hipStream_t stream);
 nnrt_status launch_unpack_float4x3(const float4* in, int64_t count, float* out, hipStream_t stream);
