@@ -424,16 +424,22 @@ StemSchurLists build_stem_schur_lists(const int32_t* edges, int E, int n0, int N
 }
 
 // ---- stem back-substitution: x_D = D^-1 (b_D - B x_C) ----
-// node update (R <- R Rodrigues(omega), t += dt) from the node's solved increment x6; updates_out gets x6
-__device__ __forceinline__ void arrow_update_node(int n, const float (&xl)[6], float* __restrict__ node_state, float* __restrict__ updates_out) {
+// node update (R <- R Rodrigues(omega), t += dt) from the node's solved increment x6; updates_out gets x6. The motion
+// the iteration started from is read from state_in (the warp field's state, or a snapshot the iteration restarts from)
+// and the result written to node_state (g is never changed by an update)
+// (state_in may equal node_state: no __restrict__ on either)
+__device__ __forceinline__ void arrow_update_node(int n, const float (&xl)[6], const float* state_in, float* node_state, float* __restrict__ updates_out) {
 	for (int c = 0; c < 6; c++) updates_out[6 * static_cast<int64_t>(n) + c] = xl[c];
+	const float* os = state_in + static_cast<int64_t>(n) * NODE_STRIDE;
 	float* ns = node_state + static_cast<int64_t>(n) * NODE_STRIDE;
-	ns[3] += xl[3];
-	ns[4] += xl[4];
-	ns[5] += xl[5];
-	float dR[9], R[9];
+	float old[12];
+	for (int i = 0; i < 12; i++) old[i] = os[3 + i];
+	ns[3] = old[0] + xl[3];
+	ns[4] = old[1] + xl[4];
+	ns[5] = old[2] + xl[5];
+	float dR[9];
 	rodrigues_device(xl[0], xl[1], xl[2], dR);
-	for (int i = 0; i < 9; i++) R[i] = ns[6 + i];
+	const float* R = old + 3;
 	for (int r = 0; r < 3; r++)
 		for (int c = 0; c < 3; c++) ns[6 + 3 * r + c] = (R[3 * r] * dR[c] + R[3 * r + 1] * dR[3 + c]) + R[3 * r + 2] * dR[6 + c];
 }
@@ -442,13 +448,13 @@ __device__ __forceinline__ void arrow_update_node(int n, const float (&xl)[6], f
 // threads [n0, n_update): the corner nodes' updates from the corner solve's x (node_state non-null only)
 __global__ void k_arrow_back(int n0, int n_update, const float* __restrict__ dinv, const int* __restrict__ edge_offsets, const int* __restrict__ edge_list,
                              const int32_t* __restrict__ edges, const float* __restrict__ wing, const float* __restrict__ rhs,
-                             float* __restrict__ x, float* __restrict__ node_state, float* __restrict__ updates_out) {
+                             float* __restrict__ x, const float* state_in, float* node_state, float* __restrict__ updates_out) {
 	const int i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n0) {
 		if (node_state && i < n_update) {
 			float xl[6];
 			for (int c = 0; c < 6; c++) xl[c] = x[6 * static_cast<int64_t>(i) + c];
-			arrow_update_node(i, xl, node_state, updates_out);
+			arrow_update_node(i, xl, state_in, node_state, updates_out);
 		}
 		return;
 	}
@@ -499,12 +505,13 @@ __global__ void k_arrow_back(int n0, int n_update, const float* __restrict__ din
 	float2* xo = reinterpret_cast<float2*>(x + 6 * static_cast<int64_t>(i));
 #pragma unroll
 	for (int q = 0; q < 3; q++) xo[q] = make_float2(o[2 * q], o[2 * q + 1]);
-	if (node_state) arrow_update_node(i, o, node_state, updates_out);
+	if (node_state) arrow_update_node(i, o, state_in, node_state, updates_out);
 }
 
 nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* edges, const float* wing, int* error_flag, hipStream_t stream,
-                                 bool arap_wings, float* node_state, float* updates_out) {
+                                 bool arap_wings, float* node_state, float* updates_out, const float* state_in) {
 	const int m = ws.m;
+	if (!state_in) state_in = node_state;
 	NNRT_CHECK_ARG(m == 0 || ws.corner, "arrowhead workspace without a corner plan");
 	if (ws.n0 > 0 || m > 0) {   // corner init and stem in one launch
 		const CornerInitArgs ia = m > 0 ? ws.corner->init_args(ws.n0) : CornerInitArgs{0, 0, 0, nullptr, nullptr, nullptr, nullptr};
@@ -538,7 +545,7 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 	const int threads = node_state ? ws.N : ws.n0;   // with node_state, the node updates ride along (all N nodes)
 	if (threads > 0) {
 		k_arrow_back<<<static_cast<unsigned>(ceil_div(threads, 64)), 64, 0, stream>>>(ws.n0, threads, ws.dinv, ws.edge_offsets, ws.edge_list, edges,
-		                                                                             wing, ws.rhs, ws.x, node_state, updates_out);
+		                                                                             wing, ws.rhs, ws.x, state_in, node_state, updates_out);
 		NNRT_LAUNCH_CHECK();
 	}
 	return NNRT_OK;
@@ -546,11 +553,11 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 
 nnrt_status launch_arrowhead_iteration(const ArrowheadWorkspace& ws, const double* acc, float lm, const int32_t* edges, const float* wing,
                                        float* node_state, const float* edge_jr, float* updates_out, float* gradient_out, float* hessian_out,
-                                       int* error_flag, hipStream_t stream) {
+                                       int* error_flag, hipStream_t stream, const float* state_in) {
 	k_arrow_prepare<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ws.N) * 32, 256)), 256, 0, stream>>>(
 	    ws.N, lm, const_cast<double*>(acc), ws.inc_off, ws.inc_list, edge_jr, ws.diag, ws.rhs, gradient_out, hessian_out);
 	NNRT_LAUNCH_CHECK();
-	return arrowhead_solve_core(ws, edges, wing, error_flag, stream, true, node_state, updates_out);
+	return arrowhead_solve_core(ws, edges, wing, error_flag, stream, true, node_state, updates_out, state_in);
 }
 
 } // namespace nnrt

@@ -525,7 +525,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 		aa.edge_layers = wf->edge_layers.ptr;
 		aa.radii = wf->radii.ptr;
 		aa.node_weights = wf->node_weights.ptr;
-		aa.node_state = wf->state.ptr;
+		aa.node_state = state_in;
 		aa.edge_jr = ft->edge_jr.ptr;
 		aa.wing = ft->wing.ptr;
 		aa.edge_residuals = ft->edge_residuals.ptr;
@@ -534,7 +534,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 		if ((st = mark(5))) return st;
 		const float lm = ft->p.preconditioning_dampening_factor;
 		if ((st = launch_arrowhead_iteration(ft->aw, ft->acc.ptr, lm, wf->edges.ptr, ft->wing.ptr, wf->state.ptr, ft->edge_jr.ptr,
-		                                     ft->updates.ptr, ft->gradient.ptr, ft->hessian.ptr, ft->error_flag.ptr, s)))
+		                                     ft->updates.ptr, ft->gradient.ptr, ft->hessian.ptr, ft->error_flag.ptr, s, state_in)))
 			return st;
 	} else {
 		if ((st = mark(5))) return st;
@@ -845,11 +845,11 @@ constexpr size_t MAX_CACHED_GRAPHS = 8;
 // iteration); the stored snapshot before the first iteration of the call only (a whole frame fit from a stored state)
 enum { RESET_NONE = 0, RESET_IDENTITY = 1, RESET_SNAPSHOT = 2, RESET_SNAPSHOT_FIRST = 3 };
 
-// A restart folded into the iteration's warp / update kernels where they support it (block-diagonal path: no ARAP
-// kernel reads the state): from the identity (<= 4 anchors: the identity-specialised warp / update), or from the
-// snapshot (the general kernels read the snapshot as the starting state). Otherwise a separate kernel restarts.
+// A restart folded into the iteration's kernels where they support it: from the identity (block-diagonal path, <= 4
+// anchors: the identity-specialised warp / update), or from the snapshot (every path: the warp, the ARAP edge terms and
+// the update read the snapshot as the starting state). Otherwise a separate kernel restarts.
 bool fold_reset(const nnrt_fitter* ft) { return ft->E == 0 && ft->K <= 4; }
-bool fold_snapshot(const nnrt_fitter* ft) { return ft->E == 0; }
+bool fold_snapshot(const nnrt_fitter*) { return true; }
 
 nnrt_status check_frame(const nnrt_fitter* ft, const nnrt_warp_field* wf, const char* who) {
 	if (!ft->prepared || ft->wf != wf || ft->wf_id != wf->id) {

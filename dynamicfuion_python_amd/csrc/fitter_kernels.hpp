@@ -216,10 +216,11 @@ StemSchurLists build_stem_schur_lists(const int32_t* edges, int E, int n0, int N
 // acc -> diagonal blocks (+lm) + rhs ; arrowhead solve ; update node state
 nnrt_status launch_arrowhead_iteration(const ArrowheadWorkspace& ws, const double* acc, float lm, const int32_t* edges, const float* wing,
                                        float* node_state, const float* edge_jr, float* updates_out, float* gradient_out, float* hessian_out,
-                                       int* error_flag, hipStream_t stream);
+                                       int* error_flag, hipStream_t stream, const float* state_in = nullptr);
 // arap_wings: the wing blocks have the ARAP structure dEi^T [0 | b I] (zero outside their last three columns);
-// node_state / updates_out (fitter): apply the solved increments to the node motion in the back-substitution launch
+// node_state / updates_out (fitter): apply the solved increments to the node motion in the back-substitution launch;
+// state_in (default: node_state): the motion the iteration started from (a snapshot the iteration restarts from)
 nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* edges, const float* wing, int* error_flag, hipStream_t stream,
-                                 bool arap_wings = false, float* node_state = nullptr, float* updates_out = nullptr);
+                                 bool arap_wings = false, float* node_state = nullptr, float* updates_out = nullptr, const float* state_in = nullptr);
 
 } // namespace nnrt

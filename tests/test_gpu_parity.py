@@ -611,8 +611,8 @@ def test_graph_policy_and_cache_invalidation(nn, S, oracle_mod):
 @pytest.mark.parametrize("name", ["S1", "S1_ARAP"])
 def test_iterate_from_snapshot(nn, S, oracle_mod, name):
     """iterate_from_snapshot(count): every iteration restarts from the stored (non-identity) node motion, so after any
-    count the state equals one iteration from the snapshot -- the benchmark step (general kernels; the block-diagonal
-    path reads the snapshot as its starting state, the ARAP path copies it back first)."""
+    count the state equals one iteration from the snapshot -- the benchmark step (general kernels; both the block-diagonal
+    and the ARAP path read the snapshot as the iteration's starting state instead of copying it back first)."""
     A, G = nn.alignment, nn.geometry
     sc = _scene(S, oracle_mod, name)
     depth = scene_target(oracle_mod, sc)
