@@ -186,6 +186,9 @@ __device__ inline void scatter_row(const FaceNdc& fn, float inv_area, int u0, in
 
 __device__ inline void scatter_rows(int rows, int slot, int32_t face0, const RasterOptions& o, uint64_t* keys, ScatterWaveLds& w, bool staged,
                                     int bu0, int bv0, int tw, int th);
+#ifdef NNRT_KERNEL_STAMPS
+__device__ unsigned long long g_raster_stamps[16384][8];   // start, setup end, end, hwid, rows, tile, pixels, max pixels per lane
+#endif
 
 // lane < SCATTER_FPW holds face face0 + lane (ok = it exists and is not masked out); all 64 lanes of the wave call this
 __device__ inline void scatter_wave(const FaceNdc& fn, bool ok, int32_t face0, const RasterOptions& o, uint64_t* keys, ScatterWaveLds& w) {
@@ -233,6 +236,9 @@ __device__ inline void scatter_rows(int rows, int slot, int32_t face0, const Ras
 	}
 	const int total = __shfl(incl, 63);
 	const int start = incl - rows;
+#ifdef NNRT_KERNEL_STAMPS
+	int px_lane = 0;
+#endif
 	for (int base = 0; base < total; base += 64) {
 #pragma clang loop unroll(disable) vectorize(disable)
 		for (int t = max(start, base); t < min(start + rows, base + 64); t++) w.row[t - base] = static_cast<uint32_t>(slot) | static_cast<uint32_t>(t - start) << 8;
@@ -254,6 +260,9 @@ __device__ inline void scatter_rows(int rows, int slot, int32_t face0, const Ras
 			const uint32_t ui = __float_as_uint(q2.z), vi = __float_as_uint(q2.w);
 			const int fu0 = static_cast<int>(ui & 0xffffu), span = static_cast<int>(ui >> 16);
 			const int v = static_cast<int>(vi & 0x7fffffffu) + r;
+#ifdef NNRT_KERNEL_STAMPS
+			px_lane += span;
+#endif
 			if (!(vi >> 31)) {
 				scatter_row<0>(g, q2.y, fu0, span, v, face0 + slot, o, staged, w.keys, bu0, bv0, tw, keys);
 			} else {
@@ -268,6 +277,19 @@ __device__ inline void scatter_rows(int rows, int slot, int32_t face0, const Ras
 		}
 		scatter_wave_sync();
 	}
+#ifdef NNRT_KERNEL_STAMPS
+	{
+		int px_sum = px_lane, px_max = px_lane;
+		for (int d = 32; d >= 1; d >>= 1) {
+			px_sum += __shfl_xor(px_sum, d);
+			px_max = max(px_max, __shfl_xor(px_max, d));
+		}
+		NNRT_WAVE_STAMP(g_raster_stamps, 4, static_cast<unsigned long long>(total));
+		NNRT_WAVE_STAMP(g_raster_stamps, 5, static_cast<unsigned long long>(tw * th) << 1 | (staged ? 1ull : 0ull));
+		NNRT_WAVE_STAMP(g_raster_stamps, 6, static_cast<unsigned long long>(px_sum));
+		NNRT_WAVE_STAMP(g_raster_stamps, 7, static_cast<unsigned long long>(px_max));
+	}
+#endif
 	if (!staged) return;
 	// merge the tile row by row: i = y * tw + x, y from a float quotient corrected to the exact one
 	const float inv_tw = 1.0f / static_cast<float>(tw);
@@ -398,7 +420,6 @@ __device__ inline bool project_mesh_face(const float4* __restrict__ wpos, int4 f
 }
 
 #ifdef NNRT_KERNEL_STAMPS
-__device__ unsigned long long g_raster_stamps[16384][4];
 extern "C" int nnrt_dev_raster_stamps(unsigned long long* out) {
 	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_raster_stamps), sizeof(g_raster_stamps)) == hipSuccess ? 0 : 1;
 }

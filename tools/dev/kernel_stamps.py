@@ -29,7 +29,7 @@ for _ in range(5):
     ft.iterate_from_snapshot(wf, 0, 1)
 torch.cuda.synchronize()
 for kname, waves in (("warp", -(-4 * len(sc.points) // 256) * 4), ("raster", -(-len(sc.faces) // 32))):
-    buf = np.zeros((16384, 4), np.uint64)
+    buf = np.zeros((16384, 8 if kname == "raster" else 4), np.uint64)
     fn = getattr(lib, f"nnrt_dev_{kname}_stamps")
     fn.argtypes = [ctypes.c_void_p]
     assert fn(buf.ctypes.data) == 0
@@ -47,5 +47,18 @@ for kname, waves in (("warp", -(-4 * len(sc.points) // 256) * 4), ("raster", -(-
     if kname == "raster":
         mid = (st[:, 1] - t0) * 10
         print(f"  raster setup (projection) mean {(mid - start).mean() / 1e3:.2f} us, scatter mean {(end - mid).mean() / 1e3:.2f} us")
+        rows, tile, pxs, pxm = st[:, 4], st[:, 5] >> 1, st[:, 6], st[:, 7]
+        staged = (st[:, 5] & 1).astype(bool)
+        busy = rows > 0
+        print(f"  waves with rows {busy.sum()}; rows/wave mean {rows[busy].mean():.1f} p90 {np.percentile(rows[busy], 90):.0f} max {rows.max()}; "
+              f"two+ row rounds {(rows > 64).sum()}; unstaged {(busy & ~staged).sum()}; pixels/wave mean {pxs[busy].mean():.0f} max {pxs.max()}; "
+              f"max pixels per lane mean {pxm[busy].mean():.1f} p90 {np.percentile(pxm[busy], 90):.0f} max {pxm.max()}")
+        slow = life >= np.percentile(life, 90)
+        for lab, m in (("slowest 10%", slow), ("rest", busy & ~slow)):
+            print(f"  {lab}: lifetime {life[m].mean() / 1e3:.2f} us, setup {(mid - start)[m].mean() / 1e3:.2f}, rows {rows[m].mean():.1f}, "
+                  f"rounds {np.ceil(rows[m] / 64).mean():.2f}, pixels {pxs[m].mean():.0f}, max px/lane {pxm[m].mean():.1f}, tile {tile[m].mean():.0f}, "
+                  f"unstaged {(~staged[m]).mean():.2f}, start {start[m].mean() / 1e3:.2f}")
+        cs = np.corrcoef(np.stack([life, rows, pxs, pxm, tile, start]).astype(float))[0]
+        print("  corr(lifetime, [rows, pixels, max px/lane, tile, start]):", [round(float(c), 2) for c in cs[1:]])
     hist, edges = np.histogram(start / 1e3, bins=10)
     print("  start histogram (us):", [(round(float(e), 2), int(h)) for e, h in zip(edges, hist)])
