@@ -476,7 +476,7 @@ __device__ inline void extract_face(int64_t f, const int64_t* faces, TVertexLoad
 	float xy[3][2];
 	if (in_range) {
 		for (int i = 0; i < 3; i++) {
-			s.ndc.project(v[i].x, v[i].y, v[i].z, &xy[i][0], &xy[i][1]);
+			s.ndc.project_rn(v[i].x, v[i].y, v[i].z, &xy[i][0], &xy[i][1]);
 			inlier |= (xy[i][1] >= s.min_y && xy[i][0] >= s.min_x && xy[i][1] <= s.max_y && xy[i][0] <= s.max_x);
 		}
 	}

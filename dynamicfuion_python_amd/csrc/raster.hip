@@ -412,7 +412,7 @@ __device__ inline bool project_mesh_face(const float4* __restrict__ wpos, int4 f
 	if (!in_range) return false;
 #pragma unroll
 	for (int i = 0; i < 3; i++) {
-		s.ndc.project(v[i].x, v[i].y, v[i].z, &fn.x[i], &fn.y[i]);
+		s.ndc.project_rn(v[i].x, v[i].y, v[i].z, &fn.x[i], &fn.y[i]);
 		fn.z[i] = v[i].z;
 		inlier |= (fn.y[i] >= s.min_y && fn.x[i] >= s.min_x && fn.y[i] <= s.max_y && fn.x[i] <= s.max_x);
 	}
