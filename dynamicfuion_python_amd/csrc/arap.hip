@@ -117,6 +117,9 @@ __global__ __launch_bounds__(256) void k_arrow_prepare(int N, float lm, double* 
 	// the term this lane sums from a source incidence / a target incidence (-1: none)
 	const int q_src = q < 27 ? q : -1;
 	const int q_tgt = (q == 15 || q == 18 || q == 20) ? 27 : (q >= 24 && q < 27) ? 28 + (q - 24) : -1;
+	// the accumulator entry first: its load (memory-side atomics' target) overlaps the incidence gathers below
+	double* ad = acc + static_cast<int64_t>(n) * ACC_STRIDE;
+	const double hq = q < 27 ? ad[q] : 0.0;
 	float arap = 0.f;
 	const int beg = inc_off[n], end = inc_off[n + 1];
 	for (int u0 = beg; u0 < end; u0 += 32) {
@@ -143,8 +146,6 @@ __global__ __launch_bounds__(256) void k_arrow_prepare(int N, float lm, double* 
 		}
 		c0 = r0 + qq;
 	}
-	double* ad = acc + static_cast<int64_t>(n) * ACC_STRIDE;
-	const double hq = ad[q];
 	ad[q] = 0.0;
 	if (q < 21) {
 		const float hd = static_cast<float>(hq);
@@ -165,18 +166,21 @@ __global__ __launch_bounds__(256) void k_arrow_prepare(int N, float lm, double* 
 }
 
 // ---- stem: D^-1 and D^-1 B per stem node, four lanes per node (each forms D^-1 with the same arithmetic and the products
-// of every fourth of the node's edges), in one launch with the corner init (blocks [0, init_blocks): corner.hip's
+// of every fourth of the node's edges), in one launch with the corner init (the last init_blocks blocks: corner.hip's
 // corner_init_thread; both read the prepared diagonal blocks and write disjoint outputs) ----
 constexpr int STEM_LANES = 4;
 __global__ __launch_bounds__(256) void k_init_stem(CornerInitArgs ia, int init_blocks, const float* __restrict__ rhs, int n0,
                                                    const float* __restrict__ diag, const int* __restrict__ edge_offsets,
                                                    const int* __restrict__ edge_list, const float* __restrict__ wing, float* __restrict__ dinv,
                                                    float* __restrict__ dinv_b, int* error_flag) {
-	if (static_cast<int>(blockIdx.x) < init_blocks) {
-		corner_init_thread(static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x, ia, diag, rhs);
+	// the stem's blocks come first: their dependent chains (Cholesky, inverse, D^-1 B) start with the launch while the
+	// corner-init blocks (independent stores) fill the rest of the machine behind them
+	const int stem_blocks = static_cast<int>(gridDim.x) - init_blocks;
+	if (static_cast<int>(blockIdx.x) >= stem_blocks) {
+		corner_init_thread(static_cast<int64_t>(blockIdx.x - stem_blocks) * blockDim.x + threadIdx.x, ia, diag, rhs);
 		return;
 	}
-	const int64_t t = static_cast<int64_t>(blockIdx.x - init_blocks) * blockDim.x + threadIdx.x;
+	const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
 	const int i = static_cast<int>(t / STEM_LANES), sub = static_cast<int>(t % STEM_LANES);
 	if (i >= n0) return;
 	// 6 x 6 blocks are 144 B = nine 16-B words: loaded and stored as float4
