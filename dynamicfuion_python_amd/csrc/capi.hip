@@ -510,10 +510,8 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 	fa.residual_mask = ft->residual_mask.ptr;
 	fa.pixel_face = ft->pixel_face.ptr;
 	fa.acc = ft->acc.ptr;
-	if ((st = launch_fit_pixels(mode, fa, s, marks ? marks[3] : nullptr))) return st;
-	if ((st = mark(4))) return st;
-	if (ft->E > 0) {
-		ArapArgs aa{};
+	if (ft->E > 0) {   // the ARAP edge terms ride in the pixel launch's extra workgroups
+		ArapArgs& aa = fa.arap;
 		aa.E = ft->E;
 		aa.N = ft->N;
 		aa.n0 = ft->n0;
@@ -530,7 +528,11 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 		aa.wing = ft->wing.ptr;
 		aa.edge_residuals = ft->edge_residuals.ptr;
 		aa.error_flag = ft->error_flag.ptr;
-		if ((st = launch_arap_edges(aa, s))) return st;
+		fa.arap_blocks = fit_pixels_arap_blocks(ft->E);
+	}
+	if ((st = launch_fit_pixels(mode, fa, s, marks ? marks[3] : nullptr))) return st;
+	if ((st = mark(4))) return st;
+	if (ft->E > 0) {
 		if ((st = mark(5))) return st;
 		const float lm = ft->p.preconditioning_dampening_factor;
 		if ((st = launch_arrowhead_iteration(ft->aw, ft->acc.ptr, lm, wf->edges.ptr, ft->wing.ptr, wf->state.ptr, ft->edge_jr.ptr,

@@ -702,6 +702,16 @@ __global__ __launch_bounds__(PIX_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) 
 #else
 	__shared__ float s_u[PIX_BLOCK / 64][WORDS];
 #endif
+	// ARAP path: the launch's last arap_blocks workgroups compute the edge terms (independent of the data term: they read
+	// the node state only), in the SIMD slots the pixel waves leave free
+	if (a.arap_blocks > 0) {
+		const int first = static_cast<int>(gridDim.x) - a.arap_blocks;
+		if (static_cast<int>(blockIdx.x) >= first) {
+			const int e = (static_cast<int>(blockIdx.x) - first) * PIX_BLOCK + static_cast<int>(threadIdx.x);
+			if (e < a.arap.E) arap_edge(a.arap, e);
+			return;
+		}
+	}
 	const int wave = static_cast<int>(threadIdx.x >> 6), lane = static_cast<int>(threadIdx.x & 63);
 	FIT_STAMP(0, __builtin_amdgcn_s_memrealtime());
 	FIT_STAMP(3, static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11))) |
@@ -737,11 +747,13 @@ extern "C" int nnrt_dev_fit_stamps(unsigned long long* out) {   // [16384][4] of
 }
 #endif
 
+int fit_pixels_arap_blocks(int E) { return static_cast<int>(ceil_div(E, PIX_BLOCK)); }
+
 nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t stream, hipEvent_t between) {
 	// `between` (stage timing) is recorded before the fused launch: the pixel-pass stage reads 0, the node-pass stage
 	// times both passes
 	if (between) NNRT_EV(hipEventRecord(between, stream));
-	const unsigned grid = static_cast<unsigned>(((4 * args.tiles_x * args.tiles_y + PIX_WAVES - 1) / PIX_WAVES + 7) / 8 * 8);
+	const unsigned grid = static_cast<unsigned>(((4 * args.tiles_x * args.tiles_y + PIX_WAVES - 1) / PIX_WAVES + 7) / 8 * 8 + args.arap_blocks);
 	// anchor slots per vertex: the common 4-anchor configuration gets its own instantiation (half the slot logic)
 	const bool k4 = args.anchor_count <= 4;
 	switch (mode) {

@@ -10,6 +10,107 @@ namespace nnrt {
 
 constexpr int ACC_STRIDE = 28;   // per node: 21 JtJ upper-triangle entries + 6 Jt r (+1 pad); 3-dof modes use 6 + 3
 
+// ARAP (regularized, mode ALL) path
+struct ArapArgs {
+	int E, N, n0;
+	float lambda;
+	int use_huber;
+	float huber_delta;
+	int coverage_variable;          // 1: edge weight = max(c2_i, c2_j)
+	const int32_t* edges;           // [E,2] virtual
+	const int8_t* edge_layers;      // [E]
+	const float* radii;             // [layers]
+	const float* node_weights;      // [N] (variable coverage)
+	const float* node_state;        // [N,16]
+	float* edge_jr;                 // [E,EDGE_TERMS]: the edge's diagonal-block / gradient terms for its two nodes
+	float* wing;                    // [E,36]: dEi^T dEj
+	float* edge_residuals;          // [3E]
+	int* error_flag;
+};
+constexpr int EDGE_TERMS = 32;  // per ARAP edge: 21 + 6 source terms, 1 + 3 target terms, 1 pad
+
+// dE^T dE for dE = [skew(a) | s I] (i side) ; returns the 21 upper-triangle entries
+__device__ inline void edge_block_i(const float* j5, float (&dE)[3][6]) {
+	const float a0 = j5[0], a1 = j5[1], a2 = j5[2];
+	const float sk[3][3] = {{0.f, -a2, a1}, {a2, 0.f, -a0}, {-a1, a0, 0.f}};
+#pragma unroll
+	for (int r = 0; r < 3; r++) {
+#pragma unroll
+		for (int c = 0; c < 3; c++) dE[r][c] = sk[r][c];
+#pragma unroll
+		for (int c = 0; c < 3; c++) dE[r][3 + c] = (r == c) ? j5[3] : 0.f;
+	}
+}
+
+// one ARAP edge: residual, Jacobian terms and wing block, run by the extra workgroups of the fused pixel launch
+// (k_fit_pixels_fused's arap_blocks), beside the data term
+__device__ inline void arap_edge(const ArapArgs& a, int e) {
+	const int i = a.edges[2 * e], j = a.edges[2 * e + 1];
+	const float* si = a.node_state + static_cast<int64_t>(i) * NODE_STRIDE;
+	const float* sj = a.node_state + static_cast<int64_t>(j) * NODE_STRIDE;
+	const f3 gi = make3(si[0], si[1], si[2]), gj = make3(sj[0], sj[1], sj[2]);
+	const f3 ti = make3(si[3], si[4], si[5]), tj = make3(sj[3], sj[4], sj[5]);
+	const f3 Rd = matvec3(si + 6, sub3(gi, gj));
+	float w_res, w_jac;
+	if (a.coverage_variable) {
+		w_res = w_jac = fmaxf(a.node_weights[i], a.node_weights[j]);
+	} else {
+		if (j >= a.E) {   // reference indexes edge_layer_indices[node_j] (A3); out of bounds there
+			atomicOr(a.error_flag, 2);
+			for (int q = 0; q < EDGE_TERMS; q++) a.edge_jr[static_cast<int64_t>(e) * EDGE_TERMS + q] = 0.f;
+			return;
+		}
+		w_res = a.radii[a.edge_layers[j]];
+		w_jac = a.radii[a.edge_layers[e]];
+	}
+	const float lw = a.lambda * w_res;
+	float r[3] = {lw * (((gi.x + ti.x) - (gj.x + tj.x)) - Rd.x), lw * (((gi.y + ti.y) - (gj.y + tj.y)) - Rd.y),
+	              lw * (((gi.z + ti.z) - (gj.z + tj.z)) - Rd.z)};
+	if (a.use_huber) {
+		const float half = 0.5f * a.huber_delta * a.huber_delta;
+#pragma unroll
+		for (int c = 0; c < 3; c++) r[c] = (r[c] >= a.huber_delta) ? fabsf(r[c]) - half : 0.5f * r[c] * r[c];
+	}
+#pragma unroll
+	for (int c = 0; c < 3; c++) a.edge_residuals[3 * e + c] = r[c];
+	const float s = -a.lambda * w_jac;
+	const float j5[5] = {s * Rd.x, s * Rd.y, s * Rd.z, a.lambda * w_jac, -a.lambda * w_jac};
+	float dEi[3][6];
+	edge_block_i(j5, dEi);
+	// wing block dEi^T dEj: dEj = [0 | b I]
+	float* wb = a.wing + static_cast<int64_t>(e) * 36;
+#pragma unroll
+	for (int r0 = 0; r0 < 6; r0++)
+#pragma unroll
+		for (int c0 = 0; c0 < 6; c0++) {
+			float v = 0.f;
+			if (c0 >= 3) {
+				const float dej[3] = {(c0 - 3 == 0) ? j5[4] : 0.f, (c0 - 3 == 1) ? j5[4] : 0.f, (c0 - 3 == 2) ? j5[4] : 0.f};
+				v = (dEi[0][r0] * dej[0] + dEi[1][r0] * dej[1]) + dEi[2][r0] * dej[2];
+			}
+			wb[6 * r0 + c0] = v;
+		}
+	// the edge's contributions to its two nodes' diagonal blocks and gradients, summed per node by k_arrow_prepare (no
+	// atomics; every node sums its incident edges in ascending edge order): source i: dEi^T dEi (21 upper-triangle
+	// entries, ComputeBlockSums) + J_i^T e (6); target j: b^2 on the translation diagonal + b e (3)
+	float* src = a.edge_jr + static_cast<int64_t>(e) * EDGE_TERMS;
+	int q = 0;
+#pragma unroll
+	for (int r0 = 0; r0 < 6; r0++)
+#pragma unroll
+		for (int c0 = r0; c0 < 6; c0++) src[q++] = (dEi[0][r0] * dEi[0][c0] + dEi[1][r0] * dEi[1][c0]) + dEi[2][r0] * dEi[2][c0];
+	const float skT[3][3] = {{0.f, j5[2], -j5[1]}, {-j5[2], 0.f, j5[0]}, {j5[1], -j5[0], 0.f}};
+#pragma unroll
+	for (int c = 0; c < 3; c++) {
+		src[21 + c] = (skT[c][0] * r[0] + skT[c][1] * r[1]) + skT[c][2] * r[2];
+		src[24 + c] = j5[3] * r[c];
+	}
+	src[27] = (j5[4] * j5[4] + 0.f * 0.f) + 0.f * 0.f;   // target j: dEj = [0 | b I]
+#pragma unroll
+	for (int c = 0; c < 3; c++) src[28 + c] = j5[4] * r[c];
+	src[31] = 0.f;
+}
+
 struct FitPixelArgs {
 	int H, W, tiles_x, tiles_y;   // tiles of 16 x 16 pixels; this launch covers tile rows [tile_row0, tile_row0 + tiles_y)
 	int tile_row0;
@@ -36,6 +137,8 @@ struct FitPixelArgs {
 	int32_t* pixel_face;    // [P]
 	double* acc;            // [N, ACC_STRIDE] fp64 data-term accumulator (21 JtJ + 6 J r)
 	float4* records;        // [P, 4] per-pixel Jacobian record (pass 1 -> pass 2)
+	ArapArgs arap;          // ARAP edge terms, computed by the launch's last arap_blocks workgroups (0: none)
+	int arap_blocks;
 };
 
 struct SolveArgs {
@@ -59,30 +162,13 @@ constexpr int FACE_NODE_MAX_NODES = (1 << 20) - 1;
 inline int face_node_slots(int K) { return K <= 4 ? 12 : 3 * MAX_ANCHORS; }
 nnrt_status launch_face_node_table(const int4* faces4, int64_t F, const int32_t* anchors, int K, uint32_t* out, hipStream_t stream);
 
-// pass 1 then pass 2 in one launch (k_fit_pixels_fused); `between` (optional, stage timing) is recorded before it
+// pass 1 then pass 2 in one launch (k_fit_pixels_fused); `between` (optional, stage timing) is recorded before it.
+// args.arap_blocks extra workgroups (fit_pixels_arap_blocks(E), 0 without ARAP) compute the ARAP edge terms.
 nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t stream, hipEvent_t between = nullptr);
+int fit_pixels_arap_blocks(int E);
 nnrt_status launch_solve_update(int mode, const SolveArgs& args, hipStream_t stream, bool from_identity = false);
 
-// ARAP (regularized, mode ALL) path
-struct ArapArgs {
-	int E, N, n0;
-	float lambda;
-	int use_huber;
-	float huber_delta;
-	int coverage_variable;          // 1: edge weight = max(c2_i, c2_j)
-	const int32_t* edges;           // [E,2] virtual
-	const int8_t* edge_layers;      // [E]
-	const float* radii;             // [layers]
-	const float* node_weights;      // [N] (variable coverage)
-	const float* node_state;        // [N,16]
-	float* edge_jr;                 // [E,EDGE_TERMS]: the edge's diagonal-block / gradient terms for its two nodes
-	float* wing;                    // [E,36]: dEi^T dEj
-	float* edge_residuals;          // [3E]
-	int* error_flag;
-};
-nnrt_status launch_arap_edges(const ArapArgs& args, hipStream_t stream);
 
-constexpr int EDGE_TERMS = 32;  // per ARAP edge: 21 + 6 source terms, 1 + 3 target terms, 1 pad
 constexpr int CORNER_NB = 64;   // Schur-corner tile size (tile columns are padded to a multiple with identity)
 inline int corner_ld(int m) { return (m + CORNER_NB - 1) / CORNER_NB * CORNER_NB; }
 
