@@ -438,6 +438,8 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 		}
 	}
 
+	const int vid_ka[3] = {vid[0] * KA, vid[1] * KA, vid[2] * KA};   // first Jacobian-row slot of each face vertex
+
 	// accumulator entry of this lane within its group
 	const int grp = lane / GROUP, e = lane % GROUP;
 	const bool e_valid = e < T::NACC;
@@ -478,14 +480,9 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 			const int room = NG_CAP - filed;
 			if (head == X && rank < room) {
 				const int pos = filed + rank;
-				const uint32_t code = head_e;
+				// the pixel lane and the face-table entry (node, per-vertex slots): decoded per association in (2a)
 				slots[pos] = __builtin_bit_cast(float, lane);
-#pragma unroll
-				for (int fv = 0; fv < 3; fv++) {
-					const int k = static_cast<int>((code >> (4 * fv)) & 0xFu);
-					slots[(1 + fv) * NG_STRIDE + pos] = __builtin_bit_cast(float, k != 0xF ? vid[fv] * KA + k : -1);
-				}
-				slots[7 * NG_STRIDE + pos] = __builtin_bit_cast(float, X);
+				slots[NG_STRIDE + pos] = __builtin_bit_cast(float, head_e);
 				head_at++;
 				head_e = head_at < NSLOT ? ent[head_at * 64 + lane] : FACE_NODE_NONE;
 			}
@@ -499,11 +496,29 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 	int4 d = make_int4(0, -1, -1, -1);
 	float4 jv[3], jn[3];
 	float4 rq[4];
-	auto gather = [&](const float* slots, int count) {
+	auto gather = [&](float* slots, int count) {
 		d = make_int4(0, -1, -1, -1);
-		if (lane < count)
-			d = make_int4(__builtin_bit_cast(int, slots[lane]), __builtin_bit_cast(int, slots[NG_STRIDE + lane]),
-			              __builtin_bit_cast(int, slots[2 * NG_STRIDE + lane]), __builtin_bit_cast(int, slots[3 * NG_STRIDE + lane]));
+		int pl = 0;
+		uint32_t code = FACE_NODE_NONE;
+		if (lane < count) {
+			pl = __builtin_bit_cast(int, slots[lane]);
+			code = __builtin_bit_cast(uint32_t, slots[NG_STRIDE + lane]);
+		}
+		// the pixel lane's vertex rows (every lane takes part in the shuffles), then the anchor slot of each face vertex
+		// holding the node (-1: none) and the node into word 7
+		int vrow[3];
+#pragma unroll
+		for (int fv = 0; fv < 3; fv++) vrow[fv] = __shfl(vid_ka[fv], pl);
+		if (lane < count) {
+			int r3[3];
+#pragma unroll
+			for (int fv = 0; fv < 3; fv++) {
+				const int k = static_cast<int>((code >> (4 * fv)) & 0xFu);
+				r3[fv] = k != 0xF ? vrow[fv] + k : -1;
+			}
+			d = make_int4(pl, r3[0], r3[1], r3[2]);
+			slots[7 * NG_STRIDE + lane] = __builtin_bit_cast(float, static_cast<int>(code >> FACE_NODE_SHIFT));
+		}
 		const int rows[3] = {d.y, d.z, d.w};
 		// unconditional loads (row -1 reads row 0, ignored in (2b)): a branch per load would make the compiler wait for
 		// each gather before issuing the next, serialising the chunk's six row fetches
