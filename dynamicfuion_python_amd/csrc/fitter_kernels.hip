@@ -363,8 +363,9 @@ __device__ inline int wave_min_i32(int v) {
 // 8x8 pixels per wave (the K1 mapping); the wave's (pixel, node) associations are processed in chunks of NG_CAP.
 // (1) Group: every contributing pixel lane holds its face's distinct anchor nodes in ascending order (the per-frame face
 //     table), so the wave's next node is the minimum of the lanes' list heads (one DPP reduction); the lanes whose head it
-//     is file one association each (pixel lane, the jv/jn row of every face vertex anchored to the node) at consecutive
-//     LDS positions (mbcnt) and advance their list. A node that does not fit the chunk continues in the next one.
+//     is file one association each (pixel lane, face-table entry) at consecutive LDS positions (mbcnt) and advance their
+//     list; the gather decodes the entry into the jv/jn row of every face vertex anchored to the node. A node that does
+//     not fit the chunk continues in the next one.
 // (2) Jacobians: one association per lane (no idle lanes); J (S floats, formed as the reference forms them) and r
 //     overwrite the association's slot.
 // (3) Sums: the wave splits into 64 / GROUP lane groups; lane e of a group owns accumulator entry e (JJᵀ upper
@@ -375,7 +376,7 @@ __device__ inline int wave_min_i32(int v) {
 constexpr int NG_CAP = 64;     // associations per chunk (one lane each in (2)); lane group g of (3) owns slots
                                // [g * NG_CAP / G, (g + 1) * NG_CAP / G), zero-padded past the chunk's count
 // Slot buffers are component-major (word c of slot i at c * NG_STRIDE + i; odd stride: the words one lane group reads
-// in (3) fall in distinct LDS banks). Words: (1) pixel lane, jv/jn row per face vertex (-1: none), node at word 7;
+// in (3) fall in distinct LDS banks). Words: (1) pixel lane, face-table entry; (2a) the node at word 7;
 // (2) J[0..S-1], r at word S (zeros past the count, whose node word repeats the chunk's last node).
 constexpr int NG_STRIDE = 65;
 constexpr int NG_ROWS = 8;     // pixel rows per wave (8 x NG_ROWS pixels)
