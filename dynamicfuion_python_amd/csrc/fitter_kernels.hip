@@ -37,6 +37,8 @@ __device__ inline int pix_quadrant(const FitPixelArgs& a) {
 	return ((b % 8) * per_xcd + b / 8) * PIX_WAVES + static_cast<int>(threadIdx.x >> 6);
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 template <int MODE>
 struct ModeTraits;
 template <>
@@ -610,18 +612,29 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 		for (int j = 0; j < SEG; j += NG_BATCH) {
 			// every LDS read of the batch is issued before the dependent double adds
 			const float* base = slots + grp * SEG + j;
+			// the products two slots at a time (v_pk_mul_f32: the same correctly rounded float products)
 			float prod[NG_BATCH];
 #pragma unroll
-			for (int q = 0; q < NG_BATCH; q++) prod[q] = base[c0 * NG_STRIDE + q] * base[c1 * NG_STRIDE + q];
+			for (int q = 0; q < NG_BATCH; q += 2) {
+				const f32x2 x = {base[c0 * NG_STRIDE + q], base[c0 * NG_STRIDE + q + 1]};
+				const f32x2 y = {base[c1 * NG_STRIDE + q], base[c1 * NG_STRIDE + q + 1]};
+				const f32x2 pr = x * y;
+				prod[q] = pr.x;
+				prod[q + 1] = pr.y;
+			}
 			// every node of a chunk forms ONE contiguous run (grouping files all of a node's pending associations at once;
 			// only a chunk's capacity splits it, into the next chunk), so a batch is entirely node `cur` iff its first
-			// and last slots are: two node reads instead of one per slot
-			const bool same = __builtin_bit_cast(int, base[7 * NG_STRIDE]) == cur && __builtin_bit_cast(int, base[7 * NG_STRIDE + NG_BATCH - 1]) == cur;
+			// and last slots are: two node reads instead of one per slot (both read: no branch between them)
+			const bool same = (__builtin_bit_cast(int, base[7 * NG_STRIDE]) == cur) & (__builtin_bit_cast(int, base[7 * NG_STRIDE + NG_BATCH - 1]) == cur);
 			if (__all(same)) {
-				// independent partial sums: the double adds of a batch do not wait on one another
-				double part[4] = {0.0, 0.0, 0.0, 0.0};
+				// independent partial sums: the double adds of a batch do not wait on one another. Each partial starts at
+				// its first product (not 0.0 + product: that differs only for -0.0, which the +0.0-started accumulator
+				// absorbs either way)
+				double part[4];
 #pragma unroll
-				for (int q = 0; q < NG_BATCH; q++) part[q & 3] += static_cast<double>(prod[q]);
+				for (int q = 0; q < 4; q++) part[q] = static_cast<double>(prod[q]);
+#pragma unroll
+				for (int q = 4; q < NG_BATCH; q++) part[q & 3] += static_cast<double>(prod[q]);
 				acc += (part[0] + part[1]) + (part[2] + part[3]);
 			} else {
 				int nodes[NG_BATCH];
