@@ -623,10 +623,16 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 				prod[q + 1] = pr.y;
 			}
 			// every node of a chunk forms ONE contiguous run (grouping files all of a node's pending associations at once;
-			// only a chunk's capacity splits it, into the next chunk), so a batch is entirely node `cur` iff its first
-			// and last slots are: two node reads instead of one per slot (both read: no branch between them)
-			const bool same = (__builtin_bit_cast(int, base[7 * NG_STRIDE]) == cur) & (__builtin_bit_cast(int, base[7 * NG_STRIDE + NG_BATCH - 1]) == cur);
-			if (__all(same)) {
+			// only a chunk's capacity splits it, into the next chunk), so a batch is a single node iff its first and last
+			// slots are: two node reads instead of one per slot. A single-node batch whose node differs from `cur` (a
+			// run starting on the batch boundary, e.g. a group's first batch of a chunk) flushes `cur` first.
+			const int n_first = __builtin_bit_cast(int, base[7 * NG_STRIDE]), n_last = __builtin_bit_cast(int, base[7 * NG_STRIDE + NG_BATCH - 1]);
+			if (__all(n_first == n_last)) {
+				if (n_first != cur) {
+					if (cur >= 0 && e_valid) ng_flush(a.acc + static_cast<int64_t>(cur) * ACC_STRIDE + e, acc);
+					acc = 0.0;
+					cur = n_first;
+				}
 				// independent partial sums: the double adds of a batch do not wait on one another. Each partial starts at
 				// its first product (not 0.0 + product: that differs only for -0.0, which the +0.0-started accumulator
 				// absorbs either way)
