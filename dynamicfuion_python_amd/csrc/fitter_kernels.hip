@@ -389,7 +389,7 @@ __device__ inline void ng_flush(double* dst, double v) { atomicAdd(dst, v); }
 // development timing build only (-DNNRT_FIT_STAMPS): per wave, shader cycles spent in pass 2's phases (group, gather +
 // Jacobians, sums, and the chunk count), read back by nnrt_dev_fit_phases
 #ifdef NNRT_FIT_STAMPS
-__device__ unsigned long long g_fit_phases[16384][4];
+__device__ unsigned long long g_fit_phases[16384][8];   // group, gather + Jacobians, sums cycles; chunks; serial batches; group steps
 #define PHASE_CLOCK() __builtin_amdgcn_s_memtime()
 #endif
 
@@ -469,11 +469,17 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 	double acc = 0.0;
 	int cur = -1;
 
+#ifdef NNRT_FIT_STAMPS
+	unsigned long long n_serial = 0, n_steps = 0;   // timing build: slot-serial sum batches, grouping steps
+#endif
 	// (1) file up to NG_CAP associations into `slots`; returns the count (0: nothing pending)
 	const uint64_t lanes_below = (1ull << lane) - 1ull;
 	auto group = [&](float* slots) -> int {
 		int filed = 0;
 		while (filed < NG_CAP) {
+#ifdef NNRT_FIT_STAMPS
+			n_steps++;
+#endif
 			const int head = static_cast<int>(head_e >> FACE_NODE_SHIFT);   // FACE_NODE_MAX_NODES: list exhausted
 			const int X = wave_min_i32(head);
 			if (X == FACE_NODE_MAX_NODES) break;
@@ -643,6 +649,9 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 				for (int q = 4; q < NG_BATCH; q++) part[q & 3] += static_cast<double>(prod[q]);
 				acc += (part[0] + part[1]) + (part[2] + part[3]);
 			} else {
+#ifdef NNRT_FIT_STAMPS
+				n_serial++;
+#endif
 				int nodes[NG_BATCH];
 #pragma unroll
 				for (int q = 0; q < NG_BATCH; q++) nodes[q] = __builtin_bit_cast(int, base[7 * NG_STRIDE + q]);
@@ -702,6 +711,10 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 		const int wid_ = static_cast<int>(blockIdx.x) * (PIX_BLOCK / 64) + static_cast<int>(threadIdx.x >> 6);
 		if (lane == 0 && wid_ < 16384)
 			for (int i = 0; i < 4; i++) g_fit_phases[wid_][i] = ph[i];
+		if (lane == 0 && wid_ < 16384) {
+			g_fit_phases[wid_][4] = n_serial;
+			g_fit_phases[wid_][5] = n_steps;
+		}
 	}
 #endif
 #undef PHASE_ADD
@@ -774,8 +787,8 @@ __global__ __launch_bounds__(PIX_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) 
 	} while (0)
 
 #ifdef NNRT_FIT_STAMPS
-extern "C" int nnrt_dev_fit_phases(unsigned long long* out) {   // [16384][4] of the last fused launch
-	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fit_phases), sizeof(unsigned long long) * 16384 * 4) == hipSuccess ? 0 : 1;
+extern "C" int nnrt_dev_fit_phases(unsigned long long* out) {   // [16384][8] of the last fused launch
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fit_phases), sizeof(unsigned long long) * 16384 * 8) == hipSuccess ? 0 : 1;
 }
 extern "C" int nnrt_dev_fit_stamps(unsigned long long* out) {   // [16384][4] of the last fused launch
 	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fit_stamps), sizeof(unsigned long long) * 16384 * 4) == hipSuccess ? 0 : 1;

@@ -67,7 +67,7 @@ if out_json:
 fnp = getattr(lib, "nnrt_dev_fit_phases", None)
 if fnp is not None:
     fnp.argtypes = [ctypes.c_void_p]
-    ph = np.zeros((16384, 4), np.uint64)
+    ph = np.zeros((16384, 8), np.uint64)
     assert fnp(ph.ctypes.data) == 0
     ph = ph[:nw].astype(np.float64)
     busy = ph[:, 3] > 0
@@ -78,3 +78,5 @@ if fnp is not None:
           f"{ph[busy, 0].mean():.0f}, gather+Jacobians {ph[busy, 1].mean():.0f}, sums {ph[busy, 2].mean():.0f} "
           f"(shares {ph[busy, 0].sum() / tot.sum():.2f} / {ph[busy, 1].sum() / tot.sum():.2f} / {ph[busy, 2].sum() / tot.sum():.2f}); "
           f"{clk:.2f} cycles per ns of pass-2 time")
+    print(f"  per wave: grouping steps {ph[busy, 5].mean():.1f}, slot-serial sum batches {ph[busy, 4].mean():.2f} of "
+          f"{4 * ph[busy, 3].mean():.1f} (wave-level batches: 4 per chunk)")
