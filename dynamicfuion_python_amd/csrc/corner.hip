@@ -774,78 +774,105 @@ struct CornerBackArgs {
 // rows, read as 16-B row pieces, BACK_BATCH tiles' loads in flight), then x_J = L_JJ^-T z by
 // column-oriented substitution on wave 0 (lane = column; x_r broadcast by readlane). x_J goes to global memory before
 // the workgroup barrier, so the chain's next column reads it like the x of earlier launches.
+// Per column only the entry tiles and their x are a memory round trip on the chain's path: the chain's column
+// descriptors are staged in LDS up front, each column's first 64 entry descriptors are fetched during the previous
+// column (wave 1, into LDS before its last barrier), and wave 0's y_J and L_JJ diagonal loads are issued with its L_JJ
+// columns, ahead of the sums (round 3: four dependent round trips per column before).
 constexpr int BACK_BATCH = 6;   // entry tiles per batch of loads (6 x (4 + 4) = 48 outstanding loads per lane)
+constexpr int BACK_COLS = 64;   // chain columns whose descriptors are staged in LDS at a time
 __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 	__shared__ __attribute__((aligned(16))) float s_part[4][TILE];
+	__shared__ int4 s_cols[BACK_COLS];
+	__shared__ int2 s_ent[2][64];   // first 64 entry descriptors of the current (q & 1) and the next column
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
 	const int2 ch = a.chains[blockIdx.x];
-	for (int q = 0; q < ch.y; q++) {
-		const int4 col = a.cols[ch.x + q];
-		const int J = col.x;
-		const float* Ld = a.ldiag + static_cast<int64_t>(J) * TILE_ELEMS;
-		float colv[TILE];   // colv[r] = L_JJ[r][lane] (wave 0; issued before the sums so the loads overlap them)
-		if (wave == 0) {
-#pragma unroll
-			for (int r = 0; r < TILE; r++) colv[r] = Ld[r * TILE + lane];
-		}
-		// z partials: lane (row quarter rq, column group cg) covers rows 16 wave + rq + 4k (k < 4) and columns 4 cg .. 4 cg + 3
-		// of every entry tile (four 16-B loads per tile), BACK_BATCH tiles' loads in flight; the four row quarters are
-		// then summed across lanes
-		const int cg = lane & 15, rq = lane >> 4;
-		float acc[4] = {0.f, 0.f, 0.f, 0.f};
-		for (int e0 = 0; e0 < col.z; e0 += 64) {
-			const int ne = col.z - e0 < 64 ? col.z - e0 : 64;
-			const int2 mine = lane < ne ? a.ent[col.y + e0 + lane] : make_int2(0, 0);
-			for (int e = 0; e < ne; e += BACK_BATCH) {
-				float4 l[BACK_BATCH][4];
-				float xv[BACK_BATCH][4];
-#pragma unroll
-				for (int j = 0; j < BACK_BATCH; j++) {
-					const bool ok = e + j < ne;   // a missing entry repeats entry e's tile against x = 0 (exact zeros)
-					const int sj = __shfl(mine.x, ok ? e + j : e);
-					const int ij = __shfl(mine.y, ok ? e + j : e);
-					const float* Lj = a.tiles + static_cast<int64_t>(sj) * TILE_ELEMS + (16 * wave + rq) * TILE + 4 * cg;
-					const float* xj = a.xp + static_cast<int64_t>(ij) * TILE + 16 * wave + rq;
-#pragma unroll
-					for (int k = 0; k < 4; k++) {
-						l[j][k] = *reinterpret_cast<const float4*>(Lj + 4 * k * TILE);
-						xv[j][k] = ok ? xj[4 * k] : 0.f;
-					}
-				}
-#pragma unroll
-				for (int j = 0; j < BACK_BATCH; j++)
-#pragma unroll
-					for (int k = 0; k < 4; k++) {
-						acc[0] += l[j][k].x * xv[j][k];
-						acc[1] += l[j][k].y * xv[j][k];
-						acc[2] += l[j][k].z * xv[j][k];
-						acc[3] += l[j][k].w * xv[j][k];
-					}
-			}
-		}
-#pragma unroll
-		for (int i = 0; i < 4; i++) {
-			acc[i] += __shfl_xor(acc[i], 16);
-			acc[i] += __shfl_xor(acc[i], 32);
-		}
-		if (lane < 16) *reinterpret_cast<float4*>(&s_part[wave][4 * lane]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+	for (int q0 = 0; q0 < ch.y; q0 += BACK_COLS) {
+		const int nq = ch.y - q0 < BACK_COLS ? ch.y - q0 : BACK_COLS;
+		if (t < nq) s_cols[t] = a.cols[ch.x + q0 + t];
 		__syncthreads();
-		if (wave == 0) {
-			const float inv_d = 1.f / Ld[lane * TILE + lane];
-			float z = a.cb[static_cast<int64_t>(J) * TILE + lane] - ((s_part[0][lane] + s_part[1][lane]) + (s_part[2][lane] + s_part[3][lane]));
-			float x = 0.f;
-#pragma unroll
-			for (int r = TILE - 1; r >= 0; r--) {
-				const float xr = lane_bcast(z, r) * lane_bcast(inv_d, r);   // x_r = z_r / L_rr
-				x = lane == r ? xr : x;
-				z -= colv[r] * xr;   // z_c -= L_rc x_r (only c < r matter)
-			}
-			const int64_t row = static_cast<int64_t>(J) * TILE + lane;
-			a.xp[row] = x;
-			const int rn = a.row_node[row];
-			if (rn >= 0) a.xout[6 * static_cast<int64_t>(rn >> 3) + (rn & 7)] = x;
+		if (wave == 1) {
+			const int4 c0 = s_cols[0];
+			s_ent[0][lane] = lane < c0.z ? a.ent[c0.y + lane] : make_int2(0, 0);
 		}
-		__syncthreads();   // x_J visible to the chain's next column; s_part free
+		__syncthreads();
+		for (int q = 0; q < nq; q++) {
+			const int4 col = s_cols[q];
+			const int J = col.x;
+			const float* Ld = a.ldiag + static_cast<int64_t>(J) * TILE_ELEMS;
+			float colv[TILE];   // colv[r] = L_JJ[r][lane] (wave 0; issued before the sums so the loads overlap them)
+			float yv = 0.f, dv = 1.f;
+			if (wave == 0) {
+	#pragma unroll
+				for (int r = 0; r < TILE; r++) colv[r] = Ld[r * TILE + lane];
+				yv = a.cb[static_cast<int64_t>(J) * TILE + lane];
+				dv = Ld[lane * TILE + lane];
+			}
+			const bool has_next = q + 1 < nq;
+			int2 nxt = make_int2(0, 0);
+			if (wave == 1 && has_next) {
+				const int4 cn = s_cols[q + 1];
+				if (lane < cn.z) nxt = a.ent[cn.y + lane];
+			}
+			// z partials: lane (row quarter rq, column group cg) covers rows 16 wave + rq + 4k (k < 4) and columns 4 cg .. 4 cg + 3
+			// of every entry tile (four 16-B loads per tile), BACK_BATCH tiles' loads in flight; the four row quarters are
+			// then summed across lanes
+			const int cg = lane & 15, rq = lane >> 4;
+			float acc[4] = {0.f, 0.f, 0.f, 0.f};
+			for (int e0 = 0; e0 < col.z; e0 += 64) {
+				const int ne = col.z - e0 < 64 ? col.z - e0 : 64;
+				const int2 mine = e0 == 0 ? s_ent[q & 1][lane] : lane < ne ? a.ent[col.y + e0 + lane] : make_int2(0, 0);
+				for (int e = 0; e < ne; e += BACK_BATCH) {
+					float4 l[BACK_BATCH][4];
+					float xv[BACK_BATCH][4];
+	#pragma unroll
+					for (int j = 0; j < BACK_BATCH; j++) {
+						const bool ok = e + j < ne;   // a missing entry repeats entry e's tile against x = 0 (exact zeros)
+						const int sj = __shfl(mine.x, ok ? e + j : e);
+						const int ij = __shfl(mine.y, ok ? e + j : e);
+						const float* Lj = a.tiles + static_cast<int64_t>(sj) * TILE_ELEMS + (16 * wave + rq) * TILE + 4 * cg;
+						const float* xj = a.xp + static_cast<int64_t>(ij) * TILE + 16 * wave + rq;
+	#pragma unroll
+						for (int k = 0; k < 4; k++) {
+							l[j][k] = *reinterpret_cast<const float4*>(Lj + 4 * k * TILE);
+							xv[j][k] = ok ? xj[4 * k] : 0.f;
+						}
+					}
+	#pragma unroll
+					for (int j = 0; j < BACK_BATCH; j++)
+	#pragma unroll
+						for (int k = 0; k < 4; k++) {
+							acc[0] += l[j][k].x * xv[j][k];
+							acc[1] += l[j][k].y * xv[j][k];
+							acc[2] += l[j][k].z * xv[j][k];
+							acc[3] += l[j][k].w * xv[j][k];
+						}
+				}
+			}
+	#pragma unroll
+			for (int i = 0; i < 4; i++) {
+				acc[i] += __shfl_xor(acc[i], 16);
+				acc[i] += __shfl_xor(acc[i], 32);
+			}
+			if (lane < 16) *reinterpret_cast<float4*>(&s_part[wave][4 * lane]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+			__syncthreads();
+			if (wave == 0) {
+				const float inv_d = 1.f / dv;
+				float z = yv - ((s_part[0][lane] + s_part[1][lane]) + (s_part[2][lane] + s_part[3][lane]));
+				float x = 0.f;
+	#pragma unroll
+				for (int r = TILE - 1; r >= 0; r--) {
+					const float xr = lane_bcast(z, r) * lane_bcast(inv_d, r);   // x_r = z_r / L_rr
+					x = lane == r ? xr : x;
+					z -= colv[r] * xr;   // z_c -= L_rc x_r (only c < r matter)
+				}
+				const int64_t row = static_cast<int64_t>(J) * TILE + lane;
+				a.xp[row] = x;
+				const int rn = a.row_node[row];
+				if (rn >= 0) a.xout[6 * static_cast<int64_t>(rn >> 3) + (rn & 7)] = x;
+			}
+			if (wave == 1 && has_next) s_ent[(q + 1) & 1][lane] = nxt;
+			__syncthreads();   // x_J visible to the chain's next column; s_part free; the next column's entries staged
+		}
 	}
 }
 
