@@ -232,10 +232,11 @@ def test_arrowhead_solver_vs_oracle(nn, oracle_mod, n0, n1, degree):
 # ---------------------------------------------------------------------------------------------------------------------
 # fused GN iteration
 # ---------------------------------------------------------------------------------------------------------------------
-def _gpu_fit(nn, sc, depth, iterations=1, lm=0.001, modes=None, tukey=False, coverage_method=0, graph=True, extrinsics=None, **fkw):
+def _gpu_fit(nn, sc, depth, iterations=1, lm=0.001, modes=None, tukey=False, coverage_method=0, graph=True, extrinsics=None,
+             anchor_count=4, **fkw):
     G, A = nn.geometry, nn.alignment
     modes = modes or [A.IterationMode.ALL]
-    wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod(coverage_method),
+    wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, anchor_count, 0, G.WarpNodeCoverageComputationMethod(coverage_method),
                                       sc.layer_count)
     ft = A.DeformableMeshToImageFitter(iterations, modes, preconditioning_dampening_factor=lm, use_tukey_penalty_for_data_term=tukey,
                                        use_hip_graph=2 if graph else 0, **fkw)
@@ -273,6 +274,32 @@ def test_fit_one_iteration_parity(nn, S, oracle_mod, name):
     _compare_iteration(dg_o, dg_g, 6, len(sc.nodes))
     assert rel_err(wf.get_node_translations(True), t_o) < 1e-4
     assert rel_err(wf.get_node_rotations(True) - np.eye(3), R_o - np.eye(3)) < 1e-4
+
+
+@pytest.mark.parametrize("name,k", [("S1", 1), ("S1", 3), ("C1", 6), ("C1", 8)])
+def test_fit_anchor_count_parity(nn, S, oracle_mod, name, k):
+    """FitToImage with anchor counts other than the common 4 (the warp field's anchor_count,
+    HierarchicalGraphWarpField.h:44): K < 4 runs the 4-slot pixel-kernel instantiation with empty slots, K > 4 the
+    MAX_ANCHORS one and the lane-per-vertex warp; every stage against the oracle iteration with the same K."""
+    sc = _scene(S, oracle_mod, name)
+    depth = scene_target(oracle_mod, sc)
+    R_o, t_o, dg_o = oracle_fit_scene(oracle_mod, sc, depth, 1, anchor_count=k)
+    wf, ft, dg_g = _gpu_fit(nn, sc, depth, 1, anchor_count=k)
+    _compare_iteration(dg_o, dg_g, 6, len(sc.nodes))
+    assert rel_err(wf.get_node_translations(True), t_o) < 1e-4
+    assert rel_err(wf.get_node_rotations(True) - np.eye(3), R_o - np.eye(3)) < 1e-4
+
+
+def test_fit_without_valid_depth_parity(nn, S, oracle_mod):
+    """A depth frame with no valid pixel (DeformableMeshToImageFitter.cpp:111-275 with an empty residual mask): no data
+    term, H = LM damping only, a zero update and the reference's |omega| = 0 Rodrigues NaN (A7) -- on both
+    implementations, NaN for NaN."""
+    sc = _scene(S, oracle_mod, "S1")
+    depth = np.zeros_like(scene_target(oracle_mod, sc))
+    _, _, dg_o = oracle_fit_scene(oracle_mod, sc, depth, 1)
+    wf, ft, dg_g = _gpu_fit(nn, sc, depth, 1)
+    assert not dg_g["residual_mask"].any() and not dg_o["residual_mask"].any()
+    _compare_iteration(dg_o, dg_g, 6, len(sc.nodes))
 
 
 @pytest.mark.parametrize("mode", ["TRANSLATION_ONLY", "ROTATION_ONLY"])
