@@ -311,6 +311,32 @@ def test_fit_single_mode_parity(nn, S, oracle_mod, mode):
     _compare_iteration(dg_o, dg_g, 3, len(sc.nodes))
 
 
+def test_fit_mode_cycle_state_synchronised(nn, S, oracle_mod):
+    """An iteration-mode list cycles over the iterations (DeformableMeshToImageFitter.cpp:111-120, mode = modes[i %
+    count]): TRANSLATION_ONLY, ROTATION_ONLY, ALL, TRANSLATION_ONLY from one prepared frame, each iteration checked
+    against the oracle's single-mode iteration started from exactly the GPU's node motion before it."""
+    G, A = nn.geometry, nn.alignment
+    sc = _scene(S, oracle_mod, "S1")
+    depth = scene_target(oracle_mod, sc)
+    N = len(sc.nodes)
+    modes = ["TRANSLATION_ONLY", "ROTATION_ONLY", "ALL"]
+    wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE,
+                                      sc.layer_count)
+    ft = A.DeformableMeshToImageFitter(4, [A.IterationMode[m] for m in modes], preconditioning_dampening_factor=0.001)
+    ft.prepare(wf, G.TriangleMesh(sc.points, sc.normals, sc.faces), depth, None, sc.K)
+    for k in range(4):
+        R0, t0 = wf.get_node_rotations(True), wf.get_node_translations(True)
+        ft.iterate(wf, k, 1)
+        m = modes[k % len(modes)]
+        _, _, dg_o = oracle_fit_scene(oracle_mod, sc, depth, 1, R0=R0, t0=t0, modes=(m,))
+        _compare_iteration(dg_o, ft.diagnostics(), 6 if m == "ALL" else 3, N)
+        R1, t1 = wf.get_node_rotations(True), wf.get_node_translations(True)
+        if m == "TRANSLATION_ONLY":
+            assert np.array_equal(R1, R0)
+        if m == "ROTATION_ONLY":
+            assert np.array_equal(t1, t0)
+
+
 def test_fit_tukey_and_variable_coverage_parity(nn, S, oracle_mod):
     sc = _scene(S, oracle_mod, "S1")
     depth = scene_target(oracle_mod, sc)
