@@ -100,7 +100,8 @@ constexpr int SCATTER_TILE_KEYS = 512;                                   // 4 Ki
 
 struct ScatterWaveLds {
 	uint64_t keys[SCATTER_TILE_KEYS];
-	float4 rec[SCATTER_FPW][3];   // x0 x1 x2 y0 | y1 y2 z0 z1 | z2 inv_area (u0 | span_u << 16) (v0 | near_all << 31)
+	float4 rec[SCATTER_FPW][4];   // x0 x1 x2 y0 | y1 y2 z0 z1 | z2 inv_area (u0 | span_u << 16) (v0 | fast << 30 | near_all << 31) |
+	                              // A x1-x2 x2-x0 x0-x1 (the rows' face constants: face_row_constants)
 	uint32_t row[64];             // one round of row tasks: face slot | row << 8
 };
 
@@ -153,16 +154,27 @@ __device__ inline bool depth_near_all_fast(const FaceNdc& f, float s0, float s1,
 	return !(depth < 0.f);
 }
 
+// A face's row-invariant terms, formed once per face in the wave's setup instead of once per row: (A = spa_cw(v0, v1, v2)
+// + K_EPSILON, x1 - x2, x2 - x0, x0 - x1) -- the same operations scatter_row used to repeat per row -- and whether a
+// near_all face's rows take depth_near_all_fast (its conditions on A, the depths and the options).
+__device__ inline float4 face_row_constants(const FaceNdc& fn) {
+	return make_float4(spa_cw(fn.x[0], fn.y[0], fn.x[1], fn.y[1], fn.x[2], fn.y[2]) + K_EPSILON, fn.x[1] - fn.x[2], fn.x[2] - fn.x[0], fn.x[0] - fn.x[1]);
+}
+__device__ inline bool face_rows_fast(const FaceNdc& fn, float A, const RasterOptions& o) {
+	return !o.clip_barycentric && o.blur < 1e20f && fabsf(A) > 1e-30f && fabsf(A) < 1e30f &&
+	       fmaxf(fmaxf(fabsf(fn.z[0]), fabsf(fn.z[1])), fabsf(fn.z[2])) < 1e10f;
+}
+
 // one face row: pixels u0 .. u0 + span - 1 of image row v. MODE 0: full test (distance included); 1: near_all face
 // (guarded quotients); 2: near_all face on the fast path (depth_near_all_fast's conditions hold).
 template <int MODE>
-__device__ inline void scatter_row(const FaceNdc& fn, float inv_area, int u0, int span, int v, int32_t face, const RasterOptions& o, bool staged,
-                                   uint64_t* tile, int tu0, int tv0, int tw, uint64_t* keys) {
+__device__ inline void scatter_row(const FaceNdc& fn, float inv_area, float4 k, int u0, int span, int v, int32_t face, const RasterOptions& o,
+                                   bool staged, uint64_t* tile, int tu0, int tv0, int tw, uint64_t* keys) {
 	const float py = pixel_ndc(v, o.ay);
-	const float A = spa_cw(fn.x[0], fn.y[0], fn.x[1], fn.y[1], fn.x[2], fn.y[2]) + K_EPSILON;
+	const float A = k.x;
 	// spa_cw(p, a, b) = (px - ax) * (ay - by) - (py - ay) * (ax - bx), edges (v1, v2), (v2, v0), (v0, v1)
 	const float c0 = fn.y[1] - fn.y[2], c1 = fn.y[2] - fn.y[0], c2 = fn.y[0] - fn.y[1];
-	const float r0 = (py - fn.y[1]) * (fn.x[1] - fn.x[2]), r1 = (py - fn.y[2]) * (fn.x[2] - fn.x[0]), r2 = (py - fn.y[0]) * (fn.x[0] - fn.x[1]);
+	const float r0 = (py - fn.y[1]) * k.y, r1 = (py - fn.y[2]) * k.z, r2 = (py - fn.y[0]) * k.w;
 	uint64_t* trow = tile + (v - tv0) * tw - tu0;
 #pragma clang loop unroll(disable) vectorize(disable)
 	for (int u = u0; u < u0 + span; u++) {
@@ -217,8 +229,11 @@ __device__ inline void scatter_wave(const FaceNdc& fn, bool ok, int32_t face0, c
 		const bool near_all = (bw * bw + bh * bh) < 0.5f * o.blur;
 		w.rec[lane][0] = make_float4(fn.x[0], fn.x[1], fn.x[2], fn.y[0]);
 		w.rec[lane][1] = make_float4(fn.y[1], fn.y[2], fn.z[0], fn.z[1]);
+		const float4 k = face_row_constants(fn);
+		const bool fast = face_rows_fast(fn, k.x, o);
 		w.rec[lane][2] = make_float4(fn.z[2], face_inv_area(fn), __uint_as_float(static_cast<uint32_t>(u0) | static_cast<uint32_t>(u1 - u0 + 1) << 16),
-		                             __uint_as_float(static_cast<uint32_t>(v0) | (near_all ? 0x80000000u : 0u)));
+		                             __uint_as_float(static_cast<uint32_t>(v0) | (fast ? 0x40000000u : 0u) | (near_all ? 0x80000000u : 0u)));
+		w.rec[lane][3] = k;
 	}
 	scatter_rows(rows, lane, face0, o, keys, w, staged, bu0, bv0, tw, th);
 }
@@ -246,7 +261,7 @@ __device__ inline void scatter_rows(int rows, int slot, int32_t face0, const Ras
 		if (base + lane < total) {
 			const uint32_t e = w.row[lane];
 			const int slot = static_cast<int>(e & 255u), r = static_cast<int>(e >> 8);
-			const float4 q0 = w.rec[slot][0], q1 = w.rec[slot][1], q2 = w.rec[slot][2];
+			const float4 q0 = w.rec[slot][0], q1 = w.rec[slot][1], q2 = w.rec[slot][2], q3 = w.rec[slot][3];
 			FaceNdc g;
 			g.x[0] = q0.x;
 			g.x[1] = q0.y;
@@ -259,21 +274,16 @@ __device__ inline void scatter_rows(int rows, int slot, int32_t face0, const Ras
 			g.z[2] = q2.x;
 			const uint32_t ui = __float_as_uint(q2.z), vi = __float_as_uint(q2.w);
 			const int fu0 = static_cast<int>(ui & 0xffffu), span = static_cast<int>(ui >> 16);
-			const int v = static_cast<int>(vi & 0x7fffffffu) + r;
+			const int v = static_cast<int>(vi & 0x3fffffffu) + r;
 #ifdef NNRT_KERNEL_STAMPS
 			px_lane += span;
 #endif
-			if (!(vi >> 31)) {
-				scatter_row<0>(g, q2.y, fu0, span, v, face0 + slot, o, staged, w.keys, bu0, bv0, tw, keys);
-			} else {
-				const float A = spa_cw(g.x[0], g.y[0], g.x[1], g.y[1], g.x[2], g.y[2]) + K_EPSILON;
-				const bool fast = !o.clip_barycentric && o.blur < 1e20f && fabsf(A) > 1e-30f && fabsf(A) < 1e30f &&
-				                  fmaxf(fmaxf(fabsf(g.z[0]), fabsf(g.z[1])), fabsf(g.z[2])) < 1e10f;
-				if (fast)
-					scatter_row<2>(g, q2.y, fu0, span, v, face0 + slot, o, staged, w.keys, bu0, bv0, tw, keys);
-				else
-					scatter_row<1>(g, q2.y, fu0, span, v, face0 + slot, o, staged, w.keys, bu0, bv0, tw, keys);
-			}
+			if (!(vi >> 31))
+				scatter_row<0>(g, q2.y, q3, fu0, span, v, face0 + slot, o, staged, w.keys, bu0, bv0, tw, keys);
+			else if ((vi >> 30) & 1u)
+				scatter_row<2>(g, q2.y, q3, fu0, span, v, face0 + slot, o, staged, w.keys, bu0, bv0, tw, keys);
+			else
+				scatter_row<1>(g, q2.y, q3, fu0, span, v, face0 + slot, o, staged, w.keys, bu0, bv0, tw, keys);
 		}
 		scatter_wave_sync();
 	}
@@ -364,12 +374,15 @@ __device__ inline void scatter_wave_pairs(const FaceNdc& fn, bool ok, int32_t fa
 	const float bw = odd ? other : side, bh = odd ? side : other;
 	const bool near_all = (bw * bw + bh * bh) < 0.5f * o.blur;
 	if (ok) {
+		const float4 k = face_row_constants(fn);   // both lanes (one instruction stream); the odd lane stores it
 		if (!odd) {
+			const bool fast = face_rows_fast(fn, k.x, o);
 			w.rec[slot][0] = make_float4(fn.x[0], fn.x[1], fn.x[2], fn.y[0]);
 			w.rec[slot][2] = make_float4(fn.z[2], face_inv_area(fn), __uint_as_float(static_cast<uint32_t>(u0) | static_cast<uint32_t>(u1 - u0 + 1) << 16),
-			                             __uint_as_float(static_cast<uint32_t>(v0) | (near_all ? 0x80000000u : 0u)));
+			                             __uint_as_float(static_cast<uint32_t>(v0) | (fast ? 0x40000000u : 0u) | (near_all ? 0x80000000u : 0u)));
 		} else {
 			w.rec[slot][1] = make_float4(fn.y[1], fn.y[2], fn.z[0], fn.z[1]);
+			w.rec[slot][3] = k;
 		}
 	}
 	scatter_rows(rows, slot, face0, o, keys, w, staged, bu0, bv0, tw, th);
