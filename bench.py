@@ -557,6 +557,10 @@ def main(argv=None):
                      "associations_E": E, "contributing_pixels": P_c,
                      "associations_note": "E and contributing pixels averaged over the timed iterations", "traffic_source": traffic_src,
                      "compulsory_bytes": node_pass_compulsory_bytes(P, P_c, F, V, Nn, 4),
+                     # the same launch against the bytes it really moves (PMC) and must move (compulsory): frac prices the
+                     # reference's stage-boundary tensors, which the fused launch never materialises
+                     "traffic_frac": (traffic / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                     "compulsory_frac": node_pass_compulsory_bytes(P, P_c, F, V, Nn, 4) / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "iteration_algorithmic_bytes": it_bytes,
                      "iteration_frac": it_bytes / (agg["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS},
         "kernels": kernels,
