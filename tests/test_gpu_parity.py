@@ -199,6 +199,33 @@ def test_rodrigues_and_block_cholesky_kats(nn, oracle_mod):
         nn.core.linalg.SolveBlockDiagonalCholesky(-L.CHOLESKY_A, L.CHOLESKY_B[:, 0])
 
 
+def test_arrowhead_long_back_substitution_chain(nn):
+    """A corner no separator splits (every corner node shares a stem node with every other: a 700-node clique, 4200
+    unknowns) is one nested-dissection group, i.e. one elimination-tree chain of 66 tile columns -- longer than the 64
+    column descriptors k_corner_back stages in LDS at a time, so the chain crosses a staging block. The solve is held to
+    the fp64 dense solution of the same system."""
+    rng = np.random.default_rng(11)
+    n0, n1 = 2, 700
+    N = n0 + n1
+    edges = np.array([(i, n0 + j) for i in range(n0) for j in range(n1)], np.int32)
+    wing = rng.normal(0, 0.3, (len(edges), 6, 6)).astype(np.float32)
+    diag = np.empty((N, 6, 6), np.float32)
+    for i in range(N):
+        A = rng.normal(size=(6, 6))
+        diag[i] = (A @ A.T + 6 * np.eye(6) * (1 + (n1 if i < n0 else n0))).astype(np.float32)
+    b = rng.normal(size=6 * N).astype(np.float32)
+    x_g = _np(nn.core.linalg.SolveBlockSparseArrowheadCholesky(diag, wing, edges, n0, b)).astype(np.float64)
+    Hd = np.zeros((6 * N, 6 * N))
+    for i in range(N):
+        Hd[6 * i:6 * i + 6, 6 * i:6 * i + 6] = diag[i]
+    for e, (i, j) in enumerate(edges):
+        Hd[6 * i:6 * i + 6, 6 * j:6 * j + 6] = wing[e]
+        Hd[6 * j:6 * j + 6, 6 * i:6 * i + 6] = wing[e].T
+    x64 = np.linalg.solve(Hd, b.astype(np.float64))
+    assert rel_err(x_g, x64) < 1e-4
+    assert np.abs(Hd @ x_g - b).max() < 1e-3 * np.abs(b).max()
+
+
 @pytest.mark.parametrize("n0,n1,degree", [(40, 6, 4), (300, 30, 4), (1, 1, 1), (2000, 200, 4)])
 def test_arrowhead_solver_vs_oracle(nn, oracle_mod, n0, n1, degree):
     rng = np.random.default_rng(n0)
