@@ -21,8 +21,9 @@ end-of-run all-gather of per-rank results. --replicas R: R inde
 its own fitter, warp field and stream on the one device (seeds rank * R + r); a step launches every replica's iteration
 on its stream; value = all sequences' iterations / the slowest rank's time.
 
-Also reported: the dominant kernel's roofline (k_fit_pixels_fused: both pixel passes in one launch, HIP-event timed on the fitter's work stream; every
-other kernel of the iteration under "kernels"), the once-per-frame setup time, and the CPU baseline (the oracle/ C++
+Also reported: the dominant kernel's roofline (k_fit_pixels_fused: both pixel passes in one launch, timed in its real
+context by nnrt_fitter_time_kernels -- graph-captured prefix sequences of iterations between HIP events on the fitter's
+stream, so the figure matches the rocprofv3 kernel trace; every other kernel of the iteration under "kernels"), the once-per-frame setup time, and the CPU baseline (the oracle/ C++
 restatement with the reference's binned rasterizer, OpenMP, on a bounded sample of the same workload, rank 0, N = 1: one
 socket's physical cores with OMP_PROC_BIND=close and this process's CPU share, the faster as the value; also 1 thread).
 """
@@ -124,9 +125,6 @@ KERNEL_STAGES = {
     "k_fit_pixels_fused": ("residual", "rasterized_jacobians", "pixel_anchor_jacobians", "jtj_jtr"),
     "k_solve_update": ("solve",),
 }
-# nnrt_fitter_iterate_timed stage -> the kernel it times
-# (the pixel-pass stage reads 0: both pixel passes run in the one launch the node-pass stage times)
-STAGE_KERNEL = {"warp": "k_warp_mesh_quad", "raster": "k_raster_scatter_mesh", "node_reduce": "k_fit_pixels_fused", "solve": "k_solve_update"}
 
 
 def arap_stage_bytes(N: int, n0: int, Ee: int) -> dict:
@@ -177,7 +175,9 @@ def parse_args(argv=None):
                          "--graph-steps-iteration frame fits from the identity warp (FitToImage's loop; raises potrf on C2, "
                          "as the reference does); identity: the first iteration of a frame per step")
     ap.add_argument("--replicas", type=int, default=1, help="independent sequences per GPU, one stream each (C4's per-rank work)")
-    ap.add_argument("--timed-steps", type=int, default=100, help="eager per-stage HIP-event timing steps (roofline)")
+    ap.add_argument("--timed-steps", type=int, default=10, help="eager per-stage HIP-event timing steps (association counts, stage_ms)")
+    ap.add_argument("--kernel-reps", type=int, default=20, help="iterations per graph of the per-kernel timing (nnrt_fitter_time_kernels)")
+    ap.add_argument("--kernel-trials", type=int, default=9, help="interleaved trials of the per-kernel timing (median)")
     ap.add_argument("--graph-steps", type=int, default=10, help="steps per captured graph launch (C2: 10 GN iterations per frame)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU-baseline sample (loop-body seconds)")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -327,6 +327,18 @@ def cpu_threads_default() -> int:
     return min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff
 
 
+def check_rank_devices(local_rank: int, world: int, backend: str, device_count: int) -> None:
+    """RCCL replicas need one GPU per local rank: fail fast, before any device is touched, instead of mapping two ranks
+    onto one device (the gloo rehearsal backend shares devices on purpose)."""
+    if backend == "gloo":
+        return
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    if local_rank >= device_count or local_world > device_count:
+        raise SystemExit(f"bench.py: {local_world} local rank(s) on the {backend} backend need one GPU each, but {device_count} "
+                         f"device(s) are visible (local rank {local_rank}); launch with --nproc-per-node <= {device_count} "
+                         f"(or NNRT_BENCH_BACKEND=gloo for a shared-device rehearsal)")
+
+
 def main(argv=None):
     args = parse_args(argv)
     rank, local_rank, world = dist_env()
@@ -339,6 +351,7 @@ def main(argv=None):
     # NNRT_BENCH_BACKEND=gloo (rehearsal only): several ranks sharing the GPUs of a smaller box (device = local rank
     # modulo the visible devices), their collectives on gloo over host tensors; the default is RCCL, one GPU per rank
     backend = os.environ.get("NNRT_BENCH_BACKEND", "nccl")
+    check_rank_devices(local_rank, world, backend, torch.cuda.device_count())
     local_dev = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
@@ -419,7 +432,7 @@ def main(argv=None):
 
     # warmup (graphs are captured on first use: use_hip_graph = 2): the requested W steps, and at least MIN_WARM_S of
     # back-to-back GPU work -- the GPU's clocks ramp up from idle: a 20-step timed region after 10 warmup steps measured
-    # 14,300 GN it/s at C2, after 200 warmup steps 15,500 (tools/dev/r3_warm.sh)
+    # 14,300 GN it/s at C2, after 200 warmup steps 15,500 (round-3 A/B r3_warm, in git history)
     for _ in range(max(1, args.warmup // per_launch)):
         if step(per_launch):
             NV.check(1)
@@ -450,9 +463,16 @@ def main(argv=None):
     agg = aggregate(args.steps * R, elapsed_max, world)
     agg["ms_per_step"] = 1000.0 * elapsed_max / args.steps   # one step = every replica's iteration
 
-    # per-stage device time (eager launches, HIP events on the fitter's work stream) over the same iterations as the
-    # timed steps (a frame's iterations for "frame", the restored iteration otherwise), one iteration at a time so that
-    # each iteration's algorithmic bytes use its own association count E
+    # per-kernel device time, each kernel in its real context: prefix sequences of graph-captured iterations from the
+    # snapshot state, replayed between HIP events on the fitter's stream (nnrt_fitter_time_kernels); these are the
+    # numbers the rocprofv3 kernel trace of the same command reports (profiles/r04_bench_kernel_stats.csv)
+    ft.restore_motion(wf)
+    ft.snapshot_motion(wf)   # "frame": the frame's start state; otherwise the restored mid-motion state
+    ktimes = ft.time_kernels(wf, reps=args.kernel_reps, trials=args.kernel_trials)
+    ft.restore_motion(wf)
+    # per-stage eager event timing over the same iterations as the timed steps (a frame's iterations for "frame", the
+    # restored iteration otherwise), one iteration at a time so that each iteration's algorithmic bytes use its own
+    # association count E (the stage times themselves carry launch / event overhead and are reported as stage_ms only)
     anchors, _ = ft.anchors(V, 4)
     stages = {k: 0.0 for k in A.TIMED_STAGES}
     samples = []   # (E, contributing pixels) per timed iteration
@@ -482,11 +502,11 @@ def main(argv=None):
     P_c = int(round(np.mean([p for _, p in samples])))
     sb = stage_bytes(P, F, V, Nn, 4, E)
     kernels = {}
-    for stage, kname in STAGE_KERNEL.items():
-        if arap and stage == "solve":
+    for kname in KERNEL_STAGES:
+        if arap and kname == "k_solve_update":
             continue
         kb = kernel_bytes(kname, sb)
-        ms = stages[stage]
+        ms = ktimes[kname if kname != "k_solve_update" else "solve"]
         kernels[kname] = dict(ms=round(ms, 5), algorithmic_bytes=kb, frac=kb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS if ms > 0 else None)
     corner = None
     if arap:
@@ -502,14 +522,14 @@ def main(argv=None):
         kernels["k_arap_edges"] = dict(ms=None, fused_into=ROOFLINE_KERNEL, algorithmic_bytes=ab["arap"], frac=None)
         fl = corner_flops(Nn - n0)
         corner = dict(kernel="arrowhead solve stage (stem Schur update + tile-sparse corner Cholesky + substitutions + update)",
-                      bound="mfma", achieved=fl / (stages["solve"] * 1e-3) / 1e12, peak=MFMA_F32_PEAK_TFS, unit="TFLOP/s",
-                      frac=fl / (stages["solve"] * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS, traffic=None, flops=fl, kernel_ms=stages["solve"],
+                      bound="mfma", achieved=fl / (ktimes["solve"] * 1e-3) / 1e12, peak=MFMA_F32_PEAK_TFS, unit="TFLOP/s",
+                      frac=fl / (ktimes["solve"] * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS, traffic=None, flops=fl, kernel_ms=ktimes["solve"],
                       n0=n0, n1=Nn - n0, corner_size=6 * (Nn - n0), edges=Ee,
                       flops_formula="SURVEY.md 8(d): (6 n1)^3 / 3 + 2 (6 n1)^2 (1 + n_rhs), n_rhs = 1 (the reference's dense corner; "
                                     "the tile-sparse factorization performs fewer: plan below)",
                       plan=ft.corner_info())
     kbytes = kernels[ROOFLINE_KERNEL]["algorithmic_bytes"]
-    k_ms = stages["node_reduce"]
+    k_ms = ktimes[ROOFLINE_KERNEL]
     achieved = kbytes / (k_ms * 1e-3) / 1e9
     it_bytes = sum(sb.values())
     traffic, traffic_src = load_traffic(args.traffic_file, workload)
@@ -533,7 +553,7 @@ def main(argv=None):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": agg["ms_per_step"],
-        "ms_per_solve": stages["solve"],
+        "ms_per_solve": ktimes["solve"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -546,9 +566,15 @@ def main(argv=None):
                                                                        f"{torch.cuda.device_count()} visible GPU(s))"}
                       if world > 1 else {})},
         "setup_ms": round(setup_ms, 3),
+        "kernel_ms": {k: round(v, 5) for k, v in ktimes.items()},
+        "kernel_ms_note": f"nnrt_fitter_time_kernels: per-iteration device time of each kernel in its real context, by differences "
+                          f"of graph-captured prefix sequences ({args.kernel_reps} iterations per graph, median of {args.kernel_trials} "
+                          f"interleaved trials); 'solve' = {'the arrowhead chain' if arap else 'k_solve_update'}; kernels.*.ms and "
+                          f"roofline.kernel_ms are these",
         "stage_ms": {k: round(v, 5) for k, v in stages.items()},
-        "stage_note": "eager launches between HIP events; pixel_jacobians is back-to-back event overhead only: both pixel "
-                      "passes run in the one launch node_reduce times (k_fit_pixels_fused)"
+        "stage_note": "single eager launches between HIP events (include launch / event overhead; not used for any fraction); "
+                      "pixel_jacobians is back-to-back event overhead only: both pixel passes run in the one launch node_reduce "
+                      "times (k_fit_pixels_fused)"
                       + ("; so is arap: the ARAP edge terms run in extra workgroups of that launch" if arap else ""),
         "roofline": {"kernel": ROOFLINE_KERNEL, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "algorithmic_bytes": kbytes, "kernel_ms": k_ms,

@@ -463,8 +463,11 @@ __global__ void k_faces_to_int4(const int64_t* __restrict__ faces, int64_t F, in
 // state_in (default: the warp field's state): where the warp and the update read the node motion the iteration starts
 // from; the update always writes the warp field's state (a restore-from-snapshot folded into the iteration reads the
 // snapshot directly instead of copying it first).
+// stages of one iteration (nnrt_fitter_time_kernels launches subsets of them)
+enum : unsigned { STAGE_WARP = 1u, STAGE_RASTER = 2u, STAGE_PIXEL = 4u, STAGE_SOLVE = 8u, STAGE_ALL = 15u };
+
 nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mode, hipStream_t s, hipEvent_t* marks = nullptr,
-                              bool from_identity = false, const float* state_in = nullptr) {
+                              bool from_identity = false, const float* state_in = nullptr, unsigned stages = STAGE_ALL) {
 	if (!state_in) state_in = wf->state.ptr;
 	nnrt_status st;
 	auto mark = [&](int i) -> nnrt_status {
@@ -473,12 +476,13 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 	};
 	if ((st = mark(0))) return st;
 	const bool with_jacobians = true;
-	if ((st = launch_warp_mesh(ft->mesh_p.ptr, ft->mesh_n.ptr, ft->V, state_in, ft->anchors.ptr, ft->weights.ptr, ft->K, ft->extr,
+	if ((stages & STAGE_WARP) &&
+	    (st = launch_warp_mesh(ft->mesh_p.ptr, ft->mesh_n.ptr, ft->V, state_in, ft->anchors.ptr, ft->weights.ptr, ft->K, ft->extr,
 	                           ft->wpos.ptr, ft->wnrm.ptr, with_jacobians ? ft->jrows.ptr : nullptr, s, from_identity)))
 		return st;
 	if ((st = mark(1))) return st;
 	const RasterOptions ro = make_raster_options(ft->H, ft->W, 0.5f / (static_cast<float>(fminf(ft->H, ft->W)) / 2.0f), ft->p.use_perspective_correction, 0, 1);
-	if ((st = launch_raster_scatter_mesh(ft->wpos.ptr, ft->faces4.ptr, ft->F, ft->ndc, 0.0f, 10.0f, ro, ft->keys.ptr, s))) return st;
+	if ((stages & STAGE_RASTER) && (st = launch_raster_scatter_mesh(ft->wpos.ptr, ft->faces4.ptr, ft->F, ft->ndc, 0.0f, 10.0f, ro, ft->keys.ptr, s))) return st;
 	if ((st = mark(2))) return st;
 	FitPixelArgs fa{};
 	fa.H = ft->H;
@@ -530,8 +534,9 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 		aa.error_flag = ft->error_flag.ptr;
 		fa.arap_blocks = fit_pixels_arap_blocks(ft->E);
 	}
-	if ((st = launch_fit_pixels(mode, fa, s, marks ? marks[3] : nullptr))) return st;
+	if ((stages & STAGE_PIXEL) && (st = launch_fit_pixels(mode, fa, s, marks ? marks[3] : nullptr))) return st;
 	if ((st = mark(4))) return st;
+	if (!(stages & STAGE_SOLVE)) return mark(6);
 	if (ft->E > 0) {
 		if ((st = mark(5))) return st;
 		const float lm = ft->p.preconditioning_dampening_factor;
@@ -664,6 +669,9 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	NNRT_CHECK_ARG(ref.depth_scale > 0.f, "depth_scale must be positive");
 	NNRT_CHECK_ARG(wf->device == ft->device, "the warp field and the fitter live on different devices");
 	DeviceGuard guard(ft->device);
+	// until this frame is fully prepared the fitter is not: a failure below (allocation, corner plan) leaves iterate()
+	// refusing rather than replaying graphs over buffers that may have been released
+	ft->prepared = false;
 	hipStream_t us = static_cast<hipStream_t>(stream);
 	const int64_t P = static_cast<int64_t>(H) * W;
 	const int N = wf->N, K = wf->anchor_count, E = wf->E();
@@ -701,7 +709,10 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 				const int64_t o = wf->h.virtual_indices.empty() ? n0 + a : wf->h.virtual_indices[static_cast<size_t>(n0 + a)];
 				for (int c = 0; c < 3; c++) cpos[3 * static_cast<size_t>(a) + c] = wf->nodes_original[3 * static_cast<size_t>(o) + c];
 			}
-			if ((st = ft->corner.prepare(wf->h.edges.data(), E, n0, N, cpos.data()))) return st;
+			if ((st = ft->corner.prepare(wf->h.edges.data(), E, n0, N, cpos.data()))) {
+				ft->drop_graphs();
+				return st;
+			}
 		}
 		if ((st = ft->wing.ensure(static_cast<size_t>(E) * 36)) || (st = ft->edge_residuals.ensure(3 * static_cast<size_t>(E))) ||
 		    (st = ft->a_diag.ensure(static_cast<size_t>(N) * 36)) || (st = ft->a_dinv.ensure(static_cast<size_t>(n0) * 36)) ||
@@ -1093,6 +1104,86 @@ nnrt_status nnrt_fitter_iterate_timed(nnrt_fitter* ft, nnrt_warp_field* wf, int3
 	for (auto& e : ev)
 		if (e) hipEventDestroy(e);
 	NNRT_HIP(hipEventRecord(ft->ev_out, ft->work));
+	NNRT_HIP(hipStreamWaitEvent(us, ft->ev_out, 0));
+	return st;
+}
+
+nnrt_status nnrt_fitter_time_kernels(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t reps, int32_t trials, float* h_kernel_ms, void* stream) {
+	NNRT_CHECK_ARG(ft && wf && h_kernel_ms && reps > 0 && trials > 0, "invalid arguments");
+	if (nnrt_status cst = check_frame(ft, wf, "nnrt_fitter_time_kernels")) return cst;
+	if (!ft->snapshot_valid) {
+		set_error("nnrt_fitter_snapshot_motion must be called after prepare() before nnrt_fitter_time_kernels");
+		return NNRT_ERROR_ARGUMENT;
+	}
+	DeviceGuard guard(ft->device);
+	hipStream_t us = static_cast<hipStream_t>(stream);
+	hipStream_t s = ft->work;
+	NNRT_HIP(hipEventRecord(ft->ev_in, us));
+	NNRT_HIP(hipStreamWaitEvent(s, ft->ev_in, 0));
+	// prefix sequences, each `reps` iterations from the snapshot state in one graph: every kernel runs after the launch
+	// it follows in a real iteration (the raster alone excepted, which repeats its own idempotent scatter)
+	const unsigned seq[4] = {STAGE_ALL, STAGE_RASTER | STAGE_PIXEL | STAGE_SOLVE, STAGE_RASTER | STAGE_PIXEL, STAGE_RASTER};
+	const int mode = ft->p.iteration_modes[0];
+	hipGraphExec_t exec[4] = {};
+	hipEvent_t ev[2] = {};
+	std::vector<float> per_rep[4];
+	nnrt_status st = NNRT_OK;
+	const size_t P = static_cast<size_t>(ft->H) * ft->W;
+	auto run = [&]() -> nnrt_status {
+		for (auto& e : ev) NNRT_HIP(hipEventCreate(&e));
+		for (int q = 0; q < 4; q++) {
+			hipGraph_t g = nullptr;
+			NNRT_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+			nnrt_status cs = NNRT_OK;
+			for (int i = 0; i < reps && !cs; i++) cs = enqueue_iteration(ft, wf, mode, s, nullptr, false, ft->snapshot.ptr, seq[q]);
+			hipError_t ce = hipStreamEndCapture(s, &g);
+			if (cs) {
+				if (g) hipGraphDestroy(g);
+				return cs;
+			}
+			NNRT_HIP(ce);
+			hipError_t ie = hipGraphInstantiate(&exec[q], g, nullptr, nullptr, 0);
+			hipGraphDestroy(g);
+			NNRT_HIP(ie);
+		}
+		// trials interleave the four sequences (clock drift cancels); consumers' state (raster keys, accumulators) is
+		// reset outside the timed region before every replay
+		for (int t = -1; t < trials; t++)
+			for (int q = 0; q < 4; q++) {
+				NNRT_HIP(hipMemsetAsync(ft->keys.ptr, 0xff, sizeof(uint64_t) * P, s));
+				NNRT_HIP(hipMemsetAsync(ft->acc.ptr, 0, sizeof(double) * static_cast<size_t>(ft->N) * ACC_STRIDE, s));
+				NNRT_HIP(hipEventRecord(ev[0], s));
+				NNRT_HIP(hipGraphLaunch(exec[q], s));
+				NNRT_HIP(hipEventRecord(ev[1], s));
+				NNRT_HIP(hipEventSynchronize(ev[1]));
+				float ms = 0.f;
+				NNRT_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
+				if (t >= 0) per_rep[q].push_back(ms / reps);   // trial -1 warms the graph
+			}
+		return NNRT_OK;
+	};
+	st = run();
+	for (auto& e : exec)
+		if (e) hipGraphExecDestroy(e);
+	for (auto& e : ev)
+		if (e) hipEventDestroy(e);
+	if (!st) {
+		float med[4];
+		for (int q = 0; q < 4; q++) {
+			std::vector<float> v = per_rep[q];
+			std::sort(v.begin(), v.end());
+			med[q] = v[v.size() / 2];
+		}
+		h_kernel_ms[0] = med[0] - med[1];   // warp
+		h_kernel_ms[1] = med[3];            // raster
+		h_kernel_ms[2] = med[2] - med[3];   // fused pixel launch
+		h_kernel_ms[3] = med[1] - med[2];   // solve + update (ARAP: the whole arrowhead chain)
+		h_kernel_ms[4] = med[0];            // whole iteration
+		// leave the fitter as an iteration would: raster keys empty, accumulators zero, motion = the snapshot's result
+		NNRT_HIP(hipMemsetAsync(ft->keys.ptr, 0xff, sizeof(uint64_t) * P, s));
+		NNRT_HIP(hipMemsetAsync(ft->acc.ptr, 0, sizeof(double) * static_cast<size_t>(ft->N) * ACC_STRIDE, s));
+	}
+	NNRT_HIP(hipEventRecord(ft->ev_out, s));
 	NNRT_HIP(hipStreamWaitEvent(us, ft->ev_out, 0));
 	return st;
 }
@@ -1654,11 +1745,18 @@ nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, cons
 			set_error("arrowhead solve: stream synchronisation failed");
 			return NNRT_ERROR_HIP;   // the plan is dropped (its device work state is unknown)
 		}
-		// the stream is drained: the plan's scratch is free for the next call with this structure
-		std::lock_guard<std::mutex> lock(g_arrow_mu);
-		auto& pool = arrow_pool();
-		pool.push_front(std::move(plan));
-		while (pool.size() > ARROW_POOL_MAX) pool.pop_back();
+		// the stream is drained: the plan's scratch is free for the next call with this structure; evicted plans are
+		// destroyed after the lock is released (hipFree synchronises the device and must not block other threads' lookups)
+		std::list<std::unique_ptr<ArrowheadPlan>> evicted;
+		{
+			std::lock_guard<std::mutex> lock(g_arrow_mu);
+			auto& pool = arrow_pool();
+			pool.push_front(std::move(plan));
+			while (pool.size() > ARROW_POOL_MAX) {
+				evicted.push_back(std::move(pool.back()));
+				pool.pop_back();
+			}
+		}
 	}
 	if (st) return st;
 	if (host_flag) {
@@ -1669,8 +1767,11 @@ nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, cons
 }
 
 void nnrt_release_arrowhead_plans(void) {
-	std::lock_guard<std::mutex> lock(g_arrow_mu);
-	arrow_pool().clear();
+	std::list<std::unique_ptr<ArrowheadPlan>> released;   // freed after the lock is dropped (hipFree synchronises)
+	{
+		std::lock_guard<std::mutex> lock(g_arrow_mu);
+		released.swap(arrow_pool());
+	}
 }
 
 // ---- DLPack entry points (include/nnrt_dlpack.h): validate, then forward to the pointer entry points ----------------

@@ -920,8 +920,30 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		std::memcpy(k.data() + at, corner_pos, sizeof(float) * nf);
 	}
 	if (k == key && (nc == 0 || tiles)) return NNRT_OK;   // same hierarchy: keep the plan and its buffers
+	// the old buffers go now: bump the generation first, so that whatever captured them (the fitter's graphs) is dropped
+	// even if the new plan fails below; a failure leaves the solver empty (released), never half-built
 	release();
+	generation++;
 	const CornerPlan p = plan_corner(edges, E, n0, N, corner_pos);
+	auto fail = [&](nnrt_status st) {
+		release();
+		return st;
+	};
+	auto alloc = [&](float*& ptr, size_t n) -> nnrt_status {
+		NNRT_HIP(hipMalloc(reinterpret_cast<void**>(&ptr), sizeof(float) * n));
+		return NNRT_OK;
+	};
+	if (p.nc > 0) {
+		nnrt_status st;
+		if ((st = alloc(tiles, p.slot_ij.size() * TILE_ELEMS)) || (st = alloc(ldiag, static_cast<size_t>(p.T) * TILE_ELEMS)) ||
+		    (st = alloc(cb, static_cast<size_t>(p.ld))) || (st = alloc(xp, static_cast<size_t>(p.ld))))
+			return fail(st);
+		if ((st = dev_upload(d_tile_slot, p.tile_slot)) || (st = dev_upload(d_slot_ij, p.slot_ij)) || (st = dev_upload(d_row_node, p.row_node)) ||
+		    (st = dev_upload(d_node_row, p.node_row)) || (st = dev_upload(d_tasks, p.tasks)) || (st = dev_upload(d_srcs, p.srcs)) ||
+		    (st = dev_upload(d_back_cols, p.back_cols)) || (st = dev_upload(d_back_ent, p.back_ent)) || (st = dev_upload(d_back_chains, p.back_chains)) ||
+		    (st = dev_upload(d_corner_edges, p.corner_edges)))
+			return fail(st);
+	}
 	nc = p.nc;
 	if (nc > 0) {
 		ld = p.ld;
@@ -929,16 +951,6 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		H = p.H;
 		slots = static_cast<int>(p.slot_ij.size());
 		n_corner_edges = static_cast<int>(p.corner_edges.size());
-		NNRT_HIP(hipMalloc(reinterpret_cast<void**>(&tiles), sizeof(float) * static_cast<size_t>(slots) * TILE_ELEMS));
-		NNRT_HIP(hipMalloc(reinterpret_cast<void**>(&ldiag), sizeof(float) * static_cast<size_t>(T) * TILE_ELEMS));
-		NNRT_HIP(hipMalloc(reinterpret_cast<void**>(&cb), sizeof(float) * static_cast<size_t>(ld)));
-		NNRT_HIP(hipMalloc(reinterpret_cast<void**>(&xp), sizeof(float) * static_cast<size_t>(ld)));
-		nnrt_status st;
-		if ((st = dev_upload(d_tile_slot, p.tile_slot)) || (st = dev_upload(d_slot_ij, p.slot_ij)) || (st = dev_upload(d_row_node, p.row_node)) ||
-		    (st = dev_upload(d_node_row, p.node_row)) || (st = dev_upload(d_tasks, p.tasks)) || (st = dev_upload(d_srcs, p.srcs)) ||
-		    (st = dev_upload(d_back_cols, p.back_cols)) || (st = dev_upload(d_back_ent, p.back_ent)) || (st = dev_upload(d_back_chains, p.back_chains)) ||
-		    (st = dev_upload(d_corner_edges, p.corner_edges)))
-			return st;
 		level_off = p.level_off;
 		level_panel = p.level_panel;
 		back_off = p.back_off;
@@ -946,7 +958,6 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		dense_tiles = static_cast<int64_t>(corner_ld(6 * nc) / TILE) * (corner_ld(6 * nc) / TILE + 1) / 2;
 	}
 	key.swap(k);
-	generation++;
 	return NNRT_OK;
 }
 

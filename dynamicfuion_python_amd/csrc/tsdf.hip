@@ -848,10 +848,12 @@ McTables build_mc_tables() {
 			if (((cfg >> edge_v[e][0]) & 1) != ((cfg >> edge_v[e][1]) & 1)) mask |= static_cast<uint16_t>(1u << e);
 		t.edge_mask[cfg] = mask;
 		int nt = 0;
-		for (int i = 0; i < 16 && MC_TRI_TABLE[cfg][i] >= 0; i += 3, nt++) {   // (a, b, c) -> (a, c, b), as Open3D emits
-			t.tri[cfg][3 * nt] = MC_TRI_TABLE[cfg][i];
-			t.tri[cfg][3 * nt + 1] = MC_TRI_TABLE[cfg][i + 2];
-			t.tri[cfg][3 * nt + 2] = MC_TRI_TABLE[cfg][i + 1];
+		// (a, b, c) -> (c, b, a): Open3D's ExtractTriangleMesh stores table vertex v at triangle slot 2 - v (third-party,
+		// absent here: restated from its published source; same winding as (a, c, b), parity unpinned)
+		for (int i = 0; i < 16 && MC_TRI_TABLE[cfg][i] >= 0; i += 3, nt++) {
+			t.tri[cfg][3 * nt] = MC_TRI_TABLE[cfg][i + 2];
+			t.tri[cfg][3 * nt + 1] = MC_TRI_TABLE[cfg][i + 1];
+			t.tri[cfg][3 * nt + 2] = MC_TRI_TABLE[cfg][i];
 		}
 		t.tri[cfg][3 * nt] = -1;
 		t.ntri[cfg] = static_cast<int8_t>(nt);

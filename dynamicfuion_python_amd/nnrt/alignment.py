@@ -14,6 +14,8 @@ from .geometry import HierarchicalGraphWarpField, TriangleMesh
 
 # nnrt_fitter_iterate_timed stage order (include/nnrt_mi355x.h, NNRT_TIMED_STAGES)
 TIMED_STAGES = ("warp", "raster", "pixel_jacobians", "node_reduce", "arap", "solve")
+# nnrt_fitter_time_kernels order (include/nnrt_mi355x.h, NNRT_KERNEL_TIMES)
+KERNEL_TIMES = ("k_warp_mesh_quad", "k_raster_scatter_mesh", "k_fit_pixels_fused", "solve", "iteration")
 
 
 class IterationMode(enum.IntEnum):
@@ -141,6 +143,13 @@ class DeformableMeshToImageFitter:
         ms = np.zeros(len(TIMED_STAGES), np.float32)
         N.check(N.lib().nnrt_fitter_iterate_timed(self._h, warp_field.handle, int(first_iteration), int(count), N.ptr(ms), N.stream_ptr(stream)))
         return {name: float(v) for name, v in zip(TIMED_STAGES, ms)}
+
+    def time_kernels(self, warp_field: HierarchicalGraphWarpField, reps: int = 20, trials: int = 5, stream=None) -> dict:
+        """Per-kernel device ms of one iteration from the snapshot state, each kernel in its real context (prefix
+        sequences of `reps` graph-captured iterations, median of `trials`; include/nnrt_mi355x.h)."""
+        ms = np.zeros(len(KERNEL_TIMES), np.float32)
+        N.check(N.lib().nnrt_fitter_time_kernels(self._h, warp_field.handle, int(reps), int(trials), N.ptr(ms), N.stream_ptr(stream)))
+        return {name: float(v) for name, v in zip(KERNEL_TIMES, ms)}
 
     def check(self, stream=None):
         N.check(N.lib().nnrt_fitter_check(self._h, N.stream_ptr(stream)))

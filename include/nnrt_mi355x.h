@@ -168,6 +168,17 @@ nnrt_status nnrt_fitter_restore_motion(nnrt_fitter* fitter, nnrt_warp_field* war
 #define NNRT_TIMED_STAGES 6
 nnrt_status nnrt_fitter_iterate_timed(nnrt_fitter* fitter, nnrt_warp_field* warp_field, int32_t first_iteration, int32_t count,
                                       float* h_stage_ms, void* stream);
+/* Per-kernel device time of one GN iteration in its real context (measurement; loop body
+ * DeformableMeshToImageFitter.cpp:111-275). Four prefix sequences of `reps` iterations from the snapshot state are each
+ * captured as one graph -- [warp, raster, pixel, solve], [raster, pixel, solve], [raster, pixel], [raster] -- and
+ * replayed `trials` times, interleaved, between HIP events on the fitter's stream; the median per-iteration times give
+ * h_kernel_ms[NNRT_KERNEL_TIMES] = 0 warp (k_warp_mesh_quad), 1 raster (k_raster_scatter_mesh), 2 fused pixel launch
+ * (k_fit_pixels_fused), 3 solve + update (k_solve_update; ARAP: the whole arrowhead chain), 4 whole iteration, by
+ * differences. Leaves raster keys empty, the accumulators zero and the node motion at the snapshot's one-iteration
+ * result. Requires nnrt_fitter_snapshot_motion after the last prepare(). Synchronizes `stream`. */
+#define NNRT_KERNEL_TIMES 5
+nnrt_status nnrt_fitter_time_kernels(nnrt_fitter* fitter, nnrt_warp_field* warp_field, int32_t reps, int32_t trials, float* h_kernel_ms,
+                                     void* stream);
 /* Reports (and clears) a failure recorded on the device by earlier iterate() calls (e.g. a non-positive-definite block,
  * which the reference raises from potrf). Synchronizes `stream`. */
 nnrt_status nnrt_fitter_check(nnrt_fitter* fitter, void* stream);
@@ -428,7 +439,7 @@ nnrt_status nnrt_voxel_grid_extract_triangle_mesh(nnrt_voxel_grid* grid, float w
 nnrt_status nnrt_voxel_grid_copy_mesh(const nnrt_voxel_grid* grid, float* d_vertices, float* d_normals, float* d_colors,
                                       int64_t* d_triangles, void* stream);
 /* the marching-cubes tables (host): tri [256][31] int8 edge triples in emission order (-1 terminated; the published
- * Lorensen-Cline / Bourke table Open3D indexes, each triangle (a, b, c) emitted as (a, c, b)), edge mask [256] */
+ * Lorensen-Cline / Bourke table Open3D indexes, each triangle (a, b, c) emitted as (c, b, a), Open3D's slot 2 - v), edge mask [256] */
 nnrt_status nnrt_marching_cubes_table(int8_t* h_tri, uint16_t* h_edge_mask);
 
 #ifdef __cplusplus

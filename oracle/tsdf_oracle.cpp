@@ -218,7 +218,8 @@ void blend(const Field& f, const int* idx, const float* w, const float* p, float
 }
 
 // ---- marching-cubes table: the published Lorensen-Cline / Bourke table Open3D indexes (oracle copy: mc_table_oracle.hpp);
-// each triangle (a, b, c) is emitted as (a, c, b), as Open3D emits it (faces away from negative tsdf) ----
+// each triangle (a, b, c) is emitted as (c, b, a): Open3D stores table vertex v at slot 2 - v (faces away from negative
+// tsdf; the slot order is restated from Open3D's published source, third-party and absent: parity unpinned) ----
 struct McTable {
 	uint16_t mask[256];
 	std::vector<int> tri[256];
@@ -234,7 +235,7 @@ const McTable& mc_table() {
 			if (((cfg >> ev[e][0]) & 1) != ((cfg >> ev[e][1]) & 1)) mask |= static_cast<uint16_t>(1 << e);
 		T.mask[cfg] = mask;
 		for (int i = 0; i < 16 && ORC_MC_TRI_TABLE[cfg][i] >= 0; i += 3)
-			T.tri[cfg].insert(T.tri[cfg].end(), {ORC_MC_TRI_TABLE[cfg][i], ORC_MC_TRI_TABLE[cfg][i + 2], ORC_MC_TRI_TABLE[cfg][i + 1]});
+			T.tri[cfg].insert(T.tri[cfg].end(), {ORC_MC_TRI_TABLE[cfg][i + 2], ORC_MC_TRI_TABLE[cfg][i + 1], ORC_MC_TRI_TABLE[cfg][i]});
 	}
 	built = true;
 	return T;

@@ -127,7 +127,9 @@ def test_algorithmic_bytes_c2():
     # every stage of the block-diagonal iteration except the ARAP rows is covered by exactly one kernel
     covered = [st for k in bench.KERNEL_STAGES.values() for st in k]
     assert sorted(covered) == sorted(sb)
-    assert set(bench.STAGE_KERNEL.values()) == set(bench.KERNEL_STAGES)
+    # every kernel the bytes are charged to has a per-kernel time (nnrt_fitter_time_kernels order)
+    from dynamicfuion_python_amd.nnrt.alignment import KERNEL_TIMES
+    assert set(bench.KERNEL_STAGES) - {"k_solve_update"} <= set(KERNEL_TIMES) and "solve" in KERNEL_TIMES
 
 
 def test_association_count():
@@ -138,3 +140,29 @@ def test_association_count():
     mask = np.array([1, 1, 1, 0])
     # pixel 0: face 0 -> {0,1,2,3,4,5} = 6 ; pixel 1: face 1 -> {0,1,2,4,5,6,7,8} = 8 ; pixel 2: no face ; pixel 3: masked
     assert bench.count_associations(pixel_faces, mask, faces, anchors) == 14
+
+
+def test_more_ranks_than_devices_fails_fast(monkeypatch):
+    """bench.main under the default (RCCL) backend with more local ranks than visible GPUs stops with a clear message
+    before touching a device or the process group (no silent device mis-mapping)."""
+    import torch
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+
+    def no_device(*a, **k):
+        raise AssertionError("a device was selected before the rank/device check")
+
+    monkeypatch.setattr(torch.cuda, "set_device", no_device)
+    monkeypatch.delenv("NNRT_BENCH_BACKEND", raising=False)
+    monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
+    for rank in (0, 1):
+        monkeypatch.setenv("RANK", str(rank))
+        monkeypatch.setenv("LOCAL_RANK", str(rank))
+        monkeypatch.setenv("WORLD_SIZE", "2")
+        with pytest.raises(SystemExit, match="need one GPU each, but 1 device"):
+            bench.main(["--gpus", "2", "--steps", "1", "--warmup", "0"])
+    # the gloo rehearsal shares devices on purpose; one rank per device passes
+    bench.check_rank_devices(1, 2, "gloo", 1)
+    bench.check_rank_devices(0, 1, "nccl", 1)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    bench.check_rank_devices(3, 16, "nccl", 8)   # two nodes of 8: local ranks 0..7 on 8 devices

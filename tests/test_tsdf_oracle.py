@@ -132,6 +132,8 @@ def test_marching_cubes_table_is_the_published_one(oracle_mod):
     for cfg in range(256):   # the product's rows end at their first -1
         end = int(np.argmax(tri_p[cfg] < 0))
         assert np.array_equal(tri_p[cfg, :end], tri_o[cfg, :end]) and (tri_o[cfg, end:] == -1).all(), cfg
+    # Bourke's row 1 is (0, 8, 3); Open3D stores table vertex v at triangle slot 2 - v, so it emits (3, 8, 0)
+    assert list(tri_o[1, :4]) == [3, 8, 0, -1] and list(tri_p[1, :4]) == [3, 8, 0, -1]
     ntri = [(tri_o[c] >= 0).sum() // 3 for c in range(256)]
     assert max(ntri) == 5 and ntri[0] == ntri[255] == 0
     for cfg in range(256):

@@ -1,3 +1,4 @@
+// Build (not committed as a binary): hipcc --offload-arch=gfx950 -O3 tools/dev/rcp_check.hip -o tools/dev/rcp_check
 // Exhaustive check (development): rcp_rn_fast(b) == RN(1/b) = (float)(1.0 / (double)b) for every float bit pattern.
 // rcp_rn_fast: hardware double reciprocal estimate + one Newton step in double, rounded to float.
 #include <hip/hip_runtime.h>
