@@ -377,7 +377,8 @@ struct nnrt_fitter {
 	DeviceBuffer<float> weights;
 	DeviceBuffer<uint32_t> face_nodes;   // [F, face_node_slots(K)] distinct anchor nodes per face (once per frame)
 	DeviceBuffer<float4> wpos, wnrm;
-	DeviceBuffer<float2> jrows;        // [V,K,3] warped-Jacobian rows (store_jacobian_row)
+	DeviceBuffer<float2> jrows;        // [V,K,3] warped-Jacobian rows (store_jacobian_row; NNRT_GATHER_ROWS builds only)
+	DeviceBuffer<float4> mesh_p4, mesh_n4;   // [V] canonical positions / normals as float4 (pass 2 forms the Jacobian rows)
 	DeviceBuffer<float4> ref_points;   // [P] reference point (x, y, z, valid)
 	DeviceBuffer<float4> records;      // [P, 4] pixel Jacobian records
 	DeviceBuffer<uint64_t> keys;
@@ -440,6 +441,14 @@ __global__ void k_prepare_reference_points(const float* __restrict__ points, con
 	out[i] = valid ? make_float4(points[3 * i], points[3 * i + 1], points[3 * i + 2], 1.f) : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// canonical vertices / normals [V,3] -> float4 [V] (w = 0): pass 2 forms the warped-surface Jacobian rows from them
+__global__ void k_to_float4(const float* __restrict__ p, const float* __restrict__ n, int64_t V, float4* __restrict__ p4, float4* __restrict__ n4) {
+	const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (i >= V) return;
+	p4[i] = make_float4(p[3 * i], p[3 * i + 1], p[3 * i + 2], 0.f);
+	n4[i] = make_float4(n[3 * i], n[3 * i + 1], n[3 * i + 2], 0.f);
+}
+
 // faces -> int4; an index outside [0, V) becomes the degenerate face (0, 0, 0) (never rasterized, never gathered out of
 // bounds) and sets error bit 4, which nnrt_fitter_check reports
 // flip_winding: the consistent NDC convention keeps rows in image order, which negates every face's NDC area relative to
@@ -475,7 +484,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 		return NNRT_OK;
 	};
 	if ((st = mark(0))) return st;
-	const bool with_jacobians = true;
+	const bool with_jacobians = NNRT_GATHER_ROWS != 0;
 	if ((stages & STAGE_WARP) &&
 	    (st = launch_warp_mesh(ft->mesh_p.ptr, ft->mesh_n.ptr, ft->V, state_in, ft->anchors.ptr, ft->weights.ptr, ft->K, ft->extr,
 	                           ft->wpos.ptr, ft->wnrm.ptr, with_jacobians ? ft->jrows.ptr : nullptr, s, from_identity)))
@@ -507,6 +516,10 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 	fa.anchors = ft->anchors.ptr;
 	fa.face_nodes = ft->face_nodes.ptr;
 	fa.jrows = ft->jrows.ptr;
+	fa.state_in = reinterpret_cast<const float4*>(state_in);
+	fa.state_identity = from_identity;
+	fa.cmesh_p = ft->mesh_p4.ptr;
+	fa.cmesh_n = ft->mesh_n4.ptr;
 	fa.weights = ft->weights.ptr;
 	fa.ref_points = ft->ref_points.ptr;
 	fa.records = ft->records.ptr;
@@ -631,6 +644,8 @@ void nnrt_fitter_destroy(nnrt_fitter* ft) {
 	ft->wpos.release();
 	ft->wnrm.release();
 	ft->jrows.release();
+	ft->mesh_p4.release();
+	ft->mesh_n4.release();
 	ft->keys.release();
 	ft->residual_mask.release();
 	ft->pixel_face.release();
@@ -686,12 +701,14 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	}
 	// (re)allocate; any reallocation invalidates captured graphs
 	const auto before = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->corner.generation,
-	                                    ft->face_nodes.ptr, ft->wpos.ptr);
+	                                    ft->face_nodes.ptr, ft->wpos.ptr, ft->mesh_p4.ptr);
 	nnrt_status st;
 	if ((st = ft->mesh_p.ensure(3 * V)) || (st = ft->mesh_n.ensure(3 * V)) || (st = ft->faces4.ensure(F)) ||
 	    (st = ft->anchors.ensure(static_cast<size_t>(V) * K)) || (st = ft->weights.ensure(static_cast<size_t>(V) * K)) ||
 	    (st = ft->face_nodes.ensure(static_cast<size_t>(F) * face_node_slots(K))) ||
-	    (st = ft->wpos.ensure(V)) || (st = ft->wnrm.ensure(V)) || (st = ft->jrows.ensure(3 * static_cast<size_t>(V) * K)) ||
+	    (st = ft->wpos.ensure(V)) || (st = ft->wnrm.ensure(V)) ||
+	    (st = ft->jrows.ensure(NNRT_GATHER_ROWS ? 3 * static_cast<size_t>(V) * K : 1)) || (st = ft->mesh_p4.ensure(V)) ||
+	    (st = ft->mesh_n4.ensure(V)) ||
 	    (st = ft->ref_points.ensure(P)) || (st = ft->records.ensure(4 * P)) || (st = ft->keys.ensure(P)) ||
 	    (st = ft->residuals.ensure(P)) || (st = ft->residual_mask.ensure(P)) || (st = ft->pixel_face.ensure(P)) ||
 	    (st = ft->acc.ensure(static_cast<size_t>(N) * ACC_STRIDE)) ||
@@ -776,7 +793,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 		ft->aw.edge_list = ft->a_list.ptr;
 	}
 	const auto after = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->corner.generation,
-	                                   ft->face_nodes.ptr, ft->wpos.ptr);
+	                                   ft->face_nodes.ptr, ft->wpos.ptr, ft->mesh_p4.ptr);
 	// Captured graphs bake every buffer pointer and the per-frame constants (NDC setup, pixel camera, extrinsics) into
 	// their kernel arguments: any change drops them. The warp field is recognised by its unique id, not its address.
 	const NdcSetup nndc = make_ndc_setup(h_K, H, W, ft->p.ndc_convention == NNRT_NDC_CONSISTENT);
@@ -806,6 +823,8 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	NNRT_HIP(hipMemcpyAsync(ft->mesh_n.ptr, d_normals, sizeof(float) * 3 * V, hipMemcpyDeviceToDevice, s));
 	k_faces_to_int4<<<static_cast<unsigned>(ceil_div(F, 256)), 256, 0, s>>>(d_faces, F, V, ft->p.ndc_convention == NNRT_NDC_CONSISTENT,
 	                                                                        ft->faces4.ptr, ft->error_flag.ptr);
+	NNRT_LAUNCH_CHECK();
+	k_to_float4<<<static_cast<unsigned>(ceil_div(V, 256)), 256, 0, s>>>(d_vertices, d_normals, V, ft->mesh_p4.ptr, ft->mesh_n4.ptr);
 	NNRT_LAUNCH_CHECK();
 	// once per frame (:96-106): anchors & weights on the canonical mesh in virtual node order
 	if ((st = launch_compute_anchors(ft->mesh_p.ptr, V, wf->node_positions.ptr, N, K, wf->coverage,

@@ -232,9 +232,10 @@ struct CornerPlan {
 	std::vector<int> level_off, level_panel;   // [H + 1] task offsets per factor launch, [H] panel tasks first
 	std::vector<CornerTask> tasks;
 	std::vector<int4> srcs;           // (slot X, slot Y, column k, 0): X Y^T update terms; rhs term L_k y_k uses X and k
+	std::vector<int> inv_off, inv_cols;   // [H + 1] per factor launch l: the columns of level l - 1 whose diagonal factor it inverts
 	std::vector<int> back_off;        // [launches + 1] back-substitution chains per launch
 	std::vector<int2> back_chains;    // (first column entry, column count): a chain of the elimination tree, root end first
-	std::vector<int4> back_cols;      // (J, entry offset, entry count, 0)
+	std::vector<int4> back_cols;      // (J, entry offset, entry count, 1 if L_JJ^-1 is formed: every column below the top level)
 	std::vector<int2> back_ent;       // (slot of L_IJ, I)
 	std::vector<int> corner_edges;    // edges between two corner nodes (>= 3 layers)
 };
@@ -388,6 +389,15 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 		}
 		p.level_off.push_back(static_cast<int>(p.tasks.size()));
 	}
+	// diagonal inverses L_JJ^-1 (back substitution as a product): launch l >= 1 inverts the columns of level l - 1, whose
+	// L_JJ the previous launch finished; the top level's columns keep the substitution
+	p.inv_off.push_back(0);
+	for (int l = 0; l < p.H; l++) {
+		if (l > 0)
+			for (int J = 0; J < T; J++)
+				if (lvl[static_cast<size_t>(J)] == l - 1) p.inv_cols.push_back(J);
+		p.inv_off.push_back(static_cast<int>(p.inv_cols.size()));
+	}
 	// back substitution over chains of the elimination tree: a chain starts at a root or at a child of a node with two or
 	// more children and follows single children down; one workgroup walks a chain from its root end, so a launch holds
 	// every chain at the same number of branchings below the root (x of every column above a chain's top is known
@@ -419,7 +429,7 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 			p.back_chains.push_back(make_int2(static_cast<int>(p.back_cols.size()), static_cast<int>(chain_cols[c].size())));
 			for (int J : chain_cols[c]) {
 				const auto& cc = cs[static_cast<size_t>(J)];
-				p.back_cols.push_back(make_int4(J, static_cast<int>(p.back_ent.size()), static_cast<int>(cc.size()), 0));
+				p.back_cols.push_back(make_int4(J, static_cast<int>(p.back_ent.size()), static_cast<int>(cc.size()), lvl[static_cast<size_t>(J)] < p.H - 1));
 				for (int I : cc) p.back_ent.push_back(make_int2(slot(I, J), I));
 			}
 		}
@@ -628,7 +638,38 @@ struct CornerFactorArgs {
 	int n_panel;
 	int* error_flag;
 	int level;
+	int n_tasks;             // workgroups [n_tasks, gridDim) invert diagonal factors of the previous level
+	const int* inv_cols;     // this launch's columns to invert
+	float* minv;             // [T, 64, 64] L_JJ^-1 (lower; zero above the diagonal)
 };
+
+// M = L^-1 for the 64 x 64 lower-triangular factor L (row-major, zero above the diagonal): the workgroup stages L in LDS,
+// wave 0 forms column c of M in lane c by forward substitution in double (rows in order, four partial sums per row), and
+// stores it rounded to float. The back substitution then forms x_J = L_JJ^-T z as the product M^T z.
+__device__ inline void invert_lower_tile(const float* __restrict__ L, float* __restrict__ M, float* s_l, int t) {
+	const float4* L4 = reinterpret_cast<const float4*>(L);
+	for (int i = t; i < TILE_ELEMS / 4; i += CT) *reinterpret_cast<float4*>(s_l + (i >> 4) * CS4 + 4 * (i & 15)) = L4[i];
+	__syncthreads();
+	if (t >= 64) return;
+	const int c = t;
+	double m[TILE];
+#pragma unroll
+	for (int r = 0; r < TILE; r++) {
+		double a[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+		for (int k4 = 0; k4 < r; k4 += 4) {
+			const float4 l = *reinterpret_cast<const float4*>(s_l + r * CS4 + k4);   // wave-uniform: LDS broadcast
+			a[0] = __builtin_fma(static_cast<double>(l.x), m[k4], a[0]);
+			if (k4 + 1 < r) a[1] = __builtin_fma(static_cast<double>(l.y), m[k4 + 1], a[1]);
+			if (k4 + 2 < r) a[2] = __builtin_fma(static_cast<double>(l.z), m[k4 + 2], a[2]);
+			if (k4 + 3 < r) a[3] = __builtin_fma(static_cast<double>(l.w), m[k4 + 3], a[3]);
+		}
+		const double d = static_cast<double>(s_l[r * CS4 + r]);
+		m[r] = ((c == r ? 1.0 : 0.0) - ((a[0] + a[1]) + (a[2] + a[3]))) / d;
+	}
+#pragma unroll
+	for (int r = 0; r < TILE; r++) M[r * TILE + c] = static_cast<float>(m[r]);
+}
 
 // One launch per level of the tile elimination tree.
 //   panel (I, J) (blockIdx < n_panel): s_d = A_JJ - sum_k L_Jk L_Jk^T and s_p = A_IJ - sum_k L_Ik L_Jk^T over the columns k of
@@ -643,6 +684,11 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 	__shared__ float s_b[TILE];         // b_J after the previous level's updates (diagonal workgroup)
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
 	CORNER_STAMP(0);
+	if (static_cast<int>(blockIdx.x) >= a.n_tasks) {   // diagonal inverse of a column finished by an earlier launch
+		const int J = a.inv_cols[blockIdx.x - a.n_tasks];
+		invert_lower_tile(a.ldiag + static_cast<int64_t>(J) * TILE_ELEMS, a.minv + static_cast<int64_t>(J) * TILE_ELEMS, s_d, t);
+		return;
+	}
 	const CornerTask tk = a.tasks[blockIdx.x];
 	const int4* src = a.srcs + tk.src;
 	if (static_cast<int>(blockIdx.x) >= a.n_panel) {
@@ -760,6 +806,7 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 struct CornerBackArgs {
 	const float* tiles;
 	const float* ldiag;
+	const float* minv;       // L_JJ^-1 of the columns whose descriptor says so (w = 1)
 	const float* cb;         // y
 	float* xp;               // [ld] x in the permuted order
 	const int* row_node;
@@ -782,6 +829,7 @@ constexpr int BACK_BATCH = 6;   // entry tiles per batch of loads (6 x (4 + 4) =
 constexpr int BACK_COLS = 64;   // chain columns whose descriptors are staged in LDS at a time
 __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 	__shared__ __attribute__((aligned(16))) float s_part[4][TILE];
+	__shared__ __attribute__((aligned(16))) float s_z[TILE];
 	__shared__ int4 s_cols[BACK_COLS];
 	__shared__ int2 s_ent[2][64];   // first 64 entry descriptors of the current (q & 1) and the next column
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
@@ -798,14 +846,15 @@ __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 		for (int q = 0; q < nq; q++) {
 			const int4 col = s_cols[q];
 			const int J = col.x;
-			const float* Ld = a.ldiag + static_cast<int64_t>(J) * TILE_ELEMS;
-			float colv[TILE];   // colv[r] = L_JJ[r][lane] (wave 0; issued before the sums so the loads overlap them)
+			const bool inv = col.w != 0;   // x_J = M^T z with M = L_JJ^-1, else the column-oriented substitution
+			const float* Ld = (inv ? a.minv : a.ldiag) + static_cast<int64_t>(J) * TILE_ELEMS;
+			float colv[TILE];   // colv[r] = L_JJ[r][lane] or M[r][lane] (wave 0; issued before the sums so the loads overlap them)
 			float yv = 0.f, dv = 1.f;
 			if (wave == 0) {
 	#pragma unroll
 				for (int r = 0; r < TILE; r++) colv[r] = Ld[r * TILE + lane];
 				yv = a.cb[static_cast<int64_t>(J) * TILE + lane];
-				dv = Ld[lane * TILE + lane];
+				if (!inv) dv = Ld[lane * TILE + lane];
 			}
 			const bool has_next = q + 1 < nq;
 			int2 nxt = make_int2(0, 0);
@@ -856,14 +905,30 @@ __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 			if (lane < 16) *reinterpret_cast<float4*>(&s_part[wave][4 * lane]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
 			__syncthreads();
 			if (wave == 0) {
-				const float inv_d = 1.f / dv;
 				float z = yv - ((s_part[0][lane] + s_part[1][lane]) + (s_part[2][lane] + s_part[3][lane]));
 				float x = 0.f;
+				if (inv) {
+					// x_c = sum_r M_rc z_r: z through this wave's LDS row (in-order within the wave), four partial sums
+					s_z[lane] = z;
+					__builtin_amdgcn_wave_barrier();
+					float xs[4] = {0.f, 0.f, 0.f, 0.f};
 	#pragma unroll
-				for (int r = TILE - 1; r >= 0; r--) {
-					const float xr = lane_bcast(z, r) * lane_bcast(inv_d, r);   // x_r = z_r / L_rr
-					x = lane == r ? xr : x;
-					z -= colv[r] * xr;   // z_c -= L_rc x_r (only c < r matter)
+					for (int r4 = 0; r4 < TILE; r4 += 4) {
+						const float4 zz = *reinterpret_cast<const float4*>(&s_z[r4]);
+						xs[0] = __builtin_fmaf(colv[r4], zz.x, xs[0]);
+						xs[1] = __builtin_fmaf(colv[r4 + 1], zz.y, xs[1]);
+						xs[2] = __builtin_fmaf(colv[r4 + 2], zz.z, xs[2]);
+						xs[3] = __builtin_fmaf(colv[r4 + 3], zz.w, xs[3]);
+					}
+					x = (xs[0] + xs[1]) + (xs[2] + xs[3]);
+				} else {
+					const float inv_d = 1.f / dv;
+	#pragma unroll
+					for (int r = TILE - 1; r >= 0; r--) {
+						const float xr = lane_bcast(z, r) * lane_bcast(inv_d, r);   // x_r = z_r / L_rr
+						x = lane == r ? xr : x;
+						z -= colv[r] * xr;   // z_c -= L_rc x_r (only c < r matter)
+					}
 				}
 				const int64_t row = static_cast<int64_t>(J) * TILE + lane;
 				a.xp[row] = x;
@@ -896,7 +961,8 @@ static void dev_free(void*& p) {
 CornerSolver::~CornerSolver() { release(); }
 
 void CornerSolver::release() {
-	for (void** p : {reinterpret_cast<void**>(&tiles), reinterpret_cast<void**>(&ldiag), reinterpret_cast<void**>(&cb),
+	for (void** p : {reinterpret_cast<void**>(&tiles), reinterpret_cast<void**>(&ldiag), reinterpret_cast<void**>(&minv), reinterpret_cast<void**>(&d_inv_cols),
+	                 reinterpret_cast<void**>(&cb),
 	                 reinterpret_cast<void**>(&xp), reinterpret_cast<void**>(&d_tile_slot), reinterpret_cast<void**>(&d_slot_ij),
 	                 reinterpret_cast<void**>(&d_row_node), reinterpret_cast<void**>(&d_node_row), reinterpret_cast<void**>(&d_tasks),
 	                 reinterpret_cast<void**>(&d_srcs), reinterpret_cast<void**>(&d_back_cols), reinterpret_cast<void**>(&d_back_ent), reinterpret_cast<void**>(&d_back_chains),
@@ -905,6 +971,7 @@ void CornerSolver::release() {
 	nc = ld = T = H = slots = n_corner_edges = 0;
 	level_off.clear();
 	level_panel.clear();
+	inv_off.clear();
 	back_off.clear();
 	key.clear();
 }
@@ -936,12 +1003,13 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 	if (p.nc > 0) {
 		nnrt_status st;
 		if ((st = alloc(tiles, p.slot_ij.size() * TILE_ELEMS)) || (st = alloc(ldiag, static_cast<size_t>(p.T) * TILE_ELEMS)) ||
+		    (st = alloc(minv, static_cast<size_t>(p.T) * TILE_ELEMS)) ||
 		    (st = alloc(cb, static_cast<size_t>(p.ld))) || (st = alloc(xp, static_cast<size_t>(p.ld))))
 			return fail(st);
 		if ((st = dev_upload(d_tile_slot, p.tile_slot)) || (st = dev_upload(d_slot_ij, p.slot_ij)) || (st = dev_upload(d_row_node, p.row_node)) ||
 		    (st = dev_upload(d_node_row, p.node_row)) || (st = dev_upload(d_tasks, p.tasks)) || (st = dev_upload(d_srcs, p.srcs)) ||
 		    (st = dev_upload(d_back_cols, p.back_cols)) || (st = dev_upload(d_back_ent, p.back_ent)) || (st = dev_upload(d_back_chains, p.back_chains)) ||
-		    (st = dev_upload(d_corner_edges, p.corner_edges)))
+		    (st = dev_upload(d_corner_edges, p.corner_edges)) || (st = dev_upload(d_inv_cols, p.inv_cols)))
 			return fail(st);
 	}
 	nc = p.nc;
@@ -953,6 +1021,7 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		n_corner_edges = static_cast<int>(p.corner_edges.size());
 		level_off = p.level_off;
 		level_panel = p.level_panel;
+		inv_off = p.inv_off;
 		back_off = p.back_off;
 		fill_tiles = static_cast<int64_t>(slots);
 		dense_tiles = static_cast<int64_t>(corner_ld(6 * nc) / TILE) * (corner_ld(6 * nc) / TILE + 1) / 2;
@@ -982,16 +1051,19 @@ nnrt_status CornerSolver::launch_offdiag(int n0, const int32_t* edges, const flo
 
 nnrt_status CornerSolver::launch_solve(float* xout, int* error_flag, hipStream_t s) const {
 	if (nc == 0) return NNRT_OK;
-	CornerFactorArgs fa{tiles, ldiag, cb, nullptr, d_srcs, 0, error_flag, 0};
+	CornerFactorArgs fa{tiles, ldiag, cb, nullptr, d_srcs, 0, error_flag, 0, 0, nullptr, minv};
 	for (int l = 0; l < H; l++) {
 		fa.level = l;
 		const int n = level_off[static_cast<size_t>(l) + 1] - level_off[static_cast<size_t>(l)];
+		const int ni = inv_off[static_cast<size_t>(l) + 1] - inv_off[static_cast<size_t>(l)];
 		fa.tasks = d_tasks + level_off[static_cast<size_t>(l)];
 		fa.n_panel = level_panel[static_cast<size_t>(l)];
-		k_corner_factor<<<n, CT, 0, s>>>(fa);
+		fa.n_tasks = n;
+		fa.inv_cols = d_inv_cols + inv_off[static_cast<size_t>(l)];
+		k_corner_factor<<<n + ni, CT, 0, s>>>(fa);
 		NNRT_LAUNCH_CHECK();
 	}
-	CornerBackArgs ba{tiles, ldiag, cb, xp, d_row_node, xout, nullptr, d_back_cols, d_back_ent};
+	CornerBackArgs ba{tiles, ldiag, minv, cb, xp, d_row_node, xout, nullptr, d_back_cols, d_back_ent};
 	for (size_t l = 0; l + 1 < back_off.size(); l++) {
 		const int n = back_off[l + 1] - back_off[l];
 		ba.chains = d_back_chains + back_off[l];

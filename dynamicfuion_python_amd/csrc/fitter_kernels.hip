@@ -381,6 +381,7 @@ constexpr int NG_CAP = 64;     // associations per chunk (one lane each in (2));
 // in (3) fall in distinct LDS banks). Words: (1) pixel lane, face-table entry; (2a) the node at word 7;
 // (2) J[0..S-1], r at word S (zeros past the count, whose node word repeats the chunk's last node).
 constexpr int NG_STRIDE = 65;
+
 constexpr int NG_ROWS = 8;     // pixel rows per wave (8 x NG_ROWS pixels)
 static_assert(2 * NG_ROWS == PIX_TILE, "pass 2 walks the pass-1 tiles");
 
@@ -505,6 +506,10 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 	int4 d = make_int4(0, -1, -1, -1);
 	float4 jv[3], jn[3];
 	float4 rq[4];
+#if !NNRT_GATHER_ROWS
+	float4 ns4[4];   // the association's node state (g, t, R), and per face vertex its canonical position / normal
+	float4 cp4[3], cn4[3];
+#endif
 	auto gather = [&](float* slots, int count) {
 		d = make_int4(0, -1, -1, -1);
 		int pl = 0;
@@ -518,6 +523,11 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 		int vrow[3];
 #pragma unroll
 		for (int fv = 0; fv < 3; fv++) vrow[fv] = __shfl(vid_ka[fv], pl);
+#if !NNRT_GATHER_ROWS
+		int vtx[3];
+#pragma unroll
+		for (int fv = 0; fv < 3; fv++) vtx[fv] = __shfl(vid[fv], pl);
+#endif
 		if (lane < count) {
 			int r3[3];
 #pragma unroll
@@ -531,6 +541,7 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 		const int rows[3] = {d.y, d.z, d.w};
 		// unconditional loads (row -1 reads row 0, ignored in (2b)): a branch per load would make the compiler wait for
 		// each gather before issuing the next, serialising the chunk's six row fetches
+#if NNRT_GATHER_ROWS
 #pragma unroll
 		for (int fv = 0; fv < 3; fv++) {
 			const int r = rows[fv] >= 0 ? rows[fv] : 0;
@@ -545,6 +556,32 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 				jn[fv] = make_float4(0.f, 0.f, 0.f, 0.f);
 			}
 		}
+#else
+		// the weight of every face vertex (translation terms) and, for the rotation terms, the node state and the
+		// canonical vertex / normal: the rows are formed in (2b) exactly as the warp forms them (warp_slot)
+		{
+			const int node = lane < count ? static_cast<int>(code >> FACE_NODE_SHIFT) : 0;
+#pragma unroll
+			for (int fv = 0; fv < 3; fv++) {
+				const int r = rows[fv] >= 0 ? rows[fv] : 0;
+				jv[fv].w = a.weights[r];
+			}
+			if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) {
+				const float4* ns = a.state_in + 4 * static_cast<int64_t>(node);
+				ns4[0] = ns[0];
+				if (!a.state_identity) {
+					ns4[1] = ns[1];
+					ns4[2] = ns[2];
+					ns4[3] = ns[3];
+				}
+#pragma unroll
+				for (int fv = 0; fv < 3; fv++) {
+					cp4[fv] = a.cmesh_p[vtx[fv]];
+					cn4[fv] = a.cmesh_n[vtx[fv]];
+				}
+			}
+		}
+#endif
 		{
 			const int64_t pp = static_cast<int64_t>(min(pv0 + (d.x >> 3), a.H - 1)) * a.W + min(pu0 + (d.x & 7), a.W - 1);
 #pragma unroll
@@ -569,6 +606,29 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 			const float rn[3] = {q[9], q[10], q[11]};
 			const float rho[3] = {q[12], q[13], q[14]};
 			float jr[3] = {0.f, 0.f, 0.f}, jt[3] = {0.f, 0.f, 0.f};
+#if !NNRT_GATHER_ROWS
+			if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) {
+				// (-w R (v - g), -w R n) per face vertex: warp_slot's expressions (kernels.hpp), bit-identical to its rows
+				const f3 g = make3(ns4[0].x, ns4[0].y, ns4[0].z);
+				float R[9];
+				if (a.state_identity) {
+#pragma unroll
+					for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.f : 0.f;
+				} else {
+					const float Rl[9] = {ns4[1].z, ns4[1].w, ns4[2].x, ns4[2].y, ns4[2].z, ns4[2].w, ns4[3].x, ns4[3].y, ns4[3].z};
+#pragma unroll
+					for (int i = 0; i < 9; i++) R[i] = Rl[i];
+				}
+#pragma unroll
+				for (int fv = 0; fv < 3; fv++) {
+					const float w = jv[fv].w;
+					const f3 Rj = matvec3(R, sub3(make3(cp4[fv].x, cp4[fv].y, cp4[fv].z), g));
+					const f3 Rnj = matvec3(R, make3(cn4[fv].x, cn4[fv].y, cn4[fv].z));
+					jv[fv] = make_float4(-w * Rj.x, -w * Rj.y, -w * Rj.z, w);
+					jn[fv] = make_float4(-w * Rnj.x, -w * Rnj.y, -w * Rnj.z, 0.f);
+				}
+			}
+#endif
 			// branch-free over the face vertices: a vertex not anchored to the node adds an exact +0 (selected, so the
 			// row it loaded in its place -- row 0 -- never reaches the sums, NaN or not)
 #pragma unroll

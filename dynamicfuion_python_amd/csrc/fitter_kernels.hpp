@@ -111,6 +111,12 @@ __device__ inline void arap_edge(const ArapArgs& a, int e) {
 	src[31] = 0.f;
 }
 
+// warped-surface Jacobian rows (-w R (v - g), -w R n): 0 = formed per association in pass 2 from the node state and the
+// canonical vertex (the warp stores positions and normals only); 1 = materialised by the warp kernel and gathered
+#ifndef NNRT_GATHER_ROWS
+#define NNRT_GATHER_ROWS 0
+#endif
+
 struct FitPixelArgs {
 	int H, W, tiles_x, tiles_y;   // tiles of 16 x 16 pixels; this launch covers tile rows [tile_row0, tile_row0 + tiles_y)
 	int tile_row0;
@@ -129,7 +135,11 @@ struct FitPixelArgs {
 	const float4* wnrm;     // [V] warped normals
 	const int32_t* anchors; // [V,K]
 	const uint32_t* face_nodes; // [F, face_node_slots(K)] per face: its unique anchor nodes, ascending (face_node_entry)
-	const float2* jrows;    // [V,K,3] (-w R (v-g), -w R n) as 24 B (store_jacobian_row)
+	const float2* jrows;    // [V,K,3] (-w R (v-g), -w R n) as 24 B (store_jacobian_row; NNRT_GATHER_ROWS builds only)
+	const float4* state_in; // [N,4] node motion the iteration started from (g, t, R: the warp's input)
+	int state_identity;     // the iteration starts from R = I, t = 0 (the state is not read, as in the warp)
+	const float4* cmesh_p;  // [V] canonical vertex positions (x, y, z, 0)
+	const float4* cmesh_n;  // [V] canonical vertex normals
 	const float* weights;   // [V,K] anchor weights w
 	const float4* ref_points; // [P] reference point (x, y, z, valid)
 	float* residuals;       // [P]
@@ -264,12 +274,12 @@ private:
 	std::vector<int32_t> key;
 	int nc = 0, ld = 0, T = 0, H = 0, slots = 0, n_corner_edges = 0;
 	int64_t fill_tiles = 0, dense_tiles = 0;
-	float *tiles = nullptr, *ldiag = nullptr, *cb = nullptr, *xp = nullptr;
-	int *d_tile_slot = nullptr, *d_row_node = nullptr, *d_node_row = nullptr, *d_corner_edges = nullptr;
+	float *tiles = nullptr, *ldiag = nullptr, *minv = nullptr, *cb = nullptr, *xp = nullptr;
+	int *d_tile_slot = nullptr, *d_row_node = nullptr, *d_node_row = nullptr, *d_corner_edges = nullptr, *d_inv_cols = nullptr;
 	int2 *d_slot_ij = nullptr, *d_back_ent = nullptr, *d_back_chains = nullptr;
 	CornerTask* d_tasks = nullptr;
 	int4 *d_srcs = nullptr, *d_back_cols = nullptr;
-	std::vector<int> level_off, level_panel, back_off;
+	std::vector<int> level_off, level_panel, inv_off, back_off;
 };
 
 struct ArrowheadWorkspace {

@@ -47,8 +47,10 @@ int main(int argc, char** argv) {
 	for (size_t s = 0; s < p.slot_ij.size(); s++) { int I = p.slot_ij[s].x, J = p.slot_ij[s].y; for (int r = 0; r < TILE; r++) for (int c = 0; c < TILE; c++) tiles[s*TE + r*TILE + c] = ent(I*TILE+r, J*TILE+c); }
 	for (int R = 0; R < p.ld; R++) { int rn = p.row_node[R]; cb[R] = rn >= 0 ? bnat[6*(rn>>3)+(rn&7)] : 0.0; }
 	auto tile = [&](int s) { return &tiles[(size_t)s * TE]; };
+	std::vector<double> minv((size_t)T * TE, 0.0);
+	std::vector<int> ldiag_launch(T, -1), inv_launch(T, -1);
 	for (int l = 0; l < p.H; l++) {
-		std::set<std::pair<int,int>> reads, writes;   // (kind, id): 0 tile slot, 1 ldiag J, 2 cb J
+		std::set<std::pair<int,int>> reads, writes;   // (kind, id): 0 tile slot, 1 ldiag J, 2 cb J, 3 minv J
 		std::vector<std::set<std::pair<int,int>>> tr, tw;
 		for (int q = p.level_off[l]; q < p.level_off[l+1]; q++) {
 			const CornerTask& tk = p.tasks[q];
@@ -69,7 +71,7 @@ int main(int argc, char** argv) {
 					auto y = rhsu(tk.J, src, tk.nd); r.insert({2,tk.J});
 					for (int i=0;i<TILE;i++){ double v=y[i]; for(int k=0;k<i;k++) v -= d[i*TILE+k]*y[k]; y[i] = v/d[i*TILE+i]; }
 					for (int i=0;i<TILE;i++) cb[tk.J*TILE+i] = y[i]; w.insert({2,tk.J});
-					std::copy(d.begin(), d.end(), &ldiag[(size_t)tk.J*TE]); w.insert({1,tk.J});
+					std::copy(d.begin(), d.end(), &ldiag[(size_t)tk.J*TE]); w.insert({1,tk.J}); ldiag_launch[tk.J] = l;
 				} else {
 					upd(pp.data(), tile(tk.slot_t), src + tk.nd, tk.np); r.insert({0,tk.slot_t});
 					// L_IJ = pp L_JJ^-T : solve X L^T = pp row by row
@@ -77,6 +79,17 @@ int main(int argc, char** argv) {
 					std::copy(pp.begin(), pp.end(), tile(tk.slot_t)); w.insert({0,tk.slot_t});
 				}
 			}
+			tr.push_back(r); tw.push_back(w);
+		}
+		// diagonal inverses of the previous level's columns (extra workgroups of the same launch): read ldiag J, write minv J
+		for (int q = p.inv_off[l]; q < p.inv_off[l+1]; q++) {
+			const int J = p.inv_cols[q];
+			std::set<std::pair<int,int>> r, w;
+			r.insert({1,J}); w.insert({3,J});
+			if (inv_launch[J] >= 0 || ldiag_launch[J] < 0 || ldiag_launch[J] >= l) { printf("INVERSE order violation: column %d at launch %d\n", J, l); return 1; }
+			const double* Ld = &ldiag[(size_t)J*TE]; double* Mi = &minv[(size_t)J*TE];
+			for (int c = 0; c < TILE; c++) for (int rr = 0; rr < TILE; rr++) { double v = rr == c ? 1.0 : 0.0; for (int k = 0; k < rr; k++) v -= Ld[rr*TILE+k]*Mi[k*TILE+c]; Mi[rr*TILE+c] = v / Ld[rr*TILE+rr]; }
+			inv_launch[J] = l;
 			tr.push_back(r); tw.push_back(w);
 		}
 		for (size_t a = 0; a < tw.size(); a++) for (size_t b = 0; b < tw.size(); b++) if (a != b) for (auto& x : tw[a]) if (tr[b].count(x) || tw[b].count(x)) { printf("RACE level %d task %zu writes (%d,%d) touched by task %zu\n", l, a, x.first, x.second, b); return 1; }
@@ -95,7 +108,13 @@ int main(int argc, char** argv) {
 					if (!ok) { printf("BACK ORDER violation: column %d needs x_%d\n", J, en.y); return 1; }
 					const double* L = tile(en.x); for (int r=0;r<TILE;r++) for (int cc=0;cc<TILE;cc++) z[cc] -= L[r*TILE+cc]*xp[en.y*TILE+r]; }
 				const double* Ld = &ldiag[(size_t)J*TE];
-				for (int i=TILE-1;i>=0;i--){ double v = z[i]; for (int k2=i+1;k2<TILE;k2++) v -= Ld[k2*TILE+i]*xp[J*TILE+k2]; xp[J*TILE+i] = v/Ld[i*TILE+i]; }
+				if (c.w) {   // x_J = M^T z with the inverse formed in the factor launches
+					if (inv_launch[J] < 0) { printf("BACK uses an inverse never formed: column %d\n", J); return 1; }
+					const double* Mi = &minv[(size_t)J*TE];
+					for (int i=0;i<TILE;i++){ double v = 0; for (int r2=0;r2<TILE;r2++) v += Mi[r2*TILE+i]*z[r2]; xp[J*TILE+i] = v; }
+				} else {
+					for (int i=TILE-1;i>=0;i--){ double v = z[i]; for (int k2=i+1;k2<TILE;k2++) v -= Ld[k2*TILE+i]*xp[J*TILE+k2]; xp[J*TILE+i] = v/Ld[i*TILE+i]; }
+				}
 				for (int i=0;i<TILE;i++){ int rn = p.row_node[J*TILE+i]; if (rn>=0) xout[6*(rn>>3)+(rn&7)] = xp[J*TILE+i]; }
 				mine.insert(J);
 			}

@@ -1,0 +1,44 @@
+// Host-only statistics of the Schur-corner plan (csrc/corner.hip plan_corner) for a structure file written by
+// tools/dev/corner_plan_stats.py: per factor launch the panel / trailing tasks and update terms, per back-substitution
+// launch the chains, their columns and entry tiles. Build: hipcc -O2 -std=c++17 --offload-arch=gfx950 -I include
+// -I dynamicfuion_python_amd/csrc -x hip tools/dev/corner_plan_stats.hip -o /tmp/corner_plan_stats
+#include "corner.hip"
+#include <cstdio>
+namespace nnrt { void set_error(const std::string& m) { fprintf(stderr, "%s\n", m.c_str()); } }
+using namespace nnrt;
+int main(int argc, char** argv) {
+	FILE* f = fopen(argv[1], "rb");
+	int E, n0, N;
+	fread(&E, 4, 1, f); fread(&n0, 4, 1, f); fread(&N, 4, 1, f);
+	std::vector<int32_t> edges(2 * E);
+	fread(edges.data(), 4, 2 * E, f);
+	std::vector<float> pos(3 * (N - n0));
+	const bool has_pos = fread(pos.data(), 4, pos.size(), f) == pos.size() && !pos.empty();
+	fclose(f);
+	CornerPlan p = plan_corner(edges.data(), E, n0, N, has_pos ? pos.data() : nullptr);
+	printf("nc %d ld %d T %d H %d slots %zu tasks %zu srcs %zu\n", p.nc, p.ld, p.T, p.H, p.slot_ij.size(), p.tasks.size(), p.srcs.size());
+	for (int l = 0; l < p.H; l++) {
+		int np = p.level_panel[l], nt = p.level_off[l + 1] - p.level_off[l] - np, cols = 0, maxsrc = 0, sumsrc = 0;
+		for (int q = p.level_off[l]; q < p.level_off[l + 1]; q++) {
+			const CornerTask& t = p.tasks[q];
+			if (q - p.level_off[l] < np && t.I == t.J) cols++;
+			maxsrc = std::max(maxsrc, t.nd + t.np);
+			sumsrc += t.nd + t.np;
+		}
+		printf("level %2d: columns %3d panel tasks %3d trailing %4d  update terms max %3d total %5d\n", l, cols, np, nt, maxsrc, sumsrc);
+	}
+	for (size_t l = 0; l + 1 < p.back_off.size(); l++) {
+		int maxlen = 0, maxent = 0, sument = 0, totcols = 0;
+		for (int c = p.back_off[l]; c < p.back_off[l + 1]; c++) {
+			const int2 ch = p.back_chains[c];
+			maxlen = std::max(maxlen, ch.y);
+			totcols += ch.y;
+			int ent = 0;
+			for (int q = 0; q < ch.y; q++) { ent += p.back_cols[ch.x + q].z; maxent = std::max(maxent, p.back_cols[ch.x + q].z); }
+			sument += ent;
+		}
+		printf("back %zu: chains %3d columns %3d longest chain %3d entries/col max %3d total %4d\n", l, p.back_off[l + 1] - p.back_off[l], totcols, maxlen, maxent, sument);
+	}
+	// the longest root-to-leaf path: columns and entries along it
+	return 0;
+}
