@@ -183,6 +183,8 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="OpenMP threads for the CPU baseline (0: this process's CPU share, see cpu_threads_default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-share-only", action="store_true", help="CPU baseline at this process's CPU share only (large configs: C3)")
+    ap.add_argument("--cpu-no-warm", action="store_true", help="CPU baseline without the untimed first call (large configs: C3)")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r03_pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch of the roofline kernel (tools/pmc_traffic.py output)")
     return ap.parse_args(argv)
@@ -236,7 +238,7 @@ def host_cpu():
 
 
 def cpu_baseline(sc, depth_host, share_threads: int, budget_s: float, step: str, iterations: int, R0=None, t0=None,
-                 single_thread_s: float = 4.0):
+                 single_thread_s: float = 4.0, share_only: bool = False, warm: bool = True):
     """The oracle (C++/OpenMP restatement of the reference CPU path; test infrastructure, used here only as the
     reported baseline) running the same steps as the GPU: `step` = "frame" -> `iterations`-iteration FitToImage loops from
     the identity warp; "snapshot" -> one GN iteration from the node state (R0, t0); "identity" -> one GN iteration from
@@ -244,7 +246,8 @@ def cpu_baseline(sc, depth_host, share_threads: int, budget_s: float, step: str,
     excluded, as in the GPU step; the rasterizer is the reference's binned one (GridBinNdcTriangles + per-pixel bin loop,
     RasterizeNdcTrianglesImpl.h:187-391), not the oracle's fast K = 1 path. Threads: the physical
     cores of one socket with OMP_PROC_BIND=close and this process's CPU share (16 on the GPU box) -- the faster of the two is
-    the value, both are listed under "samples" -- and 1."""
+    the value, both are listed under "samples" -- and 1. share_only (large configs, e.g. C3, whose binned raster takes
+    minutes per iteration on one thread): the process's CPU share only; warm = False: no untimed first call."""
     os.environ.setdefault("OMP_PROC_BIND", "close")   # read when the oracle's OpenMP runtime initialises (first load)
     os.environ.setdefault("OMP_PLACES", "cores")
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -263,17 +266,24 @@ def cpu_baseline(sc, depth_host, share_threads: int, budget_s: float, step: str,
 
     threading.Thread(target=heartbeat, daemon=True).start()
     try:
-        runs = [_cpu_sample(O, sc, refp, refm, socket, budget_s, step, iterations, R0, t0)]
-        if share_threads != socket:
-            runs.append(_cpu_sample(O, sc, refp, refm, share_threads, budget_s, step, iterations, R0, t0))
-        one = _cpu_sample(O, sc, refp, refm, 1, single_thread_s, step, iterations, R0, t0, min_timed=1)
+        _cpu_sample.warmed = not warm
+        _cpu_sample.no_warm_call = not warm
+        if share_only:
+            runs = [_cpu_sample(O, sc, refp, refm, share_threads, budget_s, step, iterations, R0, t0)]
+            one = None
+        else:
+            runs = [_cpu_sample(O, sc, refp, refm, socket, budget_s, step, iterations, R0, t0)]
+            if share_threads != socket:
+                runs.append(_cpu_sample(O, sc, refp, refm, share_threads, budget_s, step, iterations, R0, t0))
+            one = _cpu_sample(O, sc, refp, refm, 1, single_thread_s, step, iterations, R0, t0, min_timed=1)
     finally:
         done.set()
     # value: the faster multi-thread sample (the binned raster does not scale to a whole socket on a shared host)
     best = max(runs, key=lambda r: r["value"] or 0.0)
     res = dict(best)
     res["samples"] = [dict(value=r["value"], cores=r["cores"], ms_per_solve=r["ms_per_solve"], sample=r["sample"]) for r in runs]
-    res["single_thread"] = dict(value=one["value"], unit=one["unit"], cores=1, ms_per_solve=one["ms_per_solve"], sample=one["sample"])
+    res["single_thread"] = (dict(value=one["value"], unit=one["unit"], cores=1, ms_per_solve=one["ms_per_solve"], sample=one["sample"])
+                            if one else None)
     res["host"] = host
     res["omp_proc_bind"] = os.environ.get("OMP_PROC_BIND")
     return res
@@ -297,7 +307,7 @@ def _cpu_sample(O, sc, refp, refm, threads: int, budget_s: float, step: str, ite
         hk = dict(edges=h["edges"], edge_layers=h["edge_layers"], radii=h["radii"], first_layer_count=int(h["layer_counts"][0]))
     body = solve = 0.0
     iters = calls = timed = 0
-    warm = threads == 1 and getattr(_cpu_sample, "warmed", False)
+    warm = getattr(_cpu_sample, "warmed", False) and (threads == 1 or getattr(_cpu_sample, "no_warm_call", False))
     wall0 = time.perf_counter()
     while (body < budget_s and time.perf_counter() - wall0 < 3 * budget_s) or timed < min_timed:
         _, _, dg = O.fit(nodes=nodes, rotations=R0, translations=t0, mesh_points=sc.points, mesh_normals=sc.normals, faces=sc.faces,
@@ -602,7 +612,8 @@ def main(argv=None):
         threads = args.cpu_threads or cpu_threads_default()
         log(f"GPU: {agg['value']:.1f} it/s; running the CPU baseline samples (~{args.cpu_seconds:.0f} s each: one socket's physical "
             f"cores, {threads} threads, 1 thread)")
-        out["cpu_baseline"] = cpu_baseline(sc, depth.cpu().numpy(), threads, args.cpu_seconds, args.step, per_launch, R1, t1)
+        out["cpu_baseline"] = cpu_baseline(sc, depth.cpu().numpy(), threads, args.cpu_seconds, args.step, per_launch, R1, t1,
+                                           share_only=args.cpu_share_only, warm=not args.cpu_no_warm)
         out["cpu_baseline"]["host"]["sched_affinity"] = len(os.sched_getaffinity(0))
         out["cpu_baseline"]["host"]["omp_num_threads_env"] = os.environ.get("OMP_NUM_THREADS")
     if rank == 0:

@@ -360,16 +360,25 @@ __device__ __forceinline__ void arrow_update_node(int n, const float (&xl)[6], c
 }
 
 // threads [0, n0): stem back substitution (and, with node_state, that node's update from the x it just formed);
-// threads [n0, n_update): the corner nodes' updates from the corner solve's x (node_state non-null only)
+// threads [n0, n_update): the corner nodes' updates from the corner solve's x (node_state non-null only).
+// x_base (refinement pass): x holds the correction d (rhs = the residual); the solution is x_base + d, written to x_base
+// and applied (x_base is read and written by its own thread only; x is read across threads and only written by stem
+// threads at their own rows, which no thread of the launch reads).
 __global__ void k_arrow_back(int n0, int n_update, const float* __restrict__ dinv, const int* __restrict__ edge_offsets, const int* __restrict__ edge_list,
                              const int32_t* __restrict__ edges, const float* __restrict__ wing, const float* __restrict__ rhs,
-                             float* __restrict__ x, const float* state_in, float* node_state, float* __restrict__ updates_out) {
+                             float* __restrict__ x, const float* state_in, float* node_state, float* __restrict__ updates_out,
+                             float* __restrict__ x_base) {
 	const int i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n0) {
-		if (node_state && i < n_update) {
+		if (i < n_update && (node_state || x_base)) {
 			float xl[6];
 			for (int c = 0; c < 6; c++) xl[c] = x[6 * static_cast<int64_t>(i) + c];
-			arrow_update_node(i, xl, state_in, node_state, updates_out);
+			if (x_base)
+				for (int c = 0; c < 6; c++) {
+					xl[c] = x_base[6 * static_cast<int64_t>(i) + c] + xl[c];
+					x_base[6 * static_cast<int64_t>(i) + c] = xl[c];
+				}
+			if (node_state) arrow_update_node(i, xl, state_in, node_state, updates_out);
 		}
 		return;
 	}
@@ -420,7 +429,88 @@ __global__ void k_arrow_back(int n0, int n_update, const float* __restrict__ din
 	float2* xo = reinterpret_cast<float2*>(x + 6 * static_cast<int64_t>(i));
 #pragma unroll
 	for (int q = 0; q < 3; q++) xo[q] = make_float2(o[2 * q], o[2 * q + 1]);
+	if (x_base)
+#pragma unroll
+		for (int c = 0; c < 6; c++) {
+			o[c] = x_base[6 * static_cast<int64_t>(i) + c] + o[c];
+			x_base[6 * static_cast<int64_t>(i) + c] = o[c];
+		}
 	if (node_state) arrow_update_node(i, o, state_in, node_state, updates_out);
+}
+
+// ---- iterative refinement: res = rhs - H x with the sums in double (H = the prepared diagonal blocks, with LM, and the
+// wing blocks at (i, j) and, transposed, at (j, i)); 32 lanes per node: lane q < 30 takes row q % 6 of every fifth of the
+// node's incidences (CSR, ascending edge order), the five partials of a row are then added in slot order ----
+__global__ __launch_bounds__(256) void k_arrow_residual(int N, const float* __restrict__ diag, const int* __restrict__ inc_off,
+                                                        const int* __restrict__ inc_list, const int32_t* __restrict__ edges,
+                                                        const float* __restrict__ wing, const float* __restrict__ rhs, const float* __restrict__ x,
+                                                        float* __restrict__ res) {
+	const int n = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 5);
+	const int q = static_cast<int>(threadIdx.x & 31);
+	if (n >= N) return;   // uniform per 32-lane node group
+	const int c = q % 6, slot = q / 6;   // slot 5: lanes 30, 31 idle in the loop
+	double s = 0.0;
+	if (slot < 5) {
+		for (int u = inc_off[n] + slot; u < inc_off[n + 1]; u += 5) {
+			const int code = inc_list[u];
+			const int e = code >> 1;
+			const bool tgt = code & 1;   // node is the edge's target: row c of B^T, i.e. column c of B, times x_source
+			const int other = edges[2 * e + (tgt ? 0 : 1)];
+			const float* B = wing + static_cast<int64_t>(e) * 36;
+			const float* xo = x + 6 * static_cast<int64_t>(other);
+#pragma unroll
+			for (int k = 0; k < 6; k++) s += static_cast<double>(tgt ? B[6 * k + c] : B[6 * c + k]) * static_cast<double>(xo[k]);
+		}
+	}
+	// partials of row c sit in lanes c, c + 6, c + 12, c + 18, c + 24 (width-32 groups)
+	double t = s;
+#pragma unroll
+	for (int k = 1; k < 5; k++) t += __shfl(s, c + 6 * k, 32);
+	if (q < 6) {
+		const float* D = diag + static_cast<int64_t>(n) * 36;
+		const float* xn = x + 6 * static_cast<int64_t>(n);
+		double dx = 0.0;
+#pragma unroll
+		for (int k = 0; k < 6; k++) dx += static_cast<double>(D[6 * q + k]) * static_cast<double>(xn[k]);
+		res[6 * static_cast<int64_t>(n) + q] = static_cast<float>((static_cast<double>(rhs[6 * static_cast<int64_t>(n) + q]) - dx) - t);
+	}
+}
+
+// ---- refinement's corner right-hand side: rhs2[perm(a)] = r_a - sum over stem edges i->a of (D_i^-1 B_ia)^T r_i (one wave
+// per corner node, as stem_rhs_wave) ----
+__global__ __launch_bounds__(256) void k_refine_corner_rhs(int nc, int n0, const int* __restrict__ rhs_off, const int* __restrict__ rhs_edges,
+                                                           const int32_t* __restrict__ edges, const float* __restrict__ dinv_b,
+                                                           const float* __restrict__ res, const int* __restrict__ node_row, float* __restrict__ rhs2) {
+	const int a = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
+	const int lane = static_cast<int>(threadIdx.x & 63);
+	if (a >= nc) return;
+	float s[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+	for (int q = rhs_off[a] + lane; q < rhs_off[a + 1]; q += 64) {
+		const int e = rhs_edges[q];
+		const int i = edges[2 * e];
+		const float* Y = dinv_b + static_cast<int64_t>(e) * 36;
+		const float* g = res + 6 * static_cast<int64_t>(i);
+		float gk[6];
+#pragma unroll
+		for (int k = 0; k < 6; k++) gk[k] = g[k];
+#pragma unroll
+		for (int c = 0; c < 6; c++) {
+			float t = 0.f;
+#pragma unroll
+			for (int k = 0; k < 6; k++) t += Y[6 * k + c] * gk[k];
+			s[c] += t;
+		}
+	}
+#pragma unroll
+	for (int c = 0; c < 6; c++)
+#pragma unroll
+		for (int off = 32; off > 0; off >>= 1) s[c] += __shfl_xor(s[c], off);
+	if (lane < 6) {
+		float v = s[0];
+#pragma unroll
+		for (int c = 1; c < 6; c++) v = lane == c ? s[c] : v;
+		rhs2[node_row[a] + lane] = res[6 * static_cast<int64_t>(n0 + a) + lane] - v;
+	}
 }
 
 nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* edges, const float* wing, int* error_flag, hipStream_t stream,
@@ -457,12 +547,32 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 		nnrt_status st = ws.corner->launch_solve(ws.x + 6 * static_cast<int64_t>(ws.n0), error_flag, stream);
 		if (st) return st;
 	}
-	const int threads = node_state ? ws.N : ws.n0;   // with node_state, the node updates ride along (all N nodes)
+	const bool refine = ws.refine && ws.inc_off && ws.res && ws.dx;
+	// with node_state, the node updates ride along (all N nodes) in the last back-substitution launch
+	const int threads = node_state && !refine ? ws.N : ws.n0;
 	if (threads > 0) {
 		k_arrow_back<<<static_cast<unsigned>(ceil_div(threads, 64)), 64, 0, stream>>>(ws.n0, threads, ws.dinv, ws.edge_offsets, ws.edge_list, edges,
-		                                                                             wing, ws.rhs, ws.x, state_in, node_state, updates_out);
+		                                                                             wing, ws.rhs, ws.x, state_in, refine ? nullptr : node_state,
+		                                                                             updates_out, nullptr);
 		NNRT_LAUNCH_CHECK();
 	}
+	if (!refine) return NNRT_OK;
+	// one step of iterative refinement: res = rhs - H x (double sums), H d = res with the same factors, x += d
+	k_arrow_residual<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ws.N) * 32, 256)), 256, 0, stream>>>(
+	    ws.N, ws.diag, ws.inc_off, ws.inc_list, edges, wing, ws.rhs, ws.x, ws.res);
+	NNRT_LAUNCH_CHECK();
+	if (m > 0) {
+		const CornerMap cm = ws.corner->map();
+		k_refine_corner_rhs<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(m / 6) * 64, 256)), 256, 0, stream>>>(
+		    m / 6, ws.n0, ws.rhs_off, ws.rhs_edges, edges, ws.dinv_b, ws.res, cm.node_row, ws.corner->refine_rhs());
+		NNRT_LAUNCH_CHECK();
+		nnrt_status st = ws.corner->launch_resolve(ws.dx + 6 * static_cast<int64_t>(ws.n0), stream);
+		if (st) return st;
+	}
+	// every node: x += d (and, with node_state, the update)
+	k_arrow_back<<<static_cast<unsigned>(ceil_div(ws.N, 64)), 64, 0, stream>>>(ws.n0, ws.N, ws.dinv, ws.edge_offsets, ws.edge_list, edges,
+	                                                                              wing, ws.res, ws.dx, state_in, node_state, updates_out, ws.x);
+	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;
 }
 

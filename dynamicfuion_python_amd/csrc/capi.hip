@@ -390,7 +390,7 @@ struct nnrt_fitter {
 	DeviceBuffer<float> updates, gradient, hessian;
 	DeviceBuffer<int> error_flag;
 	// ARAP / arrowhead
-	DeviceBuffer<float> wing, edge_residuals, a_diag, a_dinv, a_dinvb, a_rhs, a_x;
+	DeviceBuffer<float> wing, edge_residuals, a_diag, a_dinv, a_dinvb, a_rhs, a_x, a_res, a_dx;
 	CornerSolver corner;   // Schur corner of the arrowhead solve (tile-sparse Cholesky plan + storage)
 	DeviceBuffer<int> a_offsets, a_list, a_tgt_off, a_rhs_off, a_rhs_edges, a_inc_off, a_inc_list;
 	DeviceBuffer<int2> a_tgt_ab, a_pairs;
@@ -636,7 +636,7 @@ void nnrt_fitter_destroy(nnrt_fitter* ft) {
 	ft->ref_points.release();
 	ft->records.release();
 	for (auto* b : {&ft->mesh_p, &ft->mesh_n, &ft->weights, &ft->residuals, &ft->edge_jr, &ft->updates, &ft->gradient,
-	                &ft->hessian, &ft->wing, &ft->edge_residuals, &ft->a_diag, &ft->a_dinv, &ft->a_dinvb, &ft->a_rhs, &ft->a_x})
+	                &ft->hessian, &ft->wing, &ft->edge_residuals, &ft->a_diag, &ft->a_dinv, &ft->a_dinvb, &ft->a_rhs, &ft->a_x, &ft->a_res, &ft->a_dx})
 		b->release();
 	ft->faces4.release();
 	ft->anchors.release();
@@ -736,6 +736,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 		    (st = ft->a_dinvb.ensure(static_cast<size_t>(E) * 36)) ||
 		    (st = ft->edge_jr.ensure(static_cast<size_t>(E) * EDGE_TERMS)) ||
 		    (st = ft->a_rhs.ensure(6 * static_cast<size_t>(N))) || (st = ft->a_x.ensure(6 * static_cast<size_t>(N))) ||
+		    (st = ft->a_res.ensure(6 * static_cast<size_t>(N))) || (st = ft->a_dx.ensure(6 * static_cast<size_t>(N))) ||
 		    (st = ft->a_offsets.ensure(n0 + 1)) || (st = ft->a_list.ensure(E)))
 			return st;
 		// CSR of stem edges by source node
@@ -789,6 +790,9 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 		ft->aw.dinv_b = ft->a_dinvb.ptr;
 		ft->aw.rhs = ft->a_rhs.ptr;
 		ft->aw.x = ft->a_x.ptr;
+		ft->aw.refine = NNRT_ARAP_REFINE != 0;
+		ft->aw.res = ft->a_res.ptr;
+		ft->aw.dx = ft->a_dx.ptr;
 		ft->aw.edge_offsets = ft->a_offsets.ptr;
 		ft->aw.edge_list = ft->a_list.ptr;
 	}

@@ -237,6 +237,12 @@ struct CornerPlan {
 	std::vector<int2> back_chains;    // (first column entry, column count): a chain of the elimination tree, root end first
 	std::vector<int4> back_cols;      // (J, entry offset, entry count, 1 if L_JJ^-1 is formed: every column below the top level)
 	std::vector<int2> back_ent;       // (slot of L_IJ, I)
+	// forward substitution L y = b (iterative refinement): the back chains in reverse (deepest launch first, each chain
+	// from its bottom column up); per column its row entries (slot of L_Jk, k), k < J
+	std::vector<int> fwd_off;
+	std::vector<int2> fwd_chains;     // (first column entry, column count)
+	std::vector<int4> fwd_cols;       // (J, entry offset, entry count, 1 if L_JJ^-1 is formed)
+	std::vector<int2> fwd_ent;        // (slot of L_Jk, k)
 	std::vector<int> corner_edges;    // edges between two corner nodes (>= 3 layers)
 };
 
@@ -434,6 +440,24 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 			}
 		}
 		p.back_off.push_back(static_cast<int>(p.back_chains.size()));
+	}
+	// forward chains: row entries of every column, then the back launches in reverse with each chain reversed
+	std::vector<std::vector<int2>> rows(static_cast<size_t>(T));
+	for (size_t sl = 0; sl < p.slot_ij.size(); sl++)
+		if (p.slot_ij[sl].x != p.slot_ij[sl].y) rows[static_cast<size_t>(p.slot_ij[sl].x)].push_back(make_int2(static_cast<int>(sl), p.slot_ij[sl].y));
+	p.fwd_off.push_back(0);
+	for (int l = static_cast<int>(p.back_off.size()) - 2; l >= 0; l--) {
+		for (int c = p.back_off[static_cast<size_t>(l)]; c < p.back_off[static_cast<size_t>(l) + 1]; c++) {
+			const int2 ch = p.back_chains[static_cast<size_t>(c)];
+			p.fwd_chains.push_back(make_int2(static_cast<int>(p.fwd_cols.size()), ch.y));
+			for (int q = ch.y - 1; q >= 0; q--) {
+				const int4 bc = p.back_cols[static_cast<size_t>(ch.x + q)];
+				const auto& rw = rows[static_cast<size_t>(bc.x)];
+				p.fwd_cols.push_back(make_int4(bc.x, static_cast<int>(p.fwd_ent.size()), static_cast<int>(rw.size()), bc.w));
+				p.fwd_ent.insert(p.fwd_ent.end(), rw.begin(), rw.end());
+			}
+		}
+		p.fwd_off.push_back(static_cast<int>(p.fwd_chains.size()));
 	}
 	return p;
 }
@@ -941,6 +965,108 @@ __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 	}
 }
 
+// Forward substitution L y = b along the forward chains (iterative refinement's corner solve; the first solve's forward
+// substitution rides in the factorization as the augmented row): per column J, z = b_J - sum_k L_Jk y_k over its row
+// entries (lane (row quarter, column group) covers rows 16 wave + rq + 4i and columns 4 cg .. 4 cg + 3 of every entry tile;
+// the 16 column groups are summed across lanes, so each row's sum is complete in its wave), then y_J = L_JJ^-1 z (the
+// product with M, rows of M loaded ahead) or, for top-level columns, the row-oriented substitution on wave 0. y_J
+// overwrites b_J in yb (a column reads y of its descendants only: earlier launches or earlier in its chain).
+struct CornerFwdArgs {
+	const float* tiles;
+	const float* ldiag;
+	const float* minv;
+	float* yb;               // [ld] b in, y out (permuted order)
+	const int2* chains;
+	const int4* cols;        // (J, entry offset, entry count, 1 if L_JJ^-1 is formed)
+	const int2* ent;         // (slot of L_Jk, k)
+};
+__global__ __launch_bounds__(CT) void k_corner_fwd(CornerFwdArgs a) {
+	__shared__ __attribute__((aligned(16))) float s_z[TILE];
+	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+	const int2 ch = a.chains[blockIdx.x];
+	const int cg = lane & 15, rq = lane >> 4;
+	for (int q = 0; q < ch.y; q++) {
+		const int4 col = a.cols[ch.x + q];
+		const int J = col.x;
+		const bool inv = col.w != 0;
+		// wave 0: row `lane` of M (inverse) or of L_JJ (substitution), loaded ahead of the sums
+		float rowv[TILE];
+		if (wave == 0) {
+			const float4* R4 = reinterpret_cast<const float4*>((inv ? a.minv : a.ldiag) + static_cast<int64_t>(J) * TILE_ELEMS + lane * TILE);
+#pragma unroll
+			for (int c4 = 0; c4 < TILE / 4; c4++) {
+				const float4 v = R4[c4];
+				rowv[4 * c4] = v.x;
+				rowv[4 * c4 + 1] = v.y;
+				rowv[4 * c4 + 2] = v.z;
+				rowv[4 * c4 + 3] = v.w;
+			}
+		}
+		float acc[4] = {0.f, 0.f, 0.f, 0.f};   // rows 16 wave + rq + 4 i, partial over this lane's 4 columns
+		for (int e0 = 0; e0 < col.z; e0 += 64) {
+			const int ne = col.z - e0 < 64 ? col.z - e0 : 64;
+			const int2 mine = lane < ne ? a.ent[col.y + e0 + lane] : make_int2(0, 0);
+			for (int e = 0; e < ne; e += BACK_BATCH) {
+				float4 l[BACK_BATCH][4], yv[BACK_BATCH];
+#pragma unroll
+				for (int j = 0; j < BACK_BATCH; j++) {
+					const bool ok = e + j < ne;   // a missing entry repeats entry e's tile against y = 0
+					const int sj = __shfl(mine.x, ok ? e + j : e);
+					const int kj = __shfl(mine.y, ok ? e + j : e);
+					const float* Lj = a.tiles + static_cast<int64_t>(sj) * TILE_ELEMS + (16 * wave + rq) * TILE + 4 * cg;
+#pragma unroll
+					for (int i = 0; i < 4; i++) l[j][i] = *reinterpret_cast<const float4*>(Lj + 4 * i * TILE);
+					const float4 y4 = *reinterpret_cast<const float4*>(a.yb + static_cast<int64_t>(kj) * TILE + 4 * cg);
+					yv[j] = ok ? y4 : make_float4(0.f, 0.f, 0.f, 0.f);
+				}
+#pragma unroll
+				for (int j = 0; j < BACK_BATCH; j++)
+#pragma unroll
+					for (int i = 0; i < 4; i++)
+						acc[i] += ((l[j][i].x * yv[j].x + l[j][i].y * yv[j].y) + l[j][i].z * yv[j].z) + l[j][i].w * yv[j].w;
+			}
+		}
+#pragma unroll
+		for (int i = 0; i < 4; i++)
+#pragma unroll
+			for (int m = 1; m < 16; m <<= 1) acc[i] += __shfl_xor(acc[i], m);
+		if (cg == 0) {
+#pragma unroll
+			for (int i = 0; i < 4; i++) {
+				const int r = 16 * wave + rq + 4 * i;
+				s_z[r] = a.yb[static_cast<int64_t>(J) * TILE + r] - acc[i];
+			}
+		}
+		__syncthreads();
+		if (wave == 0) {
+			float y;
+			if (inv) {   // y_c = sum_r M_cr z_r
+				float ys[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+				for (int r4 = 0; r4 < TILE; r4 += 4) {
+					const float4 zz = *reinterpret_cast<const float4*>(&s_z[r4]);
+					ys[0] = __builtin_fmaf(rowv[r4], zz.x, ys[0]);
+					ys[1] = __builtin_fmaf(rowv[r4 + 1], zz.y, ys[1]);
+					ys[2] = __builtin_fmaf(rowv[r4 + 2], zz.z, ys[2]);
+					ys[3] = __builtin_fmaf(rowv[r4 + 3], zz.w, ys[3]);
+				}
+				y = (ys[0] + ys[1]) + (ys[2] + ys[3]);
+			} else {   // row-oriented: y_c = z_c / L_cc, then z_r -= L_rc y_c for r > c
+				float z = s_z[lane];
+				y = 0.f;
+#pragma unroll
+				for (int c = 0; c < TILE; c++) {
+					const float yc = lane_bcast(z, c) / lane_bcast(rowv[c], c);
+					y = lane == c ? yc : y;
+					z -= rowv[c] * yc;   // only rows r > c matter (L_rc = 0 above the diagonal)
+				}
+			}
+			a.yb[static_cast<int64_t>(J) * TILE + lane] = y;
+		}
+		__syncthreads();   // y_J visible to the chain's next column; s_z free
+	}
+}
+
 // ===================================================================================================================
 // CornerSolver
 // ===================================================================================================================
@@ -962,6 +1088,8 @@ CornerSolver::~CornerSolver() { release(); }
 
 void CornerSolver::release() {
 	for (void** p : {reinterpret_cast<void**>(&tiles), reinterpret_cast<void**>(&ldiag), reinterpret_cast<void**>(&minv), reinterpret_cast<void**>(&d_inv_cols),
+	                 reinterpret_cast<void**>(&cb2), reinterpret_cast<void**>(&d_fwd_chains), reinterpret_cast<void**>(&d_fwd_cols),
+	                 reinterpret_cast<void**>(&d_fwd_ent),
 	                 reinterpret_cast<void**>(&cb),
 	                 reinterpret_cast<void**>(&xp), reinterpret_cast<void**>(&d_tile_slot), reinterpret_cast<void**>(&d_slot_ij),
 	                 reinterpret_cast<void**>(&d_row_node), reinterpret_cast<void**>(&d_node_row), reinterpret_cast<void**>(&d_tasks),
@@ -972,6 +1100,7 @@ void CornerSolver::release() {
 	level_off.clear();
 	level_panel.clear();
 	inv_off.clear();
+	fwd_off.clear();
 	back_off.clear();
 	key.clear();
 }
@@ -1003,14 +1132,19 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 	if (p.nc > 0) {
 		nnrt_status st;
 		if ((st = alloc(tiles, p.slot_ij.size() * TILE_ELEMS)) || (st = alloc(ldiag, static_cast<size_t>(p.T) * TILE_ELEMS)) ||
-		    (st = alloc(minv, static_cast<size_t>(p.T) * TILE_ELEMS)) ||
+		    (st = alloc(minv, static_cast<size_t>(p.T) * TILE_ELEMS)) || (st = alloc(cb2, static_cast<size_t>(p.ld))) ||
 		    (st = alloc(cb, static_cast<size_t>(p.ld))) || (st = alloc(xp, static_cast<size_t>(p.ld))))
 			return fail(st);
 		if ((st = dev_upload(d_tile_slot, p.tile_slot)) || (st = dev_upload(d_slot_ij, p.slot_ij)) || (st = dev_upload(d_row_node, p.row_node)) ||
 		    (st = dev_upload(d_node_row, p.node_row)) || (st = dev_upload(d_tasks, p.tasks)) || (st = dev_upload(d_srcs, p.srcs)) ||
 		    (st = dev_upload(d_back_cols, p.back_cols)) || (st = dev_upload(d_back_ent, p.back_ent)) || (st = dev_upload(d_back_chains, p.back_chains)) ||
-		    (st = dev_upload(d_corner_edges, p.corner_edges)) || (st = dev_upload(d_inv_cols, p.inv_cols)))
+		    (st = dev_upload(d_corner_edges, p.corner_edges)) || (st = dev_upload(d_inv_cols, p.inv_cols)) ||
+		    (st = dev_upload(d_fwd_chains, p.fwd_chains)) || (st = dev_upload(d_fwd_cols, p.fwd_cols)) || (st = dev_upload(d_fwd_ent, p.fwd_ent)))
 			return fail(st);
+		if (hipMemset(cb2, 0, sizeof(float) * static_cast<size_t>(p.ld)) != hipSuccess) {   // identity padding rows stay 0
+			set_error("hipMemset failed");
+			return fail(NNRT_ERROR_HIP);
+		}
 	}
 	nc = p.nc;
 	if (nc > 0) {
@@ -1022,6 +1156,7 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		level_off = p.level_off;
 		level_panel = p.level_panel;
 		inv_off = p.inv_off;
+		fwd_off = p.fwd_off;
 		back_off = p.back_off;
 		fill_tiles = static_cast<int64_t>(slots);
 		dense_tiles = static_cast<int64_t>(corner_ld(6 * nc) / TILE) * (corner_ld(6 * nc) / TILE + 1) / 2;
@@ -1064,6 +1199,25 @@ nnrt_status CornerSolver::launch_solve(float* xout, int* error_flag, hipStream_t
 		NNRT_LAUNCH_CHECK();
 	}
 	CornerBackArgs ba{tiles, ldiag, minv, cb, xp, d_row_node, xout, nullptr, d_back_cols, d_back_ent};
+	for (size_t l = 0; l + 1 < back_off.size(); l++) {
+		const int n = back_off[l + 1] - back_off[l];
+		ba.chains = d_back_chains + back_off[l];
+		k_corner_back<<<n, CT, 0, s>>>(ba);
+		NNRT_LAUNCH_CHECK();
+	}
+	return NNRT_OK;
+}
+
+nnrt_status CornerSolver::launch_resolve(float* xout, hipStream_t s) const {
+	if (nc == 0) return NNRT_OK;
+	CornerFwdArgs fa{tiles, ldiag, minv, cb2, nullptr, d_fwd_cols, d_fwd_ent};
+	for (size_t l = 0; l + 1 < fwd_off.size(); l++) {
+		const int n = fwd_off[l + 1] - fwd_off[l];
+		fa.chains = d_fwd_chains + fwd_off[l];
+		k_corner_fwd<<<n, CT, 0, s>>>(fa);
+		NNRT_LAUNCH_CHECK();
+	}
+	CornerBackArgs ba{tiles, ldiag, minv, cb2, xp, d_row_node, xout, nullptr, d_back_cols, d_back_ent};
 	for (size_t l = 0; l + 1 < back_off.size(); l++) {
 		const int n = back_off[l + 1] - back_off[l];
 		ba.chains = d_back_chains + back_off[l];

@@ -260,6 +260,10 @@ public:
 	nnrt_status launch_offdiag(int n0, const int32_t* edges, const float* wing, hipStream_t s) const;   // >= 3 layers
 	// factor S (after the stem's Schur update), solve S x = cb; x -> xout[6 nc] in corner-node order
 	nnrt_status launch_solve(float* xout, int* error_flag, hipStream_t s) const;
+	// iterative refinement: solve S d = rhs2 with the factor of the last launch_solve (rhs2 = refine_rhs(), permuted,
+	// written by the caller); d -> xout[6 nc] in corner-node order
+	nnrt_status launch_resolve(float* xout, hipStream_t s) const;
+	float* refine_rhs() const { return cb2; }
 	CornerMap map() const;
 	float* rhs_perm() const { return cb; }
 	int levels() const { return H; }
@@ -274,13 +278,20 @@ private:
 	std::vector<int32_t> key;
 	int nc = 0, ld = 0, T = 0, H = 0, slots = 0, n_corner_edges = 0;
 	int64_t fill_tiles = 0, dense_tiles = 0;
-	float *tiles = nullptr, *ldiag = nullptr, *minv = nullptr, *cb = nullptr, *xp = nullptr;
+	float *tiles = nullptr, *ldiag = nullptr, *minv = nullptr, *cb = nullptr, *cb2 = nullptr, *xp = nullptr;
+	int2 *d_fwd_chains = nullptr, *d_fwd_ent = nullptr;
+	int4* d_fwd_cols = nullptr;
 	int *d_tile_slot = nullptr, *d_row_node = nullptr, *d_node_row = nullptr, *d_corner_edges = nullptr, *d_inv_cols = nullptr;
 	int2 *d_slot_ij = nullptr, *d_back_ent = nullptr, *d_back_chains = nullptr;
 	CornerTask* d_tasks = nullptr;
 	int4 *d_srcs = nullptr, *d_back_cols = nullptr;
-	std::vector<int> level_off, level_panel, inv_off, back_off;
+	std::vector<int> level_off, level_panel, inv_off, back_off, fwd_off;
 };
+
+// one step of iterative refinement after the fitter's arrowhead solve; 0: the float solve alone
+#ifndef NNRT_ARAP_REFINE
+#define NNRT_ARAP_REFINE 1
+#endif
 
 struct ArrowheadWorkspace {
 	int N = 0, n0 = 0, E = 0, m = 0;
@@ -290,6 +301,11 @@ struct ArrowheadWorkspace {
 	float* dinv_b = nullptr;    // [E,36]
 	float* rhs = nullptr;       // [6N] negative gradient
 	float* x = nullptr;         // [6N]
+	// iterative refinement (refine: one step after the first solve): res [6N] = rhs - H x (fp64 sums, rounded), dx [6N]
+	// the correction; the update is x + dx
+	bool refine = false;
+	float* res = nullptr;
+	float* dx = nullptr;
 	int* edge_offsets = nullptr;// [n0+1] CSR of stem edges by source node (edges grouped by source)
 	int* edge_list = nullptr;   // [E]
 	int* inc_off = nullptr;     // [N+1] CSR of edge incidences by node (fitter only: k_arrow_prepare)
