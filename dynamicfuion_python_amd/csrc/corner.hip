@@ -243,6 +243,10 @@ struct CornerPlan {
 	std::vector<int2> fwd_chains;     // (first column entry, column count)
 	std::vector<int4> fwd_cols;       // (J, entry offset, entry count, 1 if L_JJ^-1 is formed)
 	std::vector<int2> fwd_ent;        // (slot of L_Jk, k)
+	// single-workgroup walks (k_corner_walk): per stream element (array: 0 tiles slot / 1 L_JJ^-1 / 2 L_JJ, index, x_off,
+	// info); back: columns T-1 .. 0, each its entries L_IJ (ascending I) then its head; forward: columns 0 .. T-1, each its
+	// row entries L_Jk (ascending k) then its head
+	std::vector<int4> walk_back, walk_fwd;
 	std::vector<int> corner_edges;    // edges between two corner nodes (>= 3 layers)
 };
 
@@ -440,6 +444,24 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 			}
 		}
 		p.back_off.push_back(static_cast<int>(p.back_chains.size()));
+	}
+	// single-workgroup walk streams
+	{
+		std::vector<std::vector<int>> rowk(static_cast<size_t>(T));   // rowk[J]: k < J with a stored tile (J, k), ascending
+		for (int k = 0; k < T; k++)
+			for (int I : cs[static_cast<size_t>(k)]) rowk[static_cast<size_t>(I)].push_back(k);
+		auto head = [&](int J) {
+			const bool inv = lvl[static_cast<size_t>(J)] < p.H - 1;
+			return make_int4(inv ? 1 : 2, J, J * TILE, inv ? 1 : 0);
+		};
+		for (int J = T - 1; J >= 0; J--) {
+			for (int I : cs[static_cast<size_t>(J)]) p.walk_back.push_back(make_int4(0, slot(I, J), I * TILE, -1));
+			p.walk_back.push_back(head(J));
+		}
+		for (int J = 0; J < T; J++) {
+			for (int k : rowk[static_cast<size_t>(J)]) p.walk_fwd.push_back(make_int4(0, slot(J, k), k * TILE, -1));
+			p.walk_fwd.push_back(head(J));
+		}
 	}
 	// forward chains: row entries of every column, then the back launches in reverse with each chain reversed
 	std::vector<std::vector<int2>> rows(static_cast<size_t>(T));
@@ -1068,6 +1090,229 @@ __global__ __launch_bounds__(CT) void k_corner_fwd(CornerFwdArgs a) {
 }
 
 // ===================================================================================================================
+// Single-workgroup substitution walks (the corner solves when the permuted vector fits in LDS): one launch walks every
+// tile column in order -- back substitution in descending column order (ancestors before descendants), forward in
+// ascending order -- keeping the whole solution vector in LDS, while the tiles each column needs stream through an
+// LDS ring by LDS-DMA (global_load_lds_dwordx4) issued ahead of their use. A column's stream elements are its entry
+// tiles, then its head: L_JJ^-1 (or L_JJ for top-level columns, which take the substitution). Nothing crosses
+// workgroups: no inter-workgroup ordering at all.
+// ===================================================================================================================
+constexpr int WT = 512;        // threads of the walk workgroup (8 waves)
+constexpr int WALK_MAX_LD = 8192;
+constexpr int WALK_MAX_ELEMS = 1024;
+struct WalkElem {
+	const float* tile;   // 64 x 64 row-major tile
+	int x_off;           // entry: first unknown of the tile whose x (back) / y (forward) it multiplies; head: J * 64
+	int info;            // entry: -1; head: 1 if the tile is L_JJ^-1, 0 if it is L_JJ
+};
+struct CornerWalkArgs {
+	const WalkElem* fwd;   // forward stream (n_fwd = 0: none)
+	const WalkElem* back;  // back stream (n_back = 0: none)
+	int n_fwd, n_back;
+	const float* rhs;      // [ld] permuted right-hand side (back only: y; forward + back: b)
+	const int* row_node;
+	float* xout;           // [6 nc] corner-node order
+	int ld, ring;
+};
+
+typedef __attribute__((address_space(3))) void walk_lds_t;
+typedef const __attribute__((address_space(1))) void walk_global_t;
+
+// s_waitcnt vmcnt(n) for a run-time n (even values up to 62: two DMA instructions per wave per tile)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+	switch (n) {
+#define W_(k) \
+	case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+		W_(0) W_(2) W_(4) W_(6) W_(8) W_(10) W_(12) W_(14) W_(16) W_(18) W_(20) W_(22) W_(24) W_(26) W_(28) W_(30)
+		W_(32) W_(34) W_(36) W_(38) W_(40) W_(42) W_(44) W_(46) W_(48) W_(50) W_(52) W_(54) W_(56) W_(58) W_(60) W_(62)
+#undef W_
+		default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+	}
+}
+// workgroup barrier for LDS traffic only: retires this wave's LDS operations, leaves LDS-DMA loads in flight
+__device__ __forceinline__ void lds_barrier() {
+	asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+	__builtin_amdgcn_s_barrier();
+}
+
+// one pass over a stream; x (LDS, ld floats) holds the right-hand side on entry and the solution on exit
+template <bool BACK>
+__device__ void walk_pass(const WalkElem* __restrict__ gdesc, int n, int R, WalkElem* desc, float* x, float* red, float* zt, float* ring) {
+	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+	const int rg = t >> 4, cg = t & 15;   // rows 2 rg, 2 rg + 1 and columns 4 cg .. 4 cg + 3 of a tile
+	for (int i = t; i < n; i += WT) desc[i] = gdesc[i];
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	lds_barrier();
+	int issued = 0;
+	auto issue = [&](int e) {   // tile e -> ring slot e % R: 16 KB = 16 DMA pieces of 1 KB, two per wave
+		const float* src = desc[e].tile;
+		float* dst = ring + (e % R) * TILE_ELEMS;
+#pragma unroll
+		for (int i = 0; i < 2; i++) {
+			const int chunk = 2 * wave + i;
+			__builtin_amdgcn_global_load_lds((walk_global_t*)(src + chunk * 256 + lane * 4), (walk_lds_t*)(dst + chunk * 256), 16, 0, 0);
+		}
+	};
+	while (issued < n && issued < R) issue(issued++);
+	int p = 0;
+	while (p < n) {
+		int h = p;   // the column's head (its last element)
+		while (desc[h].info < 0) h++;
+		const int J64 = desc[h].x_off;
+		float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);   // back: columns 4 cg.. partials; forward: .x / .y rows 2 rg / 2 rg + 1
+		int q = p;
+		while (true) {
+			const int last = min(h, q + R - 1);
+			wait_vmcnt(2 * (issued - 1 - last));
+			lds_barrier();   // every wave's pieces of tiles q .. last have landed
+			for (int e = q; e <= last && e < h; e++) {
+				const float* T = ring + (e % R) * TILE_ELEMS;
+				const float4 a = *reinterpret_cast<const float4*>(T + (2 * rg) * TILE + 4 * cg);
+				const float4 b = *reinterpret_cast<const float4*>(T + (2 * rg + 1) * TILE + 4 * cg);
+				const int xo = desc[e].x_off;
+				if constexpr (BACK) {
+					const float x0 = x[xo + 2 * rg], x1 = x[xo + 2 * rg + 1];
+					acc.x += a.x * x0 + b.x * x1;
+					acc.y += a.y * x0 + b.y * x1;
+					acc.z += a.z * x0 + b.z * x1;
+					acc.w += a.w * x0 + b.w * x1;
+				} else {
+					const float4 y = *reinterpret_cast<const float4*>(x + xo + 4 * cg);
+					acc.x += ((a.x * y.x + a.y * y.y) + a.z * y.z) + a.w * y.w;
+					acc.y += ((b.x * y.x + b.y * y.y) + b.z * y.z) + b.w * y.w;
+				}
+			}
+			if (last == h) break;
+			lds_barrier();   // tiles q .. last read by every wave: their slots are free
+			while (issued < n && issued <= last + R) issue(issued++);
+			q = last + 1;
+		}
+		// column finish: the head tile (slot h % R) is resident
+		const float* Hd = ring + (h % R) * TILE_ELEMS;
+		const bool inv = desc[h].info != 0;
+		if constexpr (BACK) {
+			// z_c = y_c - sum over rows: lanes 16 apart share columns; the 8 waves meet in LDS
+#pragma unroll
+			for (int m = 16; m < 64; m <<= 1) {
+				acc.x += __shfl_xor(acc.x, m);
+				acc.y += __shfl_xor(acc.y, m);
+				acc.z += __shfl_xor(acc.z, m);
+				acc.w += __shfl_xor(acc.w, m);
+			}
+			if (lane < 16) *reinterpret_cast<float4*>(red + wave * TILE + 4 * lane) = acc;
+			lds_barrier();
+			if (wave == 0) {
+				float zs = 0.f;
+#pragma unroll
+				for (int w = 0; w < WT / 64; w++) zs += red[w * TILE + lane];
+				zt[lane] = x[J64 + lane] - zs;
+			}
+			lds_barrier();
+			if (inv) {   // x_c = sum_r M_rc z_r
+				const float4 a = *reinterpret_cast<const float4*>(Hd + (2 * rg) * TILE + 4 * cg);
+				const float4 b = *reinterpret_cast<const float4*>(Hd + (2 * rg + 1) * TILE + 4 * cg);
+				const float z0 = zt[2 * rg], z1 = zt[2 * rg + 1];
+				float4 m4 = make_float4(a.x * z0 + b.x * z1, a.y * z0 + b.y * z1, a.z * z0 + b.z * z1, a.w * z0 + b.w * z1);
+#pragma unroll
+				for (int m = 16; m < 64; m <<= 1) {
+					m4.x += __shfl_xor(m4.x, m);
+					m4.y += __shfl_xor(m4.y, m);
+					m4.z += __shfl_xor(m4.z, m);
+					m4.w += __shfl_xor(m4.w, m);
+				}
+				if (lane < 16) *reinterpret_cast<float4*>(red + wave * TILE + 4 * lane) = m4;
+				lds_barrier();
+				if (wave == 0) {
+					float xs = 0.f;
+#pragma unroll
+					for (int w = 0; w < WT / 64; w++) xs += red[w * TILE + lane];
+					x[J64 + lane] = xs;
+				}
+			} else if (wave == 0) {   // column-oriented substitution with L_JJ (lane = column, L_rc from the resident tile)
+				float colv[TILE];
+#pragma unroll
+				for (int r = 0; r < TILE; r++) colv[r] = Hd[r * TILE + lane];
+				float z = zt[lane], xv = 0.f;
+#pragma unroll
+				for (int r = TILE - 1; r >= 0; r--) {
+					const float xr = lane_bcast(z, r) / lane_bcast(colv[r], r);
+					xv = lane == r ? xr : xv;
+					z -= colv[r] * xr;
+				}
+				x[J64 + lane] = xv;
+			}
+		} else {
+			// row sums across the 16 column groups of each row (within the wave)
+#pragma unroll
+			for (int m = 1; m < 16; m <<= 1) {
+				acc.x += __shfl_xor(acc.x, m);
+				acc.y += __shfl_xor(acc.y, m);
+			}
+			if (cg == 0) {
+				zt[2 * rg] = x[J64 + 2 * rg] - acc.x;
+				zt[2 * rg + 1] = x[J64 + 2 * rg + 1] - acc.y;
+			}
+			lds_barrier();
+			if (inv) {   // y_r = sum_c M_rc z_c
+				const float4 a = *reinterpret_cast<const float4*>(Hd + (2 * rg) * TILE + 4 * cg);
+				const float4 b = *reinterpret_cast<const float4*>(Hd + (2 * rg + 1) * TILE + 4 * cg);
+				const float4 z = *reinterpret_cast<const float4*>(zt + 4 * cg);
+				float y0 = ((a.x * z.x + a.y * z.y) + a.z * z.z) + a.w * z.w;
+				float y1 = ((b.x * z.x + b.y * z.y) + b.z * z.z) + b.w * z.w;
+#pragma unroll
+				for (int m = 1; m < 16; m <<= 1) {
+					y0 += __shfl_xor(y0, m);
+					y1 += __shfl_xor(y1, m);
+				}
+				if (cg == 0) {
+					x[J64 + 2 * rg] = y0;
+					x[J64 + 2 * rg + 1] = y1;
+				}
+			} else if (wave == 0) {   // row-oriented substitution with L_JJ: lane r holds row r; y_c = z_c / L_cc, z_r -= L_rc y_c
+				float rowv[TILE];
+#pragma unroll
+				for (int c4 = 0; c4 < TILE / 4; c4++) {
+					const float4 v = *reinterpret_cast<const float4*>(Hd + lane * TILE + 4 * c4);
+					rowv[4 * c4] = v.x;
+					rowv[4 * c4 + 1] = v.y;
+					rowv[4 * c4 + 2] = v.z;
+					rowv[4 * c4 + 3] = v.w;
+				}
+				float z = zt[lane], yv = 0.f;
+#pragma unroll
+				for (int c = 0; c < TILE; c++) {
+					const float yc = lane_bcast(z, c) / lane_bcast(rowv[c], c);
+					yv = lane == c ? yc : yv;
+					z -= rowv[c] * yc;   // rows r > c only matter (L_rc = 0 above the diagonal)
+				}
+				x[J64 + lane] = yv;
+			}
+		}
+		lds_barrier();   // x_J visible; the column's slots (and red / zt) free
+		while (issued < n && issued <= h + R) issue(issued++);
+		p = h + 1;
+	}
+}
+
+__global__ __launch_bounds__(WT) void k_corner_walk(CornerWalkArgs a) {
+	extern __shared__ __attribute__((aligned(16))) float s_walk[];
+	const int nd = a.n_fwd > a.n_back ? a.n_fwd : a.n_back;
+	WalkElem* desc = reinterpret_cast<WalkElem*>(s_walk);
+	float* x = s_walk + 4 * nd;
+	float* red = x + ((a.ld + 3) & ~3);
+	float* zt = red + (WT / 64) * TILE;
+	float* ring = zt + TILE;
+	for (int i = threadIdx.x; i < a.ld; i += WT) x[i] = a.rhs[i];
+	if (a.n_fwd > 0) walk_pass<false>(a.fwd, a.n_fwd, a.ring, desc, x, red, zt, ring);
+	else lds_barrier();
+	if (a.n_back > 0) walk_pass<true>(a.back, a.n_back, a.ring, desc, x, red, zt, ring);
+	for (int i = threadIdx.x; i < a.ld; i += WT) {
+		const int rn = a.row_node[i];
+		if (rn >= 0) a.xout[6 * static_cast<int64_t>(rn >> 3) + (rn & 7)] = x[i];
+	}
+}
+
+// ===================================================================================================================
 // CornerSolver
 // ===================================================================================================================
 template <typename T>
@@ -1089,7 +1334,7 @@ CornerSolver::~CornerSolver() { release(); }
 void CornerSolver::release() {
 	for (void** p : {reinterpret_cast<void**>(&tiles), reinterpret_cast<void**>(&ldiag), reinterpret_cast<void**>(&minv), reinterpret_cast<void**>(&d_inv_cols),
 	                 reinterpret_cast<void**>(&cb2), reinterpret_cast<void**>(&d_fwd_chains), reinterpret_cast<void**>(&d_fwd_cols),
-	                 reinterpret_cast<void**>(&d_fwd_ent),
+	                 reinterpret_cast<void**>(&d_fwd_ent), reinterpret_cast<void**>(&d_walk_back), reinterpret_cast<void**>(&d_walk_fwd),
 	                 reinterpret_cast<void**>(&cb),
 	                 reinterpret_cast<void**>(&xp), reinterpret_cast<void**>(&d_tile_slot), reinterpret_cast<void**>(&d_slot_ij),
 	                 reinterpret_cast<void**>(&d_row_node), reinterpret_cast<void**>(&d_node_row), reinterpret_cast<void**>(&d_tasks),
@@ -1146,6 +1391,35 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 			return fail(NNRT_ERROR_HIP);
 		}
 	}
+	walk_ok = false;
+	if (p.nc > 0 && p.ld <= WALK_MAX_LD && static_cast<int>(std::max(p.walk_back.size(), p.walk_fwd.size())) <= WALK_MAX_ELEMS) {
+		// LDS: descriptors, the solution vector, the reduction rows, then a ring of as many tiles as fit (at least the
+		// largest column's elements need not fit: a column streams through the ring in parts)
+		const size_t nd = std::max(p.walk_back.size(), p.walk_fwd.size());
+		const size_t fixed = 16 * nd + 4 * (static_cast<size_t>((p.ld + 3) & ~3) + (WT / 64) * TILE + TILE);
+		const size_t budget = 160 * 1024;
+		const int ring_tiles = fixed < budget ? static_cast<int>(std::min<size_t>(8, (budget - fixed) / (4 * TILE_ELEMS))) : 0;
+		if (ring_tiles >= 2) {
+			std::vector<WalkElem> wb, wf;
+			auto elem = [&](const int4& e) {
+				const float* base = e.x == 0 ? tiles : e.x == 1 ? minv : ldiag;
+				return WalkElem{base + static_cast<int64_t>(e.y) * TILE_ELEMS, e.z, e.w};
+			};
+			for (const auto& e : p.walk_back) wb.push_back(elem(e));
+			for (const auto& e : p.walk_fwd) wf.push_back(elem(e));
+			nnrt_status st;
+			if ((st = dev_upload(d_walk_back, wb)) || (st = dev_upload(d_walk_fwd, wf))) return fail(st);
+			walk_ring = ring_tiles;
+			walk_lds = static_cast<int>(fixed + static_cast<size_t>(ring_tiles) * 4 * TILE_ELEMS);
+			n_walk_back = static_cast<int>(wb.size());
+			n_walk_fwd = static_cast<int>(wf.size());
+			if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_corner_walk), hipFuncAttributeMaxDynamicSharedMemorySize, walk_lds) != hipSuccess) {
+				set_error("hipFuncSetAttribute (corner walk LDS) failed");
+				return fail(NNRT_ERROR_HIP);
+			}
+			walk_ok = true;
+		}
+	}
 	nc = p.nc;
 	if (nc > 0) {
 		ld = p.ld;
@@ -1198,6 +1472,12 @@ nnrt_status CornerSolver::launch_solve(float* xout, int* error_flag, hipStream_t
 		k_corner_factor<<<n + ni, CT, 0, s>>>(fa);
 		NNRT_LAUNCH_CHECK();
 	}
+	if (walk_ok) {   // the back substitution as one single-workgroup walk
+		const CornerWalkArgs wa{nullptr, d_walk_back, 0, n_walk_back, cb, d_row_node, xout, ld, walk_ring};
+		k_corner_walk<<<1, WT, walk_lds, s>>>(wa);
+		NNRT_LAUNCH_CHECK();
+		return NNRT_OK;
+	}
 	CornerBackArgs ba{tiles, ldiag, minv, cb, xp, d_row_node, xout, nullptr, d_back_cols, d_back_ent};
 	for (size_t l = 0; l + 1 < back_off.size(); l++) {
 		const int n = back_off[l + 1] - back_off[l];
@@ -1210,6 +1490,12 @@ nnrt_status CornerSolver::launch_solve(float* xout, int* error_flag, hipStream_t
 
 nnrt_status CornerSolver::launch_resolve(float* xout, hipStream_t s) const {
 	if (nc == 0) return NNRT_OK;
+	if (walk_ok) {   // forward and back substitution in one single-workgroup launch
+		const CornerWalkArgs wa{d_walk_fwd, d_walk_back, n_walk_fwd, n_walk_back, cb2, d_row_node, xout, ld, walk_ring};
+		k_corner_walk<<<1, WT, walk_lds, s>>>(wa);
+		NNRT_LAUNCH_CHECK();
+		return NNRT_OK;
+	}
 	CornerFwdArgs fa{tiles, ldiag, minv, cb2, nullptr, d_fwd_cols, d_fwd_ent};
 	for (size_t l = 0; l + 1 < fwd_off.size(); l++) {
 		const int n = fwd_off[l + 1] - fwd_off[l];

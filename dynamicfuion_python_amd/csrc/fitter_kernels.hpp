@@ -246,6 +246,8 @@ __device__ inline void corner_init_thread(int64_t idx, const CornerInitArgs& a, 
 	*reinterpret_cast<float4*>(a.tiles + static_cast<int64_t>(s) * TE + r * TL + c0) = make_float4(v[0], v[1], v[2], v[3]);
 }
 
+struct WalkElem;   // corner.hip: one tile of a single-workgroup substitution walk
+
 class CornerSolver {
 public:
 	~CornerSolver();
@@ -268,7 +270,7 @@ public:
 	float* rhs_perm() const { return cb; }
 	int levels() const { return H; }
 	int tile_columns() const { return T; }
-	int back_launches() const { return back_off.empty() ? 0 : static_cast<int>(back_off.size()) - 1; }
+	int back_launches() const { return walk_ok ? 1 : back_off.empty() ? 0 : static_cast<int>(back_off.size()) - 1; }
 	int64_t stored_tiles() const { return fill_tiles; }
 	int64_t dense_lower_tiles() const { return dense_tiles; }
 	uint64_t generation = 0;    // bumped whenever the plan (and its buffers) change
@@ -281,6 +283,11 @@ private:
 	float *tiles = nullptr, *ldiag = nullptr, *minv = nullptr, *cb = nullptr, *cb2 = nullptr, *xp = nullptr;
 	int2 *d_fwd_chains = nullptr, *d_fwd_ent = nullptr;
 	int4* d_fwd_cols = nullptr;
+	// single-workgroup substitution walks (corner.hip k_corner_walk), when the permuted vector and the descriptors fit in LDS
+	bool walk_ok = false;
+	int walk_ring = 0, walk_lds = 0, n_walk_back = 0, n_walk_fwd = 0;
+	WalkElem* d_walk_back = nullptr;
+	WalkElem* d_walk_fwd = nullptr;
 	int *d_tile_slot = nullptr, *d_row_node = nullptr, *d_node_row = nullptr, *d_corner_edges = nullptr, *d_inv_cols = nullptr;
 	int2 *d_slot_ij = nullptr, *d_back_ent = nullptr, *d_back_chains = nullptr;
 	CornerTask* d_tasks = nullptr;

@@ -170,5 +170,42 @@ int main(int argc, char** argv) {
 	double res2 = 0, b2max = 0;
 	for (int i=0;i<m;i++){ double s2 = -b2[i]; for (int j=0;j<m;j++) s2 += M[(size_t)i*m+j]*x2[j]; res2 = std::max(res2, fabs(s2)); b2max = std::max(b2max, fabs(b2[i])); }
 	printf("refinement-solve residual %.3g (|b| %.3g)\n", res2, b2max);
-	return res2 < 1e-9 * b2max ? 0 : 1;
+	if (!(res2 < 1e-9 * b2max)) return 1;
+	// single-workgroup walk streams (k_corner_walk): forward then back over b2 in stream order; every entry's vector
+	// segment must be final when read (forward: column k < J solved; back: column I > J solved), every head's tile formed
+	{
+		std::vector<double> xw(p.ld, 0.0);
+		for (int R = 0; R < p.ld; R++) { int rn = p.row_node[R]; xw[R] = rn >= 0 ? b2[6*(rn>>3)+(rn&7)] : 0.0; }
+		for (int dir = 0; dir < 2; dir++) {
+			const auto& st = dir == 0 ? p.walk_fwd : p.walk_back;
+			std::vector<char> solved(T, 0);
+			std::vector<double> acc(TILE, 0.0);
+			for (const int4& e : st) {
+				const double* tl = e.x == 0 ? tile(e.y) : e.x == 1 ? &minv[(size_t)e.y*TE] : &ldiag[(size_t)e.y*TE];
+				if (e.w < 0) {
+					const int K = e.z / TILE;
+					if (!solved[K]) { printf("WALK reads an unsolved segment %d\n", K); return 1; }
+					for (int r = 0; r < TILE; r++) for (int c = 0; c < TILE; c++) {
+						if (dir == 0) acc[r] += tl[r*TILE+c]*xw[e.z+c]; else acc[c] += tl[r*TILE+c]*xw[e.z+r]; }
+					continue;
+				}
+				const int J = e.y;
+				if (e.x == 1 && inv_launch[J] < 0) { printf("WALK head inverse never formed: %d\n", J); return 1; }
+				std::vector<double> z(TILE); for (int i=0;i<TILE;i++) z[i] = xw[J*TILE+i] - acc[i];
+				if (e.x == 1) { for (int i=0;i<TILE;i++){ double v=0; for (int k=0;k<TILE;k++) v += (dir==0 ? tl[i*TILE+k] : tl[k*TILE+i]) * z[k]; xw[J*TILE+i] = v; } }
+				else if (dir == 0) { for (int i=0;i<TILE;i++){ double v=z[i]; for (int k=0;k<i;k++) v -= tl[i*TILE+k]*xw[J*TILE+k]; xw[J*TILE+i] = v/tl[i*TILE+i]; } }
+				else { for (int i=TILE-1;i>=0;i--){ double v=z[i]; for (int k=i+1;k<TILE;k++) v -= tl[k*TILE+i]*xw[J*TILE+k]; xw[J*TILE+i] = v/tl[i*TILE+i]; } }
+				solved[J] = 1;
+				std::fill(acc.begin(), acc.end(), 0.0);
+			}
+			for (int J = 0; J < T; J++) if (!solved[J]) { printf("WALK never solved column %d\n", J); return 1; }
+		}
+		std::vector<double> xw_nat(m, 0.0);
+		for (int R = 0; R < p.ld; R++) { int rn = p.row_node[R]; if (rn >= 0) xw_nat[6*(rn>>3)+(rn&7)] = xw[R]; }
+		double res3 = 0;
+		for (int i=0;i<m;i++){ double s3 = -b2[i]; for (int j=0;j<m;j++) s3 += M[(size_t)i*m+j]*xw_nat[j]; res3 = std::max(res3, fabs(s3)); }
+		printf("walk-solve residual %.3g\n", res3);
+		if (!(res3 < 1e-9 * b2max)) return 1;
+	}
+	return 0;
 }
