@@ -359,6 +359,89 @@ __device__ __forceinline__ void arrow_update_node(int n, const float (&xl)[6], c
 		for (int c = 0; c < 3; c++) ns[6 + 3 * r + c] = (R[3 * r] * dR[c] + R[3 * r + 1] * dR[3 + c]) + R[3 * r + 2] * dR[6 + c];
 }
 
+// 6 x 6 blocks as nine float4, 6-vectors as three float2 (the same products and sums as element-wise loads)
+__device__ __forceinline__ void load36(const float* src, float (&dst)[36]) {
+	const float4* s4 = reinterpret_cast<const float4*>(src);
+#pragma unroll
+	for (int q = 0; q < 9; q++) {
+		const float4 v = s4[q];
+		dst[4 * q] = v.x;
+		dst[4 * q + 1] = v.y;
+		dst[4 * q + 2] = v.z;
+		dst[4 * q + 3] = v.w;
+	}
+}
+__device__ __forceinline__ void load6(const float* src, float (&dst)[6]) {
+	const float2* x2 = reinterpret_cast<const float2*>(src);
+#pragma unroll
+	for (int q = 0; q < 3; q++) {
+		const float2 v = x2[q];
+		dst[2 * q] = v.x;
+		dst[2 * q + 1] = v.y;
+	}
+}
+
+// stem row i of the back substitution: x_i = D_i^-1 (b_i - sum over its edges e = (i, j) of B_e x_j) in float, edges in
+// CSR order (the one arithmetic every caller shares, so a recomputation is bit-identical)
+__device__ __forceinline__ void stem_solve(int i, const float* __restrict__ dinv, const int* __restrict__ edge_offsets, const int* __restrict__ edge_list,
+                                           const int32_t* __restrict__ edges, const float* __restrict__ wing, const float* __restrict__ rhs,
+                                           const float* __restrict__ x, float (&o)[6]) {
+	float r6[6];
+	for (int c = 0; c < 6; c++) r6[c] = rhs[6 * static_cast<int64_t>(i) + c];
+	for (int ei = edge_offsets[i]; ei < edge_offsets[i + 1]; ei++) {
+		const int e = edge_list[ei];
+		const int j = edges[2 * e + 1];
+		float B[36], xj[6];
+		load36(wing + static_cast<int64_t>(e) * 36, B);
+		load6(x + 6 * static_cast<int64_t>(j), xj);
+#pragma unroll
+		for (int r = 0; r < 6; r++) {
+			float acc = 0.f;
+#pragma unroll
+			for (int k = 0; k < 6; k++) acc += B[6 * r + k] * xj[k];
+			r6[r] -= acc;
+		}
+	}
+	float D[36];
+	load36(dinv + static_cast<int64_t>(i) * 36, D);
+#pragma unroll
+	for (int r = 0; r < 6; r++) {
+		float acc = 0.f;
+#pragma unroll
+		for (int k = 0; k < 6; k++) acc += D[6 * r + k] * r6[k];
+		o[r] = acc;
+	}
+}
+
+// residual of stem row i, rhs_i - D_i x_i - sum over its edges of B_e x_j, the products and sums in double, rounded once
+// (D_i: the prepared diagonal block with LM; stem nodes couple to corner nodes only)
+__device__ __forceinline__ void stem_residual(int i, const float (&xi)[6], const float* __restrict__ diag, const int* __restrict__ edge_offsets,
+                                              const int* __restrict__ edge_list, const int32_t* __restrict__ edges, const float* __restrict__ wing,
+                                              const float* __restrict__ rhs, const float* __restrict__ x, float (&res)[6]) {
+	double r[6];
+	float D[36];
+	load36(diag + static_cast<int64_t>(i) * 36, D);
+#pragma unroll
+	for (int c = 0; c < 6; c++) {
+		double s = static_cast<double>(rhs[6 * static_cast<int64_t>(i) + c]);
+#pragma unroll
+		for (int k = 0; k < 6; k++) s -= static_cast<double>(D[6 * c + k]) * static_cast<double>(xi[k]);
+		r[c] = s;
+	}
+	for (int ei = edge_offsets[i]; ei < edge_offsets[i + 1]; ei++) {
+		const int e = edge_list[ei];
+		float B[36], xj[6];
+		load36(wing + static_cast<int64_t>(e) * 36, B);
+		load6(x + 6 * static_cast<int64_t>(edges[2 * e + 1]), xj);
+#pragma unroll
+		for (int c = 0; c < 6; c++)
+#pragma unroll
+			for (int k = 0; k < 6; k++) r[c] -= static_cast<double>(B[6 * c + k]) * static_cast<double>(xj[k]);
+	}
+#pragma unroll
+	for (int c = 0; c < 6; c++) res[c] = static_cast<float>(r[c]);
+}
+
 // threads [0, n0): stem back substitution (and, with node_state, that node's update from the x it just formed);
 // threads [n0, n_update): the corner nodes' updates from the corner solve's x (node_state non-null only).
 // x_base (refinement pass): x holds the correction d (rhs = the residual); the solution is x_base + d, written to x_base
@@ -382,50 +465,8 @@ __global__ void k_arrow_back(int n0, int n_update, const float* __restrict__ din
 		}
 		return;
 	}
-	float r6[6];
-	for (int c = 0; c < 6; c++) r6[c] = rhs[6 * static_cast<int64_t>(i) + c];
-	// 6 x 6 blocks as nine float4, 6-vectors as three float2 (the same products and sums as element-wise loads)
-	auto load36 = [](const float* src, float (&dst)[36]) {
-		const float4* s4 = reinterpret_cast<const float4*>(src);
-#pragma unroll
-		for (int q = 0; q < 9; q++) {
-			const float4 v = s4[q];
-			dst[4 * q] = v.x;
-			dst[4 * q + 1] = v.y;
-			dst[4 * q + 2] = v.z;
-			dst[4 * q + 3] = v.w;
-		}
-	};
-	for (int ei = edge_offsets[i]; ei < edge_offsets[i + 1]; ei++) {
-		const int e = edge_list[ei];
-		const int j = edges[2 * e + 1];
-		float B[36], xj[6];
-		load36(wing + static_cast<int64_t>(e) * 36, B);
-		const float2* x2 = reinterpret_cast<const float2*>(x + 6 * static_cast<int64_t>(j));
-#pragma unroll
-		for (int q = 0; q < 3; q++) {
-			const float2 v = x2[q];
-			xj[2 * q] = v.x;
-			xj[2 * q + 1] = v.y;
-		}
-#pragma unroll
-		for (int r = 0; r < 6; r++) {
-			float acc = 0.f;
-#pragma unroll
-			for (int k = 0; k < 6; k++) acc += B[6 * r + k] * xj[k];
-			r6[r] -= acc;
-		}
-	}
-	float D[36];
-	load36(dinv + static_cast<int64_t>(i) * 36, D);
 	float o[6];
-#pragma unroll
-	for (int r = 0; r < 6; r++) {
-		float acc = 0.f;
-#pragma unroll
-		for (int k = 0; k < 6; k++) acc += D[6 * r + k] * r6[k];
-		o[r] = acc;
-	}
+	stem_solve(i, dinv, edge_offsets, edge_list, edges, wing, rhs, x, o);
 	float2* xo = reinterpret_cast<float2*>(x + 6 * static_cast<int64_t>(i));
 #pragma unroll
 	for (int q = 0; q < 3; q++) xo[q] = make_float2(o[2 * q], o[2 * q + 1]);
@@ -438,78 +479,93 @@ __global__ void k_arrow_back(int n0, int n_update, const float* __restrict__ din
 	if (node_state) arrow_update_node(i, o, state_in, node_state, updates_out);
 }
 
-// ---- iterative refinement: res = rhs - H x with the sums in double (H = the prepared diagonal blocks, with LM, and the
-// wing blocks at (i, j) and, transposed, at (j, i)); 32 lanes per node: lane q < 30 takes row q % 6 of every fifth of the
-// node's incidences (CSR, ascending edge order), the five partials of a row are then added in slot order ----
-__global__ __launch_bounds__(256) void k_arrow_residual(int N, const float* __restrict__ diag, const int* __restrict__ inc_off,
-                                                        const int* __restrict__ inc_list, const int32_t* __restrict__ edges,
-                                                        const float* __restrict__ wing, const float* __restrict__ rhs, const float* __restrict__ x,
-                                                        float* __restrict__ res) {
-	const int n = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 5);
-	const int q = static_cast<int>(threadIdx.x & 31);
-	if (n >= N) return;   // uniform per 32-lane node group
-	const int c = q % 6, slot = q / 6;   // slot 5: lanes 30, 31 idle in the loop
-	double s = 0.0;
-	if (slot < 5) {
-		for (int u = inc_off[n] + slot; u < inc_off[n + 1]; u += 5) {
-			const int code = inc_list[u];
-			const int e = code >> 1;
-			const bool tgt = code & 1;   // node is the edge's target: row c of B^T, i.e. column c of B, times x_source
-			const int other = edges[2 * e + (tgt ? 0 : 1)];
-			const float* B = wing + static_cast<int64_t>(e) * 36;
-			const float* xo = x + 6 * static_cast<int64_t>(other);
+// ---- iterative refinement, after the corner solve (x_C in x): one launch forms
+//   threads [0, n0) (stem rows): x_i (stem_solve) -> x, and the residual r_i = b_i - H_i x (double sums) -> res;
+//   waves of the last workgroups, one per corner node a: the corner right-hand side of the correction,
+//     rhs2[perm(a)] = r_a - sum over stem edges i -> a of (D_i^-1 B_ia)^T r_i,
+//   with r_a = b_a - D_a x_a - sum over a's incidences of the wing blocks (B^T x_i for stem edges, B x_b / B^T x_b for
+//   corner edges) in double; the stem rows x_i and r_i it needs are recomputed here with the stem threads' own
+//   arithmetic (bit-identical), so nothing waits on another workgroup ----
+__global__ __launch_bounds__(256) void k_refine_prepare(int n0, int nc, int stem_blocks, const float* __restrict__ dinv,
+                                                        const float* __restrict__ dinv_b, const float* __restrict__ diag,
+                                                        const int* __restrict__ edge_offsets, const int* __restrict__ edge_list,
+                                                        const int* __restrict__ inc_off, const int* __restrict__ inc_list,
+                                                        const int32_t* __restrict__ edges, const float* __restrict__ wing,
+                                                        const float* __restrict__ rhs, float* __restrict__ x, float* __restrict__ res,
+                                                        const int* __restrict__ node_row, float* __restrict__ rhs2) {
+	if (static_cast<int>(blockIdx.x) < stem_blocks) {
+		const int i = blockIdx.x * blockDim.x + threadIdx.x;
+		if (i >= n0) return;
+		float xi[6], ri[6];
+		stem_solve(i, dinv, edge_offsets, edge_list, edges, wing, rhs, x, xi);
+		stem_residual(i, xi, diag, edge_offsets, edge_list, edges, wing, rhs, x, ri);
+		float2* xo = reinterpret_cast<float2*>(x + 6 * static_cast<int64_t>(i));
+		float2* ro = reinterpret_cast<float2*>(res + 6 * static_cast<int64_t>(i));
 #pragma unroll
-			for (int k = 0; k < 6; k++) s += static_cast<double>(tgt ? B[6 * k + c] : B[6 * c + k]) * static_cast<double>(xo[k]);
+		for (int q = 0; q < 3; q++) {
+			xo[q] = make_float2(xi[2 * q], xi[2 * q + 1]);
+			ro[q] = make_float2(ri[2 * q], ri[2 * q + 1]);
 		}
+		return;
 	}
-	// partials of row c sit in lanes c, c + 6, c + 12, c + 18, c + 24 (width-32 groups)
-	double t = s;
-#pragma unroll
-	for (int k = 1; k < 5; k++) t += __shfl(s, c + 6 * k, 32);
-	if (q < 6) {
-		const float* D = diag + static_cast<int64_t>(n) * 36;
-		const float* xn = x + 6 * static_cast<int64_t>(n);
-		double dx = 0.0;
-#pragma unroll
-		for (int k = 0; k < 6; k++) dx += static_cast<double>(D[6 * q + k]) * static_cast<double>(xn[k]);
-		res[6 * static_cast<int64_t>(n) + q] = static_cast<float>((static_cast<double>(rhs[6 * static_cast<int64_t>(n) + q]) - dx) - t);
-	}
-}
-
-// ---- refinement's corner right-hand side: rhs2[perm(a)] = r_a - sum over stem edges i->a of (D_i^-1 B_ia)^T r_i (one wave
-// per corner node, as stem_rhs_wave) ----
-__global__ __launch_bounds__(256) void k_refine_corner_rhs(int nc, int n0, const int* __restrict__ rhs_off, const int* __restrict__ rhs_edges,
-                                                           const int32_t* __restrict__ edges, const float* __restrict__ dinv_b,
-                                                           const float* __restrict__ res, const int* __restrict__ node_row, float* __restrict__ rhs2) {
-	const int a = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
+	const int a = static_cast<int>(((static_cast<int64_t>(blockIdx.x) - stem_blocks) * blockDim.x + threadIdx.x) >> 6);
 	const int lane = static_cast<int>(threadIdx.x & 63);
 	if (a >= nc) return;
-	float s[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-	for (int q = rhs_off[a] + lane; q < rhs_off[a + 1]; q += 64) {
-		const int e = rhs_edges[q];
-		const int i = edges[2 * e];
-		const float* Y = dinv_b + static_cast<int64_t>(e) * 36;
-		const float* g = res + 6 * static_cast<int64_t>(i);
-		float gk[6];
+	const int n = n0 + a;
+	double ra[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};   // this lane's share of sum H_an x_n over a's incidences
+	float s2[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};    // this lane's share of sum (D_i^-1 B_ia)^T r_i
+	for (int u = inc_off[n] + lane; u < inc_off[n + 1]; u += 64) {
+		const int code = inc_list[u];
+		const int e = code >> 1;
+		const bool tgt = code & 1;
+		const int other = edges[2 * e + (tgt ? 0 : 1)];
+		float B[36], xo[6];
+		load36(wing + static_cast<int64_t>(e) * 36, B);
+		if (other < n0) {   // stem edge other -> n (n is its target): x_other and r_other recomputed
+			float ri[6];
+			stem_solve(other, dinv, edge_offsets, edge_list, edges, wing, rhs, x, xo);
+			stem_residual(other, xo, diag, edge_offsets, edge_list, edges, wing, rhs, x, ri);
+			float Y[36];
+			load36(dinv_b + static_cast<int64_t>(e) * 36, Y);
 #pragma unroll
-		for (int k = 0; k < 6; k++) gk[k] = g[k];
+			for (int c = 0; c < 6; c++) {
+				float t = 0.f;
 #pragma unroll
-		for (int c = 0; c < 6; c++) {
-			float t = 0.f;
-#pragma unroll
-			for (int k = 0; k < 6; k++) t += Y[6 * k + c] * gk[k];
-			s[c] += t;
+				for (int k = 0; k < 6; k++) t += Y[6 * k + c] * ri[k];
+				s2[c] += t;
+			}
+		} else {
+			load6(x + 6 * static_cast<int64_t>(other), xo);
 		}
+#pragma unroll
+		for (int c = 0; c < 6; c++)
+#pragma unroll
+			for (int k = 0; k < 6; k++) ra[c] += static_cast<double>(tgt ? B[6 * k + c] : B[6 * c + k]) * static_cast<double>(xo[k]);
 	}
 #pragma unroll
 	for (int c = 0; c < 6; c++)
 #pragma unroll
-		for (int off = 32; off > 0; off >>= 1) s[c] += __shfl_xor(s[c], off);
+		for (int off = 32; off > 0; off >>= 1) {
+			ra[c] += __shfl_xor(ra[c], off);
+			s2[c] += __shfl_xor(s2[c], off);
+		}
 	if (lane < 6) {
-		float v = s[0];
+		double r = 0.0, t = 0.0;
+		float u = 0.f;
 #pragma unroll
-		for (int c = 1; c < 6; c++) v = lane == c ? s[c] : v;
-		rhs2[node_row[a] + lane] = res[6 * static_cast<int64_t>(n0 + a) + lane] - v;
+		for (int c = 0; c < 6; c++)
+			if (lane == c) {
+				t = ra[c];
+				u = s2[c];
+			}
+		float xa[6], Da[6];
+		load6(x + 6 * static_cast<int64_t>(n), xa);
+#pragma unroll
+		for (int k = 0; k < 6; k++) Da[k] = diag[static_cast<int64_t>(n) * 36 + 6 * lane + k];
+		r = static_cast<double>(rhs[6 * static_cast<int64_t>(n) + lane]);
+#pragma unroll
+		for (int k = 0; k < 6; k++) r -= static_cast<double>(Da[k]) * static_cast<double>(xa[k]);
+		rhs2[node_row[a] + lane] = static_cast<float>(r - t) - u;
 	}
 }
 
@@ -548,30 +604,38 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 		if (st) return st;
 	}
 	const bool refine = ws.refine && ws.inc_off && ws.res && ws.dx;
-	// with node_state, the node updates ride along (all N nodes) in the last back-substitution launch
-	const int threads = node_state && !refine ? ws.N : ws.n0;
-	if (threads > 0) {
-		k_arrow_back<<<static_cast<unsigned>(ceil_div(threads, 64)), 64, 0, stream>>>(ws.n0, threads, ws.dinv, ws.edge_offsets, ws.edge_list, edges,
-		                                                                             wing, ws.rhs, ws.x, state_in, refine ? nullptr : node_state,
-		                                                                             updates_out, nullptr);
-		NNRT_LAUNCH_CHECK();
+	if (!refine) {
+		// with node_state, the node updates ride along (all N nodes) in the back-substitution launch
+		const int threads = node_state ? ws.N : ws.n0;
+		if (threads > 0) {
+			k_arrow_back<<<static_cast<unsigned>(ceil_div(threads, 64)), 64, 0, stream>>>(ws.n0, threads, ws.dinv, ws.edge_offsets, ws.edge_list, edges,
+			                                                                             wing, ws.rhs, ws.x, state_in, node_state, updates_out, nullptr);
+			NNRT_LAUNCH_CHECK();
+		}
+		return NNRT_OK;
 	}
-	if (!refine) return NNRT_OK;
-	// one step of iterative refinement: res = rhs - H x (double sums), H d = res with the same factors, x += d
-	k_arrow_residual<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ws.N) * 32, 256)), 256, 0, stream>>>(
-	    ws.N, ws.diag, ws.inc_off, ws.inc_list, edges, wing, ws.rhs, ws.x, ws.res);
-	NNRT_LAUNCH_CHECK();
+	// one step of iterative refinement: x_D and the residual res = rhs - H x (double sums) with the correction's corner
+	// right-hand side in one launch, H d = res with the same factors (the corner: one forward + back walk), x += d
+	{
+		const int nc = m / 6;
+		const int stem_blocks = static_cast<int>(ceil_div(ws.n0, 256));
+		const int corner_blocks = static_cast<int>(ceil_div(static_cast<int64_t>(nc) * 64, 256));
+		float* rhs2 = m > 0 ? ws.corner->refine_rhs() : nullptr;
+		const int* node_row = m > 0 ? ws.corner->map().node_row : nullptr;
+		if (stem_blocks + corner_blocks > 0) {
+			k_refine_prepare<<<static_cast<unsigned>(stem_blocks + corner_blocks), 256, 0, stream>>>(
+			    ws.n0, nc, stem_blocks, ws.dinv, ws.dinv_b, ws.diag, ws.edge_offsets, ws.edge_list, ws.inc_off, ws.inc_list, edges, wing, ws.rhs,
+			    ws.x, ws.res, node_row, rhs2);
+			NNRT_LAUNCH_CHECK();
+		}
+	}
 	if (m > 0) {
-		const CornerMap cm = ws.corner->map();
-		k_refine_corner_rhs<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(m / 6) * 64, 256)), 256, 0, stream>>>(
-		    m / 6, ws.n0, ws.rhs_off, ws.rhs_edges, edges, ws.dinv_b, ws.res, cm.node_row, ws.corner->refine_rhs());
-		NNRT_LAUNCH_CHECK();
 		nnrt_status st = ws.corner->launch_resolve(ws.dx + 6 * static_cast<int64_t>(ws.n0), stream);
 		if (st) return st;
 	}
 	// every node: x += d (and, with node_state, the update)
 	k_arrow_back<<<static_cast<unsigned>(ceil_div(ws.N, 64)), 64, 0, stream>>>(ws.n0, ws.N, ws.dinv, ws.edge_offsets, ws.edge_list, edges,
-	                                                                              wing, ws.res, ws.dx, state_in, node_state, updates_out, ws.x);
+	                                                                          wing, ws.res, ws.dx, state_in, node_state, updates_out, ws.x);
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;
 }
