@@ -19,12 +19,12 @@ namespace nnrt {
 // 32 lanes per node: lane q < 21 owns upper-triangle entry q of the 6x6 block, lanes 21..26 the gradient. The ARAP
 // terms (ComputeBlockSums of dEi^T dEi / dEj^T dEj and J^T e, ArapHessianImpl.h / DeformableMeshToImageFitterImpl.h)
 // are gathered from the node's incident edges (CSR, ascending edge order; entry = 2 e + (node is the edge's target)).
-__global__ __launch_bounds__(256) void k_arrow_prepare(int N, float lm, double* __restrict__ acc, const int* __restrict__ inc_off,
-                                                       const int* __restrict__ inc_list, const float* __restrict__ edge_terms, float* __restrict__ diag,
-                                                       float* __restrict__ rhs, float* __restrict__ gradient_out, float* __restrict__ hessian_out) {
-	const int n = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 5);
-	const int q = static_cast<int>(threadIdx.x & 31);
-	if (n >= N) return;   // uniform per 32-lane node group
+// lane q of node n's 32-lane group: the node's prepared entry (q < 21: diagonal-block entry (r0, c0), r0 <= c0, with LM
+// -> *dv; 21 <= q < 27: right-hand side entry q - 21 -> *dv), its global outputs written; false for lanes q >= 27
+__device__ __forceinline__ bool prepare_node(int n, int q, float lm, double* __restrict__ acc, const int* __restrict__ inc_off,
+                                             const int* __restrict__ inc_list, const float* __restrict__ edge_terms, float* __restrict__ diag,
+                                             float* __restrict__ rhs, float* __restrict__ gradient_out, float* __restrict__ hessian_out, int& r0,
+                                             int& c0, float& dv) {
 	// the term this lane sums from a source incidence / a target incidence (-1: none)
 	const int q_src = q < 27 ? q : -1;
 	const int q_tgt = (q == 15 || q == 18 || q == 20) ? 27 : (q >= 24 && q < 27) ? 28 + (q - 24) : -1;
@@ -47,8 +47,8 @@ __global__ __launch_bounds__(256) void k_arrow_prepare(int N, float lm, double* 
 		for (int u = 0; u < 32; u++)
 			if (u < nu) arap += v[u];
 	}
-	if (q >= 27) return;
-	int r0 = 0, c0 = 0;   // upper-triangle enumeration of entry q (q < 21)
+	if (q >= 27) return false;
+	r0 = 0;   // upper-triangle enumeration of entry q (q < 21)
 	{
 		int qq = q;
 		while (r0 < 6 && qq >= 6 - r0) {
@@ -69,47 +69,27 @@ __global__ __launch_bounds__(256) void k_arrow_prepare(int N, float lm, double* 
 			hessian_out[static_cast<int64_t>(n) * 36 + 6 * r0 + c0] = hd;
 			hessian_out[static_cast<int64_t>(n) * 36 + 6 * c0 + r0] = hd;
 		}
+		dv = v;
 	} else {
 		const float g = (0.f - static_cast<float>(hq)) - arap;
 		rhs[6 * static_cast<int64_t>(n) + q - 21] = g;
 		gradient_out[6 * static_cast<int64_t>(n) + q - 21] = g;
+		dv = g;
 	}
+	return true;
 }
 
 // ---- stem: D^-1 and D^-1 B per stem node, four lanes per node (each forms D^-1 with the same arithmetic and the products
 // of every fourth of the node's edges), in one launch with the corner init (the last init_blocks blocks: corner.hip's
 // corner_init_thread; both read the prepared diagonal blocks and write disjoint outputs) ----
 constexpr int STEM_LANES = 4;
-__global__ __launch_bounds__(256) void k_init_stem(CornerInitArgs ia, int init_blocks, const float* __restrict__ rhs, int n0,
-                                                   const float* __restrict__ diag, const int* __restrict__ edge_offsets,
-                                                   const int* __restrict__ edge_list, const float* __restrict__ wing, float* __restrict__ dinv,
-                                                   float* __restrict__ dinv_b, int* error_flag) {
-	// the stem's blocks come first: their dependent chains (Cholesky, inverse, D^-1 B) start with the launch while the
-	// corner-init blocks (independent stores) fill the rest of the machine behind them
-	const int stem_blocks = static_cast<int>(gridDim.x) - init_blocks;
-	if (static_cast<int>(blockIdx.x) >= stem_blocks) {
-		corner_init_thread(static_cast<int64_t>(blockIdx.x - stem_blocks) * blockDim.x + threadIdx.x, ia, diag, rhs);
-		return;
-	}
-	const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-	const int i = static_cast<int>(t / STEM_LANES), sub = static_cast<int>(t % STEM_LANES);
-	if (i >= n0) return;
-	// 6 x 6 blocks are 144 B = nine 16-B words: loaded and stored as float4
+// stem node i, lane sub of its STEM_LANES: Cholesky of the prepared block f (potrf semantics: a failure sets the error
+// flag), D_i^-1 (lane 0 stores it) and D_i^-1 B_e for every STEM_LANES-th of its edges
+__device__ __forceinline__ void stem_factor(int i, int sub, const float (&f)[36], const int* __restrict__ edge_offsets, const int* __restrict__ edge_list,
+                                            const float* __restrict__ wing, float* __restrict__ dinv, float* __restrict__ dinv_b, int* error_flag) {
 	float L[6][6];
-	{
-		const float4* d4 = reinterpret_cast<const float4*>(diag + static_cast<int64_t>(i) * 36);
-		float f[36];
 #pragma unroll
-		for (int q = 0; q < 9; q++) {
-			const float4 v = d4[q];
-			f[4 * q] = v.x;
-			f[4 * q + 1] = v.y;
-			f[4 * q + 2] = v.z;
-			f[4 * q + 3] = v.w;
-		}
-#pragma unroll
-		for (int k = 0; k < 36; k++) L[k / 6][k % 6] = f[k];
-	}
+	for (int k = 0; k < 36; k++) L[k / 6][k % 6] = f[k];
 	if (!cholesky_small<6>(L)) {
 		if (sub == 0) atomicOr(error_flag, 1);
 		return;
@@ -148,6 +128,122 @@ __global__ __launch_bounds__(256) void k_init_stem(CornerInitArgs ia, int init_b
 		float4* Y4 = reinterpret_cast<float4*>(dinv_b + static_cast<int64_t>(e) * 36);
 #pragma unroll
 		for (int q = 0; q < 9; q++) Y4[q] = make_float4(Y[4 * q], Y[4 * q + 1], Y[4 * q + 2], Y[4 * q + 3]);
+	}
+}
+
+__global__ __launch_bounds__(256) void k_init_stem(CornerInitArgs ia, int init_blocks, const float* __restrict__ rhs, int n0,
+                                                   const float* __restrict__ diag, const int* __restrict__ edge_offsets,
+                                                   const int* __restrict__ edge_list, const float* __restrict__ wing, float* __restrict__ dinv,
+                                                   float* __restrict__ dinv_b, int* error_flag) {
+	// the stem's blocks come first: their dependent chains (Cholesky, inverse, D^-1 B) start with the launch while the
+	// corner-init blocks (independent stores) fill the rest of the machine behind them
+	const int stem_blocks = static_cast<int>(gridDim.x) - init_blocks;
+	if (static_cast<int>(blockIdx.x) >= stem_blocks) {
+		corner_init_thread(static_cast<int64_t>(blockIdx.x - stem_blocks) * blockDim.x + threadIdx.x, ia, diag, rhs);
+		return;
+	}
+	const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	const int i = static_cast<int>(t / STEM_LANES), sub = static_cast<int>(t % STEM_LANES);
+	if (i >= n0) return;
+	// 6 x 6 blocks are 144 B = nine 16-B words: loaded and stored as float4
+	float f[36];
+	{
+		const float4* d4 = reinterpret_cast<const float4*>(diag + static_cast<int64_t>(i) * 36);
+#pragma unroll
+		for (int q = 0; q < 9; q++) {
+			const float4 v = d4[q];
+			f[4 * q] = v.x;
+			f[4 * q + 1] = v.y;
+			f[4 * q + 2] = v.z;
+			f[4 * q + 3] = v.w;
+		}
+	}
+	stem_factor(i, sub, f, edge_offsets, edge_list, wing, dinv, dinv_b, error_flag);
+}
+
+// ---- the fitter's prepare + stem + corner init in one launch (the per-node prepare, k_init_stem and the corner init read and
+// write disjoint data once the prepared blocks stay inside the workgroup that forms them):
+//   blocks [0, stem_blocks): 8 stem nodes each, 32 lanes per node: prepare (prepare_node), the block through the
+//     wave's LDS to the node's first STEM_LANES lanes, which run stem_factor;
+//   blocks [stem_blocks, stem_blocks + corner_blocks): 8 corner nodes each: prepare, and the node's diagonal block into
+//     its stored corner tiles (every stored position, both triangles, as the corner init writes them) with its
+//     right-hand side into cb;
+//   the rest: the corner init of every other tile entry (zeros, identity on the padding) and the padding rows of cb.
+// The data term (acc) is consumed and re-zeroed here, as the separate prepare launch did (round 3). ----
+__global__ __launch_bounds__(256) void k_prepare_stem_init(int n0, int N, int stem_blocks, int corner_blocks, float lm, double* __restrict__ acc,
+                                                           const int* __restrict__ inc_off, const int* __restrict__ inc_list,
+                                                           const float* __restrict__ edge_terms, float* __restrict__ diag, float* __restrict__ rhs,
+                                                           float* __restrict__ gradient_out, float* __restrict__ hessian_out,
+                                                           const int* __restrict__ edge_offsets, const int* __restrict__ edge_list,
+                                                           const float* __restrict__ wing, float* __restrict__ dinv, float* __restrict__ dinv_b,
+                                                           int* error_flag, CornerInitArgs ia, CornerMap cm) {
+	__shared__ float s_blk[8][36];
+	const int b = static_cast<int>(blockIdx.x);
+	if (b >= stem_blocks + corner_blocks) {   // corner init of the entries no corner-node group writes
+		constexpr int TL = CORNER_NB, TE = CORNER_NB * CORNER_NB;
+		const int64_t idx = static_cast<int64_t>(b - stem_blocks - corner_blocks) * blockDim.x + threadIdx.x;
+		if (idx < ia.ld && ia.row_node[idx] < 0) ia.cb[idx] = 0.f;
+		if (idx >= static_cast<int64_t>(ia.slots) * (TE / 4)) return;
+		const int sl = static_cast<int>(idx / (TE / 4)), w = static_cast<int>(idx % (TE / 4));
+		const int r = w / (TL / 4), c0 = (w % (TL / 4)) * 4;
+		const int2 ij = ia.slot_ij[sl];
+		const int R = ij.x * TL + r;
+		const int rn = ia.row_node[R];
+		float v[4];
+		bool own[4], any = false;
+#pragma unroll
+		for (int j = 0; j < 4; j++) {
+			const int C = ij.y * TL + c0 + j;
+			const int cn = ia.row_node[C];
+			own[j] = rn >= 0 && cn >= 0 && (rn >> 3) == (cn >> 3);   // a node's diagonal block: its group writes it
+			v[j] = (rn < 0 || cn < 0) && R == C ? 1.f : 0.f;
+			any |= own[j];
+		}
+		float* dst = ia.tiles + static_cast<int64_t>(sl) * TE + r * TL + c0;
+		if (!any) {
+			*reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+		} else {
+#pragma unroll
+			for (int j = 0; j < 4; j++)
+				if (!own[j]) dst[j] = v[j];
+		}
+		return;
+	}
+	const bool stem = b < stem_blocks;
+	const int g = static_cast<int>(threadIdx.x >> 5), q = static_cast<int>(threadIdx.x & 31);
+	const int n = stem ? b * 8 + g : n0 + (b - stem_blocks) * 8 + g;
+	if (n >= (stem ? n0 : N)) return;   // uniform per 32-lane node group
+	int r0 = 0, c0 = 0;
+	float dv = 0.f;
+	const bool has = prepare_node(n, q, lm, acc, inc_off, inc_list, edge_terms, diag, rhs, gradient_out, hessian_out, r0, c0, dv);
+	if (stem) {
+		if (has && q < 21) {
+			s_blk[g][6 * r0 + c0] = dv;
+			s_blk[g][6 * c0 + r0] = dv;
+		}
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_wave_barrier();   // the node's 32 lanes share a wave: LDS is in order within it
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		if (q < STEM_LANES) {
+			float f[36];
+#pragma unroll
+			for (int k = 0; k < 36; k++) f[k] = s_blk[g][k];
+			stem_factor(n, q, f, edge_offsets, edge_list, wing, dinv, dinv_b, error_flag);
+		}
+		return;
+	}
+	if (!has) return;
+	const int a = n - n0, row = cm.node_row[a];
+	if (q < 21) {   // entry (r0, c0) and its mirror wherever their tile is stored
+		const int R0 = row + r0, C0 = row + c0;
+#pragma unroll
+		for (int k = 0; k < 2; k++) {
+			const int R = k ? C0 : R0, C = k ? R0 : C0;
+			const int slot = cm.tile_slot[static_cast<int64_t>(R / CORNER_NB) * cm.T + C / CORNER_NB];
+			if (slot >= 0) cm.tiles[static_cast<int64_t>(slot) * (CORNER_NB * CORNER_NB) + (R % CORNER_NB) * CORNER_NB + (C % CORNER_NB)] = dv;
+		}
+	} else {
+		ia.cb[row + q - 21] = dv;
 	}
 }
 
@@ -570,11 +666,16 @@ __global__ __launch_bounds__(256) void k_refine_prepare(int n0, int nc, int stem
 }
 
 nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* edges, const float* wing, int* error_flag, hipStream_t stream,
-                                 bool arap_wings, float* node_state, float* updates_out, const float* state_in) {
+                                 bool arap_wings, float* node_state, float* updates_out, const float* state_in, bool init_done) {
 	const int m = ws.m;
 	if (!state_in) state_in = node_state;
 	NNRT_CHECK_ARG(m == 0 || ws.corner, "arrowhead workspace without a corner plan");
-	if (ws.n0 > 0 || m > 0) {   // corner init and stem in one launch
+	if (init_done) {   // the stem and corner init ran inside the caller's prepare launch
+		if (m > 0) {
+			nnrt_status st = ws.corner->launch_offdiag(ws.n0, edges, wing, stream);   // >= 3 layers: after the init
+			if (st) return st;
+		}
+	} else if (ws.n0 > 0 || m > 0) {   // corner init and stem in one launch
 		const CornerInitArgs ia = m > 0 ? ws.corner->init_args(ws.n0) : CornerInitArgs{0, 0, 0, nullptr, nullptr, nullptr, nullptr};
 		const int init_blocks = m > 0 ? static_cast<int>(ceil_div(ia.threads(), 256)) : 0;
 		const int stem_blocks = static_cast<int>(ceil_div(static_cast<int64_t>(ws.n0) * STEM_LANES, 256));
@@ -643,10 +744,17 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 nnrt_status launch_arrowhead_iteration(const ArrowheadWorkspace& ws, const double* acc, float lm, const int32_t* edges, const float* wing,
                                        float* node_state, const float* edge_jr, float* updates_out, float* gradient_out, float* hessian_out,
                                        int* error_flag, hipStream_t stream, const float* state_in) {
-	k_arrow_prepare<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ws.N) * 32, 256)), 256, 0, stream>>>(
-	    ws.N, lm, const_cast<double*>(acc), ws.inc_off, ws.inc_list, edge_jr, ws.diag, ws.rhs, gradient_out, hessian_out);
+	// prepare (every node) + stem + corner init in one launch
+	const int stem_blocks = static_cast<int>(ceil_div(ws.n0, 8));
+	const int corner_blocks = static_cast<int>(ceil_div(ws.N - ws.n0, 8));
+	const CornerInitArgs ia = ws.m > 0 ? ws.corner->init_args(ws.n0) : CornerInitArgs{0, 0, 0, nullptr, nullptr, nullptr, nullptr};
+	const CornerMap cm = ws.m > 0 ? ws.corner->map() : CornerMap{0, nullptr, nullptr, nullptr};
+	const int init_blocks = ws.m > 0 ? static_cast<int>(ceil_div(ia.threads(), 256)) : 0;
+	k_prepare_stem_init<<<static_cast<unsigned>(stem_blocks + corner_blocks + init_blocks), 256, 0, stream>>>(
+	    ws.n0, ws.N, stem_blocks, corner_blocks, lm, const_cast<double*>(acc), ws.inc_off, ws.inc_list, edge_jr, ws.diag, ws.rhs, gradient_out,
+	    hessian_out, ws.edge_offsets, ws.edge_list, wing, ws.dinv, ws.dinv_b, error_flag, ia, cm);
 	NNRT_LAUNCH_CHECK();
-	return arrowhead_solve_core(ws, edges, wing, error_flag, stream, true, node_state, updates_out, state_in);
+	return arrowhead_solve_core(ws, edges, wing, error_flag, stream, true, node_state, updates_out, state_in, true);
 }
 
 } // namespace nnrt

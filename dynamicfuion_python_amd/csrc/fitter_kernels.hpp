@@ -340,6 +340,7 @@ nnrt_status launch_arrowhead_iteration(const ArrowheadWorkspace& ws, const doubl
 // node_state / updates_out (fitter): apply the solved increments to the node motion in the back-substitution launch;
 // state_in (default: node_state): the motion the iteration started from (a snapshot the iteration restarts from)
 nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* edges, const float* wing, int* error_flag, hipStream_t stream,
-                                 bool arap_wings = false, float* node_state = nullptr, float* updates_out = nullptr, const float* state_in = nullptr);
+                                 bool arap_wings = false, float* node_state = nullptr, float* updates_out = nullptr, const float* state_in = nullptr,
+                                 bool init_done = false);
 
 } // namespace nnrt
