@@ -1100,6 +1100,12 @@ __global__ __launch_bounds__(CT) void k_corner_fwd(CornerFwdArgs a) {
 constexpr int WT = 512;        // threads of the walk workgroup (8 waves)
 constexpr int WALK_MAX_LD = 8192;
 constexpr int WALK_MAX_ELEMS = 1024;
+// one workgroup streams every tile through one CU's load path (≈ 30-60 GB/s): the walk wins only on small corners; above
+// this many stream tiles per direction the chain launches (many CUs) take over. Measured at C5 (254 tiles per direction):
+// the walk 4 MB / ≈ 140 µs against ≈ 65 µs for the back chains (round 4)
+#ifndef NNRT_WALK_MAX_TILES
+#define NNRT_WALK_MAX_TILES 48
+#endif
 struct WalkElem {
 	const float* tile;   // 64 x 64 row-major tile
 	int x_off;           // entry: first unknown of the tile whose x (back) / y (forward) it multiplies; head: J * 64
@@ -1392,7 +1398,7 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		}
 	}
 	walk_ok = false;
-	if (p.nc > 0 && p.ld <= WALK_MAX_LD && static_cast<int>(std::max(p.walk_back.size(), p.walk_fwd.size())) <= WALK_MAX_ELEMS) {
+	if (p.nc > 0 && p.ld <= WALK_MAX_LD && static_cast<int>(std::max(p.walk_back.size(), p.walk_fwd.size())) <= std::min(WALK_MAX_ELEMS, NNRT_WALK_MAX_TILES)) {
 		// LDS: descriptors, the solution vector, the reduction rows, then a ring of as many tiles as fit (at least the
 		// largest column's elements need not fit: a column streams through the ring in parts)
 		const size_t nd = std::max(p.walk_back.size(), p.walk_fwd.size());
