@@ -537,7 +537,7 @@ def main(argv=None):
                       n0=n0, n1=Nn - n0, corner_size=6 * (Nn - n0), edges=Ee,
                       flops_formula="SURVEY.md 8(d): (6 n1)^3 / 3 + 2 (6 n1)^2 (1 + n_rhs), n_rhs = 1 (the reference's dense corner; "
                                     "the tile-sparse factorization performs fewer: plan below)",
-                      plan=ft.corner_info())
+                      plan=ft.corner_info(), refinement=ft.refine_info())
     kbytes = kernels[ROOFLINE_KERNEL]["algorithmic_bytes"]
     k_ms = ktimes[ROOFLINE_KERNEL]
     achieved = kbytes / (k_ms * 1e-3) / 1e9

@@ -1040,6 +1040,25 @@ nnrt_status nnrt_fitter_corner_info(const nnrt_fitter* ft, int64_t* h_out) {
 	return NNRT_OK;
 }
 
+nnrt_status nnrt_fitter_refine_info(nnrt_fitter* ft, float* h_out, void* stream) {
+	NNRT_CHECK_ARG(ft && h_out, "null pointer");
+	DeviceGuard guard(ft->device);
+	h_out[0] = 1.f;
+	h_out[1] = NNRT_REFINE_PIVOT_RATIO;
+	h_out[2] = 0.f;
+	if (ft->E > 0 && ft->corner.pivot_ratio()) {
+		NNRT_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+		NNRT_HIP(hipStreamSynchronize(ft->work));
+		unsigned bits = 0;
+		NNRT_HIP(hipMemcpy(&bits, ft->corner.pivot_ratio(), sizeof(bits), hipMemcpyDeviceToHost));
+		float r;
+		std::memcpy(&r, &bits, sizeof(r));
+		h_out[0] = r;
+		h_out[2] = (NNRT_ARAP_REFINE != 0 && r < NNRT_REFINE_PIVOT_RATIO) ? 1.f : 0.f;
+	}
+	return NNRT_OK;
+}
+
 int32_t nnrt_fitter_graph_count(const nnrt_fitter* ft) {
 	if (!ft) return -1;
 	int32_t n = 0;

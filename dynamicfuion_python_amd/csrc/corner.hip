@@ -687,34 +687,34 @@ struct CornerFactorArgs {
 	int n_tasks;             // workgroups [n_tasks, gridDim) invert diagonal factors of the previous level
 	const int* inv_cols;     // this launch's columns to invert
 	float* minv;             // [T, 64, 64] L_JJ^-1 (lower; zero above the diagonal)
+	const float* sdiag;      // [ld] diag(S) before the factorization (nullable)
+	unsigned* pivot_word;    // atomic minimum of pivot / diag(S) over the diagonal tasks (nullable)
 };
 
 // M = L^-1 for the 64 x 64 lower-triangular factor L (row-major, zero above the diagonal): the workgroup stages L in LDS,
-// wave 0 forms column c of M in lane c by forward substitution in double (rows in order, four partial sums per row), and
-// stores it rounded to float. The back substitution then forms x_J = L_JJ^-T z as the product M^T z.
-__device__ inline void invert_lower_tile(const float* __restrict__ L, float* __restrict__ M, float* s_l, int t) {
+// wave 0 forms column c of M in lane c by forward substitution (rows in order, the sum over earlier rows in double), its
+// column kept in LDS; M is stored rounded to float. The back substitution then forms x_J = L_JJ^-T z as the product
+// M^T z. Deliberately compact (rolled loops): these workgroups share the launch -- and instruction caches -- with the
+// panels' straight-line elimination (a fully unrolled double version made every factor launch ≈ 2 µs longer).
+__device__ inline void invert_lower_tile(const float* __restrict__ L, float* __restrict__ M, float* s_l, float* s_m, int t) {
 	const float4* L4 = reinterpret_cast<const float4*>(L);
 	for (int i = t; i < TILE_ELEMS / 4; i += CT) *reinterpret_cast<float4*>(s_l + (i >> 4) * CS4 + 4 * (i & 15)) = L4[i];
 	__syncthreads();
 	if (t >= 64) return;
 	const int c = t;
-	double m[TILE];
-#pragma unroll
+#pragma unroll 1
 	for (int r = 0; r < TILE; r++) {
-		double a[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-		for (int k4 = 0; k4 < r; k4 += 4) {
-			const float4 l = *reinterpret_cast<const float4*>(s_l + r * CS4 + k4);   // wave-uniform: LDS broadcast
-			a[0] = __builtin_fma(static_cast<double>(l.x), m[k4], a[0]);
-			if (k4 + 1 < r) a[1] = __builtin_fma(static_cast<double>(l.y), m[k4 + 1], a[1]);
-			if (k4 + 2 < r) a[2] = __builtin_fma(static_cast<double>(l.z), m[k4 + 2], a[2]);
-			if (k4 + 3 < r) a[3] = __builtin_fma(static_cast<double>(l.w), m[k4 + 3], a[3]);
+		double a0 = 0.0, a1 = 0.0;
+#pragma unroll 1
+		for (int k = 0; k + 1 < r; k += 2) {
+			a0 = __builtin_fma(static_cast<double>(s_l[r * CS4 + k]), static_cast<double>(s_m[k * CS4 + c]), a0);
+			a1 = __builtin_fma(static_cast<double>(s_l[r * CS4 + k + 1]), static_cast<double>(s_m[(k + 1) * CS4 + c]), a1);
 		}
-		const double d = static_cast<double>(s_l[r * CS4 + r]);
-		m[r] = ((c == r ? 1.0 : 0.0) - ((a[0] + a[1]) + (a[2] + a[3]))) / d;
+		if (r & 1) a0 = __builtin_fma(static_cast<double>(s_l[r * CS4 + r - 1]), static_cast<double>(s_m[(r - 1) * CS4 + c]), a0);
+		const float m = static_cast<float>(((c == r ? 1.0 : 0.0) - (a0 + a1)) / static_cast<double>(s_l[r * CS4 + r]));
+		s_m[r * CS4 + c] = m;   // read back only by this lane (its own column)
+		M[r * TILE + c] = m;
 	}
-#pragma unroll
-	for (int r = 0; r < TILE; r++) M[r * TILE + c] = static_cast<float>(m[r]);
 }
 
 // One launch per level of the tile elimination tree.
@@ -732,7 +732,7 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 	CORNER_STAMP(0);
 	if (static_cast<int>(blockIdx.x) >= a.n_tasks) {   // diagonal inverse of a column finished by an earlier launch
 		const int J = a.inv_cols[blockIdx.x - a.n_tasks];
-		invert_lower_tile(a.ldiag + static_cast<int64_t>(J) * TILE_ELEMS, a.minv + static_cast<int64_t>(J) * TILE_ELEMS, s_d, t);
+		invert_lower_tile(a.ldiag + static_cast<int64_t>(J) * TILE_ELEMS, a.minv + static_cast<int64_t>(J) * TILE_ELEMS, s_d, s_p, t);
 		return;
 	}
 	const CornerTask tk = a.tasks[blockIdx.x];
@@ -831,10 +831,20 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 	CORNER_STAMP(4);
 	if (diag) {
 		float4* wa = reinterpret_cast<float4*>(a.ldiag + static_cast<int64_t>(tk.J) * TILE_ELEMS + lane * TILE);
+		float ljj = 1.f;   // this lane's diagonal entry L_jj (j = lane)
 #pragma unroll
-		for (int q = 0; q < TILE / 4; q++)
+		for (int q = 0; q < TILE / 4; q++) {
 			wa[q] = make_float4(4 * q <= lane ? ap[4 * q].x : 0.f, 4 * q + 1 <= lane ? ap[4 * q + 1].x : 0.f,
 			                    4 * q + 2 <= lane ? ap[4 * q + 2].x : 0.f, 4 * q + 3 <= lane ? ap[4 * q + 3].x : 0.f);
+			ljj = 4 * q == lane ? ap[4 * q].x : 4 * q + 1 == lane ? ap[4 * q + 1].x : 4 * q + 2 == lane ? ap[4 * q + 2].x : 4 * q + 3 == lane ? ap[4 * q + 3].x : ljj;
+		}
+		if (a.pivot_word) {   // the refinement gate: min over the tile of pivot (L_jj^2) / diag(S)_jj
+			const float sd = a.sdiag[static_cast<int64_t>(tk.J) * TILE + lane];
+			float ratio = sd > 0.f ? (ljj * ljj) / sd : 1.f;
+#pragma unroll
+			for (int m = 1; m < 64; m <<= 1) ratio = fminf(ratio, __shfl_xor(ratio, m));
+			if (lane == 0) atomicMin(a.pivot_word, __float_as_uint(fmaxf(ratio, 0.f)));
+		}
 		if (lane == 0) {
 			float4* wb = reinterpret_cast<float4*>(a.cb + static_cast<int64_t>(tk.J) * TILE);
 #pragma unroll
@@ -850,6 +860,8 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 }
 
 struct CornerBackArgs {
+	const unsigned* gate;    // nullable: run only if the pivot ratio word is below ratio (the refinement pass)
+	float ratio;
 	const float* tiles;
 	const float* ldiag;
 	const float* minv;       // L_JJ^-1 of the columns whose descriptor says so (w = 1)
@@ -879,6 +891,7 @@ __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 	__shared__ int4 s_cols[BACK_COLS];
 	__shared__ int2 s_ent[2][64];   // first 64 entry descriptors of the current (q & 1) and the next column
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+	if (a.gate && !refine_gate_on(a.gate, a.ratio)) return;
 	const int2 ch = a.chains[blockIdx.x];
 	for (int q0 = 0; q0 < ch.y; q0 += BACK_COLS) {
 		const int nq = ch.y - q0 < BACK_COLS ? ch.y - q0 : BACK_COLS;
@@ -994,6 +1007,8 @@ __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 // product with M, rows of M loaded ahead) or, for top-level columns, the row-oriented substitution on wave 0. y_J
 // overwrites b_J in yb (a column reads y of its descendants only: earlier launches or earlier in its chain).
 struct CornerFwdArgs {
+	const unsigned* gate;
+	float ratio;
 	const float* tiles;
 	const float* ldiag;
 	const float* minv;
@@ -1005,6 +1020,7 @@ struct CornerFwdArgs {
 __global__ __launch_bounds__(CT) void k_corner_fwd(CornerFwdArgs a) {
 	__shared__ __attribute__((aligned(16))) float s_z[TILE];
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+	if (a.gate && !refine_gate_on(a.gate, a.ratio)) return;
 	const int2 ch = a.chains[blockIdx.x];
 	const int cg = lane & 15, rq = lane >> 4;
 	for (int q = 0; q < ch.y; q++) {
@@ -1112,6 +1128,8 @@ struct WalkElem {
 	int info;            // entry: -1; head: 1 if the tile is L_JJ^-1, 0 if it is L_JJ
 };
 struct CornerWalkArgs {
+	const unsigned* gate;  // nullable: run only if the pivot ratio word is below ratio (the refinement pass)
+	float ratio;
 	const WalkElem* fwd;   // forward stream (n_fwd = 0: none)
 	const WalkElem* back;  // back stream (n_back = 0: none)
 	int n_fwd, n_back;
@@ -1302,6 +1320,7 @@ __device__ void walk_pass(const WalkElem* __restrict__ gdesc, int n, int R, Walk
 
 __global__ __launch_bounds__(WT) void k_corner_walk(CornerWalkArgs a) {
 	extern __shared__ __attribute__((aligned(16))) float s_walk[];
+	if (a.gate && !refine_gate_on(a.gate, a.ratio)) return;
 	const int nd = a.n_fwd > a.n_back ? a.n_fwd : a.n_back;
 	WalkElem* desc = reinterpret_cast<WalkElem*>(s_walk);
 	float* x = s_walk + 4 * nd;
@@ -1340,6 +1359,7 @@ CornerSolver::~CornerSolver() { release(); }
 void CornerSolver::release() {
 	for (void** p : {reinterpret_cast<void**>(&tiles), reinterpret_cast<void**>(&ldiag), reinterpret_cast<void**>(&minv), reinterpret_cast<void**>(&d_inv_cols),
 	                 reinterpret_cast<void**>(&cb2), reinterpret_cast<void**>(&d_fwd_chains), reinterpret_cast<void**>(&d_fwd_cols),
+	                 reinterpret_cast<void**>(&sdiag), reinterpret_cast<void**>(&pivot_word),
 	                 reinterpret_cast<void**>(&d_fwd_ent), reinterpret_cast<void**>(&d_walk_back), reinterpret_cast<void**>(&d_walk_fwd),
 	                 reinterpret_cast<void**>(&cb),
 	                 reinterpret_cast<void**>(&xp), reinterpret_cast<void**>(&d_tile_slot), reinterpret_cast<void**>(&d_slot_ij),
@@ -1384,6 +1404,7 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		nnrt_status st;
 		if ((st = alloc(tiles, p.slot_ij.size() * TILE_ELEMS)) || (st = alloc(ldiag, static_cast<size_t>(p.T) * TILE_ELEMS)) ||
 		    (st = alloc(minv, static_cast<size_t>(p.T) * TILE_ELEMS)) || (st = alloc(cb2, static_cast<size_t>(p.ld))) ||
+		    (st = alloc(sdiag, static_cast<size_t>(p.ld))) || (st = alloc(reinterpret_cast<float*&>(pivot_word), 1)) ||
 		    (st = alloc(cb, static_cast<size_t>(p.ld))) || (st = alloc(xp, static_cast<size_t>(p.ld))))
 			return fail(st);
 		if ((st = dev_upload(d_tile_slot, p.tile_slot)) || (st = dev_upload(d_slot_ij, p.slot_ij)) || (st = dev_upload(d_row_node, p.row_node)) ||
@@ -1445,7 +1466,7 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 	return NNRT_OK;
 }
 
-CornerMap CornerSolver::map() const { return CornerMap{T, d_tile_slot, d_node_row, tiles}; }
+CornerMap CornerSolver::map() const { return CornerMap{T, d_tile_slot, d_node_row, tiles, sdiag}; }
 
 nnrt_status CornerSolver::launch_init(int n0, const float* diag, const float* rhs, const int32_t* edges, const float* wing, hipStream_t s) const {
 	if (nc == 0) return NNRT_OK;
@@ -1466,7 +1487,7 @@ nnrt_status CornerSolver::launch_offdiag(int n0, const int32_t* edges, const flo
 
 nnrt_status CornerSolver::launch_solve(float* xout, int* error_flag, hipStream_t s) const {
 	if (nc == 0) return NNRT_OK;
-	CornerFactorArgs fa{tiles, ldiag, cb, nullptr, d_srcs, 0, error_flag, 0, 0, nullptr, minv};
+	CornerFactorArgs fa{tiles, ldiag, cb, nullptr, d_srcs, 0, error_flag, 0, 0, nullptr, minv, sdiag, pivot_word};
 	for (int l = 0; l < H; l++) {
 		fa.level = l;
 		const int n = level_off[static_cast<size_t>(l) + 1] - level_off[static_cast<size_t>(l)];
@@ -1479,12 +1500,12 @@ nnrt_status CornerSolver::launch_solve(float* xout, int* error_flag, hipStream_t
 		NNRT_LAUNCH_CHECK();
 	}
 	if (walk_ok) {   // the back substitution as one single-workgroup walk
-		const CornerWalkArgs wa{nullptr, d_walk_back, 0, n_walk_back, cb, d_row_node, xout, ld, walk_ring};
+		const CornerWalkArgs wa{nullptr, 0.f, nullptr, d_walk_back, 0, n_walk_back, cb, d_row_node, xout, ld, walk_ring};
 		k_corner_walk<<<1, WT, walk_lds, s>>>(wa);
 		NNRT_LAUNCH_CHECK();
 		return NNRT_OK;
 	}
-	CornerBackArgs ba{tiles, ldiag, minv, cb, xp, d_row_node, xout, nullptr, d_back_cols, d_back_ent};
+	CornerBackArgs ba{nullptr, 0.f, tiles, ldiag, minv, cb, xp, d_row_node, xout, nullptr, d_back_cols, d_back_ent};
 	for (size_t l = 0; l + 1 < back_off.size(); l++) {
 		const int n = back_off[l + 1] - back_off[l];
 		ba.chains = d_back_chains + back_off[l];
@@ -1494,22 +1515,22 @@ nnrt_status CornerSolver::launch_solve(float* xout, int* error_flag, hipStream_t
 	return NNRT_OK;
 }
 
-nnrt_status CornerSolver::launch_resolve(float* xout, hipStream_t s) const {
+nnrt_status CornerSolver::launch_resolve(float* xout, hipStream_t s, const unsigned* gate, float refine_ratio) const {
 	if (nc == 0) return NNRT_OK;
 	if (walk_ok) {   // forward and back substitution in one single-workgroup launch
-		const CornerWalkArgs wa{d_walk_fwd, d_walk_back, n_walk_fwd, n_walk_back, cb2, d_row_node, xout, ld, walk_ring};
+		const CornerWalkArgs wa{gate, refine_ratio, d_walk_fwd, d_walk_back, n_walk_fwd, n_walk_back, cb2, d_row_node, xout, ld, walk_ring};
 		k_corner_walk<<<1, WT, walk_lds, s>>>(wa);
 		NNRT_LAUNCH_CHECK();
 		return NNRT_OK;
 	}
-	CornerFwdArgs fa{tiles, ldiag, minv, cb2, nullptr, d_fwd_cols, d_fwd_ent};
+	CornerFwdArgs fa{gate, refine_ratio, tiles, ldiag, minv, cb2, nullptr, d_fwd_cols, d_fwd_ent};
 	for (size_t l = 0; l + 1 < fwd_off.size(); l++) {
 		const int n = fwd_off[l + 1] - fwd_off[l];
 		fa.chains = d_fwd_chains + fwd_off[l];
 		k_corner_fwd<<<n, CT, 0, s>>>(fa);
 		NNRT_LAUNCH_CHECK();
 	}
-	CornerBackArgs ba{tiles, ldiag, minv, cb2, xp, d_row_node, xout, nullptr, d_back_cols, d_back_ent};
+	CornerBackArgs ba{gate, refine_ratio, tiles, ldiag, minv, cb2, xp, d_row_node, xout, nullptr, d_back_cols, d_back_ent};
 	for (size_t l = 0; l + 1 < back_off.size(); l++) {
 		const int n = back_off[l + 1] - back_off[l];
 		ba.chains = d_back_chains + back_off[l];

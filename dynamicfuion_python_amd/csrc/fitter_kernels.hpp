@@ -194,6 +194,7 @@ struct CornerMap {      // device view: permuted (row, column) -> stored entry
 	const int* tile_slot;   // [T, T]
 	const int* node_row;    // [nc] first permuted unknown of each corner node
 	float* tiles;           // [slots, 64, 64]
+	float* sdiag;           // [ld] diagonal of S before the factorization (the refinement gate's reference; nullable)
 };
 // stored position of corner entry (R, C), R >= C (permuted unknowns)
 __device__ inline float* corner_entry(const CornerMap& m, int R, int C) {
@@ -217,6 +218,8 @@ struct CornerInitArgs {
 	const int* row_node;
 	float* tiles;
 	float* cb;
+	float* sdiag;              // [ld] diag(C) (the Schur update lowers it to diag(S)); nullable
+	unsigned* pivot_word;      // reset to +inf: the factorization's minimum pivot / diag(S) ratio; nullable
 	int64_t threads() const { return std::max<int64_t>(static_cast<int64_t>(slots) * (CORNER_NB * CORNER_NB / 4), ld); }
 };
 __device__ inline void corner_init_thread(int64_t idx, const CornerInitArgs& a, const float* __restrict__ diag, const float* __restrict__ rhs) {
@@ -224,6 +227,8 @@ __device__ inline void corner_init_thread(int64_t idx, const CornerInitArgs& a, 
 	if (idx < a.ld) {
 		const int rn = a.row_node[idx];
 		a.cb[idx] = rn >= 0 ? rhs[6 * static_cast<int64_t>(a.n0 + (rn >> 3)) + (rn & 7)] : 0.f;
+		if (a.sdiag) a.sdiag[idx] = rn >= 0 ? diag[static_cast<int64_t>(a.n0 + (rn >> 3)) * 36 + 7 * (rn & 7)] : 1.f;
+		if (idx == 0 && a.pivot_word) *a.pivot_word = 0x7f800000u;
 	}
 	if (idx >= static_cast<int64_t>(a.slots) * (TE / 4)) return;
 	const int s = static_cast<int>(idx / (TE / 4)), w = static_cast<int>(idx % (TE / 4));
@@ -258,14 +263,17 @@ public:
 	// S = C (+ corner off-diagonal blocks) in the stored tiles, cb = b_C (permuted); diag [N,36], rhs [6N], edges / wing device
 	nnrt_status launch_init(int n0, const float* diag, const float* rhs, const int32_t* edges, const float* wing, hipStream_t s) const;
 	// the two halves of launch_init, for callers that run the init threads inside a launch of their own
-	CornerInitArgs init_args(int n0) const { return CornerInitArgs{n0, ld, slots, d_slot_ij, d_row_node, tiles, cb}; }
+	CornerInitArgs init_args(int n0) const { return CornerInitArgs{n0, ld, slots, d_slot_ij, d_row_node, tiles, cb, sdiag, pivot_word}; }
 	nnrt_status launch_offdiag(int n0, const int32_t* edges, const float* wing, hipStream_t s) const;   // >= 3 layers
 	// factor S (after the stem's Schur update), solve S x = cb; x -> xout[6 nc] in corner-node order
 	nnrt_status launch_solve(float* xout, int* error_flag, hipStream_t s) const;
 	// iterative refinement: solve S d = rhs2 with the factor of the last launch_solve (rhs2 = refine_rhs(), permuted,
 	// written by the caller); d -> xout[6 nc] in corner-node order
-	nnrt_status launch_resolve(float* xout, hipStream_t s) const;
+	// gate (nullable, device): skip unless the factorization's minimum pivot / diag(S) ratio is below refine_ratio
+	nnrt_status launch_resolve(float* xout, hipStream_t s, const unsigned* gate = nullptr, float refine_ratio = 0.f) const;
 	float* refine_rhs() const { return cb2; }
+	// the factorization's minimum pivot / diag(S) ratio of the last solve (device word, float bits)
+	const unsigned* pivot_ratio() const { return pivot_word; }
 	CornerMap map() const;
 	float* rhs_perm() const { return cb; }
 	int levels() const { return H; }
@@ -280,7 +288,8 @@ private:
 	std::vector<int32_t> key;
 	int nc = 0, ld = 0, T = 0, H = 0, slots = 0, n_corner_edges = 0;
 	int64_t fill_tiles = 0, dense_tiles = 0;
-	float *tiles = nullptr, *ldiag = nullptr, *minv = nullptr, *cb = nullptr, *cb2 = nullptr, *xp = nullptr;
+	float *tiles = nullptr, *ldiag = nullptr, *minv = nullptr, *cb = nullptr, *cb2 = nullptr, *xp = nullptr, *sdiag = nullptr;
+	unsigned* pivot_word = nullptr;
 	int2 *d_fwd_chains = nullptr, *d_fwd_ent = nullptr;
 	int4* d_fwd_cols = nullptr;
 	// single-workgroup substitution walks (corner.hip k_corner_walk), when the permuted vector and the descriptors fit in LDS
@@ -295,10 +304,18 @@ private:
 	std::vector<int> level_off, level_panel, inv_off, back_off, fwd_off;
 };
 
-// one step of iterative refinement after the fitter's arrowhead solve; 0: the float solve alone
+// one step of iterative refinement after the fitter's arrowhead solve; 0: the float solve alone.
+// It runs only when the corner factorization's smallest pivot / diag(S) ratio (the cancellation a float32 Cholesky loses
+// digits to) falls below NNRT_REFINE_PIVOT_RATIO; otherwise its launches return at once.
 #ifndef NNRT_ARAP_REFINE
 #define NNRT_ARAP_REFINE 1
 #endif
+#ifndef NNRT_REFINE_PIVOT_RATIO
+#define NNRT_REFINE_PIVOT_RATIO 1e-2f
+#endif
+__device__ inline bool refine_gate_on(const unsigned* gate, float ratio) {
+	return gate && __uint_as_float(*gate) < ratio;
+}
 
 struct ArrowheadWorkspace {
 	int N = 0, n0 = 0, E = 0, m = 0;
@@ -340,7 +357,6 @@ nnrt_status launch_arrowhead_iteration(const ArrowheadWorkspace& ws, const doubl
 // node_state / updates_out (fitter): apply the solved increments to the node motion in the back-substitution launch;
 // state_in (default: node_state): the motion the iteration started from (a snapshot the iteration restarts from)
 nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* edges, const float* wing, int* error_flag, hipStream_t stream,
-                                 bool arap_wings = false, float* node_state = nullptr, float* updates_out = nullptr, const float* state_in = nullptr,
-                                 bool init_done = false);
+                                 bool arap_wings = false, float* node_state = nullptr, float* updates_out = nullptr, const float* state_in = nullptr);
 
 } // namespace nnrt

@@ -144,6 +144,13 @@ class DeformableMeshToImageFitter:
         N.check(N.lib().nnrt_fitter_iterate_timed(self._h, warp_field.handle, int(first_iteration), int(count), N.ptr(ms), N.stream_ptr(stream)))
         return {name: float(v) for name, v in zip(TIMED_STAGES, ms)}
 
+    def refine_info(self, stream=None) -> dict:
+        """The last arrowhead solve's refinement gate: the corner factorization's smallest pivot / diag(S) ratio, the
+        threshold, and whether the refinement step ran."""
+        out = np.zeros(3, np.float32)
+        N.check(N.lib().nnrt_fitter_refine_info(self._h, N.ptr(out), N.stream_ptr(stream)))
+        return dict(pivot_ratio=float(out[0]), threshold=float(out[1]), refined=bool(out[2]))
+
     def time_kernels(self, warp_field: HierarchicalGraphWarpField, reps: int = 20, trials: int = 5, stream=None) -> dict:
         """Per-kernel device ms of one iteration from the snapshot state, each kernel in its real context (prefix
         sequences of `reps` graph-captured iterations, median of `trials`; include/nnrt_mi355x.h)."""

@@ -148,6 +148,10 @@ int32_t nnrt_fitter_graph_count(const nnrt_fitter* fitter);
  * 64-unknown tile columns, factorization launches (elimination-tree levels), back-substitution launches, stored
  * (structurally non-zero) tiles, lower tiles of the dense corner. */
 nnrt_status nnrt_fitter_corner_info(const nnrt_fitter* fitter, int64_t* h_out);
+/* The last arrowhead solve's refinement gate (diagnostic; synchronizes `stream`): h_out[3] = the corner factorization's
+ * smallest pivot / diag(S) ratio (1 without ARAP), the threshold below which one step of iterative refinement runs, and
+ * 1 if it ran. */
+nnrt_status nnrt_fitter_refine_info(nnrt_fitter* fitter, float* h_out, void* stream);
 /* Store the warp field's current node motion (R, t) in the fitter (a device copy on `stream`). */
 nnrt_status nnrt_fitter_snapshot_motion(nnrt_fitter* fitter, nnrt_warp_field* warp_field, void* stream);
 /* Benchmark form of iterate() that runs the general (non-identity) kernels: before every iteration the warp field's

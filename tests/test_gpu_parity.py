@@ -437,7 +437,9 @@ def _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k):
         import scipy.sparse.linalg as spl
         e_own = nan_rel_err(dg_g["updates"][: 6 * N], spl.spsolve(A_own.tocsc(), b_own))
         ratio_own = fp64_pivot_ratio(A_own)
-        solve_note = f", own-system err vs fp64 {e_own:.2g} (pivot ratio {ratio_own:.2g})"
+        gate = ft.refine_info()
+        solve_note = (f", own-system err vs fp64 {e_own:.2g} (fp64 pivot ratio {ratio_own:.2g}; corner pivot / diag(S) "
+                      f"{gate['pivot_ratio']:.2g}, refined {gate['refined']})")
         if ratio_own > REFINE_PIVOT_RATIO:
             assert e_own <= 1e-4, f"iteration {k + 1}: refined solve error {e_own:.3g} vs fp64 at pivot ratio {ratio_own:.3g}"
     if sc.layer_count > 1 and u_err >= 1e-4:
