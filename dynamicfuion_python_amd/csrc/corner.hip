@@ -232,7 +232,6 @@ struct CornerPlan {
 	std::vector<int> level_off, level_panel;   // [H + 1] task offsets per factor launch, [H] panel tasks first
 	std::vector<CornerTask> tasks;
 	std::vector<int4> srcs;           // (slot X, slot Y, column k, 0): X Y^T update terms; rhs term L_k y_k uses X and k
-	std::vector<int> inv_off, inv_cols;   // [H + 1] per factor launch l: the columns of level l - 1 whose diagonal factor it inverts
 	std::vector<int> back_off;        // [launches + 1] back-substitution chains per launch
 	std::vector<int2> back_chains;    // (first column entry, column count): a chain of the elimination tree, root end first
 	std::vector<int4> back_cols;      // (J, entry offset, entry count, 1 if L_JJ^-1 is formed: every column below the top level)
@@ -399,15 +398,7 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 		}
 		p.level_off.push_back(static_cast<int>(p.tasks.size()));
 	}
-	// diagonal inverses L_JJ^-1 (back substitution as a product): launch l >= 1 inverts the columns of level l - 1, whose
-	// L_JJ the previous launch finished; the top level's columns keep the substitution
-	p.inv_off.push_back(0);
-	for (int l = 0; l < p.H; l++) {
-		if (l > 0)
-			for (int J = 0; J < T; J++)
-				if (lvl[static_cast<size_t>(J)] == l - 1) p.inv_cols.push_back(J);
-		p.inv_off.push_back(static_cast<int>(p.inv_cols.size()));
-	}
+
 	// back substitution over chains of the elimination tree: a chain starts at a root or at a child of a node with two or
 	// more children and follows single children down; one workgroup walks a chain from its root end, so a launch holds
 	// every chain at the same number of branchings below the root (x of every column above a chain's top is known
@@ -439,7 +430,7 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 			p.back_chains.push_back(make_int2(static_cast<int>(p.back_cols.size()), static_cast<int>(chain_cols[c].size())));
 			for (int J : chain_cols[c]) {
 				const auto& cc = cs[static_cast<size_t>(J)];
-				p.back_cols.push_back(make_int4(J, static_cast<int>(p.back_ent.size()), static_cast<int>(cc.size()), lvl[static_cast<size_t>(J)] < p.H - 1));
+				p.back_cols.push_back(make_int4(J, static_cast<int>(p.back_ent.size()), static_cast<int>(cc.size()), 1));
 				for (int I : cc) p.back_ent.push_back(make_int2(slot(I, J), I));
 			}
 		}
@@ -450,10 +441,7 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 		std::vector<std::vector<int>> rowk(static_cast<size_t>(T));   // rowk[J]: k < J with a stored tile (J, k), ascending
 		for (int k = 0; k < T; k++)
 			for (int I : cs[static_cast<size_t>(k)]) rowk[static_cast<size_t>(I)].push_back(k);
-		auto head = [&](int J) {
-			const bool inv = lvl[static_cast<size_t>(J)] < p.H - 1;
-			return make_int4(inv ? 1 : 2, J, J * TILE, inv ? 1 : 0);
-		};
+		auto head = [&](int J) { return make_int4(1, J, J * TILE, 1); };   // L_JJ^-1 of every column (k_corner_invert)
 		for (int J = T - 1; J >= 0; J--) {
 			for (int I : cs[static_cast<size_t>(J)]) p.walk_back.push_back(make_int4(0, slot(I, J), I * TILE, -1));
 			p.walk_back.push_back(head(J));
@@ -684,37 +672,39 @@ struct CornerFactorArgs {
 	int n_panel;
 	int* error_flag;
 	int level;
-	int n_tasks;             // workgroups [n_tasks, gridDim) invert diagonal factors of the previous level
-	const int* inv_cols;     // this launch's columns to invert
-	float* minv;             // [T, 64, 64] L_JJ^-1 (lower; zero above the diagonal)
 	const float* sdiag;      // [ld] diag(S) before the factorization (nullable)
 	unsigned* pivot_word;    // atomic minimum of pivot / diag(S) over the diagonal tasks (nullable)
 };
 
 // M = L^-1 for the 64 x 64 lower-triangular factor L (row-major, zero above the diagonal): the workgroup stages L in LDS,
-// wave 0 forms column c of M in lane c by forward substitution (rows in order, the sum over earlier rows in double), its
-// column kept in LDS; M is stored rounded to float. The back substitution then forms x_J = L_JJ^-T z as the product
-// M^T z. Deliberately compact (rolled loops): these workgroups share the launch -- and instruction caches -- with the
-// panels' straight-line elimination (a fully unrolled double version made every factor launch ≈ 2 µs longer).
-__device__ inline void invert_lower_tile(const float* __restrict__ L, float* __restrict__ M, float* s_l, float* s_m, int t) {
-	const float4* L4 = reinterpret_cast<const float4*>(L);
+// wave 0 forms column c of M in lane c by forward substitution (rows in order, four partial sums per row) and stores it.
+// The substitutions then form L_JJ^-T z and L_JJ^-1 z as products with M.
+__global__ __launch_bounds__(CT) void k_corner_invert(const float* __restrict__ ldiag, float* __restrict__ minv) {
+	__shared__ float s_l[TILE * CS4];
+	const int t = threadIdx.x;
+	const int64_t J = blockIdx.x;
+	const float4* L4 = reinterpret_cast<const float4*>(ldiag + J * TILE_ELEMS);
 	for (int i = t; i < TILE_ELEMS / 4; i += CT) *reinterpret_cast<float4*>(s_l + (i >> 4) * CS4 + 4 * (i & 15)) = L4[i];
 	__syncthreads();
 	if (t >= 64) return;
 	const int c = t;
-#pragma unroll 1
+	float m[TILE];
+#pragma unroll
 	for (int r = 0; r < TILE; r++) {
-		double a0 = 0.0, a1 = 0.0;
-#pragma unroll 1
-		for (int k = 0; k + 1 < r; k += 2) {
-			a0 = __builtin_fma(static_cast<double>(s_l[r * CS4 + k]), static_cast<double>(s_m[k * CS4 + c]), a0);
-			a1 = __builtin_fma(static_cast<double>(s_l[r * CS4 + k + 1]), static_cast<double>(s_m[(k + 1) * CS4 + c]), a1);
+		float a[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+		for (int k4 = 0; k4 < r; k4 += 4) {
+			const float4 l = *reinterpret_cast<const float4*>(s_l + r * CS4 + k4);   // wave-uniform: LDS broadcast
+			a[0] = __builtin_fmaf(l.x, m[k4], a[0]);
+			if (k4 + 1 < r) a[1] = __builtin_fmaf(l.y, m[k4 + 1], a[1]);
+			if (k4 + 2 < r) a[2] = __builtin_fmaf(l.z, m[k4 + 2], a[2]);
+			if (k4 + 3 < r) a[3] = __builtin_fmaf(l.w, m[k4 + 3], a[3]);
 		}
-		if (r & 1) a0 = __builtin_fma(static_cast<double>(s_l[r * CS4 + r - 1]), static_cast<double>(s_m[(r - 1) * CS4 + c]), a0);
-		const float m = static_cast<float>(((c == r ? 1.0 : 0.0) - (a0 + a1)) / static_cast<double>(s_l[r * CS4 + r]));
-		s_m[r * CS4 + c] = m;   // read back only by this lane (its own column)
-		M[r * TILE + c] = m;
+		m[r] = ((c == r ? 1.f : 0.f) - ((a[0] + a[1]) + (a[2] + a[3]))) / s_l[r * CS4 + r];
 	}
+	float* M = minv + J * TILE_ELEMS;
+#pragma unroll
+	for (int r = 0; r < TILE; r++) M[r * TILE + c] = m[r];
 }
 
 // One launch per level of the tile elimination tree.
@@ -730,11 +720,6 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 	__shared__ float s_b[TILE];         // b_J after the previous level's updates (diagonal workgroup)
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
 	CORNER_STAMP(0);
-	if (static_cast<int>(blockIdx.x) >= a.n_tasks) {   // diagonal inverse of a column finished by an earlier launch
-		const int J = a.inv_cols[blockIdx.x - a.n_tasks];
-		invert_lower_tile(a.ldiag + static_cast<int64_t>(J) * TILE_ELEMS, a.minv + static_cast<int64_t>(J) * TILE_ELEMS, s_d, s_p, t);
-		return;
-	}
 	const CornerTask tk = a.tasks[blockIdx.x];
 	const int4* src = a.srcs + tk.src;
 	if (static_cast<int>(blockIdx.x) >= a.n_panel) {
@@ -1357,7 +1342,7 @@ static void dev_free(void*& p) {
 CornerSolver::~CornerSolver() { release(); }
 
 void CornerSolver::release() {
-	for (void** p : {reinterpret_cast<void**>(&tiles), reinterpret_cast<void**>(&ldiag), reinterpret_cast<void**>(&minv), reinterpret_cast<void**>(&d_inv_cols),
+	for (void** p : {reinterpret_cast<void**>(&tiles), reinterpret_cast<void**>(&ldiag), reinterpret_cast<void**>(&minv),
 	                 reinterpret_cast<void**>(&cb2), reinterpret_cast<void**>(&d_fwd_chains), reinterpret_cast<void**>(&d_fwd_cols),
 	                 reinterpret_cast<void**>(&sdiag), reinterpret_cast<void**>(&pivot_word),
 	                 reinterpret_cast<void**>(&d_fwd_ent), reinterpret_cast<void**>(&d_walk_back), reinterpret_cast<void**>(&d_walk_fwd),
@@ -1370,7 +1355,6 @@ void CornerSolver::release() {
 	nc = ld = T = H = slots = n_corner_edges = 0;
 	level_off.clear();
 	level_panel.clear();
-	inv_off.clear();
 	fwd_off.clear();
 	back_off.clear();
 	key.clear();
@@ -1410,7 +1394,7 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		if ((st = dev_upload(d_tile_slot, p.tile_slot)) || (st = dev_upload(d_slot_ij, p.slot_ij)) || (st = dev_upload(d_row_node, p.row_node)) ||
 		    (st = dev_upload(d_node_row, p.node_row)) || (st = dev_upload(d_tasks, p.tasks)) || (st = dev_upload(d_srcs, p.srcs)) ||
 		    (st = dev_upload(d_back_cols, p.back_cols)) || (st = dev_upload(d_back_ent, p.back_ent)) || (st = dev_upload(d_back_chains, p.back_chains)) ||
-		    (st = dev_upload(d_corner_edges, p.corner_edges)) || (st = dev_upload(d_inv_cols, p.inv_cols)) ||
+		    (st = dev_upload(d_corner_edges, p.corner_edges)) ||
 		    (st = dev_upload(d_fwd_chains, p.fwd_chains)) || (st = dev_upload(d_fwd_cols, p.fwd_cols)) || (st = dev_upload(d_fwd_ent, p.fwd_ent)))
 			return fail(st);
 		if (hipMemset(cb2, 0, sizeof(float) * static_cast<size_t>(p.ld)) != hipSuccess) {   // identity padding rows stay 0
@@ -1456,7 +1440,6 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		n_corner_edges = static_cast<int>(p.corner_edges.size());
 		level_off = p.level_off;
 		level_panel = p.level_panel;
-		inv_off = p.inv_off;
 		fwd_off = p.fwd_off;
 		back_off = p.back_off;
 		fill_tiles = static_cast<int64_t>(slots);
@@ -1487,18 +1470,18 @@ nnrt_status CornerSolver::launch_offdiag(int n0, const int32_t* edges, const flo
 
 nnrt_status CornerSolver::launch_solve(float* xout, int* error_flag, hipStream_t s) const {
 	if (nc == 0) return NNRT_OK;
-	CornerFactorArgs fa{tiles, ldiag, cb, nullptr, d_srcs, 0, error_flag, 0, 0, nullptr, minv, sdiag, pivot_word};
+	CornerFactorArgs fa{tiles, ldiag, cb, nullptr, d_srcs, 0, error_flag, 0, sdiag, pivot_word};
 	for (int l = 0; l < H; l++) {
 		fa.level = l;
 		const int n = level_off[static_cast<size_t>(l) + 1] - level_off[static_cast<size_t>(l)];
-		const int ni = inv_off[static_cast<size_t>(l) + 1] - inv_off[static_cast<size_t>(l)];
 		fa.tasks = d_tasks + level_off[static_cast<size_t>(l)];
 		fa.n_panel = level_panel[static_cast<size_t>(l)];
-		fa.n_tasks = n;
-		fa.inv_cols = d_inv_cols + inv_off[static_cast<size_t>(l)];
-		k_corner_factor<<<n + ni, CT, 0, s>>>(fa);
+		k_corner_factor<<<n, CT, 0, s>>>(fa);
 		NNRT_LAUNCH_CHECK();
 	}
+	// every diagonal factor's inverse, one workgroup per tile column (the substitutions multiply by them)
+	k_corner_invert<<<T, CT, 0, s>>>(ldiag, minv);
+	NNRT_LAUNCH_CHECK();
 	if (walk_ok) {   // the back substitution as one single-workgroup walk
 		const CornerWalkArgs wa{nullptr, 0.f, nullptr, d_walk_back, 0, n_walk_back, cb, d_row_node, xout, ld, walk_ring};
 		k_corner_walk<<<1, WT, walk_lds, s>>>(wa);

@@ -297,11 +297,11 @@ private:
 	int walk_ring = 0, walk_lds = 0, n_walk_back = 0, n_walk_fwd = 0;
 	WalkElem* d_walk_back = nullptr;
 	WalkElem* d_walk_fwd = nullptr;
-	int *d_tile_slot = nullptr, *d_row_node = nullptr, *d_node_row = nullptr, *d_corner_edges = nullptr, *d_inv_cols = nullptr;
+	int *d_tile_slot = nullptr, *d_row_node = nullptr, *d_node_row = nullptr, *d_corner_edges = nullptr;
 	int2 *d_slot_ij = nullptr, *d_back_ent = nullptr, *d_back_chains = nullptr;
 	CornerTask* d_tasks = nullptr;
 	int4 *d_srcs = nullptr, *d_back_cols = nullptr;
-	std::vector<int> level_off, level_panel, inv_off, back_off, fwd_off;
+	std::vector<int> level_off, level_panel, back_off, fwd_off;
 };
 
 // one step of iterative refinement after the fitter's arrowhead solve; 0: the float solve alone.

@@ -81,18 +81,14 @@ int main(int argc, char** argv) {
 			}
 			tr.push_back(r); tw.push_back(w);
 		}
-		// diagonal inverses of the previous level's columns (extra workgroups of the same launch): read ldiag J, write minv J
-		for (int q = p.inv_off[l]; q < p.inv_off[l+1]; q++) {
-			const int J = p.inv_cols[q];
-			std::set<std::pair<int,int>> r, w;
-			r.insert({1,J}); w.insert({3,J});
-			if (inv_launch[J] >= 0 || ldiag_launch[J] < 0 || ldiag_launch[J] >= l) { printf("INVERSE order violation: column %d at launch %d\n", J, l); return 1; }
-			const double* Ld = &ldiag[(size_t)J*TE]; double* Mi = &minv[(size_t)J*TE];
-			for (int c = 0; c < TILE; c++) for (int rr = 0; rr < TILE; rr++) { double v = rr == c ? 1.0 : 0.0; for (int k = 0; k < rr; k++) v -= Ld[rr*TILE+k]*Mi[k*TILE+c]; Mi[rr*TILE+c] = v / Ld[rr*TILE+rr]; }
-			inv_launch[J] = l;
-			tr.push_back(r); tw.push_back(w);
-		}
 		for (size_t a = 0; a < tw.size(); a++) for (size_t b = 0; b < tw.size(); b++) if (a != b) for (auto& x : tw[a]) if (tr[b].count(x) || tw[b].count(x)) { printf("RACE level %d task %zu writes (%d,%d) touched by task %zu\n", l, a, x.first, x.second, b); return 1; }
+	}
+	// every diagonal factor's inverse, formed after the last factor launch (k_corner_invert)
+	for (int J = 0; J < T; J++) {
+		if (ldiag_launch[J] < 0) { printf("column %d never factored\n", J); return 1; }
+		const double* Ld = &ldiag[(size_t)J*TE]; double* Mi = &minv[(size_t)J*TE];
+		for (int c = 0; c < TILE; c++) for (int rr = 0; rr < TILE; rr++) { double v = rr == c ? 1.0 : 0.0; for (int k = 0; k < rr; k++) v -= Ld[rr*TILE+k]*Mi[k*TILE+c]; Mi[rr*TILE+c] = v / Ld[rr*TILE+rr]; }
+		inv_launch[J] = p.H;
 	}
 	std::vector<int> done_launch(T, -1);   // launch index in which x_J was produced
 	printf("back launches %zu chains %zu\n", p.back_off.size() - 1, p.back_chains.size());
