@@ -861,18 +861,28 @@ struct CornerBackArgs {
 
 // Back substitution L^T x = y along chains of the elimination tree (one workgroup per chain, its columns in order; the
 // launches run from the root's chain down). Per column J: z = y_J - sum_I L_IJ^T x_I (each wave a quarter of every tile's
-// rows, read as 16-B row pieces, BACK_BATCH tiles' loads in flight), then x_J = L_JJ^-T z by
-// column-oriented substitution on wave 0 (lane = column; x_r broadcast by readlane). x_J goes to global memory before
-// the workgroup barrier, so the chain's next column reads it like the x of earlier launches.
+// rows, read as 16-B row pieces, BACK_BATCH tiles' loads in flight), then x_J = L_JJ^-T z as the product M^T z with
+// M = L_JJ^-1 (k_corner_invert; its tile streams into LDS by LDS-DMA behind the entry loads) on wave 0. x_J goes to
+// global memory before the workgroup barrier, so the chain's next column reads it like the x of earlier launches.
 // Per column only the entry tiles and their x are a memory round trip on the chain's path: the chain's column
 // descriptors are staged in LDS up front, each column's first 64 entry descriptors are fetched during the previous
-// column (wave 1, into LDS before its last barrier), and wave 0's y_J and L_JJ diagonal loads are issued with its L_JJ
-// columns, ahead of the sums (round 3: four dependent round trips per column before).
-constexpr int BACK_BATCH = 6;   // entry tiles per batch of loads (6 x (4 + 4) = 48 outstanding loads per lane)
+// column (wave 1, into LDS before its last barrier), and y_J is loaded ahead of the sums.
+constexpr int BACK_BATCH = 8;   // entry tiles per batch of loads (8 x (4 + 1) = 40 outstanding loads per lane)
 constexpr int BACK_COLS = 64;   // chain columns whose descriptors are staged in LDS at a time
+typedef __attribute__((address_space(3))) void corner_lds_t;
+typedef const __attribute__((address_space(1))) void corner_global_t;
+// the 64 x 64 tile at src -> LDS dst (row-major, no padding) by LDS-DMA: 16 pieces of 1 KB, four per wave of a
+// 256-thread workgroup; complete once the issuing waves wait for their loads (a __syncthreads() does)
+__device__ __forceinline__ void tile_to_lds(const float* src, float* dst, int wave, int lane) {
+#pragma unroll
+	for (int i = 0; i < 4; i++) {
+		const int chunk = 4 * wave + i;
+		__builtin_amdgcn_global_load_lds((corner_global_t*)(src + chunk * 256 + lane * 4), (corner_lds_t*)(dst + chunk * 256), 16, 0, 0);
+	}
+}
 __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
+	__shared__ __attribute__((aligned(16))) float s_m[TILE_ELEMS];   // L_JJ^-1 of the current column
 	__shared__ __attribute__((aligned(16))) float s_part[4][TILE];
-	__shared__ __attribute__((aligned(16))) float s_z[TILE];
 	__shared__ int4 s_cols[BACK_COLS];
 	__shared__ int2 s_ent[2][64];   // first 64 entry descriptors of the current (q & 1) and the next column
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
@@ -890,106 +900,79 @@ __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 		for (int q = 0; q < nq; q++) {
 			const int4 col = s_cols[q];
 			const int J = col.x;
-			const bool inv = col.w != 0;   // x_J = M^T z with M = L_JJ^-1, else the column-oriented substitution
-			const float* Ld = (inv ? a.minv : a.ldiag) + static_cast<int64_t>(J) * TILE_ELEMS;
-			float colv[TILE];   // colv[r] = L_JJ[r][lane] or M[r][lane] (wave 0; issued before the sums so the loads overlap them)
-			float yv = 0.f, dv = 1.f;
-			if (wave == 0) {
-	#pragma unroll
-				for (int r = 0; r < TILE; r++) colv[r] = Ld[r * TILE + lane];
-				yv = a.cb[static_cast<int64_t>(J) * TILE + lane];
-				if (!inv) dv = Ld[lane * TILE + lane];
-			}
+			// M = L_JJ^-1 streams into LDS behind the entry loads; y_J is loaded ahead of the sums (wave 0)
+			tile_to_lds(a.minv + static_cast<int64_t>(J) * TILE_ELEMS, s_m, wave, lane);
+			const float yv = wave == 0 ? a.cb[static_cast<int64_t>(J) * TILE + lane] : 0.f;
 			const bool has_next = q + 1 < nq;
 			int2 nxt = make_int2(0, 0);
 			if (wave == 1 && has_next) {
 				const int4 cn = s_cols[q + 1];
 				if (lane < cn.z) nxt = a.ent[cn.y + lane];
 			}
-			// z partials: lane (row quarter rq, column group cg) covers rows 16 wave + rq + 4k (k < 4) and columns 4 cg .. 4 cg + 3
-			// of every entry tile (four 16-B loads per tile), BACK_BATCH tiles' loads in flight; the four row quarters are
-			// then summed across lanes
+			// z partials: lane (row group rq, column group cg) covers rows 16 wave + 4 rq .. + 3 and columns 4 cg .. 4 cg + 3
+			// of every entry tile (four 16-B row loads and one 16-B x load per tile), BACK_BATCH tiles' loads in flight; the
+			// row groups are then summed across lanes
 			const int cg = lane & 15, rq = lane >> 4;
 			float acc[4] = {0.f, 0.f, 0.f, 0.f};
 			for (int e0 = 0; e0 < col.z; e0 += 64) {
 				const int ne = col.z - e0 < 64 ? col.z - e0 : 64;
 				const int2 mine = e0 == 0 ? s_ent[q & 1][lane] : lane < ne ? a.ent[col.y + e0 + lane] : make_int2(0, 0);
 				for (int e = 0; e < ne; e += BACK_BATCH) {
-					float4 l[BACK_BATCH][4];
-					float xv[BACK_BATCH][4];
-	#pragma unroll
+					float4 l[BACK_BATCH][4], xv[BACK_BATCH];
+#pragma unroll
 					for (int j = 0; j < BACK_BATCH; j++) {
 						const bool ok = e + j < ne;   // a missing entry repeats entry e's tile against x = 0 (exact zeros)
 						const int sj = __shfl(mine.x, ok ? e + j : e);
 						const int ij = __shfl(mine.y, ok ? e + j : e);
-						const float* Lj = a.tiles + static_cast<int64_t>(sj) * TILE_ELEMS + (16 * wave + rq) * TILE + 4 * cg;
-						const float* xj = a.xp + static_cast<int64_t>(ij) * TILE + 16 * wave + rq;
-	#pragma unroll
+						const float* Lj = a.tiles + static_cast<int64_t>(sj) * TILE_ELEMS + (16 * wave + 4 * rq) * TILE + 4 * cg;
+#pragma unroll
+						for (int k = 0; k < 4; k++) l[j][k] = *reinterpret_cast<const float4*>(Lj + k * TILE);
+						const float4 x4 = *reinterpret_cast<const float4*>(a.xp + static_cast<int64_t>(ij) * TILE + 16 * wave + 4 * rq);
+						xv[j] = ok ? x4 : make_float4(0.f, 0.f, 0.f, 0.f);
+					}
+#pragma unroll
+					for (int j = 0; j < BACK_BATCH; j++) {
+						const float xk[4] = {xv[j].x, xv[j].y, xv[j].z, xv[j].w};
+#pragma unroll
 						for (int k = 0; k < 4; k++) {
-							l[j][k] = *reinterpret_cast<const float4*>(Lj + 4 * k * TILE);
-							xv[j][k] = ok ? xj[4 * k] : 0.f;
+							acc[0] += l[j][k].x * xk[k];
+							acc[1] += l[j][k].y * xk[k];
+							acc[2] += l[j][k].z * xk[k];
+							acc[3] += l[j][k].w * xk[k];
 						}
 					}
-	#pragma unroll
-					for (int j = 0; j < BACK_BATCH; j++)
-	#pragma unroll
-						for (int k = 0; k < 4; k++) {
-							acc[0] += l[j][k].x * xv[j][k];
-							acc[1] += l[j][k].y * xv[j][k];
-							acc[2] += l[j][k].z * xv[j][k];
-							acc[3] += l[j][k].w * xv[j][k];
-						}
 				}
 			}
-	#pragma unroll
+#pragma unroll
 			for (int i = 0; i < 4; i++) {
 				acc[i] += __shfl_xor(acc[i], 16);
 				acc[i] += __shfl_xor(acc[i], 32);
 			}
 			if (lane < 16) *reinterpret_cast<float4*>(&s_part[wave][4 * lane]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
-			__syncthreads();
+			__syncthreads();   // also retires the M tile's LDS-DMA pieces of every wave
 			if (wave == 0) {
-				float z = yv - ((s_part[0][lane] + s_part[1][lane]) + (s_part[2][lane] + s_part[3][lane]));
-				float x = 0.f;
-				if (inv) {
-					// x_c = sum_r M_rc z_r: z through this wave's LDS row (in-order within the wave), four partial sums
-					s_z[lane] = z;
-					__builtin_amdgcn_wave_barrier();
-					float xs[4] = {0.f, 0.f, 0.f, 0.f};
-	#pragma unroll
-					for (int r4 = 0; r4 < TILE; r4 += 4) {
-						const float4 zz = *reinterpret_cast<const float4*>(&s_z[r4]);
-						xs[0] = __builtin_fmaf(colv[r4], zz.x, xs[0]);
-						xs[1] = __builtin_fmaf(colv[r4 + 1], zz.y, xs[1]);
-						xs[2] = __builtin_fmaf(colv[r4 + 2], zz.z, xs[2]);
-						xs[3] = __builtin_fmaf(colv[r4 + 3], zz.w, xs[3]);
-					}
-					x = (xs[0] + xs[1]) + (xs[2] + xs[3]);
-				} else {
-					const float inv_d = 1.f / dv;
-	#pragma unroll
-					for (int r = TILE - 1; r >= 0; r--) {
-						const float xr = lane_bcast(z, r) * lane_bcast(inv_d, r);   // x_r = z_r / L_rr
-						x = lane == r ? xr : x;
-						z -= colv[r] * xr;   // z_c -= L_rc x_r (only c < r matter)
-					}
-				}
+				// x_c = sum_r M_rc z_r, z_r broadcast from lane r; column c of M from LDS (conflict-free); four partial sums
+				const float z = yv - ((s_part[0][lane] + s_part[1][lane]) + (s_part[2][lane] + s_part[3][lane]));
+				float xs[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+				for (int r = 0; r < TILE; r++) xs[r & 3] = __builtin_fmaf(s_m[r * TILE + lane], lane_bcast(z, r), xs[r & 3]);
+				const float x = (xs[0] + xs[1]) + (xs[2] + xs[3]);
 				const int64_t row = static_cast<int64_t>(J) * TILE + lane;
 				a.xp[row] = x;
 				const int rn = a.row_node[row];
 				if (rn >= 0) a.xout[6 * static_cast<int64_t>(rn >> 3) + (rn & 7)] = x;
 			}
 			if (wave == 1 && has_next) s_ent[(q + 1) & 1][lane] = nxt;
-			__syncthreads();   // x_J visible to the chain's next column; s_part free; the next column's entries staged
+			__syncthreads();   // x_J visible to the chain's next column; s_part, s_m free; the next column's entries staged
 		}
 	}
 }
 
 // Forward substitution L y = b along the forward chains (iterative refinement's corner solve; the first solve's forward
 // substitution rides in the factorization as the augmented row): per column J, z = b_J - sum_k L_Jk y_k over its row
-// entries (lane (row quarter, column group) covers rows 16 wave + rq + 4i and columns 4 cg .. 4 cg + 3 of every entry tile;
-// the 16 column groups are summed across lanes, so each row's sum is complete in its wave), then y_J = L_JJ^-1 z (the
-// product with M, rows of M loaded ahead) or, for top-level columns, the row-oriented substitution on wave 0. y_J
+// entries (lane (row group, column group) covers rows 16 wave + 4 rq .. + 3 and columns 4 cg .. 4 cg + 3 of every entry tile;
+// the 16 column groups are summed across lanes, so each row's sum is complete in its wave), then y_J = L_JJ^-1 z, the
+// product with M (k_corner_invert; streamed into LDS by LDS-DMA behind the entry loads) split the same way. y_J
 // overwrites b_J in yb (a column reads y of its descendants only: earlier launches or earlier in its chain).
 struct CornerFwdArgs {
 	const unsigned* gate;
@@ -1003,29 +986,17 @@ struct CornerFwdArgs {
 	const int2* ent;         // (slot of L_Jk, k)
 };
 __global__ __launch_bounds__(CT) void k_corner_fwd(CornerFwdArgs a) {
+	__shared__ __attribute__((aligned(16))) float s_m[TILE_ELEMS];   // L_JJ^-1 of the current column
 	__shared__ __attribute__((aligned(16))) float s_z[TILE];
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
 	if (a.gate && !refine_gate_on(a.gate, a.ratio)) return;
 	const int2 ch = a.chains[blockIdx.x];
-	const int cg = lane & 15, rq = lane >> 4;
+	const int cg = lane & 15, rq = lane >> 4;   // rows 16 wave + 4 rq .. + 3, columns 4 cg .. 4 cg + 3
 	for (int q = 0; q < ch.y; q++) {
 		const int4 col = a.cols[ch.x + q];
 		const int J = col.x;
-		const bool inv = col.w != 0;
-		// wave 0: row `lane` of M (inverse) or of L_JJ (substitution), loaded ahead of the sums
-		float rowv[TILE];
-		if (wave == 0) {
-			const float4* R4 = reinterpret_cast<const float4*>((inv ? a.minv : a.ldiag) + static_cast<int64_t>(J) * TILE_ELEMS + lane * TILE);
-#pragma unroll
-			for (int c4 = 0; c4 < TILE / 4; c4++) {
-				const float4 v = R4[c4];
-				rowv[4 * c4] = v.x;
-				rowv[4 * c4 + 1] = v.y;
-				rowv[4 * c4 + 2] = v.z;
-				rowv[4 * c4 + 3] = v.w;
-			}
-		}
-		float acc[4] = {0.f, 0.f, 0.f, 0.f};   // rows 16 wave + rq + 4 i, partial over this lane's 4 columns
+		tile_to_lds(a.minv + static_cast<int64_t>(J) * TILE_ELEMS, s_m, wave, lane);   // behind the entry loads
+		float acc[4] = {0.f, 0.f, 0.f, 0.f};   // rows 16 wave + 4 rq + k, partial over this lane's 4 columns
 		for (int e0 = 0; e0 < col.z; e0 += 64) {
 			const int ne = col.z - e0 < 64 ? col.z - e0 : 64;
 			const int2 mine = lane < ne ? a.ent[col.y + e0 + lane] : make_int2(0, 0);
@@ -1036,57 +1007,46 @@ __global__ __launch_bounds__(CT) void k_corner_fwd(CornerFwdArgs a) {
 					const bool ok = e + j < ne;   // a missing entry repeats entry e's tile against y = 0
 					const int sj = __shfl(mine.x, ok ? e + j : e);
 					const int kj = __shfl(mine.y, ok ? e + j : e);
-					const float* Lj = a.tiles + static_cast<int64_t>(sj) * TILE_ELEMS + (16 * wave + rq) * TILE + 4 * cg;
+					const float* Lj = a.tiles + static_cast<int64_t>(sj) * TILE_ELEMS + (16 * wave + 4 * rq) * TILE + 4 * cg;
 #pragma unroll
-					for (int i = 0; i < 4; i++) l[j][i] = *reinterpret_cast<const float4*>(Lj + 4 * i * TILE);
+					for (int k = 0; k < 4; k++) l[j][k] = *reinterpret_cast<const float4*>(Lj + k * TILE);
 					const float4 y4 = *reinterpret_cast<const float4*>(a.yb + static_cast<int64_t>(kj) * TILE + 4 * cg);
 					yv[j] = ok ? y4 : make_float4(0.f, 0.f, 0.f, 0.f);
 				}
 #pragma unroll
 				for (int j = 0; j < BACK_BATCH; j++)
 #pragma unroll
-					for (int i = 0; i < 4; i++)
-						acc[i] += ((l[j][i].x * yv[j].x + l[j][i].y * yv[j].y) + l[j][i].z * yv[j].z) + l[j][i].w * yv[j].w;
+					for (int k = 0; k < 4; k++)
+						acc[k] += ((l[j][k].x * yv[j].x + l[j][k].y * yv[j].y) + l[j][k].z * yv[j].z) + l[j][k].w * yv[j].w;
 			}
 		}
 #pragma unroll
-		for (int i = 0; i < 4; i++)
+		for (int k = 0; k < 4; k++)
 #pragma unroll
-			for (int m = 1; m < 16; m <<= 1) acc[i] += __shfl_xor(acc[i], m);
+			for (int m = 1; m < 16; m <<= 1) acc[k] += __shfl_xor(acc[k], m);
 		if (cg == 0) {
 #pragma unroll
-			for (int i = 0; i < 4; i++) {
-				const int r = 16 * wave + rq + 4 * i;
-				s_z[r] = a.yb[static_cast<int64_t>(J) * TILE + r] - acc[i];
+			for (int k = 0; k < 4; k++) {
+				const int r = 16 * wave + 4 * rq + k;
+				s_z[r] = a.yb[static_cast<int64_t>(J) * TILE + r] - acc[k];
 			}
 		}
-		__syncthreads();
-		if (wave == 0) {
-			float y;
-			if (inv) {   // y_c = sum_r M_cr z_r
-				float ys[4] = {0.f, 0.f, 0.f, 0.f};
+		__syncthreads();   // z complete; the M tile's LDS-DMA pieces of every wave retired
+		{   // y_r = sum_c M_rc z_c: the same row / column-group split, summed across the 16 column groups
+			const float4 z4 = *reinterpret_cast<const float4*>(&s_z[4 * cg]);
+			float yk[4];
 #pragma unroll
-				for (int r4 = 0; r4 < TILE; r4 += 4) {
-					const float4 zz = *reinterpret_cast<const float4*>(&s_z[r4]);
-					ys[0] = __builtin_fmaf(rowv[r4], zz.x, ys[0]);
-					ys[1] = __builtin_fmaf(rowv[r4 + 1], zz.y, ys[1]);
-					ys[2] = __builtin_fmaf(rowv[r4 + 2], zz.z, ys[2]);
-					ys[3] = __builtin_fmaf(rowv[r4 + 3], zz.w, ys[3]);
-				}
-				y = (ys[0] + ys[1]) + (ys[2] + ys[3]);
-			} else {   // row-oriented: y_c = z_c / L_cc, then z_r -= L_rc y_c for r > c
-				float z = s_z[lane];
-				y = 0.f;
+			for (int k = 0; k < 4; k++) {
+				const float4 m4 = *reinterpret_cast<const float4*>(&s_m[(16 * wave + 4 * rq + k) * TILE + 4 * cg]);
+				yk[k] = ((m4.x * z4.x + m4.y * z4.y) + m4.z * z4.z) + m4.w * z4.w;
 #pragma unroll
-				for (int c = 0; c < TILE; c++) {
-					const float yc = lane_bcast(z, c) / lane_bcast(rowv[c], c);
-					y = lane == c ? yc : y;
-					z -= rowv[c] * yc;   // only rows r > c matter (L_rc = 0 above the diagonal)
-				}
+				for (int m = 1; m < 16; m <<= 1) yk[k] += __shfl_xor(yk[k], m);
 			}
-			a.yb[static_cast<int64_t>(J) * TILE + lane] = y;
+			if (cg == 0)
+#pragma unroll
+				for (int k = 0; k < 4; k++) a.yb[static_cast<int64_t>(J) * TILE + 16 * wave + 4 * rq + k] = yk[k];
 		}
-		__syncthreads();   // y_J visible to the chain's next column; s_z free
+		__syncthreads();   // y_J visible to the chain's next column; s_z, s_m free
 	}
 }
 
