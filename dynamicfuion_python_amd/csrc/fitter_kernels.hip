@@ -421,6 +421,7 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 	// this pixel's face: distinct anchor nodes still to be filed, ascending; the row waits in LDS (s_ent[wave][.][lane]),
 	// the current head in a register (head_at: its index)
 	uint32_t head_e = FACE_NODE_NONE;
+	uint32_t next_e = FACE_NODE_NONE;   // the entry after the head, read ahead: advancing the list waits on no LDS read
 	int head_at = 0;
 	int vid[3] = {0, 0, 0};
 	if (in_image) {
@@ -434,7 +435,10 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 				ent[(4 * t + 1) * 64 + lane] = e4.y;
 				ent[(4 * t + 2) * 64 + lane] = e4.z;
 				ent[(4 * t + 3) * 64 + lane] = e4.w;
-				if (t == 0) head_e = e4.x;
+				if (t == 0) {
+					head_e = e4.x;
+					next_e = e4.y;
+				}
 			}
 			vid[0] = vid_in[0];
 			vid[1] = vid_in[1];
@@ -494,7 +498,12 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 				slots[pos] = __builtin_bit_cast(float, lane);
 				slots[NG_STRIDE + pos] = __builtin_bit_cast(float, head_e);
 				head_at++;
+#if NNRT_GROUP_PREFETCH
+				head_e = next_e;
+				next_e = head_at + 1 < NSLOT ? ent[(head_at + 1) * 64 + lane] : FACE_NODE_NONE;
+#else
 				head_e = head_at < NSLOT ? ent[head_at * 64 + lane] : FACE_NODE_NONE;
+#endif
 			}
 			const int n_head = __popcll(M);
 			filed += n_head < room ? n_head : room;   // (integer select: the generic min() overload went through double)
@@ -928,6 +937,24 @@ __global__ __launch_bounds__(64) void k_solve_update(SolveArgs a) {
 	using T = ModeTraits<MODE>;
 	constexpr int S = T::S;
 	const int n = blockIdx.x * blockDim.x + threadIdx.x;
+#if NNRT_SOLVE_ACC_LDS
+	// the wave's 64 accumulator rows are one contiguous block: read and re-zeroed with coalesced 16-B accesses
+	__shared__ __attribute__((aligned(16))) double s_acc[64 * ACC_STRIDE];
+	{
+		const int64_t base = static_cast<int64_t>(blockIdx.x) * 64 * ACC_STRIDE;
+		const int64_t lim = static_cast<int64_t>(a.N) * ACC_STRIDE - base;   // doubles of this wave's rows
+		double2* g2 = reinterpret_cast<double2*>(a.acc + base);
+#pragma unroll
+		for (int i = 0; i < ACC_STRIDE / 2; i++) {
+			const int q = i * 64 + static_cast<int>(threadIdx.x);
+			if (2 * q < lim) {
+				reinterpret_cast<double2*>(s_acc)[q] = g2[q];
+				g2[q] = make_double2(0.0, 0.0);
+			}
+		}
+		__syncthreads();
+	}
+#endif
 	if (n >= a.N) return;
 	float* ns = a.node_state + static_cast<int64_t>(n) * NODE_STRIDE;
 	const float* ns_in = a.state_in + static_cast<int64_t>(n) * NODE_STRIDE;
@@ -939,7 +966,11 @@ __global__ __launch_bounds__(64) void k_solve_update(SolveArgs a) {
 #pragma unroll
 		for (int i = 0; i < 12; i++) old[i] = __builtin_nontemporal_load(ns_in + 3 + i);
 	}
+#if NNRT_SOLVE_ACC_LDS
+	const double* acc = s_acc + threadIdx.x * ACC_STRIDE;
+#else
 	double* acc = a.acc + static_cast<int64_t>(n) * ACC_STRIDE;
+#endif
 	float H[S][S], g[S];
 	int e = 0;
 #pragma unroll
@@ -953,8 +984,10 @@ __global__ __launch_bounds__(64) void k_solve_update(SolveArgs a) {
 		}
 #pragma unroll
 	for (int c = 0; c < S; c++) g[c] = 0.f - static_cast<float>(acc[T::NH + c]);
+#if !NNRT_SOLVE_ACC_LDS
 #pragma unroll
 	for (int k = 0; k < T::NACC; k++) acc[k] = 0.0;
+#endif
 	if (a.hessian_out) {
 #pragma unroll
 		for (int r = 0; r < S; r++)

@@ -8,6 +8,12 @@
 
 namespace nnrt {
 
+#ifndef NNRT_GROUP_PREFETCH
+#define NNRT_GROUP_PREFETCH 1   // pass-2 grouping keeps the entry after each list head in a register
+#endif
+#ifndef NNRT_SOLVE_ACC_LDS
+#define NNRT_SOLVE_ACC_LDS 1   // k_solve_update stages the wave's accumulator rows through LDS (coalesced read + zero)
+#endif
 constexpr int ACC_STRIDE = 28;   // per node: 21 JtJ upper-triangle entries + 6 Jt r (+1 pad); 3-dof modes use 6 + 3
 
 // ARAP (regularized, mode ALL) path
