@@ -1015,8 +1015,144 @@ __global__ __launch_bounds__(64) void k_solve_update(SolveArgs a) {
 	apply_update<MODE>(ns, old, x);
 }
 
+// Eight lanes per node (lane r of the node's group owns row r of H and of its factor L): the same operations as
+// k_solve_update, element for element, in fewer instructions per wave and over 8x the waves.
+//   Factor: column j of L in one step over the group -- lane i forms H_ij - sum_k<j L_ik L_jk (k ascending, row j
+//   broadcast from lane j), lane j's value is the pivot, sqrt on lane j, broadcast, L_ij = t / L_jj on the lanes below.
+//   Solves, Rodrigues and the rotation product: every lane runs cholesky_solve_small / apply_update's operations on
+//   the factor read back from LDS (replicated: one instruction serves all groups), and lane r stores entries r, r + 8.
+// Bit-identical to the one-lane-per-node kernel (the same float operations in the same order).
+constexpr int SOLVE_GL = 8;   // lanes per node
+__device__ __forceinline__ float group_bcast(float v, int j) {   // lane j of each 8-lane group (ds_swizzle bit mode)
+	// and-mask 0x18 keeps the group within the 32-lane half, or-mask j selects the lane: pattern and | or << 5
+	switch (j) {
+		case 0: return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x18 | (0 << 5)));
+		case 1: return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x18 | (1 << 5)));
+		case 2: return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x18 | (2 << 5)));
+		case 3: return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x18 | (3 << 5)));
+		case 4: return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x18 | (4 << 5)));
+		default: return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x18 | (5 << 5)));
+	}
+}
+
+template <int MODE, bool IDENTITY>
+__global__ __launch_bounds__(64) void k_solve_update_lanes(SolveArgs a) {
+	using T = ModeTraits<MODE>;
+	constexpr int S = T::S;
+	constexpr int NPW = 64 / SOLVE_GL;   // nodes per wave
+	__shared__ __attribute__((aligned(16))) double s_acc[NPW * ACC_STRIDE];
+	__shared__ float s_l[NPW][S * S];
+	const int lane = static_cast<int>(threadIdx.x), gl = lane & (SOLVE_GL - 1), grp = lane / SOLVE_GL;
+	const int n = static_cast<int>(blockIdx.x) * NPW + grp;
+	{   // the wave's 8 accumulator rows: one contiguous block, read and re-zeroed with coalesced 16-B accesses
+		const int64_t base = static_cast<int64_t>(blockIdx.x) * NPW * ACC_STRIDE;
+		const int64_t lim = static_cast<int64_t>(a.N) * ACC_STRIDE - base;
+		double2* g2 = reinterpret_cast<double2*>(a.acc + base);
+#pragma unroll
+		for (int q = lane; q < NPW * ACC_STRIDE / 2; q += 64)
+			if (2 * q < lim) {
+				reinterpret_cast<double2*>(s_acc)[q] = g2[q];
+				g2[q] = make_double2(0.0, 0.0);
+			}
+		__syncthreads();
+	}
+	if (n >= a.N) return;   // whole groups: the group_bcast sources stay in the active set
+	float old[12];
+	if constexpr (IDENTITY) {
+#pragma unroll
+		for (int i = 0; i < 12; i++) old[i] = (i == 3 || i == 7 || i == 11) ? 1.f : 0.f;
+	} else {
+		const float* ns_in = a.state_in + static_cast<int64_t>(n) * NODE_STRIDE;
+#pragma unroll
+		for (int i = 0; i < 12; i++) old[i] = ns_in[3 + i];
+	}
+	const double* acc = s_acc + grp * ACC_STRIDE;
+	const int r = gl < S ? gl : S - 1;   // lanes S..7 shadow row S - 1 (their results are never stored)
+	// row r of H (packed upper triangle: entry (c0, c1), c0 <= c1, at c0 S - c0 (c0 - 1) / 2 + c1 - c0)
+	float h[S];
+#pragma unroll
+	for (int c = 0; c < S; c++) {
+		const int c0 = c < r ? c : r, c1 = c < r ? r : c;
+		h[c] = static_cast<float>(acc[c0 * S - (c0 * (c0 - 1)) / 2 + (c1 - c0)]);
+	}
+	const float gr = 0.f - static_cast<float>(acc[T::NH + r]);
+	if (gl < S) {
+		if (a.hessian_out) {
+#pragma unroll
+			for (int c = 0; c < S; c++) a.hessian_out[static_cast<int64_t>(n) * S * S + r * S + c] = h[c];
+		}
+		a.gradient_out[static_cast<int64_t>(n) * S + r] = gr;
+	}
+	if (a.lm > 0.f) {
+#pragma unroll
+		for (int c = 0; c < S; c++)
+			if (c == r) h[c] += a.lm;
+	}
+	// factor: lane r holds L_r0 .. L_rr in h[0 .. r]
+	bool bad = false;
+#pragma unroll
+	for (int j = 0; j < S; j++) {
+		float t = h[j];
+#pragma unroll
+		for (int k = 0; k < j; k++) {
+			const float ljk = group_bcast(h[k], j);   // L_jk
+			t -= h[k] * ljk;
+		}
+		const bool pos = group_bcast(t, j) > 0.f;   // the pivot test on lane j's value (uniform over the group)
+		bad |= !pos;
+		const float l = group_bcast(sqrtf(t), j);
+		if (r == j) h[j] = l;
+		else if (r > j) h[j] = t / l;
+	}
+	float* Lm = s_l[grp];
+	if (gl < S) {
+#pragma unroll
+		for (int c = 0; c < S; c++) Lm[r * S + c] = c <= r ? h[c] : 0.f;
+	}
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+	float L[S][S], x[S];
+#pragma unroll
+	for (int i = 0; i < S; i++)
+#pragma unroll
+		for (int c = 0; c < S; c++) L[i][c] = Lm[i * S + c];
+#pragma unroll
+	for (int c = 0; c < S; c++) x[c] = group_bcast(gr, c);   // g
+	if (bad) {
+		if (gl == 0) atomicOr(a.error_flag, 1);
+#pragma unroll
+		for (int c = 0; c < S; c++) x[c] = NAN;
+	} else {
+		cholesky_solve_small<S>(L, x);
+	}
+	float xr = x[0];
+#pragma unroll
+	for (int c = 1; c < S; c++) xr = r == c ? x[c] : xr;
+	if (gl < S) a.updates_out[static_cast<int64_t>(n) * S + r] = xr;
+	float o[15];
+	apply_update<MODE>(o, old, x);   // o[3 .. 14]: the node's new (t, R)
+	float* ns = a.node_state + static_cast<int64_t>(n) * NODE_STRIDE;
+	float v0 = o[3], v1 = o[11];
+#pragma unroll
+	for (int c = 1; c < 8; c++) v0 = gl == c ? o[3 + c] : v0;
+#pragma unroll
+	for (int c = 1; c < 4; c++) v1 = gl == c ? o[11 + c] : v1;
+	ns[3 + gl] = v0;
+	if (gl < 4) ns[11 + gl] = v1;
+}
+
 template <bool IDENTITY>
 static nnrt_status solve_update_mode(int mode, const SolveArgs& args, hipStream_t stream) {
+#if NNRT_SOLVE_LANES
+	const unsigned grid = static_cast<unsigned>(ceil_div(args.N, 64 / SOLVE_GL));   // one wave per workgroup, 8 nodes per wave
+	switch (mode) {
+		case NNRT_ITERATION_ALL: k_solve_update_lanes<NNRT_ITERATION_ALL, IDENTITY><<<grid, 64, 0, stream>>>(args); break;
+		case NNRT_ITERATION_TRANSLATION_ONLY: k_solve_update_lanes<NNRT_ITERATION_TRANSLATION_ONLY, IDENTITY><<<grid, 64, 0, stream>>>(args); break;
+		case NNRT_ITERATION_ROTATION_ONLY: k_solve_update_lanes<NNRT_ITERATION_ROTATION_ONLY, IDENTITY><<<grid, 64, 0, stream>>>(args); break;
+		default: set_error("unknown iteration mode"); return NNRT_ERROR_ARGUMENT;
+	}
+#else
 	const unsigned grid = static_cast<unsigned>(ceil_div(args.N, 64));   // one wave per workgroup: more CUs take part
 	switch (mode) {
 		case NNRT_ITERATION_ALL: k_solve_update<NNRT_ITERATION_ALL, IDENTITY><<<grid, 64, 0, stream>>>(args); break;
@@ -1024,6 +1160,7 @@ static nnrt_status solve_update_mode(int mode, const SolveArgs& args, hipStream_
 		case NNRT_ITERATION_ROTATION_ONLY: k_solve_update<NNRT_ITERATION_ROTATION_ONLY, IDENTITY><<<grid, 64, 0, stream>>>(args); break;
 		default: set_error("unknown iteration mode"); return NNRT_ERROR_ARGUMENT;
 	}
+#endif
 	return NNRT_OK;
 }
 

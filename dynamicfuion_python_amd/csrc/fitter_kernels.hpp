@@ -11,6 +11,9 @@ namespace nnrt {
 #ifndef NNRT_GROUP_PREFETCH
 #define NNRT_GROUP_PREFETCH 1   // pass-2 grouping keeps the entry after each list head in a register
 #endif
+#ifndef NNRT_SOLVE_LANES
+#define NNRT_SOLVE_LANES 1   // block-diagonal solve + update with 8 lanes per node (k_solve_update_lanes)
+#endif
 #ifndef NNRT_SOLVE_ACC_LDS
 #define NNRT_SOLVE_ACC_LDS 1   // k_solve_update stages the wave's accumulator rows through LDS (coalesced read + zero)
 #endif

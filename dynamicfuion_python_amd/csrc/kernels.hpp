@@ -129,7 +129,15 @@ __device__ inline void rodrigues_device(float w0, float w1, float w2, float* R) 
 	const float ang = sqrtf((w0 * w0 + w1 * w1) + w2 * w2);
 	const float ax = w0 / ang, ay = w1 / ang, az = w2 / ang;
 	const float Km[3][3] = {{0.f, -az, ay}, {az, 0.f, -ax}, {-ay, ax, 0.f}};
+#ifdef __HIP_DEVICE_COMPILE__
+	// one shared argument reduction for both (the device library's sin and cos evaluate the same reduction and
+	// polynomials: bit-identical to sin_cr / cos_cr)
+	double sd, cd;
+	sincos(static_cast<double>(ang), &sd, &cd);
+	const float s = static_cast<float>(sd), c1 = 1 - static_cast<float>(cd);
+#else
 	const float s = sin_cr(ang), c1 = 1 - cos_cr(ang);
+#endif
 #pragma unroll
 	for (int r = 0; r < 3; r++) {
 #pragma unroll
