@@ -303,6 +303,37 @@ def test_fit_one_iteration_parity(nn, S, oracle_mod, name):
     assert rel_err(wf.get_node_rotations(True) - np.eye(3), R_o - np.eye(3)) < 1e-4
 
 
+@pytest.mark.parametrize("name,mode", [("C2", "ALL"), ("C1", "TRANSLATION_ONLY"), ("C1", "ROTATION_ONLY")])
+def test_block_diagonal_update_bit_exact(nn, S, oracle_mod, name, mode):
+    """The block-diagonal solve + update (k_solve_update_lanes: 8 lanes per node, lane r forming row r of the factor)
+    performs the one-lane potrf + potrs float operations in the same order: on the GPU's own H and g, its updates equal
+    the oracle's float block solve (orc_solve_block_diagonal; SolveBlockDiagonalCholeskyCUDA.cpp:59-100) bit for bit,
+    and the node motion from identity equals t = 0 + dt, R = I . Rodrigues(w) (RodriguesImpl.h:66-88, A10) exactly."""
+    sc = _scene(S, oracle_mod, name)
+    depth = scene_target(oracle_mod, sc)
+    wf, ft, dg = _gpu_fit(nn, sc, depth, 1, modes=[getattr(nn.alignment.IterationMode, mode)])
+    s, N = (6 if mode == "ALL" else 3), len(sc.nodes)
+    H = np.asarray(dg["hessian"][: N * s * s], np.float32).reshape(N, s, s)
+    g = np.asarray(dg["gradient"][: N * s], np.float32)
+    x_o, _ = oracle_mod.solve_block_diagonal(H, g, lm=0.001)
+    x_g = np.asarray(dg["updates"][: N * s], np.float32)
+    assert np.array_equal(x_g, x_o, equal_nan=True)
+    x = x_g.reshape(N, s)
+    t_g, R_g = wf.get_node_translations(True), wf.get_node_rotations(True)
+    if mode == "ALL":
+        assert np.array_equal(t_g, np.float32(0) + x[:, 3:], equal_nan=True)
+    elif mode == "TRANSLATION_ONLY":
+        assert np.array_equal(t_g, np.float32(0) + x, equal_nan=True)
+    if mode != "TRANSLATION_ONLY":
+        dR = oracle_mod.rodrigues(np.ascontiguousarray(x[:, :3])).reshape(N, 3, 3)
+        I3 = np.eye(3, dtype=np.float32)
+        R_e = np.empty_like(dR)
+        for r in range(3):
+            for c in range(3):
+                R_e[:, r, c] = (I3[r, 0] * dR[:, 0, c] + I3[r, 1] * dR[:, 1, c]) + I3[r, 2] * dR[:, 2, c]
+        assert np.array_equal(R_g.reshape(N, 3, 3), R_e, equal_nan=True)
+
+
 @pytest.mark.parametrize("name,k", [("S1", 1), ("S1", 3), ("C1", 6), ("C1", 8)])
 def test_fit_anchor_count_parity(nn, S, oracle_mod, name, k):
     """FitToImage with anchor counts other than the common 4 (the warp field's anchor_count,
