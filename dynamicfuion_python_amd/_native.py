@@ -80,6 +80,7 @@ _SIGNATURES = {
     "nnrt_fitter_iterate_timed": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     "nnrt_fitter_time_kernels": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p]),
     "nnrt_fitter_refine_info": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "nnrt_fitter_set_refine_ratio": (c_int32, [c_void_p, c_float]),
     "nnrt_fitter_check": (c_int32, [c_void_p, c_void_p]),
     "nnrt_fitter_get_diagnostics": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "nnrt_fitter_get_anchors": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p]),

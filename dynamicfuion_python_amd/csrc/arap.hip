@@ -637,10 +637,10 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 		return NNRT_OK;
 	}
 	// gated iterative refinement (one step): the corner factorization left its smallest pivot / diag(S) ratio on the
-	// device; below NNRT_REFINE_PIVOT_RATIO the next launches form res = rhs - H x (double sums) and solve H d = res with the
+	// device; below ws.refine_ratio the next launches form res = rhs - H x (double sums) and solve H d = res with the
 	// same factors, x += d; otherwise the first pass applies the update and the others return at once
 	const unsigned* gate = ws.corner->pivot_ratio();
-	const float ratio = NNRT_REFINE_PIVOT_RATIO;
+	const float ratio = ws.refine_ratio;
 	k_arrow_back<<<static_cast<unsigned>(ceil_div(ws.N, 64)), 64, 0, stream>>>(ws.n0, ws.N, ws.dinv, ws.edge_offsets, ws.edge_list, edges, wing,
 	                                                                          ws.rhs, ws.x, state_in, node_state, updates_out, nullptr, gate, ratio, 1,
 	                                                                          ws.diag, ws.res);

@@ -395,6 +395,7 @@ struct nnrt_fitter {
 	DeviceBuffer<int> a_offsets, a_list, a_tgt_off, a_rhs_off, a_rhs_edges, a_inc_off, a_inc_list;
 	DeviceBuffer<int2> a_tgt_ab, a_pairs;
 	ArrowheadWorkspace aw;
+	float refine_ratio = NNRT_REFINE_PIVOT_RATIO;   // refinement gate threshold (nnrt_fitter_set_refine_ratio)
 	int n0 = 0;
 	int last_mode = 0;
 	DeviceBuffer<float> snapshot;   // [N,16] node state stored by nnrt_fitter_snapshot_motion (restore-before-iteration runs)
@@ -791,6 +792,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 		ft->aw.rhs = ft->a_rhs.ptr;
 		ft->aw.x = ft->a_x.ptr;
 		ft->aw.refine = NNRT_ARAP_REFINE != 0;
+		ft->aw.refine_ratio = ft->refine_ratio;
 		ft->aw.res = ft->a_res.ptr;
 		ft->aw.dx = ft->a_dx.ptr;
 		ft->aw.edge_offsets = ft->a_offsets.ptr;
@@ -1044,7 +1046,7 @@ nnrt_status nnrt_fitter_refine_info(nnrt_fitter* ft, float* h_out, void* stream)
 	NNRT_CHECK_ARG(ft && h_out, "null pointer");
 	DeviceGuard guard(ft->device);
 	h_out[0] = 1.f;
-	h_out[1] = NNRT_REFINE_PIVOT_RATIO;
+	h_out[1] = ft->refine_ratio;
 	h_out[2] = 0.f;
 	if (ft->E > 0 && ft->corner.pivot_ratio()) {
 		NNRT_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
@@ -1054,8 +1056,20 @@ nnrt_status nnrt_fitter_refine_info(nnrt_fitter* ft, float* h_out, void* stream)
 		float r;
 		std::memcpy(&r, &bits, sizeof(r));
 		h_out[0] = r;
-		h_out[2] = (NNRT_ARAP_REFINE != 0 && r < NNRT_REFINE_PIVOT_RATIO) ? 1.f : 0.f;
+		h_out[2] = (NNRT_ARAP_REFINE != 0 && r < ft->refine_ratio) ? 1.f : 0.f;
 	}
+	return NNRT_OK;
+}
+
+nnrt_status nnrt_fitter_set_refine_ratio(nnrt_fitter* ft, float ratio) {
+	NNRT_CHECK_ARG(ft, "null pointer");
+	NNRT_CHECK_ARG(ratio >= 0.f, "refine ratio must be >= 0 (0: never refine)");
+	if (ratio == ft->refine_ratio) return NNRT_OK;
+	DeviceGuard guard(ft->device);
+	NNRT_HIP(hipStreamSynchronize(ft->work));
+	ft->refine_ratio = ratio;
+	ft->aw.refine_ratio = ratio;
+	ft->drop_graphs();   // the threshold is a launch argument of the captured sequences
 	return NNRT_OK;
 }
 

@@ -337,6 +337,7 @@ struct ArrowheadWorkspace {
 	// iterative refinement (refine: one step after the first solve): res [6N] = rhs - H x (fp64 sums, rounded), dx [6N]
 	// the correction; the update is x + dx
 	bool refine = false;
+	float refine_ratio = NNRT_REFINE_PIVOT_RATIO;   // gate threshold on the corner's min pivot / diag(S)
 	float* res = nullptr;
 	float* dx = nullptr;
 	int* edge_offsets = nullptr;// [n0+1] CSR of stem edges by source node (edges grouped by source)

@@ -152,6 +152,9 @@ nnrt_status nnrt_fitter_corner_info(const nnrt_fitter* fitter, int64_t* h_out);
  * smallest pivot / diag(S) ratio (1 without ARAP), the threshold below which one step of iterative refinement runs, and
  * 1 if it ran. */
 nnrt_status nnrt_fitter_refine_info(nnrt_fitter* fitter, float* h_out, void* stream);
+/* Threshold of the refinement gate (default 1e-2): the arrowhead solve refines when the corner's smallest pivot /
+ * diag(S) ratio falls below it; 0 never refines, +inf always. Drops the fitter's cached graphs (a launch argument). */
+nnrt_status nnrt_fitter_set_refine_ratio(nnrt_fitter* fitter, float ratio);
 /* Store the warp field's current node motion (R, t) in the fitter (a device copy on `stream`). */
 nnrt_status nnrt_fitter_snapshot_motion(nnrt_fitter* fitter, nnrt_warp_field* warp_field, void* stream);
 /* Benchmark form of iterate() that runs the general (non-identity) kernels: before every iteration the warp field's

@@ -555,6 +555,65 @@ def test_fit_state_synchronised_trajectory(nn, S, oracle_mod, name, iterations, 
         assert report[-1][1] == "potrf" and report[-1][0] == fails_at
 
 
+@pytest.mark.parametrize("name,iterations", [("C1_ARAP", 4), ("C2_ARAP", 5), ("C5", 4)])
+def test_refinement_gate(nn, S, oracle_mod, name, iterations):
+    """The arrowhead solve's refinement gate (one step of iterative refinement when the corner factorization's smallest
+    pivot / diag(S) falls below the threshold) against what refinement buys. Along the GPU's own
+    trajectory every iteration is solved twice from the same motion, the gate forced shut (threshold 0) and forced open
+    (inf), and both are compared with the fp64 solution of that iteration's normal equations (the GPU's data blocks and
+    right-hand side, identical in both runs). Where the product gate stays shut the plain f32 solve must already meet
+    1e-4; where it opens and the fp64 pivot ratio exceeds REFINE_PIVOT_RATIO the refined solve must."""
+    import scipy.sparse.linalg as spl
+    from dynamicfuion_python_amd._native import NnrtError
+    sc = _scene(S, oracle_mod, name)
+    depth = scene_target(oracle_mod, sc)
+    N = len(sc.nodes)
+    wf, ft = _new_fit(nn, sc, depth, iterations)
+    threshold = ft.refine_info()["threshold"]
+
+    def solve(R0, t0, k, ratio):
+        wf.set_node_rotations(R0, True)
+        wf.set_node_translations(t0, True)
+        ft.set_refine_ratio(ratio)
+        ft.iterate(wf, k, 1)
+        try:
+            ft.check()
+        except NnrtError:
+            return None
+        dg = ft.diagnostics()
+        info = ft.refine_info()
+        return dg["updates"][: 6 * N].copy(), dg["hessian"][: 36 * N].copy(), dg["gradient"][: 6 * N].copy(), info["pivot_ratio"]
+
+    rows = []
+    for k in range(iterations):
+        R0, t0 = wf.get_node_rotations(True), wf.get_node_translations(True)
+        if not np.isfinite(R0).all():
+            break   # A7 NaN rotations: the systems from here on are degenerate
+        plain = solve(R0, t0, k, 0.0)
+        refined = solve(R0, t0, k, np.inf)
+        if plain is None or refined is None:
+            break
+        assert np.array_equal(plain[1], refined[1]) and np.array_equal(plain[2], refined[2])
+        assert plain[3] == refined[3]   # the same factorization
+        A, b = arrowhead_fp64_system(oracle_mod, sc, R0, t0, hessian_diag=plain[1], gradient=plain[2])
+        x64 = spl.spsolve(A.tocsc(), b)
+        ratio64 = fp64_pivot_ratio(A)
+        e_plain, e_ref = nan_rel_err(plain[0], x64), nan_rel_err(refined[0], x64)
+        gate = plain[3]
+        rows.append((k + 1, gate, ratio64, e_plain, e_ref))
+        print(f"{name} iteration {k + 1}: corner pivot / diag(S) {gate:.3g} (gate {'open' if gate < threshold else 'shut'} at "
+              f"{threshold:g}), fp64 pivot ratio {ratio64:.3g}, err vs fp64: plain f32 {e_plain:.3g}, refined {e_ref:.3g}", flush=True)
+        if gate >= threshold:
+            assert e_plain <= 1e-4, f"iteration {k + 1}: gate shut at {gate:.3g} but the plain solve is {e_plain:.3g} from fp64"
+        elif ratio64 > REFINE_PIVOT_RATIO:
+            assert e_ref <= 1e-4, f"iteration {k + 1}: refined solve {e_ref:.3g} from fp64 at fp64 pivot ratio {ratio64:.3g}"
+        if gate >= threshold:   # continue along the product's trajectory
+            solve(R0, t0, k, 0.0)
+    ft.set_refine_ratio(threshold)
+    print(f"{name}: {rows}")
+    assert len(rows) >= 2
+
+
 def test_fit_c2_from_stored_states(nn, S, oracle_mod):
     """C2 GN iterations from ten non-identity node states (fractions of the ground-truth motion plus noise: the
     states a frame passes through between the identity and the solution) -- the general warp / update kernels on a
