@@ -37,7 +37,27 @@ int main(int argc, char** argv) {
 			for (int q = 0; q < ch.y; q++) { ent += p.back_cols[ch.x + q].z; maxent = std::max(maxent, p.back_cols[ch.x + q].z); }
 			sument += ent;
 		}
-		printf("back %zu: chains %3d columns %3d longest chain %3d entries/col max %3d total %4d\n", l, p.back_off[l + 1] - p.back_off[l], totcols, maxlen, maxent, sument);
+		// entries whose I lies in the same chain (x produced inside the launch) vs earlier launches; per chain, the
+		// tiles the chain's workgroup reads in order (entries + one L_JJ^-1 per column)
+		int inchain = 0, maxchain_tiles = 0, maxchain_inner = 0;
+		for (int c = p.back_off[l]; c < p.back_off[l + 1]; c++) {
+			const int2 ch = p.back_chains[c];
+			int tiles = 0, inner = 0;
+			for (int q = 0; q < ch.y; q++) {
+				const int4 bc = p.back_cols[ch.x + q];
+				tiles += bc.z + 1;
+				for (int e = 0; e < bc.z; e++) {
+					const int I = p.back_ent[bc.y + e].y;
+					for (int q2 = 0; q2 < q; q2++)
+						if (p.back_cols[ch.x + q2].x == I) { inchain++; inner++; }
+				}
+				inner++;
+			}
+			maxchain_tiles = std::max(maxchain_tiles, tiles);
+			maxchain_inner = std::max(maxchain_inner, inner);
+		}
+		printf("back %zu: chains %3d columns %3d longest chain %3d entries/col max %3d total %4d in-chain %4d; heaviest chain %d tiles (%d on the chain's path)\n", l,
+		       p.back_off[l + 1] - p.back_off[l], totcols, maxlen, maxent, sument, inchain, maxchain_tiles, maxchain_inner);
 	}
 	// the longest root-to-leaf path: columns and entries along it
 	return 0;
