@@ -234,14 +234,19 @@ struct CornerPlan {
 	std::vector<int4> srcs;           // (slot X, slot Y, column k, 0): X Y^T update terms; rhs term L_k y_k uses X and k
 	std::vector<int> back_off;        // [launches + 1] back-substitution chains per launch
 	std::vector<int2> back_chains;    // (first column entry, column count): a chain of the elimination tree, root end first
-	std::vector<int4> back_cols;      // (J, entry offset, entry count, 1 if L_JJ^-1 is formed: every column below the top level)
-	std::vector<int2> back_ent;       // (slot of L_IJ, I)
+	std::vector<int4> back_cols;      // (J, entry offset, entry count, outside entries)
+	std::vector<int2> back_ent;       // (slot of L_IJ, I): per column the entries whose I lies outside the column's chain
+	                                  // (x from earlier launches) first, then those inside it
+	std::vector<int> back_pre_off;    // [launches + 1] per launch, its columns with outside entries (pre-sum launches)
+	std::vector<int2> back_pre;       // (column index into back_cols, 1)
 	// forward substitution L y = b (iterative refinement): the back chains in reverse (deepest launch first, each chain
 	// from its bottom column up); per column its row entries (slot of L_Jk, k), k < J
 	std::vector<int> fwd_off;
 	std::vector<int2> fwd_chains;     // (first column entry, column count)
-	std::vector<int4> fwd_cols;       // (J, entry offset, entry count, 1 if L_JJ^-1 is formed)
-	std::vector<int2> fwd_ent;        // (slot of L_Jk, k)
+	std::vector<int4> fwd_cols;       // (J, entry offset, entry count, outside entries)
+	std::vector<int2> fwd_ent;        // (slot of L_Jk, k): outside the column's chain first, then inside
+	std::vector<int> fwd_pre_off;
+	std::vector<int2> fwd_pre;
 	// single-workgroup walks (k_corner_walk): per stream element (array: 0 tiles slot / 1 L_JJ^-1 / 2 L_JJ, index, x_off,
 	// info); back: columns T-1 .. 0, each its entries L_IJ (ascending I) then its head; forward: columns 0 .. T-1, each its
 	// row entries L_Jk (ascending k) then its head
@@ -423,18 +428,28 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 	}
 	int depth_max = 0;
 	for (int d : chain_depth) depth_max = std::max(depth_max, d);
+	std::vector<int> chain_of(static_cast<size_t>(T), -1);
+	for (size_t c = 0; c < chain_cols.size(); c++)
+		for (int J : chain_cols[c]) chain_of[static_cast<size_t>(J)] = static_cast<int>(c);
 	p.back_off.push_back(0);
+	p.back_pre_off.push_back(0);
 	for (int d = 0; d <= depth_max; d++) {
 		for (size_t c = 0; c < chain_cols.size(); c++) {
 			if (chain_depth[c] != d) continue;
 			p.back_chains.push_back(make_int2(static_cast<int>(p.back_cols.size()), static_cast<int>(chain_cols[c].size())));
 			for (int J : chain_cols[c]) {
 				const auto& cc = cs[static_cast<size_t>(J)];
-				p.back_cols.push_back(make_int4(J, static_cast<int>(p.back_ent.size()), static_cast<int>(cc.size()), 1));
-				for (int I : cc) p.back_ent.push_back(make_int2(slot(I, J), I));
+				int outside = 0;
+				for (int I : cc) outside += chain_of[static_cast<size_t>(I)] != static_cast<int>(c);
+				if (outside > 0) p.back_pre.push_back(make_int2(static_cast<int>(p.back_cols.size()), 1));
+				p.back_cols.push_back(make_int4(J, static_cast<int>(p.back_ent.size()), static_cast<int>(cc.size()), outside));
+				for (int pass = 0; pass < 2; pass++)
+					for (int I : cc)
+						if ((chain_of[static_cast<size_t>(I)] == static_cast<int>(c)) == (pass == 1)) p.back_ent.push_back(make_int2(slot(I, J), I));
 			}
 		}
 		p.back_off.push_back(static_cast<int>(p.back_chains.size()));
+		p.back_pre_off.push_back(static_cast<int>(p.back_pre.size()));
 	}
 	// single-workgroup walk streams
 	{
@@ -456,18 +471,26 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 	for (size_t sl = 0; sl < p.slot_ij.size(); sl++)
 		if (p.slot_ij[sl].x != p.slot_ij[sl].y) rows[static_cast<size_t>(p.slot_ij[sl].x)].push_back(make_int2(static_cast<int>(sl), p.slot_ij[sl].y));
 	p.fwd_off.push_back(0);
+	p.fwd_pre_off.push_back(0);
 	for (int l = static_cast<int>(p.back_off.size()) - 2; l >= 0; l--) {
 		for (int c = p.back_off[static_cast<size_t>(l)]; c < p.back_off[static_cast<size_t>(l) + 1]; c++) {
 			const int2 ch = p.back_chains[static_cast<size_t>(c)];
 			p.fwd_chains.push_back(make_int2(static_cast<int>(p.fwd_cols.size()), ch.y));
 			for (int q = ch.y - 1; q >= 0; q--) {
 				const int4 bc = p.back_cols[static_cast<size_t>(ch.x + q)];
+				const int own = chain_of[static_cast<size_t>(bc.x)];
 				const auto& rw = rows[static_cast<size_t>(bc.x)];
-				p.fwd_cols.push_back(make_int4(bc.x, static_cast<int>(p.fwd_ent.size()), static_cast<int>(rw.size()), bc.w));
-				p.fwd_ent.insert(p.fwd_ent.end(), rw.begin(), rw.end());
+				int outside = 0;
+				for (const int2& e : rw) outside += chain_of[static_cast<size_t>(e.y)] != own;
+				if (outside > 0) p.fwd_pre.push_back(make_int2(static_cast<int>(p.fwd_cols.size()), 1));
+				p.fwd_cols.push_back(make_int4(bc.x, static_cast<int>(p.fwd_ent.size()), static_cast<int>(rw.size()), outside));
+				for (int pass = 0; pass < 2; pass++)
+					for (const int2& e : rw)
+						if ((chain_of[static_cast<size_t>(e.y)] == own) == (pass == 1)) p.fwd_ent.push_back(e);
 			}
 		}
 		p.fwd_off.push_back(static_cast<int>(p.fwd_chains.size()));
+		p.fwd_pre_off.push_back(static_cast<int>(p.fwd_pre.size()));
 	}
 	return p;
 }
@@ -855,9 +878,15 @@ struct CornerBackArgs {
 	const int* row_node;
 	float* xout;             // [6 nc] x in node order
 	const int2* chains;      // this launch's chains (first column, column count)
-	const int4* cols;        // (J, entry offset, entry count, 0), each chain root end first
+	const int4* cols;        // (J, entry offset, entry count, outside entries), each chain root end first
 	const int2* ent;         // (slot of L_IJ, I)
+	float* zx;               // [ld] pre-sums y_J - sum over the outside entries (modes 1, 2)
+	int mode;                // 0: every entry; 1: pre-sum launch (outside entries -> zx); 2: inside entries from zx
 };
+// the entries a column's pass reads (offset, count) and where its y comes from, per substitution mode
+__device__ __forceinline__ int2 subst_span(const int4& c, int mode) {
+	return mode == 2 ? make_int2(c.y + c.w, c.z - c.w) : mode == 1 ? make_int2(c.y, c.w) : make_int2(c.y, c.z);
+}
 
 // Back substitution L^T x = y along chains of the elimination tree (one workgroup per chain, its columns in order; the
 // launches run from the root's chain down). Per column J: z = y_J - sum_I L_IJ^T x_I (each wave a quarter of every tile's
@@ -893,30 +922,32 @@ __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 		if (t < nq) s_cols[t] = a.cols[ch.x + q0 + t];
 		__syncthreads();
 		if (wave == 1) {
-			const int4 c0 = s_cols[0];
-			s_ent[0][lane] = lane < c0.z ? a.ent[c0.y + lane] : make_int2(0, 0);
+			const int2 sp0 = subst_span(s_cols[0], a.mode);
+			s_ent[0][lane] = lane < sp0.y ? a.ent[sp0.x + lane] : make_int2(0, 0);
 		}
 		__syncthreads();
 		for (int q = 0; q < nq; q++) {
 			const int4 col = s_cols[q];
 			const int J = col.x;
+			const int2 sp = subst_span(col, a.mode);
 			// M = L_JJ^-1 streams into LDS behind the entry loads; y_J is loaded ahead of the sums (wave 0)
-			tile_to_lds(a.minv + static_cast<int64_t>(J) * TILE_ELEMS, s_m, wave, lane);
-			const float yv = wave == 0 ? a.cb[static_cast<int64_t>(J) * TILE + lane] : 0.f;
+			if (a.mode != 1) tile_to_lds(a.minv + static_cast<int64_t>(J) * TILE_ELEMS, s_m, wave, lane);
+			const float* ysrc = a.mode == 2 && col.w > 0 ? a.zx : a.cb;
+			const float yv = wave == 0 ? ysrc[static_cast<int64_t>(J) * TILE + lane] : 0.f;
 			const bool has_next = q + 1 < nq;
 			int2 nxt = make_int2(0, 0);
 			if (wave == 1 && has_next) {
-				const int4 cn = s_cols[q + 1];
-				if (lane < cn.z) nxt = a.ent[cn.y + lane];
+				const int2 spn = subst_span(s_cols[q + 1], a.mode);
+				if (lane < spn.y) nxt = a.ent[spn.x + lane];
 			}
 			// z partials: lane (row group rq, column group cg) covers rows 16 wave + 4 rq .. + 3 and columns 4 cg .. 4 cg + 3
 			// of every entry tile (four 16-B row loads and one 16-B x load per tile), BACK_BATCH tiles' loads in flight; the
 			// row groups are then summed across lanes
 			const int cg = lane & 15, rq = lane >> 4;
 			float acc[4] = {0.f, 0.f, 0.f, 0.f};
-			for (int e0 = 0; e0 < col.z; e0 += 64) {
-				const int ne = col.z - e0 < 64 ? col.z - e0 : 64;
-				const int2 mine = e0 == 0 ? s_ent[q & 1][lane] : lane < ne ? a.ent[col.y + e0 + lane] : make_int2(0, 0);
+			for (int e0 = 0; e0 < sp.y; e0 += 64) {
+				const int ne = sp.y - e0 < 64 ? sp.y - e0 : 64;
+				const int2 mine = e0 == 0 ? s_ent[q & 1][lane] : lane < ne ? a.ent[sp.x + e0 + lane] : make_int2(0, 0);
 				for (int e = 0; e < ne; e += BACK_BATCH) {
 					float4 l[BACK_BATCH][4], xv[BACK_BATCH];
 #pragma unroll
@@ -950,7 +981,9 @@ __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 			}
 			if (lane < 16) *reinterpret_cast<float4*>(&s_part[wave][4 * lane]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
 			__syncthreads();   // also retires the M tile's LDS-DMA pieces of every wave
-			if (wave == 0) {
+			if (wave == 0 && a.mode == 1) {
+				a.zx[static_cast<int64_t>(J) * TILE + lane] = yv - ((s_part[0][lane] + s_part[1][lane]) + (s_part[2][lane] + s_part[3][lane]));
+			} else if (wave == 0) {
 				// x_c = sum_r M_rc z_r, z_r broadcast from lane r; column c of M from LDS (conflict-free); four partial sums
 				const float z = yv - ((s_part[0][lane] + s_part[1][lane]) + (s_part[2][lane] + s_part[3][lane]));
 				float xs[4] = {0.f, 0.f, 0.f, 0.f};
@@ -982,8 +1015,10 @@ struct CornerFwdArgs {
 	const float* minv;
 	float* yb;               // [ld] b in, y out (permuted order)
 	const int2* chains;
-	const int4* cols;        // (J, entry offset, entry count, 1 if L_JJ^-1 is formed)
+	const int4* cols;        // (J, entry offset, entry count, outside entries)
 	const int2* ent;         // (slot of L_Jk, k)
+	float* zx;               // [ld] pre-sums (modes 1, 2; as CornerBackArgs)
+	int mode;
 };
 __global__ __launch_bounds__(CT) void k_corner_fwd(CornerFwdArgs a) {
 	__shared__ __attribute__((aligned(16))) float s_m[TILE_ELEMS];   // L_JJ^-1 of the current column
@@ -995,11 +1030,12 @@ __global__ __launch_bounds__(CT) void k_corner_fwd(CornerFwdArgs a) {
 	for (int q = 0; q < ch.y; q++) {
 		const int4 col = a.cols[ch.x + q];
 		const int J = col.x;
-		tile_to_lds(a.minv + static_cast<int64_t>(J) * TILE_ELEMS, s_m, wave, lane);   // behind the entry loads
+		const int2 sp = subst_span(col, a.mode);
+		if (a.mode != 1) tile_to_lds(a.minv + static_cast<int64_t>(J) * TILE_ELEMS, s_m, wave, lane);   // behind the entry loads
 		float acc[4] = {0.f, 0.f, 0.f, 0.f};   // rows 16 wave + 4 rq + k, partial over this lane's 4 columns
-		for (int e0 = 0; e0 < col.z; e0 += 64) {
-			const int ne = col.z - e0 < 64 ? col.z - e0 : 64;
-			const int2 mine = lane < ne ? a.ent[col.y + e0 + lane] : make_int2(0, 0);
+		for (int e0 = 0; e0 < sp.y; e0 += 64) {
+			const int ne = sp.y - e0 < 64 ? sp.y - e0 : 64;
+			const int2 mine = lane < ne ? a.ent[sp.x + e0 + lane] : make_int2(0, 0);
 			for (int e = 0; e < ne; e += BACK_BATCH) {
 				float4 l[BACK_BATCH][4], yv[BACK_BATCH];
 #pragma unroll
@@ -1024,13 +1060,17 @@ __global__ __launch_bounds__(CT) void k_corner_fwd(CornerFwdArgs a) {
 		for (int k = 0; k < 4; k++)
 #pragma unroll
 			for (int m = 1; m < 16; m <<= 1) acc[k] += __shfl_xor(acc[k], m);
+		const float* ysrc = a.mode == 2 && col.w > 0 ? a.zx : a.yb;
 		if (cg == 0) {
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
 				const int r = 16 * wave + 4 * rq + k;
-				s_z[r] = a.yb[static_cast<int64_t>(J) * TILE + r] - acc[k];
+				const float z = ysrc[static_cast<int64_t>(J) * TILE + r] - acc[k];
+				if (a.mode == 1) a.zx[static_cast<int64_t>(J) * TILE + r] = z;
+				else s_z[r] = z;
 			}
 		}
+		if (a.mode == 1) continue;   // pre-sum launch: one column per workgroup, no barrier needed
 		__syncthreads();   // z complete; the M tile's LDS-DMA pieces of every wave retired
 		{   // y_r = sum_c M_rc z_c: the same row / column-group split, summed across the 16 column groups
 			const float4 z4 = *reinterpret_cast<const float4*>(&s_z[4 * cg]);
@@ -1310,8 +1350,11 @@ void CornerSolver::release() {
 	                 reinterpret_cast<void**>(&xp), reinterpret_cast<void**>(&d_tile_slot), reinterpret_cast<void**>(&d_slot_ij),
 	                 reinterpret_cast<void**>(&d_row_node), reinterpret_cast<void**>(&d_node_row), reinterpret_cast<void**>(&d_tasks),
 	                 reinterpret_cast<void**>(&d_srcs), reinterpret_cast<void**>(&d_back_cols), reinterpret_cast<void**>(&d_back_ent), reinterpret_cast<void**>(&d_back_chains),
-	                 reinterpret_cast<void**>(&d_corner_edges)})
+	                 reinterpret_cast<void**>(&d_corner_edges), reinterpret_cast<void**>(&zx), reinterpret_cast<void**>(&d_back_pre),
+	                 reinterpret_cast<void**>(&d_fwd_pre)})
 		dev_free(*p);
+	back_pre_off.clear();
+	fwd_pre_off.clear();
 	nc = ld = T = H = slots = n_corner_edges = 0;
 	level_off.clear();
 	level_panel.clear();
@@ -1349,13 +1392,14 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		if ((st = alloc(tiles, p.slot_ij.size() * TILE_ELEMS)) || (st = alloc(ldiag, static_cast<size_t>(p.T) * TILE_ELEMS)) ||
 		    (st = alloc(minv, static_cast<size_t>(p.T) * TILE_ELEMS)) || (st = alloc(cb2, static_cast<size_t>(p.ld))) ||
 		    (st = alloc(sdiag, static_cast<size_t>(p.ld))) || (st = alloc(reinterpret_cast<float*&>(pivot_word), 1)) ||
-		    (st = alloc(cb, static_cast<size_t>(p.ld))) || (st = alloc(xp, static_cast<size_t>(p.ld))))
+		    (st = alloc(cb, static_cast<size_t>(p.ld))) || (st = alloc(xp, static_cast<size_t>(p.ld))) || (st = alloc(zx, static_cast<size_t>(p.ld))))
 			return fail(st);
 		if ((st = dev_upload(d_tile_slot, p.tile_slot)) || (st = dev_upload(d_slot_ij, p.slot_ij)) || (st = dev_upload(d_row_node, p.row_node)) ||
 		    (st = dev_upload(d_node_row, p.node_row)) || (st = dev_upload(d_tasks, p.tasks)) || (st = dev_upload(d_srcs, p.srcs)) ||
 		    (st = dev_upload(d_back_cols, p.back_cols)) || (st = dev_upload(d_back_ent, p.back_ent)) || (st = dev_upload(d_back_chains, p.back_chains)) ||
 		    (st = dev_upload(d_corner_edges, p.corner_edges)) ||
-		    (st = dev_upload(d_fwd_chains, p.fwd_chains)) || (st = dev_upload(d_fwd_cols, p.fwd_cols)) || (st = dev_upload(d_fwd_ent, p.fwd_ent)))
+		    (st = dev_upload(d_fwd_chains, p.fwd_chains)) || (st = dev_upload(d_fwd_cols, p.fwd_cols)) || (st = dev_upload(d_fwd_ent, p.fwd_ent)) ||
+		    (st = dev_upload(d_back_pre, p.back_pre)) || (st = dev_upload(d_fwd_pre, p.fwd_pre)))
 			return fail(st);
 		if (hipMemset(cb2, 0, sizeof(float) * static_cast<size_t>(p.ld)) != hipSuccess) {   // identity padding rows stay 0
 			set_error("hipMemset failed");
@@ -1402,6 +1446,8 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		level_panel = p.level_panel;
 		fwd_off = p.fwd_off;
 		back_off = p.back_off;
+		fwd_pre_off = p.fwd_pre_off;
+		back_pre_off = p.back_pre_off;
 		fill_tiles = static_cast<int64_t>(slots);
 		dense_tiles = static_cast<int64_t>(corner_ld(6 * nc) / TILE) * (corner_ld(6 * nc) / TILE + 1) / 2;
 	}
@@ -1448,10 +1494,23 @@ nnrt_status CornerSolver::launch_solve(float* xout, int* error_flag, hipStream_t
 		NNRT_LAUNCH_CHECK();
 		return NNRT_OK;
 	}
-	CornerBackArgs ba{nullptr, 0.f, tiles, ldiag, minv, cb, xp, d_row_node, xout, nullptr, d_back_cols, d_back_ent};
+	return launch_back(cb, xout, s, nullptr, 0.f);
+}
+
+// back substitution chains over y (with NNRT_SUBST_PRESUM, each launch preceded by its columns' pre-sums)
+nnrt_status CornerSolver::launch_back(const float* y, float* xout, hipStream_t s, const unsigned* gate, float refine_ratio) const {
+	CornerBackArgs ba{gate, refine_ratio, tiles, ldiag, minv, y, xp, d_row_node, xout, nullptr, d_back_cols, d_back_ent, zx, 0};
 	for (size_t l = 0; l + 1 < back_off.size(); l++) {
 		const int n = back_off[l + 1] - back_off[l];
+		const int npre = NNRT_SUBST_PRESUM ? back_pre_off[l + 1] - back_pre_off[l] : 0;
+		if (npre > 0) {
+			ba.chains = d_back_pre + back_pre_off[l];
+			ba.mode = 1;
+			k_corner_back<<<npre, CT, 0, s>>>(ba);
+			NNRT_LAUNCH_CHECK();
+		}
 		ba.chains = d_back_chains + back_off[l];
+		ba.mode = NNRT_SUBST_PRESUM ? 2 : 0;
 		k_corner_back<<<n, CT, 0, s>>>(ba);
 		NNRT_LAUNCH_CHECK();
 	}
@@ -1466,21 +1525,22 @@ nnrt_status CornerSolver::launch_resolve(float* xout, hipStream_t s, const unsig
 		NNRT_LAUNCH_CHECK();
 		return NNRT_OK;
 	}
-	CornerFwdArgs fa{gate, refine_ratio, tiles, ldiag, minv, cb2, nullptr, d_fwd_cols, d_fwd_ent};
+	CornerFwdArgs fa{gate, refine_ratio, tiles, ldiag, minv, cb2, nullptr, d_fwd_cols, d_fwd_ent, zx, 0};
 	for (size_t l = 0; l + 1 < fwd_off.size(); l++) {
 		const int n = fwd_off[l + 1] - fwd_off[l];
+		const int npre = NNRT_SUBST_PRESUM ? fwd_pre_off[l + 1] - fwd_pre_off[l] : 0;
+		if (npre > 0) {
+			fa.chains = d_fwd_pre + fwd_pre_off[l];
+			fa.mode = 1;
+			k_corner_fwd<<<npre, CT, 0, s>>>(fa);
+			NNRT_LAUNCH_CHECK();
+		}
 		fa.chains = d_fwd_chains + fwd_off[l];
+		fa.mode = NNRT_SUBST_PRESUM ? 2 : 0;
 		k_corner_fwd<<<n, CT, 0, s>>>(fa);
 		NNRT_LAUNCH_CHECK();
 	}
-	CornerBackArgs ba{gate, refine_ratio, tiles, ldiag, minv, cb2, xp, d_row_node, xout, nullptr, d_back_cols, d_back_ent};
-	for (size_t l = 0; l + 1 < back_off.size(); l++) {
-		const int n = back_off[l + 1] - back_off[l];
-		ba.chains = d_back_chains + back_off[l];
-		k_corner_back<<<n, CT, 0, s>>>(ba);
-		NNRT_LAUNCH_CHECK();
-	}
-	return NNRT_OK;
+	return launch_back(cb2, xout, s, gate, refine_ratio);
 }
 
 #ifdef NNRT_CORNER_STAMPS

@@ -280,6 +280,7 @@ public:
 	// written by the caller); d -> xout[6 nc] in corner-node order
 	// gate (nullable, device): skip unless the factorization's minimum pivot / diag(S) ratio is below refine_ratio
 	nnrt_status launch_resolve(float* xout, hipStream_t s, const unsigned* gate = nullptr, float refine_ratio = 0.f) const;
+	nnrt_status launch_back(const float* y, float* xout, hipStream_t s, const unsigned* gate, float refine_ratio) const;
 	float* refine_rhs() const { return cb2; }
 	// the factorization's minimum pivot / diag(S) ratio of the last solve (device word, float bits)
 	const unsigned* pivot_ratio() const { return pivot_word; }
@@ -298,6 +299,9 @@ private:
 	int nc = 0, ld = 0, T = 0, H = 0, slots = 0, n_corner_edges = 0;
 	int64_t fill_tiles = 0, dense_tiles = 0;
 	float *tiles = nullptr, *ldiag = nullptr, *minv = nullptr, *cb = nullptr, *cb2 = nullptr, *xp = nullptr, *sdiag = nullptr;
+	float* zx = nullptr;   // [ld] substitution pre-sums (NNRT_SUBST_PRESUM)
+	int2 *d_back_pre = nullptr, *d_fwd_pre = nullptr;
+	std::vector<int> back_pre_off, fwd_pre_off;
 	unsigned* pivot_word = nullptr;
 	int2 *d_fwd_chains = nullptr, *d_fwd_ent = nullptr;
 	int4* d_fwd_cols = nullptr;
@@ -316,6 +320,12 @@ private:
 // one step of iterative refinement after the fitter's arrowhead solve; 0: the float solve alone.
 // It runs only when the corner factorization's smallest pivot / diag(S) ratio (the cancellation a float32 Cholesky loses
 // digits to) falls below NNRT_REFINE_PIVOT_RATIO; otherwise its launches return at once.
+// Substitution pre-sums: before each chain launch of the corner's forward / back substitution, a launch of one workgroup
+// per column sums the column's entries whose vector segments come from earlier launches (in parallel over CUs); the
+// chains then walk only the entries inside themselves. 0: the chains sum every entry.
+#ifndef NNRT_SUBST_PRESUM
+#define NNRT_SUBST_PRESUM 1
+#endif
 #ifndef NNRT_ARAP_REFINE
 #define NNRT_ARAP_REFINE 1
 #endif

@@ -92,6 +92,25 @@ int main(int argc, char** argv) {
 	}
 	std::vector<int> done_launch(T, -1);   // launch index in which x_J was produced
 	printf("back launches %zu chains %zu\n", p.back_off.size() - 1, p.back_chains.size());
+	// the pre-sum lists: per launch exactly its columns with entries outside their chain, each once
+	for (int dir = 0; dir < 2; dir++) {
+		const auto& off = dir ? p.fwd_off : p.back_off;
+		const auto& chains = dir ? p.fwd_chains : p.back_chains;
+		const auto& cols = dir ? p.fwd_cols : p.back_cols;
+		const auto& pre_off = dir ? p.fwd_pre_off : p.back_pre_off;
+		const auto& pre = dir ? p.fwd_pre : p.back_pre;
+		if (pre_off.size() != off.size()) { printf("pre-sum launch count mismatch\n"); return 1; }
+		for (size_t l = 0; l + 1 < off.size(); l++) {
+			std::set<int> want, got;
+			for (int q = off[l]; q < off[l + 1]; q++)
+				for (int k = 0; k < chains[q].y; k++)
+					if (cols[chains[q].x + k].w > 0) want.insert(chains[q].x + k);
+			for (int q = pre_off[l]; q < pre_off[l + 1]; q++) {
+				if (pre[q].y != 1 || !got.insert(pre[q].x).second) { printf("pre-sum list malformed\n"); return 1; }
+			}
+			if (want != got) { printf("pre-sum list of launch %zu (%s) differs from its outside-entry columns\n", l, dir ? "fwd" : "back"); return 1; }
+		}
+	}
 	for (size_t l = 0; l + 1 < p.back_off.size(); l++) {
 		for (int q = p.back_off[l]; q < p.back_off[l+1]; q++) {
 			int2 chn = p.back_chains[q];
@@ -102,14 +121,16 @@ int main(int argc, char** argv) {
 				for (int e=0;e<c.z;e++){ int2 en = p.back_ent[c.y+e];
 					bool ok = (done_launch[en.y] >= 0 && done_launch[en.y] < (int)l) || mine.count(en.y);
 					if (!ok) { printf("BACK ORDER violation: column %d needs x_%d\n", J, en.y); return 1; }
+					// pre-sum split: the first c.w entries are read by the launch's pre-sum pass (earlier launches only),
+					// the rest by the chain (its own earlier columns only)
+					if ((e < c.w) != !mine.count(en.y)) { printf("BACK split violation: column %d entry %d (x_%d)\n", J, e, en.y); return 1; }
 					const double* L = tile(en.x); for (int r=0;r<TILE;r++) for (int cc=0;cc<TILE;cc++) z[cc] -= L[r*TILE+cc]*xp[en.y*TILE+r]; }
 				const double* Ld = &ldiag[(size_t)J*TE];
-				if (c.w) {   // x_J = M^T z with the inverse formed in the factor launches
+				{   // x_J = M^T z with the inverse formed after the factor launches
 					if (inv_launch[J] < 0) { printf("BACK uses an inverse never formed: column %d\n", J); return 1; }
 					const double* Mi = &minv[(size_t)J*TE];
 					for (int i=0;i<TILE;i++){ double v = 0; for (int r2=0;r2<TILE;r2++) v += Mi[r2*TILE+i]*z[r2]; xp[J*TILE+i] = v; }
-				} else {
-					for (int i=TILE-1;i>=0;i--){ double v = z[i]; for (int k2=i+1;k2<TILE;k2++) v -= Ld[k2*TILE+i]*xp[J*TILE+k2]; xp[J*TILE+i] = v/Ld[i*TILE+i]; }
+					(void)Ld;
 				}
 				for (int i=0;i<TILE;i++){ int rn = p.row_node[J*TILE+i]; if (rn>=0) xout[6*(rn>>3)+(rn&7)] = xp[J*TILE+i]; }
 				mine.insert(J);
@@ -138,12 +159,12 @@ int main(int argc, char** argv) {
 				for (int e = 0; e < c.z; e++) { int2 en = p.fwd_ent[c.y+e];
 					bool ok = (fdone[en.y] >= 0 && fdone[en.y] < (int)l) || mine.count(en.y);
 					if (!ok) { printf("FWD ORDER violation: column %d needs y_%d\n", J, en.y); return 1; }
+					if ((e < c.w) != !mine.count(en.y)) { printf("FWD split violation: column %d entry %d (y_%d)\n", J, e, en.y); return 1; }
 					if (p.slot_ij[en.x].x != J || p.slot_ij[en.x].y != en.y) { printf("FWD entry mismatch\n"); return 1; }
 					const double* L = tile(en.x); for (int r=0;r<TILE;r++) for (int cc=0;cc<TILE;cc++) z[r] -= L[r*TILE+cc]*yb[en.y*TILE+cc]; }
 				const double* Ld = &ldiag[(size_t)J*TE];
-				if (c.w) { if (inv_launch[J] < 0) { printf("FWD uses an inverse never formed\n"); return 1; }
-					const double* Mi = &minv[(size_t)J*TE]; for (int r=0;r<TILE;r++){ double v=0; for(int cc=0;cc<TILE;cc++) v += Mi[r*TILE+cc]*z[cc]; yb[J*TILE+r]=v; } }
-				else { for (int r=0;r<TILE;r++){ double v=z[r]; for(int cc=0;cc<r;cc++) v -= Ld[r*TILE+cc]*yb[J*TILE+cc]; yb[J*TILE+r] = v/Ld[r*TILE+r]; } }
+				{ if (inv_launch[J] < 0) { printf("FWD uses an inverse never formed\n"); return 1; }
+					const double* Mi = &minv[(size_t)J*TE]; for (int r=0;r<TILE;r++){ double v=0; for(int cc=0;cc<TILE;cc++) v += Mi[r*TILE+cc]*z[cc]; yb[J*TILE+r]=v; } (void)Ld; }
 				mine.insert(J);
 			}
 			for (int J : mine) fdone[J] = (int)l;
