@@ -824,12 +824,7 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 		for (int v = 0; v < 16; v++) Cb[quad_row(v, lane) * CS4 + 32 + (lane & 31)] = cacc[v];
 	}
 	__syncthreads();
-#if NNRT_FACTOR_LDS_STORE
-	if (wave == 0) {
-#else
 	if (wave != 0) return;
-	{
-#endif
 #pragma unroll
 	for (int q = TILE / 8; q < TILE / 4; q++) {
 		const float4 ca = lane >= 32 ? *reinterpret_cast<const float4*>(s_d + lane * CS4 + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -843,11 +838,7 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 	eliminate_columns<TILE / 2, TILE>(ap, lane, bad);
 	CORNER_STAMP(4);
 	if (diag) {
-#if NNRT_FACTOR_LDS_STORE
-		float4* wa = reinterpret_cast<float4*>(s_d + lane * CS4);   // copied out coalesced by the whole workgroup below
-#else
 		float4* wa = reinterpret_cast<float4*>(a.ldiag + static_cast<int64_t>(tk.J) * TILE_ELEMS + lane * TILE);
-#endif
 		float ljj = 1.f;   // this lane's diagonal entry L_jj (j = lane)
 #pragma unroll
 		for (int q = 0; q < TILE / 4; q++) {
@@ -870,26 +861,10 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 		}
 		CORNER_STAMP(5);
 	} else {
-#if NNRT_FACTOR_LDS_STORE
-		float4* wp = reinterpret_cast<float4*>(s_d + lane * CS4);
-#else
 		float4* wp = reinterpret_cast<float4*>(a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS + lane * TILE);
-#endif
 #pragma unroll
 		for (int q = 0; q < TILE / 4; q++) wp[q] = make_float4(ap[4 * q].y, ap[4 * q + 1].y, ap[4 * q + 2].y, ap[4 * q + 3].y);
 	}
-	}
-#if NNRT_FACTOR_LDS_STORE
-	// the finished tile (L_JJ, upper part zeroed, or L_IJ) leaves LDS as whole 1-KB row blocks, four per wave: lane-per-row
-	// stores from one wave touched 64 partial lines per instruction
-	__syncthreads();
-	float* dst = diag ? a.ldiag + static_cast<int64_t>(tk.J) * TILE_ELEMS : a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS;
-#pragma unroll
-	for (int i = 0; i < TILE_ELEMS / 4 / CT; i++) {
-		const int idx = i * CT + t, r = idx >> 4, c4 = idx & 15;
-		*reinterpret_cast<float4*>(dst + r * TILE + 4 * c4) = *reinterpret_cast<const float4*>(s_d + r * CS4 + 4 * c4);
-	}
-#endif
 }
 
 struct CornerBackArgs {

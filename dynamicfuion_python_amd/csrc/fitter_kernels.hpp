@@ -323,11 +323,6 @@ private:
 // Substitution pre-sums: before each chain launch of the corner's forward / back substitution, a launch of one workgroup
 // per column sums the column's entries whose vector segments come from earlier launches (in parallel over CUs); the
 // chains then walk only the entries inside themselves. 0: the chains sum every entry.
-// k_corner_factor's finished tile goes through LDS and leaves as row blocks stored by all four waves (0: wave 0 stores
-// its rows directly)
-#ifndef NNRT_FACTOR_LDS_STORE
-#define NNRT_FACTOR_LDS_STORE 1
-#endif
 #ifndef NNRT_SUBST_PRESUM
 #define NNRT_SUBST_PRESUM 1
 #endif
