@@ -699,35 +699,48 @@ struct CornerFactorArgs {
 	unsigned* pivot_word;    // atomic minimum of pivot / diag(S) over the diagonal tasks (nullable)
 };
 
-// M = L^-1 for the 64 x 64 lower-triangular factor L (row-major, zero above the diagonal): the workgroup stages L in LDS,
-// wave 0 forms column c of M in lane c by forward substitution (rows in order, four partial sums per row) and stores it.
-// The substitutions then form L_JJ^-T z and L_JJ^-1 z as products with M.
+// M = L^-1 for the 64 x 64 lower-triangular factor L (row-major, zero above the diagonal), staged in LDS. Forward
+// substitution against the identity, all four waves: column c of M belongs to the lane quad (16 columns per wave), lane q
+// of the quad holds M[4 i + q][c] and sums the terms k = q mod 4 of each row (the zero upper part of L lets every lane
+// run the same unrolled stream); the quad's partials are summed by DPP and row r's entry is the sum times 1 / L_rr (the
+// 64 reciprocals formed up front), so a row waits on one FMA, two DPP adds and a multiply instead of a division.
+__device__ __forceinline__ float quad_xor(float v, int ctrl_sel) {   // 0: lanes 1,0,3,2; 1: lanes 2,3,0,1
+	const int x = __builtin_bit_cast(int, v);
+	return __builtin_bit_cast(float, ctrl_sel == 0 ? __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xf, 0xf, false)
+	                                               : __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xf, 0xf, false));
+}
 __global__ __launch_bounds__(CT) void k_corner_invert(const float* __restrict__ ldiag, float* __restrict__ minv) {
-	__shared__ float s_l[TILE * CS4];
+	__shared__ __attribute__((aligned(16))) float s_l[TILE * CS4];
+	__shared__ float s_y[TILE];
 	const int t = threadIdx.x;
 	const int64_t J = blockIdx.x;
 	const float4* L4 = reinterpret_cast<const float4*>(ldiag + J * TILE_ELEMS);
 	for (int i = t; i < TILE_ELEMS / 4; i += CT) *reinterpret_cast<float4*>(s_l + (i >> 4) * CS4 + 4 * (i & 15)) = L4[i];
 	__syncthreads();
-	if (t >= 64) return;
-	const int c = t;
-	float m[TILE];
+	if (t < TILE) s_y[t] = 1.f / s_l[t * CS4 + t];
+	__syncthreads();
+	const int lane = t & 63, c = 16 * (t >> 6) + (lane >> 2), q = lane & 3;
+	float m[TILE / 4];   // m[i] = M[4 i + q][c]
+#pragma unroll
+	for (int i = 0; i < TILE / 4; i++) m[i] = 0.f;
 #pragma unroll
 	for (int r = 0; r < TILE; r++) {
-		float a[4] = {0.f, 0.f, 0.f, 0.f};
+		float a0 = 0.f, a1 = 0.f;
 #pragma unroll
-		for (int k4 = 0; k4 < r; k4 += 4) {
-			const float4 l = *reinterpret_cast<const float4*>(s_l + r * CS4 + k4);   // wave-uniform: LDS broadcast
-			a[0] = __builtin_fmaf(l.x, m[k4], a[0]);
-			if (k4 + 1 < r) a[1] = __builtin_fmaf(l.y, m[k4 + 1], a[1]);
-			if (k4 + 2 < r) a[2] = __builtin_fmaf(l.z, m[k4 + 2], a[2]);
-			if (k4 + 3 < r) a[3] = __builtin_fmaf(l.w, m[k4 + 3], a[3]);
+		for (int i = 0; i <= (r >> 2); i++) {   // k = 4 i + q <= r + 3: L_rk = 0 above the diagonal, m = 0 where unset
+			const float l = s_l[r * CS4 + 4 * i + q];
+			if (i & 1) a1 = __builtin_fmaf(l, m[i], a1);
+			else a0 = __builtin_fmaf(l, m[i], a0);
 		}
-		m[r] = ((c == r ? 1.f : 0.f) - ((a[0] + a[1]) + (a[2] + a[3]))) / s_l[r * CS4 + r];
+		float part = a0 + a1;
+		part += quad_xor(part, 0);
+		part += quad_xor(part, 1);
+		const float v = ((c == r ? 1.f : 0.f) - part) * s_y[r];
+		m[r >> 2] = q == (r & 3) ? v : m[r >> 2];
 	}
 	float* M = minv + J * TILE_ELEMS;
 #pragma unroll
-	for (int r = 0; r < TILE; r++) M[r * TILE + c] = m[r];
+	for (int i = 0; i < TILE / 4; i++) M[(4 * i + q) * TILE + c] = m[i];
 }
 
 // One launch per level of the tile elimination tree.

@@ -421,7 +421,6 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 	// this pixel's face: distinct anchor nodes still to be filed, ascending; the row waits in LDS (s_ent[wave][.][lane]),
 	// the current head in a register (head_at: its index)
 	uint32_t head_e = FACE_NODE_NONE;
-	uint32_t next_e = FACE_NODE_NONE;   // the entry after the head, read ahead: advancing the list waits on no LDS read
 	int head_at = 0;
 	int vid[3] = {0, 0, 0};
 	if (in_image) {
@@ -435,10 +434,7 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 				ent[(4 * t + 1) * 64 + lane] = e4.y;
 				ent[(4 * t + 2) * 64 + lane] = e4.z;
 				ent[(4 * t + 3) * 64 + lane] = e4.w;
-				if (t == 0) {
-					head_e = e4.x;
-					next_e = e4.y;
-				}
+				if (t == 0) head_e = e4.x;
 			}
 			vid[0] = vid_in[0];
 			vid[1] = vid_in[1];
@@ -498,12 +494,7 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 				slots[pos] = __builtin_bit_cast(float, lane);
 				slots[NG_STRIDE + pos] = __builtin_bit_cast(float, head_e);
 				head_at++;
-#if NNRT_GROUP_PREFETCH
-				head_e = next_e;
-				next_e = head_at + 1 < NSLOT ? ent[(head_at + 1) * 64 + lane] : FACE_NODE_NONE;
-#else
 				head_e = head_at < NSLOT ? ent[head_at * 64 + lane] : FACE_NODE_NONE;
-#endif
 			}
 			const int n_head = __popcll(M);
 			filed += n_head < room ? n_head : room;   // (integer select: the generic min() overload went through double)

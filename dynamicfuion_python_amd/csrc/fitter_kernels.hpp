@@ -8,9 +8,6 @@
 
 namespace nnrt {
 
-#ifndef NNRT_GROUP_PREFETCH
-#define NNRT_GROUP_PREFETCH 1   // pass-2 grouping keeps the entry after each list head in a register
-#endif
 #ifndef NNRT_SOLVE_LANES
 #define NNRT_SOLVE_LANES 1   // block-diagonal solve + update with 8 lanes per node (k_solve_update_lanes)
 #endif
@@ -322,9 +319,10 @@ private:
 // digits to) falls below NNRT_REFINE_PIVOT_RATIO; otherwise its launches return at once.
 // Substitution pre-sums: before each chain launch of the corner's forward / back substitution, a launch of one workgroup
 // per column sums the column's entries whose vector segments come from earlier launches (in parallel over CUs); the
-// chains then walk only the entries inside themselves. 0: the chains sum every entry.
+// chains then walk only the entries inside themselves. 0 (default): the chains sum every entry -- at C5 the extra
+// launches cost more than the parallel pre-sums save (solve stage 322 vs 342 µs, round 4).
 #ifndef NNRT_SUBST_PRESUM
-#define NNRT_SUBST_PRESUM 1
+#define NNRT_SUBST_PRESUM 0
 #endif
 #ifndef NNRT_ARAP_REFINE
 #define NNRT_ARAP_REFINE 1
