@@ -776,6 +776,9 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 		return;
 	}
 	const bool diag = tk.I == tk.J;
+	// the gate's diag(S) entry of this lane's row, loaded now: after the elimination its latency would sit on the
+	// level's critical path
+	const float sd = diag && a.pivot_word && wave == 0 ? a.sdiag[static_cast<int64_t>(tk.J) * TILE + lane] : 0.f;
 	stage_tile(a.tiles, a.tiles + static_cast<int64_t>(tk.slot_d) * TILE_ELEMS, src, tk.nd, wave, lane, s_d);
 	if (!diag) {
 		stage_tile(a.tiles, a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS, src + tk.nd, tk.np, wave, lane, s_p);
@@ -860,7 +863,6 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 			ljj = 4 * q == lane ? ap[4 * q].x : 4 * q + 1 == lane ? ap[4 * q + 1].x : 4 * q + 2 == lane ? ap[4 * q + 2].x : 4 * q + 3 == lane ? ap[4 * q + 3].x : ljj;
 		}
 		if (a.pivot_word) {   // the refinement gate: min over the tile of pivot (L_jj^2) / diag(S)_jj
-			const float sd = a.sdiag[static_cast<int64_t>(tk.J) * TILE + lane];
 			float ratio = sd > 0.f ? (ljj * ljj) / sd : 1.f;
 #pragma unroll
 			for (int m = 1; m < 64; m <<= 1) ratio = fminf(ratio, __shfl_xor(ratio, m));
