@@ -251,10 +251,6 @@ struct CornerPlan {
 	// info); back: columns T-1 .. 0, each its entries L_IJ (ascending I) then its head; forward: columns 0 .. T-1, each its
 	// row entries L_Jk (ascending k) then its head
 	std::vector<int4> walk_back, walk_fwd;
-	// chain walks (k_corner_chainwalk): per back / forward chain (same order as back_chains / fwd_chains) its element
-	// stream in the walk format: each column's entries, then its head (L_JJ^-1)
-	std::vector<int4> cw_back, cw_fwd;
-	std::vector<int2> cw_back_chains, cw_fwd_chains;   // (first element, element count)
 	std::vector<int> corner_edges;    // edges between two corner nodes (>= 3 layers)
 };
 
@@ -495,25 +491,6 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 		}
 		p.fwd_off.push_back(static_cast<int>(p.fwd_chains.size()));
 		p.fwd_pre_off.push_back(static_cast<int>(p.fwd_pre.size()));
-	}
-	for (int dir = 0; dir < 2; dir++) {
-		const auto& chains = dir ? p.fwd_chains : p.back_chains;
-		const auto& cols = dir ? p.fwd_cols : p.back_cols;
-		const auto& ent = dir ? p.fwd_ent : p.back_ent;
-		auto& st = dir ? p.cw_fwd : p.cw_back;
-		auto& sc = dir ? p.cw_fwd_chains : p.cw_back_chains;
-		for (const int2& ch : chains) {
-			const int beg = static_cast<int>(st.size());
-			for (int q = 0; q < ch.y; q++) {
-				const int4 c = cols[static_cast<size_t>(ch.x + q)];
-				for (int e = 0; e < c.z; e++) {
-					const int2 en = ent[static_cast<size_t>(c.y + e)];
-					st.push_back(make_int4(0, en.x, en.y * TILE, -1));
-				}
-				st.push_back(make_int4(1, c.x, c.x * TILE, 1));
-			}
-			sc.push_back(make_int2(beg, static_cast<int>(st.size()) - beg));
-		}
 	}
 	return p;
 }
@@ -1360,55 +1337,6 @@ __global__ __launch_bounds__(WT) void k_corner_walk(CornerWalkArgs a) {
 	}
 }
 
-// Chain walks: the chain launches' workgroups as walks. One workgroup per chain (as k_corner_back / k_corner_fwd) walks
-// its chain's element stream (each column's entry tiles, then L_JJ^-1) with walk_pass: the tiles stream through an LDS
-// ring by LDS-DMA issued up to `ring` tiles ahead -- across column boundaries, so a column's loads are in flight while
-// the previous column finishes -- and the vector lives in LDS: loaded whole from global at the start (the segments of
-// earlier launches are final; back: the chain's own columns start from y), the chain's own columns written back at
-// the end. Chains of one launch are independent subtrees: none reads another's columns.
-struct CornerChainWalkArgs {
-	const unsigned* gate;  // nullable: run only if the pivot ratio word is below ratio (the refinement pass)
-	float ratio;
-	const WalkElem* elems;
-	const int2* chains;    // this launch's chains (first element, element count)
-	const float* rhs;      // back: y (read for the chain's own columns); forward: unused (in place)
-	float* xvec;           // back: x (permuted order); forward: b in, y out
-	const int* row_node;
-	float* xout;           // back: x in corner-node order (nullable)
-	int ld, ring, max_elems;
-};
-template <bool BACK>
-__global__ __launch_bounds__(WT) void k_corner_chainwalk(CornerChainWalkArgs a) {
-	extern __shared__ __attribute__((aligned(16))) float s_walk[];
-	if (a.gate && !refine_gate_on(a.gate, a.ratio)) return;
-	const int2 ch = a.chains[blockIdx.x];
-	WalkElem* desc = reinterpret_cast<WalkElem*>(s_walk);
-	float* x = s_walk + 4 * a.max_elems;
-	float* red = x + ((a.ld + 3) & ~3);
-	float* zt = red + (WT / 64) * TILE;
-	float* ring = zt + TILE;
-	const WalkElem* g = a.elems + ch.x;
-	for (int i = threadIdx.x; i < a.ld; i += WT) x[i] = a.xvec[i];
-	if constexpr (BACK) {
-		__syncthreads();   // the whole-vector copy before the own columns' y overwrite it
-		for (int i = threadIdx.x; i < ch.y * TILE; i += WT) {
-			const WalkElem e = g[i >> 6];
-			if (e.info >= 0) x[e.x_off + (i & 63)] = a.rhs[e.x_off + (i & 63)];
-		}
-	}
-	walk_pass<BACK>(g, ch.y, a.ring, desc, x, red, zt, ring);   // starts with a barrier after its descriptor copy
-	for (int i = threadIdx.x; i < ch.y * TILE; i += WT) {
-		const WalkElem e = desc[i >> 6];
-		if (e.info < 0) continue;
-		const int r = e.x_off + (i & 63);
-		a.xvec[r] = x[r];
-		if (BACK && a.xout) {
-			const int rn = a.row_node[r];
-			if (rn >= 0) a.xout[6 * static_cast<int64_t>(rn >> 3) + (rn & 7)] = x[r];
-		}
-	}
-}
-
 // ===================================================================================================================
 // CornerSolver
 // ===================================================================================================================
@@ -1438,10 +1366,8 @@ void CornerSolver::release() {
 	                 reinterpret_cast<void**>(&d_row_node), reinterpret_cast<void**>(&d_node_row), reinterpret_cast<void**>(&d_tasks),
 	                 reinterpret_cast<void**>(&d_srcs), reinterpret_cast<void**>(&d_back_cols), reinterpret_cast<void**>(&d_back_ent), reinterpret_cast<void**>(&d_back_chains),
 	                 reinterpret_cast<void**>(&d_corner_edges), reinterpret_cast<void**>(&zx), reinterpret_cast<void**>(&d_back_pre),
-	                 reinterpret_cast<void**>(&d_fwd_pre), reinterpret_cast<void**>(&d_cw_back), reinterpret_cast<void**>(&d_cw_fwd),
-	                 reinterpret_cast<void**>(&d_cw_back_chains), reinterpret_cast<void**>(&d_cw_fwd_chains)})
+	                 reinterpret_cast<void**>(&d_fwd_pre)})
 		dev_free(*p);
-	cw_ok = false;
 	back_pre_off.clear();
 	fwd_pre_off.clear();
 	nc = ld = T = H = slots = n_corner_edges = 0;
@@ -1524,36 +1450,6 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 			walk_ok = true;
 		}
 	}
-	cw_ok = false;
-	if (NNRT_CHAIN_WALK && p.nc > 0 && p.ld <= WALK_MAX_LD) {
-		int mx = 0;
-		for (const int2& c : p.cw_back_chains) mx = std::max(mx, c.y);
-		for (const int2& c : p.cw_fwd_chains) mx = std::max(mx, c.y);
-		const size_t fixed = 16 * static_cast<size_t>(mx) + 4 * (static_cast<size_t>((p.ld + 3) & ~3) + (WT / 64) * TILE + TILE);
-		const size_t budget = 160 * 1024;
-		const int ring_tiles = fixed < budget ? static_cast<int>(std::min<size_t>(8, (budget - fixed) / (4 * TILE_ELEMS))) : 0;
-		if (mx <= WALK_MAX_ELEMS && ring_tiles >= 2) {
-			std::vector<WalkElem> wb, wf;
-			auto elem = [&](const int4& e) { return WalkElem{(e.x == 0 ? tiles : minv) + static_cast<int64_t>(e.y) * TILE_ELEMS, e.z, e.w}; };
-			for (const auto& e : p.cw_back) wb.push_back(elem(e));
-			for (const auto& e : p.cw_fwd) wf.push_back(elem(e));
-			nnrt_status st;
-			if ((st = dev_upload(d_cw_back, wb)) || (st = dev_upload(d_cw_fwd, wf)) || (st = dev_upload(d_cw_back_chains, p.cw_back_chains)) ||
-			    (st = dev_upload(d_cw_fwd_chains, p.cw_fwd_chains)))
-				return fail(st);
-			cw_ring = ring_tiles;
-			cw_max = mx;
-			cw_lds = static_cast<int>(fixed + static_cast<size_t>(ring_tiles) * 4 * TILE_ELEMS);
-			if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_corner_chainwalk<true>), hipFuncAttributeMaxDynamicSharedMemorySize, cw_lds) !=
-			        hipSuccess ||
-			    hipFuncSetAttribute(reinterpret_cast<const void*>(k_corner_chainwalk<false>), hipFuncAttributeMaxDynamicSharedMemorySize, cw_lds) !=
-			        hipSuccess) {
-				set_error("hipFuncSetAttribute (corner chain walk LDS) failed");
-				return fail(NNRT_ERROR_HIP);
-			}
-			cw_ok = true;
-		}
-	}
 	nc = p.nc;
 	if (nc > 0) {
 		ld = p.ld;
@@ -1618,15 +1514,6 @@ nnrt_status CornerSolver::launch_solve(float* xout, int* error_flag, hipStream_t
 
 // back substitution chains over y (with NNRT_SUBST_PRESUM, each launch preceded by its columns' pre-sums)
 nnrt_status CornerSolver::launch_back(const float* y, float* xout, hipStream_t s, const unsigned* gate, float refine_ratio) const {
-	if (cw_ok) {
-		CornerChainWalkArgs ca{gate, refine_ratio, d_cw_back, nullptr, y, xp, d_row_node, xout, ld, cw_ring, cw_max};
-		for (size_t l = 0; l + 1 < back_off.size(); l++) {
-			ca.chains = d_cw_back_chains + back_off[l];
-			k_corner_chainwalk<true><<<back_off[l + 1] - back_off[l], WT, cw_lds, s>>>(ca);
-			NNRT_LAUNCH_CHECK();
-		}
-		return NNRT_OK;
-	}
 	CornerBackArgs ba{gate, refine_ratio, tiles, ldiag, minv, y, xp, d_row_node, xout, nullptr, d_back_cols, d_back_ent, zx, 0};
 	for (size_t l = 0; l + 1 < back_off.size(); l++) {
 		const int n = back_off[l + 1] - back_off[l];
@@ -1652,15 +1539,6 @@ nnrt_status CornerSolver::launch_resolve(float* xout, hipStream_t s, const unsig
 		k_corner_walk<<<1, WT, walk_lds, s>>>(wa);
 		NNRT_LAUNCH_CHECK();
 		return NNRT_OK;
-	}
-	if (cw_ok) {
-		CornerChainWalkArgs ca{gate, refine_ratio, d_cw_fwd, nullptr, nullptr, cb2, d_row_node, nullptr, ld, cw_ring, cw_max};
-		for (size_t l = 0; l + 1 < fwd_off.size(); l++) {
-			ca.chains = d_cw_fwd_chains + fwd_off[l];
-			k_corner_chainwalk<false><<<fwd_off[l + 1] - fwd_off[l], WT, cw_lds, s>>>(ca);
-			NNRT_LAUNCH_CHECK();
-		}
-		return launch_back(cb2, xout, s, gate, refine_ratio);
 	}
 	CornerFwdArgs fa{gate, refine_ratio, tiles, ldiag, minv, cb2, nullptr, d_fwd_cols, d_fwd_ent, zx, 0};
 	for (size_t l = 0; l + 1 < fwd_off.size(); l++) {

@@ -307,11 +307,6 @@ private:
 	int walk_ring = 0, walk_lds = 0, n_walk_back = 0, n_walk_fwd = 0;
 	WalkElem* d_walk_back = nullptr;
 	WalkElem* d_walk_fwd = nullptr;
-	// chain walks (corner.hip k_corner_chainwalk): the chain launches' workgroups as LDS-ring walks
-	bool cw_ok = false;
-	int cw_ring = 0, cw_lds = 0, cw_max = 0;
-	WalkElem *d_cw_back = nullptr, *d_cw_fwd = nullptr;
-	int2 *d_cw_back_chains = nullptr, *d_cw_fwd_chains = nullptr;
 	int *d_tile_slot = nullptr, *d_row_node = nullptr, *d_node_row = nullptr, *d_corner_edges = nullptr;
 	int2 *d_slot_ij = nullptr, *d_back_ent = nullptr, *d_back_chains = nullptr;
 	CornerTask* d_tasks = nullptr;
@@ -326,11 +321,6 @@ private:
 // per column sums the column's entries whose vector segments come from earlier launches (in parallel over CUs); the
 // chains then walk only the entries inside themselves. 0 (default): the chains sum every entry -- at C5 the extra
 // launches cost more than the parallel pre-sums save (solve stage 322 vs 342 µs, round 4).
-// corner substitutions as chain walks (k_corner_chainwalk) when the permuted vector and every chain's stream fit in LDS;
-// 0: the k_corner_back / k_corner_fwd chain kernels
-#ifndef NNRT_CHAIN_WALK
-#define NNRT_CHAIN_WALK 1
-#endif
 #ifndef NNRT_SUBST_PRESUM
 #define NNRT_SUBST_PRESUM 0
 #endif

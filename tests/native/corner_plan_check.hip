@@ -224,48 +224,5 @@ int main(int argc, char** argv) {
 		printf("walk-solve residual %.3g\n", res3);
 		if (!(res3 < 1e-9 * b2max)) return 1;
 	}
-	// chain-walk streams (k_corner_chainwalk): forward launches then back launches, one stream per chain; an entry's
-	// segment must be final from an earlier launch or produced earlier in the same chain's stream (chains of a launch
-	// never read each other's columns)
-	{
-		std::vector<double> xw(p.ld, 0.0);
-		for (int R = 0; R < p.ld; R++) { int rn = p.row_node[R]; xw[R] = rn >= 0 ? b2[6*(rn>>3)+(rn&7)] : 0.0; }
-		if (p.cw_back_chains.size() != p.back_chains.size() || p.cw_fwd_chains.size() != p.fwd_chains.size()) { printf("CHAINWALK chain count mismatch\n"); return 1; }
-		for (int dir = 0; dir < 2; dir++) {
-			const auto& st = dir == 0 ? p.cw_fwd : p.cw_back;
-			const auto& sc = dir == 0 ? p.cw_fwd_chains : p.cw_back_chains;
-			const auto& off = dir == 0 ? p.fwd_off : p.back_off;
-			std::vector<int> when(T, -1), who(T, -1);
-			for (size_t l = 0; l + 1 < off.size(); l++)
-				for (int c = off[l]; c < off[l + 1]; c++) {
-					std::vector<double> acc(TILE, 0.0);
-					for (int k = sc[c].x; k < sc[c].x + sc[c].y; k++) {
-						const int4 e = st[k];
-						const double* tl = e.x == 0 ? tile(e.y) : &minv[(size_t)e.y*TE];
-						if (e.w < 0) {
-							const int K = e.z / TILE;
-							const bool ok = (when[K] >= 0 && when[K] < (int)l) || (when[K] == (int)l && who[K] == c);
-							if (!ok) { printf("CHAINWALK reads segment %d not final (launch %zu chain %d)\n", K, l, c); return 1; }
-							for (int r = 0; r < TILE; r++) for (int cc = 0; cc < TILE; cc++) {
-								if (dir == 0) acc[r] += tl[r*TILE+cc]*xw[e.z+cc]; else acc[cc] += tl[r*TILE+cc]*xw[e.z+r]; }
-							continue;
-						}
-						const int J = e.y;
-						if (e.x != 1 || inv_launch[J] < 0 || when[J] >= 0) { printf("CHAINWALK head malformed: %d\n", J); return 1; }
-						std::vector<double> z(TILE); for (int i=0;i<TILE;i++) z[i] = xw[J*TILE+i] - acc[i];
-						for (int i=0;i<TILE;i++){ double v=0; for (int kk=0;kk<TILE;kk++) v += (dir==0 ? tl[i*TILE+kk] : tl[kk*TILE+i]) * z[kk]; xw[J*TILE+i] = v; }
-						when[J] = (int)l; who[J] = c;
-						std::fill(acc.begin(), acc.end(), 0.0);
-					}
-				}
-			for (int J = 0; J < T; J++) if (when[J] < 0) { printf("CHAINWALK never solved column %d\n", J); return 1; }
-		}
-		std::vector<double> xn(m, 0.0);
-		for (int R = 0; R < p.ld; R++) { int rn = p.row_node[R]; if (rn >= 0) xn[6*(rn>>3)+(rn&7)] = xw[R]; }
-		double res4 = 0;
-		for (int i=0;i<m;i++){ double s4 = -b2[i]; for (int j=0;j<m;j++) s4 += M[(size_t)i*m+j]*xn[j]; res4 = std::max(res4, fabs(s4)); }
-		printf("chain-walk residual %.3g\n", res4);
-		if (!(res4 < 1e-9 * b2max)) return 1;
-	}
 	return 0;
 }
