@@ -686,9 +686,21 @@ __device__ unsigned long long g_corner_stamps[256][8];
 	} while (0)
 #endif
 
+// minimum over the 64 lanes (DPP row shifts, then row broadcasts into lane 63), wave-uniform result
+__device__ inline int corner_wave_min_i32(int v) {
+	constexpr int ID = 0x7fffffff;
+	v = min(v, __builtin_amdgcn_update_dpp(ID, v, 0x111, 0xf, 0xf, false));   // row_shr:1
+	v = min(v, __builtin_amdgcn_update_dpp(ID, v, 0x112, 0xf, 0xf, false));   // row_shr:2
+	v = min(v, __builtin_amdgcn_update_dpp(ID, v, 0x114, 0xf, 0xf, false));   // row_shr:4
+	v = min(v, __builtin_amdgcn_update_dpp(ID, v, 0x118, 0xf, 0xf, false));   // row_shr:8
+	v = min(v, __builtin_amdgcn_update_dpp(ID, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+	v = min(v, __builtin_amdgcn_update_dpp(ID, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
+	return __builtin_amdgcn_readlane(v, 63);
+}
+
 struct CornerFactorArgs {
 	float* tiles;            // [slots, 64, 64]
-	float* ldiag;            // [T, 64, 64] L_JJ (lower; zero above the diagonal)
+	float* ldiag;            // [T, 64, 64] L_JJ (lower part; the part above the diagonal is not meaningful)
 	float* cb;               // [ld] b_C -> y (forward substitution)
 	const CornerTask* tasks; // this launch's tasks, panels first
 	const int4* srcs;
@@ -699,7 +711,7 @@ struct CornerFactorArgs {
 	unsigned* pivot_word;    // atomic minimum of pivot / diag(S) over the diagonal tasks (nullable)
 };
 
-// M = L^-1 for the 64 x 64 lower-triangular factor L (row-major, zero above the diagonal), staged in LDS. Forward
+// M = L^-1 for the 64 x 64 lower-triangular factor L (row-major lower part; the staging zeroes the part above the diagonal) in LDS. Forward
 // substitution against the identity, all four waves: column c of M belongs to the lane quad (16 columns per wave), lane q
 // of the quad holds M[4 i + q][c] and sums the terms k = q mod 4 of each row (the zero upper part of L lets every lane
 // run the same unrolled stream); the quad's partials are summed by DPP and row r's entry is the sum times 1 / L_rr (the
@@ -715,7 +727,12 @@ __global__ __launch_bounds__(CT) void k_corner_invert(const float* __restrict__ 
 	const int t = threadIdx.x;
 	const int64_t J = blockIdx.x;
 	const float4* L4 = reinterpret_cast<const float4*>(ldiag + J * TILE_ELEMS);
-	for (int i = t; i < TILE_ELEMS / 4; i += CT) *reinterpret_cast<float4*>(s_l + (i >> 4) * CS4 + 4 * (i & 15)) = L4[i];
+	for (int i = t; i < TILE_ELEMS / 4; i += CT) {   // the lower part; zeros above the diagonal
+		const int r = i >> 4, c0 = 4 * (i & 15);
+		const float4 v = L4[i];
+		*reinterpret_cast<float4*>(s_l + r * CS4 + c0) =
+		    make_float4(c0 <= r ? v.x : 0.f, c0 + 1 <= r ? v.y : 0.f, c0 + 2 <= r ? v.z : 0.f, c0 + 3 <= r ? v.w : 0.f);
+	}
 	__syncthreads();
 	if (t < TILE) s_y[t] = 1.f / s_l[t * CS4 + t];
 	__syncthreads();
@@ -854,19 +871,21 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 	eliminate_columns<TILE / 2, TILE>(ap, lane, bad);
 	CORNER_STAMP(4);
 	if (diag) {
+		// the rows as eliminated (the part above the diagonal is not meaningful: k_corner_invert reads the lower part only);
+		// a copy in LDS (s_d is this wave's alone now) gives each lane its diagonal entry without a 64-way select
 		float4* wa = reinterpret_cast<float4*>(a.ldiag + static_cast<int64_t>(tk.J) * TILE_ELEMS + lane * TILE);
-		float ljj = 1.f;   // this lane's diagonal entry L_jj (j = lane)
 #pragma unroll
 		for (int q = 0; q < TILE / 4; q++) {
-			wa[q] = make_float4(4 * q <= lane ? ap[4 * q].x : 0.f, 4 * q + 1 <= lane ? ap[4 * q + 1].x : 0.f,
-			                    4 * q + 2 <= lane ? ap[4 * q + 2].x : 0.f, 4 * q + 3 <= lane ? ap[4 * q + 3].x : 0.f);
-			ljj = 4 * q == lane ? ap[4 * q].x : 4 * q + 1 == lane ? ap[4 * q + 1].x : 4 * q + 2 == lane ? ap[4 * q + 2].x : 4 * q + 3 == lane ? ap[4 * q + 3].x : ljj;
+			const float4 v = make_float4(ap[4 * q].x, ap[4 * q + 1].x, ap[4 * q + 2].x, ap[4 * q + 3].x);
+			wa[q] = v;
+			*reinterpret_cast<float4*>(s_d + lane * CS4 + 4 * q) = v;
 		}
 		if (a.pivot_word) {   // the refinement gate: min over the tile of pivot (L_jj^2) / diag(S)_jj
-			float ratio = sd > 0.f ? (ljj * ljj) / sd : 1.f;
-#pragma unroll
-			for (int m = 1; m < 64; m <<= 1) ratio = fminf(ratio, __shfl_xor(ratio, m));
-			if (lane == 0) atomicMin(a.pivot_word, __float_as_uint(fmaxf(ratio, 0.f)));
+			const float ljj = s_d[lane * CS4 + lane];
+			const float ratio = sd > 0.f ? (ljj * ljj) / sd : 1.f;
+			// non-negative floats order like their bit patterns: a DPP integer minimum
+			const int rb = corner_wave_min_i32(__float_as_int(fmaxf(ratio, 0.f)));
+			if (lane == 0) atomicMin(a.pivot_word, static_cast<unsigned>(rb));
 		}
 		if (lane == 0) {
 			float4* wb = reinterpret_cast<float4*>(a.cb + static_cast<int64_t>(tk.J) * TILE);
