@@ -1056,7 +1056,7 @@ nnrt_status nnrt_fitter_refine_info(nnrt_fitter* ft, float* h_out, void* stream)
 		float r;
 		std::memcpy(&r, &bits, sizeof(r));
 		h_out[0] = r;
-		h_out[2] = (NNRT_ARAP_REFINE != 0 && r < ft->refine_ratio) ? 1.f : 0.f;
+		h_out[2] = (NNRT_ARAP_REFINE != 0 && refine_window(r, ft->refine_ratio)) ? 1.f : 0.f;
 	}
 	return NNRT_OK;
 }

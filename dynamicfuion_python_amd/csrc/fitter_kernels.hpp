@@ -330,8 +330,15 @@ private:
 #ifndef NNRT_REFINE_PIVOT_RATIO
 #define NNRT_REFINE_PIVOT_RATIO 1e-2f
 #endif
+// below this ratio one refinement step with the float32 factors no longer converges (C2_ARAP iteration 4 of the
+// state-synchronised trajectory: ratio 2e-5, fp64 pivot ratio 6e-11, the plain solve 6.2e-5 from fp64, refined 1.2e-4);
+// the solve is left as the float factorization gives it, as the reference's is
+#ifndef NNRT_REFINE_PIVOT_FLOOR
+#define NNRT_REFINE_PIVOT_FLOOR 1e-4f
+#endif
+__host__ __device__ inline bool refine_window(float r, float ratio) { return r < ratio && r >= NNRT_REFINE_PIVOT_FLOOR; }
 __device__ inline bool refine_gate_on(const unsigned* gate, float ratio) {
-	return gate && __uint_as_float(*gate) < ratio;
+	return gate && refine_window(__uint_as_float(*gate), ratio);
 }
 
 struct ArrowheadWorkspace {

@@ -149,11 +149,12 @@ int32_t nnrt_fitter_graph_count(const nnrt_fitter* fitter);
  * (structurally non-zero) tiles, lower tiles of the dense corner. */
 nnrt_status nnrt_fitter_corner_info(const nnrt_fitter* fitter, int64_t* h_out);
 /* The last arrowhead solve's refinement gate (diagnostic; synchronizes `stream`): h_out[3] = the corner factorization's
- * smallest pivot / diag(S) ratio (1 without ARAP), the threshold below which one step of iterative refinement runs, and
- * 1 if it ran. */
+ * smallest pivot / diag(S) ratio (1 without ARAP), the threshold below which one step of iterative refinement runs (it
+ * does not below 1e-4, where one step no longer converges), and 1 if it ran. */
 nnrt_status nnrt_fitter_refine_info(nnrt_fitter* fitter, float* h_out, void* stream);
 /* Threshold of the refinement gate (default 1e-2): the arrowhead solve refines when the corner's smallest pivot /
- * diag(S) ratio falls below it; 0 never refines, +inf always. Drops the fitter's cached graphs (a launch argument). */
+ * diag(S) ratio falls below it (and is at least 1e-4); 0 never refines. Drops the fitter's cached graphs (a launch
+ * argument). */
 nnrt_status nnrt_fitter_set_refine_ratio(nnrt_fitter* fitter, float ratio);
 /* Store the warp field's current node motion (R, t) in the fitter (a device copy on `stream`). */
 nnrt_status nnrt_fitter_snapshot_motion(nnrt_fitter* fitter, nnrt_warp_field* warp_field, void* stream);

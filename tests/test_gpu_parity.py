@@ -411,6 +411,7 @@ NOT_POSITIVE_DEFINITE = 3   # include/nnrt_mi355x.h NNRT_ERROR_NOT_POSITIVE_DEFI
 
 
 REFINE_PIVOT_RATIO = 1e-7   # fp64 min / max Cholesky pivot above which the refined arrowhead solve is held to 1e-4
+REFINE_FLOOR = 1e-4         # csrc/fitter_kernels.hpp NNRT_REFINE_PIVOT_FLOOR: no refinement below this corner pivot / diag(S)
 
 
 def _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k):
@@ -558,11 +559,12 @@ def test_fit_state_synchronised_trajectory(nn, S, oracle_mod, name, iterations, 
 @pytest.mark.parametrize("name,iterations", [("C1_ARAP", 4), ("C2_ARAP", 5), ("C5", 4)])
 def test_refinement_gate(nn, S, oracle_mod, name, iterations):
     """The arrowhead solve's refinement gate (one step of iterative refinement when the corner factorization's smallest
-    pivot / diag(S) falls below the threshold) against what refinement buys. Along the GPU's own
-    trajectory every iteration is solved twice from the same motion, the gate forced shut (threshold 0) and forced open
-    (inf), and both are compared with the fp64 solution of that iteration's normal equations (the GPU's data blocks and
-    right-hand side, identical in both runs). Where the product gate stays shut the plain f32 solve must already meet
-    1e-4; where it opens and the fp64 pivot ratio exceeds REFINE_PIVOT_RATIO the refined solve must."""
+    pivot / diag(S) lies in [REFINE_FLOOR, threshold)) against what refinement buys. Along the GPU's
+    own trajectory every iteration is solved twice from the same motion, the gate forced shut (threshold 0) and forced
+    open (threshold inf; still nothing below the floor, where one step does not converge), and both are compared with the
+    fp64 solution of that iteration's normal equations (the GPU's data blocks and right-hand side, identical in both
+    runs). Where the product gate stays shut above the floor the plain f32 solve must already meet 1e-4; wherever the
+    fp64 pivot ratio exceeds REFINE_PIVOT_RATIO the product's solve must."""
     import scipy.sparse.linalg as spl
     from dynamicfuion_python_amd._native import NnrtError
     sc = _scene(S, oracle_mod, name)
@@ -601,13 +603,16 @@ def test_refinement_gate(nn, S, oracle_mod, name, iterations):
         e_plain, e_ref = nan_rel_err(plain[0], x64), nan_rel_err(refined[0], x64)
         gate = plain[3]
         rows.append((k + 1, gate, ratio64, e_plain, e_ref))
-        print(f"{name} iteration {k + 1}: corner pivot / diag(S) {gate:.3g} (gate {'open' if gate < threshold else 'shut'} at "
-              f"{threshold:g}), fp64 pivot ratio {ratio64:.3g}, err vs fp64: plain f32 {e_plain:.3g}, refined {e_ref:.3g}", flush=True)
+        opens = REFINE_FLOOR <= gate < threshold
+        print(f"{name} iteration {k + 1}: corner pivot / diag(S) {gate:.3g} (gate {'open' if opens else 'shut'}: window "
+              f"[{REFINE_FLOOR:g}, {threshold:g})), fp64 pivot ratio {ratio64:.3g}, err vs fp64: plain f32 {e_plain:.3g}, "
+              f"forced refinement {e_ref:.3g}", flush=True)
         if gate >= threshold:
             assert e_plain <= 1e-4, f"iteration {k + 1}: gate shut at {gate:.3g} but the plain solve is {e_plain:.3g} from fp64"
         elif ratio64 > REFINE_PIVOT_RATIO:
-            assert e_ref <= 1e-4, f"iteration {k + 1}: refined solve {e_ref:.3g} from fp64 at fp64 pivot ratio {ratio64:.3g}"
-        if gate >= threshold:   # continue along the product's trajectory
+            e_prod = e_ref if opens else e_plain
+            assert e_prod <= 1e-4, f"iteration {k + 1}: solve {e_prod:.3g} from fp64 at fp64 pivot ratio {ratio64:.3g}"
+        if not opens:   # continue along the product's trajectory
             solve(R0, t0, k, 0.0)
     ft.set_refine_ratio(threshold)
     print(f"{name}: {rows}")
