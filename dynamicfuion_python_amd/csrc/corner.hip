@@ -523,21 +523,20 @@ __global__ void k_corner_offdiag(const int* __restrict__ corner_edges, int n0, c
 	atomicAdd(corner_entry(m, R, C), wing[static_cast<int64_t>(e) * 36 + t]);
 }
 
-// 32 x 32 quadrant (qr, qc) of X Y^T for 64 x 64 row-major tiles X, Y (lane l feeds A[i = l & 31][k'] =
-// X[32 qr + i][32 (l >> 5) + s] and B[k'][j] = Y[32 qc + j][32 (l >> 5) + s] to MFMA step s, so the 32 steps x 2 lane
-// halves cover the 64-wide k range; each lane reads 32 contiguous floats of X and of Y). C/D map: column l & 31, row
+// 32 x 32 quadrant (qr, qc) of X Y^T for 64 x 64 row-major tiles X, Y at row stride ld (lane l feeds
+// A[i = l & 31][k'] = X[32 qr + i][32 (l >> 5) + s] and B[k'][j] = Y[32 qc + j][32 (l >> 5) + s] to MFMA step s, so the 32
+// steps x 2 lane halves cover the 64-wide k range; each lane reads 32 contiguous floats). C/D map: column l & 31, row
 // (v & 3) + 8 (v >> 2) + 4 (l >> 5).
-__device__ __forceinline__ void term_load(const float* tiles, const int4 s, int qr, int qc, int lane, float4 (&vx)[8], float4 (&vy)[8]) {
+__device__ inline f32x16 quadrant_xyt(const float* X, const float* Y, int64_t ld, int qr, int qc, int lane, f32x16 acc) {
 	const int half = lane >> 5, l32 = lane & 31;
-	const float4* x4 = reinterpret_cast<const float4*>(tiles + static_cast<int64_t>(s.x) * TILE_ELEMS + (32 * qr + l32) * TILE + 32 * half);
-	const float4* y4 = reinterpret_cast<const float4*>(tiles + static_cast<int64_t>(s.y) * TILE_ELEMS + (32 * qc + l32) * TILE + 32 * half);
+	const float4* x4 = reinterpret_cast<const float4*>(X + (32 * qr + l32) * ld + 32 * half);
+	const float4* y4 = reinterpret_cast<const float4*>(Y + (32 * qc + l32) * ld + 32 * half);
+	float4 vx[8], vy[8];
 #pragma unroll
 	for (int q = 0; q < 8; q++) {
 		vx[q] = x4[q];
 		vy[q] = y4[q];
 	}
-}
-__device__ __forceinline__ f32x16 term_mfma(const float4 (&vx)[8], const float4 (&vy)[8], f32x16 acc) {
 #pragma unroll
 	for (int q = 0; q < 8; q++) {
 		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].x, vy[q].x, acc, 0, 0, 0);
@@ -550,75 +549,50 @@ __device__ __forceinline__ f32x16 term_mfma(const float4 (&vx)[8], const float4 
 
 __device__ inline int quad_row(int v, int lane) { return (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5); }
 
-// this wave's quadrant of sum X Y^T over the update terms src[0 .. nd) into accd and src[nd .. nd + np) into accp, the
-// next term's operands loaded while the current term's 32 MFMAs run (two operand sets in flight: a term's load latency
-// is paid once, not per term)
-__device__ inline void sum_updates2(const float* tiles, const int4* src, int nd, int np, int qr, int qc, int lane, f32x16& accd, f32x16& accp) {
-	accd = f32x16{};
-	accp = f32x16{};
-	const int n = nd + np;
-	if (n == 0) return;
-	float4 ax[8], ay[8], bx[8], by[8];
-	term_load(tiles, src[0], qr, qc, lane, ax, ay);
-	int e = 0;
-	for (; e + 1 < n; e += 2) {
-		term_load(tiles, src[e + 1], qr, qc, lane, bx, by);
-		if (e < nd) accd = term_mfma(ax, ay, accd);
-		else accp = term_mfma(ax, ay, accp);
-		if (e + 2 < n) term_load(tiles, src[e + 2], qr, qc, lane, ax, ay);
-		if (e + 1 < nd) accd = term_mfma(bx, by, accd);
-		else accp = term_mfma(bx, by, accp);
-	}
-	if (e < n) {
-		if (e < nd) accd = term_mfma(ax, ay, accd);
-		else accp = term_mfma(ax, ay, accp);
-	}
-}
+// sum over the update terms of X Y^T for this wave's quadrant
 __device__ inline f32x16 sum_updates(const float* tiles, const int4* src, int n, int qr, int qc, int lane) {
-	f32x16 acc, unused;
-	sum_updates2(tiles, src, n, 0, qr, qc, lane, acc, unused);
+	f32x16 acc = {};
+	for (int e = 0; e < n; e++) {
+		const int4 s = src[e];
+		acc = quadrant_xyt(tiles + static_cast<int64_t>(s.x) * TILE_ELEMS, tiles + static_cast<int64_t>(s.y) * TILE_ELEMS, TILE, qr, qc, lane, acc);
+	}
 	return acc;
 }
 
-// (L y) row t >> 2 for a 64 x 64 tile L and the 64-vector y: 4 threads per row, 16 columns each (all 4 get the sum)
-__device__ __forceinline__ void rhs_load(const float* tiles, const float* cb, const int4 q, int t, float4 (&l)[4], float4 (&y)[4]) {
-	const int r = t >> 2, q4 = t & 3;
-	const float4* L4 = reinterpret_cast<const float4*>(tiles + static_cast<int64_t>(q.x) * TILE_ELEMS + r * TILE + 16 * q4);
-	const float4* y4 = reinterpret_cast<const float4*>(cb + static_cast<int64_t>(q.z) * TILE + 16 * q4);
+// s_t = A - sum X Y^T for the workgroup's quadrant of the 64 x 64 tile A (LDS, row stride CS4)
+__device__ inline void stage_tile(const float* tiles, const float* A, const int4* src, int n, int wave, int lane, float* s_t) {
+	const int qr = wave >> 1, qc = wave & 1;
+	float tv[16];
 #pragma unroll
-	for (int i = 0; i < 4; i++) {
-		l[i] = L4[i];
-		y[i] = y4[i];
-	}
+	for (int v = 0; v < 16; v++) tv[v] = A[(32 * qr + quad_row(v, lane)) * TILE + 32 * qc + (lane & 31)];
+	const f32x16 acc = sum_updates(tiles, src, n, qr, qc, lane);
+#pragma unroll
+	for (int v = 0; v < 16; v++) s_t[(32 * qr + quad_row(v, lane)) * CS4 + 32 * qc + (lane & 31)] = tv[v] - acc[v];
 }
-__device__ __forceinline__ float rhs_dot(const float4 (&l)[4], const float4 (&y)[4]) {
+
+// (L y) row t >> 2 for a 64 x 64 tile L and the 64-vector y: 4 threads per row, 16 columns each (all 4 get the sum)
+__device__ inline float rhs_row_update(const float* L, const float* y, int t) {
+	const int r = t >> 2, q4 = t & 3;
+	const float* Lr = L + r * TILE + 16 * q4;
+	const float* yq = y + 16 * q4;
 	float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-	for (int i = 0; i < 4; i++) {
-		s0 += l[i].x * y[i].x;
-		s1 += l[i].y * y[i].y;
-		s0 += l[i].z * y[i].z;
-		s1 += l[i].w * y[i].w;
+	for (int c = 0; c < 16; c += 2) {
+		s0 += Lr[c] * yq[c];
+		s1 += Lr[c + 1] * yq[c + 1];
 	}
 	float s = s0 + s1;
 	s += __shfl_xor(s, 1);
 	s += __shfl_xor(s, 2);
 	return s;
 }
-// sum over the update terms of (L_k y_k) row t >> 2, the next term's operands loaded ahead
+
 __device__ inline float rhs_updates(const float* tiles, const int4* src, int n, const float* cb, int t) {
 	float s = 0.f;
-	if (n == 0) return s;
-	float4 al[4], ay[4], bl[4], by[4];
-	rhs_load(tiles, cb, src[0], t, al, ay);
-	int e = 0;
-	for (; e + 1 < n; e += 2) {
-		rhs_load(tiles, cb, src[e + 1], t, bl, by);
-		s += rhs_dot(al, ay);
-		if (e + 2 < n) rhs_load(tiles, cb, src[e + 2], t, al, ay);
-		s += rhs_dot(bl, by);
+	for (int e = 0; e < n; e++) {
+		const int4 q = src[e];
+		s += rhs_row_update(tiles + static_cast<int64_t>(q.x) * TILE_ELEMS, cb + static_cast<int64_t>(q.z) * TILE, t);
 	}
-	if (e < n) s += rhs_dot(al, ay);
 	return s;
 }
 
@@ -822,29 +796,12 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 	// the gate's diag(S) entry of this lane's row, loaded now: after the elimination its latency would sit on the
 	// level's critical path
 	const float sd = diag && a.pivot_word && wave == 0 ? a.sdiag[static_cast<int64_t>(tk.J) * TILE + lane] : 0.f;
-	{
-		// s_d = A_JJ - sum L_Jk L_Jk^T, s_p = A_IJ - sum L_Ik L_Jk^T over the previous level's columns k (one pipelined
-		// term stream for both); the diagonal workgroup's augmented row b_J - sum L_Jk y_k
-		const int qr = wave >> 1, qc = wave & 1;
-		const float* Ad = a.tiles + static_cast<int64_t>(tk.slot_d) * TILE_ELEMS + 32 * qc + (lane & 31);
-		const float* Ap = a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS + 32 * qc + (lane & 31);
-		float td[16], tp[16];
-#pragma unroll
-		for (int v = 0; v < 16; v++) {
-			td[v] = Ad[(32 * qr + quad_row(v, lane)) * TILE];
-			tp[v] = diag ? 0.f : Ap[(32 * qr + quad_row(v, lane)) * TILE];
-		}
-		f32x16 accd, accp;
-		sum_updates2(a.tiles, src, tk.nd, diag ? 0 : tk.np, qr, qc, lane, accd, accp);
-#pragma unroll
-		for (int v = 0; v < 16; v++) s_d[(32 * qr + quad_row(v, lane)) * CS4 + 32 * qc + (lane & 31)] = td[v] - accd[v];
-		if (!diag) {
-#pragma unroll
-			for (int v = 0; v < 16; v++) s_p[(32 * qr + quad_row(v, lane)) * CS4 + 32 * qc + (lane & 31)] = tp[v] - accp[v];
-		} else {
-			const float s = rhs_updates(a.tiles, src, tk.nd, a.cb, t);
-			if ((t & 3) == 0) s_b[t >> 2] = a.cb[static_cast<int64_t>(tk.J) * TILE + (t >> 2)] - s;
-		}
+	stage_tile(a.tiles, a.tiles + static_cast<int64_t>(tk.slot_d) * TILE_ELEMS, src, tk.nd, wave, lane, s_d);
+	if (!diag) {
+		stage_tile(a.tiles, a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS, src + tk.nd, tk.np, wave, lane, s_p);
+	} else {
+		const float s = rhs_updates(a.tiles, src, tk.nd, a.cb, t);
+		if ((t & 3) == 0) s_b[t >> 2] = a.cb[static_cast<int64_t>(tk.J) * TILE + (t >> 2)] - s;
 	}
 	__syncthreads();
 	CORNER_STAMP(1);
