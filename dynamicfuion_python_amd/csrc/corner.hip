@@ -740,15 +740,24 @@ __global__ __launch_bounds__(CT) void k_corner_invert(const float* __restrict__ 
 	float m[TILE / 4];   // m[i] = M[4 i + q][c]
 #pragma unroll
 	for (int i = 0; i < TILE / 4; i++) m[i] = 0.f;
+	// row r's L values (k = 4 i + q <= r + 3: L_rk = 0 above the diagonal, m = 0 where unset) are read one row ahead, so
+	// a row's sum waits on its last product only, not on LDS
+	float lr[TILE / 4], ln[TILE / 4];
+	lr[0] = s_l[q];
 #pragma unroll
 	for (int r = 0; r < TILE; r++) {
+		if (r + 1 < TILE) {
+#pragma unroll
+			for (int i = 0; i <= ((r + 1) >> 2); i++) ln[i] = s_l[(r + 1) * CS4 + 4 * i + q];
+		}
 		float a0 = 0.f, a1 = 0.f;
 #pragma unroll
-		for (int i = 0; i <= (r >> 2); i++) {   // k = 4 i + q <= r + 3: L_rk = 0 above the diagonal, m = 0 where unset
-			const float l = s_l[r * CS4 + 4 * i + q];
-			if (i & 1) a1 = __builtin_fmaf(l, m[i], a1);
-			else a0 = __builtin_fmaf(l, m[i], a0);
+		for (int i = 0; i <= (r >> 2); i++) {
+			if (i & 1) a1 = __builtin_fmaf(lr[i], m[i], a1);
+			else a0 = __builtin_fmaf(lr[i], m[i], a0);
 		}
+#pragma unroll
+		for (int i = 0; i < TILE / 4; i++) lr[i] = ln[i];
 		float part = a0 + a1;
 		part += quad_xor(part, 0);
 		part += quad_xor(part, 1);

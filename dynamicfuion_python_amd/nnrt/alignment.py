@@ -152,7 +152,7 @@ class DeformableMeshToImageFitter:
         return dict(pivot_ratio=float(out[0]), threshold=float(out[1]), refined=bool(out[2]))
 
     def set_refine_ratio(self, ratio: float):
-        """Threshold of the arrowhead solve's refinement gate (default 1e-2; 0: never refine, inf: always)."""
+        """Threshold of the arrowhead solve's refinement gate (default 1e-3; 0: never refine, inf: always)."""
         N.check(N.lib().nnrt_fitter_set_refine_ratio(self._h, float(ratio)))
 
     def time_kernels(self, warp_field: HierarchicalGraphWarpField, reps: int = 20, trials: int = 5, stream=None) -> dict:

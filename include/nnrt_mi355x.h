@@ -152,7 +152,7 @@ nnrt_status nnrt_fitter_corner_info(const nnrt_fitter* fitter, int64_t* h_out);
  * smallest pivot / diag(S) ratio (1 without ARAP), the threshold below which one step of iterative refinement runs (it
  * does not below 1e-4, where one step no longer converges), and 1 if it ran. */
 nnrt_status nnrt_fitter_refine_info(nnrt_fitter* fitter, float* h_out, void* stream);
-/* Threshold of the refinement gate (default 1e-2): the arrowhead solve refines when the corner's smallest pivot /
+/* Threshold of the refinement gate (default 1e-3): the arrowhead solve refines when the corner's smallest pivot /
  * diag(S) ratio falls below it (and is at least 1e-4); 0 never refines. Drops the fitter's cached graphs (a launch
  * argument). */
 nnrt_status nnrt_fitter_set_refine_ratio(nnrt_fitter* fitter, float ratio);
