@@ -120,9 +120,10 @@ def stage_bytes(P: int, F: int, V: int, N: int, K: int, E: int) -> dict:
 
 # stages fused into each kernel of one GN iteration (block-diagonal configs)
 KERNEL_STAGES = {
-    "k_warp_mesh_quad": ("warp", "warped_jacobians"),
+    "k_warp_mesh_quad": ("warp",),
     "k_raster_scatter_mesh": ("ndc", "raster"),
-    "k_fit_pixels_fused": ("residual", "rasterized_jacobians", "pixel_anchor_jacobians", "jtj_jtr"),
+    # round 4: the warped-surface Jacobians (-wR(v-g), -wRn) are formed per association in pass 2, not stored by the warp
+    "k_fit_pixels_fused": ("residual", "rasterized_jacobians", "warped_jacobians", "pixel_anchor_jacobians", "jtj_jtr"),
     "k_solve_update": ("solve",),
 }
 
@@ -185,7 +186,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-share-only", action="store_true", help="CPU baseline at this process's CPU share only (large configs: C3)")
     ap.add_argument("--cpu-no-warm", action="store_true", help="CPU baseline without the untimed first call (large configs: C3)")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r03_pmc_traffic.json"),
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r04_pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch of the roofline kernel (tools/pmc_traffic.py output)")
     return ap.parse_args(argv)
 

@@ -122,8 +122,10 @@ def test_algorithmic_bytes_c2():
     total = sum(sb.values())
     assert 330e6 < total < 400e6
     assert sb["pixel_anchor_jacobians"] == 307200 * 257 + 307200 * 72 * 4 + 4 * 1_400_000
-    assert bench.kernel_bytes("k_fit_pixels_fused", sb) == (sb["residual"] + sb["rasterized_jacobians"] + sb["pixel_anchor_jacobians"]
-                                                            + sb["jtj_jtr"])
+    # round 4: the fused pixel launch also forms the warped-surface Jacobians (the warp stores positions / normals only)
+    assert bench.kernel_bytes("k_fit_pixels_fused", sb) == (sb["residual"] + sb["rasterized_jacobians"] + sb["warped_jacobians"]
+                                                            + sb["pixel_anchor_jacobians"] + sb["jtj_jtr"])
+    assert bench.kernel_bytes("k_warp_mesh_quad", sb) == sb["warp"]
     # every stage of the block-diagonal iteration except the ARAP rows is covered by exactly one kernel
     covered = [st for k in bench.KERNEL_STAGES.values() for st in k]
     assert sorted(covered) == sorted(sb)
