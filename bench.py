@@ -589,7 +589,9 @@ def main(argv=None):
                       + ("; so is arap: the ARAP edge terms run in extra workgroups of that launch" if arap else ""),
         "roofline": {"kernel": ROOFLINE_KERNEL, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "algorithmic_bytes": kbytes, "kernel_ms": k_ms,
-                     "bytes_formula": "SURVEY.md 8(d): residuals + rasterized Jacobians + pixel-anchor Jacobians + JtJ/Jtr rows (P*58 + F*36 + P*244 + F*72 + P*257 + P*72K + 4E + E*28 + P*5 + 168N)"
+                     "bytes_formula": "SURVEY.md 8(d): residuals + rasterized Jacobians + warped-surface Jacobians (formed in pass 2 since "
+                                      "round 4) + pixel-anchor Jacobians + JtJ/Jtr rows (P*58 + F*36 + P*244 + F*72 + V*(24+36K) + P*257 "
+                                      "+ P*72K + 4E + E*28 + P*5 + 168N)"
                                       + (" + ARAP edge rows (E_e*184 + 288N, fused into the launch)" if arap else ""),
                      "associations_E": E, "contributing_pixels": P_c,
                      "associations_note": "E and contributing pixels averaged over the timed iterations", "traffic_source": traffic_src,
