@@ -486,10 +486,16 @@ __global__ void k_arrow_back(int n0, int n_update, const float* __restrict__ din
                              const float* __restrict__ diag = nullptr, float* __restrict__ res = nullptr) {
 	const int i = blockIdx.x * blockDim.x + threadIdx.x;
 	bool refining = false;
-	if (gate) {
+	if (gate && mode == 2) {
 		refining = refine_gate_on(gate, ratio);
-		if (mode == 2 && !refining) return;
-		if (mode == 1 && refining) node_state = nullptr;   // the refinement's last pass applies the update
+		if (!refining) return;
+	}
+	// mode 1: the gate word only decides what happens after the stem solve: its load is issued here and first waited for
+	// after the solve's own loads (corner-node threads use it at once)
+	const unsigned gate_word = gate && mode == 1 ? *gate : 0u;
+	if (gate && mode == 1 && i >= n0) {
+		refining = refine_window(__uint_as_float(gate_word), ratio);
+		if (refining) node_state = nullptr;   // the refinement's last pass applies the update
 	}
 	if (i >= n0) {
 		if (i < n_update && (node_state || x_base)) {
@@ -506,6 +512,10 @@ __global__ void k_arrow_back(int n0, int n_update, const float* __restrict__ din
 	}
 	float o[6];
 	stem_solve(i, dinv, edge_offsets, edge_list, edges, wing, rhs, x, o);
+	if (gate && mode == 1) {
+		refining = refine_window(__uint_as_float(gate_word), ratio);
+		if (refining) node_state = nullptr;
+	}
 	float2* xo = reinterpret_cast<float2*>(x + 6 * static_cast<int64_t>(i));
 #pragma unroll
 	for (int q = 0; q < 3; q++) xo[q] = make_float2(o[2 * q], o[2 * q + 1]);
