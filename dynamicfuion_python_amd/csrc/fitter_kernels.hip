@@ -1035,6 +1035,16 @@ __global__ __launch_bounds__(64) void k_solve_update_lanes(SolveArgs a) {
 	__shared__ float s_l[NPW][S * S];
 	const int lane = static_cast<int>(threadIdx.x), gl = lane & (SOLVE_GL - 1), grp = lane / SOLVE_GL;
 	const int n = static_cast<int>(blockIdx.x) * NPW + grp;
+	// the node's motion before the update, loaded together with the accumulator rows (one memory round trip for both)
+	float old[12];
+	if constexpr (IDENTITY) {
+#pragma unroll
+		for (int i = 0; i < 12; i++) old[i] = (i == 3 || i == 7 || i == 11) ? 1.f : 0.f;
+	} else {
+		const float* ns_in = a.state_in + static_cast<int64_t>(n < a.N ? n : 0) * NODE_STRIDE;
+#pragma unroll
+		for (int i = 0; i < 12; i++) old[i] = ns_in[3 + i];
+	}
 	{   // the wave's 8 accumulator rows: one contiguous block, read and re-zeroed with coalesced 16-B accesses
 		const int64_t base = static_cast<int64_t>(blockIdx.x) * NPW * ACC_STRIDE;
 		const int64_t lim = static_cast<int64_t>(a.N) * ACC_STRIDE - base;
@@ -1045,18 +1055,12 @@ __global__ __launch_bounds__(64) void k_solve_update_lanes(SolveArgs a) {
 				reinterpret_cast<double2*>(s_acc)[q] = g2[q];
 				g2[q] = make_double2(0.0, 0.0);
 			}
-		__syncthreads();
+		// one wave per workgroup: its own LDS writes ordered before its reads, no workgroup barrier
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 	}
 	if (n >= a.N) return;   // whole groups: the group_bcast sources stay in the active set
-	float old[12];
-	if constexpr (IDENTITY) {
-#pragma unroll
-		for (int i = 0; i < 12; i++) old[i] = (i == 3 || i == 7 || i == 11) ? 1.f : 0.f;
-	} else {
-		const float* ns_in = a.state_in + static_cast<int64_t>(n) * NODE_STRIDE;
-#pragma unroll
-		for (int i = 0; i < 12; i++) old[i] = ns_in[3 + i];
-	}
 	const double* acc = s_acc + grp * ACC_STRIDE;
 	const int r = gl < S ? gl : S - 1;   // lanes S..7 shadow row S - 1 (their results are never stored)
 	// row r of H (packed upper triangle: entry (c0, c1), c0 <= c1, at c0 S - c0 (c0 - 1) / 2 + c1 - c0)
