@@ -934,7 +934,8 @@ __device__ __forceinline__ int2 subst_span(const int4& c, int mode) {
 // Back substitution L^T x = y along chains of the elimination tree (one workgroup per chain, its columns in order; the
 // launches run from the root's chain down). Per column J: z = y_J - sum_I L_IJ^T x_I (each wave a quarter of every tile's
 // rows, read as 16-B row pieces, BACK_BATCH tiles' loads in flight), then x_J = L_JJ^-T z as the product M^T z with
-// M = L_JJ^-1 (k_corner_invert; its tile streams into LDS by LDS-DMA behind the entry loads) on wave 0. x_J goes to
+// M = L_JJ^-1 (k_corner_invert; its tile streams into LDS by LDS-DMA behind the entry loads), a quarter of the rows of M
+// per wave. x_J goes to
 // global memory before the workgroup barrier, so the chain's next column reads it like the x of earlier launches.
 // Per column only the entry tiles and their x are a memory round trip on the chain's path: the chain's column
 // descriptors are staged in LDS up front, each column's first 64 entry descriptors are fetched during the previous
@@ -955,6 +956,7 @@ __device__ __forceinline__ void tile_to_lds(const float* src, float* dst, int wa
 __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 	__shared__ __attribute__((aligned(16))) float s_m[TILE_ELEMS];   // L_JJ^-1 of the current column
 	__shared__ __attribute__((aligned(16))) float s_part[4][TILE];
+	__shared__ float s_xq[4][TILE];   // quarters of x_J = M^T z
 	__shared__ int4 s_cols[BACK_COLS];
 	__shared__ int2 s_ent[2][64];   // first 64 entry descriptors of the current (q & 1) and the next column
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
@@ -976,7 +978,7 @@ __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 			// M = L_JJ^-1 streams into LDS behind the entry loads; y_J is loaded ahead of the sums (wave 0)
 			if (a.mode != 1) tile_to_lds(a.minv + static_cast<int64_t>(J) * TILE_ELEMS, s_m, wave, lane);
 			const float* ysrc = a.mode == 2 && col.w > 0 ? a.zx : a.cb;
-			const float yv = wave == 0 ? ysrc[static_cast<int64_t>(J) * TILE + lane] : 0.f;
+			const float yv = ysrc[static_cast<int64_t>(J) * TILE + lane];   // every wave forms z
 			const bool has_next = q + 1 < nq;
 			int2 nxt = make_int2(0, 0);
 			if (wave == 1 && has_next) {
@@ -1026,20 +1028,30 @@ __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 			__syncthreads();   // also retires the M tile's LDS-DMA pieces of every wave
 			if (wave == 0 && a.mode == 1) {
 				a.zx[static_cast<int64_t>(J) * TILE + lane] = yv - ((s_part[0][lane] + s_part[1][lane]) + (s_part[2][lane] + s_part[3][lane]));
-			} else if (wave == 0) {
-				// x_c = sum_r M_rc z_r, z_r broadcast from lane r; column c of M from LDS (conflict-free); four partial sums
+			} else if (a.mode != 1) {
+				// x_c = sum_r M_rc z_r: every wave forms z (lane = row) and sums its 16 rows r, z_r broadcast from lane r,
+				// column c of M from LDS (conflict-free); the four quarters meet in LDS
 				const float z = yv - ((s_part[0][lane] + s_part[1][lane]) + (s_part[2][lane] + s_part[3][lane]));
-				float xs[4] = {0.f, 0.f, 0.f, 0.f};
+				float xs[2] = {0.f, 0.f};
 #pragma unroll
-				for (int r = 0; r < TILE; r++) xs[r & 3] = __builtin_fmaf(s_m[r * TILE + lane], lane_bcast(z, r), xs[r & 3]);
-				const float x = (xs[0] + xs[1]) + (xs[2] + xs[3]);
-				const int64_t row = static_cast<int64_t>(J) * TILE + lane;
-				a.xp[row] = x;
-				const int rn = a.row_node[row];
-				if (rn >= 0) a.xout[6 * static_cast<int64_t>(rn >> 3) + (rn & 7)] = x;
+				for (int k = 0; k < 16; k++) {
+					const int r = 16 * wave + k;
+					xs[k & 1] = __builtin_fmaf(s_m[r * TILE + lane], lane_bcast(z, r), xs[k & 1]);
+				}
+				s_xq[wave][lane] = xs[0] + xs[1];
+			}
+			if (a.mode != 1) {
+				__syncthreads();   // the quarters of x_J
+				if (wave == 0) {
+					const float x = (s_xq[0][lane] + s_xq[1][lane]) + (s_xq[2][lane] + s_xq[3][lane]);
+					const int64_t row = static_cast<int64_t>(J) * TILE + lane;
+					a.xp[row] = x;
+					const int rn = a.row_node[row];
+					if (rn >= 0) a.xout[6 * static_cast<int64_t>(rn >> 3) + (rn & 7)] = x;
+				}
 			}
 			if (wave == 1 && has_next) s_ent[(q + 1) & 1][lane] = nxt;
-			__syncthreads();   // x_J visible to the chain's next column; s_part, s_m free; the next column's entries staged
+			__syncthreads();   // x_J visible to the chain's next column; s_part, s_xq, s_m free; the next column's entries staged
 		}
 	}
 }
