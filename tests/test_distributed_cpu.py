@@ -168,3 +168,19 @@ def test_more_ranks_than_devices_fails_fast(monkeypatch):
     bench.check_rank_devices(0, 1, "nccl", 1)
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
     bench.check_rank_devices(3, 16, "nccl", 8)   # two nodes of 8: local ranks 0..7 on 8 devices
+
+
+def test_refinement_window_constants_agree():
+    """The refinement window the GPU tests assume (tests/test_gpu_parity.py REFINE_FLOOR) is the one the kernels are
+    built with (csrc/fitter_kernels.hpp NNRT_REFINE_PIVOT_FLOOR / NNRT_REFINE_PIVOT_RATIO), and the documented default
+    threshold (include/nnrt_mi355x.h) is the built one."""
+    import re
+    ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hpp = open(os.path.join(ROOT, "dynamicfuion_python_amd", "csrc", "fitter_kernels.hpp")).read()
+    floor = float(re.search(r"#define NNRT_REFINE_PIVOT_FLOOR ([0-9.e+-]+)f", hpp).group(1))
+    upper = float(re.search(r"#define NNRT_REFINE_PIVOT_RATIO ([0-9.e+-]+)f", hpp).group(1))
+    src = open(os.path.join(ROOT, "tests", "test_gpu_parity.py")).read()
+    assert float(re.search(r"^REFINE_FLOOR = ([0-9.e+-]+)", src, re.M).group(1)) == floor
+    hdr = open(os.path.join(ROOT, "include", "nnrt_mi355x.h")).read()
+    assert f"(default {upper:g})" in hdr and f"at least {floor:g}" in hdr
+    assert floor < upper
