@@ -182,5 +182,6 @@ def test_refinement_window_constants_agree():
     src = open(os.path.join(ROOT, "tests", "test_gpu_parity.py")).read()
     assert float(re.search(r"^REFINE_FLOOR = ([0-9.e+-]+)", src, re.M).group(1)) == floor
     hdr = open(os.path.join(ROOT, "include", "nnrt_mi355x.h")).read()
-    assert f"(default {upper:g})" in hdr and f"at least {floor:g}" in hdr
+    assert float(re.search(r"refinement gate \(default ([0-9.e+-]+)\)", hdr).group(1)) == upper
+    assert float(re.search(r"and is at least ([0-9.e+-]+)\)", hdr).group(1)) == floor
     assert floor < upper
