@@ -481,6 +481,10 @@ def main(argv=None):
     ft.snapshot_motion(wf)   # "frame": the frame's start state; otherwise the restored mid-motion state
     ktimes = ft.time_kernels(wf, reps=args.kernel_reps, trials=args.kernel_trials)
     ft.restore_motion(wf)
+    # kernel times are differences of medians: a short kernel can come out <= 0. Such a difference is not a
+    # time: it is reported as None and no fraction is priced on it (the roofline falls back to the whole iteration's time,
+    # a conservative lower bound on the kernel's rate)
+    ktimes = {k: (v if v > 0 else None) for k, v in ktimes.items()}
     # per-stage eager event timing over the same iterations as the timed steps (a frame's iterations for "frame", the
     # restored iteration otherwise), one iteration at a time so that each iteration's algorithmic bytes use its own
     # association count E (the stage times themselves carry launch / event overhead and are reported as stage_ms only)
@@ -518,7 +522,7 @@ def main(argv=None):
             continue
         kb = kernel_bytes(kname, sb)
         ms = ktimes[kname if kname != "k_solve_update" else "solve"]
-        kernels[kname] = dict(ms=round(ms, 5), algorithmic_bytes=kb, frac=kb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS if ms > 0 else None)
+        kernels[kname] = dict(ms=round(ms, 5) if ms else None, algorithmic_bytes=kb, frac=kb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS if ms else None)
     corner = None
     if arap:
         counts = wf.get_layer_node_counts()
@@ -529,18 +533,20 @@ def main(argv=None):
         # the ARAP edge terms run in extra workgroups of the fused pixel launch: charged to it
         kp = kernels[ROOFLINE_KERNEL]
         kp["algorithmic_bytes"] += ab["arap"]
-        kp["frac"] = kp["algorithmic_bytes"] / (kp["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS if kp["ms"] > 0 else None
+        kp["frac"] = kp["algorithmic_bytes"] / (kp["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS if kp["ms"] else None
         kernels["k_arap_edges"] = dict(ms=None, fused_into=ROOFLINE_KERNEL, algorithmic_bytes=ab["arap"], frac=None)
         fl = corner_flops(Nn - n0)
+        solve_ms = ktimes["solve"] or ktimes["iteration"]
         corner = dict(kernel="arrowhead solve stage (stem Schur update + tile-sparse corner Cholesky + substitutions + update)",
-                      bound="mfma", achieved=fl / (ktimes["solve"] * 1e-3) / 1e12, peak=MFMA_F32_PEAK_TFS, unit="TFLOP/s",
-                      frac=fl / (ktimes["solve"] * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS, traffic=None, flops=fl, kernel_ms=ktimes["solve"],
+                      bound="mfma", achieved=fl / (solve_ms * 1e-3) / 1e12, peak=MFMA_F32_PEAK_TFS, unit="TFLOP/s",
+                      frac=fl / (solve_ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS, traffic=None, flops=fl, kernel_ms=solve_ms,
+                      kernel_ms_source="solve" if ktimes["solve"] else "iteration (the solve's prefix difference was not positive)",
                       n0=n0, n1=Nn - n0, corner_size=6 * (Nn - n0), edges=Ee,
                       flops_formula="SURVEY.md 8(d): (6 n1)^3 / 3 + 2 (6 n1)^2 (1 + n_rhs), n_rhs = 1 (the reference's dense corner; "
                                     "the tile-sparse factorization performs fewer: plan below)",
                       plan=ft.corner_info(), refinement=ft.refine_info())
     kbytes = kernels[ROOFLINE_KERNEL]["algorithmic_bytes"]
-    k_ms = ktimes[ROOFLINE_KERNEL]
+    k_ms = ktimes[ROOFLINE_KERNEL] or ktimes["iteration"]
     achieved = kbytes / (k_ms * 1e-3) / 1e9
     it_bytes = sum(sb.values())
     traffic, traffic_src = load_traffic(args.traffic_file, workload)
@@ -577,7 +583,7 @@ def main(argv=None):
                                                                        f"{torch.cuda.device_count()} visible GPU(s))"}
                       if world > 1 else {})},
         "setup_ms": round(setup_ms, 3),
-        "kernel_ms": {k: round(v, 5) for k, v in ktimes.items()},
+        "kernel_ms": {k: (round(v, 5) if v else None) for k, v in ktimes.items()},
         "kernel_ms_note": f"nnrt_fitter_time_kernels: per-iteration device time of each kernel in its real context, by differences "
                           f"of graph-captured prefix sequences ({args.kernel_reps} iterations per graph, median of {args.kernel_trials} "
                           f"interleaved trials); 'solve' = {'the arrowhead chain' if arap else 'k_solve_update'}; kernels.*.ms and "

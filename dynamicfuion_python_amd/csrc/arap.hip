@@ -11,7 +11,7 @@
 #include <algorithm>
 
 
-#include "fitter_kernels.hpp"
+#include "arrow_device.hpp"
 
 namespace nnrt {
 
@@ -368,115 +368,7 @@ StemSchurLists build_stem_schur_lists(const int32_t* edges, int E, int n0, int N
 	return L;
 }
 
-// ---- stem back-substitution: x_D = D^-1 (b_D - B x_C) ----
-// node update (R <- R Rodrigues(omega), t += dt) from the node's solved increment x6; updates_out gets x6. The motion
-// the iteration started from is read from state_in (the warp field's state, or a snapshot the iteration restarts from)
-// and the result written to node_state (g is never changed by an update)
-// (state_in may equal node_state: no __restrict__ on either)
-__device__ __forceinline__ void arrow_update_node(int n, const float (&xl)[6], const float* state_in, float* node_state, float* __restrict__ updates_out) {
-	for (int c = 0; c < 6; c++) updates_out[6 * static_cast<int64_t>(n) + c] = xl[c];
-	const float* os = state_in + static_cast<int64_t>(n) * NODE_STRIDE;
-	float* ns = node_state + static_cast<int64_t>(n) * NODE_STRIDE;
-	float old[12];
-	for (int i = 0; i < 12; i++) old[i] = os[3 + i];
-	ns[3] = old[0] + xl[3];
-	ns[4] = old[1] + xl[4];
-	ns[5] = old[2] + xl[5];
-	float dR[9];
-	rodrigues_device(xl[0], xl[1], xl[2], dR);
-	const float* R = old + 3;
-	for (int r = 0; r < 3; r++)
-		for (int c = 0; c < 3; c++) ns[6 + 3 * r + c] = (R[3 * r] * dR[c] + R[3 * r + 1] * dR[3 + c]) + R[3 * r + 2] * dR[6 + c];
-}
-
-// 6 x 6 blocks as nine float4, 6-vectors as three float2 (the same products and sums as element-wise loads)
-__device__ __forceinline__ void load36(const float* src, float (&dst)[36]) {
-	const float4* s4 = reinterpret_cast<const float4*>(src);
-#pragma unroll
-	for (int q = 0; q < 9; q++) {
-		const float4 v = s4[q];
-		dst[4 * q] = v.x;
-		dst[4 * q + 1] = v.y;
-		dst[4 * q + 2] = v.z;
-		dst[4 * q + 3] = v.w;
-	}
-}
-__device__ __forceinline__ void load6(const float* src, float (&dst)[6]) {
-	const float2* x2 = reinterpret_cast<const float2*>(src);
-#pragma unroll
-	for (int q = 0; q < 3; q++) {
-		const float2 v = x2[q];
-		dst[2 * q] = v.x;
-		dst[2 * q + 1] = v.y;
-	}
-}
-
-// stem row i of the back substitution: x_i = D_i^-1 (b_i - sum over its edges e = (i, j) of B_e x_j) in float, edges in
-// CSR order (the one arithmetic every caller shares, so a recomputation is bit-identical)
-__device__ __forceinline__ void stem_solve(int i, const float* __restrict__ dinv, const int* __restrict__ edge_offsets, const int* __restrict__ edge_list,
-                                           const int32_t* __restrict__ edges, const float* __restrict__ wing, const float* __restrict__ rhs,
-                                           const float* __restrict__ x, float (&o)[6]) {
-	float r6[6];
-	for (int c = 0; c < 6; c++) r6[c] = rhs[6 * static_cast<int64_t>(i) + c];
-	for (int ei = edge_offsets[i]; ei < edge_offsets[i + 1]; ei++) {
-		const int e = edge_list[ei];
-		const int j = edges[2 * e + 1];
-		float B[36], xj[6];
-		load36(wing + static_cast<int64_t>(e) * 36, B);
-		load6(x + 6 * static_cast<int64_t>(j), xj);
-#pragma unroll
-		for (int r = 0; r < 6; r++) {
-			float acc = 0.f;
-#pragma unroll
-			for (int k = 0; k < 6; k++) acc += B[6 * r + k] * xj[k];
-			r6[r] -= acc;
-		}
-	}
-	float D[36];
-	load36(dinv + static_cast<int64_t>(i) * 36, D);
-#pragma unroll
-	for (int r = 0; r < 6; r++) {
-		float acc = 0.f;
-#pragma unroll
-		for (int k = 0; k < 6; k++) acc += D[6 * r + k] * r6[k];
-		o[r] = acc;
-	}
-}
-
-// residual of stem row i, rhs_i - D_i x_i - sum over its edges of B_e x_j, the products and sums in double, rounded once
-// (D_i: the prepared diagonal block with LM; stem nodes couple to corner nodes only)
-__device__ __forceinline__ void stem_residual(int i, const float (&xi)[6], const float* __restrict__ diag, const int* __restrict__ edge_offsets,
-                                              const int* __restrict__ edge_list, const int32_t* __restrict__ edges, const float* __restrict__ wing,
-                                              const float* __restrict__ rhs, const float* __restrict__ x, float (&res)[6]) {
-	double r[6];
-	float D[36];
-	load36(diag + static_cast<int64_t>(i) * 36, D);
-#pragma unroll
-	for (int c = 0; c < 6; c++) {
-		double s = static_cast<double>(rhs[6 * static_cast<int64_t>(i) + c]);
-#pragma unroll
-		for (int k = 0; k < 6; k++) s -= static_cast<double>(D[6 * c + k]) * static_cast<double>(xi[k]);
-		r[c] = s;
-	}
-	for (int ei = edge_offsets[i]; ei < edge_offsets[i + 1]; ei++) {
-		const int e = edge_list[ei];
-		float B[36], xj[6];
-		load36(wing + static_cast<int64_t>(e) * 36, B);
-		load6(x + 6 * static_cast<int64_t>(edges[2 * e + 1]), xj);
-#pragma unroll
-		for (int c = 0; c < 6; c++)
-#pragma unroll
-			for (int k = 0; k < 6; k++) r[c] -= static_cast<double>(B[6 * c + k]) * static_cast<double>(xj[k]);
-	}
-#pragma unroll
-	for (int c = 0; c < 6; c++) res[c] = static_cast<float>(r[c]);
-}
-
-// threads [0, n0): stem back substitution (and, with node_state, that node's update from the x it just formed);
-// threads [n0, n_update): the corner nodes' updates from the corner solve's x (node_state non-null only).
-// x_base (refinement pass): x holds the correction d (rhs = the residual); the solution is x_base + d, written to x_base
-// and applied (x_base is read and written by its own thread only; x is read across threads and only written by stem
-// threads at their own rows, which no thread of the launch reads).
+// ---- stem back-substitution: x_D = D^-1 (b_D - B x_C) (arrow_device.hpp: arrow_back_node) ----
 // gate (refinement; nullable): mode 1 = the first pass of a gated refinement: x_i always, the update only when the
 // refinement does not run, else the stem residual r_i -> res; mode 2 = the refinement's last pass: runs only when it does.
 __global__ void k_arrow_back(int n0, int n_update, const float* __restrict__ dinv, const int* __restrict__ edge_offsets, const int* __restrict__ edge_list,
@@ -490,55 +382,14 @@ __global__ void k_arrow_back(int n0, int n_update, const float* __restrict__ din
 		refining = refine_gate_on(gate, ratio);
 		if (!refining) return;
 	}
-	// mode 1: the gate word only decides what happens after the stem solve: its load is issued here and first waited for
-	// after the solve's own loads (corner-node threads use it at once)
-	const unsigned gate_word = gate && mode == 1 ? *gate : 0u;
-	if (gate && mode == 1 && i >= n0) {
-		refining = refine_window(__uint_as_float(gate_word), ratio);
-		if (refining) node_state = nullptr;   // the refinement's last pass applies the update
-	}
-	if (i >= n0) {
-		if (i < n_update && (node_state || x_base)) {
-			float xl[6];
-			for (int c = 0; c < 6; c++) xl[c] = x[6 * static_cast<int64_t>(i) + c];
-			if (x_base)
-				for (int c = 0; c < 6; c++) {
-					xl[c] = x_base[6 * static_cast<int64_t>(i) + c] + xl[c];
-					x_base[6 * static_cast<int64_t>(i) + c] = xl[c];
-				}
-			if (node_state) arrow_update_node(i, xl, state_in, node_state, updates_out);
-		}
-		return;
-	}
-	float o[6];
-	stem_solve(i, dinv, edge_offsets, edge_list, edges, wing, rhs, x, o);
-	if (gate && mode == 1) {
-		refining = refine_window(__uint_as_float(gate_word), ratio);
-		if (refining) node_state = nullptr;
-	}
-	float2* xo = reinterpret_cast<float2*>(x + 6 * static_cast<int64_t>(i));
-#pragma unroll
-	for (int q = 0; q < 3; q++) xo[q] = make_float2(o[2 * q], o[2 * q + 1]);
-	if (mode == 1 && refining) {   // the stem row's residual (reads only corner x: no thread of this launch writes those)
-		float ri[6];
-		stem_residual(i, o, diag, edge_offsets, edge_list, edges, wing, rhs, x, ri);
-		float2* ro = reinterpret_cast<float2*>(res + 6 * static_cast<int64_t>(i));
-#pragma unroll
-		for (int q = 0; q < 3; q++) ro[q] = make_float2(ri[2 * q], ri[2 * q + 1]);
-	}
-	if (x_base)
-#pragma unroll
-		for (int c = 0; c < 6; c++) {
-			o[c] = x_base[6 * static_cast<int64_t>(i) + c] + o[c];
-			x_base[6 * static_cast<int64_t>(i) + c] = o[c];
-		}
-	if (node_state) arrow_update_node(i, o, state_in, node_state, updates_out);
+	if (gate && mode == 1) refining = refine_gate_on(gate, ratio);
+	if (i >= n_update && i >= n0) return;
+	arrow_back_node(i, n0, n_update, dinv, edge_offsets, edge_list, edges, wing, rhs, x, XPlain{x}, state_in, node_state, updates_out, x_base,
+	                gate ? mode : 0, refining, diag, res);
 }
 
 // ---- iterative refinement: the correction's corner right-hand side (one wave per corner node a; runs only when the gate
-// is on): rhs2[perm(a)] = r_a - sum over stem edges i -> a of (D_i^-1 B_ia)^T r_i, with r_a = b_a - D_a x_a - sum over
-// a's incidences of the wing blocks times x (B^T x_i for stem edges, B x_b / B^T x_b for corner edges), products and sums
-// in double, rounded once; x_i, r_i of the stem rows from the first back-substitution pass ----
+// is on; arrow_device.hpp: refine_rhs_node) ----
 __global__ __launch_bounds__(256) void k_refine_corner_rhs(int n0, int nc, const float* __restrict__ dinv_b, const float* __restrict__ diag,
                                                            const int* __restrict__ inc_off, const int* __restrict__ inc_list,
                                                            const int32_t* __restrict__ edges, const float* __restrict__ wing,
@@ -548,57 +399,8 @@ __global__ __launch_bounds__(256) void k_refine_corner_rhs(int n0, int nc, const
 	const int a = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
 	const int lane = static_cast<int>(threadIdx.x & 63);
 	if (a >= nc) return;
-	const int n = n0 + a;
-	double ra[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};   // this lane's share of sum H_an x_n over a's incidences
-	float s2[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};    // this lane's share of sum (D_i^-1 B_ia)^T r_i
-	for (int u = inc_off[n] + lane; u < inc_off[n + 1]; u += 64) {
-		const int code = inc_list[u];
-		const int e = code >> 1;
-		const bool tgt = code & 1;
-		const int other = edges[2 * e + (tgt ? 0 : 1)];
-		float B[36], xo[6];
-		load36(wing + static_cast<int64_t>(e) * 36, B);
-		load6(x + 6 * static_cast<int64_t>(other), xo);
-		if (other < n0) {   // stem edge other -> n
-			float ri[6], Y[36];
-			load6(res + 6 * static_cast<int64_t>(other), ri);
-			load36(dinv_b + static_cast<int64_t>(e) * 36, Y);
-#pragma unroll
-			for (int c = 0; c < 6; c++) {
-				float t = 0.f;
-#pragma unroll
-				for (int k = 0; k < 6; k++) t += Y[6 * k + c] * ri[k];
-				s2[c] += t;
-			}
-		}
-#pragma unroll
-		for (int c = 0; c < 6; c++)
-#pragma unroll
-			for (int k = 0; k < 6; k++) ra[c] += static_cast<double>(tgt ? B[6 * k + c] : B[6 * c + k]) * static_cast<double>(xo[k]);
-	}
-#pragma unroll
-	for (int c = 0; c < 6; c++)
-#pragma unroll
-		for (int off = 32; off > 0; off >>= 1) {
-			ra[c] += __shfl_xor(ra[c], off);
-			s2[c] += __shfl_xor(s2[c], off);
-		}
-	if (lane < 6) {
-		double t = 0.0;
-		float u = 0.f;
-#pragma unroll
-		for (int c = 0; c < 6; c++)
-			if (lane == c) {
-				t = ra[c];
-				u = s2[c];
-			}
-		float xa[6];
-		load6(x + 6 * static_cast<int64_t>(n), xa);
-		double r = static_cast<double>(rhs[6 * static_cast<int64_t>(n) + lane]);
-#pragma unroll
-		for (int k = 0; k < 6; k++) r -= static_cast<double>(diag[static_cast<int64_t>(n) * 36 + 6 * lane + k]) * static_cast<double>(xa[k]);
-		rhs2[node_row[a] + lane] = static_cast<float>(r - t) - u;
-	}
+	const float v = refine_rhs_node(a, lane, n0, dinv_b, diag, inc_off, inc_list, edges, wing, rhs, x, res);
+	if (lane < 6) rhs2[node_row[a] + lane] = v;
 }
 
 nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* edges, const float* wing, int* error_flag, hipStream_t stream,
@@ -631,11 +433,50 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 			NNRT_LAUNCH_CHECK();
 		}
 	}
+	const bool refine = ws.refine && ws.inc_off && ws.res && ws.dx && m > 0;
+	if (m > 0 && ws.corner->flow_ok()) {
+		// the corner's factorization, then two dataflow launches (corner.hip k_corner_flow): the back substitution chains
+		// with the stem pass (x, the update or, when the refinement gate opens, the stem residual), and the gated
+		// refinement step (empty when the gate is shut)
+		nnrt_status st = ws.corner->launch_factor(error_flag, stream);
+		if (st) return st;
+		FlowStem fs;
+		fs.n0 = ws.n0;
+		fs.N = ws.N;
+		fs.n_update = node_state ? ws.N : ws.n0;
+		fs.mode = refine ? 1 : 0;
+		fs.dinv = ws.dinv;
+		fs.wing = wing;
+		fs.diag = ws.diag;
+		fs.dinv_b = ws.dinv_b;
+		fs.edge_offsets = ws.edge_offsets;
+		fs.edge_list = ws.edge_list;
+		fs.inc_off = ws.inc_off;
+		fs.inc_list = ws.inc_list;
+		fs.edges = edges;
+		fs.rhs = ws.rhs;
+		fs.x = ws.x;
+		fs.state_in = state_in;
+		fs.node_state = node_state;
+		fs.updates_out = updates_out;
+		fs.res = ws.res;
+		fs.gate = refine ? ws.corner->pivot_ratio() : nullptr;
+		fs.ratio = ws.refine_ratio;
+		fs.error_flag = error_flag;
+		if ((st = ws.corner->launch_flow(0, fs, stream))) return st;
+		if (!refine) return NNRT_OK;
+		fs.n_update = ws.N;
+		fs.mode = 2;
+		fs.rhs = ws.res;
+		fs.x = ws.dx;
+		fs.x_base = ws.x;
+		fs.rhs_b = ws.rhs;
+		return ws.corner->launch_flow(1, fs, stream);
+	}
 	if (m > 0) {
 		nnrt_status st = ws.corner->launch_solve(ws.x + 6 * static_cast<int64_t>(ws.n0), error_flag, stream);
 		if (st) return st;
 	}
-	const bool refine = ws.refine && ws.inc_off && ws.res && ws.dx && m > 0;
 	if (!refine) {
 		// with node_state, the node updates ride along (all N nodes) in the back-substitution launch
 		const int threads = node_state ? ws.N : ws.n0;

@@ -1,0 +1,272 @@
+// Device helpers of the arrowhead solve's stem side, shared by the per-stage kernels (arap.hip) and the corner's dataflow
+// substitution launches (corner.hip k_corner_flow): the stem back substitution x_D = D^-1 (b_D - B x_C)
+// (SolveBlockSparseArrowheadCholesky.cpp:84-90), the fp64 residual rows of the gated refinement,
+// the corner right-hand side of the refinement's correction, and the node update R <- R Rodrigues(w), t += dt
+// (HierarchicalGraphWarpField.cpp:261-282, A10).
+//
+// Vectors that another workgroup of the same launch writes are read through a loader (XSc1: sc1 loads that bypass this
+// CU's L1, the hand-off form of MI355X_MICROARCH.md "inter-workgroup visibility"); vectors from earlier launches through
+// XPlain. Both give the same values and the same arithmetic.
+#pragma once
+
+#include "fitter_kernels.hpp"
+
+namespace nnrt {
+
+typedef int flow_v2i __attribute__((ext_vector_type(2)));
+typedef int flow_v4i __attribute__((ext_vector_type(4)));
+
+// buffer descriptor over n bytes at p (p, n wave-uniform: kernel arguments)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t flow_rsrc(const void* p, int64_t bytes) {
+	return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, static_cast<int>(bytes), 0x00020000);
+}
+// sc1 (L1-bypassing) loads through a descriptor, byte offsets
+__device__ __forceinline__ float4 ld_sc1_f4(__amdgpu_buffer_rsrc_t r, int off) {
+	return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+}
+__device__ __forceinline__ float2 ld_sc1_f2(__amdgpu_buffer_rsrc_t r, int off) {
+	return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 16));
+}
+__device__ __forceinline__ float ld_sc1_f(__amdgpu_buffer_rsrc_t r, int off) {
+	return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 16));
+}
+// sc1 (write-through) store of one float
+__device__ __forceinline__ void st_sc1(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// 6 x 6 blocks as nine float4, 6-vectors as three float2 (the same products and sums as element-wise loads)
+__device__ __forceinline__ void load36(const float* src, float (&dst)[36]) {
+	const float4* s4 = reinterpret_cast<const float4*>(src);
+#pragma unroll
+	for (int q = 0; q < 9; q++) {
+		const float4 v = s4[q];
+		dst[4 * q] = v.x;
+		dst[4 * q + 1] = v.y;
+		dst[4 * q + 2] = v.z;
+		dst[4 * q + 3] = v.w;
+	}
+}
+__device__ __forceinline__ void load6(const float* src, float (&dst)[6]) {
+	const float2* x2 = reinterpret_cast<const float2*>(src);
+#pragma unroll
+	for (int q = 0; q < 3; q++) {
+		const float2 v = x2[q];
+		dst[2 * q] = v.x;
+		dst[2 * q + 1] = v.y;
+	}
+}
+
+// 6-float node rows of a vector: from an earlier launch (plain loads) ...
+struct XPlain {
+	const float* p;
+	__device__ __forceinline__ void ld6(int64_t node, float (&o)[6]) const { load6(p + 6 * node, o); }
+};
+// ... or written by other workgroups of this launch (sc1 loads; base = the vector's first float, bytes = its size)
+struct XSc1 {
+	__amdgpu_buffer_rsrc_t r;
+	__device__ __forceinline__ void ld6(int64_t node, float (&o)[6]) const {
+#pragma unroll
+		for (int q = 0; q < 3; q++) {
+			const float2 v = ld_sc1_f2(r, static_cast<int>(24 * node + 8 * q));
+			o[2 * q] = v.x;
+			o[2 * q + 1] = v.y;
+		}
+	}
+};
+
+// node update (R <- R Rodrigues(omega), t += dt) from the node's solved increment x6; updates_out gets x6. The motion
+// the iteration started from is read from state_in (the warp field's state, or a snapshot the iteration restarts from)
+// and the result written to node_state (g is never changed by an update)
+// (state_in may equal node_state: no __restrict__ on either)
+__device__ __forceinline__ void arrow_update_node(int n, const float (&xl)[6], const float* state_in, float* node_state, float* __restrict__ updates_out) {
+	for (int c = 0; c < 6; c++) updates_out[6 * static_cast<int64_t>(n) + c] = xl[c];
+	const float* os = state_in + static_cast<int64_t>(n) * NODE_STRIDE;
+	float* ns = node_state + static_cast<int64_t>(n) * NODE_STRIDE;
+	float old[12];
+	for (int i = 0; i < 12; i++) old[i] = os[3 + i];
+	ns[3] = old[0] + xl[3];
+	ns[4] = old[1] + xl[4];
+	ns[5] = old[2] + xl[5];
+	float dR[9];
+	rodrigues_device(xl[0], xl[1], xl[2], dR);
+	const float* R = old + 3;
+	for (int r = 0; r < 3; r++)
+		for (int c = 0; c < 3; c++) ns[6 + 3 * r + c] = (R[3 * r] * dR[c] + R[3 * r + 1] * dR[3 + c]) + R[3 * r + 2] * dR[6 + c];
+}
+
+// stem row i of the back substitution: x_i = D_i^-1 (b_i - sum over its edges e = (i, j) of B_e x_j) in float, edges in
+// CSR order (the one arithmetic every caller shares, so a recomputation is bit-identical)
+template <class XL>
+__device__ __forceinline__ void stem_solve(int i, const float* __restrict__ dinv, const int* __restrict__ edge_offsets, const int* __restrict__ edge_list,
+                                           const int32_t* __restrict__ edges, const float* __restrict__ wing, const float* __restrict__ rhs,
+                                           const XL& x, float (&o)[6]) {
+	float r6[6];
+	for (int c = 0; c < 6; c++) r6[c] = rhs[6 * static_cast<int64_t>(i) + c];
+	for (int ei = edge_offsets[i]; ei < edge_offsets[i + 1]; ei++) {
+		const int e = edge_list[ei];
+		const int j = edges[2 * e + 1];
+		float B[36], xj[6];
+		load36(wing + static_cast<int64_t>(e) * 36, B);
+		x.ld6(j, xj);
+#pragma unroll
+		for (int r = 0; r < 6; r++) {
+			float acc = 0.f;
+#pragma unroll
+			for (int k = 0; k < 6; k++) acc += B[6 * r + k] * xj[k];
+			r6[r] -= acc;
+		}
+	}
+	float D[36];
+	load36(dinv + static_cast<int64_t>(i) * 36, D);
+#pragma unroll
+	for (int r = 0; r < 6; r++) {
+		float acc = 0.f;
+#pragma unroll
+		for (int k = 0; k < 6; k++) acc += D[6 * r + k] * r6[k];
+		o[r] = acc;
+	}
+}
+
+// residual of stem row i, rhs_i - D_i x_i - sum over its edges of B_e x_j, the products and sums in double, rounded once
+// (D_i: the prepared diagonal block with LM; stem nodes couple to corner nodes only)
+template <class XL>
+__device__ __forceinline__ void stem_residual(int i, const float (&xi)[6], const float* __restrict__ diag, const int* __restrict__ edge_offsets,
+                                              const int* __restrict__ edge_list, const int32_t* __restrict__ edges, const float* __restrict__ wing,
+                                              const float* __restrict__ rhs, const XL& x, float (&res)[6]) {
+	double r[6];
+	float D[36];
+	load36(diag + static_cast<int64_t>(i) * 36, D);
+#pragma unroll
+	for (int c = 0; c < 6; c++) {
+		double s = static_cast<double>(rhs[6 * static_cast<int64_t>(i) + c]);
+#pragma unroll
+		for (int k = 0; k < 6; k++) s -= static_cast<double>(D[6 * c + k]) * static_cast<double>(xi[k]);
+		r[c] = s;
+	}
+	for (int ei = edge_offsets[i]; ei < edge_offsets[i + 1]; ei++) {
+		const int e = edge_list[ei];
+		float B[36], xj[6];
+		load36(wing + static_cast<int64_t>(e) * 36, B);
+		x.ld6(edges[2 * e + 1], xj);
+#pragma unroll
+		for (int c = 0; c < 6; c++)
+#pragma unroll
+			for (int k = 0; k < 6; k++) r[c] -= static_cast<double>(B[6 * c + k]) * static_cast<double>(xj[k]);
+	}
+#pragma unroll
+	for (int c = 0; c < 6; c++) res[c] = static_cast<float>(r[c]);
+}
+
+// The stem side of one arrowhead back-substitution pass for node i (one thread per node):
+// i < n0: stem back substitution (and, with node_state, that node's update from the x it just formed);
+// n0 <= i < n_update: the corner node's update from the corner solve's x (node_state non-null only).
+// x_base (refinement pass): x holds the correction d (rhs = the residual); the solution is x_base + d, written to x_base
+// and applied (x_base is read and written by its own thread only; x is read across threads and only written by stem
+// threads at their own rows, which no thread of the pass reads).
+// mode 1 = the first pass of a gated refinement (refining: the gate's decision): x_i always, the update only when the
+// refinement does not run, else the stem residual r_i -> res; mode 2 = the refinement's last pass.
+// xc: the loader of x's corner rows (written by the corner substitution).
+template <class XL>
+__device__ __forceinline__ void arrow_back_node(int i, int n0, int n_update, const float* __restrict__ dinv, const int* __restrict__ edge_offsets,
+                                                const int* __restrict__ edge_list, const int32_t* __restrict__ edges, const float* __restrict__ wing,
+                                                const float* __restrict__ rhs, float* __restrict__ x, const XL& xc, const float* state_in, float* node_state,
+                                                float* __restrict__ updates_out, float* __restrict__ x_base, int mode, bool refining,
+                                                const float* __restrict__ diag, float* __restrict__ res) {
+	if (mode == 1 && refining) node_state = nullptr;   // the refinement's last pass applies the update
+	if (i >= n0) {
+		if (i < n_update && (node_state || x_base)) {
+			float xl[6];
+			xc.ld6(i, xl);
+			if (x_base)
+				for (int c = 0; c < 6; c++) {
+					xl[c] = x_base[6 * static_cast<int64_t>(i) + c] + xl[c];
+					x_base[6 * static_cast<int64_t>(i) + c] = xl[c];
+				}
+			if (node_state) arrow_update_node(i, xl, state_in, node_state, updates_out);
+		}
+		return;
+	}
+	float o[6];
+	stem_solve(i, dinv, edge_offsets, edge_list, edges, wing, rhs, xc, o);
+	float2* xo = reinterpret_cast<float2*>(x + 6 * static_cast<int64_t>(i));
+#pragma unroll
+	for (int q = 0; q < 3; q++) xo[q] = make_float2(o[2 * q], o[2 * q + 1]);
+	if (mode == 1 && refining) {   // the stem row's residual (reads only corner x: no thread of this pass writes those)
+		float ri[6];
+		stem_residual(i, o, diag, edge_offsets, edge_list, edges, wing, rhs, xc, ri);
+		float2* ro = reinterpret_cast<float2*>(res + 6 * static_cast<int64_t>(i));
+#pragma unroll
+		for (int q = 0; q < 3; q++) ro[q] = make_float2(ri[2 * q], ri[2 * q + 1]);
+	}
+	if (x_base)
+#pragma unroll
+		for (int c = 0; c < 6; c++) {
+			o[c] = x_base[6 * static_cast<int64_t>(i) + c] + o[c];
+			x_base[6 * static_cast<int64_t>(i) + c] = o[c];
+		}
+	if (node_state) arrow_update_node(i, o, state_in, node_state, updates_out);
+}
+
+// ---- iterative refinement: the correction's corner right-hand side of corner node a (one wave; lane < 6 returns entry
+// `lane`, others 0): r_a - sum over stem edges i -> a of (D_i^-1 B_ia)^T r_i, with r_a = b_a - D_a x_a - sum over a's
+// incidences of the wing blocks times x (B^T x_i for stem edges, B x_b / B^T x_b for corner edges), products and sums in
+// double, rounded once; x (all rows) and r_i of the stem rows from the first back-substitution pass (earlier launches) ----
+__device__ __forceinline__ float refine_rhs_node(int a, int lane, int n0, const float* __restrict__ dinv_b, const float* __restrict__ diag,
+                                                 const int* __restrict__ inc_off, const int* __restrict__ inc_list, const int32_t* __restrict__ edges,
+                                                 const float* __restrict__ wing, const float* __restrict__ rhs, const float* __restrict__ x,
+                                                 const float* __restrict__ res) {
+	const int n = n0 + a;
+	double ra[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};   // this lane's share of sum H_an x_n over a's incidences
+	float s2[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};    // this lane's share of sum (D_i^-1 B_ia)^T r_i
+	for (int u = inc_off[n] + lane; u < inc_off[n + 1]; u += 64) {
+		const int code = inc_list[u];
+		const int e = code >> 1;
+		const bool tgt = code & 1;
+		const int other = edges[2 * e + (tgt ? 0 : 1)];
+		float B[36], xo[6];
+		load36(wing + static_cast<int64_t>(e) * 36, B);
+		load6(x + 6 * static_cast<int64_t>(other), xo);
+		if (other < n0) {   // stem edge other -> n
+			float ri[6], Y[36];
+			load6(res + 6 * static_cast<int64_t>(other), ri);
+			load36(dinv_b + static_cast<int64_t>(e) * 36, Y);
+#pragma unroll
+			for (int c = 0; c < 6; c++) {
+				float t = 0.f;
+#pragma unroll
+				for (int k = 0; k < 6; k++) t += Y[6 * k + c] * ri[k];
+				s2[c] += t;
+			}
+		}
+#pragma unroll
+		for (int c = 0; c < 6; c++)
+#pragma unroll
+			for (int k = 0; k < 6; k++) ra[c] += static_cast<double>(tgt ? B[6 * k + c] : B[6 * c + k]) * static_cast<double>(xo[k]);
+	}
+#pragma unroll
+	for (int c = 0; c < 6; c++)
+#pragma unroll
+		for (int off = 32; off > 0; off >>= 1) {
+			ra[c] += __shfl_xor(ra[c], off);
+			s2[c] += __shfl_xor(s2[c], off);
+		}
+	float out = 0.f;
+	if (lane < 6) {
+		double t = 0.0;
+		float u = 0.f;
+#pragma unroll
+		for (int c = 0; c < 6; c++)
+			if (lane == c) {
+				t = ra[c];
+				u = s2[c];
+			}
+		float xa[6];
+		load6(x + 6 * static_cast<int64_t>(n), xa);
+		double r = static_cast<double>(rhs[6 * static_cast<int64_t>(n) + lane]);
+#pragma unroll
+		for (int k = 0; k < 6; k++) r -= static_cast<double>(diag[static_cast<int64_t>(n) * 36 + 6 * lane + k]) * static_cast<double>(xa[k]);
+		out = static_cast<float>(r - t) - u;
+	}
+	return out;
+}
+
+} // namespace nnrt

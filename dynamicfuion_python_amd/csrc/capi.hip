@@ -396,6 +396,7 @@ struct nnrt_fitter {
 	DeviceBuffer<int2> a_tgt_ab, a_pairs;
 	ArrowheadWorkspace aw;
 	float refine_ratio = NNRT_REFINE_PIVOT_RATIO;   // refinement gate threshold (nnrt_fitter_set_refine_ratio)
+	float refine_ratio_used = NNRT_REFINE_PIVOT_RATIO;   // the threshold the last launched iterations ran with (refine_info)
 	int n0 = 0;
 	int last_mode = 0;
 	DeviceBuffer<float> snapshot;   // [N,16] node state stored by nnrt_fitter_snapshot_motion (restore-before-iteration runs)
@@ -952,6 +953,7 @@ int restart_of(int reset, bool first_of_call) {
 }
 
 nnrt_status iterate_impl(nnrt_fitter* ft, nnrt_warp_field* wf, int32_t first_iteration, int32_t count, int reset, hipStream_t us) {
+	ft->refine_ratio_used = ft->refine_ratio;
 	nnrt_status st;
 	for (int it0 = first_iteration; it0 < first_iteration + count; it0 += MAX_GRAPH_ITERATIONS) {
 		const int n = std::min(MAX_GRAPH_ITERATIONS, first_iteration + count - it0);
@@ -1045,8 +1047,10 @@ nnrt_status nnrt_fitter_corner_info(const nnrt_fitter* ft, int64_t* h_out) {
 nnrt_status nnrt_fitter_refine_info(nnrt_fitter* ft, float* h_out, void* stream) {
 	NNRT_CHECK_ARG(ft && h_out, "null pointer");
 	DeviceGuard guard(ft->device);
+	// the gate as the last launched solve applied it: its device pivot word and the threshold it ran with (a later
+	// nnrt_fitter_set_refine_ratio changes the next solve, not the report of this one: ADVICE r4)
 	h_out[0] = 1.f;
-	h_out[1] = ft->refine_ratio;
+	h_out[1] = ft->refine_ratio_used;
 	h_out[2] = 0.f;
 	if (ft->E > 0 && ft->corner.pivot_ratio()) {
 		NNRT_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
@@ -1056,7 +1060,7 @@ nnrt_status nnrt_fitter_refine_info(nnrt_fitter* ft, float* h_out, void* stream)
 		float r;
 		std::memcpy(&r, &bits, sizeof(r));
 		h_out[0] = r;
-		h_out[2] = (NNRT_ARAP_REFINE != 0 && refine_window(r, ft->refine_ratio)) ? 1.f : 0.f;
+		h_out[2] = (NNRT_ARAP_REFINE != 0 && refine_window(r, ft->refine_ratio_used)) ? 1.f : 0.f;
 	}
 	return NNRT_OK;
 }
@@ -1134,6 +1138,7 @@ nnrt_status nnrt_fitter_iterate_timed(nnrt_fitter* ft, nnrt_warp_field* wf, int3
 	NNRT_CHECK_ARG(ft && wf && h_stage_ms && count > 0, "invalid arguments");
 	if (nnrt_status cst = check_frame(ft, wf, "nnrt_fitter_iterate_timed")) return cst;
 	DeviceGuard guard(ft->device);
+	ft->refine_ratio_used = ft->refine_ratio;
 	hipStream_t us = static_cast<hipStream_t>(stream);
 	NNRT_HIP(hipEventRecord(ft->ev_in, us));
 	NNRT_HIP(hipStreamWaitEvent(ft->work, ft->ev_in, 0));
@@ -1176,6 +1181,7 @@ nnrt_status nnrt_fitter_time_kernels(nnrt_fitter* ft, nnrt_warp_field* wf, int32
 	hipStream_t s = ft->work;
 	NNRT_HIP(hipEventRecord(ft->ev_in, us));
 	NNRT_HIP(hipStreamWaitEvent(s, ft->ev_in, 0));
+	ft->refine_ratio_used = ft->refine_ratio;
 	// prefix sequences, each `reps` iterations from the snapshot state in one graph: every kernel runs after the launch
 	// it follows in a real iteration (the raster alone excepted, which repeats its own idempotent scatter)
 	const unsigned seq[4] = {STAGE_ALL, STAGE_RASTER | STAGE_PIXEL | STAGE_SOLVE, STAGE_RASTER | STAGE_PIXEL, STAGE_RASTER};
@@ -1193,11 +1199,11 @@ nnrt_status nnrt_fitter_time_kernels(nnrt_fitter* ft, nnrt_warp_field* wf, int32
 			nnrt_status cs = NNRT_OK;
 			for (int i = 0; i < reps && !cs; i++) cs = enqueue_iteration(ft, wf, mode, s, nullptr, false, ft->snapshot.ptr, seq[q]);
 			hipError_t ce = hipStreamEndCapture(s, &g);
-			if (cs) {
+			if (cs || ce != hipSuccess) {   // a partially returned graph is destroyed on every early exit
 				if (g) hipGraphDestroy(g);
-				return cs;
+				if (cs) return cs;
+				NNRT_HIP(ce);
 			}
-			NNRT_HIP(ce);
 			hipError_t ie = hipGraphInstantiate(&exec[q], g, nullptr, nullptr, 0);
 			hipGraphDestroy(g);
 			NNRT_HIP(ie);
@@ -1235,9 +1241,12 @@ nnrt_status nnrt_fitter_time_kernels(nnrt_fitter* ft, nnrt_warp_field* wf, int32
 		h_kernel_ms[2] = med[2] - med[3];   // fused pixel launch
 		h_kernel_ms[3] = med[1] - med[2];   // solve + update (ARAP: the whole arrowhead chain)
 		h_kernel_ms[4] = med[0];            // whole iteration
-		// leave the fitter as an iteration would: raster keys empty, accumulators zero, motion = the snapshot's result
+		// leave the fitter as an iteration would: raster keys empty, accumulators zero, motion = the snapshot's result;
+		// the device error flag the timing replays may have raised is cleared (nnrt_fitter_check reports the caller's
+		// own iterations only)
 		NNRT_HIP(hipMemsetAsync(ft->keys.ptr, 0xff, sizeof(uint64_t) * P, s));
 		NNRT_HIP(hipMemsetAsync(ft->acc.ptr, 0, sizeof(double) * static_cast<size_t>(ft->N) * ACC_STRIDE, s));
+		NNRT_HIP(hipMemsetAsync(ft->error_flag.ptr, 0, sizeof(int), s));
 	}
 	NNRT_HIP(hipEventRecord(ft->ev_out, s));
 	NNRT_HIP(hipStreamWaitEvent(us, ft->ev_out, 0));
@@ -1252,6 +1261,10 @@ nnrt_status nnrt_fitter_check(nnrt_fitter* ft, void* stream) {
 	int flag = 0;
 	NNRT_HIP(hipMemcpy(&flag, ft->error_flag.ptr, sizeof(int), hipMemcpyDeviceToHost));
 	NNRT_HIP(hipMemset(ft->error_flag.ptr, 0, sizeof(int)));
+	if (flag & 8) {
+		set_error("the corner's dataflow substitution launch gave up waiting on a dependency (k_corner_flow spin bound)");
+		return NNRT_ERROR_HIP;
+	}
 	if (flag & 1) {
 		set_error("potrf failed: a Hessian block (or the Schur complement) is not positive-definite (reference NNRT_LAPACK_CHECK, "
 		          "SolveBlockDiagonalCholeskyCPU.cpp:48-51)");
@@ -1815,6 +1828,10 @@ nnrt_status nnrt_solve_block_sparse_arrowhead_cholesky(const float* d_diag, cons
 		}
 	}
 	if (st) return st;
+	if (host_flag & 8) {
+		set_error("arrowhead solve: the corner's dataflow substitution launch gave up waiting on a dependency (k_corner_flow spin bound)");
+		return NNRT_ERROR_HIP;
+	}
 	if (host_flag) {
 		set_error("arrowhead solve: a stem block or the Schur complement is not positive-definite");
 		return NNRT_ERROR_NOT_POSITIVE_DEFINITE;

@@ -24,11 +24,14 @@
 // order, which changes float rounding only (the tests hold the solve against the oracle and an fp64 solution).
 #include <algorithm>
 #include <cfloat>
+#include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
+#include <set>
 #include <tuple>
 
-#include "fitter_kernels.hpp"
+#include "arrow_device.hpp"
 
 namespace nnrt {
 
@@ -252,6 +255,10 @@ struct CornerPlan {
 	// row entries L_Jk (ascending k) then its head
 	std::vector<int4> walk_back, walk_fwd;
 	std::vector<int> corner_edges;    // edges between two corner nodes (>= 3 layers)
+	// dataflow launches (k_corner_flow): per back chain b (back column first, column count, forward column first, parent
+	// back chain or -1); columns + child chains; the back chain of every tile column
+	std::vector<int4> flow_chains;
+	std::vector<int> flow_need, col_chain;
 };
 
 static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const float* corner_pos) {
@@ -433,9 +440,11 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 		for (int J : chain_cols[c]) chain_of[static_cast<size_t>(J)] = static_cast<int>(c);
 	p.back_off.push_back(0);
 	p.back_pre_off.push_back(0);
+	std::vector<int> bidx(chain_cols.size(), -1);   // chain -> back chain index
 	for (int d = 0; d <= depth_max; d++) {
 		for (size_t c = 0; c < chain_cols.size(); c++) {
 			if (chain_depth[c] != d) continue;
+			bidx[c] = static_cast<int>(p.back_chains.size());
 			p.back_chains.push_back(make_int2(static_cast<int>(p.back_cols.size()), static_cast<int>(chain_cols[c].size())));
 			for (int J : chain_cols[c]) {
 				const auto& cc = cs[static_cast<size_t>(J)];
@@ -466,6 +475,19 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 			p.walk_fwd.push_back(head(J));
 		}
 	}
+	// dataflow plan: chain parents (the chain of the top column's parent), columns + child chains, column -> chain
+	p.flow_chains.assign(p.back_chains.size(), make_int4(0, 0, 0, -1));
+	p.flow_need.assign(p.back_chains.size(), 0);
+	p.col_chain.assign(static_cast<size_t>(T), -1);
+	for (size_t c = 0; c < chain_cols.size(); c++) {
+		const int b = bidx[c];
+		const int top = chain_cols[c].front(), bottom = chain_cols[c].back();
+		const int par = parent[static_cast<size_t>(top)];
+		p.flow_chains[static_cast<size_t>(b)] = make_int4(p.back_chains[static_cast<size_t>(b)].x, p.back_chains[static_cast<size_t>(b)].y, 0,
+		                                                  par < 0 ? -1 : bidx[static_cast<size_t>(chain_of[static_cast<size_t>(par)])]);
+		p.flow_need[static_cast<size_t>(b)] = static_cast<int>(chain_cols[c].size() + kids[static_cast<size_t>(bottom)].size());
+		for (int J : chain_cols[c]) p.col_chain[static_cast<size_t>(J)] = b;
+	}
 	// forward chains: row entries of every column, then the back launches in reverse with each chain reversed
 	std::vector<std::vector<int2>> rows(static_cast<size_t>(T));
 	for (size_t sl = 0; sl < p.slot_ij.size(); sl++)
@@ -475,6 +497,7 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 	for (int l = static_cast<int>(p.back_off.size()) - 2; l >= 0; l--) {
 		for (int c = p.back_off[static_cast<size_t>(l)]; c < p.back_off[static_cast<size_t>(l) + 1]; c++) {
 			const int2 ch = p.back_chains[static_cast<size_t>(c)];
+			p.flow_chains[static_cast<size_t>(c)].z = static_cast<int>(p.fwd_cols.size());
 			p.fwd_chains.push_back(make_int2(static_cast<int>(p.fwd_cols.size()), ch.y));
 			for (int q = ch.y - 1; q >= 0; q--) {
 				const int4 bc = p.back_cols[static_cast<size_t>(ch.x + q)];
@@ -721,11 +744,15 @@ __device__ __forceinline__ float quad_xor(float v, int ctrl_sel) {   // 0: lanes
 	return __builtin_bit_cast(float, ctrl_sel == 0 ? __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xf, 0xf, false)
 	                                               : __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xf, 0xf, false));
 }
-__global__ __launch_bounds__(CT) void k_corner_invert(const float* __restrict__ ldiag, float* __restrict__ minv) {
+// (workgroup 0 also zeroes the control words of the dataflow substitution launches that follow: k_corner_flow)
+__global__ __launch_bounds__(CT) void k_corner_invert(const float* __restrict__ ldiag, float* __restrict__ minv, unsigned* __restrict__ flow_ctl,
+                                                     int n_ctl) {
 	__shared__ __attribute__((aligned(16))) float s_l[TILE * CS4];
 	__shared__ float s_y[TILE];
 	const int t = threadIdx.x;
 	const int64_t J = blockIdx.x;
+	if (J == 0)
+		for (int i = t; i < n_ctl; i += CT) flow_ctl[i] = 0u;
 	const float4* L4 = reinterpret_cast<const float4*>(ldiag + J * TILE_ELEMS);
 	for (int i = t; i < TILE_ELEMS / 4; i += CT) {   // the lower part; zeros above the diagonal
 		const int r = i >> 4, c0 = 4 * (i & 15);
@@ -953,15 +980,44 @@ __device__ __forceinline__ void tile_to_lds(const float* src, float* dst, int wa
 		__builtin_amdgcn_global_load_lds((corner_global_t*)(src + chunk * 256 + lane * 4), (corner_lds_t*)(dst + chunk * 256), 16, 0, 0);
 	}
 }
-__global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
+// the vector accesses of a substitution pass: plain loads / stores between launches; sc1 (L1-bypassing loads,
+// write-through stores) for the vectors other workgroups of a dataflow launch (k_corner_flow) write and read
+template <bool SC1>
+struct SubstVec {
+	const float* base;
+	__amdgpu_buffer_rsrc_t r;
+	__device__ __forceinline__ SubstVec(const float* p, int64_t n) : base(p) {
+		if constexpr (SC1) r = flow_rsrc(p, 4 * n);
+	}
+	// other: the bytes were written by another workgroup of this launch (sc1 load); else by this workgroup or an earlier
+	// launch (plain load: L1 holds no older copy of a line this workgroup wrote)
+	__device__ __forceinline__ float4 ld4(int64_t i, bool other = true) const {
+		if constexpr (SC1) {
+			if (other) return ld_sc1_f4(r, static_cast<int>(4 * i));
+		}
+		return *reinterpret_cast<const float4*>(base + i);
+	}
+	__device__ __forceinline__ float ld(int64_t i) const {
+		if constexpr (SC1) return ld_sc1_f(r, static_cast<int>(4 * i));
+		else return base[i];
+	}
+	__device__ __forceinline__ void st(int64_t i, float v) const {
+		if constexpr (SC1) st_sc1(const_cast<float*>(base) + i, v);
+		else const_cast<float*>(base)[i] = v;
+	}
+};
+
+// one chain of the back substitution (the body of k_corner_back; k_corner_flow runs it with SC1 vectors)
+template <bool SC1X, bool SC1Y>
+__device__ __forceinline__ void corner_back_chain(const CornerBackArgs& a, int2 ch, int ld, int64_t nxout) {
 	__shared__ __attribute__((aligned(16))) float s_m[TILE_ELEMS];   // L_JJ^-1 of the current column
 	__shared__ __attribute__((aligned(16))) float s_part[4][TILE];
 	__shared__ float s_xq[4][TILE];   // quarters of x_J = M^T z
 	__shared__ int4 s_cols[BACK_COLS];
 	__shared__ int2 s_ent[2][64];   // first 64 entry descriptors of the current (q & 1) and the next column
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-	if (a.gate && !refine_gate_on(a.gate, a.ratio)) return;
-	const int2 ch = a.chains[blockIdx.x];
+	const SubstVec<SC1X> xv_(a.xp, ld), xo_(a.xout, nxout);
+	const SubstVec<SC1Y> yv_(a.cb, ld);
 	for (int q0 = 0; q0 < ch.y; q0 += BACK_COLS) {
 		const int nq = ch.y - q0 < BACK_COLS ? ch.y - q0 : BACK_COLS;
 		if (t < nq) s_cols[t] = a.cols[ch.x + q0 + t];
@@ -977,8 +1033,8 @@ __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 			const int2 sp = subst_span(col, a.mode);
 			// M = L_JJ^-1 streams into LDS behind the entry loads; y_J is loaded ahead of the sums (wave 0)
 			if (a.mode != 1) tile_to_lds(a.minv + static_cast<int64_t>(J) * TILE_ELEMS, s_m, wave, lane);
-			const float* ysrc = a.mode == 2 && col.w > 0 ? a.zx : a.cb;
-			const float yv = ysrc[static_cast<int64_t>(J) * TILE + lane];   // every wave forms z
+			const float yv = a.mode == 2 && col.w > 0 ? a.zx[static_cast<int64_t>(J) * TILE + lane]
+			                                          : yv_.ld(static_cast<int64_t>(J) * TILE + lane);   // every wave forms z
 			const bool has_next = q + 1 < nq;
 			int2 nxt = make_int2(0, 0);
 			if (wave == 1 && has_next) {
@@ -1003,7 +1059,8 @@ __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 						const float* Lj = a.tiles + static_cast<int64_t>(sj) * TILE_ELEMS + (16 * wave + 4 * rq) * TILE + 4 * cg;
 #pragma unroll
 						for (int k = 0; k < 4; k++) l[j][k] = *reinterpret_cast<const float4*>(Lj + k * TILE);
-						const float4 x4 = *reinterpret_cast<const float4*>(a.xp + static_cast<int64_t>(ij) * TILE + 16 * wave + 4 * rq);
+						// entries outside the chain first (col.w of them: x from other workgroups), then the chain's own
+						const float4 x4 = xv_.ld4(static_cast<int64_t>(ij) * TILE + 16 * wave + 4 * rq, e0 + e + j < col.w);
 						xv[j] = ok ? x4 : make_float4(0.f, 0.f, 0.f, 0.f);
 					}
 #pragma unroll
@@ -1045,15 +1102,20 @@ __global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a) {
 				if (wave == 0) {
 					const float x = (s_xq[0][lane] + s_xq[1][lane]) + (s_xq[2][lane] + s_xq[3][lane]);
 					const int64_t row = static_cast<int64_t>(J) * TILE + lane;
-					a.xp[row] = x;
+					xv_.st(row, x);
 					const int rn = a.row_node[row];
-					if (rn >= 0) a.xout[6 * static_cast<int64_t>(rn >> 3) + (rn & 7)] = x;
+					if (rn >= 0) xo_.st(6 * static_cast<int64_t>(rn >> 3) + (rn & 7), x);
 				}
 			}
 			if (wave == 1 && has_next) s_ent[(q + 1) & 1][lane] = nxt;
 			__syncthreads();   // x_J visible to the chain's next column; s_part, s_xq, s_m free; the next column's entries staged
 		}
 	}
+}
+
+__global__ __launch_bounds__(CT) void k_corner_back(CornerBackArgs a, int ld, int64_t nxout) {
+	if (a.gate && !refine_gate_on(a.gate, a.ratio)) return;
+	corner_back_chain<false, false>(a, a.chains[blockIdx.x], ld, nxout);
 }
 
 // Forward substitution L y = b along the forward chains (iterative refinement's corner solve; the first solve's forward
@@ -1075,12 +1137,13 @@ struct CornerFwdArgs {
 	float* zx;               // [ld] pre-sums (modes 1, 2; as CornerBackArgs)
 	int mode;
 };
-__global__ __launch_bounds__(CT) void k_corner_fwd(CornerFwdArgs a) {
+// one chain of the forward substitution (the body of k_corner_fwd; k_corner_flow runs it with SC1 vectors)
+template <bool SC1>
+__device__ __forceinline__ void corner_fwd_chain(const CornerFwdArgs& a, int2 ch, int ld) {
 	__shared__ __attribute__((aligned(16))) float s_m[TILE_ELEMS];   // L_JJ^-1 of the current column
 	__shared__ __attribute__((aligned(16))) float s_z[TILE];
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-	if (a.gate && !refine_gate_on(a.gate, a.ratio)) return;
-	const int2 ch = a.chains[blockIdx.x];
+	const SubstVec<SC1> yv_(a.yb, ld);
 	const int cg = lane & 15, rq = lane >> 4;   // rows 16 wave + 4 rq .. + 3, columns 4 cg .. 4 cg + 3
 	for (int q = 0; q < ch.y; q++) {
 		const int4 col = a.cols[ch.x + q];
@@ -1101,7 +1164,7 @@ __global__ __launch_bounds__(CT) void k_corner_fwd(CornerFwdArgs a) {
 					const float* Lj = a.tiles + static_cast<int64_t>(sj) * TILE_ELEMS + (16 * wave + 4 * rq) * TILE + 4 * cg;
 #pragma unroll
 					for (int k = 0; k < 4; k++) l[j][k] = *reinterpret_cast<const float4*>(Lj + k * TILE);
-					const float4 y4 = *reinterpret_cast<const float4*>(a.yb + static_cast<int64_t>(kj) * TILE + 4 * cg);
+					const float4 y4 = yv_.ld4(static_cast<int64_t>(kj) * TILE + 4 * cg, e0 + e + j < col.w);   // outside entries first
 					yv[j] = ok ? y4 : make_float4(0.f, 0.f, 0.f, 0.f);
 				}
 #pragma unroll
@@ -1115,12 +1178,12 @@ __global__ __launch_bounds__(CT) void k_corner_fwd(CornerFwdArgs a) {
 		for (int k = 0; k < 4; k++)
 #pragma unroll
 			for (int m = 1; m < 16; m <<= 1) acc[k] += __shfl_xor(acc[k], m);
-		const float* ysrc = a.mode == 2 && col.w > 0 ? a.zx : a.yb;
 		if (cg == 0) {
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
 				const int r = 16 * wave + 4 * rq + k;
-				const float z = ysrc[static_cast<int64_t>(J) * TILE + r] - acc[k];
+				const float b = a.mode == 2 && col.w > 0 ? a.zx[static_cast<int64_t>(J) * TILE + r] : yv_.ld(static_cast<int64_t>(J) * TILE + r);
+				const float z = b - acc[k];
 				if (a.mode == 1) a.zx[static_cast<int64_t>(J) * TILE + r] = z;
 				else s_z[r] = z;
 			}
@@ -1139,10 +1202,138 @@ __global__ __launch_bounds__(CT) void k_corner_fwd(CornerFwdArgs a) {
 			}
 			if (cg == 0)
 #pragma unroll
-				for (int k = 0; k < 4; k++) a.yb[static_cast<int64_t>(J) * TILE + 16 * wave + 4 * rq + k] = yk[k];
+				for (int k = 0; k < 4; k++) yv_.st(static_cast<int64_t>(J) * TILE + 16 * wave + 4 * rq + k, yk[k]);
 		}
 		__syncthreads();   // y_J visible to the chain's next column; s_z, s_m free
 	}
+}
+
+__global__ __launch_bounds__(CT) void k_corner_fwd(CornerFwdArgs a, int ld) {
+	if (a.gate && !refine_gate_on(a.gate, a.ratio)) return;
+	corner_fwd_chain<false>(a, a.chains[blockIdx.x], ld);
+}
+
+// ===================================================================================================================
+// Dataflow substitution launches (k_corner_flow): the corner's back substitution chains and the stem pass that follows
+// them (phase 0), or the whole gated refinement step -- the correction's corner right-hand side, the forward chains, the
+// back chains and the stem pass (phase 1) -- each as ONE launch instead of one launch per chain depth plus the stem's.
+//
+// Workgroups take tickets (one relaxed agent-scope atomic add each) and a ticket fixes the role; roles are numbered so
+// that every wait is on work of a LOWER ticket: phase 1 runs [T rhs workers (one per tile column)] [forward chains,
+// deepest first] [back chains, root first] [stem workers], phase 0 [back chains] [stem workers]. A forward chain waits
+// for its columns' right-hand sides and its child chains, a back chain for its parent chain (a root: for its own forward
+// chain in phase 1), a stem worker for every back chain. A workgroup that holds a ticket is resident and waits only on
+// lower tickets, so by induction every wait ends: no assumption on dispatch order, co-residency or timing (the plan
+// emulator checks the ticket order: tests/test_corner_plan.py). Every spin is bounded (error flag bit 8 on a timeout).
+//
+// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1): the handed-off vectors (x, y, the refinement
+// rhs, the corner rows of the stem's x) are stored write-through (sc1) and read with sc1 loads only, every storing wave
+// drains its stores (s_waitcnt vmcnt(0)) before the workgroup barrier behind which one lane signals (an agent-scope
+// atomic); the waiting workgroup's lane 0 polls relaxed and the other waves load after the barrier it then joins.
+// Tiles and inverses come from earlier launches (plain loads). The control words are zeroed by k_corner_invert.
+// ===================================================================================================================
+struct FlowArgs {
+	int phase;               // 0: back chains + stem pass; 1: the refinement step (rhs + forward + back chains + stem pass)
+	int nB, T, ld;           // chains, tile columns, permuted length
+	int64_t nxout;           // 6 nc
+	unsigned* ctl;           // 2 x flow_ctl_words(nB) control words (zeroed by k_corner_invert)
+	const int4* chains;      // [nB] (back column first, column count, forward column first, parent chain or -1), root first
+	const int* fwd_need;     // [nB] columns + child chains of chain c
+	const int* col_chain;    // [T] chain of tile column J
+	const int* node_row;     // [nc] first permuted row of each corner node
+	CornerBackArgs back;     // chains unused; cb = y (phase 0: the factorization's; phase 1: fwd.yb), xout = the stem pass's corner rows
+	CornerFwdArgs fwd;       // chains unused; yb = the refinement's corner rhs -> y
+	FlowStem st;
+};
+constexpr unsigned FLOW_MAX_SPINS = 1u << 20;   // per wait: ~1 s of polling before the launch gives up (error bit 8)
+
+// lane 0 polls *w until it reaches target (relaxed agent loads, s_sleep between polls); every thread returns whether it
+// did (workgroup-uniform)
+__device__ __forceinline__ bool flow_wait(const unsigned* w, unsigned target, int* error_flag) {
+	__shared__ int s_ok;
+	if (threadIdx.x == 0) {
+		unsigned spins = 0;
+		int ok = 1;
+		while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+			if (++spins > FLOW_MAX_SPINS) {
+				ok = 0;
+				atomicOr(error_flag, 8);
+				break;
+			}
+			__builtin_amdgcn_s_sleep(2);
+		}
+		s_ok = ok;
+	}
+	__syncthreads();
+	return s_ok != 0;
+}
+// every wave drains its (sc1) stores, then one lane adds 1 to each of the (up to two) counters
+__device__ __forceinline__ void flow_signal(unsigned* w0, unsigned* w1 = nullptr) {
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		__hip_atomic_fetch_add(w0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		if (w1) __hip_atomic_fetch_add(w1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	}
+}
+
+__global__ __launch_bounds__(CT) void k_corner_flow(FlowArgs a) {
+	__shared__ int s_ticket;
+	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+	const bool refining = a.st.gate && refine_gate_on(a.st.gate, a.st.ratio);
+	if (a.phase == 1 && !refining) return;   // gate shut: the refinement launch is empty (no ticket taken)
+	const int nB = a.nB;
+	unsigned* ctl = a.ctl + a.phase * flow_ctl_words(nB);
+	unsigned* back_done = ctl + 4;   // [nB] back chain c finished
+	unsigned* fwd_cnt = back_done + nB;   // [nB] forward chain c's columns' rhs + finished child chains
+	unsigned* fwd_done = fwd_cnt + nB;    // [nB] forward chain c (a root) finished
+	if (t == 0) s_ticket = static_cast<int>(__hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+	__syncthreads();
+	int k = s_ticket;
+	if (a.phase == 1) {
+		if (k < a.T) {   // the refinement's corner right-hand side of tile column J (every node with rows in it)
+			const int J = k;
+			int seen = 0;
+			for (int r = 0; r < TILE; r++) {
+				const int rn = a.back.row_node[static_cast<int64_t>(J) * TILE + r];
+				if (rn < 0 || ((rn & 7) != 0 && r != 0)) continue;   // a node's first row, or a node entering from column J - 1
+				if ((seen++ & 3) != wave) continue;
+				const int node = rn >> 3;
+				const float v = refine_rhs_node(node, lane, a.st.n0, a.st.dinv_b, a.st.diag, a.st.inc_off, a.st.inc_list, a.st.edges, a.st.wing, a.st.rhs_b, a.st.x_base, a.st.res);
+				const int row = a.node_row[node] + lane;
+				if (lane < 6 && row >= J * TILE && row < (J + 1) * TILE) st_sc1(a.fwd.yb + row, v);
+			}
+			flow_signal(fwd_cnt + a.col_chain[J]);
+			return;
+		}
+		k -= a.T;
+		if (k < nB) {   // forward chain c, deepest first
+			const int c = nB - 1 - k;
+			const int4 ch = a.chains[c];
+			if (!flow_wait(fwd_cnt + c, static_cast<unsigned>(a.fwd_need[c]), a.st.error_flag)) return;
+			corner_fwd_chain<true>(a.fwd, make_int2(ch.z, ch.y), a.ld);
+			flow_signal(ch.w >= 0 ? fwd_cnt + ch.w : fwd_done + c);
+			return;
+		}
+		k -= nB;
+	}
+	if (k < nB) {   // back chain c, root first
+		const int4 ch = a.chains[k];
+		const unsigned* dep = ch.w >= 0 ? back_done + ch.w : a.phase == 1 ? fwd_done + k : nullptr;
+		if (dep && !flow_wait(dep, 1u, a.st.error_flag)) return;
+		if (a.phase == 1) corner_back_chain<true, true>(a.back, make_int2(ch.x, ch.y), a.ld, a.nxout);
+		else corner_back_chain<true, false>(a.back, make_int2(ch.x, ch.y), a.ld, a.nxout);
+		flow_signal(back_done + k, ctl + 1);
+		return;
+	}
+	k -= nB;
+	// stem worker: the stem back substitution and every node's update, once the corner's x is complete
+	if (!flow_wait(ctl + 1, static_cast<unsigned>(nB), a.st.error_flag)) return;
+	const int i = k * CT + t;
+	if (i >= a.st.n_update && i >= a.st.n0) return;
+	const XSc1 xc{flow_rsrc(a.st.x, 24 * static_cast<int64_t>(a.st.N))};
+	arrow_back_node(i, a.st.n0, a.st.n_update, a.st.dinv, a.st.edge_offsets, a.st.edge_list, a.st.edges, a.st.wing, a.st.rhs, a.st.x, xc, a.st.state_in, a.st.node_state,
+	                a.st.updates_out, a.phase == 1 ? a.st.x_base : nullptr, a.st.mode, refining, a.st.diag, a.st.res);
 }
 
 // ===================================================================================================================
@@ -1156,6 +1347,7 @@ __global__ __launch_bounds__(CT) void k_corner_fwd(CornerFwdArgs a) {
 constexpr int WT = 512;        // threads of the walk workgroup (8 waves)
 constexpr int WALK_MAX_LD = 8192;
 constexpr int WALK_MAX_ELEMS = 1024;
+constexpr int WALK_LDS_BUDGET = 160 * 1024;   // the CU's LDS: the walk's dynamic-LDS cap on every device
 // one workgroup streams every tile through one CU's load path (≈ 30-60 GB/s): the walk wins only on small corners; above
 // this many stream tiles per direction the chain launches (many CUs) take over. Measured at C5 (254 tiles per direction):
 // the walk 4 MB / ≈ 140 µs against ≈ 65 µs for the back chains (round 4)
@@ -1394,6 +1586,29 @@ static void dev_free(void*& p) {
 	p = nullptr;
 }
 
+// development switches (A/B builds without rebuilding): NNRT_CORNER_WALK=0 disables the single-workgroup walk for small
+// corners, NNRT_CORNER_FLOW=0 the dataflow substitution launches
+static bool env_flag(const char* name, bool dflt) {
+	const char* v = std::getenv(name);
+	return v ? std::strcmp(v, "0") != 0 : dflt;
+}
+
+// The dynamic-LDS cap of k_corner_walk is a property of the kernel on each device, not of a plan: several plans with
+// different walk_lds are live at once (every fitter, the arrowhead pool), so the cap is raised once per device to the
+// whole LDS budget, which bounds every plan's walk_lds, under a mutex.
+static bool walk_lds_cap_set() {
+	static std::mutex mu;
+	static std::set<int> done;
+	int dev = 0;
+	if (hipGetDevice(&dev) != hipSuccess) return false;
+	std::lock_guard<std::mutex> lk(mu);
+	if (done.count(dev)) return true;
+	if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_corner_walk), hipFuncAttributeMaxDynamicSharedMemorySize, WALK_LDS_BUDGET) != hipSuccess)
+		return false;
+	done.insert(dev);
+	return true;
+}
+
 CornerSolver::~CornerSolver() { release(); }
 
 void CornerSolver::release() {
@@ -1406,8 +1621,11 @@ void CornerSolver::release() {
 	                 reinterpret_cast<void**>(&d_row_node), reinterpret_cast<void**>(&d_node_row), reinterpret_cast<void**>(&d_tasks),
 	                 reinterpret_cast<void**>(&d_srcs), reinterpret_cast<void**>(&d_back_cols), reinterpret_cast<void**>(&d_back_ent), reinterpret_cast<void**>(&d_back_chains),
 	                 reinterpret_cast<void**>(&d_corner_edges), reinterpret_cast<void**>(&zx), reinterpret_cast<void**>(&d_back_pre),
-	                 reinterpret_cast<void**>(&d_fwd_pre)})
+	                 reinterpret_cast<void**>(&d_fwd_pre), reinterpret_cast<void**>(&d_flow_chains), reinterpret_cast<void**>(&d_flow_need),
+	                 reinterpret_cast<void**>(&d_col_chain), reinterpret_cast<void**>(&flow_ctl)})
 		dev_free(*p);
+	use_flow = false;
+	n_chains = n_flow_ctl = 0;
 	back_pre_off.clear();
 	fwd_pre_off.clear();
 	nc = ld = T = H = slots = n_corner_edges = 0;
@@ -1462,7 +1680,7 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		}
 	}
 	walk_ok = false;
-	if (p.nc > 0 && p.ld <= WALK_MAX_LD && static_cast<int>(std::max(p.walk_back.size(), p.walk_fwd.size())) <= std::min(WALK_MAX_ELEMS, NNRT_WALK_MAX_TILES)) {
+	if (p.nc > 0 && env_flag("NNRT_CORNER_WALK", true) && p.ld <= WALK_MAX_LD && static_cast<int>(std::max(p.walk_back.size(), p.walk_fwd.size())) <= std::min(WALK_MAX_ELEMS, NNRT_WALK_MAX_TILES)) {
 		// LDS: descriptors, the solution vector, the reduction rows, then a ring of as many tiles as fit (at least the
 		// largest column's elements need not fit: a column streams through the ring in parts)
 		const size_t nd = std::max(p.walk_back.size(), p.walk_fwd.size());
@@ -1483,12 +1701,21 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 			walk_lds = static_cast<int>(fixed + static_cast<size_t>(ring_tiles) * 4 * TILE_ELEMS);
 			n_walk_back = static_cast<int>(wb.size());
 			n_walk_fwd = static_cast<int>(wf.size());
-			if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_corner_walk), hipFuncAttributeMaxDynamicSharedMemorySize, walk_lds) != hipSuccess) {
+			if (!walk_lds_cap_set()) {
 				set_error("hipFuncSetAttribute (corner walk LDS) failed");
 				return fail(NNRT_ERROR_HIP);
 			}
 			walk_ok = true;
 		}
+	}
+	if (p.nc > 0 && !walk_ok && env_flag("NNRT_CORNER_FLOW", true)) {   // dataflow substitution launches (k_corner_flow)
+		nnrt_status st;
+		if ((st = dev_upload(d_flow_chains, p.flow_chains)) || (st = dev_upload(d_flow_need, p.flow_need)) || (st = dev_upload(d_col_chain, p.col_chain)))
+			return fail(st);
+		n_chains = static_cast<int>(p.flow_chains.size());
+		n_flow_ctl = 2 * flow_ctl_words(n_chains);
+		if ((st = alloc(reinterpret_cast<float*&>(flow_ctl), static_cast<size_t>(n_flow_ctl)))) return fail(st);
+		use_flow = true;
 	}
 	nc = p.nc;
 	if (nc > 0) {
@@ -1531,6 +1758,19 @@ nnrt_status CornerSolver::launch_offdiag(int n0, const int32_t* edges, const flo
 
 nnrt_status CornerSolver::launch_solve(float* xout, int* error_flag, hipStream_t s) const {
 	if (nc == 0) return NNRT_OK;
+	nnrt_status st = launch_factor(error_flag, s);
+	if (st) return st;
+	if (walk_ok) {   // the back substitution as one single-workgroup walk
+		const CornerWalkArgs wa{nullptr, 0.f, nullptr, d_walk_back, 0, n_walk_back, cb, d_row_node, xout, ld, walk_ring};
+		k_corner_walk<<<1, WT, walk_lds, s>>>(wa);
+		NNRT_LAUNCH_CHECK();
+		return NNRT_OK;
+	}
+	return launch_back(cb, xout, s, nullptr, 0.f);
+}
+
+nnrt_status CornerSolver::launch_factor(int* error_flag, hipStream_t s) const {
+	if (nc == 0) return NNRT_OK;
 	CornerFactorArgs fa{tiles, ldiag, cb, nullptr, d_srcs, 0, error_flag, 0, sdiag, pivot_word};
 	for (int l = 0; l < H; l++) {
 		fa.level = l;
@@ -1541,15 +1781,37 @@ nnrt_status CornerSolver::launch_solve(float* xout, int* error_flag, hipStream_t
 		NNRT_LAUNCH_CHECK();
 	}
 	// every diagonal factor's inverse, one workgroup per tile column (the substitutions multiply by them)
-	k_corner_invert<<<T, CT, 0, s>>>(ldiag, minv);
+	k_corner_invert<<<T, CT, 0, s>>>(ldiag, minv, flow_ctl, n_flow_ctl);
 	NNRT_LAUNCH_CHECK();
-	if (walk_ok) {   // the back substitution as one single-workgroup walk
-		const CornerWalkArgs wa{nullptr, 0.f, nullptr, d_walk_back, 0, n_walk_back, cb, d_row_node, xout, ld, walk_ring};
-		k_corner_walk<<<1, WT, walk_lds, s>>>(wa);
-		NNRT_LAUNCH_CHECK();
-		return NNRT_OK;
+	return NNRT_OK;
+}
+
+nnrt_status CornerSolver::launch_flow(int phase, const FlowStem& st, hipStream_t s) const {
+	if (nc == 0 || !use_flow) {
+		set_error("launch_flow without a dataflow plan");
+		return NNRT_ERROR_ARGUMENT;
 	}
-	return launch_back(cb, xout, s, nullptr, 0.f);
+	FlowArgs a{};
+	a.phase = phase;
+	a.nB = n_chains;
+	a.T = T;
+	a.ld = ld;
+	a.nxout = 6 * static_cast<int64_t>(nc);
+	a.ctl = flow_ctl;
+	a.chains = d_flow_chains;
+	a.fwd_need = d_flow_need;
+	a.col_chain = d_col_chain;
+	a.node_row = d_node_row;
+	float* xout = st.x + 6 * static_cast<int64_t>(st.n0);
+	a.back = CornerBackArgs{nullptr, 0.f, tiles, ldiag, minv, phase == 1 ? cb2 : cb, xp, d_row_node, xout, nullptr, d_back_cols, d_back_ent, zx, 0};
+	a.fwd = CornerFwdArgs{nullptr, 0.f, tiles, ldiag, minv, cb2, nullptr, d_fwd_cols, d_fwd_ent, zx, 0};
+	a.st = st;
+	const int stem_threads = std::max(st.n_update, st.n0);
+	const int stem_wg = static_cast<int>(ceil_div(stem_threads, CT));
+	const int grid = (phase == 1 ? T + 2 * n_chains : n_chains) + stem_wg;
+	k_corner_flow<<<grid, CT, 0, s>>>(a);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
 }
 
 // back substitution chains over y (with NNRT_SUBST_PRESUM, each launch preceded by its columns' pre-sums)
@@ -1561,12 +1823,12 @@ nnrt_status CornerSolver::launch_back(const float* y, float* xout, hipStream_t s
 		if (npre > 0) {
 			ba.chains = d_back_pre + back_pre_off[l];
 			ba.mode = 1;
-			k_corner_back<<<npre, CT, 0, s>>>(ba);
+			k_corner_back<<<npre, CT, 0, s>>>(ba, ld, 6 * static_cast<int64_t>(nc));
 			NNRT_LAUNCH_CHECK();
 		}
 		ba.chains = d_back_chains + back_off[l];
 		ba.mode = NNRT_SUBST_PRESUM ? 2 : 0;
-		k_corner_back<<<n, CT, 0, s>>>(ba);
+		k_corner_back<<<n, CT, 0, s>>>(ba, ld, 6 * static_cast<int64_t>(nc));
 		NNRT_LAUNCH_CHECK();
 	}
 	return NNRT_OK;
@@ -1587,12 +1849,12 @@ nnrt_status CornerSolver::launch_resolve(float* xout, hipStream_t s, const unsig
 		if (npre > 0) {
 			fa.chains = d_fwd_pre + fwd_pre_off[l];
 			fa.mode = 1;
-			k_corner_fwd<<<npre, CT, 0, s>>>(fa);
+			k_corner_fwd<<<npre, CT, 0, s>>>(fa, ld);
 			NNRT_LAUNCH_CHECK();
 		}
 		fa.chains = d_fwd_chains + fwd_off[l];
 		fa.mode = NNRT_SUBST_PRESUM ? 2 : 0;
-		k_corner_fwd<<<n, CT, 0, s>>>(fa);
+		k_corner_fwd<<<n, CT, 0, s>>>(fa, ld);
 		NNRT_LAUNCH_CHECK();
 	}
 	return launch_back(cb2, xout, s, gate, refine_ratio);

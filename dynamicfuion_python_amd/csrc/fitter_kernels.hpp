@@ -259,6 +259,26 @@ __device__ inline void corner_init_thread(int64_t idx, const CornerInitArgs& a, 
 
 struct WalkElem;   // corner.hip: one tile of a single-workgroup substitution walk
 
+// the stem side of a dataflow substitution launch (CornerSolver::launch_flow; arap.hip fills it)
+struct FlowStem {
+	int n0 = 0, N = 0, n_update = 0, mode = 0;   // mode: 0 plain, 1 first pass of a gated refinement, 2 the refinement's pass
+	const float *dinv = nullptr, *wing = nullptr, *diag = nullptr, *dinv_b = nullptr;
+	const int *edge_offsets = nullptr, *edge_list = nullptr, *inc_off = nullptr, *inc_list = nullptr;
+	const int32_t* edges = nullptr;
+	const float* rhs = nullptr;   // the stem pass's right-hand side (phase 0: b; phase 1: the residual)
+	float* x = nullptr;           // [6N] the pass's solution (phase 1: the correction d); its corner rows are the corner's output
+	const float* state_in = nullptr;
+	float* node_state = nullptr;
+	float* updates_out = nullptr;
+	float* x_base = nullptr;      // phase 1: the first pass's x (x += d; also the rhs workers' x)
+	float* res = nullptr;         // phase 0, mode 1: the stem residual (out); phase 1: the rhs workers' stem residual
+	const float* rhs_b = nullptr; // phase 1 rhs workers: b
+	const unsigned* gate = nullptr;
+	float ratio = 0.f;
+	int* error_flag = nullptr;
+};
+__host__ __device__ inline int flow_ctl_words(int nB) { return 4 + 3 * nB; }
+
 class CornerSolver {
 public:
 	~CornerSolver();
@@ -278,6 +298,12 @@ public:
 	// gate (nullable, device): skip unless the factorization's minimum pivot / diag(S) ratio is below refine_ratio
 	nnrt_status launch_resolve(float* xout, hipStream_t s, const unsigned* gate = nullptr, float refine_ratio = 0.f) const;
 	nnrt_status launch_back(const float* y, float* xout, hipStream_t s, const unsigned* gate, float refine_ratio) const;
+	// dataflow substitution (k_corner_flow): phase 0 = the back substitution of the last launch_factor + the stem pass,
+	// phase 1 = the gated refinement step; st.x + 6 n0 receives the corner's solution
+	nnrt_status launch_flow(int phase, const FlowStem& st, hipStream_t s) const;
+	// factor S and form the diagonal inverses (the first half of launch_solve; the flow launches do the rest)
+	nnrt_status launch_factor(int* error_flag, hipStream_t s) const;
+	bool flow_ok() const { return use_flow; }
 	float* refine_rhs() const { return cb2; }
 	// the factorization's minimum pivot / diag(S) ratio of the last solve (device word, float bits)
 	const unsigned* pivot_ratio() const { return pivot_word; }
@@ -304,6 +330,12 @@ private:
 	int4* d_fwd_cols = nullptr;
 	// single-workgroup substitution walks (corner.hip k_corner_walk), when the permuted vector and the descriptors fit in LDS
 	bool walk_ok = false;
+	// dataflow substitution plan (k_corner_flow): per chain (back column first, count, forward column first, parent)
+	bool use_flow = false;
+	int n_chains = 0, n_flow_ctl = 0;
+	int4* d_flow_chains = nullptr;
+	int *d_flow_need = nullptr, *d_col_chain = nullptr;
+	unsigned* flow_ctl = nullptr;
 	int walk_ring = 0, walk_lds = 0, n_walk_back = 0, n_walk_fwd = 0;
 	WalkElem* d_walk_back = nullptr;
 	WalkElem* d_walk_fwd = nullptr;

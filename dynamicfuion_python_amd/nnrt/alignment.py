@@ -152,7 +152,10 @@ class DeformableMeshToImageFitter:
         return dict(pivot_ratio=float(out[0]), threshold=float(out[1]), refined=bool(out[2]))
 
     def set_refine_ratio(self, ratio: float):
-        """Threshold of the arrowhead solve's refinement gate (default 1e-3; 0: never refine, inf: always)."""
+        """Upper end of the arrowhead solve's refinement window: one refinement step runs when the corner
+        factorization's min pivot / diag(S) lies in [1e-4, ratio) (default ratio 1e-3; 0: never refine; inf: refine
+        whenever the ratio is at least the 1e-4 floor, below which one step does not converge). refine_info() reports
+        the threshold the last launched iterations ran with."""
         N.check(N.lib().nnrt_fitter_set_refine_ratio(self._h, float(ratio)))
 
     def time_kernels(self, warp_field: HierarchicalGraphWarpField, reps: int = 20, trials: int = 5, stream=None) -> dict:

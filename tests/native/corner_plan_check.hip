@@ -188,6 +188,74 @@ int main(int argc, char** argv) {
 	for (int i=0;i<m;i++){ double s2 = -b2[i]; for (int j=0;j<m;j++) s2 += M[(size_t)i*m+j]*x2[j]; res2 = std::max(res2, fabs(s2)); b2max = std::max(b2max, fabs(b2[i])); }
 	printf("refinement-solve residual %.3g (|b| %.3g)\n", res2, b2max);
 	if (!(res2 < 1e-9 * b2max)) return 1;
+	// dataflow launches (k_corner_flow): tickets run [rhs of every column] [forward chains c = nB-1 .. 0] [back chains
+	// c = 0 .. nB-1]; every wait must be on a lower ticket (deadlock freedom), the counters a chain waits for must be
+	// complete exactly when everything it reads is, and executing the roles in ticket order must solve the system
+	{
+		const int nB = (int)p.flow_chains.size();
+		if (nB != (int)p.back_chains.size() || (int)p.flow_need.size() != nB || (int)p.col_chain.size() != T) { printf("FLOW plan size mismatch\n"); return 1; }
+		std::vector<int> kids(nB, 0), ncols_of(nB, 0);
+		for (int c = 0; c < nB; c++) {
+			const int4 f = p.flow_chains[c];
+			if (f.x != p.back_chains[c].x || f.y != p.back_chains[c].y) { printf("FLOW chain %d back columns mismatch\n", c); return 1; }
+			if (f.w >= c) { printf("FLOW chain %d waits on chain %d (not a lower back ticket)\n", c, f.w); return 1; }
+			if (f.w >= 0) kids[f.w]++;
+			for (int k = 0; k < f.y; k++) {
+				if (p.back_cols[f.x + k].x != p.fwd_cols[f.z + f.y - 1 - k].x) { printf("FLOW chain %d forward columns mismatch\n", c); return 1; }
+				if (p.col_chain[p.back_cols[f.x + k].x] != c) { printf("FLOW column chain map wrong\n"); return 1; }
+			}
+		}
+		for (int J = 0; J < T; J++) ncols_of[p.col_chain[J]]++;
+		for (int c = 0; c < nB; c++)
+			if (p.flow_need[c] != ncols_of[c] + kids[c]) { printf("FLOW chain %d need %d != columns %d + children %d\n", c, p.flow_need[c], ncols_of[c], kids[c]); return 1; }
+		std::vector<double> yf(p.ld, 0.0), xf(p.ld, 0.0), xnat(m, 0.0);
+		std::vector<int> cnt(nB, 0), fdone_c(nB, 0), bdone_c(nB, 0);
+		std::vector<char> ycol(T, 0), xcol(T, 0), rhs_col(T, 0);
+		for (int J = 0; J < T; J++) {   // rhs workers
+			for (int i = 0; i < TILE; i++) { int rn = p.row_node[J*TILE+i]; yf[J*TILE+i] = rn >= 0 ? b2[6*(rn>>3)+(rn&7)] : 0.0; }
+			rhs_col[J] = 1;
+			cnt[p.col_chain[J]]++;
+		}
+		for (int c = nB - 1; c >= 0; c--) {   // forward chains, deepest first
+			const int4 f = p.flow_chains[c];
+			if (cnt[c] != p.flow_need[c]) { printf("FLOW forward chain %d would wait forever (%d of %d)\n", c, cnt[c], p.flow_need[c]); return 1; }
+			for (int k = 0; k < f.y; k++) {
+				int4 col = p.fwd_cols[f.z + k]; int J = col.x;
+				if (!rhs_col[J]) { printf("FLOW forward reads an unwritten rhs\n"); return 1; }
+				std::vector<double> z(TILE); for (int i=0;i<TILE;i++) z[i] = yf[J*TILE+i];
+				for (int e = 0; e < col.z; e++) { int2 en = p.fwd_ent[col.y+e];
+					if (!ycol[en.y]) { printf("FLOW forward column %d reads y_%d before it is final\n", J, en.y); return 1; }
+					const double* L = tile(en.x); for (int r=0;r<TILE;r++) for (int cc=0;cc<TILE;cc++) z[r] -= L[r*TILE+cc]*yf[en.y*TILE+cc]; }
+				const double* Mi = &minv[(size_t)J*TE]; for (int r=0;r<TILE;r++){ double v=0; for(int cc=0;cc<TILE;cc++) v += Mi[r*TILE+cc]*z[cc]; yf[J*TILE+r]=v; }
+				ycol[J] = 1;
+			}
+			if (f.w >= 0) cnt[f.w]++; else fdone_c[c] = 1;
+		}
+		int btotal = 0;
+		for (int c = 0; c < nB; c++) {   // back chains, root first
+			const int4 f = p.flow_chains[c];
+			if (f.w >= 0 ? !bdone_c[f.w] : !fdone_c[c]) { printf("FLOW back chain %d would wait forever\n", c); return 1; }
+			for (int k = 0; k < f.y; k++) {
+				int4 col = p.back_cols[f.x + k]; int J = col.x;
+				if (!ycol[J]) { printf("FLOW back column %d before its y\n", J); return 1; }
+				std::vector<double> z(TILE); for (int i=0;i<TILE;i++) z[i] = yf[J*TILE+i];
+				for (int e=0;e<col.z;e++){ int2 en = p.back_ent[col.y+e];
+					if (!xcol[en.y]) { printf("FLOW back column %d reads x_%d before it is final\n", J, en.y); return 1; }
+					const double* L = tile(en.x); for (int r=0;r<TILE;r++) for (int cc=0;cc<TILE;cc++) z[cc] -= L[r*TILE+cc]*xf[en.y*TILE+r]; }
+				const double* Mi = &minv[(size_t)J*TE];
+				for (int i=0;i<TILE;i++){ double v = 0; for (int r2=0;r2<TILE;r2++) v += Mi[r2*TILE+i]*z[r2]; xf[J*TILE+i] = v; }
+				for (int i=0;i<TILE;i++){ int rn = p.row_node[J*TILE+i]; if (rn>=0) xnat[6*(rn>>3)+(rn&7)] = xf[J*TILE+i]; }
+				xcol[J] = 1;
+			}
+			bdone_c[c] = 1;
+			btotal++;
+		}
+		if (btotal != nB) { printf("FLOW stem workers would wait forever\n"); return 1; }
+		double res4 = 0;
+		for (int i=0;i<m;i++){ double s4 = -b2[i]; for (int j=0;j<m;j++) s4 += M[(size_t)i*m+j]*xnat[j]; res4 = std::max(res4, fabs(s4)); }
+		printf("flow-solve residual %.3g\n", res4);
+		if (!(res4 < 1e-9 * b2max)) return 1;
+	}
 	// single-workgroup walk streams (k_corner_walk): forward then back over b2 in stream order; every entry's vector
 	// segment must be final when read (forward: column k < J solved; back: column I > J solved), every head's tile formed
 	{

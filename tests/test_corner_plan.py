@@ -26,7 +26,7 @@ def checker():
         pytest.skip("hipcc not available")
     os.makedirs(BUILD, exist_ok=True)
     exe = os.path.join(BUILD, "corner_plan_check")
-    deps = [SRC] + [os.path.join(CSRC, f) for f in ("corner.hip", "fitter_kernels.hpp", "kernels.hpp", "common.hpp")]
+    deps = [SRC] + [os.path.join(CSRC, f) for f in ("corner.hip", "fitter_kernels.hpp", "arrow_device.hpp", "kernels.hpp", "common.hpp")]
     if not os.path.exists(exe) or os.path.getmtime(exe) < max(os.path.getmtime(d) for d in deps):
         tmp = f"{exe}.{os.getpid()}.tmp"   # concurrent workers (pytest -n) each build their own copy, then swap it in
         subprocess.check_call([HIPCC, "-O2", "-std=c++17", "--offload-arch=gfx950", "-I", os.path.join(ROOT, "include"), "-I", CSRC,

@@ -184,3 +184,69 @@ def test_plan_reuse_and_release(la):
     assert np.array_equal(x_new, x_fresh)
     x64, _ = fp64_solution(diag, wing2, edges, b2)
     assert rel_err(x_new, x64) < 1e-5
+
+
+def test_walk_plans_of_different_lds_alternate(la):
+    """Two live corner plans whose single-workgroup walks need different dynamic LDS: the larger plan is
+    prepared first, the smaller one after it, then the larger one is solved again from its cached plan. The walk's LDS
+    cap is a per-device kernel attribute raised once to the whole LDS budget, so the last plan prepared cannot lower it
+    below what an earlier plan launches with."""
+    from dynamicfuion_python_amd.nnrt import core
+    big = grid_arrowhead(12, 8, 3, True, seed=21)
+    small = grid_arrowhead(2, 2, 2, False, seed=22)
+    core.release_arrowhead_plans()
+    ref_big = la.SolveBlockSparseArrowheadCholesky(*big).cpu().numpy()
+    ref_small = la.SolveBlockSparseArrowheadCholesky(*small).cpu().numpy()
+    for _ in range(2):
+        assert np.array_equal(la.SolveBlockSparseArrowheadCholesky(*big).cpu().numpy(), ref_big)
+        assert np.array_equal(la.SolveBlockSparseArrowheadCholesky(*small).cpu().numpy(), ref_small)
+    for sy, x in ((big, ref_big), (small, ref_small)):
+        x64, _ = fp64_solution(sy[0], sy[1], sy[2], sy[4])
+        assert rel_err(x, x64) < 1e-5
+
+
+@pytest.mark.parametrize("cx,cy,spc,corner_edges", [(26, 15, 12, False), (12, 8, 4, True), (80, 80, 2, True)])
+def test_flow_matches_chain_launches(la, cx, cy, spc, corner_edges):
+    """The dataflow substitution launch (k_corner_flow: every back-substitution chain and the stem pass in one launch,
+    dependencies through ticket-ordered counters) against the per-depth chain launches: bit-identical solutions (the same
+    float operations), for a C5-sized corner, a small one with corner-corner blocks and the 38,400-unknown corner; the
+    flow solve repeated three times under two concurrent streams gives the same bits every time."""
+    import os
+    from dynamicfuion_python_amd.nnrt import core
+    sy = grid_arrowhead(cx, cy, spc, corner_edges, seed=cx + cy)
+    old = {k: os.environ.get(k) for k in ("NNRT_CORNER_FLOW", "NNRT_CORNER_WALK")}
+    try:
+        os.environ["NNRT_CORNER_WALK"] = "0"
+        xs = {}
+        for flow in ("0", "1"):
+            os.environ["NNRT_CORNER_FLOW"] = flow
+            core.release_arrowhead_plans()
+            xs[flow] = la.SolveBlockSparseArrowheadCholesky(*sy).cpu().numpy()
+        assert np.array_equal(xs["0"], xs["1"])
+        other = grid_arrowhead(20, 10, 6, True, seed=99)
+        out, errors = [], []
+
+        def load():
+            try:
+                st = torch.cuda.Stream()
+                with torch.cuda.stream(st):
+                    for _ in range(3):
+                        la.SolveBlockSparseArrowheadCholesky(*other)
+            except Exception as e:   # pragma: no cover - reported below
+                errors.append(e)
+
+        th = threading.Thread(target=load)
+        th.start()
+        for _ in range(3):
+            out.append(la.SolveBlockSparseArrowheadCholesky(*sy).cpu().numpy())
+        th.join()
+        assert not errors, errors
+        for x in out:
+            assert np.array_equal(x, xs["1"])
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        core.release_arrowhead_plans()

@@ -7,6 +7,7 @@ wave/atomic order vs the oracle's serial order differ only in double rounding), 
 compared at <= 1e-6 relative and the solved updates / node motion at <= 1e-4 relative (north_star tolerance).
 """
 import os
+from types import SimpleNamespace
 
 import numpy as np
 import pytest
@@ -450,15 +451,16 @@ def _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k):
         assert 0.0 < ratio < 1e-6, f"{msg}; fp64 min / max Cholesky pivot {ratio:.3g}"
         if not gpu_failed:
             assert np.isfinite(dg_g["updates"][: 6 * N]).all(), msg
-        return f"potrf ({'oracle' if oracle_failed else 'GPU'} only: fp64 pivot ratio {ratio:.2g})", None
+        return f"potrf ({'oracle' if oracle_failed else 'GPU'} only: fp64 pivot ratio {ratio:.2g})", None, None
     if gpu_failed:
         if dg_o is not None:   # block-diagonal: the same blocks fail (NaN updates), every other node's update agrees
             u_g, u_o = dg_g["updates"][: 6 * N], dg_o["updates"]
             assert nan_rel_err(u_g, u_o) < 1e-4
             assert np.array_equal(dg_o["pixel_faces"].astype(np.int64), dg_g["pixel_faces"].astype(np.int64))
             assert nan_rel_err(dg_g["hessian"][: N * 36], dg_o["hessian_diag"]) < 1e-6
-        return "potrf", None
+        return "potrf", None, None
     solve_note = ""
+    e_own = None
     u_err = nan_rel_err(dg_g["updates"][: 6 * N], dg_o["updates"])
     if sc.layer_count > 1:
         # The GPU's arrowhead solve (f32 factor + one step of iterative refinement with an fp64 residual) against the fp64
@@ -474,6 +476,20 @@ def _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k):
                       f"{gate['pivot_ratio']:.2g}, refined {gate['refined']})")
         if ratio_own > REFINE_PIVOT_RATIO:
             assert e_own <= 1e-4, f"iteration {k + 1}: refined solve error {e_own:.3g} vs fp64 at pivot ratio {ratio_own:.3g}"
+        # ... and against the fp64 solution of the ORACLE's normal equations: the two float systems
+        # differ by assembly rounding (delta, measured on H and g; <= 1e-6 by _compare_iteration), which the system's
+        # conditioning amplifies by about 1 / (fp64 pivot ratio). Both the fp64 solutions' own distance and the GPU
+        # update's distance from the oracle system's solution must stay inside that predicted amplification.
+        A_o, b_o = arrowhead_fp64_system(oracle_mod, sc, R0, t0, dg_o)
+        x64_o = spl.spsolve(A_o.tocsc(), b_o)
+        delta = max(nan_rel_err(dg_g["hessian"][: N * 36], dg_o["hessian_diag"]), nan_rel_err(dg_g["gradient"][: 6 * N], dg_o["gradient"]))
+        predicted = 4.0 * delta / max(ratio_own, 1e-300)
+        d64 = nan_rel_err(spl.spsolve(A_own.tocsc(), b_own), x64_o)
+        e_oracle_sys = nan_rel_err(dg_g["updates"][: 6 * N], x64_o)
+        solve_note += f", vs the oracle system's fp64 solution {e_oracle_sys:.2g} (fp64 solutions {d64:.2g} apart, predicted <= {predicted:.2g})"
+        assert d64 <= max(1e-4, predicted), f"iteration {k + 1}: fp64 solutions {d64:.3g} apart, assembly {delta:.3g} predicts {predicted:.3g}"
+        assert e_oracle_sys <= max(1e-4, e_own + predicted), \
+            f"iteration {k + 1}: update {e_oracle_sys:.3g} from the oracle system's fp64 solution (own {e_own:.3g}, predicted {predicted:.3g})"
     if sc.layer_count > 1 and u_err >= 1e-4:
         # Ill-conditioned arrowhead system: two float32 solves with different blockings cannot agree to 1e-4 (the GPU
         # factors the dense Schur corner with MFMA tiles, the oracle serially). Both are held against the fp64 solution
@@ -508,7 +524,7 @@ def _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k):
     ok = np.isfinite(R_expect)
     assert np.abs(R_g[ok] - R_expect[ok]).max(initial=0.0) < 1e-5
     nan_nodes = int(np.isnan(R_g).reshape(N, -1).any(1).sum())
-    return ("ok" if nan_nodes == 0 else f"ok, {nan_nodes} NaN rotations (A7)") + solve_note, u_err
+    return ("ok" if nan_nodes == 0 else f"ok, {nan_nodes} NaN rotations (A7)") + solve_note, u_err, e_own
 
 
 def _new_fit(nn, sc, depth, iterations):
@@ -530,6 +546,11 @@ def _new_fit(nn, sc, depth, iterations):
 # iteration 4 (condition ~1e9, both float solves 0.14 from fp64, one A7 NaN rotation) the iteration-5 system is positive
 # definite in fp64 with a pivot ratio below 1e-6: the oracle's natural-order float Cholesky breaks down, the GPU's
 # nested-dissection order does not (round 2's order broke down too) -- accepted as a one-sided breakdown, trajectory ends.
+# The C5 trajectory's solve errors vs the fp64 solution of its own system at iterations 1-3, measured 1.7e-6 / 1.8e-5 /
+# 1.0e-4 (round 5; iteration 3 refined, at an fp64 pivot ratio below REFINE_PIVOT_RATIO, where no 1e-4 rule applies):
+# pinned at 1.5x as regression bounds. Iteration 4 is degenerate (35 A7 NaN rotations, corner pivot /
+# diag(S) 3.8e-7 below the refinement floor, fp64 pivot ratio 7e-12): 0.011, the oracle's float solve 0.016.
+PINNED_SOLVE_ERRORS = {("C5", 1): 3e-6, ("C5", 2): 3e-5, ("C5", 3): 1.5e-4}
 TRAJECTORIES = [("S1", 6, 6, None), ("C2", 2, 1, 2), ("C2_ARAP", 10, 4, None), ("C5", 6, 3, None)]
 
 
@@ -545,9 +566,12 @@ def test_fit_state_synchronised_trajectory(nn, S, oracle_mod, name, iterations, 
     report = []
     for k in range(iterations):
         nan_before = int(np.isnan(wf.get_node_rotations(True)).reshape(len(sc.nodes), -1).any(1).sum())
-        status, err = _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k)
+        status, err, e_own = _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k)
         print(f"{name} iteration {k + 1}: {status}, update rel err {err}, NaN rotations before {nan_before}", flush=True)
         report.append((k + 1, status, err))
+        pin = PINNED_SOLVE_ERRORS.get((name, k + 1))
+        if pin is not None:   # the refined solve's measured error vs fp64 as a regression bound
+            assert e_own is not None and e_own <= pin, f"{name} iteration {k + 1}: solve error vs fp64 {e_own} above its pinned {pin:.3g}"
         if status.startswith("potrf"):
             break
     print(f"{name}: {report}")
@@ -619,6 +643,45 @@ def test_refinement_gate(nn, S, oracle_mod, name, iterations):
     assert len(rows) >= 2
 
 
+@pytest.mark.parametrize("name,walk", [("C5", "1"), ("C2_ARAP", "0"), ("C1_ARAP", "0")])
+def test_flow_substitution_matches_chain_launches(nn, S, oracle_mod, name, walk):
+    """The dataflow substitution launches (k_corner_flow: the back chains and the stem pass in one launch, the whole
+    gated refinement step in a second) perform the same float operations as the per-depth chain launches they replace:
+    along three GN iterations with the refinement forced open wherever the gate's floor allows (and once shut), updates,
+    node motion and gate words are bit-identical between fitters planned with NNRT_CORNER_FLOW=1 and =0
+    (NNRT_CORNER_WALK=0 makes the small C1 / C2 corners use chains instead of the single-workgroup walk)."""
+    import os
+    sc = _scene(S, oracle_mod, name)
+    depth = scene_target(oracle_mod, sc)
+    N = len(sc.nodes)
+    runs = {}
+    old = {k: os.environ.get(k) for k in ("NNRT_CORNER_FLOW", "NNRT_CORNER_WALK")}
+    try:
+        os.environ["NNRT_CORNER_WALK"] = walk
+        for flow in ("1", "0"):
+            os.environ["NNRT_CORNER_FLOW"] = flow
+            wf, ft = _new_fit(nn, sc, depth, 3)
+            rows = []
+            for k, ratio in enumerate((np.inf, 0.0, np.inf)):
+                ft.set_refine_ratio(ratio)
+                ft.iterate(wf, k, 1)
+                ft.check()
+                dg = ft.diagnostics()
+                rows.append((dg["updates"][: 6 * N].copy(), wf.get_node_rotations(True), wf.get_node_translations(True), ft.refine_info()))
+            runs[flow] = rows
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    for k, (a, b) in enumerate(zip(runs["1"], runs["0"])):
+        assert np.array_equal(a[0], b[0], equal_nan=True), f"iteration {k + 1}: updates differ"
+        assert np.array_equal(a[1], b[1], equal_nan=True) and np.array_equal(a[2], b[2], equal_nan=True), f"iteration {k + 1}: motion differs"
+        assert a[3] == b[3]
+        print(f"{name} iteration {k + 1}: gate {a[3]}", flush=True)
+
+
 def test_fit_c2_from_stored_states(nn, S, oracle_mod):
     """C2 GN iterations from ten non-identity node states (fractions of the ground-truth motion plus noise: the
     states a frame passes through between the identity and the solution) -- the general warp / update kernels on a
@@ -632,7 +695,7 @@ def test_fit_c2_from_stored_states(nn, S, oracle_mod):
         R, t = sc.partial_motion(fraction, seed=j, noise=noise)
         wf.set_node_rotations(R[vidx])
         wf.set_node_translations(t[vidx])
-        status, err = _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, j + 1)
+        status, err, _ = _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, j + 1)
         assert status.startswith("ok"), f"state {j}: {status}"
 
 
@@ -678,7 +741,7 @@ def test_fit_multilayer_arap_parity(nn, S, oracle_mod, name):
     assert e_g <= max(2.0 * e_o, 1e-4)
     wf, ft = _new_fit(nn, sc, depth, 2)
     for k in range(2):
-        status, err = _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k)
+        status, err, _ = _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k)
         print(f"{name} iteration {k + 1}: {status}, update rel err {err}")
         assert status.startswith("ok"), status
 
@@ -979,8 +1042,11 @@ def test_fit_with_extrinsics_parity(nn, S, oracle_mod):
     _compare_iteration(dg_o, dg_g, 6, len(sc.nodes))
 
 
-def test_25_node_plane_fixture_parity(nn, oracle_mod):
-    # cpp/tests/test_deformable_mesh_fitter_advanced.cpp:55-143 scene (parity of the first iteration GPU vs oracle)
+def _plane25_scene(oracle_mod):
+    """cpp/tests/test_deformable_mesh_fitter_advanced.cpp:55-128: the 25-node plane meshes and nodes flipped about y and
+    moved 1.2 away from the camera, the target rendered at 100 x 100, its depth unprojected; plus the shipped ground-truth
+    node motion (:116-120, node_{translations,rotations}_25-node_plane.npy) carried into that frame (t' = F t,
+    R' = F R F with F = diag(-1, 1, -1)): it warps the source mesh onto the target to 2.4e-7."""
     T = np.array([[-1, 0, 0, 0], [0, 1, 0, 0], [0, 0, -1, 1.2], [0, 0, 0, 1.]])
     Ps, Ns, Fs = read_ply(os.path.join(FIXTURES, "plane_skin_25_nodes_source.ply"))
     Pt, Nt, Ft = read_ply(os.path.join(FIXTURES, "plane_skin_25_nodes_target.ply"))
@@ -988,24 +1054,84 @@ def test_25_node_plane_fixture_parity(nn, oracle_mod):
     Pt, Nt = transform_mesh(Pt, Nt, T)
     nodes = np.load(os.path.join(FIXTURES, "nodes_25-node_plane.npy")).astype(np.float32)
     nodes = (nodes.astype(np.float64) @ T[:3, :3].T + T[:3, 3]).astype(np.float32)
+    F = np.diag([-1.0, 1.0, -1.0])
+    t_gt = np.load(os.path.join(FIXTURES, "node_translations_25-node_plane.npy")).astype(np.float64) @ F.T
+    R_gt = F @ np.load(os.path.join(FIXTURES, "node_rotations_25-node_plane.npy")).astype(np.float64) @ F
     K = np.array([[100.0, 0, 50], [0, 100.0, 50], [0, 0, 1]])
     fndc, fm = oracle_mod.extract_face_ndc(Pt, Ft, K, 100, 100, 0.0, 10.0)
     fi, dep, _, _ = oracle_mod.rasterize(fndc, fm, 100, 100, 0.0, 1, -1, -1, True, False, True)
-    fi_g, dep_g, _, _ = nn.rendering.rasterize_ndc_triangles(fndc, fm, (100, 100), 0.0, 1, -1, -1, True, False, True)
-    assert np.array_equal(fi, _np(fi_g)) and np.array_equal(dep, _np(dep_g))
     depth = np.where(dep[..., 0] > 0, dep[..., 0], 0).astype(np.float32)
     refp, refm = oracle_mod.unproject(depth, K, 1.0, 10.0)
     weights = oracle_mod.node_coverage_weights(nodes, 0.1)
-    I = np.tile(np.eye(3, dtype=np.float32), (25, 1, 1))
-    R_o, t_o, dg_o = oracle_mod.fit(nodes=nodes, rotations=I, translations=np.zeros((25, 3), np.float32), mesh_points=Ps, mesh_normals=Ns,
-                                    faces=Fs, ref_points=refp, ref_mask=refm, H=100, W=100, K=K, max_iterations=1, lm_factor=0.001,
-                                    coverage=0.1, coverage_method=1, node_weights=weights)
+    return SimpleNamespace(Ps=Ps, Ns=Ns, Fs=Fs, Pt=Pt, Ft=Ft, nodes=nodes, K=K, fndc=fndc, fm=fm, fi=fi, dep=dep, depth=depth,
+                           refp=refp, refm=refm, weights=weights, t_gt=t_gt, R_gt=R_gt)
+
+
+def _plane25_fitter(nn, p, iterations):
     G, A = nn.geometry, nn.alignment
-    wf = G.HierarchicalGraphWarpField(nodes, 0.1, False, 4, 0, G.WarpNodeCoverageComputationMethod.MINIMAL_K_NEIGHBOR_NODE_DISTANCE, 1)
-    assert np.array_equal(wf.get_node_coverage_weights(), weights)
-    ft = A.DeformableMeshToImageFitter(1, [A.IterationMode.ALL], 1e-6, True, 10.0, False, 0.01, 0.001)
-    ft.fit_to_image(wf, G.TriangleMesh(Ps, Ns, Fs), None, depth, depth > 0, K, np.eye(4), 1.0)
+    wf = G.HierarchicalGraphWarpField(p.nodes, 0.1, False, 4, 0, G.WarpNodeCoverageComputationMethod.MINIMAL_K_NEIGHBOR_NODE_DISTANCE, 1)
+    assert np.array_equal(wf.get_node_coverage_weights(), p.weights)
+    ft = A.DeformableMeshToImageFitter(iterations, [A.IterationMode.ALL], 1e-6, True, 10.0, False, 0.01, 0.001)
+    return wf, ft
+
+
+def _plane25_oracle_iteration(oracle_mod, p, R0, t0):
+    return oracle_mod.fit(nodes=p.nodes, rotations=R0, translations=t0, mesh_points=p.Ps, mesh_normals=p.Ns, faces=p.Fs,
+                          ref_points=p.refp, ref_mask=p.refm, H=100, W=100, K=p.K, max_iterations=1, lm_factor=0.001, coverage=0.1,
+                          coverage_method=1, node_weights=p.weights)
+
+
+def test_25_node_plane_fixture_parity(nn, oracle_mod):
+    # cpp/tests/test_deformable_mesh_fitter_advanced.cpp:55-143 scene (parity of the first iteration GPU vs oracle)
+    p = _plane25_scene(oracle_mod)
+    fi_g, dep_g, _, _ = nn.rendering.rasterize_ndc_triangles(p.fndc, p.fm, (100, 100), 0.0, 1, -1, -1, True, False, True)
+    assert np.array_equal(p.fi, _np(fi_g)) and np.array_equal(p.dep, _np(dep_g))
+    I = np.tile(np.eye(3, dtype=np.float32), (25, 1, 1))
+    R_o, t_o, dg_o = _plane25_oracle_iteration(oracle_mod, p, I, np.zeros((25, 3), np.float32))
+    wf, ft = _plane25_fitter(nn, p, 1)
+    ft.fit_to_image(wf, nn.geometry.TriangleMesh(p.Ps, p.Ns, p.Fs), None, p.depth, p.depth > 0, p.K, np.eye(4), 1.0)
     _compare_iteration(dg_o, ft.diagnostics(), 6, 25)
+
+
+def test_25_node_plane_distance_to_ground_truth(nn, oracle_mod):
+    """the fit against the reference's own ground-truth motion for its 25-node plane scene
+    (test_deformable_mesh_fitter_advanced.cpp:116-120; the reference test asserts nothing, :140-142). Three GN iterations
+    on the GPU from the identity; each is checked against the oracle iteration started from the GPU's motion, and the
+    distance of the node motion from the ground truth (mean |t - t_gt|, max |R - R_gt|, mean warped-vertex distance from
+    the target mesh) is recorded for both. The reference algorithm (block-diagonal data term, A17) does not approach its
+    own ground truth on this scene: from 0.092 (mean translation distance at the identity) it moves to 0.25 and 0.78 (the
+    reference notes its fit misbehaving at iteration 2, :135). So what is pinned is what the oracle achieves: per
+    iteration the GPU's distances equal the oracle's (1e-3 relative), and they grow or shrink where the oracle's do."""
+    p = _plane25_scene(oracle_mod)
+    wf, ft = _plane25_fitter(nn, p, 3)
+    ft.prepare(wf, nn.geometry.TriangleMesh(p.Ps, p.Ns, p.Fs), p.depth, p.depth > 0, p.K, np.eye(4), 1.0)
+    a, w = oracle_mod.compute_anchors(p.Ps, p.nodes, 4, 0.1, node_weights=p.weights)
+
+    def dist(R, t):
+        R, t = np.asarray(R, np.float32).reshape(25, 3, 3), np.asarray(t, np.float32).reshape(25, 3)
+        Pw, _ = oracle_mod.warp_mesh(p.Ps, p.Ns, p.nodes, R, t, a, w)
+        return (float(np.linalg.norm(t - p.t_gt, axis=1).mean()), float(np.abs(R - p.R_gt).max()),
+                float(np.linalg.norm(Pw - p.Pt, axis=1).mean()))
+
+    d0 = dist(np.tile(np.eye(3, dtype=np.float32), (25, 1, 1)), np.zeros((25, 3), np.float32))
+    rows_g, rows_o = [d0], [d0]
+    for k in range(3):
+        R0, t0 = wf.get_node_rotations(True), wf.get_node_translations(True)
+        ft.iterate(wf, k, 1)
+        ft.check()
+        R_o, t_o, dg_o = _plane25_oracle_iteration(oracle_mod, p, R0, t0)
+        _compare_iteration(dg_o, ft.diagnostics(), 6, 25)
+        dg_, do_ = dist(wf.get_node_rotations(True), wf.get_node_translations(True)), dist(R_o, t_o)
+        print(f"25-node plane iteration {k + 1}: distance to GT (mean |t - t_gt|, max |R - R_gt|, mean vertex) GPU {dg_}, "
+              f"oracle {do_}", flush=True)
+        for x, y in zip(dg_, do_):   # the updates agree to 1e-4 (_compare_iteration); distances derived from them to 1e-3
+            assert abs(x - y) <= 1e-3 * max(abs(y), 1e-3)
+        rows_g.append(dg_)
+        rows_o.append(do_)
+    for k in range(1, len(rows_g)):
+        for c in range(3):
+            assert (rows_g[k][c] > rows_g[k - 1][c]) == (rows_o[k][c] > rows_o[k - 1][c]), (k, c, rows_g, rows_o)
+    assert abs(rows_o[0][0] - 0.0917) < 1e-3 and rows_o[1][0] > rows_o[0][0]   # the reference's fit moves away from its GT
 
 
 # ---------------------------------------------------------------------------------------------------------------------

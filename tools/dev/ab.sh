@@ -15,7 +15,7 @@ import json, sys
 line = [l for l in open(sys.argv[2]) if l.startswith("{")][-1]
 d = json.loads(line)
 print(json.dumps({"tag": sys.argv[1], "value": round(d["value"], 1), "ms_per_step": round(d["ms_per_step"] * 1000, 2),
-                  "kernel_us": {k: round(v * 1000, 2) for k, v in d["kernel_ms"].items()}}))
+                  "kernel_us": {k: (round(v * 1000, 2) if v is not None else None) for k, v in d["kernel_ms"].items()}}))
 PY
 			tail -1 gpurun_out/ab/summary.jsonl
 		done
