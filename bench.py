@@ -30,6 +30,7 @@ socket's physical cores with OMP_PROC_BIND=close and this process's CPU share, t
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -186,7 +187,7 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-share-only", action="store_true", help="CPU baseline at this process's CPU share only (large configs: C3)")
     ap.add_argument("--cpu-no-warm", action="store_true", help="CPU baseline without the untimed first call (large configs: C3)")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "r04_pmc_traffic.json"),
+    ap.add_argument("--traffic-file", default=None,
                     help="PMC-derived HBM bytes per launch of the roofline kernel (tools/pmc_traffic.py output)")
     return ap.parse_args(argv)
 
@@ -207,15 +208,20 @@ def render_target(sc, G, Rr):
     return (d * (d > 0)).contiguous()
 
 
-def load_traffic(path: str, workload: str):
-    try:
-        with open(path) as f:
-            t = json.load(f)
-    except (OSError, ValueError):
-        return None, None
-    if t.get("workload") != workload or ROOFLINE_KERNEL not in t.get("kernels", {}):
-        return None, None
-    return t["kernels"][ROOFLINE_KERNEL].get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+def load_traffic(path, workload: str):
+    """PMC traffic file of this workload (tools/pmc_traffic.py): the given path, or else the newest
+    profiles/r*_pmc_traffic*.json whose workload matches. Returns (the file's kernels dict, its path relative to the
+    repo) or (None, None)."""
+    paths = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic*.json")), reverse=True)
+    for p in paths:
+        try:
+            with open(p) as f:
+                t = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if t.get("workload") == workload and t.get("kernels"):
+            return t["kernels"], os.path.relpath(p, ROOT)
+    return None, None
 
 
 def host_cpu():
@@ -545,11 +551,24 @@ def main(argv=None):
                       flops_formula="SURVEY.md 8(d): (6 n1)^3 / 3 + 2 (6 n1)^2 (1 + n_rhs), n_rhs = 1 (the reference's dense corner; "
                                     "the tile-sparse factorization performs fewer: plan below)",
                       plan=ft.corner_info(), refinement=ft.refine_info())
+        # the flops the tile-sparse plan actually executes on the MFMA (update-term tile products + rank-32 products) and
+        # that figure's rate, beside the dense count the fraction above prices
+        work = ft.corner_work()
+        corner["executed"] = dict(work, achieved_tflops=work["mfma_flops"] / (solve_ms * 1e-3) / 1e12,
+                                  frac=work["mfma_flops"] / (solve_ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS,
+                                  note="MFMA flops of the executed plan per solve over the whole solve stage's time")
     kbytes = kernels[ROOFLINE_KERNEL]["algorithmic_bytes"]
     k_ms = ktimes[ROOFLINE_KERNEL] or ktimes["iteration"]
     achieved = kbytes / (k_ms * 1e-3) / 1e9
     it_bytes = sum(sb.values())
-    traffic, traffic_src = load_traffic(args.traffic_file, workload)
+    pmc, traffic_src = load_traffic(args.traffic_file, workload)
+    traffic = (pmc or {}).get(ROOFLINE_KERNEL, {}).get("hbm_bytes_per_launch")
+    if pmc:   # every kernel the PMC passes measured: its HBM bytes per launch and that traffic's fraction of peak
+        for kname, kd in kernels.items():
+            pk = pmc.get(kname) or pmc.get(kname + "_lanes")
+            if pk and kd.get("ms"):
+                kd["traffic"] = pk["hbm_bytes_per_launch"]
+                kd["traffic_frac"] = pk["hbm_bytes_per_launch"] / (kd["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS
 
     # once-per-frame setup (DeformableMeshToImageFitter.cpp:96-106: anchors, reference point cloud, buffers), timed
     # on a repeated prepare() of the same frame
@@ -614,6 +633,11 @@ def main(argv=None):
         "per_replica": per_replica if R > 1 else None,
         "cpu_baseline": None,
     }
+    if corner is not None and pmc:   # the solve stage's kernels as the PMC passes measured them (bytes per launch)
+        corner["traffic_per_launch"] = {k: v["hbm_bytes_per_launch"] for k, v in pmc.items()
+                                        if k in ("k_corner_factor", "k_corner_flow", "k_corner_invert", "k_stem_schur_rhs", "k_arrow_prepare",
+                                                 "k_init_stem")}
+        corner["traffic_source"] = traffic_src
     if corner is not None:   # ARAP configs: the dense corner (MFMA-bound) is the dominant stage; the HBM one moves aside
         out["hbm_roofline"] = out["roofline"]
         out["roofline"] = corner

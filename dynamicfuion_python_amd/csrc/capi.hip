@@ -1044,6 +1044,16 @@ nnrt_status nnrt_fitter_corner_info(const nnrt_fitter* ft, int64_t* h_out) {
 	return NNRT_OK;
 }
 
+nnrt_status nnrt_fitter_corner_work(const nnrt_fitter* ft, int64_t* h_out) {
+	NNRT_CHECK_ARG(ft && h_out, "null pointer");
+	const CornerSolver& c = ft->corner;
+	const bool on = ft->E > 0;
+	h_out[0] = on ? c.mfma_flops() : 0;
+	h_out[1] = on ? c.update_terms() : 0;
+	h_out[2] = on ? c.eliminated_columns() : 0;
+	return NNRT_OK;
+}
+
 nnrt_status nnrt_fitter_refine_info(nnrt_fitter* ft, float* h_out, void* stream) {
 	NNRT_CHECK_ARG(ft && h_out, "null pointer");
 	DeviceGuard guard(ft->device);

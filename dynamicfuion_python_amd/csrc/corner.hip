@@ -36,6 +36,7 @@
 namespace nnrt {
 
 constexpr int CT = 256;                       // threads per workgroup of the corner kernels
+constexpr int CTF = 512;                      // threads per workgroup of the factor launches (k_corner_factor)
 constexpr int TILE = CORNER_NB;               // 64
 constexpr int TILE_ELEMS = TILE * TILE;
 constexpr int CS4 = TILE + 4;                 // LDS row stride of staged tiles (16-B aligned rows for ds_read_b128)
@@ -261,7 +262,7 @@ struct CornerPlan {
 	std::vector<int> flow_need, col_chain;
 };
 
-static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const float* corner_pos) {
+static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const float* corner_pos, bool trim = true) {
 	CornerPlan p;
 	const int nc = N - n0;
 	p.nc = nc;
@@ -374,10 +375,16 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 			const std::vector<int>* dterms = terms(l, J, J);
 			std::vector<int> rows(1, J);
 			rows.insert(rows.end(), cs[static_cast<size_t>(J)].begin(), cs[static_cast<size_t>(J)].end());
+			int nreal = 0;   // the column's real rows, a prefix (every ND group starts on a tile boundary); else all 64
+			for (int r = 0; r < TILE; r++) nreal += p.row_node[static_cast<size_t>(J) * TILE + r] >= 0;
+			for (int r = 0; r < TILE; r++)
+				if ((p.row_node[static_cast<size_t>(J) * TILE + r] >= 0) != (r < nreal)) nreal = TILE;
+			if (!trim) nreal = TILE;
 			for (int I : rows) {
 				CornerTask t{};
 				t.I = I;
 				t.J = J;
+				t.nreal = nreal;
 				t.slot_t = slot(I, J);
 				t.slot_d = slot(J, J);
 				t.src = static_cast<int>(p.srcs.size());
@@ -401,6 +408,7 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 			CornerTask t{};
 			t.I = I;
 			t.J = J;
+			t.nreal = TILE;
 			t.slot_t = slot(I, J);
 			t.slot_d = -1;
 			t.src = static_cast<int>(p.srcs.size());
@@ -698,12 +706,22 @@ __device__ inline void eliminate_columns(f32x2 (&ap)[TILE], int lane, int& bad) 
 // development timing build only (-DNNRT_CORNER_STAMPS, tools/dev/stamps_build.sh): shader-clock stamps of the first
 // workgroup of each factor launch at its phase boundaries, read back by nnrt_dev_corner_stamps
 #ifdef NNRT_CORNER_STAMPS
-__device__ unsigned long long g_corner_stamps[256][8];
+// [level][workgroup][8]: shader clock at the phase boundaries 0-5 of every workgroup, the constant-rate clock at its start
+// (6) and end (7, bit 62 set for trailing tasks)
+__device__ unsigned long long g_corner_stamps[64][512][8];
 #define CORNER_STAMP(i)                                                                                                  \
 	do {                                                                                                                 \
-		if (blockIdx.x == 0 && threadIdx.x == 0 && a.level < 256) g_corner_stamps[a.level][i] = __builtin_amdgcn_s_memtime(); \
+		if (threadIdx.x == 0 && a.level < 64 && blockIdx.x < 512) g_corner_stamps[a.level][blockIdx.x][i] = __builtin_amdgcn_s_memtime(); \
+	} while (0)
+#define CORNER_RT(i, flag)                                                                                               \
+	do {                                                                                                                 \
+		if (threadIdx.x == 0 && a.level < 64 && blockIdx.x < 512)                                                        \
+			g_corner_stamps[a.level][blockIdx.x][i] = __builtin_amdgcn_s_memrealtime() | (flag);                         \
 	} while (0)
 #else
+#define CORNER_RT(i, flag) \
+	do {                   \
+	} while (0)
 #define CORNER_STAMP(i) \
 	do {                \
 	} while (0)
@@ -796,22 +814,26 @@ __global__ __launch_bounds__(CT) void k_corner_invert(const float* __restrict__ 
 	for (int i = 0; i < TILE / 4; i++) M[(4 * i + q) * TILE + c] = m[i];
 }
 
-// One launch per level of the tile elimination tree.
+// One launch per level of the tile elimination tree; workgroups of 8 waves (CTF threads).
 //   panel (I, J) (blockIdx < n_panel): s_d = A_JJ - sum_k L_Jk L_Jk^T and s_p = A_IJ - sum_k L_Ik L_Jk^T over the columns k of
-//   the previous level (MFMA, one 32 x 32 quadrant per wave, into LDS); the diagonal workgroup stages b_J - sum_k L_Jk y_k
-//   as its augmented row. Wave 0 then holds both (lane = row) in registers and runs the 64 column eliminations of A_JJ,
-//   applying each to the panel row as it goes (one packed FMA per column pair), in two 32-column halves joined by a
-//   rank-32 MFMA update on the other three waves.
-//   trailing (blockIdx >= n_panel): A_IJ -= sum_k L_Ik L_Jk^T (and b_J -= sum_k L_Jk y_k on diagonal tiles).
-__global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
+//   the previous level (MFMA, one 32 x 32 quadrant per wave): waves 0-3 stage s_d while waves 4-7 stage s_p (below the
+//   diagonal) or the augmented row b_J - sum_k L_Jk y_k (the diagonal workgroup), so a panel's two tiles' update terms run
+//   side by side. Wave 0 then holds both (lane = row) in registers and eliminates the column's real columns (a tile
+//   whose last rows are identity padding stops there: the padding's columns are the identity, their elimination changes
+//   nothing), applying each to the panel row as it goes (one packed FMA per column pair): up to 32 columns in one run,
+//   else two 32-column halves joined by a rank-32 MFMA update on waves 1-3.
+//   trailing (blockIdx >= n_panel): A_IJ -= sum_k L_Ik L_Jk^T (and b_J -= sum_k L_Jk y_k on diagonal tiles), waves 0-3.
+__global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 	__shared__ float s_d[TILE * CS4];   // A_JJ after the previous level's updates
 	__shared__ float s_p[TILE * CS4];   // A_IJ after the previous level's updates (panel workgroups below the diagonal)
 	__shared__ float s_b[TILE];         // b_J after the previous level's updates (diagonal workgroup)
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
 	CORNER_STAMP(0);
+	CORNER_RT(6, 0ull);
 	const CornerTask tk = a.tasks[blockIdx.x];
 	const int4* src = a.srcs + tk.src;
 	if (static_cast<int>(blockIdx.x) >= a.n_panel) {
+		if (wave >= 4) return;   // (no workgroup barrier follows)
 		const int qr = wave >> 1, qc = wave & 1;
 		float* C = a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS + 32 * qc + (lane & 31);
 		float cv[16];
@@ -826,18 +848,21 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 			const float s = rhs_updates(a.tiles, src, tk.nd, a.cb, t);
 			if ((t & 3) == 0) bj[t >> 2] = bv - s;
 		}
+		CORNER_RT(7, 1ull << 62);
 		return;
 	}
 	const bool diag = tk.I == tk.J;
 	// the gate's diag(S) entry of this lane's row, loaded now: after the elimination its latency would sit on the
 	// level's critical path
 	const float sd = diag && a.pivot_word && wave == 0 ? a.sdiag[static_cast<int64_t>(tk.J) * TILE + lane] : 0.f;
-	stage_tile(a.tiles, a.tiles + static_cast<int64_t>(tk.slot_d) * TILE_ELEMS, src, tk.nd, wave, lane, s_d);
-	if (!diag) {
-		stage_tile(a.tiles, a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS, src + tk.nd, tk.np, wave, lane, s_p);
+	if (wave < 4) {
+		stage_tile(a.tiles, a.tiles + static_cast<int64_t>(tk.slot_d) * TILE_ELEMS, src, tk.nd, wave, lane, s_d);
+	} else if (!diag) {
+		stage_tile(a.tiles, a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS, src + tk.nd, tk.np, wave - 4, lane, s_p);
 	} else {
-		const float s = rhs_updates(a.tiles, src, tk.nd, a.cb, t);
-		if ((t & 3) == 0) s_b[t >> 2] = a.cb[static_cast<int64_t>(tk.J) * TILE + (t >> 2)] - s;
+		const int t4 = t - 4 * 64;
+		const float s = rhs_updates(a.tiles, src, tk.nd, a.cb, t4);
+		if ((t4 & 3) == 0) s_b[t4 >> 2] = a.cb[static_cast<int64_t>(tk.J) * TILE + (t4 >> 2)] - s;
 	}
 	__syncthreads();
 	CORNER_STAMP(1);
@@ -845,6 +870,7 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 	// (v_pk_fma_f32) updates the pair. Wave 0 holds them; the other waves join for the rank-32 update between the halves.
 	f32x2 ap[TILE];
 	int bad = 0;
+	const bool full = tk.nreal > TILE / 2;   // workgroup-uniform
 	if (wave == 0) {
 #pragma unroll
 		for (int q = 0; q < TILE / 4; q++) {
@@ -859,20 +885,24 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 			ap[4 * q + 2] = f32x2{va.z, vp.z};
 			ap[4 * q + 3] = f32x2{va.w, vp.w};
 		}
+		// columns past the real ones are identity padding: with at most 32 real ones the first half covers the tile
 		eliminate_columns<0, TILE / 2>(ap, lane, bad);
 		CORNER_STAMP(2);
 		// L[:, 0:32] of the A_JJ rows and of the panel rows -> LDS (s_d / s_p are free once loaded)
+		if (full) {
 #pragma unroll
-		for (int q = 0; q < TILE / 8; q++) {
-			*reinterpret_cast<float4*>(s_d + lane * CS4 + 4 * q) = make_float4(ap[4 * q].x, ap[4 * q + 1].x, ap[4 * q + 2].x, ap[4 * q + 3].x);
-			*reinterpret_cast<float4*>(s_p + lane * CS4 + 4 * q) = make_float4(ap[4 * q].y, ap[4 * q + 1].y, ap[4 * q + 2].y, ap[4 * q + 3].y);
+			for (int q = 0; q < TILE / 8; q++) {
+				*reinterpret_cast<float4*>(s_d + lane * CS4 + 4 * q) = make_float4(ap[4 * q].x, ap[4 * q + 1].x, ap[4 * q + 2].x, ap[4 * q + 3].x);
+				*reinterpret_cast<float4*>(s_p + lane * CS4 + 4 * q) = make_float4(ap[4 * q].y, ap[4 * q + 1].y, ap[4 * q + 2].y, ap[4 * q + 3].y);
+			}
 		}
 	}
+	if (full) {
 	__syncthreads();
 	// rank-32 update of columns 32..63: C = L[rows, 0:32] L_JJ[32:64, 0:32]^T on the MFMA, one 32-row block per wave
 	// (wave 1: A_JJ rows 32..63; waves 2, 3: panel rows 0..31, 32..63; A_JJ rows 0..31 lie above the diagonal there)
 	f32x16 cacc = {};
-	if (wave > 0) {
+	if (wave > 0 && wave < 4) {
 		const float* X = wave == 1 ? s_d + 32 * CS4 : s_p + 32 * (wave - 2) * CS4;
 		const int half = lane >> 5, l32 = lane & 31;
 		const float4* x4 = reinterpret_cast<const float4*>(X + l32 * CS4 + 16 * half);
@@ -887,24 +917,27 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 		}
 	}
 	__syncthreads();   // every wave is done reading L before the products overwrite it
-	if (wave > 0) {
+	if (wave > 0 && wave < 4) {
 		float* Cb = wave == 1 ? s_d + 32 * CS4 : s_p + 32 * (wave - 2) * CS4;
 #pragma unroll
 		for (int v = 0; v < 16; v++) Cb[quad_row(v, lane) * CS4 + 32 + (lane & 31)] = cacc[v];
 	}
 	__syncthreads();
-	if (wave != 0) return;
-#pragma unroll
-	for (int q = TILE / 8; q < TILE / 4; q++) {
-		const float4 ca = lane >= 32 ? *reinterpret_cast<const float4*>(s_d + lane * CS4 + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
-		const float4 cp = *reinterpret_cast<const float4*>(s_p + lane * CS4 + 4 * q);
-		ap[4 * q] -= f32x2{ca.x, cp.x};
-		ap[4 * q + 1] -= f32x2{ca.y, cp.y};
-		ap[4 * q + 2] -= f32x2{ca.z, cp.z};
-		ap[4 * q + 3] -= f32x2{ca.w, cp.w};
 	}
-	CORNER_STAMP(3);
-	eliminate_columns<TILE / 2, TILE>(ap, lane, bad);
+	if (wave != 0) return;
+	if (full) {
+#pragma unroll
+		for (int q = TILE / 8; q < TILE / 4; q++) {
+			const float4 ca = lane >= 32 ? *reinterpret_cast<const float4*>(s_d + lane * CS4 + 4 * q) : make_float4(0.f, 0.f, 0.f, 0.f);
+			const float4 cp = *reinterpret_cast<const float4*>(s_p + lane * CS4 + 4 * q);
+			ap[4 * q] -= f32x2{ca.x, cp.x};
+			ap[4 * q + 1] -= f32x2{ca.y, cp.y};
+			ap[4 * q + 2] -= f32x2{ca.z, cp.z};
+			ap[4 * q + 3] -= f32x2{ca.w, cp.w};
+		}
+		CORNER_STAMP(3);
+		eliminate_columns<TILE / 2, TILE>(ap, lane, bad);
+	}
 	CORNER_STAMP(4);
 	if (diag) {
 		// the rows as eliminated (the part above the diagonal is not meaningful: k_corner_invert reads the lower part only);
@@ -929,12 +962,13 @@ __global__ __launch_bounds__(CT) void k_corner_factor(CornerFactorArgs a) {
 			for (int q = 0; q < TILE / 4; q++) wb[q] = make_float4(ap[4 * q].y, ap[4 * q + 1].y, ap[4 * q + 2].y, ap[4 * q + 3].y);
 			if (bad) atomicOr(a.error_flag, 1);
 		}
-		CORNER_STAMP(5);
 	} else {
 		float4* wp = reinterpret_cast<float4*>(a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS + lane * TILE);
 #pragma unroll
 		for (int q = 0; q < TILE / 4; q++) wp[q] = make_float4(ap[4 * q].y, ap[4 * q + 1].y, ap[4 * q + 2].y, ap[4 * q + 3].y);
 	}
+	CORNER_STAMP(5);
+	CORNER_RT(7, 0ull);
 }
 
 struct CornerBackArgs {
@@ -1587,7 +1621,7 @@ static void dev_free(void*& p) {
 }
 
 // development switches (A/B builds without rebuilding): NNRT_CORNER_WALK=0 disables the single-workgroup walk for small
-// corners, NNRT_CORNER_FLOW=0 the dataflow substitution launches
+// corners, NNRT_CORNER_FLOW=0 the dataflow substitution launches, NNRT_CORNER_TRIM=0 the padding-trimmed eliminations
 static bool env_flag(const char* name, bool dflt) {
 	const char* v = std::getenv(name);
 	return v ? std::strcmp(v, "0") != 0 : dflt;
@@ -1651,7 +1685,7 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 	// even if the new plan fails below; a failure leaves the solver empty (released), never half-built
 	release();
 	generation++;
-	const CornerPlan p = plan_corner(edges, E, n0, N, corner_pos);
+	const CornerPlan p = plan_corner(edges, E, n0, N, corner_pos, env_flag("NNRT_CORNER_TRIM", true));
 	auto fail = [&](nnrt_status st) {
 		release();
 		return st;
@@ -1731,6 +1765,15 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		fwd_pre_off = p.fwd_pre_off;
 		back_pre_off = p.back_pre_off;
 		fill_tiles = static_cast<int64_t>(slots);
+		n_terms = static_cast<int64_t>(p.srcs.size());
+		exec_mfma_flops = n_terms * 2 * TILE * TILE * TILE;
+		elim_cols = 0;
+		for (int l = 0; l < p.H; l++)
+			for (int q = p.level_off[static_cast<size_t>(l)]; q < p.level_off[static_cast<size_t>(l)] + p.level_panel[static_cast<size_t>(l)]; q++) {
+				const CornerTask& tk = p.tasks[static_cast<size_t>(q)];
+				if (tk.nreal > TILE / 2) exec_mfma_flops += 3 * 2 * 32 * 32 * 32;   // the rank-32 products of waves 1-3
+				if (tk.I == tk.J) elim_cols += tk.nreal;
+			}
 		dense_tiles = static_cast<int64_t>(corner_ld(6 * nc) / TILE) * (corner_ld(6 * nc) / TILE + 1) / 2;
 	}
 	key.swap(k);
@@ -1777,7 +1820,7 @@ nnrt_status CornerSolver::launch_factor(int* error_flag, hipStream_t s) const {
 		const int n = level_off[static_cast<size_t>(l) + 1] - level_off[static_cast<size_t>(l)];
 		fa.tasks = d_tasks + level_off[static_cast<size_t>(l)];
 		fa.n_panel = level_panel[static_cast<size_t>(l)];
-		k_corner_factor<<<n, CT, 0, s>>>(fa);
+		k_corner_factor<<<n, CTF, 0, s>>>(fa);
 		NNRT_LAUNCH_CHECK();
 	}
 	// every diagonal factor's inverse, one workgroup per tile column (the substitutions multiply by them)
@@ -1861,8 +1904,8 @@ nnrt_status CornerSolver::launch_resolve(float* xout, hipStream_t s, const unsig
 }
 
 #ifdef NNRT_CORNER_STAMPS
-extern "C" int nnrt_dev_corner_stamps(unsigned long long* out) {   // [256][8] shader-clock stamps of the last solve
-	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_corner_stamps), sizeof(unsigned long long) * 256 * 8) == hipSuccess ? 0 : 1;
+extern "C" int nnrt_dev_corner_stamps(unsigned long long* out) {   // [64][512][8] stamps of the last solve
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_corner_stamps), sizeof(unsigned long long) * 64 * 512 * 8) == hipSuccess ? 0 : 1;
 }
 #endif
 

@@ -193,7 +193,7 @@ struct CornerTask {   // one workgroup of a factor launch
 	int I, J;           // tile (I, J), I >= J
 	int slot_t, slot_d; // slots of tile (I, J) and of the diagonal tile (J, J) (-1 for trailing tasks)
 	int src, nd, np;    // update terms in `srcs`: nd for the diagonal tile (trailing: the tile's), then np for the panel tile
-	int pad;
+	int nreal;          // panel tasks: real (non-padding) rows of column J, a prefix of its 64; the elimination stops there
 };
 struct CornerMap {      // device view: permuted (row, column) -> stored entry
 	int T;
@@ -314,13 +314,17 @@ public:
 	int back_launches() const { return walk_ok ? 1 : back_off.empty() ? 0 : static_cast<int>(back_off.size()) - 1; }
 	int64_t stored_tiles() const { return fill_tiles; }
 	int64_t dense_lower_tiles() const { return dense_tiles; }
+	// executed factorization work: MFMA flops (update terms + rank-32 products), update terms, eliminated columns
+	int64_t mfma_flops() const { return exec_mfma_flops; }
+	int64_t update_terms() const { return n_terms; }
+	int64_t eliminated_columns() const { return elim_cols; }
 	uint64_t generation = 0;    // bumped whenever the plan (and its buffers) change
 
 private:
 	void release();
 	std::vector<int32_t> key;
 	int nc = 0, ld = 0, T = 0, H = 0, slots = 0, n_corner_edges = 0;
-	int64_t fill_tiles = 0, dense_tiles = 0;
+	int64_t fill_tiles = 0, dense_tiles = 0, exec_mfma_flops = 0, n_terms = 0, elim_cols = 0;
 	float *tiles = nullptr, *ldiag = nullptr, *minv = nullptr, *cb = nullptr, *cb2 = nullptr, *xp = nullptr, *sdiag = nullptr;
 	float* zx = nullptr;   // [ld] substitution pre-sums (NNRT_SUBST_PRESUM)
 	int2 *d_back_pre = nullptr, *d_fwd_pre = nullptr;

@@ -216,6 +216,13 @@ class DeformableMeshToImageFitter:
         keys = ("corner_nodes", "tile_columns", "factor_launches", "back_launches", "stored_tiles", "dense_lower_tiles")
         return {k: int(v) for k, v in zip(keys, out)}
 
+    def corner_work(self) -> dict:
+        """The plan's factorization work as executed (csrc/corner.hip): MFMA flops (update-term tile products + rank-32
+        products), update terms, eliminated tile columns (real columns summed)."""
+        out = np.zeros(3, np.int64)
+        N.check(N.lib().nnrt_fitter_corner_work(self._h, N.ptr(out)))
+        return {k: int(v) for k, v in zip(("mfma_flops", "update_terms", "eliminated_columns"), out)}
+
     def anchors(self, vertex_count: int, anchor_count: int, stream=None):
         a = np.empty((vertex_count, anchor_count), np.int32)
         w = np.empty((vertex_count, anchor_count), np.float32)

@@ -148,6 +148,10 @@ int32_t nnrt_fitter_graph_count(const nnrt_fitter* fitter);
  * 64-unknown tile columns, factorization launches (elimination-tree levels), back-substitution launches, stored
  * (structurally non-zero) tiles, lower tiles of the dense corner. */
 nnrt_status nnrt_fitter_corner_info(const nnrt_fitter* fitter, int64_t* h_out);
+/* Work of that plan's factorization as executed (diagnostic; zeros without ARAP): h_out[3] = MFMA flops per
+ * factorization (every update term's 64 x 64 x 64 tile product + the rank-32 products of the split eliminations),
+ * update terms, tile-column eliminations (real columns summed). The reference's dense count is (6 n1)^3 / 3 + ... */
+nnrt_status nnrt_fitter_corner_work(const nnrt_fitter* fitter, int64_t* h_out);
 /* The last arrowhead solve's refinement gate (diagnostic; synchronizes `stream`): h_out[3] = the corner factorization's
  * smallest pivot / diag(S) ratio (1 without ARAP), the threshold below which one step of iterative refinement runs (it
  * does not below 1e-4, where one step no longer converges), and 1 if it ran. */

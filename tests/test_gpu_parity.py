@@ -648,18 +648,20 @@ def test_flow_substitution_matches_chain_launches(nn, S, oracle_mod, name, walk)
     """The dataflow substitution launches (k_corner_flow: the back chains and the stem pass in one launch, the whole
     gated refinement step in a second) perform the same float operations as the per-depth chain launches they replace:
     along three GN iterations with the refinement forced open wherever the gate's floor allows (and once shut), updates,
-    node motion and gate words are bit-identical between fitters planned with NNRT_CORNER_FLOW=1 and =0
-    (NNRT_CORNER_WALK=0 makes the small C1 / C2 corners use chains instead of the single-workgroup walk)."""
+    node motion and gate words are bit-identical between fitters planned with NNRT_CORNER_FLOW=1 and =0 (with
+    NNRT_CORNER_TRIM=1 / 0: eliminations stopped at a tile's real columns against full 64-column ones;
+    NNRT_CORNER_WALK=0 makes the small C1 / C2 corners use chains instead of the single-workgroup walk)."""
     import os
     sc = _scene(S, oracle_mod, name)
     depth = scene_target(oracle_mod, sc)
     N = len(sc.nodes)
     runs = {}
-    old = {k: os.environ.get(k) for k in ("NNRT_CORNER_FLOW", "NNRT_CORNER_WALK")}
+    old = {k: os.environ.get(k) for k in ("NNRT_CORNER_FLOW", "NNRT_CORNER_WALK", "NNRT_CORNER_TRIM")}
     try:
         os.environ["NNRT_CORNER_WALK"] = walk
         for flow in ("1", "0"):
             os.environ["NNRT_CORNER_FLOW"] = flow
+            os.environ["NNRT_CORNER_TRIM"] = flow   # the padding-trimmed eliminations change no bit either
             wf, ft = _new_fit(nn, sc, depth, 3)
             rows = []
             for k, ratio in enumerate((np.inf, 0.0, np.inf)):

@@ -1,6 +1,8 @@
-"""Phase timing of the Schur-corner factor launches (development; needs tools/dev/libnnrt_stamps.so: tools/dev/stamps_build.sh NNRT_CORNER_STAMPS tools/dev/libnnrt_stamps.so).
-Runs one C5 GN iteration and prints, per factor launch, the shader-clock cycles of workgroup 0's phases: staging,
-first elimination half, rank-32 update, second half, stores."""
+"""Phase timing of the Schur-corner factor launches (development; needs tools/dev/libnnrt_stamps.so:
+tools/dev/stamps_build.sh NNRT_CORNER_STAMPS tools/dev/libnnrt_stamps.so).
+Runs C5 GN iterations and prints, per factor launch, every workgroup's span on the constant-rate clock (100 MHz) and the
+shader-clock cycles of the phases of the workgroup that ends last and of the slowest panel task: staging, first
+elimination half, rank-32 update, second half, stores."""
 import ctypes
 import os
 import sys
@@ -20,17 +22,34 @@ wf = G.HierarchicalGraphWarpField(sc.nodes, sc.coverage, False, 4, 0, G.WarpNode
 depth = np.full((sc.H, sc.W), 1.2, np.float32)
 ft = A.DeformableMeshToImageFitter(1, [A.IterationMode.ALL], preconditioning_dampening_factor=0.001, use_hip_graph=0)
 ft.prepare(wf, G.TriangleMesh(sc.points, sc.normals, sc.faces), depth, None, sc.K)
-for _ in range(3):
+for _ in range(5):
     ft.iterate_from_identity(wf, 0, 1)
 torch.cuda.synchronize()
-buf = np.zeros((256, 8), np.uint64)
+buf = np.zeros((64, 512, 8), np.uint64)
 fn = getattr(lib, "nnrt_dev_corner_stamps")
 fn.argtypes = [ctypes.c_void_p]
 assert fn(buf.ctypes.data) == 0
+MASK = (1 << 62) - 1
 names = ["stage", "half1", "rank32", "half2", "store"]
-for l in range(256):
-    st = buf[l]
-    if st[0] == 0:
+
+
+def phases(st):
+    return "  ".join(f"{n} {int(st[i + 1]) - int(st[i]) if st[i + 1] and st[i] else -1:6d}" for i, n in enumerate(names))
+
+
+for lev in range(64):
+    w = buf[lev]
+    live = np.nonzero(w[:, 6])[0]
+    if len(live) == 0:
         break
-    d = [int(st[i + 1]) - int(st[i]) if st[i + 1] else -1 for i in range(5)]
-    print(f"level {l:2d}: " + "  ".join(f"{n} {v:6d}" for n, v in zip(names, d)) + f"  total {int(st[5]) - int(st[0]) if st[5] else -1}")
+    t0 = int(min(w[i, 6] for i in live))
+    ends = [(int(w[i, 7]) & MASK, i) for i in live]
+    last_end, last = max(ends)
+    trailing = [i for i in live if int(w[i, 7]) >> 62 & 1]
+    panels = [i for i in live if not int(w[i, 7]) >> 62 & 1]
+    pspan = max(((int(w[i, 7]) & MASK) - int(w[i, 6]), i) for i in panels)
+    tspan = max((((int(w[i, 7]) & MASK) - int(w[i, 6]), i) for i in trailing), default=(0, -1))
+    start_spread = max(int(w[i, 6]) for i in live) - t0
+    print(f"level {lev:2d}: {len(panels)} panel + {len(trailing)} trailing wgs, span {10 * (last_end - t0) / 1000:.2f} us "
+          f"(last: {'trailing' if last in trailing else 'panel'} wg {last}); start spread {10 * start_spread / 1000:.2f} us; "
+          f"slowest panel {10 * pspan[0] / 1000:.2f} us [{phases(w[pspan[1]])}]; slowest trailing {10 * tspan[0] / 1000:.2f} us")
