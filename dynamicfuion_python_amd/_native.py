@@ -73,6 +73,7 @@ _SIGNATURES = {
     "nnrt_fitter_graph_count": (c_int32, [c_void_p]),
     "nnrt_fitter_corner_info": (c_int32, [c_void_p, c_void_p]),
     "nnrt_fitter_corner_work": (c_int32, [c_void_p, c_void_p]),
+    "nnrt_fitter_get_warped_mesh": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "nnrt_release_arrowhead_plans": (None, []),
     "nnrt_fitter_fit_from_snapshot": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p]),
     "nnrt_fitter_restore_motion": (c_int32, [c_void_p, c_void_p, c_void_p]),

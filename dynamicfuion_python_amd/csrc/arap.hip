@@ -384,8 +384,8 @@ __global__ void k_arrow_back(int n0, int n_update, const float* __restrict__ din
 	}
 	if (gate && mode == 1) refining = refine_gate_on(gate, ratio);
 	if (i >= n_update && i >= n0) return;
-	arrow_back_node(i, n0, n_update, dinv, edge_offsets, edge_list, edges, wing, rhs, x, XPlain{x}, state_in, node_state, updates_out, x_base,
-	                gate ? mode : 0, refining, diag, res);
+	arrow_back_node<false>(i, n0, n_update, dinv, edge_offsets, edge_list, edges, wing, XPlain{rhs}, x, XPlain{x}, state_in, node_state,
+	                       updates_out, x_base, XPlain{x_base}, gate ? mode : 0, refining, diag, res);
 }
 
 // ---- iterative refinement: the correction's corner right-hand side (one wave per corner node a; runs only when the gate
@@ -399,7 +399,7 @@ __global__ __launch_bounds__(256) void k_refine_corner_rhs(int n0, int nc, const
 	const int a = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6);
 	const int lane = static_cast<int>(threadIdx.x & 63);
 	if (a >= nc) return;
-	const float v = refine_rhs_node(a, lane, n0, dinv_b, diag, inc_off, inc_list, edges, wing, rhs, x, res);
+	const float v = refine_rhs_node(a, lane, n0, dinv_b, diag, inc_off, inc_list, edges, wing, rhs, XPlain{x}, XPlain{res});
 	if (lane < 6) rhs2[node_row[a] + lane] = v;
 }
 
@@ -435,9 +435,9 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 	}
 	const bool refine = ws.refine && ws.inc_off && ws.res && ws.dx && m > 0;
 	if (m > 0 && ws.corner->flow_ok()) {
-		// the corner's factorization, then two dataflow launches (corner.hip k_corner_flow): the back substitution chains
-		// with the stem pass (x, the update or, when the refinement gate opens, the stem residual), and the gated
-		// refinement step (empty when the gate is shut)
+		// the corner's factorization, then one dataflow launch (corner.hip k_corner_flow): the back substitution chains
+		// with the stem pass (x, the update or, when the refinement gate opens, the stem residual), then the gated
+		// refinement step's roles (they return at once when the gate is shut)
 		nnrt_status st = ws.corner->launch_factor(error_flag, stream);
 		if (st) return st;
 		FlowStem fs;
@@ -456,6 +456,7 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 		fs.edges = edges;
 		fs.rhs = ws.rhs;
 		fs.x = ws.x;
+		fs.dx = ws.dx;
 		fs.state_in = state_in;
 		fs.node_state = node_state;
 		fs.updates_out = updates_out;
@@ -463,15 +464,7 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 		fs.gate = refine ? ws.corner->pivot_ratio() : nullptr;
 		fs.ratio = ws.refine_ratio;
 		fs.error_flag = error_flag;
-		if ((st = ws.corner->launch_flow(0, fs, stream))) return st;
-		if (!refine) return NNRT_OK;
-		fs.n_update = ws.N;
-		fs.mode = 2;
-		fs.rhs = ws.res;
-		fs.x = ws.dx;
-		fs.x_base = ws.x;
-		fs.rhs_b = ws.rhs;
-		return ws.corner->launch_flow(1, fs, stream);
+		return ws.corner->launch_flow(fs, stream);
 	}
 	if (m > 0) {
 		nnrt_status st = ws.corner->launch_solve(ws.x + 6 * static_cast<int64_t>(ws.n0), error_flag, stream);

@@ -73,6 +73,24 @@ struct XSc1 {
 	}
 };
 
+// where the stem pass's per-node outputs go: plain stores (read by later launches) or sc1 stores (read by other
+// workgroups of the same dataflow launch), 8 B at a time
+template <bool SC1>
+__device__ __forceinline__ void store6(float* dst, const float (&v)[6]) {
+	if constexpr (SC1) {
+#pragma unroll
+		for (int q = 0; q < 3; q++)
+			__hip_atomic_store(reinterpret_cast<unsigned long long*>(dst) + q,
+			                   static_cast<unsigned long long>(__float_as_uint(v[2 * q])) |
+			                       (static_cast<unsigned long long>(__float_as_uint(v[2 * q + 1])) << 32),
+			                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	} else {
+		float2* d2 = reinterpret_cast<float2*>(dst);
+#pragma unroll
+		for (int q = 0; q < 3; q++) d2[q] = make_float2(v[2 * q], v[2 * q + 1]);
+	}
+}
+
 // node update (R <- R Rodrigues(omega), t += dt) from the node's solved increment x6; updates_out gets x6. The motion
 // the iteration started from is read from state_in (the warp field's state, or a snapshot the iteration restarts from)
 // and the result written to node_state (g is never changed by an update)
@@ -95,12 +113,12 @@ __device__ __forceinline__ void arrow_update_node(int n, const float (&xl)[6], c
 
 // stem row i of the back substitution: x_i = D_i^-1 (b_i - sum over its edges e = (i, j) of B_e x_j) in float, edges in
 // CSR order (the one arithmetic every caller shares, so a recomputation is bit-identical)
-template <class XL>
+template <class RL, class XL>
 __device__ __forceinline__ void stem_solve(int i, const float* __restrict__ dinv, const int* __restrict__ edge_offsets, const int* __restrict__ edge_list,
-                                           const int32_t* __restrict__ edges, const float* __restrict__ wing, const float* __restrict__ rhs,
-                                           const XL& x, float (&o)[6]) {
+                                           const int32_t* __restrict__ edges, const float* __restrict__ wing, const RL& rhs, const XL& x,
+                                           float (&o)[6]) {
 	float r6[6];
-	for (int c = 0; c < 6; c++) r6[c] = rhs[6 * static_cast<int64_t>(i) + c];
+	rhs.ld6(i, r6);
 	for (int ei = edge_offsets[i]; ei < edge_offsets[i + 1]; ei++) {
 		const int e = edge_list[ei];
 		const int j = edges[2 * e + 1];
@@ -128,16 +146,18 @@ __device__ __forceinline__ void stem_solve(int i, const float* __restrict__ dinv
 
 // residual of stem row i, rhs_i - D_i x_i - sum over its edges of B_e x_j, the products and sums in double, rounded once
 // (D_i: the prepared diagonal block with LM; stem nodes couple to corner nodes only)
-template <class XL>
+template <class RL, class XL>
 __device__ __forceinline__ void stem_residual(int i, const float (&xi)[6], const float* __restrict__ diag, const int* __restrict__ edge_offsets,
                                               const int* __restrict__ edge_list, const int32_t* __restrict__ edges, const float* __restrict__ wing,
-                                              const float* __restrict__ rhs, const XL& x, float (&res)[6]) {
+                                              const RL& rhs, const XL& x, float (&res)[6]) {
 	double r[6];
 	float D[36];
 	load36(diag + static_cast<int64_t>(i) * 36, D);
+	float b6[6];
+	rhs.ld6(i, b6);
 #pragma unroll
 	for (int c = 0; c < 6; c++) {
-		double s = static_cast<double>(rhs[6 * static_cast<int64_t>(i) + c]);
+		double s = static_cast<double>(b6[c]);
 #pragma unroll
 		for (int k = 0; k < 6; k++) s -= static_cast<double>(D[6 * c + k]) * static_cast<double>(xi[k]);
 		r[c] = s;
@@ -164,45 +184,48 @@ __device__ __forceinline__ void stem_residual(int i, const float (&xi)[6], const
 // threads at their own rows, which no thread of the pass reads).
 // mode 1 = the first pass of a gated refinement (refining: the gate's decision): x_i always, the update only when the
 // refinement does not run, else the stem residual r_i -> res; mode 2 = the refinement's last pass.
-// xc: the loader of x's corner rows (written by the corner substitution).
-template <class XL>
+// Loaders: rl the right-hand side's rows, xc x's corner rows (written by the corner substitution), bl x_base's rows;
+// SC1OUT: x's stem rows and res are read by other workgroups of the same launch (sc1 stores).
+template <bool SC1OUT, class RL, class XL, class BL>
 __device__ __forceinline__ void arrow_back_node(int i, int n0, int n_update, const float* __restrict__ dinv, const int* __restrict__ edge_offsets,
                                                 const int* __restrict__ edge_list, const int32_t* __restrict__ edges, const float* __restrict__ wing,
-                                                const float* __restrict__ rhs, float* __restrict__ x, const XL& xc, const float* state_in, float* node_state,
-                                                float* __restrict__ updates_out, float* __restrict__ x_base, int mode, bool refining,
+                                                const RL& rl, float* __restrict__ x, const XL& xc, const float* state_in, float* node_state,
+                                                float* __restrict__ updates_out, float* __restrict__ x_base, const BL& bl, int mode, bool refining,
                                                 const float* __restrict__ diag, float* __restrict__ res) {
 	if (mode == 1 && refining) node_state = nullptr;   // the refinement's last pass applies the update
 	if (i >= n0) {
 		if (i < n_update && (node_state || x_base)) {
 			float xl[6];
 			xc.ld6(i, xl);
-			if (x_base)
+			if (x_base) {
+				float xb[6];
+				bl.ld6(i, xb);
 				for (int c = 0; c < 6; c++) {
-					xl[c] = x_base[6 * static_cast<int64_t>(i) + c] + xl[c];
+					xl[c] = xb[c] + xl[c];
 					x_base[6 * static_cast<int64_t>(i) + c] = xl[c];
 				}
+			}
 			if (node_state) arrow_update_node(i, xl, state_in, node_state, updates_out);
 		}
 		return;
 	}
 	float o[6];
-	stem_solve(i, dinv, edge_offsets, edge_list, edges, wing, rhs, xc, o);
-	float2* xo = reinterpret_cast<float2*>(x + 6 * static_cast<int64_t>(i));
-#pragma unroll
-	for (int q = 0; q < 3; q++) xo[q] = make_float2(o[2 * q], o[2 * q + 1]);
+	stem_solve(i, dinv, edge_offsets, edge_list, edges, wing, rl, xc, o);
+	store6<SC1OUT>(x + 6 * static_cast<int64_t>(i), o);
 	if (mode == 1 && refining) {   // the stem row's residual (reads only corner x: no thread of this pass writes those)
 		float ri[6];
-		stem_residual(i, o, diag, edge_offsets, edge_list, edges, wing, rhs, xc, ri);
-		float2* ro = reinterpret_cast<float2*>(res + 6 * static_cast<int64_t>(i));
-#pragma unroll
-		for (int q = 0; q < 3; q++) ro[q] = make_float2(ri[2 * q], ri[2 * q + 1]);
+		stem_residual(i, o, diag, edge_offsets, edge_list, edges, wing, rl, xc, ri);
+		store6<SC1OUT>(res + 6 * static_cast<int64_t>(i), ri);
 	}
-	if (x_base)
+	if (x_base) {
+		float xb[6];
+		bl.ld6(i, xb);
 #pragma unroll
 		for (int c = 0; c < 6; c++) {
-			o[c] = x_base[6 * static_cast<int64_t>(i) + c] + o[c];
+			o[c] = xb[c] + o[c];
 			x_base[6 * static_cast<int64_t>(i) + c] = o[c];
 		}
+	}
 	if (node_state) arrow_update_node(i, o, state_in, node_state, updates_out);
 }
 
@@ -210,10 +233,10 @@ __device__ __forceinline__ void arrow_back_node(int i, int n0, int n_update, con
 // `lane`, others 0): r_a - sum over stem edges i -> a of (D_i^-1 B_ia)^T r_i, with r_a = b_a - D_a x_a - sum over a's
 // incidences of the wing blocks times x (B^T x_i for stem edges, B x_b / B^T x_b for corner edges), products and sums in
 // double, rounded once; x (all rows) and r_i of the stem rows from the first back-substitution pass (earlier launches) ----
+template <class XL, class RSL>
 __device__ __forceinline__ float refine_rhs_node(int a, int lane, int n0, const float* __restrict__ dinv_b, const float* __restrict__ diag,
                                                  const int* __restrict__ inc_off, const int* __restrict__ inc_list, const int32_t* __restrict__ edges,
-                                                 const float* __restrict__ wing, const float* __restrict__ rhs, const float* __restrict__ x,
-                                                 const float* __restrict__ res) {
+                                                 const float* __restrict__ wing, const float* __restrict__ rhs, const XL& x, const RSL& res) {
 	const int n = n0 + a;
 	double ra[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};   // this lane's share of sum H_an x_n over a's incidences
 	float s2[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};    // this lane's share of sum (D_i^-1 B_ia)^T r_i
@@ -224,10 +247,10 @@ __device__ __forceinline__ float refine_rhs_node(int a, int lane, int n0, const 
 		const int other = edges[2 * e + (tgt ? 0 : 1)];
 		float B[36], xo[6];
 		load36(wing + static_cast<int64_t>(e) * 36, B);
-		load6(x + 6 * static_cast<int64_t>(other), xo);
+		x.ld6(other, xo);
 		if (other < n0) {   // stem edge other -> n
 			float ri[6], Y[36];
-			load6(res + 6 * static_cast<int64_t>(other), ri);
+			res.ld6(other, ri);
 			load36(dinv_b + static_cast<int64_t>(e) * 36, Y);
 #pragma unroll
 			for (int c = 0; c < 6; c++) {
@@ -260,7 +283,7 @@ __device__ __forceinline__ float refine_rhs_node(int a, int lane, int n0, const 
 				u = s2[c];
 			}
 		float xa[6];
-		load6(x + 6 * static_cast<int64_t>(n), xa);
+		x.ld6(n, xa);
 		double r = static_cast<double>(rhs[6 * static_cast<int64_t>(n) + lane]);
 #pragma unroll
 		for (int k = 0; k < 6; k++) r -= static_cast<double>(diag[static_cast<int64_t>(n) * 36 + 6 * lane + k]) * static_cast<double>(xa[k]);

@@ -1044,6 +1044,26 @@ nnrt_status nnrt_fitter_corner_info(const nnrt_fitter* ft, int64_t* h_out) {
 	return NNRT_OK;
 }
 
+nnrt_status nnrt_fitter_get_warped_mesh(nnrt_fitter* ft, float* h_positions, float* h_normals, void* stream) {
+	NNRT_CHECK_ARG(ft && h_positions && h_normals, "null pointer");
+	NNRT_CHECK_ARG(ft->V > 0 && ft->wpos.ptr, "no prepared frame");
+	DeviceGuard guard(ft->device);
+	NNRT_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+	NNRT_HIP(hipStreamSynchronize(ft->work));
+	std::vector<float4> p(static_cast<size_t>(ft->V)), n(static_cast<size_t>(ft->V));
+	NNRT_HIP(hipMemcpy(p.data(), ft->wpos.ptr, sizeof(float4) * p.size(), hipMemcpyDeviceToHost));
+	NNRT_HIP(hipMemcpy(n.data(), ft->wnrm.ptr, sizeof(float4) * n.size(), hipMemcpyDeviceToHost));
+	for (size_t v = 0; v < p.size(); v++) {
+		h_positions[3 * v] = p[v].x;
+		h_positions[3 * v + 1] = p[v].y;
+		h_positions[3 * v + 2] = p[v].z;
+		h_normals[3 * v] = n[v].x;
+		h_normals[3 * v + 1] = n[v].y;
+		h_normals[3 * v + 2] = n[v].z;
+	}
+	return NNRT_OK;
+}
+
 nnrt_status nnrt_fitter_corner_work(const nnrt_fitter* ft, int64_t* h_out) {
 	NNRT_CHECK_ARG(ft && h_out, "null pointer");
 	const CornerSolver& c = ft->corner;

@@ -580,12 +580,39 @@ __device__ inline f32x16 quadrant_xyt(const float* X, const float* Y, int64_t ld
 
 __device__ inline int quad_row(int v, int lane) { return (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5); }
 
-// sum over the update terms of X Y^T for this wave's quadrant
+// one update term's operands for this lane (quadrant_xyt's loads) and its 32 MFMA steps
+__device__ __forceinline__ void term_load(const float* tiles, int4 s, int qr, int qc, int lane, float4 (&vx)[8], float4 (&vy)[8]) {
+	const int half = lane >> 5, l32 = lane & 31;
+	const float4* x4 = reinterpret_cast<const float4*>(tiles + static_cast<int64_t>(s.x) * TILE_ELEMS + (32 * qr + l32) * TILE + 32 * half);
+	const float4* y4 = reinterpret_cast<const float4*>(tiles + static_cast<int64_t>(s.y) * TILE_ELEMS + (32 * qc + l32) * TILE + 32 * half);
+#pragma unroll
+	for (int q = 0; q < 8; q++) {
+		vx[q] = x4[q];
+		vy[q] = y4[q];
+	}
+}
+__device__ __forceinline__ f32x16 term_mfma(const float4 (&vx)[8], const float4 (&vy)[8], f32x16 acc) {
+#pragma unroll
+	for (int q = 0; q < 8; q++) {
+		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].x, vy[q].x, acc, 0, 0, 0);
+		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].y, vy[q].y, acc, 0, 0, 0);
+		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].z, vy[q].z, acc, 0, 0, 0);
+		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].w, vy[q].w, acc, 0, 0, 0);
+	}
+	return acc;
+}
+
+// sum over the update terms of X Y^T for this wave's quadrant, in term order (the products of quadrant_xyt). The compiler
+// streams each term's 16 operand loads into its MFMAs (two loads, a wait, four MFMAs, ...): the 8 loads of a lane's row
+// segment touch the same 64 lines, which the first of them brings into L1. Issuing all 16 first (scheduling barriers,
+// next term double-buffered) measured slower (round 5: C5 staging 22 k -> 30 k cycles per level): the 64 lines are then
+// missed 8 times over.
 __device__ inline f32x16 sum_updates(const float* tiles, const int4* src, int n, int qr, int qc, int lane) {
 	f32x16 acc = {};
 	for (int e = 0; e < n; e++) {
-		const int4 s = src[e];
-		acc = quadrant_xyt(tiles + static_cast<int64_t>(s.x) * TILE_ELEMS, tiles + static_cast<int64_t>(s.y) * TILE_ELEMS, TILE, qr, qc, lane, acc);
+		float4 vx[8], vy[8];
+		term_load(tiles, src[e], qr, qc, lane, vx, vy);
+		acc = term_mfma(vx, vy, acc);
 	}
 	return acc;
 }
@@ -1248,35 +1275,41 @@ __global__ __launch_bounds__(CT) void k_corner_fwd(CornerFwdArgs a, int ld) {
 }
 
 // ===================================================================================================================
-// Dataflow substitution launches (k_corner_flow): the corner's back substitution chains and the stem pass that follows
-// them (phase 0), or the whole gated refinement step -- the correction's corner right-hand side, the forward chains, the
-// back chains and the stem pass (phase 1) -- each as ONE launch instead of one launch per chain depth plus the stem's.
+// Dataflow substitution launch (k_corner_flow): the corner's back substitution chains and the stem pass that follows
+// them, then -- when the refinement gate opens -- the whole refinement step: the correction's corner right-hand side,
+// the forward chains, the back chains and the stem pass applying x + d; ONE launch instead of one launch per chain
+// depth per substitution plus the stem passes and the refinement's right-hand side (round 4: 2 + 12 launches at C5).
 //
 // Workgroups take tickets (one relaxed agent-scope atomic add each) and a ticket fixes the role; roles are numbered so
-// that every wait is on work of a LOWER ticket: phase 1 runs [T rhs workers (one per tile column)] [forward chains,
-// deepest first] [back chains, root first] [stem workers], phase 0 [back chains] [stem workers]. A forward chain waits
-// for its columns' right-hand sides and its child chains, a back chain for its parent chain (a root: for its own forward
-// chain in phase 1), a stem worker for every back chain. A workgroup that holds a ticket is resident and waits only on
-// lower tickets, so by induction every wait ends: no assumption on dispatch order, co-residency or timing (the plan
-// emulator checks the ticket order: tests/test_corner_plan.py). Every spin is bounded (error flag bit 8 on a timeout).
+// that every wait is on work of a LOWER ticket: [back chains, root first] [stem workers] [rhs workers, one per tile
+// column] [forward chains, deepest first] [back chains, root first] [stem workers]. A back chain waits for its parent
+// chain (the refinement's roots: for their own forward chain), the stem workers for every back chain of their pass, the
+// rhs workers for the solve's stem workers (the stem residual), a forward chain for its columns' right-hand sides and
+// its child chains. A workgroup that holds a ticket is resident and waits only on lower tickets, so by induction every
+// wait ends: no assumption on dispatch order, co-residency or timing (the plan emulator checks the chain order:
+// tests/test_corner_plan.py). Every spin is bounded (error flag bit 8 on a timeout). With the gate shut the refinement's
+// workgroups return right after their ticket.
 //
-// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1): the handed-off vectors (x, y, the refinement
-// rhs, the corner rows of the stem's x) are stored write-through (sc1) and read with sc1 loads only, every storing wave
-// drains its stores (s_waitcnt vmcnt(0)) before the workgroup barrier behind which one lane signals (an agent-scope
-// atomic); the waiting workgroup's lane 0 polls relaxed and the other waves load after the barrier it then joins.
-// Tiles and inverses come from earlier launches (plain loads). The control words are zeroed by k_corner_invert.
+// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility, table row 1): the handed-off vectors (x, y, the stem
+// residual, the refinement rhs) are stored write-through (sc1) and read by other workgroups with sc1 loads only; every
+// storing wave drains its stores (s_waitcnt vmcnt(0)) before the workgroup barrier behind which one lane signals (an
+// agent-scope atomic); the waiting workgroup's lane 0 polls relaxed and the other waves load after the barrier it then
+// joins. A chain's own earlier columns are read back with plain loads (its own writes); the refinement's back chains use
+// their own x buffer (xp2), so no CU holds an L1 copy of a line another workgroup of the launch rewrote. Tiles and
+// inverses come from earlier launches (plain loads). The control words are zeroed by k_corner_invert.
 // ===================================================================================================================
 struct FlowArgs {
-	int phase;               // 0: back chains + stem pass; 1: the refinement step (rhs + forward + back chains + stem pass)
-	int nB, T, ld;           // chains, tile columns, permuted length
+	int refine;              // the refinement step's roles follow the solve's (mode 1)
+	int nB, T, ld, stem_wg;  // chains, tile columns, permuted length, stem workgroups per pass
 	int64_t nxout;           // 6 nc
 	unsigned* ctl;           // 2 x flow_ctl_words(nB) control words (zeroed by k_corner_invert)
 	const int4* chains;      // [nB] (back column first, column count, forward column first, parent chain or -1), root first
 	const int* fwd_need;     // [nB] columns + child chains of chain c
 	const int* col_chain;    // [T] chain of tile column J
 	const int* node_row;     // [nc] first permuted row of each corner node
-	CornerBackArgs back;     // chains unused; cb = y (phase 0: the factorization's; phase 1: fwd.yb), xout = the stem pass's corner rows
-	CornerFwdArgs fwd;       // chains unused; yb = the refinement's corner rhs -> y
+	CornerBackArgs back;     // the solve's back chains (chains unused): y = the factorization's, x -> xp, xout = st.x's corner rows
+	CornerFwdArgs fwd;       // the refinement's forward chains (chains unused): yb = its corner rhs -> y
+	CornerBackArgs back2;    // the refinement's back chains: y = fwd.yb, x -> xp2 (its own buffer), xout = st.dx's corner rows
 	FlowStem st;
 };
 constexpr unsigned FLOW_MAX_SPINS = 1u << 20;   // per wait: ~1 s of polling before the launch gives up (error bit 8)
@@ -1315,59 +1348,82 @@ __global__ __launch_bounds__(CT) void k_corner_flow(FlowArgs a) {
 	__shared__ int s_ticket;
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
 	const bool refining = a.st.gate && refine_gate_on(a.st.gate, a.st.ratio);
-	if (a.phase == 1 && !refining) return;   // gate shut: the refinement launch is empty (no ticket taken)
-	const int nB = a.nB;
-	unsigned* ctl = a.ctl + a.phase * flow_ctl_words(nB);
-	unsigned* back_done = ctl + 4;   // [nB] back chain c finished
-	unsigned* fwd_cnt = back_done + nB;   // [nB] forward chain c's columns' rhs + finished child chains
-	unsigned* fwd_done = fwd_cnt + nB;    // [nB] forward chain c (a root) finished
-	if (t == 0) s_ticket = static_cast<int>(__hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+	const int nB = a.nB, S = a.stem_wg;
+	unsigned* ctl0 = a.ctl;                        // the solve: [0] ticket, [1] back chains done, [2] stem workers done
+	unsigned* back_done0 = ctl0 + 4;               // [nB] back chain c finished
+	unsigned* ctl1 = a.ctl + flow_ctl_words(nB);   // the refinement step: [1] back chains done
+	unsigned* back_done1 = ctl1 + 4;
+	unsigned* fwd_cnt = back_done1 + nB;           // [nB] forward chain c's columns' rhs + finished child chains
+	unsigned* fwd_done = fwd_cnt + nB;             // [nB] forward chain c (a root) finished
+	if (t == 0) s_ticket = static_cast<int>(__hip_atomic_fetch_add(ctl0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 	__syncthreads();
 	int k = s_ticket;
-	if (a.phase == 1) {
-		if (k < a.T) {   // the refinement's corner right-hand side of tile column J (every node with rows in it)
-			const int J = k;
-			int seen = 0;
-			for (int r = 0; r < TILE; r++) {
-				const int rn = a.back.row_node[static_cast<int64_t>(J) * TILE + r];
-				if (rn < 0 || ((rn & 7) != 0 && r != 0)) continue;   // a node's first row, or a node entering from column J - 1
-				if ((seen++ & 3) != wave) continue;
-				const int node = rn >> 3;
-				const float v = refine_rhs_node(node, lane, a.st.n0, a.st.dinv_b, a.st.diag, a.st.inc_off, a.st.inc_list, a.st.edges, a.st.wing, a.st.rhs_b, a.st.x_base, a.st.res);
-				const int row = a.node_row[node] + lane;
-				if (lane < 6 && row >= J * TILE && row < (J + 1) * TILE) st_sc1(a.fwd.yb + row, v);
-			}
-			flow_signal(fwd_cnt + a.col_chain[J]);
-			return;
-		}
-		k -= a.T;
-		if (k < nB) {   // forward chain c, deepest first
-			const int c = nB - 1 - k;
-			const int4 ch = a.chains[c];
-			if (!flow_wait(fwd_cnt + c, static_cast<unsigned>(a.fwd_need[c]), a.st.error_flag)) return;
-			corner_fwd_chain<true>(a.fwd, make_int2(ch.z, ch.y), a.ld);
-			flow_signal(ch.w >= 0 ? fwd_cnt + ch.w : fwd_done + c);
-			return;
-		}
-		k -= nB;
-	}
-	if (k < nB) {   // back chain c, root first
+	const XSc1 x_sc1{flow_rsrc(a.st.x, 24 * static_cast<int64_t>(a.st.N))};
+	// ---- the solve: back chains (root first), then the stem pass ----
+	if (k < nB) {
 		const int4 ch = a.chains[k];
-		const unsigned* dep = ch.w >= 0 ? back_done + ch.w : a.phase == 1 ? fwd_done + k : nullptr;
-		if (dep && !flow_wait(dep, 1u, a.st.error_flag)) return;
-		if (a.phase == 1) corner_back_chain<true, true>(a.back, make_int2(ch.x, ch.y), a.ld, a.nxout);
-		else corner_back_chain<true, false>(a.back, make_int2(ch.x, ch.y), a.ld, a.nxout);
-		flow_signal(back_done + k, ctl + 1);
+		if (ch.w >= 0 && !flow_wait(back_done0 + ch.w, 1u, a.st.error_flag)) return;
+		corner_back_chain<true, false>(a.back, make_int2(ch.x, ch.y), a.ld, a.nxout);
+		flow_signal(back_done0 + k, ctl0 + 1);
 		return;
 	}
 	k -= nB;
-	// stem worker: the stem back substitution and every node's update, once the corner's x is complete
-	if (!flow_wait(ctl + 1, static_cast<unsigned>(nB), a.st.error_flag)) return;
+	if (k < S) {   // x of the stem, every node's update -- or, when the refinement runs, the stem residual for it
+		if (!flow_wait(ctl0 + 1, static_cast<unsigned>(nB), a.st.error_flag)) return;
+		const int i = k * CT + t;
+		if (i < a.st.n_update || i < a.st.n0)
+			arrow_back_node<true>(i, a.st.n0, a.st.n_update, a.st.dinv, a.st.edge_offsets, a.st.edge_list, a.st.edges, a.st.wing,
+			                      XPlain{a.st.rhs}, a.st.x, x_sc1, a.st.state_in, a.st.node_state, a.st.updates_out, nullptr, XPlain{nullptr},
+			                      a.st.mode, refining, a.st.diag, a.st.res);
+		if (a.refine) flow_signal(ctl0 + 2);
+		return;
+	}
+	k -= S;
+	if (!refining) return;   // the refinement's roles when its gate is shut
+	// ---- the refinement step: the correction's corner rhs per tile column, forward chains (deepest first), back chains
+	// (root first), the stem pass applying x + d ----
+	const XSc1 res_sc1{flow_rsrc(a.st.res, 24 * static_cast<int64_t>(a.st.N))};
+	if (k < a.T) {
+		if (!flow_wait(ctl0 + 2, static_cast<unsigned>(S), a.st.error_flag)) return;
+		const int J = k;
+		int seen = 0;
+		for (int r = 0; r < TILE; r++) {
+			const int rn = a.back.row_node[static_cast<int64_t>(J) * TILE + r];
+			if (rn < 0 || ((rn & 7) != 0 && r != 0)) continue;   // a node's first row, or a node entering from column J - 1
+			if ((seen++ & 3) != wave) continue;
+			const int node = rn >> 3;
+			const float v = refine_rhs_node(node, lane, a.st.n0, a.st.dinv_b, a.st.diag, a.st.inc_off, a.st.inc_list, a.st.edges, a.st.wing,
+			                                a.st.rhs, x_sc1, res_sc1);
+			const int row = a.node_row[node] + lane;
+			if (lane < 6 && row >= J * TILE && row < (J + 1) * TILE) st_sc1(a.fwd.yb + row, v);
+		}
+		flow_signal(fwd_cnt + a.col_chain[J]);
+		return;
+	}
+	k -= a.T;
+	if (k < nB) {
+		const int c = nB - 1 - k;
+		const int4 ch = a.chains[c];
+		if (!flow_wait(fwd_cnt + c, static_cast<unsigned>(a.fwd_need[c]), a.st.error_flag)) return;
+		corner_fwd_chain<true>(a.fwd, make_int2(ch.z, ch.y), a.ld);
+		flow_signal(ch.w >= 0 ? fwd_cnt + ch.w : fwd_done + c);
+		return;
+	}
+	k -= nB;
+	if (k < nB) {
+		const int4 ch = a.chains[k];
+		if (!flow_wait(ch.w >= 0 ? back_done1 + ch.w : fwd_done + k, 1u, a.st.error_flag)) return;
+		corner_back_chain<true, true>(a.back2, make_int2(ch.x, ch.y), a.ld, a.nxout);
+		flow_signal(back_done1 + k, ctl1 + 1);
+		return;
+	}
+	k -= nB;
+	if (!flow_wait(ctl1 + 1, static_cast<unsigned>(nB), a.st.error_flag)) return;
 	const int i = k * CT + t;
-	if (i >= a.st.n_update && i >= a.st.n0) return;
-	const XSc1 xc{flow_rsrc(a.st.x, 24 * static_cast<int64_t>(a.st.N))};
-	arrow_back_node(i, a.st.n0, a.st.n_update, a.st.dinv, a.st.edge_offsets, a.st.edge_list, a.st.edges, a.st.wing, a.st.rhs, a.st.x, xc, a.st.state_in, a.st.node_state,
-	                a.st.updates_out, a.phase == 1 ? a.st.x_base : nullptr, a.st.mode, refining, a.st.diag, a.st.res);
+	if (i >= a.st.N) return;
+	arrow_back_node<false>(i, a.st.n0, a.st.N, a.st.dinv, a.st.edge_offsets, a.st.edge_list, a.st.edges, a.st.wing, res_sc1, a.st.dx,
+	                       XSc1{flow_rsrc(a.st.dx, 24 * static_cast<int64_t>(a.st.N))}, a.st.state_in, a.st.node_state, a.st.updates_out,
+	                       a.st.x, x_sc1, 2, true, a.st.diag, nullptr);
 }
 
 // ===================================================================================================================
@@ -1620,8 +1676,10 @@ static void dev_free(void*& p) {
 	p = nullptr;
 }
 
-// development switches (A/B builds without rebuilding): NNRT_CORNER_WALK=0 disables the single-workgroup walk for small
-// corners, NNRT_CORNER_FLOW=0 the dataflow substitution launches, NNRT_CORNER_TRIM=0 the padding-trimmed eliminations
+// development switches (A/B builds without rebuilding): NNRT_CORNER_WALK=1 enables the single-workgroup walk for small
+// corners (round 4's default; the dataflow launch measured faster at C1_ARAP, 7,636 vs 7,500 GN it/s, and equal at
+// C2_ARAP in round 5), NNRT_CORNER_FLOW=0 disables the dataflow substitution launch, NNRT_CORNER_TRIM=0 the
+// padding-trimmed eliminations
 static bool env_flag(const char* name, bool dflt) {
 	const char* v = std::getenv(name);
 	return v ? std::strcmp(v, "0") != 0 : dflt;
@@ -1699,7 +1757,8 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		if ((st = alloc(tiles, p.slot_ij.size() * TILE_ELEMS)) || (st = alloc(ldiag, static_cast<size_t>(p.T) * TILE_ELEMS)) ||
 		    (st = alloc(minv, static_cast<size_t>(p.T) * TILE_ELEMS)) || (st = alloc(cb2, static_cast<size_t>(p.ld))) ||
 		    (st = alloc(sdiag, static_cast<size_t>(p.ld))) || (st = alloc(reinterpret_cast<float*&>(pivot_word), 1)) ||
-		    (st = alloc(cb, static_cast<size_t>(p.ld))) || (st = alloc(xp, static_cast<size_t>(p.ld))) || (st = alloc(zx, static_cast<size_t>(p.ld))))
+		    (st = alloc(cb, static_cast<size_t>(p.ld))) || (st = alloc(xp, static_cast<size_t>(p.ld))) || (st = alloc(xp2, static_cast<size_t>(p.ld))) ||
+		    (st = alloc(zx, static_cast<size_t>(p.ld))))
 			return fail(st);
 		if ((st = dev_upload(d_tile_slot, p.tile_slot)) || (st = dev_upload(d_slot_ij, p.slot_ij)) || (st = dev_upload(d_row_node, p.row_node)) ||
 		    (st = dev_upload(d_node_row, p.node_row)) || (st = dev_upload(d_tasks, p.tasks)) || (st = dev_upload(d_srcs, p.srcs)) ||
@@ -1714,7 +1773,7 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		}
 	}
 	walk_ok = false;
-	if (p.nc > 0 && env_flag("NNRT_CORNER_WALK", true) && p.ld <= WALK_MAX_LD && static_cast<int>(std::max(p.walk_back.size(), p.walk_fwd.size())) <= std::min(WALK_MAX_ELEMS, NNRT_WALK_MAX_TILES)) {
+	if (p.nc > 0 && env_flag("NNRT_CORNER_WALK", false) && p.ld <= WALK_MAX_LD && static_cast<int>(std::max(p.walk_back.size(), p.walk_fwd.size())) <= std::min(WALK_MAX_ELEMS, NNRT_WALK_MAX_TILES)) {
 		// LDS: descriptors, the solution vector, the reduction rows, then a ring of as many tiles as fit (at least the
 		// largest column's elements need not fit: a column streams through the ring in parts)
 		const size_t nd = std::max(p.walk_back.size(), p.walk_fwd.size());
@@ -1829,29 +1888,30 @@ nnrt_status CornerSolver::launch_factor(int* error_flag, hipStream_t s) const {
 	return NNRT_OK;
 }
 
-nnrt_status CornerSolver::launch_flow(int phase, const FlowStem& st, hipStream_t s) const {
+nnrt_status CornerSolver::launch_flow(const FlowStem& st, hipStream_t s) const {
 	if (nc == 0 || !use_flow) {
 		set_error("launch_flow without a dataflow plan");
 		return NNRT_ERROR_ARGUMENT;
 	}
 	FlowArgs a{};
-	a.phase = phase;
+	a.refine = st.mode == 1;
 	a.nB = n_chains;
 	a.T = T;
 	a.ld = ld;
+	a.stem_wg = static_cast<int>(ceil_div(std::max(std::max(st.n_update, st.n0), st.mode == 1 ? st.N : 0), CT));
 	a.nxout = 6 * static_cast<int64_t>(nc);
 	a.ctl = flow_ctl;
 	a.chains = d_flow_chains;
 	a.fwd_need = d_flow_need;
 	a.col_chain = d_col_chain;
 	a.node_row = d_node_row;
-	float* xout = st.x + 6 * static_cast<int64_t>(st.n0);
-	a.back = CornerBackArgs{nullptr, 0.f, tiles, ldiag, minv, phase == 1 ? cb2 : cb, xp, d_row_node, xout, nullptr, d_back_cols, d_back_ent, zx, 0};
+	a.back = CornerBackArgs{nullptr, 0.f, tiles, ldiag, minv, cb, xp, d_row_node, st.x + 6 * static_cast<int64_t>(st.n0), nullptr, d_back_cols,
+	                        d_back_ent, zx, 0};
 	a.fwd = CornerFwdArgs{nullptr, 0.f, tiles, ldiag, minv, cb2, nullptr, d_fwd_cols, d_fwd_ent, zx, 0};
+	a.back2 = CornerBackArgs{nullptr, 0.f, tiles, ldiag, minv, cb2, xp2, d_row_node, a.refine ? st.dx + 6 * static_cast<int64_t>(st.n0) : nullptr,
+	                         nullptr, d_back_cols, d_back_ent, zx, 0};
 	a.st = st;
-	const int stem_threads = std::max(st.n_update, st.n0);
-	const int stem_wg = static_cast<int>(ceil_div(stem_threads, CT));
-	const int grid = (phase == 1 ? T + 2 * n_chains : n_chains) + stem_wg;
+	const int grid = n_chains + a.stem_wg + (a.refine ? T + 2 * n_chains + a.stem_wg : 0);
 	k_corner_flow<<<grid, CT, 0, s>>>(a);
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;

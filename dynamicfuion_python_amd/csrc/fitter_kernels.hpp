@@ -261,18 +261,17 @@ struct WalkElem;   // corner.hip: one tile of a single-workgroup substitution wa
 
 // the stem side of a dataflow substitution launch (CornerSolver::launch_flow; arap.hip fills it)
 struct FlowStem {
-	int n0 = 0, N = 0, n_update = 0, mode = 0;   // mode: 0 plain, 1 first pass of a gated refinement, 2 the refinement's pass
+	int n0 = 0, N = 0, n_update = 0, mode = 0;   // mode: 0 plain, 1 the solve's pass of a gated refinement (the refinement follows)
 	const float *dinv = nullptr, *wing = nullptr, *diag = nullptr, *dinv_b = nullptr;
 	const int *edge_offsets = nullptr, *edge_list = nullptr, *inc_off = nullptr, *inc_list = nullptr;
 	const int32_t* edges = nullptr;
-	const float* rhs = nullptr;   // the stem pass's right-hand side (phase 0: b; phase 1: the residual)
-	float* x = nullptr;           // [6N] the pass's solution (phase 1: the correction d); its corner rows are the corner's output
+	const float* rhs = nullptr;   // b
+	float* x = nullptr;           // [6N] the solve's x (its corner rows: the corner substitution's output); x + d after a refinement
+	float* dx = nullptr;          // [6N] the refinement's correction d (mode 1)
 	const float* state_in = nullptr;
 	float* node_state = nullptr;
 	float* updates_out = nullptr;
-	float* x_base = nullptr;      // phase 1: the first pass's x (x += d; also the rhs workers' x)
-	float* res = nullptr;         // phase 0, mode 1: the stem residual (out); phase 1: the rhs workers' stem residual
-	const float* rhs_b = nullptr; // phase 1 rhs workers: b
+	float* res = nullptr;         // [6N] mode 1: the stem residual (the refinement's right-hand side)
 	const unsigned* gate = nullptr;
 	float ratio = 0.f;
 	int* error_flag = nullptr;
@@ -298,9 +297,9 @@ public:
 	// gate (nullable, device): skip unless the factorization's minimum pivot / diag(S) ratio is below refine_ratio
 	nnrt_status launch_resolve(float* xout, hipStream_t s, const unsigned* gate = nullptr, float refine_ratio = 0.f) const;
 	nnrt_status launch_back(const float* y, float* xout, hipStream_t s, const unsigned* gate, float refine_ratio) const;
-	// dataflow substitution (k_corner_flow): phase 0 = the back substitution of the last launch_factor + the stem pass,
-	// phase 1 = the gated refinement step; st.x + 6 n0 receives the corner's solution
-	nnrt_status launch_flow(int phase, const FlowStem& st, hipStream_t s) const;
+	// dataflow substitution (k_corner_flow), one launch: the back substitution of the last launch_factor + the stem pass
+	// (st.x + 6 n0 receives the corner's solution) and, with st.mode 1, the gated refinement step after them
+	nnrt_status launch_flow(const FlowStem& st, hipStream_t s) const;
 	// factor S and form the diagonal inverses (the first half of launch_solve; the flow launches do the rest)
 	nnrt_status launch_factor(int* error_flag, hipStream_t s) const;
 	bool flow_ok() const { return use_flow; }
@@ -326,6 +325,7 @@ private:
 	int nc = 0, ld = 0, T = 0, H = 0, slots = 0, n_corner_edges = 0;
 	int64_t fill_tiles = 0, dense_tiles = 0, exec_mfma_flops = 0, n_terms = 0, elim_cols = 0;
 	float *tiles = nullptr, *ldiag = nullptr, *minv = nullptr, *cb = nullptr, *cb2 = nullptr, *xp = nullptr, *sdiag = nullptr;
+	float* xp2 = nullptr;   // the refinement's back substitution in a dataflow launch (its own lines: no L1 copy of xp's)
 	float* zx = nullptr;   // [ld] substitution pre-sums (NNRT_SUBST_PRESUM)
 	int2 *d_back_pre = nullptr, *d_fwd_pre = nullptr;
 	std::vector<int> back_pre_off, fwd_pre_off;

@@ -216,6 +216,13 @@ class DeformableMeshToImageFitter:
         keys = ("corner_nodes", "tile_columns", "factor_launches", "back_launches", "stored_tiles", "dense_lower_tiles")
         return {k: int(v) for k, v in zip(keys, out)}
 
+    def warped_mesh(self, vertex_count: int, stream=None):
+        """The last iteration's warped canonical mesh (positions, normals [V,3]) as the fitter rasterized it."""
+        p = np.empty((vertex_count, 3), np.float32)
+        n = np.empty((vertex_count, 3), np.float32)
+        N.check(N.lib().nnrt_fitter_get_warped_mesh(self._h, N.ptr(p), N.ptr(n), N.stream_ptr(stream)))
+        return p, n
+
     def corner_work(self) -> dict:
         """The plan's factorization work as executed (csrc/corner.hip): MFMA flops (update-term tile products + rank-32
         products), update terms, eliminated tile columns (real columns summed)."""

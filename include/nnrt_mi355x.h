@@ -152,6 +152,9 @@ nnrt_status nnrt_fitter_corner_info(const nnrt_fitter* fitter, int64_t* h_out);
  * factorization (every update term's 64 x 64 x 64 tile product + the rank-32 products of the split eliminations),
  * update terms, tile-column eliminations (real columns summed). The reference's dense count is (6 n1)^3 / 3 + ... */
 nnrt_status nnrt_fitter_corner_work(const nnrt_fitter* fitter, int64_t* h_out);
+/* The last iteration's warped canonical mesh (diagnostic; synchronizes `stream`): h_positions / h_normals [V,3] as the
+ * fitter rasterized them (Warping.cpp:222-264 of the motion the iteration started from). */
+nnrt_status nnrt_fitter_get_warped_mesh(nnrt_fitter* fitter, float* h_positions, float* h_normals, void* stream);
 /* The last arrowhead solve's refinement gate (diagnostic; synchronizes `stream`): h_out[3] = the corner factorization's
  * smallest pivot / diag(S) ratio (1 without ARAP), the threshold below which one step of iterative refinement runs (it
  * does not below 1e-4, where one step no longer converges), and 1 if it ran. */

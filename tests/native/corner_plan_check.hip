@@ -188,9 +188,10 @@ int main(int argc, char** argv) {
 	for (int i=0;i<m;i++){ double s2 = -b2[i]; for (int j=0;j<m;j++) s2 += M[(size_t)i*m+j]*x2[j]; res2 = std::max(res2, fabs(s2)); b2max = std::max(b2max, fabs(b2[i])); }
 	printf("refinement-solve residual %.3g (|b| %.3g)\n", res2, b2max);
 	if (!(res2 < 1e-9 * b2max)) return 1;
-	// dataflow launches (k_corner_flow): tickets run [rhs of every column] [forward chains c = nB-1 .. 0] [back chains
-	// c = 0 .. nB-1]; every wait must be on a lower ticket (deadlock freedom), the counters a chain waits for must be
-	// complete exactly when everything it reads is, and executing the roles in ticket order must solve the system
+	// the dataflow launch (k_corner_flow): the refinement's tickets run [rhs of every column] [forward chains c = nB-1 .. 0]
+	// [back chains c = 0 .. nB-1] (after the solve's back chains and stem pass); every wait must be on a lower ticket
+	// (deadlock freedom), the counters a chain waits for must be complete exactly when everything it reads is, and
+	// executing the roles in ticket order must solve the system
 	{
 		const int nB = (int)p.flow_chains.size();
 		if (nB != (int)p.back_chains.size() || (int)p.flow_need.size() != nB || (int)p.col_chain.size() != T) { printf("FLOW plan size mismatch\n"); return 1; }

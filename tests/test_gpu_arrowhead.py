@@ -191,15 +191,25 @@ def test_walk_plans_of_different_lds_alternate(la):
     prepared first, the smaller one after it, then the larger one is solved again from its cached plan. The walk's LDS
     cap is a per-device kernel attribute raised once to the whole LDS budget, so the last plan prepared cannot lower it
     below what an earlier plan launches with."""
+    import os
     from dynamicfuion_python_amd.nnrt import core
     big = grid_arrowhead(12, 8, 3, True, seed=21)
     small = grid_arrowhead(2, 2, 2, False, seed=22)
-    core.release_arrowhead_plans()
-    ref_big = la.SolveBlockSparseArrowheadCholesky(*big).cpu().numpy()
-    ref_small = la.SolveBlockSparseArrowheadCholesky(*small).cpu().numpy()
-    for _ in range(2):
-        assert np.array_equal(la.SolveBlockSparseArrowheadCholesky(*big).cpu().numpy(), ref_big)
-        assert np.array_equal(la.SolveBlockSparseArrowheadCholesky(*small).cpu().numpy(), ref_small)
+    old = os.environ.get("NNRT_CORNER_WALK")
+    os.environ["NNRT_CORNER_WALK"] = "1"   # the walk is a development option since round 5 (the dataflow launch is the default)
+    try:
+        core.release_arrowhead_plans()
+        ref_big = la.SolveBlockSparseArrowheadCholesky(*big).cpu().numpy()
+        ref_small = la.SolveBlockSparseArrowheadCholesky(*small).cpu().numpy()
+        for _ in range(2):
+            assert np.array_equal(la.SolveBlockSparseArrowheadCholesky(*big).cpu().numpy(), ref_big)
+            assert np.array_equal(la.SolveBlockSparseArrowheadCholesky(*small).cpu().numpy(), ref_small)
+    finally:
+        if old is None:
+            os.environ.pop("NNRT_CORNER_WALK", None)
+        else:
+            os.environ["NNRT_CORNER_WALK"] = old
+        core.release_arrowhead_plans()
     for sy, x in ((big, ref_big), (small, ref_small)):
         x64, _ = fp64_solution(sy[0], sy[1], sy[2], sy[4])
         assert rel_err(x, x64) < 1e-5

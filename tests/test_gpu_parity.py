@@ -84,6 +84,29 @@ def test_warp_bit_exact(nn, S, oracle_mod, extrinsic):
     assert np.array_equal(wn_o, _np(m.vertex_normals))
 
 
+@pytest.mark.parametrize("name,from_identity", [("C1", False), ("C1", True), ("C2", False)])
+def test_fitter_warp_bit_exact(nn, S, oracle_mod, name, from_identity):
+    """The fitter's own warp (k_warp_mesh_mv: several 16-vertex runs per wave, canonical float4 inputs) -- the mesh an
+    iteration rasterizes -- equals the oracle's warp of the motion the iteration started from, bit for bit: from the
+    ground-truth motion (general kernel) and from the identity (iterate_from_identity's IDENTITY kernel)."""
+    sc = _scene(S, oracle_mod, name)
+    depth = scene_target(oracle_mod, sc)
+    wf, ft = _new_fit(nn, sc, depth, 1)
+    V, Nn = len(sc.points), len(sc.nodes)
+    if from_identity:
+        ft.iterate_from_identity(wf, 0, 1)
+        R0, t0 = np.tile(np.eye(3, dtype=np.float32), (Nn, 1, 1)), np.zeros((Nn, 3), np.float32)
+    else:
+        wf.set_node_rotations(sc.gt_rotations)   # original node order
+        wf.set_node_translations(sc.gt_translations)
+        R0, t0 = wf.get_node_rotations(True), wf.get_node_translations(True)
+        ft.iterate(wf, 0, 1)
+    p_g, n_g = ft.warped_mesh(V)
+    a, w = ft.anchors(V, 4)
+    p_o, n_o = oracle_mod.warp_mesh(sc.points, sc.normals, wf.get_node_positions(True), R0, t0, a, w)
+    assert np.array_equal(p_g, p_o) and np.array_equal(n_g, n_o)
+
+
 def test_ndc_extraction_bit_exact_and_fixture(nn, S, oracle_mod):
     V, N, F = xy_plane(1.2615, (0, 0, 1), 4)
     K = np.array([[580., 0., 320.], [0., 580., 240.], [0., 0., 1.]])
