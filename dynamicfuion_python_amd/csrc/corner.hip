@@ -554,43 +554,11 @@ __global__ void k_corner_offdiag(const int* __restrict__ corner_edges, int n0, c
 	atomicAdd(corner_entry(m, R, C), wing[static_cast<int64_t>(e) * 36 + t]);
 }
 
-// 32 x 32 quadrant (qr, qc) of X Y^T for 64 x 64 row-major tiles X, Y at row stride ld (lane l feeds
-// A[i = l & 31][k'] = X[32 qr + i][32 (l >> 5) + s] and B[k'][j] = Y[32 qc + j][32 (l >> 5) + s] to MFMA step s, so the 32
-// steps x 2 lane halves cover the 64-wide k range; each lane reads 32 contiguous floats). C/D map: column l & 31, row
-// (v & 3) + 8 (v >> 2) + 4 (l >> 5).
-__device__ inline f32x16 quadrant_xyt(const float* X, const float* Y, int64_t ld, int qr, int qc, int lane, f32x16 acc) {
-	const int half = lane >> 5, l32 = lane & 31;
-	const float4* x4 = reinterpret_cast<const float4*>(X + (32 * qr + l32) * ld + 32 * half);
-	const float4* y4 = reinterpret_cast<const float4*>(Y + (32 * qc + l32) * ld + 32 * half);
-	float4 vx[8], vy[8];
-#pragma unroll
-	for (int q = 0; q < 8; q++) {
-		vx[q] = x4[q];
-		vy[q] = y4[q];
-	}
-#pragma unroll
-	for (int q = 0; q < 8; q++) {
-		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].x, vy[q].x, acc, 0, 0, 0);
-		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].y, vy[q].y, acc, 0, 0, 0);
-		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].z, vy[q].z, acc, 0, 0, 0);
-		acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx[q].w, vy[q].w, acc, 0, 0, 0);
-	}
-	return acc;
-}
-
 __device__ inline int quad_row(int v, int lane) { return (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5); }
 
-// one update term's operands for this lane (quadrant_xyt's loads) and its 32 MFMA steps
-__device__ __forceinline__ void term_load(const float* tiles, int4 s, int qr, int qc, int lane, float4 (&vx)[8], float4 (&vy)[8]) {
-	const int half = lane >> 5, l32 = lane & 31;
-	const float4* x4 = reinterpret_cast<const float4*>(tiles + static_cast<int64_t>(s.x) * TILE_ELEMS + (32 * qr + l32) * TILE + 32 * half);
-	const float4* y4 = reinterpret_cast<const float4*>(tiles + static_cast<int64_t>(s.y) * TILE_ELEMS + (32 * qc + l32) * TILE + 32 * half);
-#pragma unroll
-	for (int q = 0; q < 8; q++) {
-		vx[q] = x4[q];
-		vy[q] = y4[q];
-	}
-}
+// 32 MFMA steps of quadrant (qr, qc) of X Y^T for 64 x 64 tiles: lane l feeds A[i = l & 31][k'] = X[32 qr + i][32 (l >> 5) + s]
+// and B[k'][j] = Y[32 qc + j][32 (l >> 5) + s] to step s (vx / vy: the lane's 32 contiguous floats of its X / Y row), so
+// the 32 steps x 2 lane halves cover the 64-wide k range. C/D map: column l & 31, row (v & 3) + 8 (v >> 2) + 4 (l >> 5).
 __device__ __forceinline__ f32x16 term_mfma(const float4 (&vx)[8], const float4 (&vy)[8], f32x16 acc) {
 #pragma unroll
 	for (int q = 0; q < 8; q++) {
@@ -602,30 +570,62 @@ __device__ __forceinline__ f32x16 term_mfma(const float4 (&vx)[8], const float4 
 	return acc;
 }
 
-// sum over the update terms of X Y^T for this wave's quadrant, in term order (the products of quadrant_xyt). The compiler
-// streams each term's 16 operand loads into its MFMAs (two loads, a wait, four MFMAs, ...): the 8 loads of a lane's row
-// segment touch the same 64 lines, which the first of them brings into L1. Issuing all 16 first (scheduling barriers,
-// next term double-buffered) measured slower (round 5: C5 staging 22 k -> 30 k cycles per level): the 64 lines are then
-// missed 8 times over.
-__device__ inline f32x16 sum_updates(const float* tiles, const int4* src, int n, int qr, int qc, int lane) {
-	f32x16 acc = {};
-	for (int e = 0; e < n; e++) {
-		float4 vx[8], vy[8];
-		term_load(tiles, src[e], qr, qc, lane, vx, vy);
-		acc = term_mfma(vx, vy, acc);
+// s_waitcnt vmcnt(n) for a run-time n (even values up to 62: two DMA instructions per wave per tile)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+	switch (n) {
+#define W_(k) \
+	case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+		W_(0) W_(2) W_(4) W_(6) W_(8) W_(10) W_(12) W_(14) W_(16) W_(18) W_(20) W_(22) W_(24) W_(26) W_(28) W_(30)
+		W_(32) W_(34) W_(36) W_(38) W_(40) W_(42) W_(44) W_(46) W_(48) W_(50) W_(52) W_(54) W_(56) W_(58) W_(60) W_(62)
+#undef W_
+		default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
 	}
-	return acc;
+}
+// workgroup barrier for LDS traffic only: retires this wave's LDS operations, leaves LDS-DMA loads in flight
+__device__ __forceinline__ void lds_barrier() {
+	asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+	__builtin_amdgcn_s_barrier();
 }
 
-// s_t = A - sum X Y^T for the workgroup's quadrant of the 64 x 64 tile A (LDS, row stride CS4)
-__device__ inline void stage_tile(const float* tiles, const float* A, const int4* src, int n, int wave, int lane, float* s_t) {
-	const int qr = wave >> 1, qc = wave & 1;
-	float tv[16];
+// ---- panel staging through LDS (k_corner_factor's panel tasks) ----
+// A term's operand tiles X, Y (64 x 64, row-major) arrive in LDS by LDS-DMA (global_load_lds, 16 B per lane, 1 KB per
+// instruction: every request reads whole lines), laid out with the 16-B chunks of row r XOR-swizzled by r mod 16 so that
+// the MFMA operand reads -- lane l: 32 contiguous floats of row 32 q + (l mod 32) -- fall in distinct banks; a group of
+// four waves double-buffers its terms (the next term's DMA in flight while the current term's MFMAs run). Direct loads
+// of the operands streamed them into the MFMAs one pair at a time, a memory round trip per quarter term (round 5 stamps:
+// 4.7 k cycles per term, 2 k of them MFMA; issuing all 16 loads of a term first was slower still, the 64 lines of a
+// lane group's rows then missed L1 8 times over). LDS-DMA staging: C5 staging 22 k -> 17 k cycles per level.
+typedef __attribute__((address_space(3))) void factor_lds_t;
+typedef const __attribute__((address_space(1))) void factor_global_t;
+constexpr int TERM_FLOATS = 2 * TILE_ELEMS;   // one term's X and Y
+constexpr int STAGE_WORDS = 2 * 2 * TERM_FLOATS;   // two groups x two buffers
+static_assert(2 * TILE * CS4 <= 2 * TERM_FLOATS, "the staged tiles alias the first buffers");
+// wave w (0..3) of a group: its 8 of the term's 32 pieces (4 of X, 4 of Y), swizzled
+__device__ __forceinline__ void term_dma(const float* tiles, int4 s, float* buf, int w, int lane) {
 #pragma unroll
-	for (int v = 0; v < 16; v++) tv[v] = A[(32 * qr + quad_row(v, lane)) * TILE + 32 * qc + (lane & 31)];
-	const f32x16 acc = sum_updates(tiles, src, n, qr, qc, lane);
+	for (int h = 0; h < 2; h++) {
+		const float* src = tiles + static_cast<int64_t>(h == 0 ? s.x : s.y) * TILE_ELEMS;
+		float* dst = buf + h * TILE_ELEMS;
 #pragma unroll
-	for (int v = 0; v < 16; v++) s_t[(32 * qr + quad_row(v, lane)) * CS4 + 32 * qc + (lane & 31)] = tv[v] - acc[v];
+		for (int i = 0; i < 4; i++) {
+			const int piece = 4 * w + i;                // rows 4 piece .. 4 piece + 3
+			const int r = 4 * piece + (lane >> 4);      // this lane's row and physical chunk
+			const int c = (lane & 15) ^ (r & 15);       // the logical chunk that lands there
+			__builtin_amdgcn_global_load_lds((factor_global_t*)(src + r * TILE + 4 * c), (factor_lds_t*)(dst + piece * 256), 16, 0, 0);
+		}
+	}
+}
+// the term's 32 MFMA steps for quadrant (qr, qc) from a staged (swizzled) buffer
+__device__ __forceinline__ f32x16 term_mfma_lds(const float* buf, int qr, int qc, int lane, f32x16 acc) {
+	const int half = lane >> 5, l32 = lane & 31;
+	const int rx = 32 * qr + l32, ry = 32 * qc + l32;
+	float4 vx[8], vy[8];
+#pragma unroll
+	for (int q = 0; q < 8; q++) {
+		vx[q] = *reinterpret_cast<const float4*>(buf + rx * TILE + 4 * ((8 * half + q) ^ (rx & 15)));
+		vy[q] = *reinterpret_cast<const float4*>(buf + TILE_ELEMS + ry * TILE + 4 * ((8 * half + q) ^ (ry & 15)));
+	}
+	return term_mfma(vx, vy, acc);
 }
 
 // (L y) row t >> 2 for a 64 x 64 tile L and the 64-vector y: 4 threads per row, 16 columns each (all 4 get the sum)
@@ -851,8 +851,11 @@ __global__ __launch_bounds__(CT) void k_corner_invert(const float* __restrict__ 
 //   else two 32-column halves joined by a rank-32 MFMA update on waves 1-3.
 //   trailing (blockIdx >= n_panel): A_IJ -= sum_k L_Ik L_Jk^T (and b_J -= sum_k L_Jk y_k on diagonal tiles), waves 0-3.
 __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
-	__shared__ float s_d[TILE * CS4];   // A_JJ after the previous level's updates
-	__shared__ float s_p[TILE * CS4];   // A_IJ after the previous level's updates (panel workgroups below the diagonal)
+	// the term buffers of the panel staging; then A_JJ (s_d) and A_IJ (s_p) after the previous level's updates, in the
+	// first buffers of groups 0 and 1
+	__shared__ __attribute__((aligned(16))) float s_stage[STAGE_WORDS];
+	float* const s_d = s_stage;
+	float* const s_p = s_stage + 2 * TERM_FLOATS;
 	__shared__ float s_b[TILE];         // b_J after the previous level's updates (diagonal workgroup)
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
 	CORNER_STAMP(0);
@@ -860,20 +863,36 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 	const CornerTask tk = a.tasks[blockIdx.x];
 	const int4* src = a.srcs + tk.src;
 	if (static_cast<int>(blockIdx.x) >= a.n_panel) {
-		if (wave >= 4) return;   // (no workgroup barrier follows)
-		const int qr = wave >> 1, qc = wave & 1;
-		float* C = a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS + 32 * qc + (lane & 31);
-		float cv[16];
+		// waves 0-3: the tile's quadrants, the terms double-buffered in LDS as in the panel staging; waves 4-7: b_J's
+		// terms on diagonal tiles
+		const int w4 = wave & 3, qr = w4 >> 1, qc = w4 & 1;
+		const int n_g = wave < 4 ? tk.nd : 0;
+		f32x16 acc = {};
+		if (n_g > 0) term_dma(a.tiles, src[0], s_stage, w4, lane);
+		float bs = 0.f, bv = 0.f;
+		float* bj = a.cb + static_cast<int64_t>(tk.J) * TILE;
+		const int t4 = t - 4 * 64;
+		if (wave >= 4 && tk.I == tk.J) {
+			bv = (t4 & 3) == 0 ? bj[t4 >> 2] : 0.f;
+			bs = rhs_updates(a.tiles, src, tk.nd, a.cb, t4);
+		}
+		for (int e = 0; e < tk.nd; e++) {
+			const bool more = e + 1 < n_g;
+			if (more) term_dma(a.tiles, src[e + 1], s_stage + ((e + 1) & 1) * TERM_FLOATS, w4, lane);
+			if (e < n_g) wait_vmcnt(more ? 8 : 0);
+			lds_barrier();
+			if (e < n_g) acc = term_mfma_lds(s_stage + (e & 1) * TERM_FLOATS, qr, qc, lane, acc);
+			lds_barrier();
+		}
+		if (wave < 4) {
+			float* C = a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS + 32 * qc + (lane & 31);
+			float cv[16];
 #pragma unroll
-		for (int v = 0; v < 16; v++) cv[v] = C[(32 * qr + quad_row(v, lane)) * TILE];
-		const f32x16 acc = sum_updates(a.tiles, src, tk.nd, qr, qc, lane);
+			for (int v = 0; v < 16; v++) cv[v] = C[(32 * qr + quad_row(v, lane)) * TILE];
 #pragma unroll
-		for (int v = 0; v < 16; v++) C[(32 * qr + quad_row(v, lane)) * TILE] = cv[v] - acc[v];
-		if (tk.I == tk.J) {
-			float* bj = a.cb + static_cast<int64_t>(tk.J) * TILE;
-			const float bv = (t & 3) == 0 ? bj[t >> 2] : 0.f;
-			const float s = rhs_updates(a.tiles, src, tk.nd, a.cb, t);
-			if ((t & 3) == 0) bj[t >> 2] = bv - s;
+			for (int v = 0; v < 16; v++) C[(32 * qr + quad_row(v, lane)) * TILE] = cv[v] - acc[v];
+		} else if (tk.I == tk.J && (t4 & 3) == 0) {
+			bj[t4 >> 2] = bv - bs;
 		}
 		CORNER_RT(7, 1ull << 62);
 		return;
@@ -882,14 +901,42 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 	// the gate's diag(S) entry of this lane's row, loaded now: after the elimination its latency would sit on the
 	// level's critical path
 	const float sd = diag && a.pivot_word && wave == 0 ? a.sdiag[static_cast<int64_t>(tk.J) * TILE + lane] : 0.f;
-	if (wave < 4) {
-		stage_tile(a.tiles, a.tiles + static_cast<int64_t>(tk.slot_d) * TILE_ELEMS, src, tk.nd, wave, lane, s_d);
-	} else if (!diag) {
-		stage_tile(a.tiles, a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS, src + tk.nd, tk.np, wave - 4, lane, s_p);
-	} else {
-		const int t4 = t - 4 * 64;
-		const float s = rhs_updates(a.tiles, src, tk.nd, a.cb, t4);
-		if ((t4 & 3) == 0) s_b[t4 >> 2] = a.cb[static_cast<int64_t>(tk.J) * TILE + (t4 >> 2)] - s;
+	{
+		// group 0 (waves 0-3) stages A_JJ with the nd terms, group 1 A_IJ with the np terms (the diagonal task: b_J with
+		// direct loads); one quadrant per wave, the terms double-buffered in LDS. Both groups run max(nd, np) rounds of
+		// two workgroup barriers each.
+		const int g = wave >> 2, w4 = wave & 3, qr = w4 >> 1, qc = w4 & 1;
+		const int n_g = g == 0 ? tk.nd : diag ? 0 : tk.np;
+		const int4* src_g = g == 0 ? src : src + tk.nd;
+		const int rounds = tk.nd > tk.np ? tk.nd : tk.np;
+		float* bufs = s_stage + g * 2 * TERM_FLOATS;
+		f32x16 acc = {};
+		if (n_g > 0) term_dma(a.tiles, src_g[0], bufs, w4, lane);
+		float bs = 0.f;
+		if (g == 1 && diag) {   // b_J's update terms (direct loads, L y over the same columns)
+			const int t4 = t - 4 * 64;
+			bs = rhs_updates(a.tiles, src, tk.nd, a.cb, t4);
+		}
+		for (int e = 0; e < rounds; e++) {
+			const bool more = e + 1 < n_g;
+			if (more) term_dma(a.tiles, src_g[e + 1], bufs + ((e + 1) & 1) * TERM_FLOATS, w4, lane);
+			if (e < n_g) wait_vmcnt(more ? 8 : 0);   // this wave's pieces of term e have landed
+			lds_barrier();                           // every wave's have
+			if (e < n_g) acc = term_mfma_lds(bufs + (e & 1) * TERM_FLOATS, qr, qc, lane, acc);
+			lds_barrier();                           // term e's buffer is read: round e + 1 refills it
+		}
+		const float* A = a.tiles + static_cast<int64_t>(g == 0 ? tk.slot_d : tk.slot_t) * TILE_ELEMS;
+		if (g == 0 || !diag) {   // s_t = A - sum of the terms (the quadrant of term_mfma's C / D layout)
+			float* s_t = g == 0 ? s_d : s_p;
+			float tv[16];
+#pragma unroll
+			for (int v = 0; v < 16; v++) tv[v] = A[(32 * qr + quad_row(v, lane)) * TILE + 32 * qc + (lane & 31)];
+#pragma unroll
+			for (int v = 0; v < 16; v++) s_t[(32 * qr + quad_row(v, lane)) * CS4 + 32 * qc + (lane & 31)] = tv[v] - acc[v];
+		} else {
+			const int t4 = t - 4 * 64;
+			if ((t4 & 3) == 0) s_b[t4 >> 2] = a.cb[static_cast<int64_t>(tk.J) * TILE + (t4 >> 2)] - bs;
+		}
 	}
 	__syncthreads();
 	CORNER_STAMP(1);
@@ -1463,23 +1510,6 @@ struct CornerWalkArgs {
 
 typedef __attribute__((address_space(3))) void walk_lds_t;
 typedef const __attribute__((address_space(1))) void walk_global_t;
-
-// s_waitcnt vmcnt(n) for a run-time n (even values up to 62: two DMA instructions per wave per tile)
-__device__ __forceinline__ void wait_vmcnt(int n) {
-	switch (n) {
-#define W_(k) \
-	case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-		W_(0) W_(2) W_(4) W_(6) W_(8) W_(10) W_(12) W_(14) W_(16) W_(18) W_(20) W_(22) W_(24) W_(26) W_(28) W_(30)
-		W_(32) W_(34) W_(36) W_(38) W_(40) W_(42) W_(44) W_(46) W_(48) W_(50) W_(52) W_(54) W_(56) W_(58) W_(60) W_(62)
-#undef W_
-		default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-	}
-}
-// workgroup barrier for LDS traffic only: retires this wave's LDS operations, leaves LDS-DMA loads in flight
-__device__ __forceinline__ void lds_barrier() {
-	asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-	__builtin_amdgcn_s_barrier();
-}
 
 // one pass over a stream; x (LDS, ld floats) holds the right-hand side on entry and the solution on exit
 template <bool BACK>
