@@ -777,6 +777,13 @@ struct CornerFactorArgs {
 	int level;
 	const float* sdiag;      // [ld] diag(S) before the factorization (nullable)
 	unsigned* pivot_word;    // atomic minimum of pivot / diag(S) over the diagonal tasks (nullable)
+	// the last level's launch (fold_invert: no k_corner_invert launch): its diagonal tasks invert their own tile after
+	// the elimination, and n_inv extra workgroups (blockIdx >= n_tasks) invert the earlier levels' tiles inv_cols[.]
+	int n_tasks, n_inv, invert_self;
+	const int* inv_cols;
+	float* minv;             // [T, 64, 64] M = L_JJ^-1
+	unsigned* flow_ctl;      // zeroed by block 0 (the dataflow substitution's control words; nullable)
+	int n_ctl;
 };
 
 // M = L^-1 for the 64 x 64 lower-triangular factor L (row-major lower part; the staging zeroes the part above the diagonal) in LDS. Forward
@@ -789,25 +796,22 @@ __device__ __forceinline__ float quad_xor(float v, int ctrl_sel) {   // 0: lanes
 	return __builtin_bit_cast(float, ctrl_sel == 0 ? __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xf, 0xf, false)
 	                                               : __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xf, 0xf, false));
 }
-// (workgroup 0 also zeroes the control words of the dataflow substitution launches that follow: k_corner_flow)
-__global__ __launch_bounds__(CT) void k_corner_invert(const float* __restrict__ ldiag, float* __restrict__ minv, unsigned* __restrict__ flow_ctl,
-                                                     int n_ctl) {
-	__shared__ __attribute__((aligned(16))) float s_l[TILE * CS4];
-	__shared__ float s_y[TILE];
-	const int t = threadIdx.x;
-	const int64_t J = blockIdx.x;
-	if (J == 0)
-		for (int i = t; i < n_ctl; i += CT) flow_ctl[i] = 0u;
-	const float4* L4 = reinterpret_cast<const float4*>(ldiag + J * TILE_ELEMS);
-	for (int i = t; i < TILE_ELEMS / 4; i += CT) {   // the lower part; zeros above the diagonal
+// the lower part of the row-major tile L (global) into s_l (row stride CS4), zeros above the diagonal; nt threads
+__device__ __forceinline__ void lower_to_lds(const float* L, float* s_l, int t, int nt) {
+	const float4* L4 = reinterpret_cast<const float4*>(L);
+	for (int i = t; i < TILE_ELEMS / 4; i += nt) {
 		const int r = i >> 4, c0 = 4 * (i & 15);
 		const float4 v = L4[i];
 		*reinterpret_cast<float4*>(s_l + r * CS4 + c0) =
 		    make_float4(c0 <= r ? v.x : 0.f, c0 + 1 <= r ? v.y : 0.f, c0 + 2 <= r ? v.z : 0.f, c0 + 3 <= r ? v.w : 0.f);
 	}
-	__syncthreads();
+}
+// M = L^-1 from s_l (written and made visible by the caller); s_y: 64 floats of scratch LDS. Every thread of the
+// workgroup calls it (one barrier inside); threads t < CT (four waves) compute and store M.
+__device__ __forceinline__ void invert_lower_lds(const float* s_l, float* s_y, float* __restrict__ M, int t) {
 	if (t < TILE) s_y[t] = 1.f / s_l[t * CS4 + t];
 	__syncthreads();
+	if (t >= CT) return;
 	const int lane = t & 63, c = 16 * (t >> 6) + (lane >> 2), q = lane & 3;
 	float m[TILE / 4];   // m[i] = M[4 i + q][c]
 #pragma unroll
@@ -836,9 +840,22 @@ __global__ __launch_bounds__(CT) void k_corner_invert(const float* __restrict__ 
 		const float v = ((c == r ? 1.f : 0.f) - part) * s_y[r];
 		m[r >> 2] = q == (r & 3) ? v : m[r >> 2];
 	}
-	float* M = minv + J * TILE_ELEMS;
 #pragma unroll
 	for (int i = 0; i < TILE / 4; i++) M[(4 * i + q) * TILE + c] = m[i];
+}
+
+// (workgroup 0 also zeroes the control words of the dataflow substitution launches that follow: k_corner_flow)
+__global__ __launch_bounds__(CT) void k_corner_invert(const float* __restrict__ ldiag, float* __restrict__ minv, unsigned* __restrict__ flow_ctl,
+                                                     int n_ctl) {
+	__shared__ __attribute__((aligned(16))) float s_l[TILE * CS4];
+	__shared__ float s_y[TILE];
+	const int t = threadIdx.x;
+	const int64_t J = blockIdx.x;
+	if (J == 0)
+		for (int i = t; i < n_ctl; i += CT) flow_ctl[i] = 0u;
+	lower_to_lds(ldiag + J * TILE_ELEMS, s_l, t, CT);
+	__syncthreads();
+	invert_lower_lds(s_l, s_y, minv + J * TILE_ELEMS, t);
 }
 
 // One launch per level of the tile elimination tree; workgroups of 8 waves (CTF threads).
@@ -860,6 +877,15 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
 	CORNER_STAMP(0);
 	CORNER_RT(6, 0ull);
+	if (a.flow_ctl && blockIdx.x == 0)
+		for (int i = t; i < a.n_ctl; i += CTF) a.flow_ctl[i] = 0u;
+	if (static_cast<int>(blockIdx.x) >= a.n_tasks) {   // an earlier level's diagonal inverse (the last launch's extra workgroups)
+		const int64_t J = a.inv_cols[blockIdx.x - a.n_tasks];
+		lower_to_lds(a.ldiag + J * TILE_ELEMS, s_stage, t, CTF);
+		__syncthreads();
+		invert_lower_lds(s_stage, s_b, a.minv + J * TILE_ELEMS, t);
+		return;
+	}
 	const CornerTask tk = a.tasks[blockIdx.x];
 	const int4* src = a.srcs + tk.src;
 	if (static_cast<int>(blockIdx.x) >= a.n_panel) {
@@ -998,7 +1024,9 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 	}
 	__syncthreads();
 	}
-	if (wave != 0) return;
+	const bool self_inv = diag && a.invert_self;   // the last level's diagonal tasks invert their own tile (all waves)
+	if (wave != 0 && !self_inv) return;
+	if (wave == 0) {
 	if (full) {
 #pragma unroll
 		for (int q = TILE / 8; q < TILE / 4; q++) {
@@ -1014,14 +1042,17 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 	}
 	CORNER_STAMP(4);
 	if (diag) {
-		// the rows as eliminated (the part above the diagonal is not meaningful: k_corner_invert reads the lower part only);
-		// a copy in LDS (s_d is this wave's alone now) gives each lane its diagonal entry without a 64-way select
+		// the rows as eliminated (the part above the diagonal is not meaningful: the inverse reads the lower part only);
+		// a copy in LDS with zeros above the diagonal (s_d is this wave's alone now) gives each lane its diagonal entry
+		// without a 64-way select, and is the inverse's input (lower_to_lds's layout)
 		float4* wa = reinterpret_cast<float4*>(a.ldiag + static_cast<int64_t>(tk.J) * TILE_ELEMS + lane * TILE);
 #pragma unroll
 		for (int q = 0; q < TILE / 4; q++) {
 			const float4 v = make_float4(ap[4 * q].x, ap[4 * q + 1].x, ap[4 * q + 2].x, ap[4 * q + 3].x);
 			wa[q] = v;
-			*reinterpret_cast<float4*>(s_d + lane * CS4 + 4 * q) = v;
+			const int c0 = 4 * q;
+			*reinterpret_cast<float4*>(s_d + lane * CS4 + 4 * q) =
+			    make_float4(c0 <= lane ? v.x : 0.f, c0 + 1 <= lane ? v.y : 0.f, c0 + 2 <= lane ? v.z : 0.f, c0 + 3 <= lane ? v.w : 0.f);
 		}
 		if (a.pivot_word) {   // the refinement gate: min over the tile of pivot (L_jj^2) / diag(S)_jj
 			const float ljj = s_d[lane * CS4 + lane];
@@ -1043,6 +1074,11 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 	}
 	CORNER_STAMP(5);
 	CORNER_RT(7, 0ull);
+	}   // wave 0
+	if (self_inv) {
+		__syncthreads();   // s_d: L_JJ, zeros above the diagonal
+		invert_lower_lds(s_d, s_b, a.minv + static_cast<int64_t>(tk.J) * TILE_ELEMS, t);
+	}
 }
 
 struct CornerBackArgs {
@@ -1744,9 +1780,11 @@ void CornerSolver::release() {
 	                 reinterpret_cast<void**>(&d_srcs), reinterpret_cast<void**>(&d_back_cols), reinterpret_cast<void**>(&d_back_ent), reinterpret_cast<void**>(&d_back_chains),
 	                 reinterpret_cast<void**>(&d_corner_edges), reinterpret_cast<void**>(&zx), reinterpret_cast<void**>(&d_back_pre),
 	                 reinterpret_cast<void**>(&d_fwd_pre), reinterpret_cast<void**>(&d_flow_chains), reinterpret_cast<void**>(&d_flow_need),
-	                 reinterpret_cast<void**>(&d_col_chain), reinterpret_cast<void**>(&flow_ctl)})
+	                 reinterpret_cast<void**>(&d_col_chain), reinterpret_cast<void**>(&flow_ctl), reinterpret_cast<void**>(&d_inv_cols)})
 		dev_free(*p);
 	use_flow = false;
+	fold_invert = false;
+	n_inv_cols = 0;
 	n_chains = n_flow_ctl = 0;
 	back_pre_off.clear();
 	fwd_pre_off.clear();
@@ -1864,6 +1902,21 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 				if (tk.I == tk.J) elim_cols += tk.nreal;
 			}
 		dense_tiles = static_cast<int64_t>(corner_ld(6 * nc) / TILE) * (corner_ld(6 * nc) / TILE + 1) / 2;
+		// the diagonal inverses ride in the last factor launch: its diagonal tasks invert their own tile, extra workgroups
+		// the other levels' (NNRT_CORNER_FOLD_INV=0: one k_corner_invert launch after the factorization)
+		fold_invert = env_flag("NNRT_CORNER_FOLD_INV", true);
+		if (fold_invert) {
+			const size_t l0 = static_cast<size_t>(p.level_off[static_cast<size_t>(p.H) - 1]);
+			std::vector<char> last(static_cast<size_t>(p.T), 0);
+			for (size_t q = l0; q < l0 + static_cast<size_t>(p.level_panel[static_cast<size_t>(p.H) - 1]); q++)
+				if (p.tasks[q].I == p.tasks[q].J) last[static_cast<size_t>(p.tasks[q].J)] = 1;
+			std::vector<int> cols;
+			for (int J = 0; J < p.T; J++)
+				if (!last[static_cast<size_t>(J)]) cols.push_back(J);
+			n_inv_cols = static_cast<int>(cols.size());
+			nnrt_status st;
+			if (!cols.empty() && (st = dev_upload(d_inv_cols, cols))) return fail(st);
+		}
 	}
 	key.swap(k);
 	return NNRT_OK;
@@ -1903,18 +1956,35 @@ nnrt_status CornerSolver::launch_solve(float* xout, int* error_flag, hipStream_t
 
 nnrt_status CornerSolver::launch_factor(int* error_flag, hipStream_t s) const {
 	if (nc == 0) return NNRT_OK;
-	CornerFactorArgs fa{tiles, ldiag, cb, nullptr, d_srcs, 0, error_flag, 0, sdiag, pivot_word};
+	CornerFactorArgs fa{};
+	fa.tiles = tiles;
+	fa.ldiag = ldiag;
+	fa.cb = cb;
+	fa.srcs = d_srcs;
+	fa.error_flag = error_flag;
+	fa.sdiag = sdiag;
+	fa.pivot_word = pivot_word;
+	fa.minv = minv;
+	fa.inv_cols = d_inv_cols;
 	for (int l = 0; l < H; l++) {
 		fa.level = l;
 		const int n = level_off[static_cast<size_t>(l) + 1] - level_off[static_cast<size_t>(l)];
 		fa.tasks = d_tasks + level_off[static_cast<size_t>(l)];
 		fa.n_panel = level_panel[static_cast<size_t>(l)];
-		k_corner_factor<<<n, CTF, 0, s>>>(fa);
+		fa.n_tasks = n;
+		const bool last = fold_invert && l == H - 1;
+		fa.n_inv = last ? n_inv_cols : 0;
+		fa.invert_self = last ? 1 : 0;
+		fa.flow_ctl = last ? flow_ctl : nullptr;
+		fa.n_ctl = last ? n_flow_ctl : 0;
+		k_corner_factor<<<n + fa.n_inv, CTF, 0, s>>>(fa);
 		NNRT_LAUNCH_CHECK();
 	}
-	// every diagonal factor's inverse, one workgroup per tile column (the substitutions multiply by them)
-	k_corner_invert<<<T, CT, 0, s>>>(ldiag, minv, flow_ctl, n_flow_ctl);
-	NNRT_LAUNCH_CHECK();
+	if (!fold_invert) {
+		// every diagonal factor's inverse, one workgroup per tile column (the substitutions multiply by them)
+		k_corner_invert<<<T, CT, 0, s>>>(ldiag, minv, flow_ctl, n_flow_ctl);
+		NNRT_LAUNCH_CHECK();
+	}
 	return NNRT_OK;
 }
 

@@ -340,6 +340,9 @@ private:
 	int4* d_flow_chains = nullptr;
 	int *d_flow_need = nullptr, *d_col_chain = nullptr;
 	unsigned* flow_ctl = nullptr;
+	bool fold_invert = false;   // the diagonal inverses in the last factor launch (no k_corner_invert launch)
+	int n_inv_cols = 0;         // tile columns inverted by that launch's extra workgroups
+	int* d_inv_cols = nullptr;
 	int walk_ring = 0, walk_lds = 0, n_walk_back = 0, n_walk_fwd = 0;
 	WalkElem* d_walk_back = nullptr;
 	WalkElem* d_walk_fwd = nullptr;

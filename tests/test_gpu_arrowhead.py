@@ -219,17 +219,19 @@ def test_walk_plans_of_different_lds_alternate(la):
 def test_flow_matches_chain_launches(la, cx, cy, spc, corner_edges):
     """The dataflow substitution launch (k_corner_flow: every back-substitution chain and the stem pass in one launch,
     dependencies through ticket-ordered counters) against the per-depth chain launches: bit-identical solutions (the same
-    float operations), for a C5-sized corner, a small one with corner-corner blocks and the 38,400-unknown corner; the
-    flow solve repeated three times under two concurrent streams gives the same bits every time."""
+    float operations; with the diagonal inverses formed in the last factor launch against a k_corner_invert launch), for a
+    C5-sized corner, a small one with corner-corner blocks and the 38,400-unknown corner; the flow solve repeated three
+    times under two concurrent streams gives the same bits every time."""
     import os
     from dynamicfuion_python_amd.nnrt import core
     sy = grid_arrowhead(cx, cy, spc, corner_edges, seed=cx + cy)
-    old = {k: os.environ.get(k) for k in ("NNRT_CORNER_FLOW", "NNRT_CORNER_WALK")}
+    old = {k: os.environ.get(k) for k in ("NNRT_CORNER_FLOW", "NNRT_CORNER_WALK", "NNRT_CORNER_FOLD_INV")}
     try:
         os.environ["NNRT_CORNER_WALK"] = "0"
         xs = {}
         for flow in ("0", "1"):
             os.environ["NNRT_CORNER_FLOW"] = flow
+            os.environ["NNRT_CORNER_FOLD_INV"] = flow   # the diagonal inverses in the last factor launch or their own
             core.release_arrowhead_plans()
             xs[flow] = la.SolveBlockSparseArrowheadCholesky(*sy).cpu().numpy()
         assert np.array_equal(xs["0"], xs["1"])

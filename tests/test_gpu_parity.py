@@ -673,18 +673,20 @@ def test_flow_substitution_matches_chain_launches(nn, S, oracle_mod, name, walk)
     along three GN iterations with the refinement forced open wherever the gate's floor allows (and once shut), updates,
     node motion and gate words are bit-identical between fitters planned with NNRT_CORNER_FLOW=1 and =0 (with
     NNRT_CORNER_TRIM=1 / 0: eliminations stopped at a tile's real columns against full 64-column ones;
+    NNRT_CORNER_FOLD_INV=1 / 0: the diagonal inverses formed in the last factor launch against a k_corner_invert launch;
     NNRT_CORNER_WALK=0 makes the small C1 / C2 corners use chains instead of the single-workgroup walk)."""
     import os
     sc = _scene(S, oracle_mod, name)
     depth = scene_target(oracle_mod, sc)
     N = len(sc.nodes)
     runs = {}
-    old = {k: os.environ.get(k) for k in ("NNRT_CORNER_FLOW", "NNRT_CORNER_WALK", "NNRT_CORNER_TRIM")}
+    old = {k: os.environ.get(k) for k in ("NNRT_CORNER_FLOW", "NNRT_CORNER_WALK", "NNRT_CORNER_TRIM", "NNRT_CORNER_FOLD_INV")}
     try:
         os.environ["NNRT_CORNER_WALK"] = walk
         for flow in ("1", "0"):
             os.environ["NNRT_CORNER_FLOW"] = flow
             os.environ["NNRT_CORNER_TRIM"] = flow   # the padding-trimmed eliminations change no bit either
+            os.environ["NNRT_CORNER_FOLD_INV"] = flow   # nor the inverses' launch
             wf, ft = _new_fit(nn, sc, depth, 3)
             rows = []
             for k, ratio in enumerate((np.inf, 0.0, np.inf)):
