@@ -59,6 +59,21 @@ int main(int argc, char** argv) {
 		printf("back %zu: chains %3d columns %3d longest chain %3d entries/col max %3d total %4d in-chain %4d; heaviest chain %d tiles (%d on the chain's path)\n", l,
 		       p.back_off[l + 1] - p.back_off[l], totcols, maxlen, maxent, sument, inchain, maxchain_tiles, maxchain_inner);
 	}
-	// the longest root-to-leaf path: columns and entries along it
+	// the dataflow launch's critical path (k_corner_flow): a back chain starts when its parent chain ends; per chain its
+	// columns and entry tiles, the deepest path in columns and entries
+	{
+		const int nB = static_cast<int>(p.flow_chains.size());
+		std::vector<int> depth_cols(nB, 0), depth_ent(nB, 0);
+		int best = 0, best_ent = 0;
+		for (int c = 0; c < nB; c++) {   // root first: a parent precedes its children
+			const int4 ch = p.flow_chains[c];
+			int ent = 0;
+			for (int q = 0; q < ch.y; q++) ent += p.back_cols[ch.x + q].z;
+			depth_cols[c] = ch.y + (ch.w >= 0 ? depth_cols[ch.w] : 0);
+			depth_ent[c] = ent + (ch.w >= 0 ? depth_ent[ch.w] : 0);
+			if (depth_cols[c] > best) { best = depth_cols[c]; best_ent = depth_ent[c]; }
+		}
+		printf("flow: chains %d, critical path %d columns with %d entry tiles\n", nB, best, best_ent);
+	}
 	return 0;
 }
