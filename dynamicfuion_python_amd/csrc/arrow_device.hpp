@@ -144,6 +144,71 @@ __device__ __forceinline__ void stem_solve(int i, const float* __restrict__ dinv
 	}
 }
 
+// The part of a stem row's back substitution that does not depend on the corner solution, done while a dataflow stem
+// worker waits for the corner (k_corner_flow): the row's edge and corner-node indices into registers, and one load
+// from every 64-B line the row reads after the wait (wing blocks, D_i^-1, b_i, the node state) so those lines are in
+// L2 by then. n = -1: more than STEM_PRE_EDGES edges (the caller takes stem_solve).
+constexpr int STEM_PRE_EDGES = 8;
+struct StemPre {
+	int n;
+	int e[STEM_PRE_EDGES], j[STEM_PRE_EDGES];
+};
+__device__ __forceinline__ void touch_lines(const float* p, int floats) {   // one load per 64-B line, kept by an empty asm
+	for (int q = 0; q < floats; q += 16) {
+		const float v = p[q];
+		asm volatile("" ::"v"(v));
+	}
+}
+__device__ __forceinline__ StemPre stem_prefetch(int i, const float* __restrict__ dinv, const int* __restrict__ edge_offsets,
+                                                 const int* __restrict__ edge_list, const int32_t* __restrict__ edges,
+                                                 const float* __restrict__ wing, const float* rhs, const float* state_in) {
+	StemPre pre;
+	const int beg = edge_offsets[i], end = edge_offsets[i + 1];
+	pre.n = end - beg <= STEM_PRE_EDGES ? end - beg : -1;
+#pragma unroll
+	for (int q = 0; q < STEM_PRE_EDGES; q++) {
+		const bool ok = q < pre.n;
+		const int e = ok ? edge_list[beg + q] : 0;
+		pre.e[q] = e;
+		pre.j[q] = ok ? edges[2 * e + 1] : 0;
+		if (ok) touch_lines(wing + static_cast<int64_t>(e) * 36, 36);
+	}
+	touch_lines(dinv + static_cast<int64_t>(i) * 36, 36);
+	touch_lines(rhs + 6 * static_cast<int64_t>(i), 6);
+	if (state_in) touch_lines(state_in + static_cast<int64_t>(i) * NODE_STRIDE, NODE_STRIDE);
+	return pre;
+}
+// stem_solve with the row's indices from stem_prefetch: the same arithmetic in the same order (bit-identical)
+template <class RL, class XL>
+__device__ __forceinline__ void stem_solve_pre(int i, const StemPre& pre, const float* __restrict__ dinv, const float* __restrict__ wing,
+                                               const RL& rhs, const XL& x, float (&o)[6]) {
+	float r6[6];
+	rhs.ld6(i, r6);
+#pragma unroll
+	for (int q = 0; q < STEM_PRE_EDGES; q++) {   // constant indices: pre stays in registers
+		if (q >= pre.n) break;
+		float B[36], xj[6];
+		load36(wing + static_cast<int64_t>(pre.e[q]) * 36, B);
+		x.ld6(pre.j[q], xj);
+#pragma unroll
+		for (int r = 0; r < 6; r++) {
+			float acc = 0.f;
+#pragma unroll
+			for (int k = 0; k < 6; k++) acc += B[6 * r + k] * xj[k];
+			r6[r] -= acc;
+		}
+	}
+	float D[36];
+	load36(dinv + static_cast<int64_t>(i) * 36, D);
+#pragma unroll
+	for (int r = 0; r < 6; r++) {
+		float acc = 0.f;
+#pragma unroll
+		for (int k = 0; k < 6; k++) acc += D[6 * r + k] * r6[k];
+		o[r] = acc;
+	}
+}
+
 // residual of stem row i, rhs_i - D_i x_i - sum over its edges of B_e x_j, the products and sums in double, rounded once
 // (D_i: the prepared diagonal block with LM; stem nodes couple to corner nodes only)
 template <class RL, class XL>

@@ -1081,6 +1081,22 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 	}
 }
 
+// development timing build only (-DNNRT_CORNER_STAMPS): per role of the dataflow launch (its ticket), the constant-rate
+// clock at its start, the end of its wait and its end ([64]), and per back-chain column q < 64: its start, the end of
+// its entry sums, the end of x = M^T z and its end, read back by nnrt_dev_flow_stamps (tools/dev/flow_stamps.py)
+#ifdef NNRT_CORNER_STAMPS
+__device__ unsigned long long g_flow_stamps[128][66][4];
+__shared__ int s_flow_row;
+#define FLOW_RT(row, col, i)                                                                                            \
+	do {                                                                                                                \
+		if (threadIdx.x == 0 && (row) >= 0 && (row) < 128 && (col) < 66) g_flow_stamps[row][col][i] = __builtin_amdgcn_s_memrealtime(); \
+	} while (0)
+#else
+#define FLOW_RT(row, col, i) \
+	do {                     \
+	} while (0)
+#endif
+
 struct CornerBackArgs {
 	const unsigned* gate;    // nullable: run only if the pivot ratio word is below ratio (the refinement pass)
 	float ratio;
@@ -1172,6 +1188,10 @@ __device__ __forceinline__ void corner_back_chain(const CornerBackArgs& a, int2 
 		}
 		__syncthreads();
 		for (int q = 0; q < nq; q++) {
+#ifdef NNRT_CORNER_STAMPS
+			const int srow = SC1X ? s_flow_row : -1;
+#endif
+			FLOW_RT(srow, q0 + q, 0);
 			const int4 col = s_cols[q];
 			const int J = col.x;
 			const int2 sp = subst_span(col, a.mode);
@@ -1226,6 +1246,7 @@ __device__ __forceinline__ void corner_back_chain(const CornerBackArgs& a, int2 
 				acc[i] += __shfl_xor(acc[i], 32);
 			}
 			if (lane < 16) *reinterpret_cast<float4*>(&s_part[wave][4 * lane]) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+			FLOW_RT(srow, q0 + q, 1);
 			__syncthreads();   // also retires the M tile's LDS-DMA pieces of every wave
 			if (wave == 0 && a.mode == 1) {
 				a.zx[static_cast<int64_t>(J) * TILE + lane] = yv - ((s_part[0][lane] + s_part[1][lane]) + (s_part[2][lane] + s_part[3][lane]));
@@ -1242,6 +1263,7 @@ __device__ __forceinline__ void corner_back_chain(const CornerBackArgs& a, int2 
 				s_xq[wave][lane] = xs[0] + xs[1];
 			}
 			if (a.mode != 1) {
+				FLOW_RT(srow, q0 + q, 2);
 				__syncthreads();   // the quarters of x_J
 				if (wave == 0) {
 					const float x = (s_xq[0][lane] + s_xq[1][lane]) + (s_xq[2][lane] + s_xq[3][lane]);
@@ -1253,6 +1275,7 @@ __device__ __forceinline__ void corner_back_chain(const CornerBackArgs& a, int2 
 			}
 			if (wave == 1 && has_next) s_ent[(q + 1) & 1][lane] = nxt;
 			__syncthreads();   // x_J visible to the chain's next column; s_part, s_xq, s_m free; the next column's entries staged
+			FLOW_RT(srow, q0 + q, 3);
 		}
 	}
 }
@@ -1441,24 +1464,47 @@ __global__ __launch_bounds__(CT) void k_corner_flow(FlowArgs a) {
 	if (t == 0) s_ticket = static_cast<int>(__hip_atomic_fetch_add(ctl0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 	__syncthreads();
 	int k = s_ticket;
+#ifdef NNRT_CORNER_STAMPS
+	if (t == 0) s_flow_row = k;
+	__syncthreads();
+#endif
+	FLOW_RT(k, 64, 0);
 	const XSc1 x_sc1{flow_rsrc(a.st.x, 24 * static_cast<int64_t>(a.st.N))};
 	// ---- the solve: back chains (root first), then the stem pass ----
 	if (k < nB) {
 		const int4 ch = a.chains[k];
 		if (ch.w >= 0 && !flow_wait(back_done0 + ch.w, 1u, a.st.error_flag)) return;
+		FLOW_RT(k, 64, 1);
 		corner_back_chain<true, false>(a.back, make_int2(ch.x, ch.y), a.ld, a.nxout);
 		flow_signal(back_done0 + k, ctl0 + 1);
+		FLOW_RT(k, 64, 2);
 		return;
 	}
 	k -= nB;
 	if (k < S) {   // x of the stem, every node's update -- or, when the refinement runs, the stem residual for it
-		if (!flow_wait(ctl0 + 1, static_cast<unsigned>(nB), a.st.error_flag)) return;
 		const int i = k * CT + t;
-		if (i < a.st.n_update || i < a.st.n0)
+		const bool live = i < a.st.n_update || i < a.st.n0;
+		// while the corner chains run: the stem row's indices, and every line it reads after the wait pulled into L2
+		// (the refinement's residual pass keeps the general path)
+		StemPre pre{};
+		pre.n = -1;
+		if (live && !refining) {
+			if (i < a.st.n0) pre = stem_prefetch(i, a.st.dinv, a.st.edge_offsets, a.st.edge_list, a.st.edges, a.st.wing, a.st.rhs, a.st.node_state ? a.st.state_in : nullptr);
+			else if (a.st.node_state) touch_lines(a.st.state_in + static_cast<int64_t>(i) * NODE_STRIDE, NODE_STRIDE);
+		}
+		if (!flow_wait(ctl0 + 1, static_cast<unsigned>(nB), a.st.error_flag)) return;
+		FLOW_RT(k + nB, 64, 1);
+		if (live && i < a.st.n0 && pre.n >= 0) {   // arrow_back_node's stem path (mode 0, or mode 1 with the gate shut)
+			float o[6];
+			stem_solve_pre(i, pre, a.st.dinv, a.st.wing, XPlain{a.st.rhs}, x_sc1, o);
+			store6<true>(a.st.x + 6 * static_cast<int64_t>(i), o);
+			if (a.st.node_state) arrow_update_node(i, o, a.st.state_in, a.st.node_state, a.st.updates_out);
+		} else if (live)
 			arrow_back_node<true>(i, a.st.n0, a.st.n_update, a.st.dinv, a.st.edge_offsets, a.st.edge_list, a.st.edges, a.st.wing,
 			                      XPlain{a.st.rhs}, a.st.x, x_sc1, a.st.state_in, a.st.node_state, a.st.updates_out, nullptr, XPlain{nullptr},
 			                      a.st.mode, refining, a.st.diag, a.st.res);
 		if (a.refine) flow_signal(ctl0 + 2);
+		FLOW_RT(k + nB, 64, 2);
 		return;
 	}
 	k -= S;
@@ -2064,6 +2110,9 @@ nnrt_status CornerSolver::launch_resolve(float* xout, hipStream_t s, const unsig
 }
 
 #ifdef NNRT_CORNER_STAMPS
+extern "C" int nnrt_dev_flow_stamps(unsigned long long* out) {   // [128][66][4] stamps of the last dataflow launch
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_flow_stamps), sizeof(unsigned long long) * 128 * 66 * 4) == hipSuccess ? 0 : 1;
+}
 extern "C" int nnrt_dev_corner_stamps(unsigned long long* out) {   // [64][512][8] stamps of the last solve
 	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_corner_stamps), sizeof(unsigned long long) * 64 * 512 * 8) == hipSuccess ? 0 : 1;
 }

@@ -256,6 +256,16 @@ extern "C" int nnrt_dev_warp_stamps(unsigned long long* out) {
 }
 #endif
 
+// workgroups per launch, the quads strided over them (development; round 5: a cap of 1024 / 2048 -- every wave
+// resident, looping -- measured 74.0 / 67.8 µs at C3 against 62.4 µs with one quad step per lane)
+#ifndef NNRT_WARP_MAX_WGS
+#define NNRT_WARP_MAX_WGS (int64_t{1} << 40)
+#endif
+constexpr int64_t WARP_MAX_WGS = NNRT_WARP_MAX_WGS;
+#ifndef NNRT_WARP_UNROLL
+#define NNRT_WARP_UNROLL 1
+#endif
+constexpr int WARP_UNROLL = NNRT_WARP_UNROLL;
 template <bool IDENTITY>
 __global__ __launch_bounds__(256) void k_warp_mesh_quad(const float* __restrict__ points, const float* __restrict__ normals, int64_t V,
                                                         const float* __restrict__ node_state, const int32_t* __restrict__ anchors,
@@ -263,50 +273,70 @@ __global__ __launch_bounds__(256) void k_warp_mesh_quad(const float* __restrict_
                                                         float4* __restrict__ out_n, float2* __restrict__ jrows) {
 	NNRT_WAVE_STAMP(g_warp_stamps, 0, __builtin_amdgcn_s_memrealtime());
 	NNRT_WAVE_STAMP(g_warp_stamps, 3, NNRT_STAMP_HWID());
-	const int64_t tid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-	const int64_t v = tid >> 2;
-	const int k = static_cast<int>(tid & 3);
-	const bool vertex_ok = v < V;
-	const bool slot_ok = vertex_ok && k < K;
-	f3 cp = make3(0.f, 0.f, 0.f), cn = make3(0.f, 0.f, 0.f);   // this slot's contribution
-	bool valid = false;
-	if (slot_ok) {
-		const f3 p = make3(points[3 * v], points[3 * v + 1], points[3 * v + 2]);
-		const f3 n = make3(normals[3 * v], normals[3 * v + 1], normals[3 * v + 2]);
-		f3 pc = p, nc = n;
-		if (!E.identity) {
-			pc = apply_extrinsics_point(E, p);
-			nc = apply_extrinsics_normal(E, n);
-		}
-		const int32_t a = anchors[v * K + k];
-		float4 ojv = make_float4(0.f, 0.f, 0.f, 0.f), ojn = make_float4(0.f, 0.f, 0.f, 0.f);
-		if (a != -1) {
-			valid = true;
-			warp_slot<IDENTITY>(node_state, a, weights[v * K + k], p, n, pc, nc, E.identity, cp, cn, ojv, ojn);
-		}
-		if (jrows) store_jacobian_row(jrows, v * K + k, ojv, ojn);
-	}
-	// serial slot-order sum on the quad's first lane: ((0 + c0) + c1) + c2) + c3, skipping invalid anchors
-	const float vf = valid ? 1.f : 0.f;
-	float c[4][7];
-	const float mine[7] = {cp.x, cp.y, cp.z, cn.x, cn.y, cn.z, vf};
+	// The input loads (canonical vertex, normal, anchor, weight) are issued unconditionally at clamped indices, so they
+	// leave together ahead of the node-state gathers (round 5: C3 74.7 -> 62.4 µs against the loads inside the
+	// `slot_ok` branch). WARP_UNROLL quads per lane per step (development: 2 / 4 measured no faster -- the extra
+	// registers cost waves) over a workgroup-strided loop (one step per lane unless WARP_MAX_WGS caps the launch).
+	constexpr int U = WARP_UNROLL;
+	const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+	for (int64_t base = static_cast<int64_t>(blockIdx.x) * blockDim.x; base < 4 * V; base += U * stride) {
+		int64_t v[U];
+		int k[U];
+		bool vertex_ok[U], slot_ok[U];
+		f3 p[U], n[U];
+		int32_t a[U];
+		float w[U];
 #pragma unroll
-	for (int i = 0; i < 7; i++) {
-		c[0][i] = quad_bcast<0x00>(mine[i]);
-		c[1][i] = quad_bcast<0x55>(mine[i]);
-		c[2][i] = quad_bcast<0xAA>(mine[i]);
-		c[3][i] = quad_bcast<0xFF>(mine[i]);
-	}
-	if (vertex_ok && k == 0) {
-		float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-		for (int q = 0; q < 4; q++) {
-			if (q >= K || c[q][6] == 0.f) continue;
-#pragma unroll
-			for (int i = 0; i < 6; i++) acc[i] += c[q][i];
+		for (int u = 0; u < U; u++) {   // inputs (clamped indices: every load is issued, the unused ones ignored)
+			const int64_t tid = base + u * stride + threadIdx.x;
+			v[u] = tid >> 2;
+			k[u] = static_cast<int>(tid & 3);
+			vertex_ok[u] = v[u] < V;
+			slot_ok[u] = vertex_ok[u] && k[u] < K;
+			const int64_t vv = vertex_ok[u] ? v[u] : 0;
+			const int kk = slot_ok[u] ? k[u] : 0;
+			p[u] = make3(points[3 * vv], points[3 * vv + 1], points[3 * vv + 2]);
+			n[u] = make3(normals[3 * vv], normals[3 * vv + 1], normals[3 * vv + 2]);
+			a[u] = anchors[vv * K + kk];
+			w[u] = weights[vv * K + kk];
 		}
-		out_p[v] = make_float4(acc[0], acc[1], acc[2], 0.f);
-		out_n[v] = make_float4(acc[3], acc[4], acc[5], 0.f);
+#pragma unroll
+		for (int u = 0; u < U; u++) {
+			f3 cp = make3(0.f, 0.f, 0.f), cn = make3(0.f, 0.f, 0.f);   // this slot's contribution
+			const bool valid = slot_ok[u] && a[u] != -1;
+			{
+				f3 pc = p[u], nc = n[u];
+				if (!E.identity) {
+					pc = apply_extrinsics_point(E, p[u]);
+					nc = apply_extrinsics_normal(E, n[u]);
+				}
+				float4 ojv = make_float4(0.f, 0.f, 0.f, 0.f), ojn = make_float4(0.f, 0.f, 0.f, 0.f);
+				if (valid) warp_slot<IDENTITY>(node_state, a[u], w[u], p[u], n[u], pc, nc, E.identity, cp, cn, ojv, ojn);
+				if (jrows && slot_ok[u]) store_jacobian_row(jrows, v[u] * K + k[u], ojv, ojn);
+			}
+			// serial slot-order sum on the quad's first lane: ((0 + c0) + c1) + c2) + c3, skipping invalid anchors
+			const float vf = valid ? 1.f : 0.f;
+			float c[4][7];
+			const float mine[7] = {cp.x, cp.y, cp.z, cn.x, cn.y, cn.z, vf};
+#pragma unroll
+			for (int i = 0; i < 7; i++) {
+				c[0][i] = quad_bcast<0x00>(mine[i]);
+				c[1][i] = quad_bcast<0x55>(mine[i]);
+				c[2][i] = quad_bcast<0xAA>(mine[i]);
+				c[3][i] = quad_bcast<0xFF>(mine[i]);
+			}
+			if (vertex_ok[u] && k[u] == 0) {
+				float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+				for (int q = 0; q < 4; q++) {
+					if (q >= K || c[q][6] == 0.f) continue;
+#pragma unroll
+					for (int i = 0; i < 6; i++) acc[i] += c[q][i];
+				}
+				out_p[v[u]] = make_float4(acc[0], acc[1], acc[2], 0.f);
+				out_n[v[u]] = make_float4(acc[3], acc[4], acc[5], 0.f);
+			}
+		}
 	}
 	NNRT_WAVE_STAMP(g_warp_stamps, 2, __builtin_amdgcn_s_memrealtime());
 }
@@ -316,7 +346,7 @@ nnrt_status launch_warp_mesh(const float* points, const float* normals, int64_t 
                              hipStream_t stream, bool from_identity) {
 	if (V == 0) return NNRT_OK;
 	if (K <= 4) {
-		const unsigned grid = static_cast<unsigned>(ceil_div(4 * V, 256));
+		const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(4 * V, 256), WARP_MAX_WGS));
 		if (from_identity)
 			k_warp_mesh_quad<true><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n, jrows);
 		else
