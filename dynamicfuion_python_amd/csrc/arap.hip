@@ -18,31 +18,23 @@ namespace nnrt {
 // ---- data acc + ARAP edge terms -> full diagonal blocks (+LM) and rhs = negative gradient ----
 // 32 lanes per node: lane q < 21 owns upper-triangle entry q of the 6x6 block, lanes 21..26 the gradient. The ARAP
 // terms (ComputeBlockSums of dEi^T dEi / dEj^T dEj and J^T e, ArapHessianImpl.h / DeformableMeshToImageFitterImpl.h)
-// are gathered from the node's incident edges (CSR, ascending edge order; entry = 2 e + (node is the edge's target)).
+// come from the node's incidence slots (edge_terms: node-major, ascending edge order per node; the ARAP edge kernel
+// wrote each edge's terms for its two nodes there, laid out as the prepared row), lane q summing entry q.
 // lane q of node n's 32-lane group: the node's prepared entry (q < 21: diagonal-block entry (r0, c0), r0 <= c0, with LM
 // -> *dv; 21 <= q < 27: right-hand side entry q - 21 -> *dv), its global outputs written; false for lanes q >= 27
 __device__ __forceinline__ bool prepare_node(int n, int q, float lm, double* __restrict__ acc, const int* __restrict__ inc_off,
-                                             const int* __restrict__ inc_list, const float* __restrict__ edge_terms, float* __restrict__ diag,
-                                             float* __restrict__ rhs, float* __restrict__ gradient_out, float* __restrict__ hessian_out, int& r0,
-                                             int& c0, float& dv) {
-	// the term this lane sums from a source incidence / a target incidence (-1: none)
-	const int q_src = q < 27 ? q : -1;
-	const int q_tgt = (q == 15 || q == 18 || q == 20) ? 27 : (q >= 24 && q < 27) ? 28 + (q - 24) : -1;
-	// the accumulator entry first: its load (memory-side atomics' target) overlaps the incidence gathers below
+                                             const float* __restrict__ edge_terms, float* __restrict__ diag, float* __restrict__ rhs,
+                                             float* __restrict__ gradient_out, float* __restrict__ hessian_out, int& r0, int& c0, float& dv) {
+	// the accumulator entry first: its load (memory-side atomics' target) overlaps the slot loads below
 	double* ad = acc + static_cast<int64_t>(n) * ACC_STRIDE;
 	const double hq = q < 27 ? ad[q] : 0.0;
 	float arap = 0.f;
 	const int beg = inc_off[n], end = inc_off[n + 1];
 	for (int u0 = beg; u0 < end; u0 += 32) {
 		const int nu = end - u0 < 32 ? end - u0 : 32;
-		const int mine = q < nu ? inc_list[u0 + q] : 0;   // one incidence per lane, broadcast below
 		float v[32];
 #pragma unroll
-		for (int u = 0; u < 32; u++) {
-			const int code = __shfl(mine, u, 32);
-			const int col = (code & 1) ? q_tgt : q_src;
-			v[u] = (u < nu && col >= 0) ? edge_terms[static_cast<int64_t>(code >> 1) * EDGE_TERMS + col] : 0.f;
-		}
+		for (int u = 0; u < 32; u++) v[u] = (u < nu && q < 27) ? edge_terms[static_cast<int64_t>(u0 + u) * EDGE_TERMS + q] : 0.f;
 #pragma unroll
 		for (int u = 0; u < 32; u++)
 			if (u < nu) arap += v[u];
@@ -81,14 +73,14 @@ __device__ __forceinline__ bool prepare_node(int n, int q, float lm, double* __r
 
 // ---- data acc + ARAP edge terms -> full diagonal blocks (+LM) and rhs = negative gradient (every node) ----
 __global__ __launch_bounds__(256) void k_arrow_prepare(int N, float lm, double* __restrict__ acc, const int* __restrict__ inc_off,
-                                                       const int* __restrict__ inc_list, const float* __restrict__ edge_terms, float* __restrict__ diag,
-                                                       float* __restrict__ rhs, float* __restrict__ gradient_out, float* __restrict__ hessian_out) {
+                                                       const float* __restrict__ edge_terms, float* __restrict__ diag, float* __restrict__ rhs,
+                                                       float* __restrict__ gradient_out, float* __restrict__ hessian_out) {
 	const int n = static_cast<int>((static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 5);
 	const int q = static_cast<int>(threadIdx.x & 31);
 	if (n >= N) return;   // uniform per 32-lane node group
 	int r0, c0;
 	float dv;
-	prepare_node(n, q, lm, acc, inc_off, inc_list, edge_terms, diag, rhs, gradient_out, hessian_out, r0, c0, dv);
+	prepare_node(n, q, lm, acc, inc_off, edge_terms, diag, rhs, gradient_out, hessian_out, r0, c0, dv);
 }
 
 // ---- stem: D^-1 and D^-1 B per stem node, four lanes per node (each forms D^-1 with the same arithmetic and the products
@@ -507,7 +499,7 @@ nnrt_status launch_arrowhead_iteration(const ArrowheadWorkspace& ws, const doubl
 	// (one launch of prepare + stem + corner init, every node's block kept in its workgroup, measured 22.4 µs at C5 against
 	// 11.6 + 9.1 µs as two launches: the stem phase then ran on 4 of every 32 lanes; round 4, not kept)
 	k_arrow_prepare<<<static_cast<unsigned>(ceil_div(static_cast<int64_t>(ws.N) * 32, 256)), 256, 0, stream>>>(
-	    ws.N, lm, const_cast<double*>(acc), ws.inc_off, ws.inc_list, edge_jr, ws.diag, ws.rhs, gradient_out, hessian_out);
+	    ws.N, lm, const_cast<double*>(acc), ws.inc_off, edge_jr, ws.diag, ws.rhs, gradient_out, hessian_out);
 	NNRT_LAUNCH_CHECK();
 	return arrowhead_solve_core(ws, edges, wing, error_flag, stream, true, node_state, updates_out, state_in);
 }

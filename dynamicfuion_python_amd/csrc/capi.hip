@@ -392,7 +392,7 @@ struct nnrt_fitter {
 	// ARAP / arrowhead
 	DeviceBuffer<float> wing, edge_residuals, a_diag, a_dinv, a_dinvb, a_rhs, a_x, a_res, a_dx;
 	CornerSolver corner;   // Schur corner of the arrowhead solve (tile-sparse Cholesky plan + storage)
-	DeviceBuffer<int> a_offsets, a_list, a_tgt_off, a_rhs_off, a_rhs_edges, a_inc_off, a_inc_list;
+	DeviceBuffer<int> a_offsets, a_list, a_tgt_off, a_rhs_off, a_rhs_edges, a_inc_off, a_inc_list, a_inc_slot;
 	DeviceBuffer<int2> a_tgt_ab, a_pairs;
 	ArrowheadWorkspace aw;
 	float refine_ratio = NNRT_REFINE_PIVOT_RATIO;   // refinement gate threshold (nnrt_fitter_set_refine_ratio)
@@ -544,6 +544,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 		aa.node_weights = wf->node_weights.ptr;
 		aa.node_state = state_in;
 		aa.edge_jr = ft->edge_jr.ptr;
+		aa.inc_slot = ft->a_inc_slot.ptr;
 		aa.wing = ft->wing.ptr;
 		aa.edge_residuals = ft->edge_residuals.ptr;
 		aa.error_flag = ft->error_flag.ptr;
@@ -661,6 +662,7 @@ void nnrt_fitter_destroy(nnrt_fitter* ft) {
 	ft->a_pairs.release();
 	ft->a_inc_off.release();
 	ft->a_inc_list.release();
+	ft->a_inc_slot.release();
 	if (ft->ev_in) hipEventDestroy(ft->ev_in);
 	if (ft->ev_out) hipEventDestroy(ft->ev_out);
 
@@ -736,7 +738,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 		if ((st = ft->wing.ensure(static_cast<size_t>(E) * 36)) || (st = ft->edge_residuals.ensure(3 * static_cast<size_t>(E))) ||
 		    (st = ft->a_diag.ensure(static_cast<size_t>(N) * 36)) || (st = ft->a_dinv.ensure(static_cast<size_t>(n0) * 36)) ||
 		    (st = ft->a_dinvb.ensure(static_cast<size_t>(E) * 36)) ||
-		    (st = ft->edge_jr.ensure(static_cast<size_t>(E) * EDGE_TERMS)) ||
+		    (st = ft->edge_jr.ensure(2 * static_cast<size_t>(E) * EDGE_TERMS)) ||
 		    (st = ft->a_rhs.ensure(6 * static_cast<size_t>(N))) || (st = ft->a_x.ensure(6 * static_cast<size_t>(N))) ||
 		    (st = ft->a_res.ensure(6 * static_cast<size_t>(N))) || (st = ft->a_dx.ensure(6 * static_cast<size_t>(N))) ||
 		    (st = ft->a_offsets.ensure(n0 + 1)) || (st = ft->a_list.ensure(E)))
@@ -769,7 +771,11 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 				inc_list[static_cast<size_t>(fill_inc[static_cast<size_t>(wf->h.edges[2 * e + 1])]++)] = 2 * e + 1;
 			}
 		}
-		if ((st = upload(ft->a_inc_off, inc_off)) || (st = upload(ft->a_inc_list, inc_list))) return st;
+		// the slot of each incidence in that order: the ARAP edge kernel writes its two nodes' terms there (node-major, so
+		// k_arrow_prepare reads each node's terms contiguously, without the incidence list)
+		std::vector<int> inc_slot(2 * static_cast<size_t>(E));
+		for (size_t q = 0; q < inc_list.size(); q++) inc_slot[static_cast<size_t>(inc_list[q])] = static_cast<int>(q);
+		if ((st = upload(ft->a_inc_off, inc_off)) || (st = upload(ft->a_inc_list, inc_list)) || (st = upload(ft->a_inc_slot, inc_slot))) return st;
 		ft->aw.inc_off = ft->a_inc_off.ptr;
 		ft->aw.inc_list = ft->a_inc_list.ptr;
 		const StemSchurLists sl = build_stem_schur_lists(wf->h.edges.data(), E, n0, N);

@@ -28,12 +28,17 @@ struct ArapArgs {
 	const float* radii;             // [layers]
 	const float* node_weights;      // [N] (variable coverage)
 	const float* node_state;        // [N,16]
-	float* edge_jr;                 // [E,EDGE_TERMS]: the edge's diagonal-block / gradient terms for its two nodes
+	float* edge_jr;                 // [2E,EDGE_TERMS]: per node incidence (inc_slot order), the edge's diagonal-block /
+	                                // gradient terms for that node (node-major: a node's incidences are contiguous)
+	const int* inc_slot;            // [2E]: slot of incidence 2 e (source) / 2 e + 1 (target) in the node-ordered list
 	float* wing;                    // [E,36]: dEi^T dEj
 	float* edge_residuals;          // [3E]
 	int* error_flag;
 };
-constexpr int EDGE_TERMS = 32;  // per ARAP edge: 21 + 6 source terms, 1 + 3 target terms, 1 pad
+// per node incidence: the 27 entries of the node's prepared row (21 diagonal-block upper-triangle entries, 6 gradient)
+// the edge adds there -- a source incidence all 27, a target incidence b^2 at the translation diagonal (15, 18, 20) and
+// b e at 24..26 -- zeros elsewhere, 5 pad
+constexpr int EDGE_TERMS = 32;
 
 // dE^T dE for dE = [skew(a) | s I] (i side) ; returns the 21 upper-triangle entries
 __device__ inline void edge_block_i(const float* j5, float (&dE)[3][6]) {
@@ -63,7 +68,8 @@ __device__ inline void arap_edge(const ArapArgs& a, int e) {
 	} else {
 		if (j >= a.E) {   // reference indexes edge_layer_indices[node_j] (A3); out of bounds there
 			atomicOr(a.error_flag, 2);
-			for (int q = 0; q < EDGE_TERMS; q++) a.edge_jr[static_cast<int64_t>(e) * EDGE_TERMS + q] = 0.f;
+			for (int h = 0; h < 2; h++)
+				for (int q = 0; q < EDGE_TERMS; q++) a.edge_jr[static_cast<int64_t>(a.inc_slot[2 * e + h]) * EDGE_TERMS + q] = 0.f;
 			return;
 		}
 		w_res = a.radii[a.edge_layers[j]];
@@ -98,23 +104,38 @@ __device__ inline void arap_edge(const ArapArgs& a, int e) {
 		}
 	// the edge's contributions to its two nodes' diagonal blocks and gradients, summed per node by k_arrow_prepare (no
 	// atomics; every node sums its incident edges in ascending edge order): source i: dEi^T dEi (21 upper-triangle
-	// entries, ComputeBlockSums) + J_i^T e (6); target j: b^2 on the translation diagonal + b e (3)
-	float* src = a.edge_jr + static_cast<int64_t>(e) * EDGE_TERMS;
+	// entries, ComputeBlockSums) + J_i^T e (6); target j: b^2 on the translation diagonal + b e (3). Each goes to its
+	// incidence's slot, laid out as the node's prepared row (zeros where the edge adds nothing)
+	float s27[EDGE_TERMS];
 	int q = 0;
 #pragma unroll
 	for (int r0 = 0; r0 < 6; r0++)
 #pragma unroll
-		for (int c0 = r0; c0 < 6; c0++) src[q++] = (dEi[0][r0] * dEi[0][c0] + dEi[1][r0] * dEi[1][c0]) + dEi[2][r0] * dEi[2][c0];
+		for (int c0 = r0; c0 < 6; c0++) s27[q++] = (dEi[0][r0] * dEi[0][c0] + dEi[1][r0] * dEi[1][c0]) + dEi[2][r0] * dEi[2][c0];
 	const float skT[3][3] = {{0.f, j5[2], -j5[1]}, {-j5[2], 0.f, j5[0]}, {j5[1], -j5[0], 0.f}};
 #pragma unroll
 	for (int c = 0; c < 3; c++) {
-		src[21 + c] = (skT[c][0] * r[0] + skT[c][1] * r[1]) + skT[c][2] * r[2];
-		src[24 + c] = j5[3] * r[c];
+		s27[21 + c] = (skT[c][0] * r[0] + skT[c][1] * r[1]) + skT[c][2] * r[2];
+		s27[24 + c] = j5[3] * r[c];
 	}
-	src[27] = (j5[4] * j5[4] + 0.f * 0.f) + 0.f * 0.f;   // target j: dEj = [0 | b I]
 #pragma unroll
-	for (int c = 0; c < 3; c++) src[28 + c] = j5[4] * r[c];
-	src[31] = 0.f;
+	for (int k = 27; k < EDGE_TERMS; k++) s27[k] = 0.f;
+	const float b2 = (j5[4] * j5[4] + 0.f * 0.f) + 0.f * 0.f;   // target j: dEj = [0 | b I]
+	float t27[EDGE_TERMS];
+#pragma unroll
+	for (int k = 0; k < EDGE_TERMS; k++) t27[k] = 0.f;
+	t27[15] = b2;
+	t27[18] = b2;
+	t27[20] = b2;
+#pragma unroll
+	for (int c = 0; c < 3; c++) t27[24 + c] = j5[4] * r[c];
+	float4* so = reinterpret_cast<float4*>(a.edge_jr + static_cast<int64_t>(a.inc_slot[2 * e]) * EDGE_TERMS);
+	float4* to = reinterpret_cast<float4*>(a.edge_jr + static_cast<int64_t>(a.inc_slot[2 * e + 1]) * EDGE_TERMS);
+#pragma unroll
+	for (int k = 0; k < EDGE_TERMS / 4; k++) {
+		so[k] = make_float4(s27[4 * k], s27[4 * k + 1], s27[4 * k + 2], s27[4 * k + 3]);
+		to[k] = make_float4(t27[4 * k], t27[4 * k + 1], t27[4 * k + 2], t27[4 * k + 3]);
+	}
 }
 
 // warped-surface Jacobian rows (-w R (v - g), -w R n): 0 = formed per association in pass 2 from the node state and the
