@@ -380,6 +380,8 @@ struct nnrt_fitter {
 	DeviceBuffer<float2> jrows;        // [V,K,3] warped-Jacobian rows (store_jacobian_row; NNRT_GATHER_ROWS builds only)
 	DeviceBuffer<float4> mesh_p4, mesh_n4;   // [V] canonical positions / normals as float4 (pass 2 forms the Jacobian rows)
 	DeviceBuffer<float4> ref_points;   // [P] reference point (x, y, z, valid)
+	DeviceBuffer<int> tile_flags, tile_order;   // the pixel launch's per-frame workgroup -> tile table (launch_tile_order)
+	bool use_tile_order = false;
 	DeviceBuffer<float4> records;      // [P, 4] pixel Jacobian records
 	DeviceBuffer<uint64_t> keys;
 	DeviceBuffer<float> residuals;
@@ -524,6 +526,10 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 	fa.cmesh_n = ft->mesh_n4.ptr;
 	fa.weights = ft->weights.ptr;
 	fa.ref_points = ft->ref_points.ptr;
+	if (ft->use_tile_order) {
+		fa.tile_order = ft->tile_order.ptr;
+		fa.order_blocks = tile_order_blocks(fa.tiles_x * fa.tiles_y);
+	}
 	fa.records = ft->records.ptr;
 	fa.residuals = ft->residuals.ptr;
 	fa.residual_mask = ft->residual_mask.ptr;
@@ -637,6 +643,8 @@ void nnrt_fitter_destroy(nnrt_fitter* ft) {
 	ft->drop_graphs();
 	ft->acc.release();
 	ft->ref_points.release();
+	ft->tile_flags.release();
+	ft->tile_order.release();
 	ft->records.release();
 	for (auto* b : {&ft->mesh_p, &ft->mesh_n, &ft->weights, &ft->residuals, &ft->edge_jr, &ft->updates, &ft->gradient,
 	                &ft->hessian, &ft->wing, &ft->edge_residuals, &ft->a_diag, &ft->a_dinv, &ft->a_dinvb, &ft->a_rhs, &ft->a_x, &ft->a_res, &ft->a_dx})
@@ -705,7 +713,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	}
 	// (re)allocate; any reallocation invalidates captured graphs
 	const auto before = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->corner.generation,
-	                                    ft->face_nodes.ptr, ft->wpos.ptr, ft->mesh_p4.ptr);
+	                                    ft->face_nodes.ptr, ft->wpos.ptr, ft->mesh_p4.ptr, ft->tile_order.ptr);
 	nnrt_status st;
 	if ((st = ft->mesh_p.ensure(3 * V)) || (st = ft->mesh_n.ensure(3 * V)) || (st = ft->faces4.ensure(F)) ||
 	    (st = ft->anchors.ensure(static_cast<size_t>(V) * K)) || (st = ft->weights.ensure(static_cast<size_t>(V) * K)) ||
@@ -719,6 +727,23 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	    (st = ft->updates.ensure(static_cast<size_t>(N) * 6)) || (st = ft->gradient.ensure(static_cast<size_t>(N) * 6)) ||
 	    (st = ft->hessian.ensure(static_cast<size_t>(N) * 36)))
 		return st;
+	// the pixel launch's per-frame tile order, for launches of more than one residency round (5 waves per SIMD): their
+	// last round's workgroups decide the tail, and the order gives those the tiles without reference pixels (C3 fused
+	// launch 214 -> 197 us). In one round every wave starts at once and the table load only delays it (C2 40.2 -> 41.8).
+	// NNRT_TILE_ORDER=0: never, =2: always.
+	const size_t tiles = static_cast<size_t>(ceil_div(W, 16)) * static_cast<size_t>(ceil_div(H, 16));
+	const bool tile_order = [&] {
+		const char* v = std::getenv("NNRT_TILE_ORDER");
+		if (v && *v == '0') return false;
+		if (v && *v == '2') return true;
+		int cus = 0;
+		if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ft->device) != hipSuccess || cus <= 0) cus = 256;
+		return 4 * tiles > static_cast<size_t>(5 * 4 * cus);
+	}();
+	{
+		if (tile_order && ((st = ft->tile_flags.ensure(tiles)) || (st = ft->tile_order.ensure(static_cast<size_t>(tile_order_blocks(static_cast<int>(tiles)))))))
+			return st;
+	}
 	// ARAP workspace
 	ft->E = E;
 	ft->n0 = wf->h.layer_counts.empty() ? N : wf->h.layer_counts[0];
@@ -806,16 +831,17 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 		ft->aw.edge_list = ft->a_list.ptr;
 	}
 	const auto after = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->corner.generation,
-	                                   ft->face_nodes.ptr, ft->wpos.ptr, ft->mesh_p4.ptr);
+	                                   ft->face_nodes.ptr, ft->wpos.ptr, ft->mesh_p4.ptr, ft->tile_order.ptr);
 	// Captured graphs bake every buffer pointer and the per-frame constants (NDC setup, pixel camera, extrinsics) into
 	// their kernel arguments: any change drops them. The warp field is recognised by its unique id, not its address.
 	const NdcSetup nndc = make_ndc_setup(h_K, H, W, ft->p.ndc_convention == NNRT_NDC_CONSISTENT);
 	const Camera npix = pixel_camera(h_K);
 	const WarpExtrinsics ne = make_extrinsics(h_E);
-	if (before != after || ft->wf != wf || ft->wf_id != wf->id || ft->V != V || ft->F != F || ft->H != H || ft->W != W || ft->N != N ||
+	if (before != after || ft->use_tile_order != tile_order || ft->wf != wf || ft->wf_id != wf->id || ft->V != V || ft->F != F || ft->H != H || ft->W != W || ft->N != N ||
 	    ft->K != K || std::memcmp(&nndc, &ft->ndc, sizeof(nndc)) != 0 || std::memcmp(&npix, &ft->pix, sizeof(npix)) != 0 ||
 	    std::memcmp(&ne, &ft->extr, sizeof(ne)) != 0)
 		ft->drop_graphs();
+	ft->use_tile_order = tile_order;
 	ft->V = V;
 	ft->F = F;
 	ft->H = H;
@@ -853,6 +879,11 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	else
 		k_prepare_reference_points<<<static_cast<unsigned>(ceil_div(P, 256)), 256, 0, s>>>(ref.points, ref.mask, P, ft->ref_points.ptr);
 	NNRT_LAUNCH_CHECK();
+	// the pixel launch's tile order for this frame's reference points
+	if (ft->use_tile_order &&
+	    (st = launch_tile_order(ft->ref_points.ptr, H, W, static_cast<int>(ceil_div(W, 16)), static_cast<int>(ceil_div(H, 16)), ft->tile_flags.ptr,
+	                            ft->tile_order.ptr, s)))
+		return st;
 	NNRT_HIP(hipMemsetAsync(ft->keys.ptr, 0xff, sizeof(uint64_t) * P, s));
 	NNRT_HIP(hipMemsetAsync(ft->acc.ptr, 0, sizeof(double) * N * ACC_STRIDE, s));
 	NNRT_HIP(hipEventRecord(ft->ev_out, s));

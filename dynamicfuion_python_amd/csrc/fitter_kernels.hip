@@ -31,6 +31,7 @@ static_assert(PIX_WAVES == 1 || PIX_WAVES == 2 || PIX_WAVES == 4, "waves per wor
 // round-robin over the 8 XCDs, so each XCD gets a contiguous band of quadrants (neighbouring pixels share vertices,
 // anchors and nodes -> L2 reuse within the XCD).
 __device__ inline int pix_quadrant(const FitPixelArgs& a) {
+	if (PIX_WAVES == 4 && a.tile_order) return a.tile_order[blockIdx.x] * 4 + static_cast<int>(threadIdx.x >> 6);   // (one scalar load)
 	const int blocks = (4 * a.tiles_x * a.tiles_y + PIX_WAVES - 1) / PIX_WAVES;
 	const int per_xcd = (blocks + 7) / 8;
 	const int b = static_cast<int>(blockIdx.x);
@@ -857,11 +858,81 @@ extern "C" int nnrt_dev_fit_stamps(unsigned long long* out) {   // [16384][4] of
 
 int fit_pixels_arap_blocks(int E) { return static_cast<int>(ceil_div(E, PIX_BLOCK)); }
 
+// ---- per-frame tile order of the pixel launch (launch_tile_order) ----
+__host__ __device__ inline int tiles_per_band(int tiles) { return (tiles + 7) / 8 + 1; }   // ceil(w / 8) + ceil(i / 8) <= this
+int tile_order_blocks(int tiles) { return 8 * tiles_per_band(tiles); }
+
+// per 16 x 16 tile (one wave): does any pixel hold a valid reference point
+__global__ __launch_bounds__(64) void k_tile_flags(const float4* __restrict__ ref, int H, int W, int tiles_x, int* __restrict__ flags) {
+	const int tile = static_cast<int>(blockIdx.x), lane = static_cast<int>(threadIdx.x);
+	const int tu = tile % tiles_x, tv = tile / tiles_x;
+	bool any = false;
+#pragma unroll
+	for (int k = 0; k < 4; k++) {
+		const int q = lane + 64 * k, u = tu * PIX_TILE + (q & 15), v = tv * PIX_TILE + (q >> 4);
+		if (u < W && v < H) any |= ref[static_cast<int64_t>(v) * W + u].w != 0.f;
+	}
+	const unsigned long long b = __ballot(any);
+	if (lane == 0) flags[tile] = b != 0ull;
+}
+
+// one workgroup: ranks of the working / idle tiles in raster order (chunked block scan), then each XCD band x (the
+// workgroups b = x + 8 k, k = 0, 1, ... of the launch, dispatched in k order) gets its eighth of the working tiles at
+// k = 0.. and its eighth of the idle tiles after them; unused entries hold `tiles` (a workgroup with no pixels)
+constexpr int ORDER_THREADS = 1024;
+__global__ __launch_bounds__(ORDER_THREADS) void k_tile_order(const int* __restrict__ flags, int tiles, int* __restrict__ order) {
+	__shared__ int s_w[ORDER_THREADS], s_i[ORDER_THREADS];
+	const int t = static_cast<int>(threadIdx.x);
+	const int per_band = tiles_per_band(tiles);
+	for (int i = t; i < 8 * per_band; i += ORDER_THREADS) order[i] = tiles;
+	const int c = (tiles + ORDER_THREADS - 1) / ORDER_THREADS, t0 = t * c, t1 = t0 + c < tiles ? t0 + c : tiles;
+	int nw = 0, ni = 0;
+	for (int q = t0; q < t1; q++) (flags[q] ? nw : ni)++;
+	s_w[t] = nw;
+	s_i[t] = ni;
+	__syncthreads();
+	for (int d = 1; d < ORDER_THREADS; d <<= 1) {   // inclusive scan (Hillis-Steele)
+		const int aw = t >= d ? s_w[t - d] : 0, ai = t >= d ? s_i[t - d] : 0;
+		__syncthreads();
+		s_w[t] += aw;
+		s_i[t] += ai;
+		__syncthreads();
+	}
+	const int W = s_w[ORDER_THREADS - 1], I = s_i[ORDER_THREADS - 1];
+	int m = s_w[t] - nw, n = s_i[t] - ni;   // ranks of this chunk's first working / idle tile
+	__syncthreads();   // (the pad fill above is ordered before the entries below by the scan's barriers)
+	for (int q = t0; q < t1; q++) {
+		if (flags[q]) {
+			int x = 7;
+			while (x > 0 && (static_cast<int64_t>(x) * W) / 8 > m) x--;
+			order[x * per_band + (m - static_cast<int>((static_cast<int64_t>(x) * W) / 8))] = q;
+			m++;
+		} else {
+			int x = 7;
+			while (x > 0 && (static_cast<int64_t>(x) * I) / 8 > n) x--;
+			const int wx = static_cast<int>((static_cast<int64_t>(x + 1) * W) / 8 - (static_cast<int64_t>(x) * W) / 8);
+			order[x * per_band + wx + (n - static_cast<int>((static_cast<int64_t>(x) * I) / 8))] = q;
+			n++;
+		}
+	}
+}
+
+nnrt_status launch_tile_order(const float4* ref_points, int H, int W, int tiles_x, int tiles_y, int* flags, int* order, hipStream_t stream) {
+	const int tiles = tiles_x * tiles_y;
+	if (tiles == 0) return NNRT_OK;
+	k_tile_flags<<<static_cast<unsigned>(tiles), 64, 0, stream>>>(ref_points, H, W, tiles_x, flags);
+	NNRT_LAUNCH_CHECK();
+	k_tile_order<<<1, ORDER_THREADS, 0, stream>>>(flags, tiles, order);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
 nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t stream, hipEvent_t between) {
 	// `between` (stage timing) is recorded before the fused launch: the pixel-pass stage reads 0, the node-pass stage
 	// times both passes
 	if (between) NNRT_EV(hipEventRecord(between, stream));
-	const unsigned grid = static_cast<unsigned>(((4 * args.tiles_x * args.tiles_y + PIX_WAVES - 1) / PIX_WAVES + 7) / 8 * 8 + args.arap_blocks);
+	const unsigned grid = static_cast<unsigned>((args.tile_order ? args.order_blocks : ((4 * args.tiles_x * args.tiles_y + PIX_WAVES - 1) / PIX_WAVES + 7) / 8 * 8) +
+	                                            args.arap_blocks);
 	// anchor slots per vertex: the common 4-anchor configuration gets its own instantiation (half the slot logic)
 	const bool k4 = args.anchor_count <= 4;
 	switch (mode) {

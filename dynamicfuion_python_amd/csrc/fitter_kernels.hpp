@@ -176,6 +176,8 @@ struct FitPixelArgs {
 	float4* records;        // [P, 4] per-pixel Jacobian record (pass 1 -> pass 2)
 	ArapArgs arap;          // ARAP edge terms, computed by the launch's last arap_blocks workgroups (0: none)
 	int arap_blocks;
+	const int* tile_order;  // [order_blocks] workgroup -> tile (launch_tile_order; nullable: the arithmetic XCD bands)
+	int order_blocks;
 };
 
 struct SolveArgs {
@@ -203,6 +205,11 @@ nnrt_status launch_face_node_table(const int4* faces4, int64_t F, const int32_t*
 // args.arap_blocks extra workgroups (fit_pixels_arap_blocks(E), 0 without ARAP) compute the ARAP edge terms.
 nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t stream, hipEvent_t between = nullptr);
 int fit_pixels_arap_blocks(int E);
+// once per frame: the pixel launch's workgroup -> tile table. Tiles with a valid reference pixel (the only ones the data
+// term can use) fill the front of each XCD's band in raster order, the others its end: the workgroups dispatched last --
+// the fifth per CU -- get the tiles with nothing to sum. flags: [tiles] scratch; order: [tile_order_blocks(tiles)]
+int tile_order_blocks(int tiles);
+nnrt_status launch_tile_order(const float4* ref_points, int H, int W, int tiles_x, int tiles_y, int* flags, int* order, hipStream_t stream);
 nnrt_status launch_solve_update(int mode, const SolveArgs& args, hipStream_t stream, bool from_identity = false);
 
 

@@ -1195,6 +1195,36 @@ def test_c3_raster_parity_and_iteration_properties(nn, S, oracle_mod):
     assert per_node.max() <= 3999
 
 
+@pytest.mark.parametrize("name", ["C2", "S1"])
+def test_pixel_tile_order_same_iteration(nn, S, oracle_mod, name):
+    """The pixel launch's per-frame tile order (tiles without reference pixels dealt to each XCD band's end; on by default
+    beyond one residency round, forced here with NNRT_TILE_ORDER=2) changes which workgroup runs which tile, not the
+    iteration: pixel faces, masks and residuals identical, H and g within the fp64 summation order (1e-6), updates 1e-5,
+    against the arithmetic XCD bands (NNRT_TILE_ORDER=0)."""
+    import os
+    sc = _scene(S, oracle_mod, name)
+    depth = scene_target(oracle_mod, sc)
+    N = len(sc.nodes)
+    old = os.environ.get("NNRT_TILE_ORDER")
+    out = {}
+    try:
+        for v in ("2", "0"):
+            os.environ["NNRT_TILE_ORDER"] = v
+            _, _, dg = _gpu_fit(nn, sc, depth, 1)
+            out[v] = dg
+    finally:
+        if old is None:
+            os.environ.pop("NNRT_TILE_ORDER", None)
+        else:
+            os.environ["NNRT_TILE_ORDER"] = old
+    a, b = out["2"], out["0"]
+    assert np.array_equal(a["pixel_faces"], b["pixel_faces"]) and np.array_equal(a["residual_mask"], b["residual_mask"])
+    assert np.array_equal(a["residuals"], b["residuals"])
+    assert rel_err(a["hessian"][: 36 * N], b["hessian"][: 36 * N]) < 1e-6
+    assert rel_err(a["gradient"][: 6 * N], b["gradient"][: 6 * N]) < 1e-6
+    assert nan_rel_err(a["updates"][: 6 * N], b["updates"][: 6 * N]) < 1e-5
+
+
 def test_errors_fail_loudly(nn, S, oracle_mod):
     A, G = nn.alignment, nn.geometry
     with pytest.raises(RuntimeError):
