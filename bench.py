@@ -638,6 +638,13 @@ def main(argv=None):
                                         if k in ("k_corner_factor", "k_corner_flow", "k_corner_invert", "k_stem_schur_rhs", "k_arrow_prepare",
                                                  "k_init_stem")}
         corner["traffic_source"] = traffic_src
+        tpl = corner["traffic_per_launch"]
+        if "k_corner_factor" in tpl and corner.get("kernel_ms"):
+            # the solve stage's HBM bytes per iteration (every launch of it: the factor once per level) against the HBM peak
+            # over the stage's time: how far from memory-bound this MFMA-priced stage runs
+            per_iter = sum(v * (corner.get("plan", {}).get("factor_launches", 1) if k == "k_corner_factor" else 1) for k, v in tpl.items())
+            corner["traffic"] = per_iter
+            corner["traffic_frac"] = per_iter / (corner["kernel_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS
     if corner is not None:   # ARAP configs: the dense corner (MFMA-bound) is the dominant stage; the HBM one moves aside
         out["hbm_roofline"] = out["roofline"]
         out["roofline"] = corner
