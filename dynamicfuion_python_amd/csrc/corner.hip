@@ -894,6 +894,12 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 		const int w4 = wave & 3, qr = w4 >> 1, qc = w4 & 1;
 		const int n_g = wave < 4 ? tk.nd : 0;
 		f32x16 acc = {};
+		float* C = a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS + 32 * qc + (lane & 31);
+		float cv[16];   // the tile's own entries first (they land while the terms stream)
+		if (wave < 4) {
+#pragma unroll
+			for (int v = 0; v < 16; v++) cv[v] = C[(32 * qr + quad_row(v, lane)) * TILE];
+		}
 		if (n_g > 0) term_dma(a.tiles, src[0], s_stage, w4, lane);
 		float bs = 0.f, bv = 0.f;
 		float* bj = a.cb + static_cast<int64_t>(tk.J) * TILE;
@@ -911,10 +917,6 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 			lds_barrier();
 		}
 		if (wave < 4) {
-			float* C = a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS + 32 * qc + (lane & 31);
-			float cv[16];
-#pragma unroll
-			for (int v = 0; v < 16; v++) cv[v] = C[(32 * qr + quad_row(v, lane)) * TILE];
 #pragma unroll
 			for (int v = 0; v < 16; v++) C[(32 * qr + quad_row(v, lane)) * TILE] = cv[v] - acc[v];
 		} else if (tk.I == tk.J && (t4 & 3) == 0) {
@@ -937,12 +939,19 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 		const int rounds = tk.nd > tk.np ? tk.nd : tk.np;
 		float* bufs = s_stage + g * 2 * TERM_FLOATS;
 		f32x16 acc = {};
+		// the staged tile's own entries (this wave's quadrant) and b_J first: their loads land while the terms stream,
+		// instead of a memory round trip after the last term
+		const float* A = a.tiles + static_cast<int64_t>(g == 0 ? tk.slot_d : tk.slot_t) * TILE_ELEMS;
+		float tv[16];
+		if (g == 0 || !diag) {
+#pragma unroll
+			for (int v = 0; v < 16; v++) tv[v] = A[(32 * qr + quad_row(v, lane)) * TILE + 32 * qc + (lane & 31)];
+		}
+		const int t4 = t - 4 * 64;
+		const float cbj = g == 1 && diag && (t4 & 3) == 0 ? a.cb[static_cast<int64_t>(tk.J) * TILE + (t4 >> 2)] : 0.f;
 		if (n_g > 0) term_dma(a.tiles, src_g[0], bufs, w4, lane);
 		float bs = 0.f;
-		if (g == 1 && diag) {   // b_J's update terms (direct loads, L y over the same columns)
-			const int t4 = t - 4 * 64;
-			bs = rhs_updates(a.tiles, src, tk.nd, a.cb, t4);
-		}
+		if (g == 1 && diag) bs = rhs_updates(a.tiles, src, tk.nd, a.cb, t4);   // b_J's update terms (direct loads, L y)
 		for (int e = 0; e < rounds; e++) {
 			const bool more = e + 1 < n_g;
 			if (more) term_dma(a.tiles, src_g[e + 1], bufs + ((e + 1) & 1) * TERM_FLOATS, w4, lane);
@@ -951,17 +960,12 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 			if (e < n_g) acc = term_mfma_lds(bufs + (e & 1) * TERM_FLOATS, qr, qc, lane, acc);
 			lds_barrier();                           // term e's buffer is read: round e + 1 refills it
 		}
-		const float* A = a.tiles + static_cast<int64_t>(g == 0 ? tk.slot_d : tk.slot_t) * TILE_ELEMS;
 		if (g == 0 || !diag) {   // s_t = A - sum of the terms (the quadrant of term_mfma's C / D layout)
 			float* s_t = g == 0 ? s_d : s_p;
-			float tv[16];
-#pragma unroll
-			for (int v = 0; v < 16; v++) tv[v] = A[(32 * qr + quad_row(v, lane)) * TILE + 32 * qc + (lane & 31)];
 #pragma unroll
 			for (int v = 0; v < 16; v++) s_t[(32 * qr + quad_row(v, lane)) * CS4 + 32 * qc + (lane & 31)] = tv[v] - acc[v];
 		} else {
-			const int t4 = t - 4 * 64;
-			if ((t4 & 3) == 0) s_b[t4 >> 2] = a.cb[static_cast<int64_t>(tk.J) * TILE + (t4 >> 2)] - bs;
+			if ((t4 & 3) == 0) s_b[t4 >> 2] = cbj - bs;
 		}
 	}
 	__syncthreads();

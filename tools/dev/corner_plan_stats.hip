@@ -59,6 +59,39 @@ int main(int argc, char** argv) {
 		printf("back %zu: chains %3d columns %3d longest chain %3d entries/col max %3d total %4d in-chain %4d; heaviest chain %d tiles (%d on the chain's path)\n", l,
 		       p.back_off[l + 1] - p.back_off[l], totcols, maxlen, maxent, sument, inchain, maxchain_tiles, maxchain_inner);
 	}
+	// staging MFMA steps per level (the slowest panel task): every term 32 steps of 32x32x2, against skipping the steps
+	// whose k lies in the source column's identity padding (possible when the column has <= 32 real columns)
+	{
+		std::vector<int> nreal(p.T, 64);
+		for (int l = 0; l < p.H; l++)
+			for (int q = p.level_off[l]; q < p.level_off[l] + p.level_panel[l]; q++)
+				if (p.tasks[q].I == p.tasks[q].J) nreal[p.tasks[q].J] = p.tasks[q].nreal;
+		int le32 = 0;
+		for (int J = 0; J < p.T; J++) le32 += nreal[J] <= 32;
+		long tot_now = 0, tot_skip = 0;
+		for (int l = 0; l < p.H; l++) {
+			int worst_now = 0, worst_skip = 0;
+			for (int q = p.level_off[l]; q < p.level_off[l] + p.level_panel[l]; q++) {
+				const CornerTask& tk = p.tasks[q];
+				const bool diag = tk.I == tk.J;
+				const int rounds = std::max(tk.nd, diag ? 0 : tk.np);
+				int now = 0, skip = 0;
+				for (int e = 0; e < rounds; e++) {
+					int sd = e < tk.nd ? 32 : 0, sp = (!diag && e < tk.np) ? 32 : 0;
+					int kd = e < tk.nd ? p.srcs[tk.src + e].z : -1, kp = (!diag && e < tk.np) ? p.srcs[tk.src + tk.nd + e].z : -1;
+					int td = kd >= 0 ? (nreal[kd] <= 32 ? nreal[kd] : 32) : 0, tp = kp >= 0 ? (nreal[kp] <= 32 ? nreal[kp] : 32) : 0;
+					now += sd + sp;   // both groups share the SIMDs
+					skip += td + tp;
+				}
+				worst_now = std::max(worst_now, now);
+				worst_skip = std::max(worst_skip, skip);
+			}
+			tot_now += worst_now;
+			tot_skip += worst_skip;
+			printf("level %2d: staging MFMA steps per SIMD (slowest panel) %4d, with padding skipped %4d\n", l, worst_now, worst_skip);
+		}
+		printf("columns with <= 32 real columns: %d of %d; staging steps over the levels %ld -> %ld\n", le32, p.T, tot_now, tot_skip);
+	}
 	// the dataflow launch's critical path (k_corner_flow): a back chain starts when its parent chain ends; per chain its
 	// columns and entry tiles, the deepest path in columns and entries
 	{
