@@ -835,6 +835,9 @@ __global__ __launch_bounds__(PIX_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) 
 	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
 	__builtin_amdgcn_wave_barrier();
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#ifdef NNRT_DEV_PASS1_ONLY   // timing build only: pass 1 alone (instruction counts per pass by difference)
+	if (face != -2) return;
+#endif
 	node_body<MODE, MAXK>(a, w, w + 8 * NG_STRIDE, reinterpret_cast<uint32_t*>(w + 2 * 8 * NG_STRIDE), face, vid);
 	FIT_STAMP(2, __builtin_amdgcn_s_memrealtime());
 }
