@@ -730,12 +730,67 @@ __device__ inline void eliminate_columns(f32x2 (&ap)[TILE], int lane, int& bad) 
 	}
 }
 
+// Multi-wave elimination of a panel (k_corner_factor, NNRT_CORNER_ELIM_WAVES = EW > 0): the tile's 16 four-column
+// blocks are dealt cyclically over EW waves (block b on wave b mod EW, lane = row, the A_JJ row and the panel row as
+// one f32x2 per column as in eliminate_columns). Per block: its owner factors it (the 4 x 4 diagonal sub-block by
+// readlane, wave-uniform, then every row), writes the block's L columns of every row to LDS, one workgroup barrier, and
+// each wave applies them to its own later blocks (four packed FMAs per column, multipliers L_c,jb..jb+3 from a
+// wave-uniform 16-B LDS read), nearest block first: the next owner's block is ready one update after the barrier, the
+// other updates run on the other waves while it factors. Every element sees its updates in ascending column order.
+#ifndef NNRT_CORNER_ELIM_WAVES
+#define NNRT_CORNER_ELIM_WAVES 8
+#endif
+#ifndef NNRT_CORNER_ELIM_BW
+#define NNRT_CORNER_ELIM_BW 4
+#endif
+constexpr int ELIM_WAVES = NNRT_CORNER_ELIM_WAVES;
+constexpr int ELIM_BW = NNRT_CORNER_ELIM_BW;   // columns per block (8: two four-column sub-blocks factored by the owner)
+static_assert(ELIM_WAVES == 0 || ELIM_WAVES == 4 || ELIM_WAVES == 8, "elimination waves");
+static_assert((ELIM_BW == 4 || ELIM_BW == 8) && TILE / ELIM_BW >= ELIM_WAVES, "elimination blocks");
+__device__ __forceinline__ void factor_block(f32x2* c4, int jb, int& bad) {
+	float M[4][4], Lu[4][4], rsv[4];
+#pragma unroll
+	for (int q = 0; q < 4; q++)
+#pragma unroll
+		for (int i = q; i < 4; i++) M[i][q] = lane_bcast(c4[q].x, jb + i);
+#pragma unroll
+	for (int q = 0; q < 4; q++) {
+		const float piv = M[q][q];   // (not clamped: a non-positive pivot flags the factorization, whose values are dropped)
+		bad |= !(piv > 0.f);
+		rsv[q] = __builtin_amdgcn_rsqf(piv);
+#pragma unroll
+		for (int i = q; i < 4; i++) Lu[i][q] = M[i][q] * rsv[q];
+#pragma unroll
+		for (int q2 = q + 1; q2 < 4; q2++)
+#pragma unroll
+			for (int i = q2; i < 4; i++) M[i][q2] = __builtin_fmaf(-Lu[i][q], Lu[q2][q], M[i][q2]);
+	}
+#pragma unroll
+	for (int q = 0; q < 4; q++) {
+		const f32x2 l = c4[q] * rsv[q];
+		c4[q] = l;
+		const f32x2 nl = -l;
+#pragma unroll
+		for (int q2 = q + 1; q2 < 4; q2++) {
+			const float lc = Lu[q2][q];
+			c4[q2] = __builtin_elementwise_fma(nl, f32x2{lc, lc}, c4[q2]);
+		}
+	}
+}
+
 // development timing build only (-DNNRT_CORNER_STAMPS, tools/dev/stamps_build.sh): shader-clock stamps of the first
 // workgroup of each factor launch at its phase boundaries, read back by nnrt_dev_corner_stamps
 #ifdef NNRT_CORNER_STAMPS
 // [level][workgroup][8]: shader clock at the phase boundaries 0-5 of every workgroup, the constant-rate clock at its start
 // (6) and end (7, bit 62 set for trailing tasks)
 __device__ unsigned long long g_corner_stamps[64][512][8];
+// [level][workgroup][block][4]: multi-wave elimination, shader clock of block b + 1's owner at the start of iteration b,
+// after its update by block b, after publishing block b + 1, and after the iteration's barrier
+__device__ unsigned long long g_elim_stamps[16][128][16][4];
+#define ELIM_STAMP(blk, i)                                                                                              \
+	do {                                                                                                                \
+		if (lane == 0 && a.level < 16 && blockIdx.x < 128 && (blk) < 16) g_elim_stamps[a.level][blockIdx.x][blk][i] = __builtin_amdgcn_s_memtime(); \
+	} while (0)
 #define CORNER_STAMP(i)                                                                                                  \
 	do {                                                                                                                 \
 		if (threadIdx.x == 0 && a.level < 64 && blockIdx.x < 512) g_corner_stamps[a.level][blockIdx.x][i] = __builtin_amdgcn_s_memtime(); \
@@ -751,6 +806,9 @@ __device__ unsigned long long g_corner_stamps[64][512][8];
 	} while (0)
 #define CORNER_STAMP(i) \
 	do {                \
+	} while (0)
+#define ELIM_STAMP(blk, i) \
+	do {                   \
 	} while (0)
 #endif
 
@@ -970,6 +1028,169 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 	}
 	__syncthreads();
 	CORNER_STAMP(1);
+#if NNRT_CORNER_ELIM_WAVES
+	const bool self_inv = diag && a.invert_self;   // the last level's diagonal tasks invert their own tile (all waves)
+	{
+		constexpr int BW = ELIM_BW, NBO = TILE / BW / ELIM_WAVES;   // block width, blocks per wave
+		constexpr int LW = 2 * BW;                                   // LDS words per row of a block's L columns
+		const int nb = (tk.nreal + BW - 1) / BW;    // blocks holding real columns (the rest is identity padding: kept)
+		float* const s_lb = s_stage + TERM_FLOATS;  // [3][64 rows][LW]: a block's L columns (A_JJ rows, then panel rows)
+		int bad = 0;
+		f32x2 ap[NBO][BW];
+		if (wave < ELIM_WAVES) {
+#pragma unroll
+			for (int k = 0; k < NBO; k++)
+#pragma unroll
+				for (int h = 0; h < BW; h += 4) {
+					const int c0 = BW * (k * ELIM_WAVES + wave) + h;
+					const float4 va = *reinterpret_cast<const float4*>(s_d + lane * CS4 + c0);
+					float4 vp;
+					if (diag)   // the augmented row: b_J on lane 0, zero elsewhere
+						vp = lane == 0 ? *reinterpret_cast<const float4*>(s_b + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
+					else
+						vp = *reinterpret_cast<const float4*>(s_p + lane * CS4 + c0);
+					ap[k][h] = f32x2{va.x, vp.x};
+					ap[k][h + 1] = f32x2{va.y, vp.y};
+					ap[k][h + 2] = f32x2{va.z, vp.z};
+					ap[k][h + 3] = f32x2{va.w, vp.w};
+				}
+		}
+		// block bb's owner: factor it (ap[bb / ELIM_WAVES], all of block bb - 1's updates applied) and publish its L columns
+		auto factor_publish = [&](int bb) {
+			f32x2* cb = ap[bb / ELIM_WAVES];
+			factor_block(cb, BW * bb, bad);
+			if (BW == 8) {   // the second sub-block: its columns updated by the first (multipliers by readlane), factored
+#pragma unroll
+				for (int q = 0; q < 4; q++) {
+					const f32x2 nq = -cb[q];
+#pragma unroll
+					for (int c = 4; c < 8; c++) {
+						const float lc = lane_bcast(cb[q].x, BW * bb + c);   // L_c,q
+						cb[c] = __builtin_elementwise_fma(nq, f32x2{lc, lc}, cb[c]);
+					}
+				}
+				factor_block(cb + 4, BW * bb + 4, bad);
+			}
+			float* const out = s_lb + (bb % 3) * (TILE * LW);
+#pragma unroll
+			for (int h = 0; h < BW; h += 4) {
+				*reinterpret_cast<float4*>(out + lane * LW + h) = make_float4(cb[h].x, cb[h + 1].x, cb[h + 2].x, cb[h + 3].x);
+				*reinterpret_cast<float4*>(out + lane * LW + BW + h) = make_float4(cb[h].y, cb[h + 1].y, cb[h + 2].y, cb[h + 3].y);
+			}
+		};
+		// block bb's columns of this wave's block k updated with block b's L columns (published in buf; nl: -this row's)
+		auto apply = [&](int k, int bb, const float* buf, const f32x2 (&nl)[BW]) {
+			float Lm[BW][BW];   // Lm[c][q] = L_c,q of column c of block bb, q of block b: wave-uniform reads
+#pragma unroll
+			for (int c = 0; c < BW; c++)
+#pragma unroll
+				for (int h = 0; h < BW; h += 4) {
+					const float4 v = *reinterpret_cast<const float4*>(buf + (BW * bb + c) * LW + h);
+					Lm[c][h] = v.x;
+					Lm[c][h + 1] = v.y;
+					Lm[c][h + 2] = v.z;
+					Lm[c][h + 3] = v.w;
+				}
+#pragma unroll
+			for (int q = 0; q < BW; q++)
+#pragma unroll
+				for (int c = 0; c < BW; c++) ap[k][c] = __builtin_elementwise_fma(nl[q], f32x2{Lm[c][q], Lm[c][q]}, ap[k][c]);
+		};
+		// -(this row's L columns of block bb)
+		auto row_l = [&](const float* buf, f32x2 (&nl)[BW]) {
+#pragma unroll
+			for (int h = 0; h < BW; h += 4) {
+				const float4 lx = *reinterpret_cast<const float4*>(buf + lane * LW + h);
+				const float4 ly = *reinterpret_cast<const float4*>(buf + lane * LW + BW + h);
+				nl[h] = f32x2{-lx.x, -ly.x};
+				nl[h + 1] = f32x2{-lx.y, -ly.y};
+				nl[h + 2] = f32x2{-lx.z, -ly.z};
+				nl[h + 3] = f32x2{-lx.w, -ly.w};
+			}
+		};
+		if (nb > 0 && wave == 0) factor_publish(0);
+		__syncthreads();
+		// per block b: block b + 1's owner applies block b to it first, factors and publishes it, and defers block b's
+		// updates of its other blocks to iteration b + 1 (before block b + 1's); every other wave applies block b to its
+		// later blocks. Three L buffers (block b's stays readable through iteration b + 1); one barrier per block.
+#pragma unroll
+		for (int b = 0; b < TILE / BW; b++) {
+			if (b < nb) {   // workgroup-uniform
+				const float* const buf = s_lb + (b % 3) * (TILE * LW);
+				if (wave < ELIM_WAVES) {
+					const bool owner = b >= 1 && wave == b % ELIM_WAVES;   // published block b in iteration b - 1
+					if (b >= 1 && owner) {   // its deferred updates by block b - 1
+						const float* const prev = s_lb + ((b - 1) % 3) * (TILE * LW);
+						f32x2 np[BW];
+						row_l(prev, np);
+#pragma unroll
+						for (int k = 0; k < NBO; k++) {
+							const int b2 = k * ELIM_WAVES + wave;
+							if (b2 > b && b2 < nb) apply(k, b2, prev, np);
+						}
+					}
+					f32x2 nl[BW];
+					row_l(buf, nl);
+					const bool next_owner = b + 1 < nb && wave == (b + 1) % ELIM_WAVES;
+					if (b + 1 < TILE / BW && next_owner) {
+						ELIM_STAMP(b + 1, 0);
+						apply((b + 1) / ELIM_WAVES, b + 1, buf, nl);
+						ELIM_STAMP(b + 1, 1);
+						factor_publish(b + 1);
+						ELIM_STAMP(b + 1, 2);
+					} else {
+#pragma unroll
+						for (int k = 0; k < NBO; k++) {
+							const int b2 = k * ELIM_WAVES + wave;
+							if (b2 > b && b2 < nb) apply(k, b2, buf, nl);   // wave-uniform
+						}
+					}
+				}
+				__syncthreads();
+				if (b + 1 < nb && wave == (b + 1) % ELIM_WAVES) ELIM_STAMP(b + 1, 3);
+			}
+		}
+		CORNER_STAMP(2);
+		CORNER_STAMP(3);
+		__syncthreads();   // every wave's s_d / s_p reads are done (also when no block was eliminated)
+		CORNER_STAMP(4);
+		if (wave < ELIM_WAVES) {
+#pragma unroll
+			for (int k = 0; k < NBO; k++)
+#pragma unroll
+			for (int h = 0; h < BW; h += 4) {
+				const int c0 = BW * (k * ELIM_WAVES + wave) + h;
+				const float4 vx = make_float4(ap[k][h].x, ap[k][h + 1].x, ap[k][h + 2].x, ap[k][h + 3].x);
+				const float4 vy = make_float4(ap[k][h].y, ap[k][h + 1].y, ap[k][h + 2].y, ap[k][h + 3].y);
+				if (diag) {
+					// the rows as eliminated (the part above the diagonal is not meaningful: the inverse reads the lower part
+					// only), and a copy in LDS with zeros above the diagonal: the pivot gate's and the inverse's input
+					*reinterpret_cast<float4*>(a.ldiag + static_cast<int64_t>(tk.J) * TILE_ELEMS + lane * TILE + c0) = vx;
+					*reinterpret_cast<float4*>(s_d + lane * CS4 + c0) =
+					    make_float4(c0 <= lane ? vx.x : 0.f, c0 + 1 <= lane ? vx.y : 0.f, c0 + 2 <= lane ? vx.z : 0.f, c0 + 3 <= lane ? vx.w : 0.f);
+					if (lane == 0) *reinterpret_cast<float4*>(a.cb + static_cast<int64_t>(tk.J) * TILE + c0) = vy;
+				} else {
+					*reinterpret_cast<float4*>(a.tiles + static_cast<int64_t>(tk.slot_t) * TILE_ELEMS + lane * TILE + c0) = vy;
+				}
+			}
+			if (diag && lane == 0 && bad) atomicOr(a.error_flag, 1);
+		}
+		if (diag && (a.pivot_word || self_inv)) {
+			__syncthreads();   // s_d complete
+			if (a.pivot_word && wave == 0) {   // the refinement gate: min over the tile of pivot (L_jj^2) / diag(S)_jj
+				const float ljj = s_d[lane * CS4 + lane];
+				const float ratio = sd > 0.f ? (ljj * ljj) / sd : 1.f;
+				// non-negative floats order like their bit patterns: a DPP integer minimum
+				const int rb = corner_wave_min_i32(__float_as_int(fmaxf(ratio, 0.f)));
+				if (lane == 0) atomicMin(a.pivot_word, static_cast<unsigned>(rb));
+			}
+		}
+		CORNER_STAMP(5);
+		CORNER_RT(7, 0ull);
+	}
+	if (self_inv) invert_lower_lds(s_d, s_b, a.minv + static_cast<int64_t>(tk.J) * TILE_ELEMS, t);
+	return;
+#else
 	// ap[c] = (A_JJ[lane][c], A_IJ[lane][c]): both rows see the same column operations, so one packed FMA
 	// (v_pk_fma_f32) updates the pair. Wave 0 holds them; the other waves join for the rank-32 update between the halves.
 	f32x2 ap[TILE];
@@ -1083,6 +1304,7 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 		__syncthreads();   // s_d: L_JJ, zeros above the diagonal
 		invert_lower_lds(s_d, s_b, a.minv + static_cast<int64_t>(tk.J) * TILE_ELEMS, t);
 	}
+#endif
 }
 
 // development timing build only (-DNNRT_CORNER_STAMPS): per role of the dataflow launch (its ticket), the constant-rate
@@ -1948,7 +2170,7 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		for (int l = 0; l < p.H; l++)
 			for (int q = p.level_off[static_cast<size_t>(l)]; q < p.level_off[static_cast<size_t>(l)] + p.level_panel[static_cast<size_t>(l)]; q++) {
 				const CornerTask& tk = p.tasks[static_cast<size_t>(q)];
-				if (tk.nreal > TILE / 2) exec_mfma_flops += 3 * 2 * 32 * 32 * 32;   // the rank-32 products of waves 1-3
+				if (ELIM_WAVES == 0 && tk.nreal > TILE / 2) exec_mfma_flops += 3 * 2 * 32 * 32 * 32;   // the rank-32 products of waves 1-3
 				if (tk.I == tk.J) elim_cols += tk.nreal;
 			}
 		dense_tiles = static_cast<int64_t>(corner_ld(6 * nc) / TILE) * (corner_ld(6 * nc) / TILE + 1) / 2;
@@ -2119,6 +2341,9 @@ extern "C" int nnrt_dev_flow_stamps(unsigned long long* out) {   // [128][66][4]
 }
 extern "C" int nnrt_dev_corner_stamps(unsigned long long* out) {   // [64][512][8] stamps of the last solve
 	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_corner_stamps), sizeof(unsigned long long) * 64 * 512 * 8) == hipSuccess ? 0 : 1;
+}
+extern "C" int nnrt_dev_elim_stamps(unsigned long long* out) {   // [16][128][16][4] stamps of the last solve
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_elim_stamps), sizeof(unsigned long long) * 16 * 128 * 16 * 4) == hipSuccess ? 0 : 1;
 }
 #endif
 

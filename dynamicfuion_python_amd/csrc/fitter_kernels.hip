@@ -1088,16 +1088,25 @@ __global__ __launch_bounds__(64) void k_solve_update(SolveArgs a) {
 //   the factor read back from LDS (replicated: one instruction serves all groups), and lane r stores entries r, r + 8.
 // Bit-identical to the one-lane-per-node kernel (the same float operations in the same order).
 constexpr int SOLVE_GL = 8;   // lanes per node
-__device__ __forceinline__ float group_bcast(float v, int j) {   // lane j of each 8-lane group (ds_swizzle bit mode)
-	// and-mask 0x18 keeps the group within the 32-lane half, or-mask j selects the lane: pattern and | or << 5
-	switch (j) {
-		case 0: return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x18 | (0 << 5)));
-		case 1: return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x18 | (1 << 5)));
-		case 2: return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x18 | (2 << 5)));
-		case 3: return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x18 | (3 << 5)));
-		case 4: return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x18 | (4 << 5)));
-		default: return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), 0x18 | (5 << 5)));
+// lane s of each quad (DPP quad_perm [s, s, s, s]); s is a constant after unrolling
+__device__ __forceinline__ int quad_bcast(int v, int s) {
+	switch (s) {
+		case 0: return __builtin_amdgcn_update_dpp(0, v, 0x00, 0xf, 0xf, false);
+		case 1: return __builtin_amdgcn_update_dpp(0, v, 0x55, 0xf, 0xf, false);
+		case 2: return __builtin_amdgcn_update_dpp(0, v, 0xAA, 0xf, 0xf, false);
+		default: return __builtin_amdgcn_update_dpp(0, v, 0xFF, 0xf, 0xf, false);
 	}
+}
+// lane j of each 8-lane group in VALU DPP moves, no LDS round trip (a ds_swizzle broadcast waited ~100 cycles on the
+// factor's critical chain; 0.8 us of the launch at C2): the quad holding lane j reads it by quad_perm, the other quad
+// reads the half-row mirror image (lane i <- lane 7 - i), where lane j sits at quad position 3 - (j & 3)
+__device__ __forceinline__ float group_bcast(float v, int j) {
+	const int iv = __builtin_bit_cast(int, v);
+	const int same = quad_bcast(iv, j & 3);
+	const int mirrored = __builtin_amdgcn_update_dpp(0, iv, 0x141, 0xf, 0xf, false);   // row_half_mirror
+	const int other = quad_bcast(mirrored, 3 - (j & 3));
+	const bool in_quad = static_cast<int>((threadIdx.x >> 2) & 1) == (j >> 2);
+	return __builtin_bit_cast(float, in_quad ? same : other);
 }
 
 template <int MODE, bool IDENTITY>
@@ -1167,9 +1176,9 @@ __global__ __launch_bounds__(64) void k_solve_update_lanes(SolveArgs a) {
 			const float ljk = group_bcast(h[k], j);   // L_jk
 			t -= h[k] * ljk;
 		}
-		const bool pos = group_bcast(t, j) > 0.f;   // the pivot test on lane j's value (uniform over the group)
-		bad |= !pos;
+		// the pivot test on lane j's t through its square root (t > 0 iff sqrt(t) > 0, NaN included): one broadcast
 		const float l = group_bcast(sqrtf(t), j);
+		bad |= !(l > 0.f);
 		if (r == j) h[j] = l;
 		else if (r > j) h[j] = t / l;
 	}

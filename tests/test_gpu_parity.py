@@ -569,11 +569,13 @@ def _new_fit(nn, sc, depth, iterations):
 # iteration 4 (condition ~1e9, both float solves 0.14 from fp64, one A7 NaN rotation) the iteration-5 system is positive
 # definite in fp64 with a pivot ratio below 1e-6: the oracle's natural-order float Cholesky breaks down, the GPU's
 # nested-dissection order does not (round 2's order broke down too) -- accepted as a one-sided breakdown, trajectory ends.
-# The C5 trajectory's solve errors vs the fp64 solution of its own system at iterations 1-3, measured 1.7e-6 / 1.8e-5 /
-# 1.0e-4 (round 5; iteration 3 refined, at an fp64 pivot ratio below REFINE_PIVOT_RATIO, where no 1e-4 rule applies):
-# pinned at 1.5x as regression bounds. Iteration 4 is degenerate (35 A7 NaN rotations, corner pivot /
+# The C5 trajectory's solve errors vs the fp64 solution of its own system at iterations 1-3, measured 1.6e-6 / 1.8e-5 /
+# 1.7e-4 (round 5, multi-wave panel elimination; iteration 3 at an fp64 pivot ratio 2.1e-8, below REFINE_PIVOT_RATIO, where
+# no 1e-4 rule applies; its corner pivot / diag(S) 7.7e-5 lies just under the refinement floor, so it is not refined --
+# the one-wave elimination's rounding put it above and refined it to 1.0e-4, a floor of 5e-5 refines it to 1.3e-4; the
+# oracle's own float solve is 6.8e-4 from fp64): pinned at 1.5x as regression bounds. Iteration 4 is degenerate (35 A7 NaN rotations, corner pivot /
 # diag(S) 3.8e-7 below the refinement floor, fp64 pivot ratio 7e-12): 0.011, the oracle's float solve 0.016.
-PINNED_SOLVE_ERRORS = {("C5", 1): 3e-6, ("C5", 2): 3e-5, ("C5", 3): 1.5e-4}
+PINNED_SOLVE_ERRORS = {("C5", 1): 3e-6, ("C5", 2): 3e-5, ("C5", 3): 2.6e-4}
 TRAJECTORIES = [("S1", 6, 6, None), ("C2", 2, 1, 2), ("C2_ARAP", 10, 4, None), ("C5", 6, 3, None)]
 
 

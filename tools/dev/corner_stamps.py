@@ -53,3 +53,27 @@ for lev in range(64):
     print(f"level {lev:2d}: {len(panels)} panel + {len(trailing)} trailing wgs, span {10 * (last_end - t0) / 1000:.2f} us "
           f"(last: {'trailing' if last in trailing else 'panel'} wg {last}); start spread {10 * start_spread / 1000:.2f} us; "
           f"slowest panel {10 * pspan[0] / 1000:.2f} us [{phases(w[pspan[1]])}]; slowest trailing {10 * tspan[0] / 1000:.2f} us")
+
+
+# multi-wave elimination (NNRT_CORNER_ELIM_WAVES > 0): per block of the slowest panel of levels 2-5, block b's owner's
+# cycles from the start of iteration b - 1 to its update by block b - 1, to publishing block b, to the barrier
+fe = getattr(lib, "nnrt_dev_elim_stamps", None)
+if fe is not None:
+    fe.argtypes = [ctypes.c_void_p]
+    eb = np.zeros((16, 128, 16, 4), np.uint64)
+    assert fe(eb.ctypes.data) == 0
+    for lev in range(2, 6):
+        w = buf[lev]
+        panels = [i for i in np.nonzero(w[:, 6])[0] if not int(w[i, 7]) >> 62 & 1 and i < 128]
+        if not panels:
+            continue
+        slow = max(panels, key=lambda i: (int(w[i, 7]) & MASK) - int(w[i, 6]))
+        rows = []
+        for blk in range(1, 16):
+            st = [int(x) for x in eb[lev, slow, blk]]
+            if st[0] and st[3]:
+                rows.append((st[1] - st[0], st[2] - st[1], st[3] - st[2]))
+        if rows:
+            r = np.array(rows)
+            print(f"level {lev} panel wg {slow}: per block (update, factor + publish, to barrier) mean {r.mean(0).round(0)} "
+                  f"over {len(rows)} blocks; first {rows[0]}, last {rows[-1]}")
