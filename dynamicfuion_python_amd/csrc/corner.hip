@@ -743,11 +743,22 @@ __device__ inline void eliminate_columns(f32x2 (&ap)[TILE], int lane, int& bad) 
 #ifndef NNRT_CORNER_ELIM_BW
 #define NNRT_CORNER_ELIM_BW 4
 #endif
+#ifndef NNRT_CORNER_ELIM_PRIO
+#define NNRT_CORNER_ELIM_PRIO 1
+#endif
+constexpr bool ELIM_PRIO = NNRT_CORNER_ELIM_PRIO != 0;   // the next block's owner at raised wave priority
 constexpr int ELIM_WAVES = NNRT_CORNER_ELIM_WAVES;
 constexpr int ELIM_BW = NNRT_CORNER_ELIM_BW;   // columns per block (8: two four-column sub-blocks factored by the owner)
 static_assert(ELIM_WAVES == 0 || ELIM_WAVES == 4 || ELIM_WAVES == 8, "elimination waves");
 static_assert((ELIM_BW == 4 || ELIM_BW == 8) && TILE / ELIM_BW >= ELIM_WAVES, "elimination blocks");
 __device__ __forceinline__ void factor_block(f32x2* c4, int jb, int& bad) {
+#ifdef NNRT_DEV_ELIM_NOFACTOR   // timing build only: no factorization (values meaningless)
+	(void)jb;
+	(void)bad;
+#pragma unroll
+	for (int q = 0; q < 4; q++) c4[q] = c4[q] * 0.5f;
+	return;
+#endif
 	float M[4][4], Lu[4][4], rsv[4];
 #pragma unroll
 	for (int q = 0; q < 4; q++)
@@ -787,10 +798,16 @@ __device__ unsigned long long g_corner_stamps[64][512][8];
 // [level][workgroup][block][4]: multi-wave elimination, shader clock of block b + 1's owner at the start of iteration b,
 // after its update by block b, after publishing block b + 1, and after the iteration's barrier
 __device__ unsigned long long g_elim_stamps[16][128][16][4];
+#ifdef NNRT_ELIM_STAMPS
 #define ELIM_STAMP(blk, i)                                                                                              \
 	do {                                                                                                                \
 		if (lane == 0 && a.level < 16 && blockIdx.x < 128 && (blk) < 16) g_elim_stamps[a.level][blockIdx.x][blk][i] = __builtin_amdgcn_s_memtime(); \
 	} while (0)
+#else
+#define ELIM_STAMP(blk, i) \
+	do {                   \
+	} while (0)
+#endif
 #define CORNER_STAMP(i)                                                                                                  \
 	do {                                                                                                                 \
 		if (threadIdx.x == 0 && a.level < 64 && blockIdx.x < 512) g_corner_stamps[a.level][blockIdx.x][i] = __builtin_amdgcn_s_memtime(); \
@@ -1073,39 +1090,32 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 			}
 			float* const out = s_lb + (bb % 3) * (TILE * LW);
 #pragma unroll
-			for (int h = 0; h < BW; h += 4) {
-				*reinterpret_cast<float4*>(out + lane * LW + h) = make_float4(cb[h].x, cb[h + 1].x, cb[h + 2].x, cb[h + 3].x);
-				*reinterpret_cast<float4*>(out + lane * LW + BW + h) = make_float4(cb[h].y, cb[h + 1].y, cb[h + 2].y, cb[h + 3].y);
-			}
+			for (int h = 0; h < BW; h += 2)   // row-major (A_JJ row, panel row) pairs: the f32x2 registers as they are
+				*reinterpret_cast<float4*>(out + lane * LW + 2 * h) = make_float4(cb[h].x, cb[h].y, cb[h + 1].x, cb[h + 1].y);
 		};
-		// block bb's columns of this wave's block k updated with block b's L columns (published in buf; nl: -this row's)
-		auto apply = [&](int k, int bb, const float* buf, const f32x2 (&nl)[BW]) {
-			float Lm[BW][BW];   // Lm[c][q] = L_c,q of column c of block bb, q of block b: wave-uniform reads
+		// block bb's columns of this wave's block k updated with block b's L columns (published in buf; l: this row's)
+		auto apply = [&](int k, int bb, const float* buf, const f32x2 (&l)[BW]) {
+			float Lm[BW][BW];   // Lm[c][q] = L_c,q of column c of block bb, q of block b: wave-uniform reads (A_JJ rows)
 #pragma unroll
 			for (int c = 0; c < BW; c++)
 #pragma unroll
-				for (int h = 0; h < BW; h += 4) {
-					const float4 v = *reinterpret_cast<const float4*>(buf + (BW * bb + c) * LW + h);
+				for (int h = 0; h < BW; h += 2) {
+					const float4 v = *reinterpret_cast<const float4*>(buf + (BW * bb + c) * LW + 2 * h);
 					Lm[c][h] = v.x;
-					Lm[c][h + 1] = v.y;
-					Lm[c][h + 2] = v.z;
-					Lm[c][h + 3] = v.w;
+					Lm[c][h + 1] = v.z;
 				}
 #pragma unroll
 			for (int q = 0; q < BW; q++)
 #pragma unroll
-				for (int c = 0; c < BW; c++) ap[k][c] = __builtin_elementwise_fma(nl[q], f32x2{Lm[c][q], Lm[c][q]}, ap[k][c]);
+				for (int c = 0; c < BW; c++) ap[k][c] = __builtin_elementwise_fma(-l[q], f32x2{Lm[c][q], Lm[c][q]}, ap[k][c]);
 		};
-		// -(this row's L columns of block bb)
-		auto row_l = [&](const float* buf, f32x2 (&nl)[BW]) {
+		// this row's L columns of a published block
+		auto row_l = [&](const float* buf, f32x2 (&l)[BW]) {
 #pragma unroll
-			for (int h = 0; h < BW; h += 4) {
-				const float4 lx = *reinterpret_cast<const float4*>(buf + lane * LW + h);
-				const float4 ly = *reinterpret_cast<const float4*>(buf + lane * LW + BW + h);
-				nl[h] = f32x2{-lx.x, -ly.x};
-				nl[h + 1] = f32x2{-lx.y, -ly.y};
-				nl[h + 2] = f32x2{-lx.z, -ly.z};
-				nl[h + 3] = f32x2{-lx.w, -ly.w};
+			for (int h = 0; h < BW; h += 2) {
+				const float4 v = *reinterpret_cast<const float4*>(buf + lane * LW + 2 * h);
+				l[h] = f32x2{v.x, v.y};
+				l[h + 1] = f32x2{v.z, v.w};
 			}
 		};
 		if (nb > 0 && wave == 0) factor_publish(0);
@@ -1134,9 +1144,11 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 					const bool next_owner = b + 1 < nb && wave == (b + 1) % ELIM_WAVES;
 					if (b + 1 < TILE / BW && next_owner) {
 						ELIM_STAMP(b + 1, 0);
+						if (ELIM_PRIO) __builtin_amdgcn_s_setprio(2);   // the critical path: ahead of the SIMD's other wave
 						apply((b + 1) / ELIM_WAVES, b + 1, buf, nl);
 						ELIM_STAMP(b + 1, 1);
 						factor_publish(b + 1);
+						if (ELIM_PRIO) __builtin_amdgcn_s_setprio(0);
 						ELIM_STAMP(b + 1, 2);
 					} else {
 #pragma unroll
@@ -1146,7 +1158,11 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 						}
 					}
 				}
+#ifdef NNRT_DEV_ELIM_NOBARRIER   // timing build only: no barrier per block (values meaningless)
+				__builtin_amdgcn_wave_barrier();
+#else
 				__syncthreads();
+#endif
 				if (b + 1 < nb && wave == (b + 1) % ELIM_WAVES) ELIM_STAMP(b + 1, 3);
 			}
 		}

@@ -8,7 +8,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["NNRT_LIB_PATH"] = os.path.join(ROOT, "tools", "dev", "libnnrt_stamps.so")
+os.environ["NNRT_LIB_PATH"] = os.environ.get("STAMPS_LIB", os.path.join(ROOT, "tools", "dev", "libnnrt_stamps.so"))
 sys.path[:0] = [ROOT]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
