@@ -367,6 +367,21 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 		auto it = contrib.find(std::make_tuple(launch, J, I));
 		return it == contrib.end() ? nullptr : &it->second;
 	};
+	// per column: its real rows, a prefix (every ND group starts on a tile boundary); else all 64
+	std::vector<int> col_real(static_cast<size_t>(T), TILE);
+	for (int J = 0; J < T && trim; J++) {
+		int nreal = 0;
+		for (int r = 0; r < TILE; r++) nreal += p.row_node[static_cast<size_t>(J) * TILE + r] >= 0;
+		for (int r = 0; r < TILE; r++)
+			if ((p.row_node[static_cast<size_t>(J) * TILE + r] >= 0) != (r < nreal)) nreal = TILE;
+		col_real[static_cast<size_t>(J)] = nreal;
+	}
+	// a term over source column k runs the MFMA steps s < its real columns (the 32 x 32 x 2 step s consumes k-columns s
+	// and 32 + s; the padding columns of L_Ik are exact zeros), in groups of four: srcs.w
+	auto src = [&](int a, int b, int k) {
+		const int nr = col_real[static_cast<size_t>(k)];
+		return make_int4(a, b, k, nr > TILE / 2 ? 8 : (nr + 3) / 4);
+	};
 	p.level_off.push_back(0);
 	for (int l = 0; l < p.H; l++) {
 		int panels = 0;
@@ -375,11 +390,7 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 			const std::vector<int>* dterms = terms(l, J, J);
 			std::vector<int> rows(1, J);
 			rows.insert(rows.end(), cs[static_cast<size_t>(J)].begin(), cs[static_cast<size_t>(J)].end());
-			int nreal = 0;   // the column's real rows, a prefix (every ND group starts on a tile boundary); else all 64
-			for (int r = 0; r < TILE; r++) nreal += p.row_node[static_cast<size_t>(J) * TILE + r] >= 0;
-			for (int r = 0; r < TILE; r++)
-				if ((p.row_node[static_cast<size_t>(J) * TILE + r] >= 0) != (r < nreal)) nreal = TILE;
-			if (!trim) nreal = TILE;
+			const int nreal = col_real[static_cast<size_t>(J)];
 			for (int I : rows) {
 				CornerTask t{};
 				t.I = I;
@@ -389,12 +400,12 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 				t.slot_d = slot(J, J);
 				t.src = static_cast<int>(p.srcs.size());
 				if (dterms)
-					for (int k : *dterms) p.srcs.push_back(make_int4(slot(J, k), slot(J, k), k, 0));
+					for (int k : *dterms) p.srcs.push_back(src(slot(J, k), slot(J, k), k));
 				t.nd = dterms ? static_cast<int>(dterms->size()) : 0;
 				if (I != J) {
 					const std::vector<int>* pterms = terms(l, J, I);
 					if (pterms)
-						for (int k : *pterms) p.srcs.push_back(make_int4(slot(I, k), slot(J, k), k, 0));
+						for (int k : *pterms) p.srcs.push_back(src(slot(I, k), slot(J, k), k));
 					t.np = pterms ? static_cast<int>(pterms->size()) : 0;
 				}
 				p.tasks.push_back(t);
@@ -412,7 +423,7 @@ static CornerPlan plan_corner(const int32_t* edges, int E, int n0, int N, const 
 			t.slot_t = slot(I, J);
 			t.slot_d = -1;
 			t.src = static_cast<int>(p.srcs.size());
-			for (int k : it->second) p.srcs.push_back(make_int4(slot(I, k), slot(J, k), k, 0));
+			for (int k : it->second) p.srcs.push_back(src(slot(I, k), slot(J, k), k));
 			t.nd = static_cast<int>(it->second.size());
 			p.tasks.push_back(t);
 		}
@@ -615,17 +626,32 @@ __device__ __forceinline__ void term_dma(const float* tiles, int4 s, float* buf,
 		}
 	}
 }
-// the term's 32 MFMA steps for quadrant (qr, qc) from a staged (swizzled) buffer
-__device__ __forceinline__ f32x16 term_mfma_lds(const float* buf, int qr, int qc, int lane, f32x16 acc) {
+// the term's MFMA steps for quadrant (qr, qc) from a staged (swizzled) buffer: the first 4 nq of the 32 (nq = srcs.w:
+// the steps past the source column's real columns multiply exact zeros, and adding them changes nothing)
+__device__ __forceinline__ f32x16 term_mfma_lds(const float* buf, int qr, int qc, int lane, f32x16 acc, int nq) {
 	const int half = lane >> 5, l32 = lane & 31;
 	const int rx = 32 * qr + l32, ry = 32 * qc + l32;
-	float4 vx[8], vy[8];
+	if (nq >= 8) {
+		float4 vx[8], vy[8];
+#pragma unroll
+		for (int q = 0; q < 8; q++) {
+			vx[q] = *reinterpret_cast<const float4*>(buf + rx * TILE + 4 * ((8 * half + q) ^ (rx & 15)));
+			vy[q] = *reinterpret_cast<const float4*>(buf + TILE_ELEMS + ry * TILE + 4 * ((8 * half + q) ^ (ry & 15)));
+		}
+		return term_mfma(vx, vy, acc);
+	}
 #pragma unroll
 	for (int q = 0; q < 8; q++) {
-		vx[q] = *reinterpret_cast<const float4*>(buf + rx * TILE + 4 * ((8 * half + q) ^ (rx & 15)));
-		vy[q] = *reinterpret_cast<const float4*>(buf + TILE_ELEMS + ry * TILE + 4 * ((8 * half + q) ^ (ry & 15)));
+		if (q < nq) {   // wave-uniform
+			const float4 vx = *reinterpret_cast<const float4*>(buf + rx * TILE + 4 * ((8 * half + q) ^ (rx & 15)));
+			const float4 vy = *reinterpret_cast<const float4*>(buf + TILE_ELEMS + ry * TILE + 4 * ((8 * half + q) ^ (ry & 15)));
+			acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx.x, vy.x, acc, 0, 0, 0);
+			acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx.y, vy.y, acc, 0, 0, 0);
+			acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx.z, vy.z, acc, 0, 0, 0);
+			acc = __builtin_amdgcn_mfma_f32_32x32x2f32(vx.w, vy.w, acc, 0, 0, 0);
+		}
 	}
-	return term_mfma(vx, vy, acc);
+	return acc;
 }
 
 // (L y) row t >> 2 for a 64 x 64 tile L and the 64-vector y: 4 threads per row, 16 columns each (all 4 get the sum)
@@ -988,7 +1014,7 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 			if (more) term_dma(a.tiles, src[e + 1], s_stage + ((e + 1) & 1) * TERM_FLOATS, w4, lane);
 			if (e < n_g) wait_vmcnt(more ? 8 : 0);
 			lds_barrier();
-			if (e < n_g) acc = term_mfma_lds(s_stage + (e & 1) * TERM_FLOATS, qr, qc, lane, acc);
+			if (e < n_g) acc = term_mfma_lds(s_stage + (e & 1) * TERM_FLOATS, qr, qc, lane, acc, src[e].w);
 			lds_barrier();
 		}
 		if (wave < 4) {
@@ -1032,7 +1058,7 @@ __global__ __launch_bounds__(CTF) void k_corner_factor(CornerFactorArgs a) {
 			if (more) term_dma(a.tiles, src_g[e + 1], bufs + ((e + 1) & 1) * TERM_FLOATS, w4, lane);
 			if (e < n_g) wait_vmcnt(more ? 8 : 0);   // this wave's pieces of term e have landed
 			lds_barrier();                           // every wave's have
-			if (e < n_g) acc = term_mfma_lds(bufs + (e & 1) * TERM_FLOATS, qr, qc, lane, acc);
+			if (e < n_g) acc = term_mfma_lds(bufs + (e & 1) * TERM_FLOATS, qr, qc, lane, acc, src_g[e].w);
 			lds_barrier();                           // term e's buffer is read: round e + 1 refills it
 		}
 		if (g == 0 || !diag) {   // s_t = A - sum of the terms (the quadrant of term_mfma's C / D layout)
@@ -2181,7 +2207,8 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		back_pre_off = p.back_pre_off;
 		fill_tiles = static_cast<int64_t>(slots);
 		n_terms = static_cast<int64_t>(p.srcs.size());
-		exec_mfma_flops = n_terms * 2 * TILE * TILE * TILE;
+		exec_mfma_flops = 0;
+		for (const int4& q : p.srcs) exec_mfma_flops += static_cast<int64_t>(q.w) * 4 * 2 * TILE * TILE * 2;   // 4 nq steps of 64 x 64 x 2
 		elim_cols = 0;
 		for (int l = 0; l < p.H; l++)
 			for (int q = p.level_off[static_cast<size_t>(l)]; q < p.level_off[static_cast<size_t>(l)] + p.level_panel[static_cast<size_t>(l)]; q++) {
