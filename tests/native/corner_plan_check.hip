@@ -57,7 +57,16 @@ int main(int argc, char** argv) {
 			const bool panel = q - p.level_off[l] < p.level_panel[l];
 			std::set<std::pair<int,int>> r, w;
 			const int4* src = &p.srcs[tk.src];
-			auto upd = [&](double* out, const double* A, const int4* s, int n) { for (int i=0;i<TILE;i++) for(int j=0;j<TILE;j++){ double v = A[i*TILE+j]; for (int e=0;e<n;e++){ const double* X = tile(s[e].x); const double* Y = tile(s[e].y); for(int k=0;k<TILE;k++) v -= X[i*TILE+k]*Y[j*TILE+k]; r.insert({0,s[e].x}); r.insert({0,s[e].y}); } out[i*TILE+j]=v; } };
+			// a term runs the MFMA steps s < 4 srcs.w only (k-columns s and 32 + s): the skipped ones must be padding
+			for (int e = 0; e < tk.nd + tk.np; e++) {
+				const int4 q = src[e];
+				if (q.w < 1 || q.w > 8) { printf("term step groups %d out of range\n", q.w); return 1; }
+				if (q.w < 8)
+					for (int k = 4 * q.w; k < TILE; k++)
+						if (p.row_node[(size_t)q.z * TILE + k] >= 0) { printf("term over column %d skips its real column %d\n", q.z, k); return 1; }
+			}
+			auto kin = [](int w, int k) { return w >= 8 || (k & 31) < 4 * w; };
+			auto upd = [&](double* out, const double* A, const int4* s, int n) { for (int i=0;i<TILE;i++) for(int j=0;j<TILE;j++){ double v = A[i*TILE+j]; for (int e=0;e<n;e++){ const double* X = tile(s[e].x); const double* Y = tile(s[e].y); for(int k=0;k<TILE;k++) if (kin(s[e].w, k)) v -= X[i*TILE+k]*Y[j*TILE+k]; r.insert({0,s[e].x}); r.insert({0,s[e].y}); } out[i*TILE+j]=v; } };
 			auto rhsu = [&](int J, const int4* s, int n) { std::vector<double> o(TILE); for (int i=0;i<TILE;i++){ double v = cb[J*TILE+i]; for(int e=0;e<n;e++){ const double* X = tile(s[e].x); for (int k=0;k<TILE;k++) v -= X[i*TILE+k]*cb[s[e].z*TILE+k]; r.insert({2,s[e].z}); r.insert({0,s[e].x}); } o[i]=v; } return o; };
 			if (!panel) {
 				std::vector<double> o(TE); upd(o.data(), tile(tk.slot_t), src, tk.nd); r.insert({0,tk.slot_t}); w.insert({0,tk.slot_t});
