@@ -55,7 +55,7 @@ def dist_env():
 def max_over_ranks(value: float, device=None) -> float:
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return float(value)
     t = torch.tensor([float(value)], dtype=torch.float64, device=device if device is not None else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -65,11 +65,12 @@ def max_over_ranks(value: float, device=None) -> float:
 MIN_WARM_S = 0.05   # seconds of untimed back-to-back GPU work before the timed region (clock ramp-up)
 
 
-def timed_region(step, launches: int, per_launch: int, world: int, sync) -> tuple:
+def timed_region(step, launches: int, per_launch: int, world: int, sync, dist_on=None) -> tuple:
     """The timed protocol: barrier + device sync, `launches` x step(per_launch), device sync, barrier. Returns (OR of
-    the step return codes, this rank's elapsed seconds)."""
+    the step return codes, this rank's elapsed seconds). dist_on: barriers on (default: world > 1)."""
     import torch.distributed as dist
-    if world > 1:
+    dist_on = world > 1 if dist_on is None else dist_on
+    if dist_on:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
@@ -78,7 +79,7 @@ def timed_region(step, launches: int, per_launch: int, world: int, sync) -> tupl
         bad |= step(per_launch)
     sync()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         dist.barrier()
     return bad, elapsed
 
@@ -87,7 +88,7 @@ def exchange_per_rank(steps: int, elapsed: float, update_norm: float, device=Non
     """End-of-run all-gather of per-rank (iterations/s, seconds, final |update|); None at N = 1."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return None
     mine = torch.tensor([steps / elapsed, elapsed, update_norm], dtype=torch.float64, device=device if device is not None else "cpu")
     got = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
@@ -372,7 +373,10 @@ def main(argv=None):
     local_dev = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
-    if world > 1:
+    # NNRT_BENCH_DIST_ONE_RANK=1: the process group, barriers and collectives also at WORLD_SIZE 1 (a one-GPU box can
+    # run the RCCL branch itself: torch.distributed.run --nproc-per-node 1)
+    use_dist = world > 1 or os.environ.get("NNRT_BENCH_DIST_ONE_RANK") == "1"
+    if use_dist:
         if backend == "gloo":
             dist.init_process_group(backend="gloo")
         else:
@@ -465,7 +469,7 @@ def main(argv=None):
 
     launches = -(-args.steps // per_launch)
     args.steps = launches * per_launch   # whole graphs only: the timed step count is rounded up to a multiple
-    bad, elapsed = timed_region(step, launches, per_launch, world, lambda: torch.cuda.synchronize(dev))
+    bad, elapsed = timed_region(step, launches, per_launch, world, lambda: torch.cuda.synchronize(dev), dist_on=use_dist)
     if bad:
         NV.check(bad)
     per_replica = []
@@ -600,7 +604,7 @@ def main(argv=None):
                    "parallelism": f"replicas{world * R}" if world * R > 1 else "single", "replicas_per_gpu": R,
                    **({"collectives": "rccl" if backend == "nccl" else f"{backend} (rehearsal: {world} ranks on "
                                                                        f"{torch.cuda.device_count()} visible GPU(s))"}
-                      if world > 1 else {})},
+                      if use_dist else {})},
         "setup_ms": round(setup_ms, 3),
         "kernel_ms": {k: (round(v, 5) if v else None) for k, v in ktimes.items()},
         "kernel_ms_note": f"nnrt_fitter_time_kernels: per-iteration device time of each kernel in its real context, by differences "
@@ -658,7 +662,7 @@ def main(argv=None):
         out["cpu_baseline"]["host"]["omp_num_threads_env"] = os.environ.get("OMP_NUM_THREADS")
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
 
