@@ -87,6 +87,16 @@ __global__ __launch_bounds__(256) void k_arrow_prepare(int N, float lm, double* 
 // of every fourth of the node's edges), in one launch with the corner init (the last init_blocks blocks: corner.hip's
 // corner_init_thread; both read the prepared diagonal blocks and write disjoint outputs) ----
 constexpr int STEM_LANES = 4;
+// lane s of each quad (DPP quad_perm [s, s, s, s]); s is a constant after unrolling
+__device__ __forceinline__ float stem_quad_bcast(float v, int s) {
+	const int x = __builtin_bit_cast(int, v);
+	switch (s) {
+		case 0: return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x00, 0xf, 0xf, false));
+		case 1: return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x55, 0xf, 0xf, false));
+		case 2: return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0xAA, 0xf, 0xf, false));
+		default: return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0xFF, 0xf, 0xf, false));
+	}
+}
 // stem node i, lane sub of its STEM_LANES: Cholesky of the prepared block f (potrf semantics: a failure sets the error
 // flag), D_i^-1 (lane 0 stores it) and D_i^-1 B_e for every STEM_LANES-th of its edges
 __device__ __forceinline__ void stem_factor(int i, int sub, const float (&f)[36], const int* __restrict__ edge_offsets, const int* __restrict__ edge_list,
@@ -98,8 +108,23 @@ __device__ __forceinline__ void stem_factor(int i, int sub, const float (&f)[36]
 		if (sub == 0) atomicOr(error_flag, 1);
 		return;
 	}
+	// D_i^-1 one potrs per identity column (invert_from_cholesky_small's operations), the columns dealt over the node's
+	// four lanes (columns sub and sub + 4) and broadcast within the quad by DPP: a third of the dependent divisions per
+	// lane, bit-identical
+	static_assert(STEM_LANES == 4, "quad broadcasts");
+	float cv[2][6];
+#pragma unroll
+	for (int k = 0; k < 2; k++) {
+		const int c = sub + 4 * k;   // (6, 7: an all-zero column, never broadcast)
+#pragma unroll
+		for (int r = 0; r < 6; r++) cv[k][r] = r == c ? 1.f : 0.f;
+		cholesky_solve_small<6>(L, cv[k]);
+	}
 	float Di[6][6];
-	invert_from_cholesky_small<6>(L, Di);
+#pragma unroll
+	for (int c = 0; c < 6; c++)
+#pragma unroll
+		for (int r = 0; r < 6; r++) Di[r][c] = stem_quad_bcast(cv[c / 4][r], c % 4);
 	if (sub == 0) {
 		float4* o4 = reinterpret_cast<float4*>(dinv + static_cast<int64_t>(i) * 36);
 #pragma unroll
