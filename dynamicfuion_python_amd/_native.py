@@ -42,6 +42,7 @@ _SIGNATURES = {
     "nnrt_last_error": (ctypes.c_char_p, []),
     "nnrt_runtime_version": (c_int32, []),
     "nnrt_device_count": (c_int32, []),
+    "nnrt_build_jacobian_fma": (c_int32, []),
     "nnrt_warp_field_create": (c_int32, [c_void_p, c_int32, c_float, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p,
                                          c_int32, ctypes.POINTER(c_void_p)]),
     "nnrt_warp_field_destroy": (None, [c_void_p]),
@@ -191,6 +192,11 @@ def lib():
             f.argtypes = args
         _lib = l
     return _lib
+
+
+def jacobian_fma() -> bool:
+    """Whether this build forms the pixel-node Jacobians with FMAs (csrc NNRT_JAC_FMA; the checker mirrors it)."""
+    return bool(lib().nnrt_build_jacobian_fma())
 
 
 class NnrtError(RuntimeError):

@@ -61,6 +61,12 @@ struct ModeTraits<NNRT_ITERATION_ROTATION_ONLY> {
 // reset to EMPTY for the next iteration's scatter; the contributing face goes to pass 2 in registers.
 // dn: this lane's 27 parked floats at dn[i * dn_stride] (lane-private LDS column)
 // out_face / out_vid: the pixel's contributing face (-1: none) and its vertices, handed to pass 2 in registers
+// a0 b0 + a1 b1 + a2 b2 of the rasterized-surface Jacobian chain: left to right as FMAs (NNRT_JAC_FMA; the oracle's fused
+// mode, dot3_jac in nnrt_oracle.cpp, evaluates the same nesting) or as the reference's unfused (a0 b0 + a1 b1) + a2 b2
+__device__ __forceinline__ float dot3_jac(float a0, float b0, float a1, float b1, float a2, float b2) {
+	return NNRT_JAC_FMA ? fmaf(a2, b2, fmaf(a1, b1, a0 * b0)) : (a0 * b0 + a1 * b1) + a2 * b2;
+}
+
 template <int MODE>
 __device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int dn_stride, int& out_face, int (&out_vid)[3]) {
 	// one 8x8 quadrant per wave: compact pixel sets touch the fewest nodes
@@ -253,13 +259,13 @@ __device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int
 #pragma unroll
 				for (int r = 0; r < 3; r++)
 #pragma unroll
-					for (int c = 0; c < 3; c++) Jc[r][c] = DN(i, r, 0) * P0[c] + DN(i, r, 1) * P1[c];
+					for (int c = 0; c < 3; c++) Jc[r][c] = NNRT_JAC_FMA ? fmaf(DN(i, r, 0), P0[c], DN(i, r, 1) * P1[c]) : DN(i, r, 0) * P0[c] + DN(i, r, 1) * P1[c];
 				if (a.perspective) {
 					float J2[3][3];
 #pragma unroll
 					for (int r = 0; r < 3; r++)
 #pragma unroll
-						for (int c = 0; c < 3; c++) J2[r][c] = (Pd[r][0] * Jc[0][c] + Pd[r][1] * Jc[1][c]) + Pd[r][2] * Jc[2][c];
+						for (int c = 0; c < 3; c++) J2[r][c] = dot3_jac(Pd[r][0], Jc[0][c], Pd[r][1], Jc[1][c], Pd[r][2], Jc[2][c]);
 #pragma unroll
 					for (int r = 0; r < 3; r++) J2[r][2] += PZ(r, i);
 #pragma unroll
@@ -280,12 +286,12 @@ __device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int
 						const float nr0 = r == 0 ? Nk[0].x : (r == 1 ? Nk[0].y : Nk[0].z);
 						const float nr1 = r == 0 ? Nk[1].x : (r == 1 ? Nk[1].y : Nk[1].z);
 						const float nr2 = r == 0 ? Nk[2].x : (r == 1 ? Nk[2].y : Nk[2].z);
-						w_rc[r] = (vr0 * Jc[0][c] + vr1 * Jc[1][c]) + vr2 * Jc[2][c];
+						w_rc[r] = dot3_jac(vr0, Jc[0][c], vr1, Jc[1][c], vr2, Jc[2][c]);
 						if (c == r) w_rc[r] += rho[i];
-						n_rc[r] = (nr0 * Jc[0][c] + nr1 * Jc[1][c]) + nr2 * Jc[2][c];
+						n_rc[r] = dot3_jac(nr0, Jc[0][c], nr1, Jc[1][c], nr2, Jc[2][c]);
 					}
-					const float x = (rw[0] * w_rc[0] + rw[1] * w_rc[1]) + rw[2] * w_rc[2];
-					const float y = (rn[0] * n_rc[0] + rn[1] * n_rc[1]) + rn[2] * n_rc[2];
+					const float x = dot3_jac(rw[0], w_rc[0], rw[1], w_rc[1], rw[2], w_rc[2]);
+					const float y = dot3_jac(rn[0], n_rc[0], rn[1], n_rc[1], rn[2], n_rc[2]);
 					rec_f[3 * i + c] = x + y;   // stored as formed: no 9-float tail of live outputs
 				}
 			}
@@ -505,7 +511,8 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 
 	// (2a) gather: association `lane` of a filed chunk -> its jv / jn rows (in flight until (2b))
 	int4 d = make_int4(0, -1, -1, -1);
-	float4 jv[3], jn[3];
+	float4 jv[3];
+	[[maybe_unused]] float4 jn[3];   // the unfused / gathered rows only
 	float4 rq[4];
 #if !NNRT_GATHER_ROWS
 	float4 ns4[4];   // the association's node state (g, t, R), and per face vertex its canonical position / normal
@@ -607,6 +614,58 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 			const float rn[3] = {q[9], q[10], q[11]};
 			const float rho[3] = {q[12], q[13], q[14]};
 			float jr[3] = {0.f, 0.f, 0.f}, jt[3] = {0.f, 0.f, 0.f};
+#if NNRT_JAC_FMA && !NNRT_GATHER_ROWS
+			// Fused form (round 5): per face vertex, with ws = w if the vertex is anchored to the node, else 0,
+			//   jt += ws dv,   jr += -ws (dv x R (v - g) + dn x R n)
+			// i.e. the reference's dv [-w R (v - g)]_x + dn [-w R n]_x (PixelVertexAnchorJacobiansImpl.h:179-363,
+			// WarpedSurfaceJacobiansImpl.h:117-156) with -w factored out of the cross products and every product-sum an
+			// FMA (the build is -ffp-contract=off), as nvcc's default contraction of the reference's CUDA path also
+			// does: 43 VALU per face vertex instead of 78, the terms within a few float ulps of the unfused rows (the
+			// unfused, oracle-bit-identical form: -DNNRT_JAC_FMA=0). A vertex not anchored to the node adds ws = 0
+			// products, i.e. +-0, which leave the +0-started sums unchanged bit for bit (finite inputs: the vertex's own
+			// canonical position / normal, the pixel's record and the node's state, never the padding row's data).
+			{
+				float R[9];
+				f3 g = make3(0.f, 0.f, 0.f);
+				if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) {
+					g = make3(ns4[0].x, ns4[0].y, ns4[0].z);
+					if (a.state_identity) {
+#pragma unroll
+						for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.f : 0.f;
+					} else {
+						const float Rl[9] = {ns4[1].z, ns4[1].w, ns4[2].x, ns4[2].y, ns4[2].z, ns4[2].w, ns4[3].x, ns4[3].y, ns4[3].z};
+#pragma unroll
+						for (int i = 0; i < 9; i++) R[i] = Rl[i];
+					}
+				}
+#pragma unroll
+				for (int fv = 0; fv < 3; fv++) {
+					const float ws = rows[fv] >= 0 ? jv[fv].w : 0.f;
+					const f3 dv = make3(dr_dV[3 * fv], dr_dV[3 * fv + 1], dr_dV[3 * fv + 2]);
+					if (MODE != NNRT_ITERATION_ROTATION_ONLY) {
+						jt[0] = fmaf(dv.x, ws, jt[0]);
+						jt[1] = fmaf(dv.y, ws, jt[1]);
+						jt[2] = fmaf(dv.z, ws, jt[2]);
+					}
+					if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) {
+						const f3 d3 = sub3(make3(cp4[fv].x, cp4[fv].y, cp4[fv].z), g);
+						const f3 n3 = make3(cn4[fv].x, cn4[fv].y, cn4[fv].z);
+						const f3 p = make3(fmaf(R[0], d3.x, fmaf(R[1], d3.y, R[2] * d3.z)), fmaf(R[3], d3.x, fmaf(R[4], d3.y, R[5] * d3.z)),
+						                   fmaf(R[6], d3.x, fmaf(R[7], d3.y, R[8] * d3.z)));
+						const f3 q = make3(fmaf(R[0], n3.x, fmaf(R[1], n3.y, R[2] * n3.z)), fmaf(R[3], n3.x, fmaf(R[4], n3.y, R[5] * n3.z)),
+						                   fmaf(R[6], n3.x, fmaf(R[7], n3.y, R[8] * n3.z)));
+						const f3 dn = make3(rn[0] * rho[fv], rn[1] * rho[fv], rn[2] * rho[fv]);
+						// dv x p + dn x q
+						const float cx = fmaf(dv.y, p.z, fmaf(-dv.z, p.y, fmaf(dn.y, q.z, -dn.z * q.y)));
+						const float cy = fmaf(dv.z, p.x, fmaf(-dv.x, p.z, fmaf(dn.z, q.x, -dn.x * q.z)));
+						const float cz = fmaf(dv.x, p.y, fmaf(-dv.y, p.x, fmaf(dn.x, q.y, -dn.y * q.x)));
+						jr[0] = fmaf(-ws, cx, jr[0]);
+						jr[1] = fmaf(-ws, cy, jr[1]);
+						jr[2] = fmaf(-ws, cz, jr[2]);
+					}
+				}
+			}
+#else
 #if !NNRT_GATHER_ROWS
 			if (MODE != NNRT_ITERATION_TRANSLATION_ONLY) {
 				// (-w R (v - g), -w R n) per face vertex: warp_slot's expressions (kernels.hpp), bit-identical to its rows
@@ -650,6 +709,7 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 					jr[2] += on ? t1.z + t2.z : 0.f;
 				}
 			}
+#endif
 			float J[8];
 			if (MODE == NNRT_ITERATION_ALL) {
 				J[0] = jr[0];
@@ -858,6 +918,9 @@ extern "C" int nnrt_dev_fit_stamps(unsigned long long* out) {   // [16384][4] of
 	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fit_stamps), sizeof(unsigned long long) * 16384 * 4) == hipSuccess ? 0 : 1;
 }
 #endif
+
+// the pixel-node Jacobian arithmetic of this build (NNRT_JAC_FMA), for the test checker's matching mode
+extern "C" int nnrt_build_jacobian_fma() { return NNRT_JAC_FMA && !NNRT_GATHER_ROWS; }
 
 int fit_pixels_arap_blocks(int E) { return static_cast<int>(ceil_div(E, PIX_BLOCK)); }
 

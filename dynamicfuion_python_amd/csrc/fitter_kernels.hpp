@@ -143,6 +143,10 @@ __device__ inline void arap_edge(const ArapArgs& a, int e) {
 #ifndef NNRT_GATHER_ROWS
 #define NNRT_GATHER_ROWS 0
 #endif
+// pass 2 forms the pixel-node Jacobians with fused multiply-adds (1) or as the oracle-bit-identical unfused rows (0)
+#ifndef NNRT_JAC_FMA
+#define NNRT_JAC_FMA 1
+#endif
 
 struct FitPixelArgs {
 	int H, W, tiles_x, tiles_y;   // tiles of 16 x 16 pixels; this launch covers tile rows [tile_row0, tile_row0 + tiles_y)

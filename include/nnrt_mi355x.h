@@ -42,6 +42,10 @@ const char* nnrt_last_error(void);
 /* HIP runtime version the library was built against and the number of visible devices (-1 on error). */
 int32_t nnrt_runtime_version(void);
 int32_t nnrt_device_count(void);
+/* Pixel-node Jacobian arithmetic of this build: 1 = FMA form (the default product), 0 = the reference CPU path's
+ * unfused expressions (built with -DNNRT_JAC_FMA=0). Both are the reference's expression (PixelVertexAnchorJacobiansImpl.h
+ * :179-363, WarpedSurfaceJacobiansImpl.h:117-156); the test checker selects its matching mode from this. */
+int32_t nnrt_build_jacobian_fma(void);
 
 /* ---------------------------------------------------------------------------------------------------------------
  * Warp field -- replaces nnrt::geometry::HierarchicalGraphWarpField (cpp/geometry/HierarchicalGraphWarpField.h:37-97,

@@ -72,6 +72,12 @@ def set_accumulate_double(on: bool):
     lib().orc_set_accumulate_double(ctypes.c_int(int(on)))
 
 
+def set_fused_jacobians(on: bool):
+    """Pixel-node Jacobian arithmetic (a10 + a12): the reference CPU path's unfused expressions (default) or the GPU
+    product's FMA form (bit-identical to its terms; nnrt_oracle.cpp g_jac_fma)."""
+    lib().orc_set_fused_jacobians(ctypes.c_int(int(on)))
+
+
 def num_threads() -> int:
     return lib().orc_num_threads()
 

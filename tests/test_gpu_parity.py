@@ -327,6 +327,32 @@ def test_fit_one_iteration_parity(nn, S, oracle_mod, name):
     assert rel_err(wf.get_node_rotations(True) - np.eye(3), R_o - np.eye(3)) < 1e-4
 
 
+@pytest.mark.parametrize("name", ["S1", "C1", "C2"])
+def test_fused_jacobians_vs_reference_arithmetic(nn, S, oracle_mod, name):
+    """north_star's bar against the reference CPU path's own arithmetic: the GPU forms the pixel-node Jacobians as FMA
+    chains (csrc/fitter_kernels.hip NNRT_JAC_FMA; the other GPU tests check it against the oracle's bit-identical fused
+    mode), the reference's CPU build as unfused products (the oracle's default, restored here). On identical inputs the
+    rasterization and mask agree exactly, residuals to 1e-6 absolute, node updates and motion to north_star's 1e-4
+    relative, and the assembled H / g to 1e-5 relative (per-term rounding of a few ulps, summed over a node's pixels)."""
+    oracle_mod.set_fused_jacobians(False)
+    sc = _scene(S, oracle_mod, name)
+    depth = scene_target(oracle_mod, sc)
+    R_o, t_o, dg_o = oracle_fit_scene(oracle_mod, sc, depth, 1)
+    wf, ft, dg_g = _gpu_fit(nn, sc, depth, 1)
+    N = len(sc.nodes)
+    assert np.array_equal(dg_o["pixel_faces"].astype(np.int64), dg_g["pixel_faces"].astype(np.int64))
+    assert np.array_equal(dg_o["residual_mask"], dg_g["residual_mask"])
+    assert np.allclose(dg_o["residuals"], dg_g["residuals"], rtol=0, atol=1e-6, equal_nan=True)
+    h_err = nan_rel_err(dg_g["hessian"][: N * 36], dg_o["hessian_diag"])
+    g_err = nan_rel_err(dg_g["gradient"][: N * 6], dg_o["gradient"])
+    u_err = nan_rel_err(dg_g["updates"][: N * 6], dg_o["updates"])
+    print(f"{name}: reference arithmetic vs fused GPU: H {h_err:.2g}, g {g_err:.2g}, updates {u_err:.2g}")
+    assert h_err < 1e-5 and g_err < 1e-5
+    assert u_err < 1e-4
+    assert rel_err(wf.get_node_translations(True), t_o) < 1e-4
+    assert rel_err(wf.get_node_rotations(True) - np.eye(3), R_o - np.eye(3)) < 1e-4
+
+
 @pytest.mark.parametrize("name,mode", [("C2", "ALL"), ("C1", "TRANSLATION_ONLY"), ("C1", "ROTATION_ONLY")])
 def test_block_diagonal_update_bit_exact(nn, S, oracle_mod, name, mode):
     """The block-diagonal solve + update (k_solve_update_lanes: 8 lanes per node, lane r forming row r of the factor)
@@ -575,7 +601,12 @@ def _new_fit(nn, sc, depth, iterations):
 # the one-wave elimination's rounding put it above and refined it to 1.0e-4, a floor of 5e-5 refines it to 1.3e-4; the
 # oracle's own float solve is 6.8e-4 from fp64): pinned at 1.5x as regression bounds. Iteration 4 is degenerate (35 A7 NaN rotations, corner pivot /
 # diag(S) 3.8e-7 below the refinement floor, fp64 pivot ratio 7e-12): 0.011, the oracle's float solve 0.016.
+# The FMA-formed Jacobians (csrc NNRT_JAC_FMA, the product build) assemble a system a few float ulps away per term, and
+# from iteration 2 on the trajectory visits different states (iteration 2: 1 A7 NaN rotation; iteration 3: fp64 pivot
+# ratio 7.4e-9, corner pivot / diag(S) 7.5e-5, unrefined): measured 1.6e-6 / 2.5e-5 / 1.04e-3, the oracle's own float
+# solve of that iteration-3 system 6.0e-4 from fp64. Each build's trajectory is pinned at its own measurement.
 PINNED_SOLVE_ERRORS = {("C5", 1): 3e-6, ("C5", 2): 3e-5, ("C5", 3): 2.6e-4}
+PINNED_SOLVE_ERRORS_FMA = {("C5", 1): 3e-6, ("C5", 2): 3e-5, ("C5", 3): 1.6e-3}
 TRAJECTORIES = [("S1", 6, 6, None), ("C2", 2, 1, 2), ("C2_ARAP", 10, 4, None), ("C5", 6, 3, None)]
 
 
@@ -594,7 +625,8 @@ def test_fit_state_synchronised_trajectory(nn, S, oracle_mod, name, iterations, 
         status, err, e_own = _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k)
         print(f"{name} iteration {k + 1}: {status}, update rel err {err}, NaN rotations before {nan_before}", flush=True)
         report.append((k + 1, status, err))
-        pin = PINNED_SOLVE_ERRORS.get((name, k + 1))
+        from dynamicfuion_python_amd import _native
+        pin = (PINNED_SOLVE_ERRORS_FMA if _native.jacobian_fma() else PINNED_SOLVE_ERRORS).get((name, k + 1))
         if pin is not None:   # the refined solve's measured error vs fp64 as a regression bound
             assert e_own is not None and e_own <= pin, f"{name} iteration {k + 1}: solve error vs fp64 {e_own} above its pinned {pin:.3g}"
         if status.startswith("potrf"):
