@@ -61,12 +61,6 @@ struct ModeTraits<NNRT_ITERATION_ROTATION_ONLY> {
 // reset to EMPTY for the next iteration's scatter; the contributing face goes to pass 2 in registers.
 // dn: this lane's 27 parked floats at dn[i * dn_stride] (lane-private LDS column)
 // out_face / out_vid: the pixel's contributing face (-1: none) and its vertices, handed to pass 2 in registers
-// a0 b0 + a1 b1 + a2 b2 of the rasterized-surface Jacobian chain: left to right as FMAs (NNRT_JAC_FMA; the oracle's fused
-// mode, dot3_jac in nnrt_oracle.cpp, evaluates the same nesting) or as the reference's unfused (a0 b0 + a1 b1) + a2 b2
-__device__ __forceinline__ float dot3_jac(float a0, float b0, float a1, float b1, float a2, float b2) {
-	return NNRT_JAC_FMA ? fmaf(a2, b2, fmaf(a1, b1, a0 * b0)) : (a0 * b0 + a1 * b1) + a2 * b2;
-}
-
 template <int MODE>
 __device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int dn_stride, int& out_face, int (&out_vid)[3]) {
 	// one 8x8 quadrant per wave: compact pixel sets touch the fewest nodes
@@ -259,13 +253,13 @@ __device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int
 #pragma unroll
 				for (int r = 0; r < 3; r++)
 #pragma unroll
-					for (int c = 0; c < 3; c++) Jc[r][c] = NNRT_JAC_FMA ? fmaf(DN(i, r, 0), P0[c], DN(i, r, 1) * P1[c]) : DN(i, r, 0) * P0[c] + DN(i, r, 1) * P1[c];
+					for (int c = 0; c < 3; c++) Jc[r][c] = DN(i, r, 0) * P0[c] + DN(i, r, 1) * P1[c];
 				if (a.perspective) {
 					float J2[3][3];
 #pragma unroll
 					for (int r = 0; r < 3; r++)
 #pragma unroll
-						for (int c = 0; c < 3; c++) J2[r][c] = dot3_jac(Pd[r][0], Jc[0][c], Pd[r][1], Jc[1][c], Pd[r][2], Jc[2][c]);
+						for (int c = 0; c < 3; c++) J2[r][c] = (Pd[r][0] * Jc[0][c] + Pd[r][1] * Jc[1][c]) + Pd[r][2] * Jc[2][c];
 #pragma unroll
 					for (int r = 0; r < 3; r++) J2[r][2] += PZ(r, i);
 #pragma unroll
@@ -286,12 +280,12 @@ __device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int
 						const float nr0 = r == 0 ? Nk[0].x : (r == 1 ? Nk[0].y : Nk[0].z);
 						const float nr1 = r == 0 ? Nk[1].x : (r == 1 ? Nk[1].y : Nk[1].z);
 						const float nr2 = r == 0 ? Nk[2].x : (r == 1 ? Nk[2].y : Nk[2].z);
-						w_rc[r] = dot3_jac(vr0, Jc[0][c], vr1, Jc[1][c], vr2, Jc[2][c]);
+						w_rc[r] = (vr0 * Jc[0][c] + vr1 * Jc[1][c]) + vr2 * Jc[2][c];
 						if (c == r) w_rc[r] += rho[i];
-						n_rc[r] = dot3_jac(nr0, Jc[0][c], nr1, Jc[1][c], nr2, Jc[2][c]);
+						n_rc[r] = (nr0 * Jc[0][c] + nr1 * Jc[1][c]) + nr2 * Jc[2][c];
 					}
-					const float x = dot3_jac(rw[0], w_rc[0], rw[1], w_rc[1], rw[2], w_rc[2]);
-					const float y = dot3_jac(rn[0], n_rc[0], rn[1], n_rc[1], rn[2], n_rc[2]);
+					const float x = (rw[0] * w_rc[0] + rw[1] * w_rc[1]) + rw[2] * w_rc[2];
+					const float y = (rn[0] * n_rc[0] + rn[1] * n_rc[1]) + rn[2] * n_rc[2];
 					rec_f[3 * i + c] = x + y;   // stored as formed: no 9-float tail of live outputs
 				}
 			}

@@ -786,10 +786,6 @@ ORC_API void orc_point_to_plane(const float* n1, const float* v1, const float* v
 static int g_jac_fma = 0;
 ORC_API void orc_set_fused_jacobians(int on) { g_jac_fma = on; }
 namespace {
-// a0 b0 + a1 b1 + a2 b2 in the selected arithmetic: the GPU's fused nesting (csrc dot3_jac) or the reference's unfused
-inline float dot3_jac(float a0, float b0, float a1, float b1, float a2, float b2) {
-	return g_jac_fma ? std::fmaf(a2, b2, std::fmaf(a1, b1, a0 * b0)) : (a0 * b0 + a1 * b1) + a2 * b2;
-}
 inline void matvec3_fma(const float* R, const float* v, float* o) {
 	o[0] = std::fmaf(R[0], v[0], std::fmaf(R[1], v[1], R[2] * v[2]));
 	o[1] = std::fmaf(R[3], v[0], std::fmaf(R[4], v[1], R[5] * v[2]));
@@ -902,8 +898,7 @@ ORC_API void orc_rasterized_surface_jacobians(const float* verts, const float* n
 			const float z2 = z * z;
 			float Pj[2][3] = {{cam.fx / z, 0.f, -cam.fx * V3[i][0] / z2}, {0.f, cam.fy / z, -cam.fy * V3[i][1] / z2}};
 			for (int r = 0; r < 3; r++)
-				for (int c = 0; c < 3; c++)
-					J[r][3 * i + c] = g_jac_fma ? std::fmaf(Dn[i][r][0], Pj[0][c], Dn[i][r][1] * Pj[1][c]) : Dn[i][r][0] * Pj[0][c] + Dn[i][r][1] * Pj[1][c];
+				for (int c = 0; c < 3; c++) J[r][3 * i + c] = Dn[i][r][0] * Pj[0][c] + Dn[i][r][1] * Pj[1][c];
 		}
 		if (perspective_correct) {
 			const float z0 = V3[0][2], z1 = V3[1][2], z2 = V3[2][2];
@@ -923,7 +918,7 @@ ORC_API void orc_rasterized_surface_jacobians(const float* verts, const float* n
 			for (int r = 0; r < 3; r++) for (int c = 0; c < 3; c++) { Pd[r][c] /= den2; Pz[r][c] /= den2; }
 			float J2[3][9];
 			for (int r = 0; r < 3; r++)
-				for (int c = 0; c < 9; c++) J2[r][c] = dot3_jac(Pd[r][0], J[0][c], Pd[r][1], J[1][c], Pd[r][2], J[2][c]);
+				for (int c = 0; c < 9; c++) J2[r][c] = (Pd[r][0] * J[0][c] + Pd[r][1] * J[1][c]) + Pd[r][2] * J[2][c];
 			for (int r = 0; r < 3; r++) for (int i = 0; i < 3; i++) J2[r][3 * i + 2] += Pz[r][i];
 			std::memcpy(J, J2, sizeof(J));
 		}
@@ -931,8 +926,8 @@ ORC_API void orc_rasterized_surface_jacobians(const float* verts, const float* n
 		float* on = out_nj + pix * 30;
 		for (int r = 0; r < 3; r++) {
 			for (int c = 0; c < 9; c++) {
-				ov[9 * r + c] = dot3_jac(V3[0][r], J[0][c], V3[1][r], J[1][c], V3[2][r], J[2][c]);
-				on[9 * r + c] = dot3_jac(N3[0][r], J[0][c], N3[1][r], J[1][c], N3[2][r], J[2][c]);
+				ov[9 * r + c] = (V3[0][r] * J[0][c] + V3[1][r] * J[1][c]) + V3[2][r] * J[2][c];
+				on[9 * r + c] = (N3[0][r] * J[0][c] + N3[1][r] * J[1][c]) + N3[2][r] * J[2][c];
 			}
 			for (int i = 0; i < 3; i++) ov[9 * r + 3 * i + r] += rho[i];   // + rho (x) I_3 (KroneckerTensorProduct.h)
 		}
@@ -999,8 +994,8 @@ ORC_API void orc_pixel_vertex_anchor_jacobians(const float* rast_vj, const float
 		const float* Jn = rast_nj + pix * 30;
 		float dr_dV[9], dr_dN[9];
 		for (int c = 0; c < 9; c++) {
-			float a = dot3_jac(dr_dwl[0], Jw[c], dr_dwl[1], Jw[9 + c], dr_dwl[2], Jw[18 + c]);
-			float b = dot3_jac(dr_dnl[0], Jn[c], dr_dnl[1], Jn[9 + c], dr_dnl[2], Jn[18 + c]);
+			float a = (dr_dwl[0] * Jw[c] + dr_dwl[1] * Jw[9 + c]) + dr_dwl[2] * Jw[18 + c];
+			float b = (dr_dnl[0] * Jn[c] + dr_dnl[1] * Jn[9 + c]) + dr_dnl[2] * Jn[18 + c];
 			dr_dV[c] = a + b;
 		}
 		for (int i = 0; i < 3; i++) for (int c = 0; c < 3; c++) dr_dN[3 * i + c] = dr_dnl[c] * Jn[27 + i];
