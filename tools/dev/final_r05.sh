@@ -5,8 +5,9 @@
 set -u
 export TAG=${TAG:-r05f}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-for cfg in ${PMC_CONFIGS:-C2 C3 C5}; do
-	CONFIG=$cfg STAGES="prof pmc" bash tools/measure.sh || exit 1
+for cfg in ${PMC_CONFIGS-C2 C3 C5}; do
+	K=""; [ $cfg = C5 ] && K="k_fit_pixels_fused k_raster_scatter_mesh k_warp_mesh_quad k_arrow_prepare k_init_stem k_stem_schur_rhs k_corner_factor k_corner_flow"
+	KERNELS="$K" CONFIG=$cfg STAGES="prof pmc" bash tools/measure.sh || exit 1
 	lc=$(echo $cfg | tr 'A-Z' 'a-z')
 	cp gpurun_out/$TAG/pmc_traffic_$cfg.json profiles/r05_pmc_traffic_$lc.json || exit 1
 done
