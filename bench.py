@@ -185,6 +185,8 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bound on the CPU-baseline sample (loop-body seconds)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="OpenMP threads for the CPU baseline (0: this process's CPU share, see cpu_threads_default)")
+    ap.add_argument("--refine-ratio", type=float, default=None,
+                    help="ARAP: upper end of the arrowhead solve's refinement window (default: the library's; inf: refine every solve)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-share-only", action="store_true", help="CPU baseline at this process's CPU share only (large configs: C3)")
     ap.add_argument("--cpu-no-warm", action="store_true", help="CPU baseline without the untimed first call (large configs: C3)")
@@ -421,6 +423,8 @@ def main(argv=None):
         wf_r = G.HierarchicalGraphWarpField(scene.nodes, scene.coverage, False, 4, 0, G.WarpNodeCoverageComputationMethod.FIXED_NODE_COVERAGE,
                                             scene.layer_count)
         ft_r = A.DeformableMeshToImageFitter(1, [A.IterationMode.ALL], preconditioning_dampening_factor=0.001, use_hip_graph=A.GRAPH_ALWAYS)
+        if args.refine_ratio is not None:
+            ft_r.set_refine_ratio(args.refine_ratio)
         mesh_r = G.TriangleMesh(scene.points, scene.normals, scene.faces)
         if args.step == "snapshot":
             R_mid, t_mid = scene.partial_motion(0.5)

@@ -43,6 +43,7 @@ _SIGNATURES = {
     "nnrt_runtime_version": (c_int32, []),
     "nnrt_device_count": (c_int32, []),
     "nnrt_build_jacobian_fma": (c_int32, []),
+    "nnrt_build_refine_floor": (c_float, []),
     "nnrt_warp_field_create": (c_int32, [c_void_p, c_int32, c_float, c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p,
                                          c_int32, ctypes.POINTER(c_void_p)]),
     "nnrt_warp_field_destroy": (None, [c_void_p]),
@@ -74,7 +75,8 @@ _SIGNATURES = {
     "nnrt_fitter_graph_count": (c_int32, [c_void_p]),
     "nnrt_fitter_corner_info": (c_int32, [c_void_p, c_void_p]),
     "nnrt_fitter_corner_work": (c_int32, [c_void_p, c_void_p]),
-    "nnrt_fitter_get_warped_mesh": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "nnrt_fitter_get_arrowhead_system": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p]),
+    "nnrt_fitter_get_warped_mesh": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "nnrt_release_arrowhead_plans": (None, []),
     "nnrt_fitter_fit_from_snapshot": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p]),
     "nnrt_fitter_restore_motion": (c_int32, [c_void_p, c_void_p, c_void_p]),
@@ -197,6 +199,11 @@ def lib():
 def jacobian_fma() -> bool:
     """Whether this build forms the pixel-node Jacobians with FMAs (csrc NNRT_JAC_FMA; the checker mirrors it)."""
     return bool(lib().nnrt_build_jacobian_fma())
+
+
+def refine_floor() -> float:
+    """The refinement floor this build's arrowhead solve was compiled with (csrc NNRT_REFINE_PIVOT_FLOOR)."""
+    return float(lib().nnrt_build_refine_floor())
 
 
 class NnrtError(RuntimeError):

@@ -420,6 +420,22 @@ __global__ __launch_bounds__(256) void k_refine_corner_rhs(int n0, int nc, const
 	if (lane < 6) rhs2[node_row[a] + lane] = v;
 }
 
+// ---- the refinement's safeguarded last step (arrow_device.hpp), per-stage form: run only when the gate is on ----
+__global__ __launch_bounds__(64) void k_refine_correction(int n0, int N, const float* __restrict__ dinv, const int* __restrict__ edge_offsets,
+                                                          const int* __restrict__ edge_list, const int32_t* __restrict__ edges,
+                                                          const float* __restrict__ wing, const float* __restrict__ res, float* __restrict__ dx,
+                                                          const float* __restrict__ x, const unsigned* gate, float ratio, unsigned* guard) {
+	if (!refine_gate_on(gate, ratio)) return;
+	refine_correction_node<false>(static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x), n0, N, dinv, edge_offsets, edge_list, edges, wing,
+	                              XPlain{res}, dx, XPlain{dx}, XPlain{x}, guard);
+}
+__global__ __launch_bounds__(64) void k_refine_apply(int N, const float* __restrict__ dx, float* __restrict__ x, const float* state_in, float* node_state,
+                                                     float* __restrict__ updates_out, const unsigned* gate, float ratio, const unsigned* guard) {
+	if (!refine_gate_on(gate, ratio)) return;
+	refine_apply_node(static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x), N, refine_guard_accepts(guard), XPlain{dx}, XPlain{x}, x, state_in,
+	                  node_state, updates_out);
+}
+
 nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* edges, const float* wing, int* error_flag, hipStream_t stream,
                                  bool arap_wings, float* node_state, float* updates_out, const float* state_in) {
 	const int m = ws.m;
@@ -479,6 +495,7 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 		fs.updates_out = updates_out;
 		fs.res = ws.res;
 		fs.gate = refine ? ws.corner->pivot_ratio() : nullptr;
+		fs.guard = refine ? ws.corner->refine_guard() : nullptr;
 		fs.ratio = ws.refine_ratio;
 		fs.error_flag = error_flag;
 		return ws.corner->launch_flow(fs, stream);
@@ -512,8 +529,12 @@ nnrt_status arrowhead_solve_core(const ArrowheadWorkspace& ws, const int32_t* ed
 	NNRT_LAUNCH_CHECK();
 	nnrt_status st = ws.corner->launch_resolve(ws.dx + 6 * static_cast<int64_t>(ws.n0), stream, gate, ratio);
 	if (st) return st;
-	k_arrow_back<<<static_cast<unsigned>(ceil_div(ws.N, 64)), 64, 0, stream>>>(ws.n0, ws.N, ws.dinv, ws.edge_offsets, ws.edge_list, edges, wing,
-	                                                                          ws.res, ws.dx, state_in, node_state, updates_out, ws.x, gate, ratio, 2);
+	// the safeguarded step: correction pass (the stem rows of d, max |d| / max |x|), then the apply pass
+	k_refine_correction<<<static_cast<unsigned>(ceil_div(ws.N, 64)), 64, 0, stream>>>(ws.n0, ws.N, ws.dinv, ws.edge_offsets, ws.edge_list, edges, wing,
+	                                                                                 ws.res, ws.dx, ws.x, gate, ratio, ws.corner->refine_guard());
+	NNRT_LAUNCH_CHECK();
+	k_refine_apply<<<static_cast<unsigned>(ceil_div(ws.N, 64)), 64, 0, stream>>>(ws.N, ws.dx, ws.x, state_in, node_state, updates_out, gate, ratio,
+	                                                                            ws.corner->refine_guard());
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;
 }

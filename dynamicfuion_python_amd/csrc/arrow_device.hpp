@@ -294,6 +294,71 @@ __device__ __forceinline__ void arrow_back_node(int i, int n0, int n_update, con
 	if (node_state) arrow_update_node(i, o, state_in, node_state, updates_out);
 }
 
+// ---- the refinement's last passes (round 6: a safeguarded step) ----
+// correction pass, node i (one thread per node): d_i -- stem rows solved from the residual (the stem back substitution
+// of H d = r, rl = r, xc = the corner rows of d), stored into dx; corner rows already in dx (the corner substitution) --
+// and its max |d_i| / max |x_i| (x from bl) folded into the guard words (one atomic max per wave); a non-finite d
+// counts as +inf, so the step is rejected
+template <bool SC1OUT, class RL, class XL, class BL>
+__device__ __forceinline__ void refine_correction_node(int i, int n0, int n_update, const float* __restrict__ dinv, const int* __restrict__ edge_offsets,
+                                                       const int* __restrict__ edge_list, const int32_t* __restrict__ edges,
+                                                       const float* __restrict__ wing, const RL& rl, float* __restrict__ dx, const XL& xc, const BL& bl,
+                                                       unsigned* guard) {
+	float dm = 0.f, xm = 0.f;
+	if (i < n0 || i < n_update) {
+		float d[6], xb[6];
+		if (i < n0) {
+			stem_solve(i, dinv, edge_offsets, edge_list, edges, wing, rl, xc, d);
+			store6<SC1OUT>(dx + 6 * static_cast<int64_t>(i), d);
+		} else {
+			xc.ld6(i, d);
+		}
+		bl.ld6(i, xb);
+		bool finite = true;
+#pragma unroll
+		for (int c = 0; c < 6; c++) {
+			finite &= __builtin_isfinite(d[c]);
+			dm = fmaxf(dm, fabsf(d[c]));
+			xm = fmaxf(xm, fabsf(xb[c]));
+		}
+		if (!finite) dm = __builtin_inff();
+	}
+#pragma unroll
+	for (int off = 32; off > 0; off >>= 1) {
+		dm = fmaxf(dm, __shfl_xor(dm, off));
+		xm = fmaxf(xm, __shfl_xor(xm, off));
+	}
+	if ((threadIdx.x & 63) == 0) {
+		__hip_atomic_fetch_max(guard + REFINE_GUARD_D, __float_as_uint(dm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		__hip_atomic_fetch_max(guard + REFINE_GUARD_X, __float_as_uint(xm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	}
+}
+// whether the guard words (every correction pass done) accept the step
+__device__ __forceinline__ bool refine_guard_accepts(const unsigned* guard) {
+	const float dm = __uint_as_float(__hip_atomic_load(guard + REFINE_GUARD_D, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+	const float xm = __uint_as_float(__hip_atomic_load(guard + REFINE_GUARD_X, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+	return refine_accept(dm, xm);
+}
+// apply pass, node i < n_update: x = x_base + d when the step is accepted (the same addition as before the safeguard),
+// else x_base; x_base <- x and the node's update (the solve's own pass skipped it while refining)
+template <class DL, class BL>
+__device__ __forceinline__ void refine_apply_node(int i, int n_update, bool accept, const DL& dl, const BL& bl, float* __restrict__ x_base,
+                                                  const float* state_in, float* node_state, float* __restrict__ updates_out) {
+	if (i >= n_update) return;
+	float o[6];
+	bl.ld6(i, o);
+	if (accept) {
+		float d[6];
+		dl.ld6(i, d);
+#pragma unroll
+		for (int c = 0; c < 6; c++) {
+			o[c] = o[c] + d[c];
+			x_base[6 * static_cast<int64_t>(i) + c] = o[c];
+		}
+	}
+	if (node_state) arrow_update_node(i, o, state_in, node_state, updates_out);
+}
+
 // ---- iterative refinement: the correction's corner right-hand side of corner node a (one wave; lane < 6 returns entry
 // `lane`, others 0): r_a - sum over stem edges i -> a of (D_i^-1 B_ia)^T r_i, with r_a = b_a - D_a x_a - sum over a's
 // incidences of the wing blocks times x (B^T x_i for stem edges, B x_b / B^T x_b for corner edges), products and sums in

@@ -732,7 +732,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	// launch 214 -> 197 us). In one round every wave starts at once and the table load only delays it (C2 40.2 -> 41.8).
 	// NNRT_TILE_ORDER=0: never, =2: always.
 	const size_t tiles = static_cast<size_t>(ceil_div(W, 16)) * static_cast<size_t>(ceil_div(H, 16));
-	const bool tile_order = [&] {
+	const bool tile_order = fit_pixels_tile_order_supported() && [&] {
 		const char* v = std::getenv("NNRT_TILE_ORDER");
 		if (v && *v == '0') return false;
 		if (v && *v == '2') return true;
@@ -1081,9 +1081,11 @@ nnrt_status nnrt_fitter_corner_info(const nnrt_fitter* ft, int64_t* h_out) {
 	return NNRT_OK;
 }
 
-nnrt_status nnrt_fitter_get_warped_mesh(nnrt_fitter* ft, float* h_positions, float* h_normals, void* stream) {
+nnrt_status nnrt_fitter_get_warped_mesh(nnrt_fitter* ft, float* h_positions, float* h_normals, int64_t vertex_count, void* stream) {
 	NNRT_CHECK_ARG(ft && h_positions && h_normals, "null pointer");
 	NNRT_CHECK_ARG(ft->V > 0 && ft->wpos.ptr, "no prepared frame");
+	// the host buffers hold vertex_count rows: a mismatch with the prepared mesh is refused, not written past
+	NNRT_CHECK_ARG(vertex_count == ft->V, "vertex_count differs from the prepared mesh's vertex count");
 	DeviceGuard guard(ft->device);
 	NNRT_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
 	NNRT_HIP(hipStreamSynchronize(ft->work));
@@ -1098,6 +1100,20 @@ nnrt_status nnrt_fitter_get_warped_mesh(nnrt_fitter* ft, float* h_positions, flo
 		h_normals[3 * v + 1] = n[v].y;
 		h_normals[3 * v + 2] = n[v].z;
 	}
+	return NNRT_OK;
+}
+
+nnrt_status nnrt_fitter_get_arrowhead_system(nnrt_fitter* ft, float* h_diag, float* h_wing, float* h_rhs, int64_t node_count, int64_t edge_count,
+                                             void* stream) {
+	NNRT_CHECK_ARG(ft && h_diag && h_wing && h_rhs, "null pointer");
+	NNRT_CHECK_ARG(ft->E > 0 && ft->a_diag.ptr && ft->wing.ptr && ft->a_rhs.ptr, "no prepared ARAP frame (the arrowhead system needs layer_count > 1)");
+	NNRT_CHECK_ARG(node_count == ft->N && edge_count == ft->E, "node_count / edge_count differ from the prepared frame's");
+	DeviceGuard guard(ft->device);
+	NNRT_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+	NNRT_HIP(hipStreamSynchronize(ft->work));
+	NNRT_HIP(hipMemcpy(h_diag, ft->a_diag.ptr, sizeof(float) * 36 * static_cast<size_t>(ft->N), hipMemcpyDeviceToHost));
+	NNRT_HIP(hipMemcpy(h_wing, ft->wing.ptr, sizeof(float) * 36 * static_cast<size_t>(ft->E), hipMemcpyDeviceToHost));
+	NNRT_HIP(hipMemcpy(h_rhs, ft->a_rhs.ptr, sizeof(float) * 6 * static_cast<size_t>(ft->N), hipMemcpyDeviceToHost));
 	return NNRT_OK;
 }
 
@@ -1119,15 +1135,22 @@ nnrt_status nnrt_fitter_refine_info(nnrt_fitter* ft, float* h_out, void* stream)
 	h_out[0] = 1.f;
 	h_out[1] = ft->refine_ratio_used;
 	h_out[2] = 0.f;
+	h_out[3] = 0.f;
+	h_out[4] = 0.f;
 	if (ft->E > 0 && ft->corner.pivot_ratio()) {
 		NNRT_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
 		NNRT_HIP(hipStreamSynchronize(ft->work));
-		unsigned bits = 0;
-		NNRT_HIP(hipMemcpy(&bits, ft->corner.pivot_ratio(), sizeof(bits), hipMemcpyDeviceToHost));
-		float r;
-		std::memcpy(&r, &bits, sizeof(r));
+		unsigned w[REFINE_WORDS] = {};
+		NNRT_HIP(hipMemcpy(w, ft->corner.pivot_ratio(), sizeof(w), hipMemcpyDeviceToHost));
+		float r, dm, xm;
+		std::memcpy(&r, &w[0], sizeof(r));
+		std::memcpy(&dm, &w[REFINE_GUARD_D], sizeof(dm));
+		std::memcpy(&xm, &w[REFINE_GUARD_X], sizeof(xm));
+		const bool ran = NNRT_ARAP_REFINE != 0 && refine_window(r, ft->refine_ratio_used);
 		h_out[0] = r;
-		h_out[2] = (NNRT_ARAP_REFINE != 0 && refine_window(r, ft->refine_ratio_used)) ? 1.f : 0.f;
+		h_out[2] = ran ? 1.f : 0.f;
+		h_out[3] = ran ? (xm > 0.f ? dm / xm : dm) : 0.f;
+		h_out[4] = ran && refine_accept(dm, xm) ? 1.f : 0.f;
 	}
 	return NNRT_OK;
 }
@@ -1249,6 +1272,11 @@ nnrt_status nnrt_fitter_time_kernels(nnrt_fitter* ft, nnrt_warp_field* wf, int32
 	NNRT_HIP(hipEventRecord(ft->ev_in, us));
 	NNRT_HIP(hipStreamWaitEvent(s, ft->ev_in, 0));
 	ft->refine_ratio_used = ft->refine_ratio;
+	// an error the caller's own earlier iterations raised and has not checked yet survives the timing replays (their
+	// flags are discarded below): saved here, restored at the end
+	int pending_flag = 0;
+	NNRT_HIP(hipStreamSynchronize(s));
+	NNRT_HIP(hipMemcpy(&pending_flag, ft->error_flag.ptr, sizeof(int), hipMemcpyDeviceToHost));
 	// prefix sequences, each `reps` iterations from the snapshot state in one graph: every kernel runs after the launch
 	// it follows in a real iteration (the raster alone excepted, which repeats its own idempotent scatter)
 	const unsigned seq[4] = {STAGE_ALL, STAGE_RASTER | STAGE_PIXEL | STAGE_SOLVE, STAGE_RASTER | STAGE_PIXEL, STAGE_RASTER};
@@ -1309,11 +1337,12 @@ nnrt_status nnrt_fitter_time_kernels(nnrt_fitter* ft, nnrt_warp_field* wf, int32
 		h_kernel_ms[3] = med[1] - med[2];   // solve + update (ARAP: the whole arrowhead chain)
 		h_kernel_ms[4] = med[0];            // whole iteration
 		// leave the fitter as an iteration would: raster keys empty, accumulators zero, motion = the snapshot's result;
-		// the device error flag the timing replays may have raised is cleared (nnrt_fitter_check reports the caller's
-		// own iterations only)
+		// the device error flag goes back to what the caller's own iterations left (the replays' flags are dropped:
+		// nnrt_fitter_check reports the caller's iterations only)
 		NNRT_HIP(hipMemsetAsync(ft->keys.ptr, 0xff, sizeof(uint64_t) * P, s));
 		NNRT_HIP(hipMemsetAsync(ft->acc.ptr, 0, sizeof(double) * static_cast<size_t>(ft->N) * ACC_STRIDE, s));
-		NNRT_HIP(hipMemsetAsync(ft->error_flag.ptr, 0, sizeof(int), s));
+		NNRT_HIP(hipStreamSynchronize(s));
+		NNRT_HIP(hipMemcpy(ft->error_flag.ptr, &pending_flag, sizeof(int), hipMemcpyHostToDevice));
 	}
 	NNRT_HIP(hipEventRecord(ft->ev_out, s));
 	NNRT_HIP(hipStreamWaitEvent(us, ft->ev_out, 0));

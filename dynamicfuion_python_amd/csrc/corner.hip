@@ -1656,7 +1656,8 @@ __global__ __launch_bounds__(CT) void k_corner_fwd(CornerFwdArgs a, int ld) {
 //
 // Workgroups take tickets (one relaxed agent-scope atomic add each) and a ticket fixes the role; roles are numbered so
 // that every wait is on work of a LOWER ticket: [back chains, root first] [stem workers] [rhs workers, one per tile
-// column] [forward chains, deepest first] [back chains, root first] [stem workers]. A back chain waits for its parent
+// column] [forward chains, deepest first] [back chains, root first] [correction workers] [apply workers] (the last two:
+// the safeguarded step, round 6). A back chain waits for its parent
 // chain (the refinement's roots: for their own forward chain), the stem workers for every back chain of their pass, the
 // rhs workers for the solve's stem workers (the stem residual), a forward chain for its columns' right-hand sides and
 // its child chains. A workgroup that holds a ticket is resident and waits only on lower tickets, so by induction every
@@ -1815,12 +1816,21 @@ __global__ __launch_bounds__(CT) void k_corner_flow(FlowArgs a) {
 		return;
 	}
 	k -= nB;
-	if (!flow_wait(ctl1 + 1, static_cast<unsigned>(nB), a.st.error_flag)) return;
-	const int i = k * CT + t;
-	if (i >= a.st.N) return;
-	arrow_back_node<false>(i, a.st.n0, a.st.N, a.st.dinv, a.st.edge_offsets, a.st.edge_list, a.st.edges, a.st.wing, res_sc1, a.st.dx,
-	                       XSc1{flow_rsrc(a.st.dx, 24 * static_cast<int64_t>(a.st.N))}, a.st.state_in, a.st.node_state, a.st.updates_out,
-	                       a.st.x, x_sc1, 2, true, a.st.diag, nullptr);
+	// the safeguarded step (arrow_device.hpp): a correction pass (the stem rows of d, max |d| and max |x| into the guard
+	// words), then an apply pass that waits for every correction workgroup and applies x + d -- or x, when the guard
+	// rejects the step -- with each node's update
+	const XSc1 dx_sc1{flow_rsrc(a.st.dx, 24 * static_cast<int64_t>(a.st.N))};
+	unsigned* guard = a.st.guard;
+	if (k < S) {
+		if (!flow_wait(ctl1 + 1, static_cast<unsigned>(nB), a.st.error_flag)) return;
+		refine_correction_node<true>(k * CT + t, a.st.n0, a.st.N, a.st.dinv, a.st.edge_offsets, a.st.edge_list, a.st.edges, a.st.wing, res_sc1,
+		                             a.st.dx, dx_sc1, x_sc1, guard);
+		flow_signal(guard + REFINE_GUARD_COUNT);
+		return;
+	}
+	k -= S;
+	if (!flow_wait(guard + REFINE_GUARD_COUNT, static_cast<unsigned>(S), a.st.error_flag)) return;
+	refine_apply_node(k * CT + t, a.st.N, refine_guard_accepts(guard), dx_sc1, x_sc1, a.st.x, a.st.state_in, a.st.node_state, a.st.updates_out);
 }
 
 // ===================================================================================================================
@@ -2138,7 +2148,7 @@ nnrt_status CornerSolver::prepare(const int32_t* edges, int E, int n0, int N, co
 		nnrt_status st;
 		if ((st = alloc(tiles, p.slot_ij.size() * TILE_ELEMS)) || (st = alloc(ldiag, static_cast<size_t>(p.T) * TILE_ELEMS)) ||
 		    (st = alloc(minv, static_cast<size_t>(p.T) * TILE_ELEMS)) || (st = alloc(cb2, static_cast<size_t>(p.ld))) ||
-		    (st = alloc(sdiag, static_cast<size_t>(p.ld))) || (st = alloc(reinterpret_cast<float*&>(pivot_word), 1)) ||
+		    (st = alloc(sdiag, static_cast<size_t>(p.ld))) || (st = alloc(reinterpret_cast<float*&>(pivot_word), REFINE_WORDS)) ||
 		    (st = alloc(cb, static_cast<size_t>(p.ld))) || (st = alloc(xp, static_cast<size_t>(p.ld))) || (st = alloc(xp2, static_cast<size_t>(p.ld))) ||
 		    (st = alloc(zx, static_cast<size_t>(p.ld))))
 			return fail(st);
@@ -2326,7 +2336,7 @@ nnrt_status CornerSolver::launch_flow(const FlowStem& st, hipStream_t s) const {
 	a.back2 = CornerBackArgs{nullptr, 0.f, tiles, ldiag, minv, cb2, xp2, d_row_node, a.refine ? st.dx + 6 * static_cast<int64_t>(st.n0) : nullptr,
 	                         nullptr, d_back_cols, d_back_ent, zx, 0};
 	a.st = st;
-	const int grid = n_chains + a.stem_wg + (a.refine ? T + 2 * n_chains + a.stem_wg : 0);
+	const int grid = n_chains + a.stem_wg + (a.refine ? T + 2 * n_chains + 2 * a.stem_wg : 0);
 	k_corner_flow<<<grid, CT, 0, s>>>(a);
 	NNRT_LAUNCH_CHECK();
 	return NNRT_OK;

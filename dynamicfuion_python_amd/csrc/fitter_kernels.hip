@@ -31,7 +31,12 @@ static_assert(PIX_WAVES == 1 || PIX_WAVES == 2 || PIX_WAVES == 4, "waves per wor
 // round-robin over the 8 XCDs, so each XCD gets a contiguous band of quadrants (neighbouring pixels share vertices,
 // anchors and nodes -> L2 reuse within the XCD).
 __device__ inline int pix_quadrant(const FitPixelArgs& a) {
-	if (PIX_WAVES == 4 && a.tile_order) return a.tile_order[blockIdx.x] * 4 + static_cast<int>(threadIdx.x >> 6);   // (one scalar load)
+	if (PIX_WAVES == 4 && a.tile_order) {
+		// the per-frame table holds XCD band x (the workgroups b = x + 8 k, dispatched round-robin over the XCDs) at
+		// [x * per_band, (x + 1) * per_band), in k order (k_tile_order); one scalar load
+		const int b = static_cast<int>(blockIdx.x), per_band = a.order_blocks >> 3;
+		return a.tile_order[(b & 7) * per_band + (b >> 3)] * 4 + static_cast<int>(threadIdx.x >> 6);
+	}
 	const int blocks = (4 * a.tiles_x * a.tiles_y + PIX_WAVES - 1) / PIX_WAVES;
 	const int per_xcd = (blocks + 7) / 8;
 	const int b = static_cast<int>(blockIdx.x);
@@ -915,8 +920,12 @@ extern "C" int nnrt_dev_fit_stamps(unsigned long long* out) {   // [16384][4] of
 
 // the pixel-node Jacobian arithmetic of this build (NNRT_JAC_FMA), for the test checker's matching mode
 extern "C" int nnrt_build_jacobian_fma() { return NNRT_JAC_FMA && !NNRT_GATHER_ROWS; }
+extern "C" float nnrt_build_refine_floor() { return NNRT_REFINE_PIVOT_FLOOR; }
 
 int fit_pixels_arap_blocks(int E) { return static_cast<int>(ceil_div(E, PIX_BLOCK)); }
+// the per-frame tile table maps one 16 x 16 tile per 4-wave workgroup; other NNRT_PIX_WAVES builds use the arithmetic
+// mapping, whose grid the table's would not cover
+bool fit_pixels_tile_order_supported() { return PIX_WAVES == 4; }
 
 // ---- per-frame tile order of the pixel launch (launch_tile_order) ----
 __host__ __device__ inline int tiles_per_band(int tiles) { return (tiles + 7) / 8 + 1; }   // ceil(w / 8) + ceil(i / 8) <= this

@@ -146,15 +146,16 @@ class DeformableMeshToImageFitter:
 
     def refine_info(self, stream=None) -> dict:
         """The last arrowhead solve's refinement gate: the corner factorization's smallest pivot / diag(S) ratio, the
-        threshold, and whether the refinement step ran."""
-        out = np.zeros(3, np.float32)
+        threshold, whether the refinement step ran, its max |d| / max |x| and whether its safeguard accepted it."""
+        out = np.zeros(5, np.float32)
         N.check(N.lib().nnrt_fitter_refine_info(self._h, N.ptr(out), N.stream_ptr(stream)))
-        return dict(pivot_ratio=float(out[0]), threshold=float(out[1]), refined=bool(out[2]))
+        return dict(pivot_ratio=float(out[0]), threshold=float(out[1]), refined=bool(out[2]), correction=float(out[3]),
+                    accepted=bool(out[4]))
 
     def set_refine_ratio(self, ratio: float):
         """Upper end of the arrowhead solve's refinement window: one refinement step runs when the corner
-        factorization's min pivot / diag(S) lies in [1e-4, ratio) (default ratio 1e-3; 0: never refine; inf: refine
-        whenever the ratio is at least the 1e-4 floor, below which one step does not converge). refine_info() reports
+        factorization's min pivot / diag(S) lies in [floor, ratio) (floor 1e-5, _native.refine_floor(); default ratio
+        1e-2; 0: never refine; inf: refine whenever the ratio is at least the floor). refine_info() reports
         the threshold the last launched iterations ran with."""
         N.check(N.lib().nnrt_fitter_set_refine_ratio(self._h, float(ratio)))
 
@@ -216,11 +217,22 @@ class DeformableMeshToImageFitter:
         keys = ("corner_nodes", "tile_columns", "factor_launches", "back_launches", "stored_tiles", "dense_lower_tiles")
         return {k: int(v) for k, v in zip(keys, out)}
 
+    def arrowhead_system(self, node_count: int, edge_count: int, stream=None):
+        """The last ARAP iteration's float arrowhead system as the fitter solved it (virtual order): diagonal blocks
+        [N,6,6] with LM, wing blocks [E,6,6] (block (i, j) of edge (i, j)), right-hand side [6N]."""
+        d = np.empty((node_count, 6, 6), np.float32)
+        w = np.empty((edge_count, 6, 6), np.float32)
+        b = np.empty(6 * node_count, np.float32)
+        N.check(N.lib().nnrt_fitter_get_arrowhead_system(self._h, N.ptr(d), N.ptr(w), N.ptr(b), int(node_count), int(edge_count),
+                                                          N.stream_ptr(stream)))
+        return d, w, b
+
     def warped_mesh(self, vertex_count: int, stream=None):
-        """The last iteration's warped canonical mesh (positions, normals [V,3]) as the fitter rasterized it."""
+        """The last iteration's warped canonical mesh (positions, normals [V,3]) as the fitter rasterized it; vertex_count
+        must equal the prepared mesh's (the C-ABI refuses a mismatch instead of writing past the buffers)."""
         p = np.empty((vertex_count, 3), np.float32)
         n = np.empty((vertex_count, 3), np.float32)
-        N.check(N.lib().nnrt_fitter_get_warped_mesh(self._h, N.ptr(p), N.ptr(n), N.stream_ptr(stream)))
+        N.check(N.lib().nnrt_fitter_get_warped_mesh(self._h, N.ptr(p), N.ptr(n), int(vertex_count), N.stream_ptr(stream)))
         return p, n
 
     def corner_work(self) -> dict:

@@ -42,10 +42,13 @@ const char* nnrt_last_error(void);
 /* HIP runtime version the library was built against and the number of visible devices (-1 on error). */
 int32_t nnrt_runtime_version(void);
 int32_t nnrt_device_count(void);
-/* Pixel-node Jacobian arithmetic of this build: 1 = FMA form (the default product), 0 = the reference CPU path's
- * unfused expressions (built with -DNNRT_JAC_FMA=0). Both are the reference's expression (PixelVertexAnchorJacobiansImpl.h
+/* Pixel-node Jacobian arithmetic of this build: 0 = the reference CPU path's unfused expressions (the product), 1 = FMA
+ * form (a development build, -DNNRT_JAC_FMA=1). Both are the reference's expression (PixelVertexAnchorJacobiansImpl.h
  * :179-363, WarpedSurfaceJacobiansImpl.h:117-156); the test checker selects its matching mode from this. */
 int32_t nnrt_build_jacobian_fma(void);
+/* The arrowhead solve's refinement floor of this build (NNRT_REFINE_PIVOT_FLOOR): no refinement step below this corner
+ * pivot / diag(S) ratio. */
+float nnrt_build_refine_floor(void);
 
 /* ---------------------------------------------------------------------------------------------------------------
  * Warp field -- replaces nnrt::geometry::HierarchicalGraphWarpField (cpp/geometry/HierarchicalGraphWarpField.h:37-97,
@@ -158,13 +161,20 @@ nnrt_status nnrt_fitter_corner_info(const nnrt_fitter* fitter, int64_t* h_out);
 nnrt_status nnrt_fitter_corner_work(const nnrt_fitter* fitter, int64_t* h_out);
 /* The last iteration's warped canonical mesh (diagnostic; synchronizes `stream`): h_positions / h_normals [V,3] as the
  * fitter rasterized them (Warping.cpp:222-264 of the motion the iteration started from). */
-nnrt_status nnrt_fitter_get_warped_mesh(nnrt_fitter* fitter, float* h_positions, float* h_normals, void* stream);
-/* The last arrowhead solve's refinement gate (diagnostic; synchronizes `stream`): h_out[3] = the corner factorization's
+nnrt_status nnrt_fitter_get_warped_mesh(nnrt_fitter* fitter, float* h_positions, float* h_normals, int64_t vertex_count, void* stream);
+/* The last ARAP iteration's float arrowhead system exactly as the fitter factored and refined it (diagnostic; synchronizes
+ * `stream`; virtual node order): h_diag [N,36] diagonal blocks (data + ARAP + LM), h_wing [E,36] wing blocks (block (i, j)
+ * of edge e = (i, j), its transpose at (j, i)), h_rhs [6N] right-hand side (negative gradient). The reference holds the
+ * same system between ComputeArapHessian and SolveBlockSparseArrowheadCholesky (DeformableMeshToImageFitter.cpp:223-247). */
+nnrt_status nnrt_fitter_get_arrowhead_system(nnrt_fitter* fitter, float* h_diag, float* h_wing, float* h_rhs, int64_t node_count,
+                                             int64_t edge_count, void* stream);
+/* The last arrowhead solve's refinement gate (diagnostic; synchronizes `stream`): h_out[5] = the corner factorization's
  * smallest pivot / diag(S) ratio (1 without ARAP), the threshold below which one step of iterative refinement runs (it
- * does not below 1e-4, where one step no longer converges), and 1 if it ran. */
+ * does not below the build's floor, 1e-5, where one step is not relied on), 1 if it ran, the step's max |d| / max |x|
+ * and 1 if its safeguard accepted it (max |d| <= 1e-2 max |x|; else the plain solve stands). */
 nnrt_status nnrt_fitter_refine_info(nnrt_fitter* fitter, float* h_out, void* stream);
-/* Threshold of the refinement gate (default 1e-3): the arrowhead solve refines when the corner's smallest pivot /
- * diag(S) ratio falls below it (and is at least 1e-4); 0 never refines. Drops the fitter's cached graphs (a launch
+/* Threshold of the refinement gate (default 1e-2): the arrowhead solve refines when the corner's smallest pivot /
+ * diag(S) ratio falls below it (and is at least 1e-5); 0 never refines. Drops the fitter's cached graphs (a launch
  * argument). */
 nnrt_status nnrt_fitter_set_refine_ratio(nnrt_fitter* fitter, float ratio);
 /* Store the warp field's current node motion (R, t) in the fitter (a device copy on `stream`). */

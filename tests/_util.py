@@ -165,6 +165,51 @@ def arrowhead_fp64_solution(oracle_mod, sc, R0, t0, dg_o, lm=0.001, arap_weight=
     return spl.spsolve(A, b)
 
 
+def fp64_system_from_blocks(diag, wing, edges, rhs):
+    """fp64 matrix and right-hand side of a float arrowhead system given by its blocks -- the fitter's own system as it
+    factored and refined it (nnrt_fitter_get_arrowhead_system: diagonal blocks [N,6,6] with LM, wing block (i, j) of edge
+    e = (i, j) and its transpose at (j, i), rhs [6N]), every stored float taken exactly, nothing re-assembled."""
+    import scipy.sparse as sp
+    diag = np.asarray(diag, np.float64).reshape(-1, 6, 6)
+    wing = np.asarray(wing, np.float64).reshape(-1, 6, 6)
+    edges = np.asarray(edges, np.int64).reshape(-1, 2)
+    N = len(diag)
+    bi, bj = np.meshgrid(np.arange(6), np.arange(6), indexing="ij")
+    n = np.arange(N)[:, None]
+    rows = [(6 * n + bi.ravel()).ravel()]
+    cols = [(6 * n + bj.ravel()).ravel()]
+    vals = [diag.reshape(N, 36).ravel()]
+    i, j = edges[:, :1], edges[:, 1:]
+    rows += [(6 * i + bi.ravel()).ravel(), (6 * j + bi.ravel()).ravel()]
+    cols += [(6 * j + bj.ravel()).ravel(), (6 * i + bj.ravel()).ravel()]
+    vals += [wing.reshape(-1, 36).ravel(), np.transpose(wing, (0, 2, 1)).reshape(-1, 36).ravel()]
+    A = sp.csc_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))), shape=(6 * N, 6 * N))
+    return A, np.asarray(rhs, np.float64)
+
+
+def exact_system_solution(ft, wf, N):
+    """(fp64 solution, fp64 pivot ratio) of the fitter's last arrowhead system exactly as stored on the device; (None,
+    None) when it holds non-finite entries."""
+    import scipy.sparse.linalg as spl
+    edges = wf.get_edges()
+    d, w, b = ft.arrowhead_system(N, len(edges))
+    if not (np.isfinite(d).all() and np.isfinite(w).all() and np.isfinite(b).all()):
+        return None, None   # A7 NaN rotations upstream: no finite system to solve
+    A, b = fp64_system_from_blocks(d, w, edges, b)
+    return spl.spsolve(A.tocsc(), b), fp64_pivot_ratio(A)
+
+
+def rodrigues64(w):
+    """fp64 Rodrigues rotations [n,3,3] of rotation vectors w [n,3] (RodriguesImpl.h:66-99; NaN at |w| = 0, quirk A7)."""
+    w = np.asarray(w, np.float64).reshape(-1, 3)
+    th = np.linalg.norm(w, axis=1)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        a = w / th[:, None]
+    K = np.zeros((len(w), 3, 3))
+    K[:, 0, 1], K[:, 0, 2], K[:, 1, 0], K[:, 1, 2], K[:, 2, 0], K[:, 2, 1] = -a[:, 2], a[:, 1], a[:, 2], -a[:, 0], -a[:, 1], a[:, 0]
+    return np.eye(3) + np.sin(th)[:, None, None] * K + (1 - np.cos(th))[:, None, None] * (K @ K)
+
+
 def fp64_pivot_ratio(A):
     """min / max of the fp64 Cholesky pivots (LDLᵀ diagonal) of the symmetric sparse matrix A under a symmetric
     fill-reducing order; <= 0: not positive definite."""

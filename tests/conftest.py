@@ -22,10 +22,11 @@ def oracle_mod():
 
 @pytest.fixture(autouse=True)
 def _checker_jacobian_arithmetic(request):
-    """GPU tests check the HIP path against the oracle in the library's own pixel-node Jacobian arithmetic (the FMA form
-    of csrc/fitter_kernels.hip, NNRT_JAC_FMA: bit-identical terms, so H / g stay held to 1e-6); the reference CPU path's
-    unfused arithmetic is the oracle's default and is checked against the GPU at north_star's tolerance in
-    tests/test_gpu_parity.py::test_fused_jacobians_vs_reference_arithmetic."""
+    """GPU tests check the HIP path against the oracle in the library's own pixel-node Jacobian arithmetic: the product
+    build forms them as the reference CPU path's unfused products (the oracle's default, NNRT_JAC_FMA=0), so every GPU
+    test runs against the reference arithmetic; a development build with FMA-formed Jacobians switches the oracle to its
+    bit-identical fused mode, and tests/test_gpu_parity.py::test_reference_arithmetic_margins then holds that build
+    against the reference arithmetic at north_star's tolerance."""
     if request.node.get_closest_marker("gpu") is None:
         yield
         return

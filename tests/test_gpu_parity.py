@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-from _util import (FIXTURES, arrowhead_fp64_solution, arrowhead_fp64_system, fp64_pivot_ratio, oracle_fit_scene, read_ply,  # noqa: E402
+from _util import (FIXTURES, arrowhead_fp64_solution, arrowhead_fp64_system, exact_system_solution, fp64_pivot_ratio, oracle_fit_scene, read_ply,  # noqa: E402
                    rel_err, scene_target, transform_mesh, xy_plane)
 from golden import kat_literals as L  # noqa: E402
 
@@ -327,13 +327,14 @@ def test_fit_one_iteration_parity(nn, S, oracle_mod, name):
     assert rel_err(wf.get_node_rotations(True) - np.eye(3), R_o - np.eye(3)) < 1e-4
 
 
-@pytest.mark.parametrize("name", ["S1", "C1", "C2"])
-def test_fused_jacobians_vs_reference_arithmetic(nn, S, oracle_mod, name):
-    """north_star's bar against the reference CPU path's own arithmetic: the GPU forms the pixel-node Jacobians as FMA
-    chains (csrc/fitter_kernels.hip NNRT_JAC_FMA; the other GPU tests check it against the oracle's bit-identical fused
-    mode), the reference's CPU build as unfused products (the oracle's default, restored here). On identical inputs the
-    rasterization and mask agree exactly, residuals to 1e-6 absolute, node updates and motion to north_star's 1e-4
-    relative, and the assembled H / g to 1e-5 relative (per-term rounding of a few ulps, summed over a node's pixels)."""
+@pytest.mark.parametrize("name", ["S1", "C1", "C2", "C1_ARAP", "C2_ARAP", "C5"])
+def test_reference_arithmetic_margins(nn, S, oracle_mod, name):
+    """north_star's bar against the reference CPU path's own arithmetic (the oracle's default mode, restored here whatever
+    the library build): one GN iteration per config, block-diagonal and ARAP. The product forms the pixel-node Jacobians
+    as the reference's unfused products (csrc NNRT_JAC_FMA=0), so H and g agree to the fp64 summation order (1e-6); a
+    development build with FMA-formed Jacobians (NNRT_JAC_FMA=1) is held to 1e-5 there. Faces and mask exact, residuals
+    1e-6 absolute, updates, node translations and max |R - I| 1e-4 relative; every margin is printed."""
+    from dynamicfuion_python_amd import _native
     oracle_mod.set_fused_jacobians(False)
     sc = _scene(S, oracle_mod, name)
     depth = scene_target(oracle_mod, sc)
@@ -342,15 +343,19 @@ def test_fused_jacobians_vs_reference_arithmetic(nn, S, oracle_mod, name):
     N = len(sc.nodes)
     assert np.array_equal(dg_o["pixel_faces"].astype(np.int64), dg_g["pixel_faces"].astype(np.int64))
     assert np.array_equal(dg_o["residual_mask"], dg_g["residual_mask"])
-    assert np.allclose(dg_o["residuals"], dg_g["residuals"], rtol=0, atol=1e-6, equal_nan=True)
+    r_abs = float(np.nanmax(np.abs(dg_o["residuals"] - dg_g["residuals"]))) if len(dg_o["residuals"]) else 0.0
     h_err = nan_rel_err(dg_g["hessian"][: N * 36], dg_o["hessian_diag"])
     g_err = nan_rel_err(dg_g["gradient"][: N * 6], dg_o["gradient"])
     u_err = nan_rel_err(dg_g["updates"][: N * 6], dg_o["updates"])
-    print(f"{name}: reference arithmetic vs fused GPU: H {h_err:.2g}, g {g_err:.2g}, updates {u_err:.2g}")
-    assert h_err < 1e-5 and g_err < 1e-5
-    assert u_err < 1e-4
-    assert rel_err(wf.get_node_translations(True), t_o) < 1e-4
-    assert rel_err(wf.get_node_rotations(True) - np.eye(3), R_o - np.eye(3)) < 1e-4
+    t_err = rel_err(wf.get_node_translations(True), t_o)
+    r_err = rel_err(wf.get_node_rotations(True) - np.eye(3), R_o - np.eye(3))
+    fma = _native.jacobian_fma()
+    print(f"{name} ({'FMA' if fma else 'unfused'} Jacobians) vs the reference arithmetic: residuals {r_abs:.2g} abs, H {h_err:.2g}, "
+          f"g {g_err:.2g}, updates {u_err:.2g}, t {t_err:.2g}, R - I {r_err:.2g}")
+    hg_bar = 1e-5 if fma else 1e-6
+    assert r_abs <= 1e-6
+    assert h_err < hg_bar and g_err < hg_bar
+    assert u_err < 1e-4 and t_err < 1e-4 and r_err < 1e-4
 
 
 @pytest.mark.parametrize("name,mode", [("C2", "ALL"), ("C1", "TRANSLATION_ONLY"), ("C1", "ROTATION_ONLY")])
@@ -460,8 +465,9 @@ def test_fit_tukey_and_variable_coverage_parity(nn, S, oracle_mod):
 NOT_POSITIVE_DEFINITE = 3   # include/nnrt_mi355x.h NNRT_ERROR_NOT_POSITIVE_DEFINITE
 
 
-REFINE_PIVOT_RATIO = 1e-7   # fp64 min / max Cholesky pivot above which the refined arrowhead solve is held to 1e-4
-REFINE_FLOOR = 1e-4         # csrc/fitter_kernels.hpp NNRT_REFINE_PIVOT_FLOOR: no refinement below this corner pivot / diag(S)
+REFINE_PIVOT_RATIO = 1e-7   # fp64 min / max Cholesky pivot above which the arrowhead solve is held to 1e-4
+REFINED_PIVOT_RATIO = 1e-12  # ... and above which an accepted refinement step is (measured converging down to 6e-12)
+REFINE_FLOOR = 1e-5         # csrc/fitter_kernels.hpp NNRT_REFINE_PIVOT_FLOOR: no refinement below this corner pivot / diag(S)
 
 
 def _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k):
@@ -500,18 +506,36 @@ def _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k):
         assert 0.0 < ratio < 1e-6, f"{msg}; fp64 min / max Cholesky pivot {ratio:.3g}"
         if not gpu_failed:
             assert np.isfinite(dg_g["updates"][: 6 * N]).all(), msg
-        return f"potrf ({'oracle' if oracle_failed else 'GPU'} only: fp64 pivot ratio {ratio:.2g})", None, None
+        return f"potrf ({'oracle' if oracle_failed else 'GPU'} only: fp64 pivot ratio {ratio:.2g})", None, {}
     if gpu_failed:
         if dg_o is not None:   # block-diagonal: the same blocks fail (NaN updates), every other node's update agrees
             u_g, u_o = dg_g["updates"][: 6 * N], dg_o["updates"]
             assert nan_rel_err(u_g, u_o) < 1e-4
             assert np.array_equal(dg_o["pixel_faces"].astype(np.int64), dg_g["pixel_faces"].astype(np.int64))
             assert nan_rel_err(dg_g["hessian"][: N * 36], dg_o["hessian_diag"]) < 1e-6
-        return "potrf", None, None
+        return "potrf", None, {}
     solve_note = ""
     e_own = None
+    info = {"own": None, "exact": None, "oracle_float": None, "gate": None}
     u_err = nan_rel_err(dg_g["updates"][: 6 * N], dg_o["updates"])
     if sc.layer_count > 1:
+        # the solve against the fp64 solution of EXACTLY the float system the GPU factored and refined (its diagonal
+        # blocks with LM, wing blocks and right-hand side, exported by nnrt_fitter_get_arrowhead_system): the solver's own
+        # error, free of any assembly difference. A refined solve, and any solve of a system whose
+        # fp64 pivot ratio exceeds REFINE_PIVOT_RATIO, must be within 1e-4 of it.
+        x_exact, ratio_exact = exact_system_solution(ft, wf, N)
+        gate = ft.refine_info()
+        info["gate"] = gate
+        if x_exact is not None:
+            e_exact = nan_rel_err(dg_g["updates"][: 6 * N], x_exact)
+            info["exact"] = e_exact
+            solve_note += (f", exact-system err {e_exact:.2g} (its fp64 pivot ratio {ratio_exact:.2g}; corner pivot / diag(S) "
+                           f"{gate['pivot_ratio']:.2g}, refined {gate['refined']})")
+            solve_note += f", correction {gate['correction']:.2g} accepted {gate['accepted']}" if gate["refined"] else ""
+            if (gate["refined"] and gate["accepted"] and ratio_exact > REFINED_PIVOT_RATIO) or ratio_exact > REFINE_PIVOT_RATIO:
+                assert e_exact <= 1e-4, (f"iteration {k + 1}: solve {e_exact:.3g} from the fp64 solution of its own float system "
+                                         f"(refined {gate['refined']}, accepted {gate['accepted']}, corner pivot / diag(S) "
+                                         f"{gate['pivot_ratio']:.3g}, fp64 pivot ratio {ratio_exact:.3g})")
         # The GPU's arrowhead solve (f32 factor + one step of iterative refinement with an fp64 residual) against the fp64
         # solution of the GPU's own normal equations (its data blocks and right-hand side): wherever the system's fp64
         # Cholesky pivot ratio exceeds REFINE_PIVOT_RATIO the solve must reach 1e-4 (the 2x-oracle rule below
@@ -520,9 +544,8 @@ def _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k):
         import scipy.sparse.linalg as spl
         e_own = nan_rel_err(dg_g["updates"][: 6 * N], spl.spsolve(A_own.tocsc(), b_own))
         ratio_own = fp64_pivot_ratio(A_own)
-        gate = ft.refine_info()
-        solve_note = (f", own-system err vs fp64 {e_own:.2g} (fp64 pivot ratio {ratio_own:.2g}; corner pivot / diag(S) "
-                      f"{gate['pivot_ratio']:.2g}, refined {gate['refined']})")
+        info["own"] = e_own
+        solve_note += f", assembled-system err vs fp64 {e_own:.2g} (fp64 pivot ratio {ratio_own:.2g})"
         if ratio_own > REFINE_PIVOT_RATIO:
             assert e_own <= 1e-4, f"iteration {k + 1}: refined solve error {e_own:.3g} vs fp64 at pivot ratio {ratio_own:.3g}"
         # ... and against the fp64 solution of the ORACLE's normal equations: the two float systems
@@ -535,6 +558,7 @@ def _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k):
         predicted = 4.0 * delta / max(ratio_own, 1e-300)
         d64 = nan_rel_err(spl.spsolve(A_own.tocsc(), b_own), x64_o)
         e_oracle_sys = nan_rel_err(dg_g["updates"][: 6 * N], x64_o)
+        info["oracle_float"] = nan_rel_err(dg_o["updates"], x64_o)   # the reference-order float solve's own error
         solve_note += f", vs the oracle system's fp64 solution {e_oracle_sys:.2g} (fp64 solutions {d64:.2g} apart, predicted <= {predicted:.2g})"
         assert d64 <= max(1e-4, predicted), f"iteration {k + 1}: fp64 solutions {d64:.3g} apart, assembly {delta:.3g} predicts {predicted:.3g}"
         assert e_oracle_sys <= max(1e-4, e_own + predicted), \
@@ -573,7 +597,7 @@ def _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k):
     ok = np.isfinite(R_expect)
     assert np.abs(R_g[ok] - R_expect[ok]).max(initial=0.0) < 1e-5
     nan_nodes = int(np.isnan(R_g).reshape(N, -1).any(1).sum())
-    return ("ok" if nan_nodes == 0 else f"ok, {nan_nodes} NaN rotations (A7)") + solve_note, u_err, e_own
+    return ("ok" if nan_nodes == 0 else f"ok, {nan_nodes} NaN rotations (A7)") + solve_note, u_err, info
 
 
 def _new_fit(nn, sc, depth, iterations):
@@ -607,6 +631,11 @@ def _new_fit(nn, sc, depth, iterations):
 # solve of that iteration-3 system 6.0e-4 from fp64. Each build's trajectory is pinned at its own measurement.
 PINNED_SOLVE_ERRORS = {("C5", 1): 3e-6, ("C5", 2): 3e-5, ("C5", 3): 2.6e-4}
 PINNED_SOLVE_ERRORS_FMA = {("C5", 1): 3e-6, ("C5", 2): 3e-5, ("C5", 3): 1.6e-3}
+# the same iterations against the fp64 solution of exactly the float system the GPU solved (nnrt_fitter_get_arrowhead_system;
+# round 6, floor 1e-5, window to 1e-2, safeguarded step): measured 1.4e-6 (unrefined, gate 0.27) / 2.2e-8 / 3.0e-7 (refined,
+# gates 0.0018 and 7.4e-5, corrections 8.3e-6 and 5.4e-4 accepted) -- VERDICT r5 item 2's C5 iteration 3, refined to well
+# under 1e-4 of its exact solution
+PINNED_EXACT_ERRORS = {("C5", 1): 3e-6, ("C5", 2): 1e-6, ("C5", 3): 1e-6}
 TRAJECTORIES = [("S1", 6, 6, None), ("C2", 2, 1, 2), ("C2_ARAP", 10, 4, None), ("C5", 6, 3, None)]
 
 
@@ -622,13 +651,19 @@ def test_fit_state_synchronised_trajectory(nn, S, oracle_mod, name, iterations, 
     report = []
     for k in range(iterations):
         nan_before = int(np.isnan(wf.get_node_rotations(True)).reshape(len(sc.nodes), -1).any(1).sum())
-        status, err, e_own = _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k)
+        status, err, info = _synchronised_iteration(nn, oracle_mod, sc, depth, wf, ft, k)
         print(f"{name} iteration {k + 1}: {status}, update rel err {err}, NaN rotations before {nan_before}", flush=True)
         report.append((k + 1, status, err))
         from dynamicfuion_python_amd import _native
         pin = (PINNED_SOLVE_ERRORS_FMA if _native.jacobian_fma() else PINNED_SOLVE_ERRORS).get((name, k + 1))
-        if pin is not None:   # the refined solve's measured error vs fp64 as a regression bound
+        if pin is not None:   # the measured errors vs fp64 as regression bounds
+            e_own, e_exact, e_of = info.get("own"), info.get("exact"), info.get("oracle_float")
             assert e_own is not None and e_own <= pin, f"{name} iteration {k + 1}: solve error vs fp64 {e_own} above its pinned {pin:.3g}"
+            # ... and never less accurate than the reference-order float solve of the oracle's own system
+            assert e_own <= max(e_of, 1e-5), f"{name} iteration {k + 1}: GPU {e_own:.3g} vs fp64, the oracle's float solve {e_of:.3g}"
+            pin_x = PINNED_EXACT_ERRORS.get((name, k + 1))
+            if pin_x is not None:
+                assert e_exact is not None and e_exact <= pin_x, f"{name} iteration {k + 1}: exact-system error {e_exact} above {pin_x:.3g}"
         if status.startswith("potrf"):
             break
     print(f"{name}: {report}")
@@ -653,6 +688,8 @@ def test_refinement_gate(nn, S, oracle_mod, name, iterations):
     N = len(sc.nodes)
     wf, ft = _new_fit(nn, sc, depth, iterations)
     threshold = ft.refine_info()["threshold"]
+    from dynamicfuion_python_amd import _native
+    floor = _native.refine_floor()   # REFINE_FLOOR in the product build; development builds may lower it
 
     def solve(R0, t0, k, ratio):
         wf.set_node_rotations(R0, True)
@@ -665,7 +702,7 @@ def test_refinement_gate(nn, S, oracle_mod, name, iterations):
             return None
         dg = ft.diagnostics()
         info = ft.refine_info()
-        return dg["updates"][: 6 * N].copy(), dg["hessian"][: 36 * N].copy(), dg["gradient"][: 6 * N].copy(), info["pivot_ratio"]
+        return dg["updates"][: 6 * N].copy(), dg["hessian"][: 36 * N].copy(), dg["gradient"][: 6 * N].copy(), info["pivot_ratio"], info
 
     rows = []
     for k in range(iterations):
@@ -678,21 +715,35 @@ def test_refinement_gate(nn, S, oracle_mod, name, iterations):
             break
         assert np.array_equal(plain[1], refined[1]) and np.array_equal(plain[2], refined[2])
         assert plain[3] == refined[3]   # the same factorization
-        A, b = arrowhead_fp64_system(oracle_mod, sc, R0, t0, hessian_diag=plain[1], gradient=plain[2])
-        x64 = spl.spsolve(A.tocsc(), b)
-        ratio64 = fp64_pivot_ratio(A)
+        # judged against the fp64 solution of exactly the float system both solves factored (the fitter's export; VERDICT
+        # r5 item 2) -- until round 5 against a system re-assembled from the oracle's ARAP blocks, whose 2^-24 entry
+        # differences alone moved the fp64 solution by up to 2.6e-4 at these pivot ratios
+        x64, ratio64 = exact_system_solution(ft, wf, N)
+        if x64 is None:
+            break
         e_plain, e_ref = nan_rel_err(plain[0], x64), nan_rel_err(refined[0], x64)
         gate = plain[3]
         rows.append((k + 1, gate, ratio64, e_plain, e_ref))
-        opens = REFINE_FLOOR <= gate < threshold
+        refines = gate >= floor                 # the forced-open solve ran the refinement step
+        opens = refines and gate < threshold    # ... and the product's gate does
         print(f"{name} iteration {k + 1}: corner pivot / diag(S) {gate:.3g} (gate {'open' if opens else 'shut'}: window "
-              f"[{REFINE_FLOOR:g}, {threshold:g})), fp64 pivot ratio {ratio64:.3g}, err vs fp64: plain f32 {e_plain:.3g}, "
+              f"[{floor:g}, {threshold:g})), exact-system fp64 pivot ratio {ratio64:.3g}, err vs fp64: plain f32 {e_plain:.3g}, "
               f"forced refinement {e_ref:.3g}", flush=True)
+        accepted = refined[4]["accepted"]
+        print(f"    forced step: max |d| / max |x| {refined[4]['correction']:.3g}, accepted {accepted}", flush=True)
         if gate >= threshold:
             assert e_plain <= 1e-4, f"iteration {k + 1}: gate shut at {gate:.3g} but the plain solve is {e_plain:.3g} from fp64"
+        if refines:
+            # the safeguard: a step never leaves the solve further from the exact solution than the plain solve (a rejected
+            # step keeps the plain solve bit for bit) ...
+            assert e_ref <= max(e_plain, 1e-4), f"iteration {k + 1}: refined {e_ref:.3g} vs plain {e_plain:.3g}"
+            if not accepted:
+                assert np.array_equal(refined[0], plain[0])
+            # ... and an accepted one converges wherever the system is not degenerate
+            if accepted and ratio64 > REFINED_PIVOT_RATIO:
+                assert e_ref <= 1e-4, f"iteration {k + 1}: refined solve {e_ref:.3g} from fp64 at corner pivot / diag(S) {gate:.3g}"
         elif ratio64 > REFINE_PIVOT_RATIO:
-            e_prod = e_ref if opens else e_plain
-            assert e_prod <= 1e-4, f"iteration {k + 1}: solve {e_prod:.3g} from fp64 at fp64 pivot ratio {ratio64:.3g}"
+            assert e_plain <= 1e-4, f"iteration {k + 1}: unrefined solve {e_plain:.3g} from fp64 at fp64 pivot ratio {ratio64:.3g}"
         if not opens:   # continue along the product's trajectory
             solve(R0, t0, k, 0.0)
     ft.set_refine_ratio(threshold)
@@ -1215,9 +1266,10 @@ def test_c3_raster_parity_and_iteration_properties(nn, S, oracle_mod):
     assert np.isfinite(dg["updates"]).all()
     # the full GN iteration against the oracle at 1280x960 / 4.5 M triangles / 3000 nodes (DeformableMeshToImageFitter.cpp:
     # 111-275): pixel faces exact, residuals, H and g <= 1e-6, updates <= 1e-4
-    _, t_o, dg_o = oracle_fit_scene(oracle_mod, sc, depth, 1)
+    R_o, t_o, dg_o = oracle_fit_scene(oracle_mod, sc, depth, 1)
     _compare_iteration(dg_o, dg, 6, N)
     assert rel_err(wf.get_node_translations(True), t_o) < 1e-4
+    assert rel_err(wf.get_node_rotations(True) - np.eye(3), R_o - np.eye(3)) < 1e-4
     # SURVEY 8(d) C3's parity condition (A4, PixelVertexAnchorJacobiansImpl.h:33, :348-358): no node's pixel list reaches
     # the reference's 4000-entry cap, so its capped lists hold the same associations as the uncapped math here
     a, _ = ft.anchors(len(sc.points), 4)

@@ -24,7 +24,7 @@ for l in ${LINES:-c5 c3 c1 c1_arap c2_arap_frame replicas8}; do
 		c3) line c3 400 --config C3 --cpu-share-only --cpu-no-warm --cpu-seconds 1 || exit 1 ;;
 		c1) line c1 400 --config C1 || exit 1 ;;
 		c1_arap) line c1_arap 400 --config C1_ARAP || exit 1 ;;
-		c2_arap_frame) line c2_arap_frame 400 --config C2_ARAP --step frame --graph-steps 10 || exit 1 ;;
+		c2_arap_frame) line c2_arap_frame 400 --config C2_ARAP --step frame --graph-steps 6 || exit 1 ;;
 		replicas8) line replicas8 300 --config C2 --replicas 8 --no-cpu-baseline || exit 1 ;;
 	esac
 done
