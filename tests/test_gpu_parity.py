@@ -631,8 +631,8 @@ def _new_fit(nn, sc, depth, iterations):
 # solve of that iteration-3 system 6.0e-4 from fp64. Each build's trajectory is pinned at its own measurement.
 # Round 6: these errors are measured against a system re-assembled from the ORACLE's ARAP blocks, whose own 2^-24 entry
 # rounding moves the fp64 solution by 8.7e-6 (iteration 2) .. 4e-6 (iteration 3) here -- the floor any solver meets them
-# at (the GPU's refined solves are 2.4e-8 / 3.0e-7 from the fp64 solution of their OWN system: PINNED_EXACT_ERRORS); a
-# float re-association elsewhere in the solve moved iteration 2's from 2.0e-5 to 3.0e-5 with its exact error unchanged
+# at (the GPU's refined solves are 2e-8 / 3e-7 from the fp64 solution of their OWN system: PINNED_EXACT_ERRORS); a
+# development build that re-associated the substitution sums moved iteration 2's from 2.0e-5 to 3.0e-5, its exact error unchanged
 PINNED_SOLVE_ERRORS = {("C5", 1): 3e-6, ("C5", 2): 5e-5, ("C5", 3): 2.6e-4}
 PINNED_SOLVE_ERRORS_FMA = {("C5", 1): 3e-6, ("C5", 2): 3e-5, ("C5", 3): 1.6e-3}
 # the same iterations against the fp64 solution of exactly the float system the GPU solved (nnrt_fitter_get_arrowhead_system;
