@@ -65,13 +65,14 @@ def max_over_ranks(value: float, device=None) -> float:
 MIN_WARM_S = 0.05   # seconds of untimed back-to-back GPU work before the timed region (clock ramp-up)
 
 
-def timed_region(step, launches: int, per_launch: int, world: int, sync, dist_on=None) -> tuple:
+def timed_region(step, launches: int, per_launch: int, world: int, sync, dist_on=None, group=None) -> tuple:
     """The timed protocol: barrier + device sync, `launches` x step(per_launch), device sync, barrier. Returns (OR of
-    the step return codes, this rank's elapsed seconds). dist_on: barriers on (default: world > 1)."""
+    the step return codes, this rank's elapsed seconds). dist_on: barriers on (default: world > 1); group: the process
+    group the barriers run on (default: the world group)."""
     import torch.distributed as dist
     dist_on = world > 1 if dist_on is None else dist_on
     if dist_on:
-        dist.barrier()
+        dist.barrier(group=group)
     sync()
     t0 = time.perf_counter()
     bad = 0
@@ -80,7 +81,7 @@ def timed_region(step, launches: int, per_launch: int, world: int, sync, dist_on
     sync()
     elapsed = time.perf_counter() - t0
     if dist_on:
-        dist.barrier()
+        dist.barrier(group=group)
     return bad, elapsed
 
 
@@ -378,11 +379,18 @@ def main(argv=None):
     # NNRT_BENCH_DIST_ONE_RANK=1: the process group, barriers and collectives also at WORLD_SIZE 1 (a one-GPU box can
     # run the RCCL branch itself: torch.distributed.run --nproc-per-node 1)
     use_dist = world > 1 or os.environ.get("NNRT_BENCH_DIST_ONE_RANK") == "1"
+    ctrl_group = None
     if use_dist:
         if backend == "gloo":
             dist.init_process_group(backend="gloo")
         else:
-            dist.init_process_group(backend="nccl", device_id=dev)
+            # RCCL carries the collectives over device tensors (max-over-ranks, the per-rank all-gather). Its communicator
+            # is created lazily by the first of them, AFTER the timed region: with the communicator up (and its proxy
+            # thread) a one-rank RCCL line ran 0.6-3.7 % slower than the plain line, the graph replay itself 0.8 %
+            # (round 6, tools/dev/rccl_overhead.sh; a gloo process group cost 0.5 %). The timed region's two barriers run
+            # on a gloo group of the same ranks -- no data-path collective exists to overlap (replicas).
+            dist.init_process_group(backend="nccl")
+            ctrl_group = dist.new_group(backend="gloo")
     coll_dev = "cpu" if backend == "gloo" else dev
 
     from dynamicfuion_python_amd import _native as NV
@@ -473,7 +481,7 @@ def main(argv=None):
 
     launches = -(-args.steps // per_launch)
     args.steps = launches * per_launch   # whole graphs only: the timed step count is rounded up to a multiple
-    bad, elapsed = timed_region(step, launches, per_launch, world, lambda: torch.cuda.synchronize(dev), dist_on=use_dist)
+    bad, elapsed = timed_region(step, launches, per_launch, world, lambda: torch.cuda.synchronize(dev), dist_on=use_dist, group=ctrl_group)
     if bad:
         NV.check(bad)
     per_replica = []
@@ -606,7 +614,7 @@ def main(argv=None):
         "config": {"workload": workload, "config": args.config, "frame": [sc.H, sc.W], "nodes": Nn, "vertices": V, "triangles": F,
                    "anchors": 4, "iteration_mode": "ALL", "lm_damping": 0.001, "hip_graph": True, "steps_per_graph": per_launch, "step": args.step,
                    "parallelism": f"replicas{world * R}" if world * R > 1 else "single", "replicas_per_gpu": R,
-                   **({"collectives": "rccl" if backend == "nccl" else f"{backend} (rehearsal: {world} ranks on "
+                   **({"collectives": "rccl (max-over-ranks, per-rank all-gather; timed-region barriers on a gloo group)" if backend == "nccl" else f"{backend} (rehearsal: {world} ranks on "
                                                                        f"{torch.cuda.device_count()} visible GPU(s))"}
                       if use_dist else {})},
         "setup_ms": round(setup_ms, 3),
