@@ -11,6 +11,7 @@
 #include "kernels.hpp"
 
 #include <hipcub/hipcub.hpp>
+#include <cstdlib>
 
 namespace nnrt {
 
@@ -98,12 +99,23 @@ constexpr int SCATTER_FPW = 32;                                          // face
 constexpr int SCATTER_FACES_PER_BLOCK = SCATTER_WAVES * SCATTER_FPW;
 constexpr int SCATTER_TILE_KEYS = 512;                                   // 4 KiB per wave
 
-struct ScatterWaveLds {
-	uint64_t keys[SCATTER_TILE_KEYS];
-	float4 rec[SCATTER_FPW][4];   // x0 x1 x2 y0 | y1 y2 z0 z1 | z2 inv_area (u0 | span_u << 16) (v0 | fast << 30 | near_all << 31) |
+template <int FPW, int KEYS>
+struct ScatterLds {
+	static constexpr int faces = FPW, tile_keys = KEYS;
+	uint64_t keys[KEYS];
+	float4 rec[FPW][4];           // x0 x1 x2 y0 | y1 y2 z0 z1 | z2 inv_area (u0 | span_u << 16) (v0 | fast << 30 | near_all << 31) |
 	                              // A x1-x2 x2-x0 x0-x1 (the rows' face constants: face_row_constants)
 	uint32_t row[64];             // one round of row tasks: face slot | row << 8
 };
+using ScatterWaveLds = ScatterLds<SCATTER_FPW, SCATTER_TILE_KEYS>;
+// Dense meshes (more faces than pixels, e.g. C3's 4.5 M mostly sub-pixel triangles at 1280 x 960): one face per lane, 64
+// per wave -- the wave's fixed costs (face loads in flight, box reductions, row dealing, tile clear and merge) serve
+// twice the faces, and half the waves run the launch's latency rounds -- with a 256-key tile (64 consecutive sub-pixel
+// faces cover a small pixel box), which keeps six waves per SIMD. The per-face operations are face_pixel_range's, the
+// scatter the same keyed minimum: results identical to the lane-pair path (round 6).
+constexpr int DENSE_FPW = 64;
+constexpr int DENSE_TILE_KEYS = 256;
+using DenseWaveLds = ScatterLds<DENSE_FPW, DENSE_TILE_KEYS>;
 
 __device__ inline void scatter_wave_sync() {
 	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -196,14 +208,16 @@ __device__ inline void scatter_row(const FaceNdc& fn, float inv_area, float4 k, 
 	}
 }
 
-__device__ inline void scatter_rows(int rows, int slot, int32_t face0, const RasterOptions& o, uint64_t* keys, ScatterWaveLds& w, bool staged,
+template <class W>
+__device__ inline void scatter_rows(int rows, int slot, int32_t face0, const RasterOptions& o, uint64_t* keys, W& w, bool staged,
                                     int bu0, int bv0, int tw, int th);
 #ifdef NNRT_KERNEL_STAMPS
 __device__ unsigned long long g_raster_stamps[16384][8];   // start, setup end, end, hwid, rows, tile, pixels, max pixels per lane
 #endif
 
-// lane < SCATTER_FPW holds face face0 + lane (ok = it exists and is not masked out); all 64 lanes of the wave call this
-__device__ inline void scatter_wave(const FaceNdc& fn, bool ok, int32_t face0, const RasterOptions& o, uint64_t* keys, ScatterWaveLds& w) {
+// lane < W::faces holds face face0 + lane (ok = it exists and is not masked out); all 64 lanes of the wave call this
+template <class W>
+__device__ inline void scatter_wave(const FaceNdc& fn, bool ok, int32_t face0, const RasterOptions& o, uint64_t* keys, W& w) {
 	const int lane = static_cast<int>(threadIdx.x & 63);
 	int u0 = 0, u1 = -1, v0 = 0, v1 = -1;
 	if (ok) ok = face_pixel_range(fn, o, u0, u1, v0, v1);
@@ -217,7 +231,7 @@ __device__ inline void scatter_wave(const FaceNdc& fn, bool ok, int32_t face0, c
 	}
 	if (bu1 < 0) return;   // wave-uniform: none of the wave's faces covers a pixel
 	const int tw = bu1 - bu0 + 1, th = bv1 - bv0 + 1;
-	const bool staged = tw * th <= SCATTER_TILE_KEYS;
+	const bool staged = tw * th <= W::tile_keys;
 	if (staged)
 		for (int i = lane; i < tw * th; i += 64) w.keys[i] = EMPTY_KEY;
 	const int rows = ok ? v1 - v0 + 1 : 0;
@@ -240,7 +254,8 @@ __device__ inline void scatter_wave(const FaceNdc& fn, bool ok, int32_t face0, c
 
 // Deals the wave's face rows one per lane (rows: this lane's face's box rows, slot: its face's record) and scatters
 // them, then merges the staged tile into the image. All 64 lanes call this.
-__device__ inline void scatter_rows(int rows, int slot, int32_t face0, const RasterOptions& o, uint64_t* keys, ScatterWaveLds& w, bool staged,
+template <class W>
+__device__ inline void scatter_rows(int rows, int slot, int32_t face0, const RasterOptions& o, uint64_t* keys, W& w, bool staged,
                                     int bu0, int bv0, int tw, int th) {
 	const int lane = static_cast<int>(threadIdx.x & 63);
 	int incl = rows;
@@ -454,10 +469,33 @@ __global__ __launch_bounds__(SCATTER_BLOCK) void k_raster_scatter_mesh(const flo
 	NNRT_WAVE_STAMP(g_raster_stamps, 2, __builtin_amdgcn_s_memrealtime());
 }
 
+// dense meshes: one face per lane (DenseWaveLds)
+__global__ __launch_bounds__(SCATTER_BLOCK) void k_raster_scatter_mesh_dense(const float4* __restrict__ wpos, const int4* __restrict__ faces4,
+                                                                             int64_t F, NdcSetup s, float near_clip, float far_clip, RasterOptions o,
+                                                                             uint64_t* __restrict__ keys) {
+	__shared__ DenseWaveLds s_wave[SCATTER_WAVES];
+	const int64_t face0 = (static_cast<int64_t>(blockIdx.x) * SCATTER_WAVES + (threadIdx.x >> 6)) * DENSE_FPW;
+	const int64_t f = face0 + static_cast<int>(threadIdx.x & 63);
+	FaceNdc fn{};
+	const bool ok = f < F && project_mesh_face(wpos, faces4[f], s, near_clip, far_clip, fn);
+	scatter_wave(fn, ok, static_cast<int32_t>(face0), o, keys, s_wave[threadIdx.x >> 6]);
+}
+
+bool raster_mesh_dense(int64_t F, const RasterOptions& o) {
+	if (const char* v = std::getenv("NNRT_RASTER_DENSE")) return *v == '1';   // development switch: 0 / 1 force a path
+	return F >= static_cast<int64_t>(o.H) * o.W;
+}
+
 nnrt_status launch_raster_scatter_mesh(const float4* wpos, const int4* faces4, int64_t F, const NdcSetup& s, float near_clip, float far_clip,
                                        const RasterOptions& o, uint64_t* keys, hipStream_t stream) {
 	if (F == 0) return NNRT_OK;
 	NNRT_CHECK_ARG(o.W < 65536 && F < (int64_t(1) << 31), "image wider than 65535 pixels or more than 2^31 faces");
+	if (raster_mesh_dense(F, o)) {
+		k_raster_scatter_mesh_dense<<<static_cast<unsigned>(ceil_div(F, SCATTER_WAVES * DENSE_FPW)), SCATTER_BLOCK, 0, stream>>>(wpos, faces4, F, s, near_clip,
+		                                                                                                                   far_clip, o, keys);
+		NNRT_LAUNCH_CHECK();
+		return NNRT_OK;
+	}
 	k_raster_scatter_mesh<<<static_cast<unsigned>(ceil_div(F, SCATTER_FACES_PER_BLOCK)), SCATTER_BLOCK, 0, stream>>>(wpos, faces4, F, s, near_clip,
 	                                                                                                                 far_clip, o, keys);
 	NNRT_LAUNCH_CHECK();

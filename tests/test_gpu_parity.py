@@ -1316,6 +1316,38 @@ def test_pixel_tile_order_same_iteration(nn, S, oracle_mod, name):
     assert nan_rel_err(a["updates"][: 6 * N], b["updates"][: 6 * N]) < 1e-5
 
 
+@pytest.mark.parametrize("name", ["S1", "C2"])
+def test_raster_dense_path_same_iteration(nn, S, oracle_mod, name):
+    """The dense-mesh scatter (one face per lane, 64 per wave; the default when a mesh has at least as many faces as the
+    image has pixels, e.g. C3) and the lane-pair scatter (C1 / C2) perform the same per-face operations into the same
+    keyed minimum: forced on (NNRT_RASTER_DENSE=1) and off (=0) on sparser scenes, the rasterization is bit-identical (faces,
+    masks, residuals) and the data term equal to its fp64 summation order."""
+    import os
+    sc = _scene(S, oracle_mod, name)
+    depth = scene_target(oracle_mod, sc)
+    N = len(sc.nodes)
+    old = os.environ.get("NNRT_RASTER_DENSE")
+    out = {}
+    try:
+        for v in ("1", "0"):
+            os.environ["NNRT_RASTER_DENSE"] = v
+            _, _, dg = _gpu_fit(nn, sc, depth, 1)
+            out[v] = dg
+    finally:
+        if old is None:
+            os.environ.pop("NNRT_RASTER_DENSE", None)
+        else:
+            os.environ["NNRT_RASTER_DENSE"] = old
+    a, b = out["1"], out["0"]
+    assert (a["pixel_faces"] >= 0).sum() > 1000
+    for k in ("pixel_faces", "residual_mask", "residuals"):
+        assert np.array_equal(a[k], b[k]), k
+    # (H and g: the fp64 atomics' order differs run to run, as in test_pixel_tile_order_same_iteration)
+    assert rel_err(a["hessian"][: 36 * N], b["hessian"][: 36 * N]) < 1e-6
+    assert rel_err(a["gradient"][: 6 * N], b["gradient"][: 6 * N]) < 1e-6
+    assert nan_rel_err(a["updates"][: 6 * N], b["updates"][: 6 * N]) < 1e-5
+
+
 def test_errors_fail_loudly(nn, S, oracle_mod):
     A, G = nn.alignment, nn.geometry
     with pytest.raises(RuntimeError):
