@@ -2,6 +2,8 @@
 // NDC face extraction, depth unprojection, attribute interpolation, Rodrigues.
 #include "kernels.hpp"
 
+#include <cstdlib>
+
 namespace nnrt {
 
 // =====================================================================================================================
@@ -341,10 +343,85 @@ __global__ __launch_bounds__(256) void k_warp_mesh_quad(const float* __restrict_
 	NNRT_WAVE_STAMP(g_warp_stamps, 2, __builtin_amdgcn_s_memrealtime());
 }
 
+// Large meshes (C3: 2.25 M vertices): one lane per vertex, its K <= 4 anchor slots' loads (anchors and weights as one
+// 16-B load each when K = 4) and node-state gathers issued together, the slots summed in slot order as the quad kernel's
+// slot-0 lane sums them (warp_slot's contributions, invalid slots skipped): bit-identical positions and normals, a
+// quarter of the waves, four gathers in flight per lane (round 6; the quad kernel's 140 k waves ran 17 residency rounds
+// of two dependent memory round trips each). Positions and normals only (the fitter's warp: no Jacobian rows).
+template <bool IDENTITY, bool VEC4>
+__global__ __launch_bounds__(256) void k_warp_mesh_vertex(const float* __restrict__ points, const float* __restrict__ normals, int64_t V,
+                                                          const float* __restrict__ node_state, const int32_t* __restrict__ anchors,
+                                                          const float* __restrict__ weights, int K, WarpExtrinsics E, float4* __restrict__ out_p,
+                                                          float4* __restrict__ out_n) {
+	const int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (v >= V) return;
+	const f3 p = make3(points[3 * v], points[3 * v + 1], points[3 * v + 2]);
+	const f3 n = make3(normals[3 * v], normals[3 * v + 1], normals[3 * v + 2]);
+	int32_t a[4];
+	float w[4];
+	if constexpr (VEC4) {
+		const int4 a4 = reinterpret_cast<const int4*>(anchors)[v];
+		const float4 w4 = reinterpret_cast<const float4*>(weights)[v];
+		a[0] = a4.x, a[1] = a4.y, a[2] = a4.z, a[3] = a4.w;
+		w[0] = w4.x, w[1] = w4.y, w[2] = w4.z, w[3] = w4.w;
+	} else {
+#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			a[k] = k < K ? anchors[v * K + k] : -1;
+			w[k] = k < K ? weights[v * K + k] : 0.f;
+		}
+	}
+	f3 pc = p, nc = n;
+	if (!E.identity) {
+		pc = apply_extrinsics_point(E, p);
+		nc = apply_extrinsics_normal(E, n);
+	}
+	// every slot's node state first (clamped indices, no branch: the four gathers leave together)
+	float4 ns[4][4];
+#pragma unroll
+	for (int k = 0; k < 4; k++) load_warp_state<IDENTITY>(node_state, (k < K && a[k] != -1) ? a[k] : 0, ns[k]);
+	f3 wp = make3(0.f, 0.f, 0.f), wn = make3(0.f, 0.f, 0.f);
+#pragma unroll
+	for (int k = 0; k < 4; k++) {
+		const bool valid = k < K && a[k] != -1;
+		f3 cp, cn;
+		float4 ojv, ojn;   // (unused: no rows on this path)
+		warp_slot_state<IDENTITY>(ns[k], w[k], p, n, pc, nc, E.identity, cp, cn, ojv, ojn);
+		if (valid) {
+			wp.x += cp.x;
+			wp.y += cp.y;
+			wp.z += cp.z;
+			wn.x += cn.x;
+			wn.y += cn.y;
+			wn.z += cn.z;
+		}
+	}
+	out_p[v] = make_float4(wp.x, wp.y, wp.z, 0.f);
+	out_n[v] = make_float4(wn.x, wn.y, wn.z, 0.f);
+}
+
+static bool warp_vertex_path(int64_t V) {
+	if (const char* e = std::getenv("NNRT_WARP_VERTEX")) return *e == '1';   // development switch: 0 / 1 force a path
+	return V >= (int64_t{1} << 19);
+}
+
 nnrt_status launch_warp_mesh(const float* points, const float* normals, int64_t V, const float* node_state, const int32_t* anchors,
                              const float* weights, int K, const WarpExtrinsics& E, float4* out_p, float4* out_n, float2* jrows,
                              hipStream_t stream, bool from_identity) {
 	if (V == 0) return NNRT_OK;
+	if (K <= 4 && !jrows && warp_vertex_path(V)) {
+		const unsigned grid = static_cast<unsigned>(ceil_div(V, 256));
+		const bool vec4 = K == 4 && (reinterpret_cast<uintptr_t>(anchors) & 15) == 0 && (reinterpret_cast<uintptr_t>(weights) & 15) == 0;
+		if (from_identity) {
+			if (vec4) k_warp_mesh_vertex<true, true><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n);
+			else k_warp_mesh_vertex<true, false><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n);
+		} else {
+			if (vec4) k_warp_mesh_vertex<false, true><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n);
+			else k_warp_mesh_vertex<false, false><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n);
+		}
+		NNRT_LAUNCH_CHECK();
+		return NNRT_OK;
+	}
 	if (K <= 4) {
 		const unsigned grid = static_cast<unsigned>(std::min<int64_t>(ceil_div(4 * V, 256), WARP_MAX_WGS));
 		if (from_identity)

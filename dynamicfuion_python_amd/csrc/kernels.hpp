@@ -16,9 +16,8 @@ WarpExtrinsics make_extrinsics(const double* E);
 // p / n: the vertex as stored; pc / nc: after the extrinsics. IDENTITY: R = I, t = 0 without reading them. Shared by
 // the warp kernels.
 template <bool IDENTITY>
-__device__ inline void warp_slot(const float* __restrict__ node_state, int32_t a, float w, f3 p, f3 n, f3 pc, f3 nc, int extr_identity, f3& cp,
-                                 f3& cn, float4& ojv, float4& ojn) {
-	const float4* ns = reinterpret_cast<const float4*>(node_state + static_cast<int64_t>(a) * NODE_STRIDE);
+__device__ inline void warp_slot_state(const float4 (&ns)[4], float w, f3 p, f3 n, f3 pc, f3 nc, int extr_identity, f3& cp, f3& cn, float4& ojv,
+                                       float4& ojn) {
 	f3 g, t;
 	float R[9];
 	if constexpr (IDENTITY) {
@@ -43,6 +42,27 @@ __device__ inline void warp_slot(const float* __restrict__ node_state, int32_t a
 	const f3 Rnj = extr_identity ? Rn : matvec3(R, n);
 	ojv = make_float4(-w * Rj.x, -w * Rj.y, -w * Rj.z, w);
 	ojn = make_float4(-w * Rnj.x, -w * Rnj.y, -w * Rnj.z, 0.f);
+}
+// the node's state rows (g, t, R: one 64-B line; IDENTITY: g only), loaded ahead of warp_slot_state by callers that keep
+// several slots' gathers in flight
+template <bool IDENTITY>
+__device__ inline void load_warp_state(const float* __restrict__ node_state, int32_t a, float4 (&ns)[4]) {
+	const float4* q = reinterpret_cast<const float4*>(node_state + static_cast<int64_t>(a) * NODE_STRIDE);
+	ns[0] = q[0];
+	if constexpr (!IDENTITY) {
+		ns[1] = q[1];
+		ns[2] = q[2];
+		ns[3] = q[3];
+	} else {
+		ns[1] = ns[2] = ns[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+	}
+}
+template <bool IDENTITY>
+__device__ inline void warp_slot(const float* __restrict__ node_state, int32_t a, float w, f3 p, f3 n, f3 pc, f3 nc, int extr_identity, f3& cp,
+                                 f3& cn, float4& ojv, float4& ojn) {
+	float4 ns[4];
+	load_warp_state<IDENTITY>(node_state, a, ns);
+	warp_slot_state<IDENTITY>(ns, w, p, n, pc, nc, extr_identity, cp, cn, ojv, ojn);
 }
 
 // one (vertex, anchor) slot's warped-Jacobian row as 24 B: (jv.x, jv.y) (jv.z, jn.x) (jn.y, jn.z); the weight w is not

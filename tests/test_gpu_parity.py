@@ -84,11 +84,14 @@ def test_warp_bit_exact(nn, S, oracle_mod, extrinsic):
     assert np.array_equal(wn_o, _np(m.vertex_normals))
 
 
-@pytest.mark.parametrize("name,from_identity", [("C1", False), ("C1", True), ("C2", False)])
-def test_fitter_warp_bit_exact(nn, S, oracle_mod, name, from_identity):
-    """The fitter's own warp (k_warp_mesh_mv: several 16-vertex runs per wave, canonical float4 inputs) -- the mesh an
-    iteration rasterizes -- equals the oracle's warp of the motion the iteration started from, bit for bit: from the
-    ground-truth motion (general kernel) and from the identity (iterate_from_identity's IDENTITY kernel)."""
+@pytest.mark.parametrize("name,from_identity,vertex_path", [("C1", False, "0"), ("C1", True, "0"), ("C2", False, "0"), ("C1", False, "1"),
+                                                             ("C1", True, "1"), ("C2", False, "1")])
+def test_fitter_warp_bit_exact(nn, S, oracle_mod, name, from_identity, vertex_path, monkeypatch):
+    """The fitter's own warp -- the mesh an iteration rasterizes -- equals the oracle's warp of the motion the iteration
+    started from, bit for bit: from the ground-truth motion (general kernel) and from the identity (iterate_from_identity's
+    IDENTITY kernel); with the lane-per-(vertex, slot) quad kernel (C1 / C2 size) and, forced by NNRT_WARP_VERTEX=1, the
+    lane-per-vertex kernel large meshes take (C3)."""
+    monkeypatch.setenv("NNRT_WARP_VERTEX", vertex_path)
     sc = _scene(S, oracle_mod, name)
     depth = scene_target(oracle_mod, sc)
     wf, ft = _new_fit(nn, sc, depth, 1)
