@@ -1719,6 +1719,29 @@ __device__ __forceinline__ void flow_signal(unsigned* w0, unsigned* w1 = nullptr
 	}
 }
 
+// While a dataflow back chain waits for its parent chain (k_corner_flow), it pulls the entry tiles of its columns into
+// this XCD's L2: one 16-B LDS-DMA piece per 64-B segment of every tile (256 threads x 64 B = one 16-KB tile per
+// instruction), the data itself dropped in a 4-KB LDS scratch. The tiles were written by the factor launches on any XCD;
+// the chain's entry sums then hit L2 instead of going to memory on their critical path. Bounded by FLOW_PREFETCH_TILES
+// (NNRT_FLOW_PREFETCH=0: off). The DMA completes in the background; the chain's first tile_to_lds wait retires it.
+#ifndef NNRT_FLOW_PREFETCH
+#define NNRT_FLOW_PREFETCH 64
+#endif
+constexpr int FLOW_PREFETCH_TILES = NNRT_FLOW_PREFETCH;
+__device__ __forceinline__ void flow_prefetch_chain(const CornerBackArgs& a, int2 ch) {
+	__shared__ __attribute__((aligned(16))) float s_pf[CT * 4];
+	const int t = threadIdx.x, wave = t >> 6;
+	int left = FLOW_PREFETCH_TILES;
+	for (int q = 0; q < ch.y && left > 0; q++) {
+		const int4 col = a.cols[ch.x + q];   // wave-uniform (scalar loads)
+		for (int e = 0; e < col.z && left > 0; e++, left--) {
+			const int slot = a.ent[col.y + e].x;
+			const float* src = a.tiles + static_cast<int64_t>(slot) * TILE_ELEMS + 16 * t;
+			__builtin_amdgcn_global_load_lds((corner_global_t*)src, (corner_lds_t*)(s_pf + wave * 256), 16, 0, 0);
+		}
+	}
+}
+
 __global__ __launch_bounds__(CT) void k_corner_flow(FlowArgs a) {
 	__shared__ int s_ticket;
 	const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
@@ -1742,6 +1765,7 @@ __global__ __launch_bounds__(CT) void k_corner_flow(FlowArgs a) {
 	// ---- the solve: back chains (root first), then the stem pass ----
 	if (k < nB) {
 		const int4 ch = a.chains[k];
+		if (FLOW_PREFETCH_TILES > 0 && ch.w >= 0) flow_prefetch_chain(a.back, make_int2(ch.x, ch.y));
 		if (ch.w >= 0 && !flow_wait(back_done0 + ch.w, 1u, a.st.error_flag)) return;
 		FLOW_RT(k, 64, 1);
 		corner_back_chain<true, false>(a.back, make_int2(ch.x, ch.y), a.ld, a.nxout);
