@@ -106,6 +106,19 @@ def test_argument_errors_are_reported(native):
     assert b"ndc_convention" in lib.nnrt_last_error()
 
 
+def test_diagnostic_exports_refuse_bad_arguments(native):
+    """The diagnostic copies (nnrt_fitter_get_arrowhead_system, nnrt_fitter_get_warped_mesh) check their pointers and the
+    prepared frame before touching the device (a caller-sized host buffer is never written past); the build
+    reports its refinement floor and Jacobian arithmetic."""
+    lib = native.lib()
+    buf = np.zeros(64, np.float32)
+    assert lib.nnrt_fitter_get_arrowhead_system(None, native.ptr(buf), native.ptr(buf), native.ptr(buf), 1, 1, None) == 1
+    assert b"null" in lib.nnrt_last_error()
+    assert lib.nnrt_fitter_get_warped_mesh(None, native.ptr(buf), native.ptr(buf), 1, None) == 1
+    assert native.refine_floor() == pytest.approx(1e-5)
+    assert native.jacobian_fma() is False   # the product: the reference CPU path's unfused arithmetic
+
+
 def test_overlapping_outputs_are_rejected(native):
     """outputs that overlap an input the kernel still reads are refused before any device work (pointer
     arithmetic only, so this runs without a GPU): InvertTriangularBlocks into its own blocks, BlockSparseAndVectorProduct
