@@ -15,7 +15,7 @@ def per_dispatch(path_glob, counter, kernel_prefix):
     vals = []
     for path in glob.glob(path_glob, recursive=True):
         for r in csv.DictReader(open(path)):
-            if r["Counter_Name"] == counter and kernel_prefix in r["Kernel_Name"]:
+            if r["Counter_Name"] == counter and any(k in r["Kernel_Name"] for k in kernel_prefix.split("|")):
                 vals.append(float(r["Counter_Value"]))
     return vals
 
@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--fetch", default="gpurun_out/pmc_fetch/**/*counter_collection.csv")
     ap.add_argument("--write", default="gpurun_out/pmc_write/**/*counter_collection.csv")
     ap.add_argument("--kernels", nargs="+", default=["k_fit_pixels_fused<0, 4>", "k_raster_scatter_mesh",
-                                                      "k_warp_mesh_quad", "k_solve_update_lanes<0"])
+                                                      "k_warp_mesh_quad|k_warp_mesh_vertex", "k_solve_update_lanes<0"])
     ap.add_argument("--workload", required=True, help="bench.py config.workload string the passes ran")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -37,7 +37,8 @@ def main():
             raise SystemExit(f"no dispatches of {sym}: fetch {len(f)} write {len(w)}")
         fetch_kib = sum(f) / len(f)
         write_kib = sum(w) / len(w)
-        kernels[sym.split("<")[0]] = {"kernel_symbol": sym, "dispatches": [len(f), len(w)], "fetch_size_kib": fetch_kib,
+        # "a|b": the kernel under either name (the warp's launch path depends on the mesh size), keyed by the first
+        kernels[sym.split("|")[0].split("<")[0]] = {"kernel_symbol": sym, "dispatches": [len(f), len(w)], "fetch_size_kib": fetch_kib,
                                       "write_size_kib": write_kib, "hbm_bytes_per_launch": (2 * fetch_kib + write_kib) * 1024.0}
     out = {"workload": a.workload, "kernels": kernels,
            "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count correction)"}
