@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/../../dynamicfuion_python_amd/csrc"
 name=$1; defs=$2
 mkdir -p variants build/var_$name
-FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -munsafe-fp-atomics -Wno-unused-result -I../../include"
+FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -munsafe-fp-atomics -Wno-unused-result -Wno-unused-value -I../../include"
 for src in *.hip; do
 	/opt/rocm/bin/hipcc $FLAGS $defs -x hip -c $src -o build/var_$name/${src%.hip}.o &
 done
