@@ -343,11 +343,13 @@ __global__ __launch_bounds__(256) void k_warp_mesh_quad(const float* __restrict_
 	NNRT_WAVE_STAMP(g_warp_stamps, 2, __builtin_amdgcn_s_memrealtime());
 }
 
-// Large meshes (C3: 2.25 M vertices): one lane per vertex, its K <= 4 anchor slots' loads (anchors and weights as one
+// Meshes of 64 k vertices and more (C1 / C2 / C5: 77 k, C3: 2.25 M): one lane per vertex, its K <= 4 anchor slots' loads (anchors and weights as one
 // 16-B load each when K = 4) and node-state gathers issued together, the slots summed in slot order as the quad kernel's
 // slot-0 lane sums them (warp_slot's contributions, invalid slots skipped): bit-identical positions and normals, a
 // quarter of the waves, four gathers in flight per lane (round 6; the quad kernel's 140 k waves ran 17 residency rounds
-// of two dependent memory round trips each). Positions and normals only (the fitter's warp: no Jacobian rows).
+// of two dependent memory round trips each: C3 61.7 -> 45 us; C2 4.9 -> 4.7 us). Smaller meshes keep the quad kernel's
+// four lanes per vertex (more waves for a launch that is mostly latency). Positions and normals only (the fitter's warp:
+// no Jacobian rows).
 template <bool IDENTITY, bool VEC4>
 __global__ __launch_bounds__(256) void k_warp_mesh_vertex(const float* __restrict__ points, const float* __restrict__ normals, int64_t V,
                                                           const float* __restrict__ node_state, const int32_t* __restrict__ anchors,
@@ -402,7 +404,7 @@ __global__ __launch_bounds__(256) void k_warp_mesh_vertex(const float* __restric
 
 static bool warp_vertex_path(int64_t V) {
 	if (const char* e = std::getenv("NNRT_WARP_VERTEX")) return *e == '1';   // development switch: 0 / 1 force a path
-	return V >= (int64_t{1} << 19);
+	return V >= (int64_t{1} << 16);
 }
 
 nnrt_status launch_warp_mesh(const float* points, const float* normals, int64_t V, const float* node_state, const int32_t* anchors,
