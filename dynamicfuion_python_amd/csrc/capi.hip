@@ -382,6 +382,7 @@ struct nnrt_fitter {
 	DeviceBuffer<float4> ref_points;   // [P] reference point (x, y, z, valid)
 	DeviceBuffer<int> tile_flags, tile_order;   // the pixel launch's per-frame workgroup -> tile table (launch_tile_order)
 	bool use_tile_order = false;
+	bool pix_low_occupancy = false;   // the pixel launch's 4-waves-per-SIMD build (launches of several residency rounds)
 	DeviceBuffer<float4> records;      // [P, 4] pixel Jacobian records
 	DeviceBuffer<uint64_t> keys;
 	DeviceBuffer<float> residuals;
@@ -531,6 +532,7 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 		fa.order_blocks = tile_order_blocks(fa.tiles_x * fa.tiles_y);
 	}
 	fa.records = ft->records.ptr;
+	fa.low_occupancy = ft->pix_low_occupancy ? 1 : 0;
 	fa.residuals = ft->residuals.ptr;
 	fa.residual_mask = ft->residual_mask.ptr;
 	fa.pixel_face = ft->pixel_face.ptr;
@@ -732,13 +734,22 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	// launch 214 -> 197 us). In one round every wave starts at once and the table load only delays it (C2 40.2 -> 41.8).
 	// NNRT_TILE_ORDER=0: never, =2: always.
 	const size_t tiles = static_cast<size_t>(ceil_div(W, 16)) * static_cast<size_t>(ceil_div(H, 16));
+	int cus = 0;
+	if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ft->device) != hipSuccess || cus <= 0) cus = 256;
+	const bool multi_round = 4 * tiles > static_cast<size_t>(5 * 4 * cus);
 	const bool tile_order = fit_pixels_tile_order_supported() && [&] {
 		const char* v = std::getenv("NNRT_TILE_ORDER");
 		if (v && *v == '0') return false;
 		if (v && *v == '2') return true;
-		int cus = 0;
-		if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ft->device) != hipSuccess || cus <= 0) cus = 256;
-		return 4 * tiles > static_cast<size_t>(5 * 4 * cus);
+		return multi_round;
+	}();
+	// the same launches take the pixel kernel's 4-waves-per-SIMD build: their pass-2 gathers miss L2 (C3's 72-MB
+	// canonical mesh) and fewer, spill-free waves congest the memory pipeline less (C3 fused launch 198.6 -> 188 us; at C2,
+	// one round, 40.4 -> 47.2). NNRT_PIX_WPE4=0 / 1 forces.
+	const bool pix_low = [&] {
+		const char* v = std::getenv("NNRT_PIX_WPE4");
+		if (v) return *v == '1';
+		return multi_round;
 	}();
 	{
 		if (tile_order && ((st = ft->tile_flags.ensure(tiles)) || (st = ft->tile_order.ensure(static_cast<size_t>(tile_order_blocks(static_cast<int>(tiles)))))))
@@ -837,11 +848,12 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	const NdcSetup nndc = make_ndc_setup(h_K, H, W, ft->p.ndc_convention == NNRT_NDC_CONSISTENT);
 	const Camera npix = pixel_camera(h_K);
 	const WarpExtrinsics ne = make_extrinsics(h_E);
-	if (before != after || ft->use_tile_order != tile_order || ft->wf != wf || ft->wf_id != wf->id || ft->V != V || ft->F != F || ft->H != H || ft->W != W || ft->N != N ||
+	if (before != after || ft->use_tile_order != tile_order || ft->pix_low_occupancy != pix_low || ft->wf != wf || ft->wf_id != wf->id || ft->V != V || ft->F != F || ft->H != H || ft->W != W || ft->N != N ||
 	    ft->K != K || std::memcmp(&nndc, &ft->ndc, sizeof(nndc)) != 0 || std::memcmp(&npix, &ft->pix, sizeof(npix)) != 0 ||
 	    std::memcmp(&ne, &ft->extr, sizeof(ne)) != 0)
 		ft->drop_graphs();
 	ft->use_tile_order = tile_order;
+	ft->pix_low_occupancy = pix_low;
 	ft->V = V;
 	ft->F = F;
 	ft->H = H;

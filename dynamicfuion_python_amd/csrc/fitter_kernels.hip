@@ -861,8 +861,11 @@ __device__ unsigned long long g_fit_stamps[16384][4];
 	} while (0)
 #endif
 
-template <int MODE, int MAXK>
-__global__ __launch_bounds__(PIX_BLOCK) __attribute__((amdgpu_waves_per_eu(5))) void k_fit_pixels_fused(FitPixelArgs a) {
+// WPE: the waves per SIMD the launch is compiled for. 5 (96 VGPRs, one dword spilled; the LDS allows 5 workgroups per
+// CU): single-round launches (C2: 40.4 us; 47.2 at 4). 4 (108 VGPRs, no spill): launches of several residency rounds,
+// whose pass-2 gathers miss L2 and congest the memory pipeline (C3: 198.6 -> 188 us) -- FitPixelArgs::low_occupancy.
+template <int MODE, int MAXK, int WPE>
+__global__ __launch_bounds__(PIX_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_fit_pixels_fused(FitPixelArgs a) {
 	constexpr int NODE_WORDS = 2 * 8 * NG_STRIDE + 3 * MAXK * 64;
 	constexpr int WORDS = NODE_WORDS > 27 * 64 ? NODE_WORDS : 27 * 64;
 #ifdef NNRT_DEV_PIX_LDS_WORDS   // timing build only: per-wave LDS region padded to this many words (occupancy probe)
@@ -1004,18 +1007,22 @@ nnrt_status launch_fit_pixels(int mode, const FitPixelArgs& args, hipStream_t st
 	                                            args.arap_blocks);
 	// anchor slots per vertex: the common 4-anchor configuration gets its own instantiation (half the slot logic)
 	const bool k4 = args.anchor_count <= 4;
+	const bool low = args.low_occupancy != 0;
 	switch (mode) {
 		case NNRT_ITERATION_ALL:
-			if (k4) k_fit_pixels_fused<NNRT_ITERATION_ALL, 4><<<grid, PIX_BLOCK, 0, stream>>>(args);
-			else k_fit_pixels_fused<NNRT_ITERATION_ALL, MAX_ANCHORS><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			if (k4 && low) k_fit_pixels_fused<NNRT_ITERATION_ALL, 4, 4><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			else if (k4) k_fit_pixels_fused<NNRT_ITERATION_ALL, 4, 5><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			else k_fit_pixels_fused<NNRT_ITERATION_ALL, MAX_ANCHORS, 5><<<grid, PIX_BLOCK, 0, stream>>>(args);
 			break;
 		case NNRT_ITERATION_TRANSLATION_ONLY:
-			if (k4) k_fit_pixels_fused<NNRT_ITERATION_TRANSLATION_ONLY, 4><<<grid, PIX_BLOCK, 0, stream>>>(args);
-			else k_fit_pixels_fused<NNRT_ITERATION_TRANSLATION_ONLY, MAX_ANCHORS><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			if (k4 && low) k_fit_pixels_fused<NNRT_ITERATION_TRANSLATION_ONLY, 4, 4><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			else if (k4) k_fit_pixels_fused<NNRT_ITERATION_TRANSLATION_ONLY, 4, 5><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			else k_fit_pixels_fused<NNRT_ITERATION_TRANSLATION_ONLY, MAX_ANCHORS, 5><<<grid, PIX_BLOCK, 0, stream>>>(args);
 			break;
 		case NNRT_ITERATION_ROTATION_ONLY:
-			if (k4) k_fit_pixels_fused<NNRT_ITERATION_ROTATION_ONLY, 4><<<grid, PIX_BLOCK, 0, stream>>>(args);
-			else k_fit_pixels_fused<NNRT_ITERATION_ROTATION_ONLY, MAX_ANCHORS><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			if (k4 && low) k_fit_pixels_fused<NNRT_ITERATION_ROTATION_ONLY, 4, 4><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			else if (k4) k_fit_pixels_fused<NNRT_ITERATION_ROTATION_ONLY, 4, 5><<<grid, PIX_BLOCK, 0, stream>>>(args);
+			else k_fit_pixels_fused<NNRT_ITERATION_ROTATION_ONLY, MAX_ANCHORS, 5><<<grid, PIX_BLOCK, 0, stream>>>(args);
 			break;
 		default: set_error("unknown iteration mode"); return NNRT_ERROR_ARGUMENT;
 	}

@@ -181,6 +181,7 @@ struct FitPixelArgs {
 	int32_t* pixel_face;    // [P]
 	double* acc;            // [N, ACC_STRIDE] fp64 data-term accumulator (21 JtJ + 6 J r)
 	float4* records;        // [P, 4] per-pixel Jacobian record (pass 1 -> pass 2)
+	int low_occupancy;      // the 4-waves-per-SIMD build of the launch (several residency rounds; k_fit_pixels_fused)
 	ArapArgs arap;          // ARAP edge terms, computed by the launch's last arap_blocks workgroups (0: none)
 	int arap_blocks;
 	const int* tile_order;  // [order_blocks] workgroup -> tile (launch_tile_order; nullable: the arithmetic XCD bands)

@@ -24,7 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fetch", default="gpurun_out/pmc_fetch/**/*counter_collection.csv")
     ap.add_argument("--write", default="gpurun_out/pmc_write/**/*counter_collection.csv")
-    ap.add_argument("--kernels", nargs="+", default=["k_fit_pixels_fused<0, 4>", "k_raster_scatter_mesh",
+    ap.add_argument("--kernels", nargs="+", default=["k_fit_pixels_fused<0, 4", "k_raster_scatter_mesh",
                                                       "k_warp_mesh_quad|k_warp_mesh_vertex", "k_solve_update_lanes<0"])
     ap.add_argument("--workload", required=True, help="bench.py config.workload string the passes ran")
     ap.add_argument("--out", default=None)
