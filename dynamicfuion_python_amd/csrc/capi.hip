@@ -374,6 +374,8 @@ struct nnrt_fitter {
 	DeviceBuffer<float> mesh_p, mesh_n;
 	DeviceBuffer<int4> faces4;
 	DeviceBuffer<int32_t> anchors;
+	DeviceBuffer<uint2> anchors16;   // [V] the anchors as 4 x 16 bits (K = 4, N < 65535): the vertex warp's loads
+	bool use_anchors16 = false;
 	DeviceBuffer<float> weights;
 	DeviceBuffer<uint32_t> face_nodes;   // [F, face_node_slots(K)] distinct anchor nodes per face (once per frame)
 	DeviceBuffer<float4> wpos, wnrm;
@@ -492,7 +494,8 @@ nnrt_status enqueue_iteration(nnrt_fitter* ft, const nnrt_warp_field* wf, int mo
 	const bool with_jacobians = NNRT_GATHER_ROWS != 0;
 	if ((stages & STAGE_WARP) &&
 	    (st = launch_warp_mesh(ft->mesh_p.ptr, ft->mesh_n.ptr, ft->V, state_in, ft->anchors.ptr, ft->weights.ptr, ft->K, ft->extr,
-	                           ft->wpos.ptr, ft->wnrm.ptr, with_jacobians ? ft->jrows.ptr : nullptr, s, from_identity)))
+	                           ft->wpos.ptr, ft->wnrm.ptr, with_jacobians ? ft->jrows.ptr : nullptr, s, from_identity,
+	                           ft->use_anchors16 ? ft->anchors16.ptr : nullptr)))
 		return st;
 	if ((st = mark(1))) return st;
 	const RasterOptions ro = make_raster_options(ft->H, ft->W, 0.5f / (static_cast<float>(fminf(ft->H, ft->W)) / 2.0f), ft->p.use_perspective_correction, 0, 1);
@@ -653,6 +656,7 @@ void nnrt_fitter_destroy(nnrt_fitter* ft) {
 		b->release();
 	ft->faces4.release();
 	ft->anchors.release();
+	ft->anchors16.release();
 	ft->face_nodes.release();
 	ft->wpos.release();
 	ft->wnrm.release();
@@ -715,14 +719,14 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	}
 	// (re)allocate; any reallocation invalidates captured graphs
 	const auto before = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->corner.generation,
-	                                    ft->face_nodes.ptr, ft->wpos.ptr, ft->mesh_p4.ptr, ft->tile_order.ptr);
+	                                    ft->face_nodes.ptr, ft->wpos.ptr, ft->mesh_p4.ptr, ft->tile_order.ptr, ft->anchors16.ptr);
 	nnrt_status st;
 	if ((st = ft->mesh_p.ensure(3 * V)) || (st = ft->mesh_n.ensure(3 * V)) || (st = ft->faces4.ensure(F)) ||
 	    (st = ft->anchors.ensure(static_cast<size_t>(V) * K)) || (st = ft->weights.ensure(static_cast<size_t>(V) * K)) ||
 	    (st = ft->face_nodes.ensure(static_cast<size_t>(F) * face_node_slots(K))) ||
 	    (st = ft->wpos.ensure(V)) || (st = ft->wnrm.ensure(V)) ||
 	    (st = ft->jrows.ensure(NNRT_GATHER_ROWS ? 3 * static_cast<size_t>(V) * K : 1)) || (st = ft->mesh_p4.ensure(V)) ||
-	    (st = ft->mesh_n4.ensure(V)) ||
+	    (st = ft->mesh_n4.ensure(V)) || (st = ft->anchors16.ensure(K == 4 && N < 65535 ? static_cast<size_t>(V) : 1)) ||
 	    (st = ft->ref_points.ensure(P)) || (st = ft->records.ensure(4 * P)) || (st = ft->keys.ensure(P)) ||
 	    (st = ft->residuals.ensure(P)) || (st = ft->residual_mask.ensure(P)) || (st = ft->pixel_face.ensure(P)) ||
 	    (st = ft->acc.ensure(static_cast<size_t>(N) * ACC_STRIDE)) ||
@@ -842,7 +846,7 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 		ft->aw.edge_list = ft->a_list.ptr;
 	}
 	const auto after = std::make_tuple(ft->mesh_p.ptr, ft->faces4.ptr, ft->anchors.ptr, ft->keys.ptr, ft->acc.ptr, ft->wing.ptr, ft->corner.generation,
-	                                   ft->face_nodes.ptr, ft->wpos.ptr, ft->mesh_p4.ptr, ft->tile_order.ptr);
+	                                   ft->face_nodes.ptr, ft->wpos.ptr, ft->mesh_p4.ptr, ft->tile_order.ptr, ft->anchors16.ptr);
 	// Captured graphs bake every buffer pointer and the per-frame constants (NDC setup, pixel camera, extrinsics) into
 	// their kernel arguments: any change drops them. The warp field is recognised by its unique id, not its address.
 	const NdcSetup nndc = make_ndc_setup(h_K, H, W, ft->p.ndc_convention == NNRT_NDC_CONSISTENT);
@@ -884,6 +888,12 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 		return st;
 	// the faces' distinct anchor nodes (AssociateFacesWithAnchors, :105), consumed by the node pass of every iteration
 	if ((st = launch_face_node_table(ft->faces4.ptr, F, ft->anchors.ptr, K, ft->face_nodes.ptr, s))) return st;
+	// the warp's 16-bit anchor copy (every index fits: N < 65535; -1 as 0xFFFF)
+	ft->use_anchors16 = K == 4 && N < 65535 && [] {
+		const char* v = std::getenv("NNRT_ANCHORS16");   // development switch: 0 = the int32 anchors
+		return !(v && *v == '0');
+	}();
+	if (ft->use_anchors16 && (st = launch_pack_anchors16(ft->anchors.ptr, V, ft->anchors16.ptr, s))) return st;
 	// reference point cloud (:289-306): depth / scale with 0 < d < max_depth, AND the user mask; stored as depth (0 = masked)
 	if (ref.depth)
 		k_prepare_reference_depth<<<static_cast<unsigned>(ceil_div(P, 256)), 256, 0, s>>>(ref.depth, ref.mask, H, W, ref.depth_scale,

@@ -354,7 +354,7 @@ template <bool IDENTITY, bool VEC4>
 __global__ __launch_bounds__(256) void k_warp_mesh_vertex(const float* __restrict__ points, const float* __restrict__ normals, int64_t V,
                                                           const float* __restrict__ node_state, const int32_t* __restrict__ anchors,
                                                           const float* __restrict__ weights, int K, WarpExtrinsics E, float4* __restrict__ out_p,
-                                                          float4* __restrict__ out_n) {
+                                                          float4* __restrict__ out_n, const uint2* __restrict__ anchors16) {
 	const int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
 	if (v >= V) return;
 	const f3 p = make3(points[3 * v], points[3 * v + 1], points[3 * v + 2]);
@@ -362,9 +362,16 @@ __global__ __launch_bounds__(256) void k_warp_mesh_vertex(const float* __restric
 	int32_t a[4];
 	float w[4];
 	if constexpr (VEC4) {
-		const int4 a4 = reinterpret_cast<const int4*>(anchors)[v];
+		if (anchors16) {   // the per-frame 16-bit copy (launch_pack_anchors16): 8 B per vertex instead of 16
+			const uint2 q = anchors16[v];
+			const uint32_t h[4] = {q.x & 0xFFFFu, q.x >> 16, q.y & 0xFFFFu, q.y >> 16};
+#pragma unroll
+			for (int k = 0; k < 4; k++) a[k] = h[k] == 0xFFFFu ? -1 : static_cast<int32_t>(h[k]);
+		} else {
+			const int4 a4 = reinterpret_cast<const int4*>(anchors)[v];
+			a[0] = a4.x, a[1] = a4.y, a[2] = a4.z, a[3] = a4.w;
+		}
 		const float4 w4 = reinterpret_cast<const float4*>(weights)[v];
-		a[0] = a4.x, a[1] = a4.y, a[2] = a4.z, a[3] = a4.w;
 		w[0] = w4.x, w[1] = w4.y, w[2] = w4.z, w[3] = w4.w;
 	} else {
 #pragma unroll
@@ -407,19 +414,35 @@ static bool warp_vertex_path(int64_t V) {
 	return V >= (int64_t{1} << 16);
 }
 
+// [V, 4] int32 anchors (every index < 65535, -1 for none) -> 4 x 16 bits per vertex (0xFFFF: none), for the
+// lane-per-vertex warp's anchor loads (C3: 36 of its ~200 MB per launch as int32)
+__global__ void k_pack_anchors16(const int4* __restrict__ anchors, int64_t V, uint2* __restrict__ out) {
+	const int64_t v = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+	if (v >= V) return;
+	const int4 a = anchors[v];
+	auto h = [](int x) { return x < 0 ? 0xFFFFu : static_cast<uint32_t>(x); };
+	out[v] = make_uint2(h(a.x) | h(a.y) << 16, h(a.z) | h(a.w) << 16);
+}
+nnrt_status launch_pack_anchors16(const int32_t* anchors, int64_t V, uint2* out, hipStream_t stream) {
+	if (V == 0) return NNRT_OK;
+	k_pack_anchors16<<<static_cast<unsigned>(ceil_div(V, 256)), 256, 0, stream>>>(reinterpret_cast<const int4*>(anchors), V, out);
+	NNRT_LAUNCH_CHECK();
+	return NNRT_OK;
+}
+
 nnrt_status launch_warp_mesh(const float* points, const float* normals, int64_t V, const float* node_state, const int32_t* anchors,
                              const float* weights, int K, const WarpExtrinsics& E, float4* out_p, float4* out_n, float2* jrows,
-                             hipStream_t stream, bool from_identity) {
+                             hipStream_t stream, bool from_identity, const uint2* anchors16) {
 	if (V == 0) return NNRT_OK;
 	if (K <= 4 && !jrows && warp_vertex_path(V)) {
 		const unsigned grid = static_cast<unsigned>(ceil_div(V, 256));
 		const bool vec4 = K == 4 && (reinterpret_cast<uintptr_t>(anchors) & 15) == 0 && (reinterpret_cast<uintptr_t>(weights) & 15) == 0;
 		if (from_identity) {
-			if (vec4) k_warp_mesh_vertex<true, true><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n);
-			else k_warp_mesh_vertex<true, false><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n);
+			if (vec4) k_warp_mesh_vertex<true, true><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n, vec4 ? anchors16 : nullptr);
+			else k_warp_mesh_vertex<true, false><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n, vec4 ? anchors16 : nullptr);
 		} else {
-			if (vec4) k_warp_mesh_vertex<false, true><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n);
-			else k_warp_mesh_vertex<false, false><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n);
+			if (vec4) k_warp_mesh_vertex<false, true><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n, vec4 ? anchors16 : nullptr);
+			else k_warp_mesh_vertex<false, false><<<grid, 256, 0, stream>>>(points, normals, V, node_state, anchors, weights, K, E, out_p, out_n, vec4 ? anchors16 : nullptr);
 		}
 		NNRT_LAUNCH_CHECK();
 		return NNRT_OK;

@@ -87,7 +87,9 @@ nnrt_status launch_compute_anchors(const float* points, int64_t V, const float* 
                                    int threshold = -1);   // -1: threshold iff minimum_valid > 0 (the anchor API); 0 / 1: forced
 nnrt_status launch_warp_mesh(const float* points, const float* normals, int64_t V, const float* node_state, const int32_t* anchors,
                              const float* weights, int K, const WarpExtrinsics& E, float4* out_p, float4* out_n, float2* jrows,
-                             hipStream_t stream, bool from_identity = false);
+                             hipStream_t stream, bool from_identity = false, const uint2* anchors16 = nullptr);
+// K = 4 anchors with every index below 65535 as 4 x 16 bits per vertex (the lane-per-vertex warp's anchors16)
+nnrt_status launch_pack_anchors16(const int32_t* anchors, int64_t V, uint2* out, hipStream_t stream);
 nnrt_status launch_pack_nodes(const float* nodes, const float* R, const float* t, int N, float* state, hipStream_t stream);
 nnrt_status launch_unpack_float4x3(const float4* in, int64_t count, float* out, hipStream_t stream);
 nnrt_status launch_extract_face_ndc(const float* verts, const int64_t* faces, int64_t F, const NdcSetup& s, float near_clip, float far_clip,
