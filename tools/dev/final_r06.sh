@@ -6,7 +6,7 @@ set -u
 export TAG=${TAG:-r06f}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for cfg in ${PMC_CONFIGS-C2 C3 C5}; do
-	K=""; [ $cfg = C5 ] && K="k_fit_pixels_fused k_raster_scatter_mesh k_warp_mesh_quad k_arrow_prepare k_init_stem k_stem_schur_rhs k_corner_factor k_corner_flow"
+	K=""; [ $cfg = C5 ] && K="k_fit_pixels_fused k_raster_scatter_mesh k_warp_mesh_quad|k_warp_mesh_vertex k_arrow_prepare k_init_stem k_stem_schur_rhs k_corner_factor k_corner_flow"
 	KERNELS="$K" CONFIG=$cfg STAGES="prof pmc" bash tools/measure.sh || exit 1
 	lc=$(echo $cfg | tr 'A-Z' 'a-z')
 	cp gpurun_out/$TAG/pmc_traffic_$cfg.json profiles/r06_pmc_traffic_$lc.json || exit 1

@@ -5,7 +5,7 @@
 set -u
 export TAG=${TAG:-r06p}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-ARAPK="k_fit_pixels_fused k_raster_scatter_mesh k_warp_mesh_quad k_arrow_prepare k_init_stem k_stem_schur_rhs k_corner_factor k_corner_flow"
+ARAPK="k_fit_pixels_fused k_raster_scatter_mesh k_warp_mesh_quad|k_warp_mesh_vertex k_arrow_prepare k_init_stem k_stem_schur_rhs k_corner_factor k_corner_flow"
 run() {   # name config kernels bench-args
 	KERNELS="$3" CONFIG=$2 STAGES=pmc BENCH_ARGS="$4" bash tools/measure.sh || exit 1
 	cp gpurun_out/$TAG/pmc_traffic_$2.json profiles/r06_pmc_traffic_$1.json || exit 1

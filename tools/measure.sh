@@ -23,7 +23,7 @@ for s in $STAGES; do
 		     python3 tools/pmc_traffic.py --fetch "$OUT/pmc_fetch_$CONFIG/**/*counter_collection.csv" --write "$OUT/pmc_write_$CONFIG/**/*counter_collection.csv" --workload "$W" ${KERNELS:+--kernels $KERNELS} --out $OUT/pmc_traffic_$CONFIG.json > /dev/null || exit 1 ;;
 		sq) step pmc_sq_$CONFIG 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --output-format csv -d $OUT/pmc_sq_$CONFIG -o run -- $B --steps 20 --warmup 5 --kernel-trials 1 --no-cpu-baseline || exit 1
 		    f=$(find $OUT/pmc_sq_$CONFIG -name "*counter_collection.csv" | head -1)
-		    python3 tools/sq_summary.py "$f" ${SQ_KERNELS:-k_fit_pixels_fused k_raster_scatter_mesh k_warp_mesh_quad k_solve_update} > $OUT/sq_summary_$CONFIG.txt 2>&1 || exit 1 ;;
+		    python3 tools/sq_summary.py "$f" ${SQ_KERNELS:-k_fit_pixels_fused k_raster_scatter_mesh k_warp_mesh k_solve_update} > $OUT/sq_summary_$CONFIG.txt 2>&1 || exit 1 ;;
 	esac
 done
 echo done
