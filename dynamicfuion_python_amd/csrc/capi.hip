@@ -852,12 +852,18 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 	const NdcSetup nndc = make_ndc_setup(h_K, H, W, ft->p.ndc_convention == NNRT_NDC_CONSISTENT);
 	const Camera npix = pixel_camera(h_K);
 	const WarpExtrinsics ne = make_extrinsics(h_E);
-	if (before != after || ft->use_tile_order != tile_order || ft->pix_low_occupancy != pix_low || ft->wf != wf || ft->wf_id != wf->id || ft->V != V || ft->F != F || ft->H != H || ft->W != W || ft->N != N ||
+	// the warp's 16-bit anchor copy (every index fits: N < 65535; -1 as 0xFFFF), filled with the anchors below
+	const bool anchors16 = K == 4 && N < 65535 && [] {
+		const char* v = std::getenv("NNRT_ANCHORS16");   // development switch: 0 = the int32 anchors
+		return !(v && *v == '0');
+	}();
+	if (before != after || ft->use_tile_order != tile_order || ft->pix_low_occupancy != pix_low || ft->use_anchors16 != anchors16 || ft->wf != wf || ft->wf_id != wf->id || ft->V != V || ft->F != F || ft->H != H || ft->W != W || ft->N != N ||
 	    ft->K != K || std::memcmp(&nndc, &ft->ndc, sizeof(nndc)) != 0 || std::memcmp(&npix, &ft->pix, sizeof(npix)) != 0 ||
 	    std::memcmp(&ne, &ft->extr, sizeof(ne)) != 0)
 		ft->drop_graphs();
 	ft->use_tile_order = tile_order;
 	ft->pix_low_occupancy = pix_low;
+	ft->use_anchors16 = anchors16;
 	ft->V = V;
 	ft->F = F;
 	ft->H = H;
@@ -888,11 +894,6 @@ nnrt_status prepare_frame(nnrt_fitter* ft, nnrt_warp_field* wf, const float* d_v
 		return st;
 	// the faces' distinct anchor nodes (AssociateFacesWithAnchors, :105), consumed by the node pass of every iteration
 	if ((st = launch_face_node_table(ft->faces4.ptr, F, ft->anchors.ptr, K, ft->face_nodes.ptr, s))) return st;
-	// the warp's 16-bit anchor copy (every index fits: N < 65535; -1 as 0xFFFF)
-	ft->use_anchors16 = K == 4 && N < 65535 && [] {
-		const char* v = std::getenv("NNRT_ANCHORS16");   // development switch: 0 = the int32 anchors
-		return !(v && *v == '0');
-	}();
 	if (ft->use_anchors16 && (st = launch_pack_anchors16(ft->anchors.ptr, V, ft->anchors16.ptr, s))) return st;
 	// reference point cloud (:289-306): depth / scale with 0 < d < max_depth, AND the user mask; stored as depth (0 = masked)
 	if (ref.depth)
