@@ -66,8 +66,11 @@ struct ModeTraits<NNRT_ITERATION_ROTATION_ONLY> {
 // reset to EMPTY for the next iteration's scatter; the contributing face goes to pass 2 in registers.
 // dn: this lane's 27 parked floats at dn[i * dn_stride] (lane-private LDS column)
 // out_face / out_vid: the pixel's contributing face (-1: none) and its vertices, handed to pass 2 in registers
-template <int MODE>
-__device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int dn_stride, int& out_face, int (&out_vid)[3]) {
+// RK: the record stays in the pixel lane's registers (rk) instead of memory, and pass 2 takes it by cross-lane reads
+// (the 4-wave build, whose 128-VGPR budget holds it: at C3 the launch is bound by its memory requests, 17 per
+// association of which the record's were 4)
+template <int MODE, bool RK>
+__device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int dn_stride, int& out_face, int (&out_vid)[3], float (&rk)[16]) {
 	// one 8x8 quadrant per wave: compact pixel sets touch the fewest nodes
 	const int tiles = a.tiles_x * a.tiles_y;
 	const int qd = pix_quadrant(a), tile = qd >> 2, quad = qd & 3;
@@ -238,10 +241,20 @@ __device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int
 			}
 			// record [dr/dV (9), dr/dn_l (3), rho (3), r]; everything but dr/dV first, so it is not held across the columns
 			float* rec_f = reinterpret_cast<float*>(a.records + 4 * p);
-			rec_f[9] = dr_dnl.x;
-			rec_f[10] = dr_dnl.y;
-			rec_f[11] = dr_dnl.z;
-			reinterpret_cast<float4*>(rec_f)[3] = make_float4(rho[0], rho[1], rho[2], residual);
+			if constexpr (RK) {
+				rk[9] = dr_dnl.x;
+				rk[10] = dr_dnl.y;
+				rk[11] = dr_dnl.z;
+				rk[12] = rho[0];
+				rk[13] = rho[1];
+				rk[14] = rho[2];
+				rk[15] = residual;
+			} else {
+				rec_f[9] = dr_dnl.x;
+				rec_f[10] = dr_dnl.y;
+				rec_f[11] = dr_dnl.z;
+				reinterpret_cast<float4*>(rec_f)[3] = make_float4(rho[0], rho[1], rho[2], residual);
+			}
 			// dr/dV = dr/dwl * dwl/dV + dr/dnl * dnl/dV ; dr/dN = dr/dnl (rho (x) I)
 			const float rw[3] = {dr_dwl.x, dr_dwl.y, dr_dwl.z};
 			rn[0] = dr_dnl.x;
@@ -291,7 +304,8 @@ __device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int
 					}
 					const float x = (rw[0] * w_rc[0] + rw[1] * w_rc[1]) + rw[2] * w_rc[2];
 					const float y = (rn[0] * n_rc[0] + rn[1] * n_rc[1]) + rn[2] * n_rc[2];
-					rec_f[3 * i + c] = x + y;   // stored as formed: no 9-float tail of live outputs
+					if constexpr (RK) rk[3 * i + c] = x + y;
+					else rec_f[3 * i + c] = x + y;   // stored as formed: no 9-float tail of live outputs
 				}
 			}
 #undef DN
@@ -402,9 +416,9 @@ __device__ unsigned long long g_fit_phases[16384][8];   // group, gather + Jacob
 
 // slots0 / slots1: this wave's two chunk buffers (8 * NG_STRIDE words each); ent: its face-table rows ([NSLOT][64])
 // face_in / vid_in: this lane's pixel's contributing face (-1: none) and its vertices, from pass 1
-template <int MODE, int MAXK>
+template <int MODE, int MAXK, bool RK>
 __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, float* slots1, uint32_t* ent, int face_in,
-                                          const int (&vid_in)[3]) {
+                                          const int (&vid_in)[3], const float (&rk)[16]) {
 	using T = ModeTraits<MODE>;
 	constexpr int S = T::S;
 	constexpr int NSLOT = 3 * MAXK;
@@ -589,7 +603,11 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 			}
 		}
 #endif
-		{
+		if constexpr (RK) {   // the record from its pixel lane's registers
+#pragma unroll
+			for (int w = 0; w < 4; w++)
+				rq[w] = make_float4(__shfl(rk[4 * w], d.x), __shfl(rk[4 * w + 1], d.x), __shfl(rk[4 * w + 2], d.x), __shfl(rk[4 * w + 3], d.x));
+		} else {
 			const int64_t pp = static_cast<int64_t>(min(pv0 + (d.x >> 3), a.H - 1)) * a.W + min(pu0 + (d.x & 7), a.W - 1);
 #pragma unroll
 			for (int w = 0; w < 4; w++) rq[w] = a.records[4 * pp + w];
@@ -864,6 +882,9 @@ __device__ unsigned long long g_fit_stamps[16384][4];
 // WPE: the waves per SIMD the launch is compiled for. 5 (96 VGPRs, one dword spilled; the LDS allows 5 workgroups per
 // CU): single-round launches (C2: 40.4 us; 47.2 at 4). 4 (108 VGPRs, no spill): launches of several residency rounds,
 // whose pass-2 gathers miss L2 and congest the memory pipeline (C3: 198.6 -> 188 us) -- FitPixelArgs::low_occupancy.
+#ifndef NNRT_PIX_KEEP_RECORDS
+#define NNRT_PIX_KEEP_RECORDS 1
+#endif
 template <int MODE, int MAXK, int WPE>
 __global__ __launch_bounds__(PIX_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_fit_pixels_fused(FitPixelArgs a) {
 	constexpr int NODE_WORDS = 2 * 8 * NG_STRIDE + 3 * MAXK * 64;
@@ -889,7 +910,11 @@ __global__ __launch_bounds__(PIX_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
 	                 (static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11))) << 32));
 	float* w = s_u[wave];
 	int face = -1, vid[3] = {0, 0, 0};
-	pixel_body<MODE>(a, w + lane, 64, face, vid);
+	constexpr bool RK = WPE == 4 && NNRT_PIX_KEEP_RECORDS;
+	float rk[16];
+#pragma unroll
+	for (int i = 0; i < 16; i++) rk[i] = 0.f;
+	pixel_body<MODE, RK>(a, w + lane, 64, face, vid, rk);
 	FIT_STAMP(1, __builtin_amdgcn_s_memrealtime());
 	// the node pass reads the records / keys this wave just stored (other lanes' pixels; same CU, same L1): workgroup-scope
 	// release + acquire (an agent-scope release writes back L2 on gfx950: 10x slower); the LDS region is reused in program
@@ -900,7 +925,7 @@ __global__ __launch_bounds__(PIX_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
 #ifdef NNRT_DEV_PASS1_ONLY   // timing build only: pass 1 alone (instruction counts per pass by difference)
 	if (face != -2) return;
 #endif
-	node_body<MODE, MAXK>(a, w, w + 8 * NG_STRIDE, reinterpret_cast<uint32_t*>(w + 2 * 8 * NG_STRIDE), face, vid);
+	node_body<MODE, MAXK, RK>(a, w, w + 8 * NG_STRIDE, reinterpret_cast<uint32_t*>(w + 2 * 8 * NG_STRIDE), face, vid, rk);
 	FIT_STAMP(2, __builtin_amdgcn_s_memrealtime());
 }
 
