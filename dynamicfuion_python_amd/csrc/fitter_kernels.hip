@@ -70,7 +70,8 @@ struct ModeTraits<NNRT_ITERATION_ROTATION_ONLY> {
 // (the 4-wave build, whose 128-VGPR budget holds it: at C3 the launch is bound by its memory requests, 17 per
 // association of which the record's were 4)
 template <int MODE, bool RK>
-__device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int dn_stride, int& out_face, int (&out_vid)[3], float (&rk)[16]) {
+__device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int dn_stride, int& out_face, int (&out_vid)[3], float (&rk)[16],
+                                           int& out_nodes) {
 	// one 8x8 quadrant per wave: compact pixel sets touch the fewest nodes
 	const int tiles = a.tiles_x * a.tiles_y;
 	const int qd = pix_quadrant(a), tile = qd >> 2, quad = qd & 3;
@@ -94,6 +95,7 @@ __device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int
 		if (key != EMPTY_KEY) {
 			face = static_cast<int32_t>(key & 0xffffffffu);
 			const int4 fi = a.faces4[face];
+			out_nodes = fi.w;   // the face's distinct anchor nodes (k_face_node_table)
 			vid[0] = fi.x;
 			vid[1] = fi.y;
 			vid[2] = fi.z;
@@ -317,7 +319,9 @@ __device__ __forceinline__ void pixel_body(const FitPixelArgs& a, float* dn, int
 
 // ---- once per frame: the face -> distinct anchor node table (AssociateFacesWithAnchorsImpl.h:34-107) --------------------
 template <int MAXK>
-__global__ __launch_bounds__(256) void k_face_node_table(const int4* __restrict__ faces4, int64_t F, const int32_t* __restrict__ anchors, int K,
+// (also stores the face's distinct-node count in faces4[f].w, which the pixel launch reads with the face's vertices: its
+// pass 2 then loads only the table row's used 16-B pieces)
+__global__ __launch_bounds__(256) void k_face_node_table(int4* __restrict__ faces4, int64_t F, const int32_t* __restrict__ anchors, int K,
                                                          uint32_t* __restrict__ out) {
 	constexpr int NS = 3 * MAXK;
 	const int64_t f = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -357,9 +361,10 @@ __global__ __launch_bounds__(256) void k_face_node_table(const int4* __restrict_
 	}
 	uint32_t* o = out + f * NS;
 	for (int i = 0; i < NS; i++) o[i] = i < n ? (static_cast<uint32_t>(node[i]) << FACE_NODE_SHIFT) | code[i] : FACE_NODE_NONE;
+	reinterpret_cast<int*>(faces4)[4 * f + 3] = n;
 }
 
-nnrt_status launch_face_node_table(const int4* faces4, int64_t F, const int32_t* anchors, int K, uint32_t* out, hipStream_t stream) {
+nnrt_status launch_face_node_table(int4* faces4, int64_t F, const int32_t* anchors, int K, uint32_t* out, hipStream_t stream) {
 	if (F == 0) return NNRT_OK;
 	const unsigned grid = static_cast<unsigned>(ceil_div(F, 256));
 	if (K <= 4) k_face_node_table<4><<<grid, 256, 0, stream>>>(faces4, F, anchors, K, out);
@@ -418,7 +423,7 @@ __device__ unsigned long long g_fit_phases[16384][8];   // group, gather + Jacob
 // face_in / vid_in: this lane's pixel's contributing face (-1: none) and its vertices, from pass 1
 template <int MODE, int MAXK, bool RK>
 __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, float* slots1, uint32_t* ent, int face_in,
-                                          const int (&vid_in)[3], const float (&rk)[16]) {
+                                          const int (&vid_in)[3], const float (&rk)[16], int nodes_in) {
 	using T = ModeTraits<MODE>;
 	constexpr int S = T::S;
 	constexpr int NSLOT = 3 * MAXK;
@@ -449,7 +454,8 @@ __device__ __forceinline__ void node_body(const FitPixelArgs& a, float* slots0, 
 			const uint4* fn4 = reinterpret_cast<const uint4*>(a.face_nodes + static_cast<int64_t>(face) * NSLOT);
 #pragma unroll
 			for (int t = 0; t < NSLOT / 4; t++) {
-				const uint4 e4 = fn4[t];
+				// pieces past the face's node count hold FACE_NODE_NONE only: not loaded
+				const uint4 e4 = t == 0 || 4 * t < nodes_in ? fn4[t] : make_uint4(FACE_NODE_NONE, FACE_NODE_NONE, FACE_NODE_NONE, FACE_NODE_NONE);
 				ent[(4 * t) * 64 + lane] = e4.x;
 				ent[(4 * t + 1) * 64 + lane] = e4.y;
 				ent[(4 * t + 2) * 64 + lane] = e4.z;
@@ -909,12 +915,12 @@ __global__ __launch_bounds__(PIX_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
 	FIT_STAMP(3, static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11))) |
 	                 (static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11))) << 32));
 	float* w = s_u[wave];
-	int face = -1, vid[3] = {0, 0, 0};
+	int face = -1, vid[3] = {0, 0, 0}, nodes = 3 * MAXK;
 	constexpr bool RK = WPE == 4 && NNRT_PIX_KEEP_RECORDS;
 	float rk[16];
 #pragma unroll
 	for (int i = 0; i < 16; i++) rk[i] = 0.f;
-	pixel_body<MODE, RK>(a, w + lane, 64, face, vid, rk);
+	pixel_body<MODE, RK>(a, w + lane, 64, face, vid, rk, nodes);
 	FIT_STAMP(1, __builtin_amdgcn_s_memrealtime());
 	// the node pass reads the records / keys this wave just stored (other lanes' pixels; same CU, same L1): workgroup-scope
 	// release + acquire (an agent-scope release writes back L2 on gfx950: 10x slower); the LDS region is reused in program
@@ -925,7 +931,7 @@ __global__ __launch_bounds__(PIX_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))
 #ifdef NNRT_DEV_PASS1_ONLY   // timing build only: pass 1 alone (instruction counts per pass by difference)
 	if (face != -2) return;
 #endif
-	node_body<MODE, MAXK, RK>(a, w, w + 8 * NG_STRIDE, reinterpret_cast<uint32_t*>(w + 2 * 8 * NG_STRIDE), face, vid, rk);
+	node_body<MODE, MAXK, RK>(a, w, w + 8 * NG_STRIDE, reinterpret_cast<uint32_t*>(w + 2 * 8 * NG_STRIDE), face, vid, rk, nodes);
 	FIT_STAMP(2, __builtin_amdgcn_s_memrealtime());
 }
 

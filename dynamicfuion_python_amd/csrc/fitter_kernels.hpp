@@ -207,7 +207,7 @@ constexpr uint32_t FACE_NODE_NONE = 0xFFFFFFFFu;
 constexpr int FACE_NODE_SHIFT = 12;
 constexpr int FACE_NODE_MAX_NODES = (1 << 20) - 1;
 inline int face_node_slots(int K) { return K <= 4 ? 12 : 3 * MAX_ANCHORS; }
-nnrt_status launch_face_node_table(const int4* faces4, int64_t F, const int32_t* anchors, int K, uint32_t* out, hipStream_t stream);
+nnrt_status launch_face_node_table(int4* faces4, int64_t F, const int32_t* anchors, int K, uint32_t* out, hipStream_t stream);
 
 // pass 1 then pass 2 in one launch (k_fit_pixels_fused); `between` (optional, stage timing) is recorded before it.
 // args.arap_blocks extra workgroups (fit_pixels_arap_blocks(E), 0 without ARAP) compute the ARAP edge terms.
