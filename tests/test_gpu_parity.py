@@ -1351,6 +1351,37 @@ def test_raster_dense_path_same_iteration(nn, S, oracle_mod, name):
     assert nan_rel_err(a["updates"][: 6 * N], b["updates"][: 6 * N]) < 1e-5
 
 
+@pytest.mark.parametrize("name", ["S1", "C2"])
+def test_pixel_launch_builds_same_iteration(nn, S, oracle_mod, name):
+    """The pixel launch's two builds -- 5 waves per SIMD with the per-pixel records in memory (one-round launches, C2) and
+    4 waves per SIMD with each record kept in its pixel lane's registers and read by cross-lane shuffles (launches of
+    several residency rounds, C3) -- transport the same record floats: forced (NNRT_PIX_WPE4=1 / 0) on the same scene,
+    the residuals are bit-identical and the data term equal up to its fp64 atomics' order."""
+    import os
+    sc = _scene(S, oracle_mod, name)
+    depth = scene_target(oracle_mod, sc)
+    N = len(sc.nodes)
+    old = os.environ.get("NNRT_PIX_WPE4")
+    out = {}
+    try:
+        for v in ("1", "0"):
+            os.environ["NNRT_PIX_WPE4"] = v
+            _, _, dg = _gpu_fit(nn, sc, depth, 1)
+            out[v] = dg
+    finally:
+        if old is None:
+            os.environ.pop("NNRT_PIX_WPE4", None)
+        else:
+            os.environ["NNRT_PIX_WPE4"] = old
+    a, b = out["1"], out["0"]
+    assert (a["pixel_faces"] >= 0).sum() > 500
+    for k in ("pixel_faces", "residual_mask", "residuals"):
+        assert np.array_equal(a[k], b[k]), k
+    assert rel_err(a["hessian"][: 36 * N], b["hessian"][: 36 * N]) < 1e-6
+    assert rel_err(a["gradient"][: 6 * N], b["gradient"][: 6 * N]) < 1e-6
+    assert nan_rel_err(a["updates"][: 6 * N], b["updates"][: 6 * N]) < 1e-5
+
+
 def test_errors_fail_loudly(nn, S, oracle_mod):
     A, G = nn.alignment, nn.geometry
     with pytest.raises(RuntimeError):
