@@ -85,13 +85,16 @@ def test_warp_bit_exact(nn, S, oracle_mod, extrinsic):
 
 
 @pytest.mark.parametrize("name,from_identity,vertex_path", [("C1", False, "0"), ("C1", True, "0"), ("C2", False, "0"), ("C1", False, "1"),
-                                                             ("C1", True, "1"), ("C2", False, "1")])
+                                                             ("C1", True, "1"), ("C2", False, "1"), ("C2", False, "1-int32"),
+                                                             ("C1", True, "1-int32")])
 def test_fitter_warp_bit_exact(nn, S, oracle_mod, name, from_identity, vertex_path, monkeypatch):
     """The fitter's own warp -- the mesh an iteration rasterizes -- equals the oracle's warp of the motion the iteration
     started from, bit for bit: from the ground-truth motion (general kernel) and from the identity (iterate_from_identity's
-    IDENTITY kernel); with the lane-per-(vertex, slot) quad kernel (C1 / C2 size) and, forced by NNRT_WARP_VERTEX=1, the
-    lane-per-vertex kernel large meshes take (C3)."""
-    monkeypatch.setenv("NNRT_WARP_VERTEX", vertex_path)
+    IDENTITY kernel); with the lane-per-(vertex, slot) quad kernel (NNRT_WARP_VERTEX=0) and the lane-per-vertex kernel
+    meshes of 64 k vertices and more take (=1), the latter reading the per-frame 16-bit anchor copy or, with
+    NNRT_ANCHORS16=0 ("1-int32"), the int32 anchors."""
+    monkeypatch.setenv("NNRT_WARP_VERTEX", vertex_path[0])
+    monkeypatch.setenv("NNRT_ANCHORS16", "0" if vertex_path.endswith("int32") else "1")
     sc = _scene(S, oracle_mod, name)
     depth = scene_target(oracle_mod, sc)
     wf, ft = _new_fit(nn, sc, depth, 1)
